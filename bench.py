@@ -1,0 +1,223 @@
+"""bench.py -- explained target-edges/s of the TempME explanation hot path on MI355X.
+
+Metric (BASELINE.json): explained target-edges/sec (TGN+Enron, n_degree=20).  One unit = one
+target event with its fake destination, 2-hop subgraphs x3 sides, temporal walks x3 with
+motif categories and edge counts, encoder forward x3 and retrieve_explanation (eval)
+(SURVEY.md §8(d)); the base TGN's contrast is excluded.
+
+Workload: BASELINE configs[1] = enron_sampled + TGN explainer scoring on 1 MI355X, n_degree=20.
+Enron is not available offline, so the graph is a seeded synthetic replica of its shape
+(tempme_amd/workload.py: V=183, E=18,780, Pareto(1.2) endpoints, ts in [0, 1e8), de=32,
+dn=172); explainer weights are a seeded random init of the TempME architecture.
+
+A step = one pass of the hot path over one batch of synthetic input: --batches reference
+batches of --batch-size (default 64 x 100 = 6,400) target events per GPU, all on-device
+(tm_sample_events -> tm_encoder_fwd -> tm_edge_importance).  Multi-GPU: one process per GPU
+(torch.distributed.run), whole batches sharded across ranks, no data-path collective
+(weak scaling); barrier + max-over-ranks timing.
+
+Run:  python bench.py [--gpus N --steps K --warmup W]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+METRIC = "explained target-edges/sec (TGN+Enron, n_degree=20) at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
+FP32_MFMA_PEAK_TF = 157.3      # MI355X_MICROARCH.md: FP32 matrix (spec)
+
+
+def flops_model(de, dn, h, N, M):
+    """Algorithmic MACs per unit for each encoder kernel."""
+    kev = de + 3 + dn
+    per_pos_gcn = kev * dn + 2 * (dn * h + h * h)                       # lin_event + event_gcn MLP x2
+    per_walk_head = 3 * (2 * h) ** 2 + (2 * h) * h + h * h + (h + 12) ** 2 + (h + 12) * h + h + 2 * 2 * h
+    per_pos_gate = (de + dn) * h + h * (h // 2) + h // 2
+    W = N * M
+    return dict(gcn_kernel=2 * per_pos_gcn * 3, head_kernel=2 * per_walk_head, explain_kernel=2 * per_pos_gate * 3,
+                per_walk=2 * (3 * per_pos_gcn + per_walk_head + 3 * per_pos_gate), W=W)
+
+
+def sampling_bytes_per_event(N, M):
+    """SURVEY.md §8(d) compulsory-traffic model for (a)+(b), per target event (3 sides)."""
+    W = N * M
+    khop = (N + N * N) * 16 + (N + N * N) * 12 + (1 + N) * 32
+    walks = N * 128 + W * 188
+    return 3 * (khop + walks)
+
+
+def cpu_baseline(g, rows, events, pool, N, M, B, seed, sd, budget_s=12.0, max_batches=8):
+    """The oracle port (C sampler + torch-fp32 encoder) on the host cores, bounded sample."""
+    from oracle import encoder_ref as er
+    from oracle import oracle as orc
+    threads = int(os.environ.get("TEMPME_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    torch.set_num_threads(threads)
+    src, dst, ts, eidx = events
+    og = orc.OracleGraph(g["src"][rows], g["dst"][rows], g["eidx"][rows], g["ts"][rows], g["n_nodes"])
+    nf, ef = torch.from_numpy(g["n_feat"]), torch.from_numpy(g["e_feat"])
+    done, t0 = 0, time.perf_counter()
+    while done < max_batches * B and time.perf_counter() - t0 < budget_s:
+        sl = slice(done % len(src), done % len(src) + B)
+        if sl.stop > len(src):
+            sl = slice(0, B)
+        o = orc.event_pipeline(og, seed, 1, N, M, src[sl], dst[sl], ts[sl], eidx[sl], np.arange(done, done + B),
+                               pool, threads)
+        with torch.no_grad():
+            for s in range(3):
+                imp = er.forward(sd, nf, ef, o["node6"][:, s], o["eid3"][:, s], o["ts3"][:, s], o["cat"][:, s],
+                                 ts[sl], o["cnt"][:, s].astype(np.float64))
+                er.edge_importance(sd, ef, imp, o["eid3"][:, s], o["ts3"][:, s],
+                                   [o["sub1_node"][:, s], o["sub2_node"][:, s]],
+                                   [o["sub1_eid"][:, s], o["sub2_eid"][:, s]])
+        done += B
+    el = time.perf_counter() - t0
+    return {"value": round(done / el, 2), "unit": "edges/s", "cores": threads, "kind": "port",
+            "sample": f"{done} target events ({done // B} reference batches of {B}) of the same workload: "
+                      f"oracle/tempme_oracle.c sampling+motif ({threads} OpenMP threads) + oracle/encoder_ref.py "
+                      f"torch-fp32 encoder+explanation ({threads} threads), {el:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batches", type=int, default=64, help="reference batches per step per GPU")
+    ap.add_argument("--batch-size", type=int, default=100, help="temp_exp_main --test_bs")
+    ap.add_argument("--n-degree", type=int, default=20)
+    ap.add_argument("--alpha", type=float, default=1.2)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import tempme_amd as tm
+    from tempme_amd import _lib as L
+    from tempme_amd.pipeline import ExplainPipeline
+    from tempme_amd.workload import enron_like, split
+
+    N, M, B = args.n_degree, 3, args.batch_size
+    E = args.batches * B
+    g = enron_like(alpha=args.alpha, seed=args.seed)
+    (src, dst, ts, eidx), rows, pool = split(g)
+    finder = tm.NeighborFinder.from_edges(g["src"][rows], g["dst"][rows], g["eidx"][rows], g["ts"][rows],
+                                          g["n_nodes"], device=dev, seed=args.seed, split=tm.SPLIT_TEST)
+
+    class Base:
+        n_feat_th = torch.from_numpy(g["n_feat"])
+        e_feat_th = torch.from_numpy(g["e_feat"])
+        node_raw_features = torch.nn.Embedding.from_pretrained(n_feat_th, padding_idx=0, freeze=True)
+        edge_raw_features = torch.nn.Embedding.from_pretrained(e_feat_th, padding_idx=0, freeze=True)
+
+    torch.manual_seed(args.seed)
+    ex = tm.TempME(Base(), "tgn", "enron_sampled", out_dim=40, hid_dim=64, device=dev,
+                   null_model={k: 1.0 / 12 for k in range(1, 13)}).to(dev).eval()
+    pipe = ExplainPipeline(ex, finder.graph, torch.from_numpy(pool), N, M, B, seed=args.seed)
+
+    # inputs for every step resident in HBM before timing: events cycle through the test split
+    n_steps = args.warmup + args.steps
+    n_test = len(src)
+    gidx = [((np.arange(E) + (k * world + rank) * E) % n_test) for k in range(n_steps)]
+    to = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)  # noqa: E731
+    inputs = [(to(src[i], np.int32), to(dst[i], np.int32), to(ts[i], np.float64), to(eidx[i], np.int32),
+               to((np.arange(E, dtype=np.int64) + (k * world + rank) * E).astype(np.uint32).view(np.int32), np.int32))
+              for k, i in enumerate(gidx)]
+
+    for k in range(args.warmup):
+        pipe.run(*inputs[k])
+    torch.cuda.synchronize()
+    pipe.check_errors()
+
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    L.profile_enable(True)
+    t0 = time.perf_counter()
+    for k in range(args.warmup, n_steps):
+        pipe.run(*inputs[k])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    prof = L.profile_read()
+    L.profile_enable(False)
+    pipe.check_errors()
+    if dist:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    if rank == 0:
+        fm = flops_model(g["e_feat"].shape[1], g["n_feat"].shape[1], 64, N, M)
+        W = fm["W"]
+        units = {"events_kernel": ("hbm", sampling_bytes_per_event(N, M) * E),
+                 "gcn_kernel": ("mfma", fm["gcn_kernel"] * 3 * E * W),
+                 "head_kernel": ("mfma", fm["head_kernel"] * 3 * E * W),
+                 "explain_kernel": ("mfma", fm["explain_kernel"] * 3 * E * W)}
+        kernels = {}
+        for name, (ms, cnt) in prof.items():
+            avg_ms = ms / max(cnt, 1)
+            ent = {"avg_ms": round(avg_ms, 4), "launches": cnt}
+            if name in units:
+                bound, work = units[name]
+                if bound == "hbm":
+                    ach = work / (avg_ms * 1e-3) / 1e9
+                    ent.update(bound="hbm", achieved=round(ach, 1), unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4))
+                else:
+                    ach = work / (avg_ms * 1e-3) / 1e12
+                    ent.update(bound="mfma", achieved=round(ach, 2), unit="TFLOP/s",
+                               frac=round(ach / FP32_MFMA_PEAK_TF, 4))
+            kernels[name] = ent
+        dom = max((k for k in kernels if "bound" in kernels[k]), key=lambda k: kernels[k]["avg_ms"])
+        d = kernels[dom]
+        roof = {"bound": d["bound"], "achieved": d["achieved"],
+                "peak": HBM_PEAK_GBS if d["bound"] == "hbm" else FP32_MFMA_PEAK_TF, "unit": d["unit"],
+                "frac": d["frac"], "traffic": None, "kernel": dom}
+        pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            with open(pmc) as fh:
+                tr = json.load(fh).get(dom)
+            if tr is not None:
+                roof["traffic"] = tr
+        total = world * args.steps * E
+        out = {"metric": METRIC, "value": round(total / el, 2), "unit": "edges/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+               "data": "synthetic (seeded enron_sampled-shaped graph, random-init TempME weights)",
+               "config": {"workload": "configs[1]: enron_sampled-shaped synthetic graph (V=183, E=18,780, "
+                                      f"Pareto {args.alpha}) + TGN explainer scoring, n_degree={N}",
+                          "n_degree": N, "walks_per_slot": M, "batch_size": B, "batches_per_step_per_gpu": args.batches,
+                          "events_per_step_per_gpu": E, "parallelism": f"dp{world} (whole batches per rank)"},
+               "roofline": roof, "kernels": kernels,
+               "sampling_roofline": kernels.get("events_kernel")}
+        if world == 1 and not args.no_cpu_baseline:
+            sd = {k: v.detach().cpu() for k, v in ex.state_dict().items()}
+            out["cpu_baseline"] = cpu_baseline(g, rows, (src, dst, ts, eidx), pool, N, M, B, args.seed, sd)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,166 @@
+/* tempme.h -- C ABI of libtempme_hip.so, the MI355X (gfx950) TempME explanation hot path.
+ *
+ * Plain pointers and sizes only; no torch types.  All sampling/encoder entry points
+ * take DEVICE pointers and a hipStream_t (passed as void*, NULL = default stream) and
+ * are stream-ordered and asynchronous.  Graph build/export and weight creation take
+ * HOST pointers.  Every entry point returns TM_OK (0) or a negative TM_E_* code;
+ * tm_last_error() gives the message (thread-local).  No C++ exception crosses the ABI.
+ *
+ * Keyed-RNG contract (replaces the reference's unseeded np.random.randint, see
+ * oracle/philox.py):  key = (seed lo, seed hi); counter = (event, split<<16 | side<<8 |
+ * stage, row, j>>2); word j&3 of Philox4x32-10; draw(high) = (u32 * high) >> 32.
+ *
+ * The reference interface each entry point replaces is cited as file:line in
+ * dharunm236/TempME.
+ */
+#ifndef TEMPME_H_
+#define TEMPME_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TM_OK 0
+#define TM_E_EDGE_NOT_IN_LIST (-1) /* IndexError, utils/graph.py:134-135 */
+#define TM_E_SHAPE (-2)            /* assert, utils/graph.py:127, :317, :378; explainer_new.py:180 */
+#define TM_E_HIP (-3)              /* HIP runtime failure */
+#define TM_E_ARG (-4)              /* bad argument (NULL pointer, negative size, ...) */
+#define TM_E_UNSUPPORTED (-5)      /* input outside what the build supports (message says what) */
+
+/* sides and stages of the RNG contract */
+#define TM_SIDE_NONE 0
+#define TM_SIDE_SRC 1
+#define TM_SIDE_TGT 2
+#define TM_SIDE_BGD 3
+#define TM_STAGE_STEP2 16
+#define TM_STAGE_STEP3 17
+#define TM_STAGE_NEG 32
+#define TM_STAGE_PERM 48
+#define TM_SPLIT_TRAIN 0
+#define TM_SPLIT_TEST 1
+#define TM_SPLIT_NULL 2
+
+typedef struct tm_graph tm_graph;     /* opaque, immutable after build; device-resident */
+typedef struct tm_weights tm_weights; /* opaque, packed encoder weights on one device */
+
+typedef struct {
+    uint64_t seed;
+    uint32_t split;
+    uint32_t side;
+} tm_rng;
+
+const char *tm_last_error(void);
+int tm_version(void);
+
+/* ---------------------------------------------------------------- graph (host inputs)
+ * Replaces NeighborFinder.__init__ / init_off_set / get_ts2idx (utils/graph.py:13-101).
+ * Adjacency lists in insertion order, owner-major: entries [in_off[u], in_off[u+1]) are
+ * node u's (ngh, eid, ts) triples in the order the caller appended them
+ * (temp_exp_main.py:135-144).  The build stable-sorts every list by ts, simulates
+ * get_ts2idx (trailing-tie quirk included) and uploads the CSR to `device`. */
+int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int32_t *ngh, const int32_t *eid,
+                   const double *ts, int device, tm_graph **out);
+int tm_graph_free(tm_graph *g);
+int tm_graph_info(const tm_graph *g, int32_t *n_nodes, int64_t *n_entries, int32_t *max_eid);
+/* host copy of node_idx_l / edge_idx_l / node_ts_l / off_set_l (utils/graph.py:23-27) and
+ * per-entry nodeedge2idx[owner][eid] raw value (may be negative, see get_ts2idx). */
+int tm_graph_export(const tm_graph *g, int64_t *off, int32_t *ngh, int32_t *eid, double *ts, int32_t *dict_val);
+
+/* ---------------------------------------------------------------- sampling (device)
+ * find_k_hop (utils/graph.py:233-262) + get_temporal_neighbor (:197-231) for B rows.
+ * Hop h (1..k) writes B*N^h entries at offset sum_{i<h} B*N^i of out_*; hop-h row r belongs
+ * to event event_ids[r / N^(h-1)], row-in-event r % N^(h-1), RNG stage h.
+ * eidx == NULL: hop 1 uses the time path (bisect_left on ts, :129); otherwise the
+ * e_idx path (:133); hops >= 2 always use the e_idx path (:247-250).
+ * *err_flag (device int32, may be NULL) is set to TM_E_EDGE_NOT_IN_LIST on a missing e_idx. */
+int tm_sample_khop(const tm_graph *g, tm_rng rng, int32_t k, int32_t N, int32_t B, const int32_t *root,
+                   const double *cut, const int32_t *eidx, const uint32_t *event_ids, int32_t *out_node,
+                   int32_t *out_eid, float *out_ts, int32_t *err_flag, void *stream);
+
+/* find_k_walks (utils/graph.py:265-306) = get_next_step (:308-333) + get_final_step (:335-476).
+ * h1_*: hop-1 results [B, N]; W = N*M walks per row.  Outputs node6 [B,W,6] = [s3,t3,s2,t2,s1,t1],
+ * eid3 [B,W,3] = [e3,e2,e1], ts3 [B,W,3], anony3 [B,W,3] (nullable), cat [B,W] (nullable,
+ * marginal's category id, processed/data_preprocess.py:171-178). */
+int tm_sample_walks(const tm_graph *g, tm_rng rng, int32_t N, int32_t M, int32_t B, const int32_t *root,
+                    const int32_t *h1_node, const int32_t *h1_eid, const float *h1_ts, const uint32_t *event_ids,
+                    int32_t *out_node6, int32_t *out_eid3, float *out_ts3, int32_t *out_anony3, int32_t *out_cat,
+                    void *stream);
+
+/* RandEdgeSampler.sample (utils/batch_loader.py:39-42): out[i] = list[draw(stage NEG, event_ids[i], row 0,
+ * draw j)]; j = 0 is the src draw (:40), j = 1 the dst draw (:41).  rng.side is ignored (NONE). */
+int tm_neg_sample(tm_rng rng, const int32_t *list, int64_t n_list, const uint32_t *event_ids, int32_t n, int32_t j,
+                  int32_t *out, void *stream);
+
+/* Sort keys of the keyed permutation that replaces np.random.permutation(n) in
+ * load_data_shuffle (utils/null_model.py:23): out_keys[i] = Philox word 0 of counter
+ * (i, split<<16 | STAGE_PERM, 0, 0); the permutation is the stable argsort of the keys. */
+int tm_perm_keys(uint64_t seed, uint32_t split, int64_t n, uint32_t *out_keys, void *stream);
+
+/* Motif histogram over n walks' anony codes [n,3].  null_order=0: marginal's category order
+ * (data_preprocess.py:171-193); 1: null-model key order (utils/null_model.py:90, key-1).
+ * hist12 (device u64[12]) is accumulated into (zero it first).  out_cat nullable. */
+int tm_motif_hist(const int32_t *anony3, int64_t n, int32_t null_order, int32_t *out_cat,
+                  unsigned long long *hist12, void *stream);
+
+/* new_edge_info (data_preprocess.py:327-343): cnt[g,w,p,q] = #{w' : eid3[g,w',q] == eid3[g,w,p]}. */
+int tm_edge_counts(const int32_t *eid3, int32_t n_groups, int32_t W, float *out_cnt, void *stream);
+
+/* Fused per-target-event sampler: what data_preprocess.py:106-134 + marginal's category id +
+ * new_edge_info do, for n_events events and all three sides (src, tgt, bgd) in one launch.
+ * Outputs are side-major: sub1_* [3,E,N], sub2_* [3,E,N*N], node6 [3,E,W,6], eid3 [3,E,W,3],
+ * ts3 [3,E,W,3], cat [3,E,W], cnt [3,E,W,3,3] (f32), dst_fake [E]; hist12 accumulates the
+ * category histogram (device u64[12], marginal order).  Bit-identical to the separate calls. */
+int tm_sample_events(const tm_graph *g, uint64_t seed, uint32_t split, int32_t N, int32_t M, int32_t n_events,
+                     const int32_t *src, const int32_t *dst, const double *ts, const int32_t *eidx,
+                     const uint32_t *event_ids, const int32_t *dst_list, int64_t n_dst, int32_t *dst_fake,
+                     int32_t *sub1_node, int32_t *sub1_eid, float *sub1_ts, int32_t *sub2_node, int32_t *sub2_eid,
+                     float *sub2_ts, int32_t *node6, int32_t *eid3, float *ts3, int32_t *cat, float *cnt,
+                     unsigned long long *hist12, int32_t *err_flag, void *stream);
+
+/* ---------------------------------------------------------------- encoder (device)
+ * Weights: the 28 fp32 tensors of TempME (models/explainer_new.py:103-171), row-major as
+ * nn.Linear stores them, in this order (DEVICE pointers):
+ *   0/1 event_conv.lin_event.{weight,bias}   2/3 event_conv.MLP.0   4/5 event_conv.MLP.2
+ *   6/7 attention.W1   8/9 attention.W2   10/11 attention.MLP.0   12/13 attention.MLP.3
+ *   14/15 MLP.0   16/17 MLP.3   18/19 MLP.5   20/21 edge_dependency_gcn.0   22/23 .3   24/25 .6
+ *   26 time_encoder.basis_freq   27 time_encoder.phase
+ * de = edge feature dim, dn = node feature dim (= time dim), h = hid_dim (64 supported). */
+#define TM_N_WEIGHTS 28
+int tm_weights_create(int32_t de, int32_t dn, int32_t h, int device, tm_weights **out);
+int tm_weights_pack(tm_weights *w, const float *const *tensors, void *stream);
+int tm_weights_free(tm_weights *w);
+
+/* Workspace bytes tm_encoder_fwd needs for n_walks walks. */
+int64_t tm_encoder_workspace_bytes(const tm_weights *w, int64_t n_walks);
+
+/* TempME.forward (explainer_new.py:174-201), eval, for n_groups groups of B*W walks each
+ * (one group = one reference call: one side of one batch; the attention's time std is
+ * batch-global per group, :828).  Walk arrays are [G,B,W,...]; cut [G,B] (f64, event time);
+ * cnt [G,B,W,3,3] f32.  out_imp [G,B,W] (graphlet importance, sigmoid output). */
+int tm_encoder_fwd(const tm_weights *w, const float *n_feat, const float *e_feat, int32_t n_groups, int32_t B,
+                   int32_t W, const int32_t *node6, const int32_t *eid3, const float *ts3, const int32_t *cat,
+                   const double *cut, const float *cnt, void *workspace, float *out_imp, void *stream);
+
+/* retrieve_edge_imp_node, eval (explainer_new.py:354-406, :420-430) for each of the G*B
+ * (group, event) rows: dependency gate, walk->edge scatter-max, gather at the subgraph eids,
+ * Beta mean, node==0 mask.  sub1_* [G,B,N], sub2_* [G,B,N*N]; out_h1 [G,B,N], out_h2 [G,B,N*N]
+ * (= the [3B,N] / [3B,N^2] of retrieve_explanation when G = the 3 sides of one batch). */
+int tm_edge_importance(const tm_weights *w, const float *e_feat, int32_t n_groups, int32_t B, int32_t W, int32_t N,
+                       const int32_t *eid3, const float *ts3, const float *imp, const int32_t *sub1_node,
+                       const int32_t *sub1_eid, const int32_t *sub2_node, const int32_t *sub2_eid, float *out_h1,
+                       float *out_h2, void *stream);
+
+/* ---------------------------------------------------------------- per-kernel timing
+ * tm_profile_enable(1) clears and starts recording a HIP event pair around every kernel
+ * launch, on that launch's stream; tm_profile_sync() waits and aggregates, returning the
+ * number of kernel names; tm_profile_entry(i) gives name, total ms and launch count. */
+int tm_profile_enable(int on);
+int tm_profile_sync(void);
+int tm_profile_entry(int i, const char **name, double *total_ms, int64_t *count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TEMPME_H_ */

@@ -1,0 +1,105 @@
+"""TEST INFRASTRUCTURE ONLY -- torch-fp32 CPU restatement of the TempME motif encoder.
+
+Functional restatement (no nn.Module) of models/explainer_new.py:
+  forward                 :174-201   (event features, event_gcn x2, attention, cat one-hot, MLP, sigmoid)
+  retrieve_time_features  :318-330   (dt relative to walk position 2, TimeEncode :45-59)
+  TemporalAwareAttention  :789-846   (batch-global unbiased std of |cut - t|)
+  retrieve_edge_imp_node  :354-406   (dependency gate, scatter-max walk->edge, gather, Beta mean, mask)
+  kl_loss                 :432-453   (empirical prior; null vector in null-model key order)
+Eval semantics only (dropout = identity, Beta mean instead of rsample).
+Pinned against tests/golden/encoder_uslegis.npz (outputs of the reference module).
+"""
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+
+def _lin(sd, name, x):
+    return F.linear(x, sd[name + ".weight"], sd[name + ".bias"])
+
+
+def time_encode(sd, t):
+    """TimeEncode.forward: cos(t * basis_freq + phase) in fp32 (explainer_new.py:51-59)."""
+    m = t.unsqueeze(-1) * sd["time_encoder.basis_freq"]
+    m = m + sd["time_encoder.phase"]
+    return torch.cos(m)
+
+
+def forward(sd, n_feat, e_feat, node, eid, ts, cat, cut, edge_count):
+    """graphlet importance [B, W, 1] for one side (explainer_new.py:174-201)."""
+    node = torch.as_tensor(np.asarray(node), dtype=torch.long)
+    eid = torch.as_tensor(np.asarray(eid), dtype=torch.long)
+    t = torch.as_tensor(np.asarray(ts, dtype=np.float64)).float()
+    cut = torch.as_tensor(np.asarray(cut, dtype=np.float64)).float()
+    cnt = torch.as_tensor(np.asarray(edge_count, dtype=np.float64)).float()
+    B, W = eid.shape[0], eid.shape[1]
+    ef = e_feat[eid]                                             # [B,W,3,de]
+    dt = t[:, :, 2:3] - t                                        # relative to position 2
+    tf = time_encode(sd, dt.reshape(B, -1)).reshape(B, W, 3, -1)
+    ev = torch.cat([ef, cnt, tf], dim=-1)
+    xs = n_feat[node[:, :, [0, 2, 4]]]
+    xt = n_feat[node[:, :, [1, 3, 5]]]
+    lev = _lin(sd, "event_conv.lin_event", ev)
+
+    def mlp(x):
+        return _lin(sd, "event_conv.MLP.2", torch.relu(_lin(sd, "event_conv.MLP.0", x)))
+    us = mlp(xs + torch.relu(xt + lev))
+    ut = mlp(xt + torch.relu(xs + lev))
+    f = torch.cat([us, ut], dim=-1)                              # [B,W,3,2h]
+    src = f[:, :, 2, :]
+    tgt = f[:, :, 0:2, :]
+    wp = _lin(sd, "attention.W1", src)                           # [B,W,2h]
+    wq = _lin(sd, "attention.W2", tgt)                           # [B,W,2,2h]
+    scores = (wp.unsqueeze(2) * wq).sum(-1)                      # [B,W,2]
+    diff = torch.abs(cut.view(B, 1, 1) - t[:, :, :2])
+    tw = torch.exp(-diff / (diff.std() + 1e-6))
+    scores = scores * (1.0 - 0.3 + 0.3 * tw)
+    alpha = torch.softmax(scores, dim=-1)
+    out = src + (alpha.unsqueeze(-1) * wq).sum(2)
+    out = _lin(sd, "attention.MLP.3", torch.relu(_lin(sd, "attention.MLP.0", out)))
+    oh = F.one_hot(torch.as_tensor(np.asarray(cat), dtype=torch.long).reshape(B, W), 12).float()
+    x = torch.cat([out, oh], dim=-1)
+    x = torch.relu(_lin(sd, "MLP.0", x))
+    x = torch.relu(_lin(sd, "MLP.3", x))
+    return torch.sigmoid(_lin(sd, "MLP.5", x))
+
+
+def beta_mean(p):
+    a = torch.clamp(p * 10, min=1.0)
+    b = torch.clamp((1 - p) * 10, min=1.0)
+    return a / (a + b)
+
+
+def edge_importance(sd, e_feat, imp, walk_eid, walk_ts, sub_node, sub_eid):
+    """retrieve_edge_imp_node, eval (explainer_new.py:354-406).  sub_*: [hop1 [B,N], hop2 [B,N^2]]."""
+    B = imp.shape[0]
+    ew = torch.as_tensor(np.asarray(walk_eid), dtype=torch.long).reshape(B, -1)
+    tw = torch.as_tensor(np.asarray(walk_ts, dtype=np.float64)).float().reshape(B, -1)
+    wimp = imp.repeat(1, 1, 3).view(B, -1)
+    g = torch.cat([e_feat[ew], time_encode(sd, tw)], dim=-1)
+    g = torch.relu(_lin(sd, "edge_dependency_gcn.0", g))
+    g = torch.relu(_lin(sd, "edge_dependency_gcn.3", g))
+    g = _lin(sd, "edge_dependency_gcn.6", g).squeeze(-1)
+    wimp = wimp * (0.5 + 0.5 * torch.sigmoid(g))
+    i0 = torch.as_tensor(np.asarray(sub_eid[0]), dtype=torch.long)
+    i1 = torch.as_tensor(np.asarray(sub_eid[1]), dtype=torch.long)
+    n_e = int(max(ew.max(), i0.max(), i1.max()) + 1)
+    dense = torch.zeros(B, n_e).scatter_reduce(-1, ew, wimp, "amax", include_self=False)
+    outs = []
+    for idx, nd in ((i0, sub_node[0]), (i1, sub_node[1])):
+        v = beta_mean(torch.gather(dense, -1, idx))
+        outs.append(v.masked_fill(torch.as_tensor(np.asarray(nd)) == 0, 0))
+    return outs
+
+
+def kl_loss(imp, cat, null_vec, target=0.3):
+    """kl_loss, prior='empirical' (explainer_new.py:432-448)."""
+    p = torch.clamp(imp, 1e-6, 1 - 1e-6)
+    B = p.shape[0]
+    s = p.mean(dim=1)                                            # [B,1]
+    c = torch.as_tensor(np.asarray(cat), dtype=torch.long).reshape(B, -1, 1)
+    emp = torch.zeros(B, 12, 1).scatter_reduce(1, c, p, "mean", include_self=False).reshape(B, 12)
+    emp = s * emp
+    null = target * torch.as_tensor(np.asarray(null_vec), dtype=torch.float32).reshape(-1, 12)
+    return ((1 - s) * torch.log((1 - s) / (1 - target + 1e-6) + 1e-6)
+            + emp * torch.log(emp / (null + 1e-6) + 1e-6)).mean()

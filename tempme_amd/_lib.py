@@ -1,0 +1,161 @@
+"""ctypes binding of libtempme_hip.so (the C ABI in include/tempme.h).
+
+The library is built in-tree (``tempme_amd/lib/libtempme_hip.so``, see
+``__graft_entry__.build()``).  There is no fallback: if the library is missing or
+no HIP device is visible, every entry point raises.
+
+``import torch`` happens before the library is loaded so that its
+``libamdhip64.so.7`` dependency binds to the HIP runtime torch already loaded
+(one runtime per process: torch's streams and device pointers are then valid in
+the library).
+"""
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libtempme_hip.so")
+
+TM_OK = 0
+TM_E_EDGE_NOT_IN_LIST = -1
+TM_E_SHAPE = -2
+TM_E_HIP = -3
+TM_E_ARG = -4
+TM_E_UNSUPPORTED = -5
+
+SIDE_NONE, SIDE_SRC, SIDE_TGT, SIDE_BGD = 0, 1, 2, 3
+SPLIT_TRAIN, SPLIT_TEST, SPLIT_NULL = 0, 1, 2
+N_WEIGHTS = 28
+
+# every symbol include/tempme.h declares
+EXPORTS = (
+    "tm_last_error", "tm_version", "tm_graph_build", "tm_graph_free", "tm_graph_info", "tm_graph_export",
+    "tm_sample_khop", "tm_sample_walks", "tm_neg_sample", "tm_perm_keys", "tm_motif_hist", "tm_edge_counts",
+    "tm_sample_events", "tm_weights_create", "tm_weights_pack", "tm_weights_free", "tm_encoder_workspace_bytes",
+    "tm_encoder_fwd", "tm_edge_importance", "tm_profile_enable", "tm_profile_sync", "tm_profile_entry",
+)
+
+
+class TmRng(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("split", C.c_uint32), ("side", C.c_uint32)]
+
+
+class TempMEError(RuntimeError):
+    pass
+
+
+_lib = None
+vp = C.c_void_p
+i32, i64, u32, u64 = C.c_int32, C.c_int64, C.c_uint32, C.c_uint64
+
+
+def _sig(L):
+    L.tm_last_error.restype = C.c_char_p
+    L.tm_version.restype = C.c_int
+    L.tm_graph_build.argtypes = [i32, vp, vp, vp, vp, C.c_int, C.POINTER(vp)]
+    L.tm_graph_free.argtypes = [vp]
+    L.tm_graph_info.argtypes = [vp, C.POINTER(i32), C.POINTER(i64), C.POINTER(i32)]
+    L.tm_graph_export.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.tm_sample_khop.argtypes = [vp, TmRng, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.tm_sample_walks.argtypes = [vp, TmRng, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.tm_neg_sample.argtypes = [TmRng, vp, i64, vp, i32, i32, vp, vp]
+    L.tm_perm_keys.argtypes = [u64, u32, i64, vp, vp]
+    L.tm_motif_hist.argtypes = [vp, i64, i32, vp, vp, vp]
+    L.tm_edge_counts.argtypes = [vp, i32, i32, vp, vp]
+    L.tm_sample_events.argtypes = [vp, u64, u32, i32, i32, i32, vp, vp, vp, vp, vp, vp, i64] + [vp] * 17
+    L.tm_weights_create.argtypes = [i32, i32, i32, C.c_int, C.POINTER(vp)]
+    L.tm_weights_pack.argtypes = [vp, C.POINTER(vp), vp]
+    L.tm_weights_free.argtypes = [vp]
+    L.tm_encoder_workspace_bytes.restype = i64
+    L.tm_encoder_workspace_bytes.argtypes = [vp, i64]
+    L.tm_encoder_fwd.argtypes = [vp, vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.tm_edge_importance.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.tm_profile_enable.argtypes = [C.c_int]
+    L.tm_profile_entry.argtypes = [C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(i64)]
+    for name in EXPORTS:
+        if name not in ("tm_last_error", "tm_encoder_workspace_bytes"):
+            getattr(L, name).restype = C.c_int
+
+
+def lib():
+    """The loaded library; raises if it was not built (no fallback path exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"tempme_amd: HIP library not built ({LIB_PATH} missing); run __graft_entry__.build() "
+                "or `make -C tempme_amd/csrc`")
+        L = C.CDLL(LIB_PATH)
+        _sig(L)
+        _lib = L
+    return _lib
+
+
+def check(rc, what=""):
+    """Map a TM_E_* code to the exception type the reference raises for the same condition."""
+    if rc == TM_OK:
+        return
+    msg = lib().tm_last_error().decode(errors="replace")
+    if rc == TM_E_EDGE_NOT_IN_LIST:
+        raise IndexError(msg or f"{what}: e_idx not found in edge list")
+    if rc == TM_E_SHAPE:
+        raise AssertionError(msg or what)
+    if rc in (TM_E_ARG,):
+        raise ValueError(f"{what}: {msg}")
+    if rc == TM_E_UNSUPPORTED:
+        raise NotImplementedError(f"{what}: {msg}")
+    raise TempMEError(f"{what}: {msg} (code {rc})")
+
+
+def raise_device_error(code, what):
+    """Device-side error flag (set by the kernels) -> reference exception."""
+    if code == 0:
+        return
+    if code == TM_E_EDGE_NOT_IN_LIST:
+        raise IndexError(f"{what}: e_idx not found in edge list of its node (utils/graph.py:134-135)")
+    if code == TM_E_ARG:
+        raise IndexError(f"{what}: node index out of range")
+    raise TempMEError(f"{what}: device error {code}")
+
+
+def ptr(t):
+    """Raw device (or host) pointer of a torch tensor, None for None."""
+    if t is None:
+        return None
+    return C.c_void_p(t.data_ptr())
+
+
+def stream_ptr(device=None):
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_device(device=None):
+    """The torch.device the hot path runs on.  Fails loudly without a HIP GPU."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("tempme_amd: no HIP device visible; the hot path has no CPU fallback")
+    if device is None:
+        return torch.device("cuda", torch.cuda.current_device())
+    device = torch.device(device)
+    if device.type != "cuda":
+        raise RuntimeError(f"tempme_amd: device {device} is not a HIP device; the hot path has no CPU fallback")
+    if device.index is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    return device
+
+
+def profile_enable(on=True):
+    check(lib().tm_profile_enable(1 if on else 0), "tm_profile_enable")
+
+
+def profile_read():
+    """{kernel name: (total_ms, launches)} recorded since profile_enable(True)."""
+    n = lib().tm_profile_sync()
+    if n < 0:
+        check(n, "tm_profile_sync")
+    out = {}
+    for i in range(n):
+        name, ms, cnt = C.c_char_p(), C.c_double(), i64()
+        check(lib().tm_profile_entry(i, C.byref(name), C.byref(ms), C.byref(cnt)), "tm_profile_entry")
+        out[name.value.decode()] = (ms.value, cnt.value)
+    return out

@@ -1,0 +1,147 @@
+// Shared internals of libtempme_hip.so (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/tempme.h"
+
+namespace tmk {
+
+void set_error(const std::string &msg);
+int fail(int code, const std::string &msg);
+
+// per-kernel HIP-event timing (prof.cpp); no-ops unless tm_profile_enable(1)
+hipEvent_t prof_begin(hipStream_t s);
+void prof_end(const char *name, hipStream_t s, hipEvent_t a);
+
+#define TM_HIP(expr)                                                                            \
+    do {                                                                                        \
+        hipError_t _e = (expr);                                                                 \
+        if (_e != hipSuccess)                                                                   \
+            return ::tmk::fail(TM_E_HIP, std::string(#expr ": ") + hipGetErrorString(_e));       \
+    } while (0)
+
+#define TM_CHECK_LAUNCH()                                                                       \
+    do {                                                                                        \
+        hipError_t _e = hipGetLastError();                                                      \
+        if (_e != hipSuccess)                                                                   \
+            return ::tmk::fail(TM_E_HIP, std::string("kernel launch: ") + hipGetErrorString(_e)); \
+    } while (0)
+
+// ------------------------------------------------------------------ device graph layout
+// One 16-byte record per adjacency entry, so a sampled slot is one dwordx4 load.
+struct __attribute__((aligned(16))) Rec {
+    int32_t ngh;
+    int32_t eid;
+    double ts;
+};
+
+// e_idx -> (owner, slice length) for the (at most two) owners of an edge id.
+// len = length of neighbors[:nodeedge2idx[owner][eid]] (the dict value, clamped the way
+// Python slicing treats a negative stop).  node = -1: absent.
+struct __attribute__((aligned(16))) EdgeEnds {
+    int32_t node_a, len_a, node_b, len_b;
+};
+
+// Pair index: each node's entries re-sorted by (neighbor, position); 8 bytes.
+struct __attribute__((aligned(8))) Pair {
+    int32_t ngh;
+    int32_t pos;
+};
+
+struct DevGraph {
+    int32_t n_nodes;
+    int32_t max_eid;
+    int64_t n_entries;
+    const int32_t *off;     // [V+1]
+    const Rec *rec;         // [n_entries]
+    const EdgeEnds *ends;   // [max_eid+1]
+    const Pair *pair;       // [n_entries]
+};
+
+// ------------------------------------------------------------------ Philox4x32-10
+__device__ __forceinline__ uint32_t philox_word(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                                uint32_t k1, uint32_t w) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0;
+        c1 = lo1;
+        c2 = n2;
+        c3 = lo0;
+    }
+    return w == 0 ? c0 : w == 1 ? c1 : w == 2 ? c2 : c3;
+}
+
+struct Key {
+    uint32_t k0, k1, tagbase;  // tagbase = split << 16 | side << 8
+};
+
+__host__ __device__ inline Key make_key(uint64_t seed, uint32_t split, uint32_t side) {
+    return Key{(uint32_t)seed, (uint32_t)(seed >> 32), (split << 16) | (side << 8)};
+}
+
+// draw in [0, high) for (stage, event, row, j)
+__device__ __forceinline__ int32_t draw(Key k, uint32_t stage, uint32_t event, uint32_t row, uint32_t j,
+                                        uint32_t high) {
+    uint32_t u = philox_word(event, k.tagbase | stage, row, j >> 2, k.k0, k.k1, j & 3);
+    return (int32_t)(((uint64_t)u * (uint64_t)high) >> 32);
+}
+
+// ------------------------------------------------------------------ lookups
+// nodeedge2idx[u].get(e): slice length, or -1 for None
+__device__ __forceinline__ int32_t edge_len(const DevGraph &g, int32_t u, int32_t e) {
+    if (e < 0 || e > g.max_eid) return -1;
+    EdgeEnds x = g.ends[e];
+    if (x.node_a == u) return x.len_a;
+    if (x.node_b == u) return x.len_b;
+    return -1;
+}
+
+__device__ __forceinline__ int32_t deg(const DevGraph &g, int32_t u) { return g.off[u + 1] - g.off[u]; }
+
+// bisect_left over node u's f64 timestamps (utils/graph.py:511-530)
+__device__ __forceinline__ int32_t bisect_ts(const DevGraph &g, int32_t u, double x) {
+    int32_t s = g.off[u], lo = 0, hi = g.off[u + 1] - s;
+    while (lo < hi) {
+        int32_t mid = (lo + hi) >> 1;
+        if (g.rec[s + mid].ts < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// first index in node u's pair list with (ngh, pos) >= (x, p)
+__device__ __forceinline__ int32_t pair_lb(const DevGraph &g, int32_t u, int32_t x, int32_t p) {
+    int32_t lo = g.off[u], hi = g.off[u + 1];
+    while (lo < hi) {
+        int32_t mid = (lo + hi) >> 1;
+        Pair q = g.pair[mid];
+        if (q.ngh < x || (q.ngh == x && q.pos < p)) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+}  // namespace tmk
+
+struct tm_graph {
+    int device;
+    tmk::DevGraph d;
+    // device allocations
+    int32_t *d_off;
+    tmk::Rec *d_rec;
+    tmk::EdgeEnds *d_ends;
+    tmk::Pair *d_pair;
+    // host copies (export)
+    int64_t *h_off;
+    int32_t *h_ngh, *h_eid, *h_dict;
+    double *h_ts;
+};

@@ -1,0 +1,629 @@
+// TempME motif encoder + edge-importance retrieval on gfx950 (fp32 MFMA, v_mfma_f32_16x16x4_f32).
+//
+// Reference (dharunm236/TempME, models/explainer_new.py):
+//   forward :174-201  event features (:176-179, time :318-330, TimeEncode :45-59), node features
+//                     (:343-352), event_gcn x2 (:79-96, lin_event shared), TemporalAwareAttention
+//                     (:789-846, batch-global std :828), one-hot category (:308-315), MLP + sigmoid
+//   retrieve_edge_imp_node :354-406 (dependency gate :367-386, scatter-max :389, gather :392-393,
+//                     beta_sample eval :420-430, padding mask :400-404)
+//
+// Kernels (one launch each):
+//   std_kernel      per group: unbiased std of |cut - t| over the [B,W,2] walk times (f64 accumulate)
+//   gcn_kernel      per 32 walk-positions: [E(e)|cnt|cos(dt*w+phi)] -> lin_event -> (A,B) -> MLP -> F rows
+//   head_kernel     per 32 walks: W1/W2 attention with temporal scaling, softmax, MLP, one-hot, MLP, sigmoid
+//   explain_kernel  per (group, event): dependency-gate MLP, LDS hash scatter-max over walk edge ids,
+//                   gather at subgraph edge ids, Beta mean, node==0 mask
+// Every dense projection runs on MFMA with the packed weight stream read from L2 and the
+// activations staged in LDS (row stride K16+8 floats: conflict-free ds_read_b128).
+#include <vector>
+
+#include "common.h"
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+namespace tmk {
+
+constexpr int HID = 64;   // hid_dim supported by this build (reference default --hid_dim 64)
+constexpr int TILE_ROWS = 32;
+
+__host__ __device__ constexpr int r16(int x) { return (x + 15) & ~15; }
+
+struct Lin {
+    const float4 *w;  // packed [nt][nq][64 lanes] float4
+    const float *b;   // [nt*16] zero padded
+    int nt, nq, nout, k;
+};
+
+struct EncW {
+    int de, dn, kev, kdep;
+    Lin ev, g1, g2, w1, w2, a1, a2, m1, m2, d1, d2;
+    const float *m3w, *m3b, *d3w, *d3b, *freq, *phase;
+};
+
+// ------------------------------------------------------------------ MFMA tile GEMM
+// out[16mt.., 16nt..] = X[rows][ldx] (LDS) * W^T for tiles t = wave*2, wave*2+1, ... ; the
+// epilogue gets (mt, nt, acc) with acc[r] = D[4*(lane>>4)+r][lane&15].
+template <class Epi>
+__device__ __forceinline__ void gemm(const float *X, int ldx, const Lin &L, int MT, Epi epi) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int arow = lane & 15, akoff = 4 * (lane >> 4);
+    const int T = MT * L.nt, nq = L.nq;
+    for (int t = wave * 2; t < T; t += nw * 2) {
+        const int t1 = t + 1;
+        const bool has1 = t1 < T;
+        const int mt0 = t / L.nt, nt0 = t % L.nt, mt1 = has1 ? t1 / L.nt : mt0, nt1 = has1 ? t1 % L.nt : nt0;
+        floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+        const float *xa0 = X + (mt0 * 16 + arow) * ldx + akoff;
+        const float *xa1 = X + (mt1 * 16 + arow) * ldx + akoff;
+        const float4 *wb0 = L.w + (size_t)nt0 * nq * 64 + lane;
+        const float4 *wb1 = L.w + (size_t)nt1 * nq * 64 + lane;
+        for (int q = 0; q < nq; ++q) {
+            const float4 b0 = wb0[q * 64], b1 = wb1[q * 64];
+            const float4 a0 = *reinterpret_cast<const float4 *>(xa0 + 16 * q);
+            const float4 a1 = *reinterpret_cast<const float4 *>(xa1 + 16 * q);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, b0.x, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, b1.x, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, b0.y, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, b1.y, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, b0.z, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, b1.z, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, b0.w, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, b1.w, acc1, 0, 0, 0);
+        }
+        epi(mt0, nt0, acc0);
+        if (has1) epi(mt1, nt1, acc1);
+    }
+}
+
+__device__ __forceinline__ int erow(int mt, int r) { return mt * 16 + 4 * ((threadIdx.x & 63) >> 4) + r; }
+__device__ __forceinline__ int ecol(int nt) { return nt * 16 + (threadIdx.x & 15); }
+
+// cos(t * w + phi) with the multiply and add rounded separately, as torch does
+// (TimeEncode.forward, explainer_new.py:56-58); never contracted into an fma.
+__device__ __forceinline__ float time_cos(float t, float w, float phi) { return cosf(__fadd_rn(__fmul_rn(t, w), phi)); }
+
+__device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
+
+// ------------------------------------------------------------------ std over |cut - t| per group
+__global__ void __launch_bounds__(256) std_kernel(int32_t B, int32_t W, const double *__restrict__ cut,
+                                                  const float *__restrict__ ts3, float *__restrict__ std_out) {
+    __shared__ double red[256];
+    const int64_t g = blockIdx.x, n = (int64_t)B * W * 2;
+    const float *t = ts3 + g * (int64_t)B * W * 3;
+    double s = 0.0;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const int64_t w = i >> 1, b = w / W;
+        const float c = (float)cut[g * B + b];
+        s += (double)fabsf(c - t[w * 3 + (i & 1)]);
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
+    }
+    const double mean = red[0] / (double)n;
+    __syncthreads();
+    double v = 0.0;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const int64_t w = i >> 1, b = w / W;
+        const float c = (float)cut[g * B + b];
+        const double d = (double)fabsf(c - t[w * 3 + (i & 1)]) - mean;
+        v += d * d;
+    }
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) std_out[g] = n > 1 ? (float)sqrt(red[0] / (double)(n - 1)) : __builtin_nanf("");
+}
+
+// ------------------------------------------------------------------ event_gcn: 32 walk-positions per block
+// F[row] = [MLP(x_s + relu(x_t + L)) | MLP(x_t + relu(x_s + L))],  L = lin_event([E(e) | cnt | cos(dt)])
+__global__ void __launch_bounds__(256) gcn_kernel(EncW P, int64_t n_rows, const float *__restrict__ n_feat,
+                                                  const float *__restrict__ e_feat, const int32_t *__restrict__ node6,
+                                                  const int32_t *__restrict__ eid3, const float *__restrict__ ts3,
+                                                  const float *__restrict__ cnt, float *__restrict__ F) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int de = P.de, dn = P.dn, kev = P.kev, kev16 = r16(kev), dn16 = r16(dn);
+    const int ldx = kev16 + 8, ldab = dn16 + 8, ldh = HID + 8;
+    const int xsz = max(TILE_ROWS * ldx, 2 * TILE_ROWS * ldh);
+    float *X = smem;                                  // [32][ldx]      event features
+    float *AB = X + xsz;                              // [64][ldab]     A rows 0..31, B rows 32..63
+    float *H = X;                                     // [64][ldh]      aliases X after lin_event
+    __shared__ int32_t s_eid[TILE_ROWS], s_ns[TILE_ROWS], s_nt[TILE_ROWS];
+    __shared__ float s_dt[TILE_ROWS], s_cnt[TILE_ROWS * 3];
+    const int64_t row0 = (int64_t)blockIdx.x * TILE_ROWS;
+    const int tid = threadIdx.x;
+    if (tid < TILE_ROWS) {
+        const int64_t r = row0 + tid;
+        if (r < n_rows) {
+            const int64_t w = r / 3;
+            const int p = (int)(r % 3);
+            s_eid[tid] = eid3[w * 3 + p];
+            s_ns[tid] = node6[w * 6 + 2 * p];       // src nodes: columns 0, 2, 4 (:348)
+            s_nt[tid] = node6[w * 6 + 2 * p + 1];   // tgt nodes: columns 1, 3, 5 (:349)
+            s_dt[tid] = ts3[w * 3 + 2] - ts3[w * 3 + p];   // relative to walk position 2 (:326)
+            for (int q = 0; q < 3; ++q) s_cnt[tid * 3 + q] = cnt[w * 9 + p * 3 + q];
+        } else {
+            s_eid[tid] = 0; s_ns[tid] = 0; s_nt[tid] = 0; s_dt[tid] = 0.f;
+            for (int q = 0; q < 3; ++q) s_cnt[tid * 3 + q] = 0.f;
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < TILE_ROWS * kev16; i += blockDim.x) {
+        const int r = i / kev16, c = i % kev16;
+        float v = 0.f;
+        if (row0 + r < n_rows) {
+            if (c < de) v = e_feat[(int64_t)s_eid[r] * de + c];
+            else if (c < de + 3) v = s_cnt[r * 3 + (c - de)];
+            else if (c < kev) v = time_cos(s_dt[r], P.freq[c - de - 3], P.phase[c - de - 3]);
+        }
+        X[r * ldx + c] = v;
+    }
+    __syncthreads();
+    // L = lin_event(X); A = x_s + relu(x_t + L); B = x_t + relu(x_s + L)
+    gemm(X, ldx, P.ev, 2, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) {
+            const int row = erow(mt, r);
+            float a = 0.f, b = 0.f;
+            if (c < dn) {
+                const float L = acc[r] + P.ev.b[c];
+                const float xs = n_feat[(int64_t)s_ns[row] * dn + c], xt = n_feat[(int64_t)s_nt[row] * dn + c];
+                a = xs + relu(xt + L);
+                b = xt + relu(xs + L);
+            }
+            AB[row * ldab + c] = a;
+            AB[(row + TILE_ROWS) * ldab + c] = b;
+        }
+    });
+    __syncthreads();
+    gemm(AB, ldab, P.g1, 4, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) H[erow(mt, r) * ldh + c] = relu(acc[r] + P.g1.b[c]);
+    });
+    __syncthreads();
+    gemm(H, ldh, P.g2, 4, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) {
+            const int row = erow(mt, r);
+            const int rr = row & (TILE_ROWS - 1), half = row >> 5;
+            const int64_t gr = row0 + rr;
+            if (gr < n_rows) F[gr * (2 * HID) + half * HID + c] = acc[r] + P.g2.b[c];
+        }
+    });
+}
+
+// ------------------------------------------------------------------ attention head + final MLP: 32 walks per block
+__global__ void __launch_bounds__(256) head_kernel(EncW P, int64_t n_walks, int64_t walks_per_group, int32_t W,
+                                                   const float *__restrict__ F, const float *__restrict__ ts3,
+                                                   const double *__restrict__ cut, const int32_t *__restrict__ cat,
+                                                   const float *__restrict__ stdv, float *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int D2 = 2 * HID, LD = D2 + 8, LDM = r16(HID + 12) + 8, LDH = HID + 8;
+    float *T = smem;                  // [64][LD]  positions 0,1 (rows p*32 + w)  -> later S, P
+    float *Q = T + 2 * TILE_ROWS * LD;  // [64][LD]  W2(tgt)
+    float *S = T;                     // [32][LD]  position 2
+    float *Pp = T + TILE_ROWS * LD;   // [32][LD]  W1(src) -> later O
+    float *H1 = Q;                    // [32][LDH]
+    float *X = S;                     // [32][LDM]
+    float *M1 = Pp;                   // [32][LDM]
+    float *M2 = Q;                    // [32][LDH]
+    __shared__ float s_score[TILE_ROWS * 2], s_tw[TILE_ROWS * 2], s_alpha[TILE_ROWS * 2];
+    __shared__ int32_t s_cat[TILE_ROWS];
+    const int64_t w0 = (int64_t)blockIdx.x * TILE_ROWS;
+    const int tid = threadIdx.x;
+    // stage positions 0,1
+    for (int i = tid; i < 2 * TILE_ROWS * (D2 / 4); i += blockDim.x) {
+        const int row = i / (D2 / 4), c4 = i % (D2 / 4), p = row / TILE_ROWS, w = row % TILE_ROWS;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (w0 + w < n_walks) v = reinterpret_cast<const float4 *>(F + ((w0 + w) * 3 + p) * D2)[c4];
+        *reinterpret_cast<float4 *>(T + row * LD + 4 * c4) = v;
+    }
+    if (tid < TILE_ROWS * 2) {
+        const int w = tid >> 1, p = tid & 1;
+        const int64_t gw = w0 + w;
+        float tw = 0.f;
+        if (gw < n_walks) {
+            const int64_t g = gw / walks_per_group, b = (gw % walks_per_group) / W;
+            const float c = (float)cut[g * (walks_per_group / W) + b];
+            const float diff = fabsf(c - ts3[gw * 3 + p]);
+            tw = expf(-diff / (stdv[g] + 1e-6f));
+        }
+        s_tw[tid] = tw;
+    }
+    if (tid < TILE_ROWS) s_cat[tid] = (w0 + tid < n_walks) ? cat[w0 + tid] : -1;
+    __syncthreads();
+    gemm(T, LD, P.w2, 4, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) Q[erow(mt, r) * LD + c] = acc[r] + P.w2.b[c];
+    });
+    __syncthreads();
+    // stage position 2 into S (T is dead)
+    for (int i = tid; i < TILE_ROWS * (D2 / 4); i += blockDim.x) {
+        const int w = i / (D2 / 4), c4 = i % (D2 / 4);
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (w0 + w < n_walks) v = reinterpret_cast<const float4 *>(F + ((w0 + w) * 3 + 2) * D2)[c4];
+        *reinterpret_cast<float4 *>(S + w * LD + 4 * c4) = v;
+    }
+    __syncthreads();
+    gemm(S, LD, P.w1, 2, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) Pp[erow(mt, r) * LD + c] = acc[r] + P.w1.b[c];
+    });
+    __syncthreads();
+    // scores[w][p] = <W1 src, W2 tgt_p>, 4 lanes per dot product
+    {
+        const int pair = tid >> 2, sub = tid & 3, w = pair >> 1, p = pair & 1;
+        float s = 0.f;
+        for (int c = sub; c < D2; c += 4) s += Pp[w * LD + c] * Q[(p * TILE_ROWS + w) * LD + c];
+        s += __shfl_xor(s, 1, 4);
+        s += __shfl_xor(s, 2, 4);
+        if (sub == 0) {
+            // scores * (1.0 - 0.3 + 0.3 * time_weight)   (:835-836)
+            const float m = __fadd_rn(0.7f, __fmul_rn(0.3f, s_tw[pair]));
+            s_score[pair] = s * m;
+        }
+    }
+    __syncthreads();
+    if (tid < TILE_ROWS) {
+        const float s0 = s_score[2 * tid], s1 = s_score[2 * tid + 1], mx = fmaxf(s0, s1);
+        const float e0 = expf(s0 - mx), e1 = expf(s1 - mx), sum = e0 + e1;
+        s_alpha[2 * tid] = e0 / sum;
+        s_alpha[2 * tid + 1] = e1 / sum;
+    }
+    __syncthreads();
+    // O = src + alpha . Wq   (into Pp)
+    for (int i = tid; i < TILE_ROWS * D2; i += blockDim.x) {
+        const int w = i / D2, c = i % D2;
+        const float o = s_alpha[2 * w] * Q[w * LD + c] + s_alpha[2 * w + 1] * Q[(TILE_ROWS + w) * LD + c];
+        Pp[w * LD + c] = S[w * LD + c] + o;
+    }
+    __syncthreads();
+    gemm(Pp, LD, P.a1, 2, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) H1[erow(mt, r) * LDH + c] = relu(acc[r] + P.a1.b[c]);
+    });
+    __syncthreads();
+    // X = [attention MLP out | one-hot(cat)]
+    gemm(H1, LDH, P.a2, 2, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) X[erow(mt, r) * LDM + c] = acc[r] + P.a2.b[c];
+    });
+    for (int i = tid; i < TILE_ROWS * 16; i += blockDim.x) {
+        const int w = i >> 4, c = i & 15;
+        X[w * LDM + HID + c] = (c < 12 && s_cat[w] == c) ? 1.f : 0.f;
+    }
+    __syncthreads();
+    gemm(X, LDM, P.m1, 2, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) M1[erow(mt, r) * LDM + c] = c < P.m1.nout ? relu(acc[r] + P.m1.b[c]) : 0.f;
+    });
+    __syncthreads();
+    gemm(M1, LDM, P.m2, 2, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) M2[erow(mt, r) * LDH + c] = relu(acc[r] + P.m2.b[c]);
+    });
+    __syncthreads();
+    {
+        const int w = tid >> 3, sub = tid & 7;
+        float s = 0.f;
+        for (int c = sub; c < HID; c += 8) s += M2[w * LDH + c] * P.m3w[c];
+        s += __shfl_xor(s, 1, 8);
+        s += __shfl_xor(s, 2, 8);
+        s += __shfl_xor(s, 4, 8);
+        if (sub == 0 && w0 + w < n_walks) {
+            const float z = s + P.m3b[0];
+            out[w0 + w] = 1.f / (1.f + expf(-z));
+        }
+    }
+}
+
+// ------------------------------------------------------------------ edge importance: one block per (group, event)
+__device__ __forceinline__ uint32_t hash_eid(int32_t e) { return (uint32_t)e * 0x9E3779B1u; }
+
+__global__ void __launch_bounds__(256) explain_kernel(EncW P, int32_t W, int32_t N, int32_t hbits,
+                                                      const float *__restrict__ e_feat, const int32_t *__restrict__ eid3,
+                                                      const float *__restrict__ ts3, const float *__restrict__ imp,
+                                                      const int32_t *__restrict__ sub1_node,
+                                                      const int32_t *__restrict__ sub1_eid,
+                                                      const int32_t *__restrict__ sub2_node,
+                                                      const int32_t *__restrict__ sub2_eid, float *__restrict__ out1,
+                                                      float *__restrict__ out2) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int de = P.de, kdep = P.kdep, kd16 = r16(kdep), ldx = kd16 + 8, ldg = HID + 8,
+              ldg2 = HID / 2 + 8;
+    const int hsize = 1 << hbits;
+    float *X = smem;                       // [32][ldx]
+    float *G1 = X + TILE_ROWS * ldx;       // [32][ldg]
+    float *G2 = G1 + TILE_ROWS * ldg;      // [32][ldg2]
+    int32_t *hkey = reinterpret_cast<int32_t *>(G2 + TILE_ROWS * ldg2);   // [hsize]
+    uint32_t *hval = reinterpret_cast<uint32_t *>(hkey + hsize);         // [hsize] float bits
+    __shared__ int32_t s_eid[TILE_ROWS];
+    __shared__ float s_t[TILE_ROWS];
+    const int64_t ge = blockIdx.x;         // (group, event) row
+    const int tid = threadIdx.x, nrow = 3 * W;
+    const int32_t *e3 = eid3 + ge * (int64_t)W * 3;
+    const float *t3 = ts3 + ge * (int64_t)W * 3;
+    for (int i = tid; i < hsize; i += blockDim.x) {
+        hkey[i] = -1;
+        hval[i] = 0u;
+    }
+    for (int c0 = 0; c0 < nrow; c0 += TILE_ROWS) {
+        __syncthreads();
+        if (tid < TILE_ROWS) {
+            const int r = c0 + tid;
+            s_eid[tid] = r < nrow ? e3[r] : 0;
+            s_t[tid] = r < nrow ? t3[r] : 0.f;   // raw event time (:371), not dt
+        }
+        __syncthreads();
+        for (int i = tid; i < TILE_ROWS * kd16; i += blockDim.x) {
+            const int r = i / kd16, c = i % kd16;
+            float v = 0.f;
+            if (c0 + r < nrow) {
+                if (c < de) v = e_feat[(int64_t)s_eid[r] * de + c];
+                else if (c < kdep) v = time_cos(s_t[r], P.freq[c - de], P.phase[c - de]);
+            }
+            X[r * ldx + c] = v;
+        }
+        __syncthreads();
+        gemm(X, ldx, P.d1, 2, [&](int mt, int nt, floatx4 acc) {
+            const int c = ecol(nt);
+            for (int r = 0; r < 4; ++r) G1[erow(mt, r) * ldg + c] = relu(acc[r] + P.d1.b[c]);
+        });
+        __syncthreads();
+        gemm(G1, ldg, P.d2, 2, [&](int mt, int nt, floatx4 acc) {
+            const int c = ecol(nt);
+            for (int r = 0; r < 4; ++r) G2[erow(mt, r) * ldg2 + c] = relu(acc[r] + P.d2.b[c]);
+        });
+        __syncthreads();
+        {
+            const int r = tid >> 3, sub = tid & 7;
+            float s = 0.f;
+            for (int c = sub; c < HID / 2; c += 8) s += G2[r * ldg2 + c] * P.d3w[c];
+            s += __shfl_xor(s, 1, 8);
+            s += __shfl_xor(s, 2, 8);
+            s += __shfl_xor(s, 4, 8);
+            const int gr = c0 + r;
+            if (sub == 0 && gr < nrow) {
+                const float z = s + P.d3b[0];
+                const float gate = 1.f / (1.f + expf(-z));
+                // walk_imp = graphlet_imp (repeated over 3 positions) * (0.5 + 0.5 * gate)   (:364, :386)
+                const float v = imp[ge * W + gr / 3] * (0.5f + 0.5f * gate);
+                const int32_t key = s_eid[r];
+                uint32_t h = hash_eid(key) >> (32 - hbits);
+                while (true) {
+                    const int32_t prev = atomicCAS(&hkey[h], -1, key);
+                    if (prev == -1 || prev == key) break;
+                    h = (h + 1) & (hsize - 1);
+                }
+                atomicMax(&hval[h], __float_as_uint(v));   // v >= 0: uint order == float order
+            }
+        }
+    }
+    __syncthreads();
+    // gather at the subgraph edge ids, Beta mean (eval), padding mask
+    const int n1 = N, n2 = N * N;
+    for (int i = tid; i < n1 + n2; i += blockDim.x) {
+        const bool h1 = i < n1;
+        const int64_t o = h1 ? ge * n1 + i : ge * n2 + (i - n1);
+        const int32_t key = h1 ? sub1_eid[o] : sub2_eid[o];
+        const int32_t nd = h1 ? sub1_node[o] : sub2_node[o];
+        uint32_t h = hash_eid(key) >> (32 - hbits);
+        float p = 0.f;   // edges no walk touched: scatter fill value 0
+        while (true) {
+            const int32_t k = hkey[h];
+            if (k == key) {
+                p = __uint_as_float(hval[h]);
+                break;
+            }
+            if (k == -1) break;
+            h = (h + 1) & (hsize - 1);
+        }
+        const float a = fmaxf(p * 10.f, 1.f), b = fmaxf((1.f - p) * 10.f, 1.f);
+        const float v = nd == 0 ? 0.f : a / (a + b);
+        if (h1) out1[o] = v;
+        else out2[o] = v;
+    }
+}
+
+// ------------------------------------------------------------------ weight packing
+// packed[((nt*nq + q)*64 + l)*4 + s] = W[16nt + (l&15)][16q + 4(l>>4) + s]
+__global__ void pack_kernel(const float *__restrict__ W, int nout, int k, int nt, int nq, float *__restrict__ out) {
+    const int64_t n = (int64_t)nt * nq * 256;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int s = i & 3, l = (i >> 2) & 63;
+        const int64_t tq = i >> 8;
+        const int q = (int)(tq % nq), t = (int)(tq / nq);
+        const int o = 16 * t + (l & 15), c = 16 * q + 4 * (l >> 4) + s;
+        out[i] = (o < nout && c < k) ? W[(int64_t)o * k + c] : 0.f;
+    }
+}
+
+__global__ void copy_pad_kernel(const float *__restrict__ src, int n, int npad, float *__restrict__ dst) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < npad; i += gridDim.x * blockDim.x) dst[i] = i < n ? src[i] : 0.f;
+}
+
+}  // namespace tmk
+
+using namespace tmk;
+
+struct tm_weights {
+    int device;
+    int de, dn, h;
+    float *buf;
+    size_t n_floats;
+    EncW P;
+    // per linear: raw tensor index, nout, k
+    struct Spec {
+        Lin *lin;
+        int wi, nout, k;
+    };
+    std::vector<Spec> specs;
+    std::vector<std::pair<int, float **>> vecs;
+};
+
+static inline hipStream_t S_(void *s) { return (hipStream_t)s; }
+
+extern "C" int tm_weights_create(int32_t de, int32_t dn, int32_t h, int device, tm_weights **out) {
+    if (!out || de <= 0 || dn <= 0) return fail(TM_E_ARG, "tm_weights_create: bad arguments");
+    if (h != HID) return fail(TM_E_UNSUPPORTED, "tm_weights_create: hid_dim must be 64 in this build");
+    *out = nullptr;
+    tm_weights *w = new tm_weights();
+    w->device = device;
+    w->de = de;
+    w->dn = dn;
+    w->h = h;
+    EncW &P = w->P;
+    P.de = de;
+    P.dn = dn;
+    P.kev = de + 3 + dn;
+    P.kdep = de + dn;
+    const int h2 = 2 * h, hm = h + 12;
+    struct L {
+        Lin *lin;
+        int wi, nout, k;
+    } ls[] = {{&P.ev, 0, dn, P.kev}, {&P.g1, 2, h, dn},  {&P.g2, 4, h, h},   {&P.w1, 6, h2, h2},
+              {&P.w2, 8, h2, h2},    {&P.a1, 10, h, h2}, {&P.a2, 12, h, h},  {&P.m1, 14, hm, hm},
+              {&P.m2, 16, h, hm},    {&P.d1, 20, h, P.kdep}, {&P.d2, 22, h / 2, h}};
+    size_t total = 0;
+    std::vector<size_t> woff, boff;
+    for (auto &l : ls) {
+        l.lin->nt = r16(l.nout) / 16;
+        l.lin->nq = r16(l.k) / 16;
+        l.lin->nout = l.nout;
+        l.lin->k = l.k;
+        woff.push_back(total);
+        total += (size_t)l.lin->nt * l.lin->nq * 256;
+        boff.push_back(total);
+        total += (size_t)l.lin->nt * 16;
+        w->specs.push_back({l.lin, l.wi, l.nout, l.k});
+    }
+    const size_t m3w = total; total += 64;
+    const size_t m3b = total; total += 4;
+    const size_t d3w = total; total += 64;
+    const size_t d3b = total; total += 4;
+    const size_t fq = total; total += r16(dn);
+    const size_t ph = total; total += r16(dn);
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (hipSetDevice(device) != hipSuccess || hipMalloc(&w->buf, total * sizeof(float)) != hipSuccess ||
+        hipMemset(w->buf, 0, total * sizeof(float)) != hipSuccess) {
+        (void)hipSetDevice(prev);
+        delete w;
+        return fail(TM_E_HIP, "tm_weights_create: allocation failed");
+    }
+    (void)hipSetDevice(prev);
+    w->n_floats = total;
+    for (size_t i = 0; i < w->specs.size(); ++i) {
+        Lin *l = w->specs[i].lin;
+        l->w = reinterpret_cast<const float4 *>(w->buf + woff[i]);
+        l->b = w->buf + boff[i];
+    }
+    P.m3w = w->buf + m3w;
+    P.m3b = w->buf + m3b;
+    P.d3w = w->buf + d3w;
+    P.d3b = w->buf + d3b;
+    P.freq = w->buf + fq;
+    P.phase = w->buf + ph;
+    *out = w;
+    return TM_OK;
+}
+
+extern "C" int tm_weights_pack(tm_weights *w, const float *const *t, void *stream) {
+    if (!w || !t) return fail(TM_E_ARG, "tm_weights_pack: bad arguments");
+    for (int i = 0; i < TM_N_WEIGHTS; ++i)
+        if (!t[i]) return fail(TM_E_ARG, "tm_weights_pack: NULL tensor " + std::to_string(i));
+    hipStream_t s = S_(stream);
+    for (auto &sp : w->specs) {
+        Lin *l = sp.lin;
+        pack_kernel<<<dim3(64), 256, 0, s>>>(t[sp.wi], sp.nout, sp.k, l->nt, l->nq, const_cast<float *>(reinterpret_cast<const float *>(l->w)));
+        copy_pad_kernel<<<dim3(1), 256, 0, s>>>(t[sp.wi + 1], sp.nout, l->nt * 16, const_cast<float *>(l->b));
+    }
+    copy_pad_kernel<<<dim3(1), 256, 0, s>>>(t[18], w->h, 64, const_cast<float *>(w->P.m3w));
+    copy_pad_kernel<<<dim3(1), 256, 0, s>>>(t[19], 1, 4, const_cast<float *>(w->P.m3b));
+    copy_pad_kernel<<<dim3(1), 256, 0, s>>>(t[24], w->h / 2, 64, const_cast<float *>(w->P.d3w));
+    copy_pad_kernel<<<dim3(1), 256, 0, s>>>(t[25], 1, 4, const_cast<float *>(w->P.d3b));
+    copy_pad_kernel<<<dim3(1), 256, 0, s>>>(t[26], w->dn, r16(w->dn), const_cast<float *>(w->P.freq));
+    copy_pad_kernel<<<dim3(1), 256, 0, s>>>(t[27], w->dn, r16(w->dn), const_cast<float *>(w->P.phase));
+    TM_CHECK_LAUNCH();
+    return TM_OK;
+}
+
+extern "C" int tm_weights_free(tm_weights *w) {
+    if (!w) return TM_OK;
+    if (w->buf) (void)hipFree(w->buf);
+    delete w;
+    return TM_OK;
+}
+
+extern "C" int64_t tm_encoder_workspace_bytes(const tm_weights *w, int64_t n_walks) {
+    (void)w;
+    return n_walks * 3 * 2 * HID * (int64_t)sizeof(float) + (n_walks + 64) * (int64_t)sizeof(float) + 256;
+}
+
+static size_t gcn_lds(const EncW &P) {
+    const int xsz = std::max(TILE_ROWS * (r16(P.kev) + 8), 2 * TILE_ROWS * (HID + 8));
+    return sizeof(float) * (xsz + 2 * TILE_ROWS * (r16(P.dn) + 8));
+}
+static size_t head_lds() { return sizeof(float) * (4 * TILE_ROWS * (2 * HID + 8)); }
+
+extern "C" int tm_encoder_fwd(const tm_weights *w, const float *n_feat, const float *e_feat, int32_t n_groups,
+                              int32_t B, int32_t W, const int32_t *node6, const int32_t *eid3, const float *ts3,
+                              const int32_t *cat, const double *cut, const float *cnt, void *workspace,
+                              float *out_imp, void *stream) {
+    if (!w || n_groups < 0 || B < 0 || W < 0) return fail(TM_E_ARG, "tm_encoder_fwd: bad arguments");
+    const int64_t n_walks = (int64_t)n_groups * B * W;
+    if (n_walks == 0) return TM_OK;
+    if (!n_feat || !e_feat || !node6 || !eid3 || !ts3 || !cat || !cut || !cnt || !workspace || !out_imp)
+        return fail(TM_E_ARG, "tm_encoder_fwd: NULL pointer");
+    const EncW &P = w->P;
+    const size_t lds_g = gcn_lds(P), lds_h = head_lds();
+    if (lds_g > 160 * 1024) return fail(TM_E_UNSUPPORTED, "tm_encoder_fwd: feature dims too large for LDS tile");
+    hipStream_t s = S_(stream);
+    float *F = reinterpret_cast<float *>(workspace);
+    float *stdv = F + n_walks * 3 * 2 * HID;
+    hipEvent_t pe = prof_begin(s);
+    std_kernel<<<dim3(n_groups), 256, 0, s>>>(B, W, cut, ts3, stdv);
+    TM_CHECK_LAUNCH();
+    prof_end("std_kernel", s, pe);
+    const int64_t n_rows = n_walks * 3;
+    pe = prof_begin(s);
+    gcn_kernel<<<dim3((unsigned)((n_rows + TILE_ROWS - 1) / TILE_ROWS)), 256, lds_g, s>>>(
+        P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, F);
+    TM_CHECK_LAUNCH();
+    prof_end("gcn_kernel", s, pe);
+    pe = prof_begin(s);
+    head_kernel<<<dim3((unsigned)((n_walks + TILE_ROWS - 1) / TILE_ROWS)), 256, lds_h, s>>>(
+        P, n_walks, (int64_t)B * W, W, F, ts3, cut, cat, stdv, out_imp);
+    TM_CHECK_LAUNCH();
+    prof_end("head_kernel", s, pe);
+    return TM_OK;
+}
+
+extern "C" int tm_edge_importance(const tm_weights *w, const float *e_feat, int32_t n_groups, int32_t B, int32_t W,
+                                  int32_t N, const int32_t *eid3, const float *ts3, const float *imp,
+                                  const int32_t *sub1_node, const int32_t *sub1_eid, const int32_t *sub2_node,
+                                  const int32_t *sub2_eid, float *out_h1, float *out_h2, void *stream) {
+    if (!w || n_groups < 0 || B < 0 || W <= 0 || N <= 0) return fail(TM_E_ARG, "tm_edge_importance: bad arguments");
+    const int64_t rows = (int64_t)n_groups * B;
+    if (rows == 0) return TM_OK;
+    if (!e_feat || !eid3 || !ts3 || !imp || !sub1_node || !sub1_eid || !sub2_node || !sub2_eid || !out_h1 || !out_h2)
+        return fail(TM_E_ARG, "tm_edge_importance: NULL pointer");
+    int hbits = 6;
+    while ((1 << hbits) < 2 * 3 * W) ++hbits;
+    if (hbits > 14) return fail(TM_E_UNSUPPORTED, "tm_edge_importance: too many walks per event");
+    const EncW &P = w->P;
+    const size_t lds = sizeof(float) * (TILE_ROWS * (r16(P.kdep) + 8) + TILE_ROWS * (HID + 8) + TILE_ROWS * (HID / 2 + 8)) +
+                       2 * sizeof(int32_t) * (1u << hbits);
+    if (lds > 160 * 1024) return fail(TM_E_UNSUPPORTED, "tm_edge_importance: LDS budget exceeded");
+    hipEvent_t pe = prof_begin(S_(stream));
+    explain_kernel<<<dim3((unsigned)rows), 256, lds, S_(stream)>>>(P, W, N, hbits, e_feat, eid3, ts3, imp, sub1_node,
+                                                                  sub1_eid, sub2_node, sub2_eid, out_h1, out_h2);
+    TM_CHECK_LAUNCH();
+    prof_end("explain_kernel", S_(stream), pe);
+    return TM_OK;
+}

@@ -1,0 +1,551 @@
+// Temporal k-hop sampling, temporal-walk motif enumeration and motif bookkeeping on gfx950.
+//
+// Reference (dharunm236/TempME):
+//   k-hop:  utils/graph.py:103-146 (find_before), :197-231 (get_temporal_neighbor), :233-262 (find_k_hop)
+//   walks:  utils/graph.py:149-194 (find_before_walk), :265-306 (find_k_walks), :308-333 (get_next_step),
+//           :335-476 (get_final_step)
+//   motif:  processed/data_preprocess.py:148-214 (marginal), :327-343 (new_edge_info);
+//           utils/null_model.py:75-121 (statistic); utils/batch_loader.py:39-42 (RandEdgeSampler.sample)
+//
+// Layout: adjacency records are 16-byte {ngh, eid, ts(f64)} so every sampled slot is one
+// dwordx4 gather; e_idx -> position is an O(1) per-edge table (EdgeEnds); the filtered
+// step-3 candidate sets of get_final_step are counted and indexed through a per-node
+// (neighbor, position)-sorted pair index with binary searches instead of O(deg) scans.
+#include "common.h"
+
+namespace tmk {
+
+constexpr int kMaxN = 64;   // n_degree supported by the sampling kernels (reference: 20..60)
+constexpr int kMaxM = 8;    // walks per hop-1 slot (reference: 3, null model 1)
+
+__device__ __forceinline__ void set_err(int32_t *err, int32_t code) {
+    if (err) atomicCAS(err, 0, code);
+}
+
+// cut length of find_before (graph.py:103-146); time path or e_idx path
+__device__ __forceinline__ int32_t find_before_len(const DevGraph &g, int32_t u, bool time_path, double cut,
+                                                   int32_t e, int32_t *err) {
+    if (u < 0 || u >= g.n_nodes) {
+        set_err(err, TM_E_ARG);
+        return 0;
+    }
+    if (time_path) return bisect_ts(g, u, cut);
+    if (!(u > 0)) return 0;
+    int32_t l = edge_len(g, u, e);
+    if (l < 0) {
+        set_err(err, TM_E_EDGE_NOT_IN_LIST);
+        return 0;
+    }
+    return l;
+}
+
+// cut of find_before_walk (graph.py:171-176): missing e_idx -> 0
+__device__ __forceinline__ int32_t walk_len(const DevGraph &g, int32_t u, int32_t e) {
+    if (!(u > 0) || u >= g.n_nodes) return 0;
+    int32_t l = edge_len(g, u, e);
+    return l < 0 ? 0 : l;
+}
+
+// cut of get_final_step (graph.py:357, :366, ...): None -> whole list ([:None] leak)
+__device__ __forceinline__ int32_t final_len(const DevGraph &g, int32_t u, int32_t e) {
+    if (!(u > 0) || u >= g.n_nodes) return 0;
+    int32_t l = edge_len(g, u, e);
+    return l < 0 ? deg(g, u) : l;
+}
+
+// rank-th smallest position of the union of two sorted, disjoint position lists
+__device__ __forceinline__ int32_t kth_of_two(const Pair *p1, int32_t n1, const Pair *p2, int32_t n2, int32_t r) {
+    int32_t lo = max(0, r + 1 - n2), hi = min(n1, r + 1);
+    while (lo < hi) {
+        int32_t mid = (lo + hi) >> 1, j = r + 1 - mid;
+        if (j == 0 || p1[mid].pos > p2[j - 1].pos) hi = mid;
+        else lo = mid + 1;
+    }
+    int32_t i = lo, j = r + 1 - lo;
+    int32_t a = i > 0 ? p1[i - 1].pos : -1, b = j > 0 ? p2[j - 1].pos : -1;
+    return a > b ? a : b;
+}
+
+struct Step3 {
+    int32_t src, ngh, eid;
+    float ts;
+    int32_t code, t;
+};
+
+// get_final_step for one walk (graph.py:353-474), incl. quirks:
+//  * case order A (src1==src2 && tgt1!=tgt2) / B (tgt1==src2 && src1!=tgt2) / C (else)
+//  * nodeedge2idx[..].get(e2) of None slices the WHOLE list (future leak)
+//  * node 0 is padding (cut 0) even when it is a real node
+__device__ Step3 final_step(const DevGraph &g, Key key, uint32_t ev, uint32_t w, int32_t src1, int32_t tgt1,
+                            int32_t src2, int32_t tgt2, int32_t e2) {
+    int32_t code, a_node, a1 = 0, a2 = 0, b_node, bf = 0;
+    bool filt;
+    if (src1 == src2 && tgt1 != tgt2) {
+        code = 2; a_node = src1; a1 = tgt1; a2 = tgt2; b_node = tgt2; bf = tgt1; filt = true;
+    } else if (tgt1 == src2 && src1 != tgt2) {
+        code = 3; a_node = tgt1; a1 = src1; a2 = tgt2; b_node = tgt2; bf = src1; filt = true;
+    } else {
+        code = 1; a_node = tgt1; b_node = tgt2; filt = false;
+    }
+    const int32_t ca = final_len(g, a_node, e2), cb = final_len(g, b_node, e2);
+    int32_t na, nb, lb1 = 0, n1 = 0, lb2 = 0, n2 = 0, lbb = 0;
+    if (filt) {
+        if (ca > 0) {
+            lb1 = pair_lb(g, a_node, a1, 0);
+            n1 = pair_lb(g, a_node, a1, ca) - lb1;
+            lb2 = pair_lb(g, a_node, a2, 0);
+            n2 = pair_lb(g, a_node, a2, ca) - lb2;
+        }
+        na = n1 + n2;
+        nb = 0;
+        if (cb > 0) {
+            lbb = pair_lb(g, b_node, bf, 0);
+            nb = pair_lb(g, b_node, bf, cb) - lbb;
+        }
+    } else {
+        na = ca;
+        nb = cb;
+    }
+    Step3 o{0, 0, 0, 0.f, code, 0};
+    if (na + nb == 0) return o;
+    const int32_t r = draw(key, TM_STAGE_STEP3, ev, w, 0, (uint32_t)(na + nb));
+    int32_t ent;
+    if (r < na) {
+        o.src = a_node;
+        int32_t pos = filt ? kth_of_two(g.pair + lb1, n1, g.pair + lb2, n2, r) : r;
+        ent = g.off[a_node] + pos;
+    } else {
+        o.src = b_node;
+        int32_t rr = r - na;
+        int32_t pos = filt ? g.pair[lbb + rr].pos : rr;
+        ent = g.off[b_node] + pos;
+    }
+    const Rec rc = g.rec[ent];
+    o.ngh = rc.ngh;
+    o.eid = rc.eid;
+    o.ts = (float)rc.ts;
+    int32_t t;
+    const int32_t s = o.src, n = o.ngh;
+    if (code == 2) {
+        t = (s == src1 && n == tgt1) ? 1 : (s == src1 && n == tgt2) ? 2 : (s == tgt1 && n == tgt2) ? 3 : 0;
+    } else if (code == 3) {
+        t = (s == tgt1 && n == src1) ? 1 : (s == tgt1 && n == tgt2) ? 3 : (s == tgt2 && n == src1) ? 2 : 0;
+    } else {
+        t = (s == src1 && n != tgt1) ? 3 : (s == tgt1 && n != src1) ? 2 : (s == src1 && n == tgt1) ? 1
+            : (s == tgt1 && n == src1) ? 1 : 0;
+    }
+    o.t = t;
+    return o;
+}
+
+// anony [1, code, t] -> category id (marginal order, data_preprocess.py:171-178) or null key-1
+__device__ __forceinline__ int32_t cat_of(int32_t code, int32_t t, int null_order) {
+    if (t < 0 || t > 3) return -1;
+    // packed 4-bit tables indexed by t
+    const uint32_t cat2 = 0x2103, cat3 = 0x5647, cat1 = 0x89AB;      // t=0..3 -> {3,0,1,2} {7,4,6,5} {11,10,9,8}
+    const uint32_t nul2 = 0x2310, nul3 = 0x6754, nul1 = 0xBA98;      // {0,1,3,2} {4,5,7,6} {8,9,10,11}
+    uint32_t tab = null_order ? (code == 2 ? nul2 : code == 3 ? nul3 : code == 1 ? nul1 : 0xFFFF)
+                              : (code == 2 ? cat2 : code == 3 ? cat3 : code == 1 ? cat1 : 0xFFFF);
+    uint32_t v = (tab >> (4 * t)) & 0xF;
+    return v == 0xF ? -1 : (int32_t)v;
+}
+
+// step 2 of one walk: the m-th smallest of the M draws over the concatenated candidates
+// [root's prefix before e1 | v1's prefix before e1] (graph.py:323-332).
+struct Step2 {
+    int32_t src, ngh, eid;
+    float ts;
+};
+
+__device__ __forceinline__ Step2 next_step(const DevGraph &g, Key key, uint32_t ev, uint32_t slot, int32_t M,
+                                           int32_t m, int32_t u, int32_t v1, int32_t e1) {
+    Step2 o{0, 0, 0, 0.f};
+    const int32_t cu = walk_len(g, u, e1), cv = walk_len(g, v1, e1), tot = cu + cv;
+    if (tot == 0) return o;
+    uint32_t dv[kMaxM];
+#pragma unroll
+    for (int k = 0; k < kMaxM; ++k) dv[k] = k < M ? (uint32_t)draw(key, TM_STAGE_STEP2, ev, slot, k, tot) : 0xFFFFFFFFu;
+    uint32_t sel = 0;
+#pragma unroll
+    for (int k = 0; k < kMaxM; ++k) {
+        int32_t rank = 0;
+#pragma unroll
+        for (int i = 0; i < kMaxM; ++i) rank += (dv[i] < dv[k]) || (i < k && dv[i] == dv[k]);
+        if (k < M && rank == m) sel = dv[k];
+    }
+    const int32_t x = (int32_t)sel;
+    int32_t ent;
+    if (x < cu) {
+        o.src = u;
+        ent = g.off[u] + x;
+    } else {
+        o.src = v1;
+        ent = g.off[v1] + (x - cu);
+    }
+    const Rec rc = g.rec[ent];
+    o.ngh = rc.ngh;
+    o.eid = rc.eid;
+    o.ts = (float)rc.ts;
+    return o;
+}
+
+// ------------------------------------------------------------------ k-hop: one row per L-lane group
+// Each lane j < N draws one index; its slot in the np.sort order is its rank among the
+// row's draws (ties by lane), found with shuffles inside the group.
+template <int L>
+__global__ void __launch_bounds__(256) khop_kernel(DevGraph g, Key key, uint32_t stage, int32_t N, int64_t rows,
+                                                   int64_t rows_per_event, const int32_t *__restrict__ root,
+                                                   const double *__restrict__ cut, const int32_t *__restrict__ eidx,
+                                                   int time_path, const float *__restrict__ tin,
+                                                   const uint32_t *__restrict__ event_ids, int32_t *__restrict__ on,
+                                                   int32_t *__restrict__ oe, float *__restrict__ ot, int32_t *err) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t r = gid / L;
+    const int j = threadIdx.x & (L - 1);
+    if (r >= rows) return;
+    const int32_t u = root[r];
+    const int32_t c = find_before_len(g, u, time_path, time_path ? cut[r] : 0.0, time_path ? 0 : eidx[r], j == 0 ? err : nullptr);
+    (void)tin;
+    uint32_t d = 0xFFFFFFFFu;
+    if (c > 0 && j < N) d = (uint32_t)draw(key, stage, event_ids[r / rows_per_event], (uint32_t)(r % rows_per_event), j, c);
+    int32_t rank = 0;
+    for (int k = 0; k < N; ++k) {
+        uint32_t dk = __shfl(d, k, L);
+        rank += (dk < d) || (k < j && dk == d);
+    }
+    if (j >= N) return;
+    const int64_t o = r * N + rank;
+    if (c == 0) {
+        on[r * N + j] = 0;
+        oe[r * N + j] = 0;
+        ot[r * N + j] = 0.f;
+        return;
+    }
+    const Rec rc = g.rec[g.off[u] + (int32_t)d];
+    on[o] = rc.ngh;
+    oe[o] = rc.eid;
+    ot[o] = (float)rc.ts;
+}
+
+// ------------------------------------------------------------------ walks: one thread per walk
+__global__ void __launch_bounds__(256) walks_kernel(DevGraph g, Key key, int32_t N, int32_t M, int64_t n_walks,
+                                                    const int32_t *__restrict__ root, const int32_t *__restrict__ h1n,
+                                                    const int32_t *__restrict__ h1e, const float *__restrict__ h1t,
+                                                    const uint32_t *__restrict__ event_ids, int32_t *__restrict__ node6,
+                                                    int32_t *__restrict__ eid3, float *__restrict__ ts3,
+                                                    int32_t *__restrict__ anony3, int32_t *__restrict__ cat) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_walks) return;
+    const int32_t W = N * M;
+    const int64_t b = i / W;
+    const int32_t w = (int32_t)(i % W), j = w / M, m = w % M;
+    const uint32_t ev = event_ids[b];
+    const int32_t u = root[b], v1 = h1n[b * N + j], e1 = h1e[b * N + j];
+    const float t1 = h1t[b * N + j];
+    const Step2 s2 = next_step(g, key, ev, j, M, m, u, v1, e1);
+    const Step3 s3 = final_step(g, key, ev, w, u, v1, s2.src, s2.ngh, s2.eid);
+    int32_t *nd = node6 + i * 6;
+    nd[0] = s3.src; nd[1] = s3.ngh; nd[2] = s2.src; nd[3] = s2.ngh; nd[4] = u; nd[5] = v1;
+    eid3[i * 3 + 0] = s3.eid; eid3[i * 3 + 1] = s2.eid; eid3[i * 3 + 2] = e1;
+    ts3[i * 3 + 0] = s3.ts; ts3[i * 3 + 1] = s2.ts; ts3[i * 3 + 2] = t1;
+    if (anony3) {
+        anony3[i * 3 + 0] = 1; anony3[i * 3 + 1] = s3.code; anony3[i * 3 + 2] = s3.t;
+    }
+    if (cat) cat[i] = cat_of(s3.code, s3.t, 0);
+}
+
+__global__ void neg_kernel(Key key, const int32_t *__restrict__ list, uint32_t n_list,
+                           const uint32_t *__restrict__ event_ids, int32_t n, uint32_t j, int32_t *__restrict__ out) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = list[draw(key, TM_STAGE_NEG, event_ids[i], 0, j, n_list)];
+}
+
+// one Philox word per position: sort keys of the keyed permutation (utils/null_model.py:23)
+__global__ void perm_keys_kernel(Key key, int64_t n, uint32_t *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = philox_word((uint32_t)i, key.tagbase | TM_STAGE_PERM, 0, 0, key.k0, key.k1, 0);
+}
+
+__global__ void __launch_bounds__(256) hist_kernel(const int32_t *__restrict__ anony3, int64_t n, int null_order,
+                                                   int32_t *__restrict__ cat, unsigned long long *__restrict__ hist) {
+    __shared__ unsigned int bins[12];
+    if (threadIdx.x < 12) bins[threadIdx.x] = 0;
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t c = cat_of(anony3[i * 3 + 1], anony3[i * 3 + 2], null_order);
+        if (cat) cat[i] = c;
+        if (c >= 0) atomicAdd(&bins[c], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 12 && bins[threadIdx.x]) atomicAdd(&hist[threadIdx.x], (unsigned long long)bins[threadIdx.x]);
+}
+
+// new_edge_info for one group of W walks: eids staged in LDS, each (w,p) counts its id per column q
+__device__ __forceinline__ void edge_counts_group(const int32_t *e_lds, int32_t W, float *out) {
+    for (int32_t wp = threadIdx.x; wp < W * 3; wp += blockDim.x) {
+        const int32_t x = e_lds[wp];
+        int32_t c0 = 0, c1 = 0, c2 = 0;
+        for (int32_t w2 = 0; w2 < W; ++w2) {
+            c0 += e_lds[w2 * 3 + 0] == x;
+            c1 += e_lds[w2 * 3 + 1] == x;
+            c2 += e_lds[w2 * 3 + 2] == x;
+        }
+        out[wp * 3 + 0] = (float)c0;
+        out[wp * 3 + 1] = (float)c1;
+        out[wp * 3 + 2] = (float)c2;
+    }
+}
+
+__global__ void __launch_bounds__(256) edge_counts_kernel(const int32_t *__restrict__ eid3, int32_t W,
+                                                          float *__restrict__ out) {
+    extern __shared__ int32_t e_lds[];
+    const int64_t base = (int64_t)blockIdx.x * W * 3;
+    for (int32_t i = threadIdx.x; i < W * 3; i += blockDim.x) e_lds[i] = eid3[base + i];
+    __syncthreads();
+    edge_counts_group(e_lds, W, out + base * 3);
+}
+
+// ------------------------------------------------------------------ fused per-(event, side) sampler
+// One 256-thread workgroup per (event, side): hop 1 -> hop 2 -> step 2 -> step 3 -> category ->
+// edge counts, intermediates in LDS.  Side 0/1: root = src/dst, e_idx path (data_preprocess.py:114,
+// :118); side 2: root = negative dst, time path (:122).
+struct EventArgs {
+    DevGraph g;
+    uint64_t seed;
+    uint32_t split;
+    int32_t N, M, E;
+    const int32_t *src, *dst, *eidx;
+    const double *ts;
+    const uint32_t *event_ids;
+    const int32_t *dst_list;
+    uint32_t n_dst;
+    int32_t *dst_fake;
+    int32_t *sub1_node, *sub1_eid;
+    float *sub1_ts;
+    int32_t *sub2_node, *sub2_eid;
+    float *sub2_ts;
+    int32_t *node6, *eid3;
+    float *ts3;
+    int32_t *cat;
+    float *cnt;
+    unsigned long long *hist;
+    int32_t *err;
+};
+
+__global__ void __launch_bounds__(256) events_kernel(EventArgs a) {
+    __shared__ int32_t h1n[kMaxN], h1e[kMaxN];
+    __shared__ float h1t[kMaxN];
+    __shared__ uint32_t d2[kMaxN * kMaxN];
+    __shared__ int32_t c2[kMaxN];
+    __shared__ int32_t weid[kMaxN * kMaxM * 3];
+    __shared__ unsigned int bins[12];
+    const DevGraph &g = a.g;
+    const int32_t e = blockIdx.x, s = blockIdx.y, N = a.N, M = a.M, W = N * M, tid = threadIdx.x;
+    const uint32_t ev = a.event_ids[e];
+    const Key key = make_key(a.seed, a.split, (uint32_t)(s + 1));
+    if (tid < 12) bins[tid] = 0;
+    // ---- root
+    int32_t u;
+    if (s == 0) u = a.src[e];
+    else if (s == 1) u = a.dst[e];
+    else u = a.dst_list[draw(make_key(a.seed, a.split, TM_SIDE_NONE), TM_STAGE_NEG, ev, 0, 1, a.n_dst)];
+    if (s == 2 && tid == 0) a.dst_fake[e] = u;
+    const int64_t se = (int64_t)s * a.E + e;
+    // ---- hop 1 (one row, N draws), lanes of wave 0
+    if (tid < 64) {
+        const int32_t c = find_before_len(g, u, s == 2, a.ts[e], a.eidx ? a.eidx[e] : 0, tid == 0 ? a.err : nullptr);
+        uint32_t d = 0xFFFFFFFFu;
+        if (c > 0 && tid < N) d = (uint32_t)draw(key, 1, ev, 0, tid, c);
+        int32_t rank = 0;
+        for (int k = 0; k < N; ++k) {
+            uint32_t dk = __shfl(d, k, 64);
+            rank += (dk < d) || (k < tid && dk == d);
+        }
+        if (tid < N) {
+            int32_t n_ = 0, e_ = 0;
+            float t_ = 0.f;
+            int32_t slot = tid;
+            if (c > 0) {
+                const Rec rc = g.rec[g.off[u] + (int32_t)d];
+                n_ = rc.ngh; e_ = rc.eid; t_ = (float)rc.ts; slot = rank;
+            }
+            h1n[slot] = n_; h1e[slot] = e_; h1t[slot] = t_;
+            a.sub1_node[se * N + slot] = n_;
+            a.sub1_eid[se * N + slot] = e_;
+            a.sub1_ts[se * N + slot] = t_;
+        }
+    }
+    __syncthreads();
+    // ---- hop 2 (N rows x N draws; e_idx path, graph.py:247-250)
+    if (tid < N) c2[tid] = find_before_len(g, h1n[tid], false, 0.0, h1e[tid], a.err);
+    __syncthreads();
+    for (int32_t x = tid; x < N * N; x += blockDim.x) {
+        const int32_t j = x / N, k = x % N, c = c2[j];
+        d2[x] = c > 0 ? (uint32_t)draw(key, 2, ev, j, k, c) : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    for (int32_t x = tid; x < N * N; x += blockDim.x) {
+        const int32_t j = x / N, k = x % N, c = c2[j];
+        const uint32_t d = d2[x];
+        int32_t rank = 0;
+        for (int32_t i = 0; i < N; ++i) {
+            const uint32_t di = d2[j * N + i];
+            rank += (di < d) || (i < k && di == d);
+        }
+        int32_t n_ = 0, e_ = 0, slot = x;
+        float t_ = 0.f;
+        if (c > 0) {
+            const Rec rc = g.rec[g.off[h1n[j]] + (int32_t)d];
+            n_ = rc.ngh; e_ = rc.eid; t_ = (float)rc.ts; slot = j * N + rank;
+        }
+        const int64_t o = se * N * N + slot;
+        a.sub2_node[o] = n_;
+        a.sub2_eid[o] = e_;
+        a.sub2_ts[o] = t_;
+    }
+    // ---- steps 2 + 3, one thread per walk
+    for (int32_t w = tid; w < W; w += blockDim.x) {
+        const int32_t j = w / M, m = w % M;
+        const int32_t v1 = h1n[j], e1 = h1e[j];
+        const Step2 s2 = next_step(g, key, ev, j, M, m, u, v1, e1);
+        const Step3 s3 = final_step(g, key, ev, w, u, v1, s2.src, s2.ngh, s2.eid);
+        const int64_t o = se * W + w;
+        int32_t *nd = a.node6 + o * 6;
+        nd[0] = s3.src; nd[1] = s3.ngh; nd[2] = s2.src; nd[3] = s2.ngh; nd[4] = u; nd[5] = v1;
+        a.eid3[o * 3 + 0] = s3.eid; a.eid3[o * 3 + 1] = s2.eid; a.eid3[o * 3 + 2] = e1;
+        a.ts3[o * 3 + 0] = s3.ts; a.ts3[o * 3 + 1] = s2.ts; a.ts3[o * 3 + 2] = h1t[j];
+        const int32_t c = cat_of(s3.code, s3.t, 0);
+        a.cat[o] = c;
+        if (c >= 0) atomicAdd(&bins[c], 1u);
+        weid[w * 3 + 0] = s3.eid; weid[w * 3 + 1] = s2.eid; weid[w * 3 + 2] = e1;
+    }
+    __syncthreads();
+    edge_counts_group(weid, W, a.cnt + se * W * 9);
+    if (tid < 12 && bins[tid]) atomicAdd(&a.hist[tid], (unsigned long long)bins[tid]);
+}
+
+}  // namespace tmk
+
+using namespace tmk;
+
+static inline hipStream_t S(void *s) { return (hipStream_t)s; }
+
+extern "C" int tm_sample_khop(const tm_graph *g, tm_rng rng, int32_t k, int32_t N, int32_t B, const int32_t *root,
+                              const double *cut, const int32_t *eidx, const uint32_t *event_ids, int32_t *out_node,
+                              int32_t *out_eid, float *out_ts, int32_t *err_flag, void *stream) {
+    if (!g || k < 0 || B < 0 || N <= 0) return fail(TM_E_ARG, "tm_sample_khop: bad arguments");
+    if (N > kMaxN) return fail(TM_E_UNSUPPORTED, "tm_sample_khop: num_neighbors > 64");
+    if (k == 0 || B == 0) return TM_OK;
+    if (!root || !event_ids || !out_node || !out_eid || !out_ts || (!eidx && !cut))
+        return fail(TM_E_ARG, "tm_sample_khop: NULL pointer");
+    const Key key = make_key(rng.seed, rng.split, rng.side);
+    int64_t rows = B, rpe = 1, off = 0;
+    const int32_t *rn = root, *re = eidx;
+    for (int32_t h = 1; h <= k; ++h) {
+        const bool tp = (h == 1 && eidx == nullptr);
+        int32_t *on = out_node + off, *oe = out_eid + off;
+        float *ot = out_ts + off;
+        const int L = N <= 8 ? 8 : N <= 16 ? 16 : N <= 32 ? 32 : 64;
+        const int64_t threads = rows * L;
+        const dim3 grid((unsigned)((threads + 255) / 256));
+#define KH(LL)                                                                                                  \
+    khop_kernel<LL><<<grid, 256, 0, S(stream)>>>(g->d, key, (uint32_t)h, N, rows, rpe, rn, cut, re, tp ? 1 : 0, \
+                                                 nullptr, event_ids, on, oe, ot, err_flag)
+        if (L == 8) KH(8);
+        else if (L == 16) KH(16);
+        else if (L == 32) KH(32);
+        else KH(64);
+#undef KH
+        TM_CHECK_LAUNCH();
+        rn = on;
+        re = oe;
+        off += rows * N;
+        rows *= N;
+        rpe *= N;
+        if (rows > ((int64_t)1 << 40)) return fail(TM_E_UNSUPPORTED, "tm_sample_khop: too many rows");
+    }
+    return TM_OK;
+}
+
+extern "C" int tm_sample_walks(const tm_graph *g, tm_rng rng, int32_t N, int32_t M, int32_t B, const int32_t *root,
+                               const int32_t *h1_node, const int32_t *h1_eid, const float *h1_ts,
+                               const uint32_t *event_ids, int32_t *out_node6, int32_t *out_eid3, float *out_ts3,
+                               int32_t *out_anony3, int32_t *out_cat, void *stream) {
+    if (!g || N <= 0 || M <= 0 || B < 0) return fail(TM_E_ARG, "tm_sample_walks: bad arguments");
+    if (M > kMaxM) return fail(TM_E_UNSUPPORTED, "tm_sample_walks: num_neighbors (walks per slot) > 8");
+    if (B == 0) return TM_OK;
+    if (!root || !h1_node || !h1_eid || !h1_ts || !event_ids || !out_node6 || !out_eid3 || !out_ts3)
+        return fail(TM_E_ARG, "tm_sample_walks: NULL pointer");
+    const int64_t n = (int64_t)B * N * M;
+    walks_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, S(stream)>>>(
+        g->d, make_key(rng.seed, rng.split, rng.side), N, M, n, root, h1_node, h1_eid, h1_ts, event_ids, out_node6,
+        out_eid3, out_ts3, out_anony3, out_cat);
+    TM_CHECK_LAUNCH();
+    return TM_OK;
+}
+
+extern "C" int tm_neg_sample(tm_rng rng, const int32_t *list, int64_t n_list, const uint32_t *event_ids, int32_t n,
+                             int32_t j, int32_t *out, void *stream) {
+    if (n < 0 || n_list <= 0 || n_list > UINT32_MAX || j < 0) return fail(TM_E_ARG, "tm_neg_sample: bad arguments");
+    if (n == 0) return TM_OK;
+    if (!list || !event_ids || !out) return fail(TM_E_ARG, "tm_neg_sample: NULL pointer");
+    neg_kernel<<<dim3((n + 255) / 256), 256, 0, S(stream)>>>(make_key(rng.seed, rng.split, TM_SIDE_NONE), list,
+                                                             (uint32_t)n_list, event_ids, n, (uint32_t)j, out);
+    TM_CHECK_LAUNCH();
+    return TM_OK;
+}
+
+extern "C" int tm_perm_keys(uint64_t seed, uint32_t split, int64_t n, uint32_t *out_keys, void *stream) {
+    if (n < 0) return fail(TM_E_ARG, "tm_perm_keys: bad arguments");
+    if (n == 0) return TM_OK;
+    if (!out_keys) return fail(TM_E_ARG, "tm_perm_keys: NULL pointer");
+    perm_keys_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, S(stream)>>>(make_key(seed, split, TM_SIDE_NONE), n,
+                                                                             out_keys);
+    TM_CHECK_LAUNCH();
+    return TM_OK;
+}
+
+extern "C" int tm_motif_hist(const int32_t *anony3, int64_t n, int32_t null_order, int32_t *out_cat,
+                             unsigned long long *hist12, void *stream) {
+    if (n < 0 || !hist12) return fail(TM_E_ARG, "tm_motif_hist: bad arguments");
+    if (n == 0) return TM_OK;
+    if (!anony3) return fail(TM_E_ARG, "tm_motif_hist: NULL anony");
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 2048);
+    hist_kernel<<<dim3((unsigned)blocks), 256, 0, S(stream)>>>(anony3, n, null_order, out_cat, hist12);
+    TM_CHECK_LAUNCH();
+    return TM_OK;
+}
+
+extern "C" int tm_edge_counts(const int32_t *eid3, int32_t n_groups, int32_t W, float *out_cnt, void *stream) {
+    if (n_groups < 0 || W <= 0 || W > 8192) return fail(TM_E_ARG, "tm_edge_counts: bad arguments");
+    if (n_groups == 0) return TM_OK;
+    if (!eid3 || !out_cnt) return fail(TM_E_ARG, "tm_edge_counts: NULL pointer");
+    edge_counts_kernel<<<dim3(n_groups), 256, sizeof(int32_t) * W * 3, S(stream)>>>(eid3, W, out_cnt);
+    TM_CHECK_LAUNCH();
+    return TM_OK;
+}
+
+extern "C" int tm_sample_events(const tm_graph *g, uint64_t seed, uint32_t split, int32_t N, int32_t M,
+                                int32_t n_events, const int32_t *src, const int32_t *dst, const double *ts,
+                                const int32_t *eidx, const uint32_t *event_ids, const int32_t *dst_list,
+                                int64_t n_dst, int32_t *dst_fake, int32_t *sub1_node, int32_t *sub1_eid,
+                                float *sub1_ts, int32_t *sub2_node, int32_t *sub2_eid, float *sub2_ts,
+                                int32_t *node6, int32_t *eid3, float *ts3, int32_t *cat, float *cnt,
+                                unsigned long long *hist12, int32_t *err_flag, void *stream) {
+    if (!g || N <= 0 || M <= 0 || n_events < 0 || n_dst <= 0 || n_dst > UINT32_MAX)
+        return fail(TM_E_ARG, "tm_sample_events: bad arguments");
+    if (N > kMaxN || M > kMaxM) return fail(TM_E_UNSUPPORTED, "tm_sample_events: N > 64 or M > 8");
+    if (n_events == 0) return TM_OK;
+    if (n_events > 65535 * 1024) return fail(TM_E_UNSUPPORTED, "tm_sample_events: too many events per launch");
+    if (!src || !dst || !ts || !eidx || !event_ids || !dst_list || !dst_fake || !sub1_node || !sub1_eid ||
+        !sub1_ts || !sub2_node || !sub2_eid || !sub2_ts || !node6 || !eid3 || !ts3 || !cat || !cnt || !hist12)
+        return fail(TM_E_ARG, "tm_sample_events: NULL pointer");
+    EventArgs a{g->d,     seed,     split,     N,         M,        n_events, src,  dst,   eidx, ts,     event_ids,
+                dst_list, (uint32_t)n_dst, dst_fake, sub1_node, sub1_eid, sub1_ts, sub2_node, sub2_eid, sub2_ts,
+                node6,    eid3,     ts3,       cat,       cnt,      hist12,   err_flag};
+    hipEvent_t pe = prof_begin(S(stream));
+    events_kernel<<<dim3(n_events, 3), 256, 0, S(stream)>>>(a);
+    TM_CHECK_LAUNCH();
+    prof_end("events_kernel", S(stream), pe);
+    return TM_OK;
+}

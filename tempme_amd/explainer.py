@@ -1,0 +1,354 @@
+"""Drop-in ``TempME`` explainer (models/explainer_new.py:99-453) on the HIP encoder.
+
+Same constructor, submodule names (so a reference ``state_dict`` loads as is), same
+construction order (so ``torch.manual_seed(s); TempME(...)`` draws the same initial
+weights as the reference), same ``forward`` / ``retrieve_edge_imp_node`` /
+``retrieve_explanation`` / ``beta_sample`` / ``kl_loss`` signatures and shapes.
+
+Eval-mode scoring (``forward`` under ``model.eval()`` and
+``retrieve_explanation(..., training=False)``) runs entirely in libtempme_hip.so:
+tm_encoder_fwd (event features, event_gcn x2, temporal-aware attention, MLP) and
+tm_edge_importance (dependency gate, walk->edge scatter-max, gather, Beta mean,
+mask).  Training-mode calls (dropout active, Beta ``rsample``, gradients) use an
+autograd formulation in torch ops on the same device; HIP backward kernels are the
+next step.
+"""
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib as L
+from .null_model import get_null_distribution
+
+
+class TimeEncode(nn.Module):
+    """explainer_new.py:45-59."""
+
+    def __init__(self, expand_dim):
+        super().__init__()
+        self.time_dim = expand_dim
+        self.basis_freq = nn.Parameter(torch.from_numpy(1 / 10 ** np.linspace(0, 9, self.time_dim)).float())
+        self.phase = nn.Parameter(torch.zeros(self.time_dim).float())
+
+    def forward(self, ts):
+        b, s = ts.size(0), ts.size(1)
+        m = ts.view(b, s, 1) * self.basis_freq.view(1, 1, -1)
+        m = m + self.phase.view(1, 1, -1)
+        return torch.cos(m)
+
+
+class Attention(nn.Module):
+    """explainer_new.py:12-43 (use_temporal_guidance=False)."""
+
+    def __init__(self, input_dim, hid_dim):
+        super().__init__()
+        self.hidden_size = hid_dim
+        self.W1 = nn.Linear(input_dim, input_dim)
+        self.W2 = nn.Linear(input_dim, input_dim)
+        self.MLP = nn.Sequential(nn.Linear(input_dim, hid_dim), nn.ReLU(), nn.Linear(hid_dim, hid_dim))
+        nn.init.xavier_uniform_(self.W2.weight.data)
+        self.W2.bias.data.fill_(0.1)
+
+
+class TemporalAwareAttention(nn.Module):
+    """explainer_new.py:768-846."""
+
+    def __init__(self, input_dim, hid_dim, dropout_p=0.1):
+        super().__init__()
+        self.hidden_size = hid_dim
+        self.W1 = nn.Linear(input_dim, input_dim)
+        self.W2 = nn.Linear(input_dim, input_dim)
+        self.W_time = nn.Linear(1, input_dim)
+        self.dropout = nn.Dropout(dropout_p)
+        self.MLP = nn.Sequential(nn.Linear(input_dim, hid_dim), nn.ReLU(), nn.Dropout(dropout_p),
+                                 nn.Linear(hid_dim, hid_dim))
+        nn.init.xavier_uniform_(self.W2.weight.data)
+        self.W2.bias.data.fill_(0.1)
+        nn.init.xavier_uniform_(self.W_time.weight.data)
+
+
+class _MergeLayer(nn.Module):
+    def __init__(self, input_dim, hid_dim):
+        super().__init__()
+        self.fc1 = nn.Linear(2 * input_dim, hid_dim)
+        self.fc2 = nn.Linear(hid_dim, 1)
+        nn.init.xavier_normal_(self.fc1.weight)
+        nn.init.xavier_normal_(self.fc2.weight)
+        self.act = nn.ReLU()
+
+
+class event_gcn(nn.Module):  # noqa: N801  (reference name, kept for state_dict keys)
+    def __init__(self, event_dim, node_dim, hid_dim):
+        super().__init__()
+        self.lin_event = nn.Linear(event_dim, node_dim)
+        self.relu = nn.ReLU()
+        self.MLP = nn.Sequential(nn.Linear(node_dim, hid_dim), nn.ReLU(), nn.Linear(hid_dim, hid_dim))
+
+    def forward(self, event_feature, src_features, tgt_features):
+        event = self.lin_event(event_feature)
+        return self.MLP(src_features + self.relu(tgt_features + event))
+
+
+def _to(x, device, dtype):
+    if isinstance(x, torch.Tensor):
+        return x.to(device=device, dtype=dtype)
+    return torch.from_numpy(np.ascontiguousarray(x)).to(device=device, dtype=dtype)
+
+
+class TempME(nn.Module):
+    def __init__(self, base, base_model_type, data, out_dim, hid_dim, prior="empirical", temp=0.07,
+                 if_cat_feature=True, dropout_p=0.1, device=None, use_temporal_guidance=True,
+                 use_dependency_aware_sampling=True, *, null_model=None, data_dir=None, seed=0):
+        super().__init__()
+        self.node_dim = base.n_feat_th.shape[1]
+        self.edge_dim = base.e_feat_th.shape[1]
+        self.time_dim = self.node_dim
+        self.out_dim = out_dim
+        self.hid_dim = hid_dim
+        self.base_type = base_model_type
+        self.dropout_p = dropout_p
+        self.temp = temp
+        self.prior = prior
+        self.if_cat = if_cat_feature
+        self.dropout = nn.Dropout(dropout_p)
+        self.device = device
+        self.event_dim = self.edge_dim + self.time_dim + 3
+        self.event_conv = event_gcn(event_dim=self.event_dim, node_dim=self.node_dim, hid_dim=self.hid_dim)
+        self.use_temporal_guidance = use_temporal_guidance
+        self.attention = (TemporalAwareAttention(2 * self.hid_dim, self.hid_dim) if use_temporal_guidance
+                          else Attention(2 * self.hid_dim, self.hid_dim))
+        self.mlp_dim = self.hid_dim + 12 if self.if_cat else self.hid_dim
+        self.MLP = nn.Sequential(nn.Linear(self.mlp_dim, self.mlp_dim), nn.ReLU(), nn.Dropout(self.dropout_p),
+                                 nn.Linear(self.mlp_dim, self.hid_dim), nn.ReLU(), nn.Linear(self.hid_dim, 1))
+        self.final_linear = nn.Linear(2 * self.hid_dim, self.hid_dim)
+        self.node_emd_dim = self.hid_dim + 12 + self.node_dim if self.if_cat else self.hid_dim + self.node_dim
+        self.affinity_score = _MergeLayer(self.node_emd_dim, self.node_emd_dim)
+        self.edge_raw_embed = base.edge_raw_features
+        self.node_raw_embed = base.node_raw_features
+        self.time_encoder = TimeEncode(expand_dim=self.time_dim)
+        self.null_model = (null_model if null_model is not None
+                           else get_null_distribution(data, data_dir=data_dir, seed=seed, device=device))
+        num_nodes = base.n_feat_th.shape[0]
+        self.node_degree = torch.ones(num_nodes, device=device if device else torch.device("cpu"))
+        self.use_dependency_aware_sampling = use_dependency_aware_sampling
+        if use_dependency_aware_sampling:
+            self.edge_dependency_gcn = nn.Sequential(
+                nn.Linear(self.edge_dim + self.time_dim, self.hid_dim), nn.ReLU(), nn.Dropout(dropout_p * 1.5),
+                nn.Linear(self.hid_dim, self.hid_dim // 2), nn.ReLU(), nn.Dropout(dropout_p),
+                nn.Linear(self.hid_dim // 2, 1))
+            self.edge_importance_attention = nn.MultiheadAttention(embed_dim=self.hid_dim, num_heads=4,
+                                                                   dropout=dropout_p, batch_first=True)
+            self.edge_to_node_transform = nn.Sequential(nn.Linear(self.edge_dim, self.hid_dim), nn.ReLU(),
+                                                        nn.Linear(self.hid_dim, self.hid_dim))
+            self.gumbel_temperature = 1.0
+            self.min_gumbel_temperature = 0.5
+            self.gumbel_anneal_rate = 0.003
+        self._packed = None
+        self._packed_key = None
+
+    # ------------------------------------------------------------------ HIP plumbing
+    def _dev(self):
+        return L.require_device(self.device)
+
+    def _hip_ok(self):
+        return (self.use_temporal_guidance and self.use_dependency_aware_sampling and self.if_cat
+                and self.hid_dim == 64)
+
+    def _weight_list(self):
+        at, ec, m, d = self.attention, self.event_conv, self.MLP, self.edge_dependency_gcn
+        mods = [ec.lin_event, ec.MLP[0], ec.MLP[2], at.W1, at.W2, at.MLP[0], at.MLP[3], m[0], m[3], m[5],
+                d[0], d[3], d[6]]
+        ts = []
+        for mod in mods:
+            ts += [mod.weight, mod.bias]
+        return ts + [self.time_encoder.basis_freq, self.time_encoder.phase]
+
+    def packed_weights(self):
+        """tm_weights handle, re-packed whenever a parameter changed (version counters)."""
+        dev = self._dev()
+        ws = self._weight_list()
+        key = tuple((w.data_ptr(), w._version) for w in ws)
+        if self._packed is None or self._packed_key != key:
+            if self._packed is None:
+                h = L.C.c_void_p()
+                L.check(L.lib().tm_weights_create(self.edge_dim, self.node_dim, self.hid_dim, dev.index,
+                                                  L.C.byref(h)), "tm_weights_create")
+                self._packed = _Packed(h)
+            self._raw = [w.detach().to(device=dev, dtype=torch.float32).contiguous() for w in ws]
+            arr = (L.C.c_void_p * L.N_WEIGHTS)(*[w.data_ptr() for w in self._raw])
+            L.check(L.lib().tm_weights_pack(self._packed.h, arr, L.stream_ptr(dev)), "tm_weights_pack")
+            self._packed_key = key
+        return self._packed.h
+
+    def feature_tables(self):
+        dev = self._dev()
+        key = (self.node_raw_embed.weight.data_ptr(), self.edge_raw_embed.weight.data_ptr())
+        if getattr(self, "_tables_key", None) != key:
+            self._n_tab = self.node_raw_embed.weight.detach().to(device=dev, dtype=torch.float32).contiguous()
+            self._e_tab = self.edge_raw_embed.weight.detach().to(device=dev, dtype=torch.float32).contiguous()
+            self._tables_key = key
+        return self._n_tab, self._e_tab
+
+    def encoder_fwd(self, node6, eid3, ts3, cat, cut, cnt, n_groups, B, W, out=None, workspace=None):
+        """tm_encoder_fwd on device tensors (int32 node6 [G,B,W,6], eid3, f32 ts3, int32 cat [G,B,W],
+        f64 cut [G,B], f32 cnt [G,B,W,3,3]) -> f32 [G,B,W]."""
+        dev = self._dev()
+        nt, et = self.feature_tables()
+        n_walks = n_groups * B * W
+        if out is None:
+            out = torch.empty(max(n_walks, 1), dtype=torch.float32, device=dev)
+        if workspace is None:
+            nbytes = L.lib().tm_encoder_workspace_bytes(self.packed_weights(), n_walks)
+            workspace = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        L.check(L.lib().tm_encoder_fwd(self.packed_weights(), L.ptr(nt), L.ptr(et), n_groups, B, W, L.ptr(node6),
+                                       L.ptr(eid3), L.ptr(ts3), L.ptr(cat), L.ptr(cut), L.ptr(cnt),
+                                       L.ptr(workspace), L.ptr(out), L.stream_ptr(dev)), "TempME.forward")
+        return out
+
+    def edge_importance(self, eid3, ts3, imp, s1n, s1e, s2n, s2e, n_groups, B, W, N, out1=None, out2=None):
+        dev = self._dev()
+        _, et = self.feature_tables()
+        if out1 is None:
+            out1 = torch.empty(max(n_groups * B * N, 1), dtype=torch.float32, device=dev)
+            out2 = torch.empty(max(n_groups * B * N * N, 1), dtype=torch.float32, device=dev)
+        L.check(L.lib().tm_edge_importance(self.packed_weights(), L.ptr(et), n_groups, B, W, N, L.ptr(eid3),
+                                           L.ptr(ts3), L.ptr(imp), L.ptr(s1n), L.ptr(s1e), L.ptr(s2n), L.ptr(s2e),
+                                           L.ptr(out1), L.ptr(out2), L.stream_ptr(dev)), "retrieve_edge_imp_node")
+        return out1, out2
+
+    # ------------------------------------------------------------------ reference API
+    def forward(self, walks, cut_time_l, edge_identify):
+        """explainer_new.py:174-201 -> [bsz, n_walks, 1]."""
+        node_idx, edge_idx, time_idx, cat_feat, _ = walks
+        dev = self._dev()
+        B, W = np.shape(edge_idx)[0], np.shape(edge_idx)[1]
+        assert np.shape(edge_identify)[-1] == 3 and np.shape(edge_idx)[-1] == 3, "event_dim mismatch (:180)"
+        if self.training or not self._hip_ok():
+            return self._forward_torch(walks, cut_time_l, edge_identify)
+        out = self.encoder_fwd(_to(node_idx, dev, torch.int32).contiguous(), _to(edge_idx, dev, torch.int32).contiguous(),
+                               _to(time_idx, dev, torch.float32).contiguous(),
+                               _to(cat_feat, dev, torch.int32).reshape(B, W).contiguous(),
+                               _to(cut_time_l, dev, torch.float64).contiguous(),
+                               _to(edge_identify, dev, torch.float32).contiguous(), 1, B, W)
+        return out[:B * W].view(B, W, 1)
+
+    def retrieve_edge_imp_node(self, subgraph, graphlet_imp, walks, training=True):
+        """explainer_new.py:354-406 -> (hop-1 [B,N], hop-2 [B,N^2])."""
+        node_record, eidx_record, _ = subgraph
+        dev = self._dev()
+        if training or graphlet_imp.requires_grad or not self._hip_ok():
+            return self._edge_imp_torch(subgraph, graphlet_imp, walks, training)
+        B, N = np.shape(node_record[0])[0], np.shape(node_record[0])[1]
+        W = np.shape(walks[1])[1]
+        o1, o2 = self.edge_importance(_to(walks[1], dev, torch.int32).contiguous(),
+                                      _to(walks[2], dev, torch.float32).contiguous(),
+                                      graphlet_imp.detach().to(dev, torch.float32).contiguous(),
+                                      _to(node_record[0], dev, torch.int32).contiguous(),
+                                      _to(eidx_record[0], dev, torch.int32).contiguous(),
+                                      _to(node_record[1], dev, torch.int32).contiguous(),
+                                      _to(eidx_record[1], dev, torch.int32).contiguous(), 1, B, W, N)
+        return o1[:B * N].view(B, N), o2[:B * N * N].view(B, N * N)
+
+    def retrieve_explanation(self, subgraph_src, graphlet_imp_src, walks_src, subgraph_tgt, graphlet_imp_tgt,
+                             walks_tgt, subgraph_bgd, graphlet_imp_bgd, walks_bgd, training=True):
+        """explainer_new.py:408-418."""
+        s0, s1 = self.retrieve_edge_imp_node(subgraph_src, graphlet_imp_src, walks_src, training=training)
+        t0, t1 = self.retrieve_edge_imp_node(subgraph_tgt, graphlet_imp_tgt, walks_tgt, training=training)
+        b0, b1 = self.retrieve_edge_imp_node(subgraph_bgd, graphlet_imp_bgd, walks_bgd, training=training)
+        if self.base_type == "tgn":
+            return [torch.cat([s0, t0, b0], dim=0), torch.cat([s1, t1, b1], dim=0)]
+        return [torch.cat([s0, t0, b0], dim=0)]
+
+    def beta_sample(self, prob, training):
+        """explainer_new.py:420-430."""
+        alpha = torch.clamp(prob * 10, min=1.0)
+        beta = torch.clamp((1 - prob) * 10, min=1.0)
+        if training:
+            return torch.distributions.Beta(alpha, beta).rsample()
+        return alpha / (alpha + beta)
+
+    def kl_loss(self, prob, walks, target=0.3):
+        """explainer_new.py:432-453."""
+        _, _, _, cat_feat, _ = walks
+        prob = torch.clamp(prob, 1e-6, 1 - 1e-6)
+        if self.prior == "empirical":
+            s = torch.mean(prob, dim=1)
+            null = torch.tensor(list(self.null_model.values())).to(prob.device)
+            num_cat = len(self.null_model.keys())
+            cat = _to(cat_feat, prob.device, torch.long).reshape(prob.shape[0], -1, 1)
+            emp = torch.zeros(prob.shape[0], num_cat, 1, device=prob.device, dtype=prob.dtype)
+            emp = emp.scatter_reduce(1, cat, prob, "mean", include_self=False)
+            emp = s * emp.reshape(-1, num_cat)
+            null = target * null.reshape(-1, num_cat)
+            return ((1 - s) * torch.log((1 - s) / (1 - target + 1e-6) + 1e-6)
+                    + emp * torch.log(emp / (null + 1e-6) + 1e-6)).mean()
+        return (prob * torch.log(prob / target + 1e-6)
+                + (1 - prob) * torch.log((1 - prob) / (1 - target + 1e-6) + 1e-6)).mean()
+
+    # ------------------------------------------------------------------ autograd formulation (training)
+    def _forward_torch(self, walks, cut_time_l, edge_identify):
+        node_idx, edge_idx, time_idx, cat_feat, _ = walks
+        dev = self.node_raw_embed.weight.device if self.device is None else self.device
+        eid = _to(edge_idx, dev, torch.long)
+        t = _to(time_idx, dev, torch.float32)
+        B, W = eid.shape[0], eid.shape[1]
+        ef = self.edge_raw_embed(eid)
+        cnt = _to(edge_identify, dev, torch.float32)
+        dt = t[:, :, 2:3] - t
+        tf = self.time_encoder(dt.reshape(B, -1)).reshape(B, W, 3, -1)
+        ev = torch.cat([ef, cnt, tf], dim=-1)
+        node = _to(node_idx, dev, torch.long)
+        xs = self.node_raw_embed(node[:, :, [0, 2, 4]])
+        xt = self.node_raw_embed(node[:, :, [1, 3, 5]])
+        us = self.event_conv(ev, xs, xt)
+        ut = self.event_conv(ev, xt, xs)
+        f = torch.cat([us, ut], dim=-1)
+        at = self.attention
+        src = f[:, :, 2, :]
+        wq = at.W2(f[:, :, 0:2, :])
+        scores = (at.W1(src).unsqueeze(2) * wq).sum(-1)
+        if isinstance(at, TemporalAwareAttention):
+            cut = _to(cut_time_l, dev, torch.float32)
+            diff = torch.abs(cut.view(B, 1, 1) - t[:, :, :2])
+            tw = torch.exp(-diff / (diff.std() + 1e-6))
+            scores = scores * (1.0 - 0.3 + 0.3 * tw)
+        alpha = torch.softmax(scores, dim=-1)
+        if isinstance(at, TemporalAwareAttention):
+            alpha = at.dropout(alpha)
+        out = at.MLP(src + (alpha.unsqueeze(-1) * wq).sum(2))
+        if self.if_cat:
+            oh = F.one_hot(_to(cat_feat, dev, torch.long).reshape(B, W), num_classes=12)
+            out = torch.cat([out, oh.to(out.dtype)], dim=-1)
+        return self.MLP(out).sigmoid()
+
+    def _edge_imp_torch(self, subgraph, graphlet_imp, walks, training):
+        node_record, eidx_record, _ = subgraph
+        dev = graphlet_imp.device
+        i0 = _to(eidx_record[0], dev, torch.long)
+        i1 = _to(eidx_record[1], dev, torch.long)
+        B = graphlet_imp.shape[0]
+        ew = _to(walks[1], dev, torch.long).reshape(B, -1)
+        n_e = int(max(ew.max(), i0.max(), i1.max()) + 1)
+        wimp = graphlet_imp.repeat(1, 1, 3).view(B, -1)
+        if self.use_dependency_aware_sampling:
+            tw = _to(walks[2], dev, torch.float32).reshape(B, -1)
+            g = torch.cat([self.edge_raw_embed(ew), self.time_encoder(tw.unsqueeze(-1)).squeeze(-1)], dim=-1)
+            wimp = wimp * (0.5 + 0.5 * torch.sigmoid(self.edge_dependency_gcn(g).squeeze(-1)))
+        dense = torch.zeros(B, n_e, device=dev, dtype=wimp.dtype).scatter_reduce(-1, ew, wimp, "amax",
+                                                                                  include_self=False)
+        e0 = self.beta_sample(torch.gather(dense, -1, i0), training)
+        e1 = self.beta_sample(torch.gather(dense, -1, i1), training)
+        e0 = e0.masked_fill(_to(node_record[0], dev, torch.long) == 0, 0)
+        e1 = e1.masked_fill(_to(node_record[1], dev, torch.long) == 0, 0)
+        return e0, e1
+
+
+class _Packed:
+    def __init__(self, h):
+        self.h = h
+
+    def __del__(self):
+        if self.h is not None and L._lib is not None:
+            L._lib.tm_weights_free(self.h)
+            self.h = None

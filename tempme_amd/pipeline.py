@@ -1,0 +1,75 @@
+"""Device-resident explanation scoring of many target events per launch.
+
+One call = what temp_exp_main.py's eval loop does per batch for ``E / B`` batches of
+``B`` events (sampling as data_preprocess.py:106-134, TempME.forward x3,
+retrieve_explanation(training=False)), without host round trips:
+
+    tm_sample_events   fake dst, 2-hop subgraphs x3, walks x3, categories, edge counts
+    tm_encoder_fwd     graphlet importance for the 3 * E/B groups (one std per group)
+    tm_edge_importance explanation weights hop-1 [3, E, N] and hop-2 [3, E, N^2]
+
+Outputs are side-major: rows [s, b*B:(b+1)*B] of batch b are the reference's
+``retrieve_explanation`` rows [s*B:(s+1)*B].
+"""
+import torch
+
+from . import _lib as L
+from .preprocess import EventBuffers, sample_events
+
+
+class ExplainPipeline:
+    def __init__(self, explainer, graph, dst_list, N, M=3, B=100, seed=0, split=L.SPLIT_TEST):
+        self.ex = explainer
+        self.graph = graph
+        self.dev = graph.device
+        self.dst_list = dst_list.to(self.dev, torch.int32).contiguous()
+        self.N, self.M, self.B, self.W = int(N), int(M), int(B), int(N) * int(M)
+        self.seed, self.split = int(seed), int(split)
+        self._E = None
+
+    def _alloc(self, E):
+        if self._E == E:
+            return
+        dev, W, N = self.dev, self.W, self.N
+        self.buf = EventBuffers(E, N, self.M, dev)
+        n_walks = 3 * E * W
+        self.imp = torch.empty(max(n_walks, 1), dtype=torch.float32, device=dev)
+        nbytes = L.lib().tm_encoder_workspace_bytes(self.ex.packed_weights(), n_walks)
+        self.ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        self.h1 = torch.empty(max(3 * E * N, 1), dtype=torch.float32, device=dev)
+        self.h2 = torch.empty(max(3 * E * N * N, 1), dtype=torch.float32, device=dev)
+        self._E = E
+
+    def sample(self, src, dst, ts, eidx, event_ids):
+        self._alloc(int(src.numel()))
+        return sample_events(self.graph, self.seed, self.split, self.N, self.M, src, dst, ts, eidx, event_ids,
+                             self.dst_list, out=self.buf, check=False)
+
+    def encode(self, ts):
+        E, B, W = self._E, self.B, self.W
+        assert E % B == 0, "events per call must be a multiple of the batch size"
+        G = 3 * (E // B)
+        b = self.buf
+        cut = ts.repeat(3).contiguous()
+        self.ex.encoder_fwd(b.node6, b.eid3, b.ts3, b.cat, cut, b.cnt, G, B, W, out=self.imp, workspace=self.ws)
+        return self.imp
+
+    def explain(self):
+        E, B, W, N = self._E, self.B, self.W, self.N
+        G = 3 * (E // B)
+        b = self.buf
+        self.ex.edge_importance(b.eid3, b.ts3, self.imp, b.sub1_node, b.sub1_eid, b.sub2_node, b.sub2_eid, G, B, W,
+                                N, out1=self.h1, out2=self.h2)
+        return self.h1, self.h2
+
+    def run(self, src, dst, ts, eidx, event_ids):
+        """Returns (imp [3,E,W], hop-1 weights [3,E,N], hop-2 weights [3,E,N^2]) device tensors."""
+        self.sample(src, dst, ts, eidx, event_ids)
+        self.encode(ts)
+        self.explain()
+        E, N, W = self._E, self.N, self.W
+        return self.imp[:3 * E * W].view(3, E, W), self.h1[:3 * E * N].view(3, E, N), \
+            self.h2[:3 * E * N * N].view(3, E, N * N)
+
+    def check_errors(self):
+        L.raise_device_error(int(self.buf.err.item()), "ExplainPipeline")

@@ -1,0 +1,288 @@
+"""GPU parity: the HIP path through the C ABI vs (a) vectors produced by the reference
+itself (tests/golden) and (b) the CPU oracle on the same seeded inputs.
+
+Bit-exact for every sampled index / id / time / category / count; encoder outputs within
+rtol 1e-5, atol 1e-6 (BASELINE.json north_star).
+"""
+import json
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from oracle import encoder_ref as er
+from oracle import oracle as orc
+from oracle import philox as px
+
+pytestmark = pytest.mark.gpu
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+RTOL, ATOL = 1e-5, 1e-6
+
+
+@pytest.fixture(scope="module")
+def tm():
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a HIP device")
+    import tempme_amd
+    return tempme_amd
+
+
+def _finder(tm, src, dst, eidx, ts, n_nodes=None, seed=0, split=px.SPLIT_TEST):
+    return tm.NeighborFinder.from_edges(src, dst, eidx, ts, n_nodes, seed=seed, split=split)
+
+
+def test_graph_build_matches_oracle(tm):
+    z = np.load(os.path.join(G, "synth_small.npz"))
+    f = _finder(tm, z["src"], z["dst"], z["eidx"], z["ts"])
+    assert np.array_equal(f.off_set_l, z["csr_off"])
+    assert np.array_equal(f.node_idx_l, z["csr_node"])
+    assert np.array_equal(f.edge_idx_l, z["csr_eid"])
+    assert np.array_equal(f.node_ts_l, z["csr_ts"])
+    for u, e, p in z["nodeedge2idx"]:
+        assert f.nodeedge2idx[int(u)][int(e)] == p
+
+
+def test_kat_tie(tm):
+    k = json.load(open(os.path.join(G, "kats.json")))["kat_tie"]
+    adj = [[] for _ in range(k["n_nodes"])]
+    for s, d, e, t in zip(k["src"], k["dst"], k["eidx"], k["ts"]):
+        adj[s].append((d, e, t))
+        adj[d].append((s, e, t))
+    f = tm.NeighborFinder(adj)
+    assert {str(a): b for a, b in f.nodeedge2idx[1].items()} == k["nodeedge2idx_1"]
+    assert len(f.find_before(1, 4.0, e_idx=7)[0]) == 6
+    assert len(f.find_before(1, 4.0)[0]) == 4
+    # the device e_idx path must agree with the host dict: draw 1 neighbour before e=7 and e=4
+    n, e, t = f.get_temporal_neighbor(np.array([1, 1]), np.array([4.0, 4.0]), 8, e_idx_l=np.array([7, 4]),
+                                      event_ids=[0, 1])
+    assert set(e[0].tolist()) <= {1, 2, 3, 4, 5, 6} and set(e[1].tolist()) <= {1, 2, 3}
+
+
+def test_kat_leak(tm):
+    k = json.load(open(os.path.join(G, "kats.json")))["kat_leak"]
+    f = _finder(tm, k["src"], k["dst"], k["eidx"], k["ts"], k["n_nodes"], seed=k["seed"], split=k["split"])
+    sub = f.find_k_hop(2, np.array([1]), np.array([10.0]), k["N"], event_ids=[0], side=k["side"])
+    for h, key in enumerate(("hop1", "hop2")):
+        assert sub[0][h].tolist() == k[key][0] and sub[1][h].tolist() == k[key][1] and sub[2][h].tolist() == k[key][2]
+    w = f.find_k_walks(k["N"], np.array([1]), 1, sub, event_ids=[0], side=k["side"])
+    assert w[0].tolist() == k["walk_node"] and w[1].tolist() == k["walk_eid"]
+    assert w[2].tolist() == k["walk_ts"] and w[3].tolist() == k["walk_anony"]
+
+
+def test_khop_3hop_time_path(tm):
+    z = np.load(os.path.join(G, "synth_small.npz"))
+    f = _finder(tm, z["src"], z["dst"], z["eidx"], z["ts"], seed=3, split=px.SPLIT_TRAIN)
+    n = f.off_set_l.shape[0] - 1
+    sub = f.find_k_hop(3, np.arange(n), np.linspace(0, 41, n), 4, event_ids=100 + np.arange(n), side=px.SIDE_BGD)
+    for h in range(3):
+        assert np.array_equal(sub[0][h], z[f"khop3_node{h}"])
+        assert np.array_equal(sub[1][h], z[f"khop3_eid{h}"])
+        assert np.array_equal(sub[2][h], z[f"khop3_ts{h}"])
+
+
+def _check_events(tm, f, z, pre, seed, split, N, M, src, dst, ts, eidx, dst_list, n):
+    from tempme_amd.preprocess import sample_events
+    dev = f.device
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a[:n], dtype=dt)).to(dev)  # noqa: E731
+    b = sample_events(f.graph, seed, split, N, M, t(src, np.int32), t(dst, np.int32), t(ts, np.float64),
+                      t(eidx, np.int32), torch.arange(n, dtype=torch.int32, device=dev),
+                      torch.from_numpy(np.asarray(dst_list, np.int32)).to(dev))
+    h = lambda x: x.cpu().numpy()  # noqa: E731
+    assert np.array_equal(h(b.dst_fake[:n]), z[pre + "dst_fake"])
+    for s, side in enumerate(("src", "tgt", "bgd")):
+        for hop, sub in ((0, "sub1"), (1, "sub2")):
+            for fld in ("node", "eid", "ts"):
+                assert np.array_equal(h(getattr(b, f"{sub}_{fld}")[s]), z[f"{pre}subgraph_{side}_{hop}_{fld}"]), \
+                    (side, hop, fld)
+        assert np.array_equal(h(b.node6[s]), z[f"{pre}walks_{side}_node"]), side
+        assert np.array_equal(h(b.eid3[s]), z[f"{pre}walks_{side}_eid"]), side
+        assert np.array_equal(h(b.ts3[s]), z[f"{pre}walks_{side}_ts"]), side
+        assert np.array_equal(h(b.cat[s]), z[f"{pre}walks_{side}_cat"]), side
+        assert np.array_equal(h(b.cnt[s]).astype(np.int32), z[f"{pre}edge"][s]), side
+    W = N * M
+    freq = h(b.hist).astype(np.float64) / (n * W * 3)
+    for s, side in enumerate(("src", "tgt", "bgd")):
+        assert np.array_equal(freq[h(b.cat[s])], z[f"{pre}walks_{side}_marg"])
+    return b
+
+
+def test_fused_events_small(tm):
+    z = np.load(os.path.join(G, "synth_small.npz"))
+    f = _finder(tm, z["src"], z["dst"], z["eidx"], z["ts"])
+    for N in (5, 8):
+        _check_events(tm, f, z, f"N{N}_", 11, px.SPLIT_TEST, N, 3, z["src"], z["dst"], z["ts"], z["eidx"],
+                      np.unique(z["dst"]), 24)
+
+
+@pytest.mark.parametrize("mode", ["train", "test"])
+def test_fused_events_uslegis(tm, mode):
+    z = np.load(os.path.join(G, "uslegis_pipeline.npz"))
+    src, dst, ts, eidx = z[f"{mode}_src"], z[f"{mode}_dst"], z[f"{mode}_ts"], z[f"{mode}_eidx"]
+    if mode == "train":
+        f = _finder(tm, src, dst, eidx, ts, 224, split=px.SPLIT_TRAIN)
+    else:
+        df = pd.read_csv(os.path.join(G, "data", "ml_uslegis_sampled.csv"))
+        f = _finder(tm, df.u.values, df.i.values, df.idx.values, df.ts.values, 224)
+    split = px.SPLIT_TRAIN if mode == "train" else px.SPLIT_TEST
+    for N, n in ((20, 32), (30, 12)):
+        _check_events(tm, f, z, f"{mode}_N{N}_", 0, split, N, 3, src, dst, ts, eidx, z[f"{mode}_sampler_dst"], n)
+
+
+def test_separate_calls_equal_fused(tm):
+    """find_k_hop + find_k_walks + RandEdgeSampler + marginal + calculate_edge drop-ins reproduce
+    the reference pipeline (data_preprocess.py:106-134) event by event."""
+    z = np.load(os.path.join(G, "uslegis_pipeline.npz"))
+    df = pd.read_csv(os.path.join(G, "data", "ml_uslegis_sampled.csv"))
+    f = _finder(tm, df.u.values, df.i.values, df.idx.values, df.ts.values, 224)
+    sampler = tm.RandEdgeSampler((z["test_sampler_src"],), (z["test_sampler_dst"],), seed=0, split=px.SPLIT_TEST)
+    pre, N, n = "test_N20_", 20, 32
+    src, dst, ts, eidx = z["test_src"], z["test_dst"], z["test_ts"], z["test_eidx"]
+    ws = {s: [] for s in ("src", "tgt", "bgd")}
+    for k in range(n):
+        _, fake = sampler.sample(1, event_ids=[k])
+        assert fake[0] == z[pre + "dst_fake"][k]
+        for s_i, (side, root, e_l) in enumerate((("src", src[k:k + 1], eidx[k:k + 1]), ("tgt", dst[k:k + 1], eidx[k:k + 1]),
+                                                ("bgd", fake, None))):
+            sub = f.find_k_hop(2, root, ts[k:k + 1], N, e_idx_l=e_l, event_ids=[k], side=s_i + 1)
+            for hop in (0, 1):
+                assert np.array_equal(sub[0][hop][0], z[f"{pre}subgraph_{side}_{hop}_node"][k])
+                assert np.array_equal(sub[1][hop][0], z[f"{pre}subgraph_{side}_{hop}_eid"][k])
+            w = f.find_k_walks(N, root, 3, sub, event_ids=[k], side=s_i + 1)
+            assert np.array_equal(w[0][0], z[f"{pre}walks_{side}_node"][k])
+            assert np.array_equal(w[1][0], z[f"{pre}walks_{side}_eid"][k])
+            ws[side].append(np.concatenate([w[0], w[1], w[2], w[3]], -1).astype(np.float64))
+    wsn = tm.marginal(*[np.concatenate(ws[s]) for s in ("src", "tgt", "bgd")])
+    for s_i, side in enumerate(("src", "tgt", "bgd")):
+        assert np.array_equal(wsn[s_i][:, :, 12].astype(np.int32), z[f"{pre}walks_{side}_cat"])
+        assert np.array_equal(wsn[s_i][:, :, 13], z[f"{pre}walks_{side}_marg"])
+    edge = tm.calculate_edge(*wsn)
+    assert np.array_equal(edge.astype(np.int32), z[pre + "edge"])
+
+
+def test_pre_processing_dropin(tm):
+    z = np.load(os.path.join(G, "synth_small.npz"))
+    f = _finder(tm, z["src"], z["dst"], z["eidx"], z["ts"], seed=11)
+    sampler = tm.RandEdgeSampler((z["src"],), (z["dst"],))
+    out = tm.pre_processing(f, sampler, z["src"][:25], z["dst"][:25], z["ts"][:25], z["eidx"][:25], 8)
+    assert np.array_equal(out["walks_src"][:, :, 6:9].astype(np.int32), z["N8_walks_src_eid"])
+    assert np.array_equal(out["walks_bgd"][:, :, 12:15].astype(np.int32), z["N8_walks_bgd_anony"])
+    assert np.array_equal(out["subgraph_tgt_1"][:, 64:128].astype(np.int32), z["N8_subgraph_tgt_1_eid"])
+    assert np.array_equal(out["dst_fake"].astype(np.int32), z["N8_dst_fake"])
+
+
+def test_index_error_like_reference(tm):
+    f = _finder(tm, [1, 2], [2, 3], [1, 2], [1.0, 2.0], 4)
+    with pytest.raises(IndexError):
+        f.find_k_hop(2, np.array([1]), np.array([5.0]), 4, e_idx_l=np.array([2]))   # edge 2 is not on node 1
+    with pytest.raises(IndexError):
+        f.find_before(1, 5.0, e_idx=2)
+
+
+def test_empty_and_node0(tm):
+    f = _finder(tm, [0, 1, 2], [1, 2, 3], [1, 2, 3], [1.0, 2.0, 3.0], 4)
+    sub = f.find_k_hop(2, np.array([], np.int64), np.array([]), 4)
+    assert sub[0][0].shape == (0, 4) and sub[0][1].shape == (0, 16)
+    # node 0 is padding on the e_idx path even though it is a real node here (graph.py:133)
+    sub = f.find_k_hop(1, np.array([0]), np.array([9.0]), 4, e_idx_l=np.array([1]))
+    assert (sub[0][0] == 0).all()
+    # ... but the time path samples its list (graph.py:129)
+    sub = f.find_k_hop(1, np.array([0]), np.array([9.0]), 4)
+    assert (sub[1][0] == 1).all()
+
+
+def test_null_model(tm):
+    ref = json.load(open(os.path.join(G, "null_uslegis.json")))
+    d = tm.get_null_distribution("uslegis_sampled", data_dir=os.path.join(G, "data"), seed=ref["seed"])
+    assert {str(k): v for k, v in d.items()} == ref["dist"]
+
+
+# ------------------------------------------------------------------ encoder
+class _Base:
+    def __init__(self, n_feat, e_feat, dev):
+        self.n_feat_th = torch.as_tensor(n_feat)
+        self.e_feat_th = torch.as_tensor(e_feat)
+        self.node_raw_features = torch.nn.Embedding.from_pretrained(self.n_feat_th.to(dev), padding_idx=0, freeze=True)
+        self.edge_raw_features = torch.nn.Embedding.from_pretrained(self.e_feat_th.to(dev), padding_idx=0, freeze=True)
+
+
+def _explainer(tm, d):
+    dev = torch.device("cuda", 0)
+    null = {k + 1: float(v) for k, v in enumerate(d["null"])}
+    ex = tm.TempME(_Base(d["n_feat"], d["e_feat"], dev), "tgn", "uslegis_sampled", out_dim=40, hid_dim=64,
+                   device=dev, null_model=null)
+    missing, unexpected = ex.load_state_dict(d["sd"], strict=False)
+    assert not unexpected
+    assert all(not k.startswith(("event_conv", "attention.W1", "attention.W2", "attention.MLP", "MLP",
+                                 "edge_dependency_gcn", "time_encoder")) for k in missing)
+    return ex.to(dev).eval()
+
+
+@pytest.mark.parametrize("case", ["uslegis", "synth"])
+def test_encoder_matches_reference_goldens(tm, case):
+    from tests.encoder_inputs import SIDES, load
+    d = load(case)
+    ex = _explainer(tm, d)
+    imps, subs, walks = [], [], []
+    for s in SIDES:
+        x = d[s]
+        w = (x["node"], x["eid"], x["ts"], x["cat"], x["marg"])
+        imp = ex(w, d["ts_cut"], x["cnt"])
+        np.testing.assert_allclose(imp.cpu().numpy(), x["imp"], rtol=RTOL, atol=ATOL)
+        imps.append(imp)
+        subs.append((x["sub_node"], x["sub_eid"], x["sub_ts"]))
+        walks.append(w)
+    expl = ex.retrieve_explanation(subs[0], imps[0], walks[0], subs[1], imps[1], walks[1], subs[2], imps[2],
+                                   walks[2], training=False)
+    np.testing.assert_allclose(expl[0].cpu().numpy(), d["expl0"], rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(expl[1].cpu().numpy(), d["expl1"], rtol=RTOL, atol=ATOL)
+    for k, s in enumerate(SIDES):
+        kl = ex.kl_loss(imps[k], walks[k], target=0.3)
+        np.testing.assert_allclose(float(kl), d["kl"][k], rtol=RTOL, atol=ATOL)
+
+
+def test_pipeline_full_size_vs_oracle(tm):
+    """Bench workload shape (enron-like, N=20, B=100): sampled outputs bit-exact vs the C oracle on
+    every event of one batch per side, encoder + explanation vs the torch-fp32 oracle."""
+    from tempme_amd.pipeline import ExplainPipeline
+    from tempme_amd.workload import enron_like, split
+    g = enron_like(node_feat="uniform")
+    (src, dst, ts, eidx), rows, pool = split(g)
+    dev = torch.device("cuda", 0)
+    f = _finder(tm, g["src"][rows], g["dst"][rows], g["eidx"][rows], g["ts"][rows], g["n_nodes"], seed=5)
+    torch.manual_seed(0)
+    ex = tm.TempME(_Base(g["n_feat"], g["e_feat"], dev), "tgn", "enron_sampled", 40, 64, device=dev,
+                   null_model={k: 1 / 12 for k in range(1, 13)}).to(dev).eval()
+    N, B, E = 20, 100, 400
+    pipe = ExplainPipeline(ex, f.graph, torch.from_numpy(pool), N, 3, B, seed=5, split=px.SPLIT_TEST)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a[:E], dtype=dt)).to(dev)  # noqa: E731
+    imp, h1, h2 = pipe.run(t(src, np.int32), t(dst, np.int32), t(ts, np.float64), t(eidx, np.int32),
+                           torch.arange(E, dtype=torch.int32, device=dev))
+    torch.cuda.synchronize()
+    pipe.check_errors()
+    og = orc.OracleGraph(g["src"][rows], g["dst"][rows], g["eidx"][rows], g["ts"][rows], g["n_nodes"])
+    o = orc.event_pipeline(og, 5, px.SPLIT_TEST, N, 3, src[:E], dst[:E], ts[:E], eidx[:E], np.arange(E), pool, 8)
+    b = pipe.buf
+    h = lambda x: x.cpu().numpy()  # noqa: E731
+    assert np.array_equal(h(b.dst_fake[:E]), o["dst_fake"])
+    for name in ("node6", "eid3", "ts3", "cat", "sub1_node", "sub1_eid", "sub1_ts", "sub2_node", "sub2_eid", "sub2_ts"):
+        assert np.array_equal(h(getattr(b, name)).swapaxes(0, 1), o[name]), name
+    assert np.array_equal(h(b.cnt).swapaxes(0, 1).astype(np.int32), o["cnt"])
+    # encoder: one reference batch per side (batch 1 of 4) through the torch-fp32 oracle
+    sd = {k: v.detach().cpu() for k, v in ex.state_dict().items()}
+    nf, ef = torch.from_numpy(g["n_feat"]), torch.from_numpy(g["e_feat"])
+    W = N * 3
+    bi = 1
+    sl = slice(bi * B, (bi + 1) * B)
+    for s in range(3):
+        ref = er.forward(sd, nf, ef, o["node6"][sl, s], o["eid3"][sl, s], o["ts3"][sl, s], o["cat"][sl, s],
+                         ts[sl], o["cnt"][sl, s].astype(np.float64))
+        np.testing.assert_allclose(h(imp[s, sl]), ref.numpy()[..., 0], rtol=RTOL, atol=ATOL)
+        e0, e1 = er.edge_importance(sd, ef, ref, o["eid3"][sl, s], o["ts3"][sl, s],
+                                    [o["sub1_node"][sl, s], o["sub2_node"][sl, s]],
+                                    [o["sub1_eid"][sl, s], o["sub2_eid"][sl, s]])
+        np.testing.assert_allclose(h(h1[s, sl]), e0.numpy(), rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(h(h2[s, sl]), e1.numpy(), rtol=RTOL, atol=ATOL)
+    assert W == imp.shape[-1]
