@@ -63,7 +63,7 @@ def _sig(L):
     L.tm_perm_keys.argtypes = [u64, u32, i64, vp, vp]
     L.tm_motif_hist.argtypes = [vp, i64, i32, vp, vp, vp]
     L.tm_edge_counts.argtypes = [vp, i32, i32, vp, vp]
-    L.tm_sample_events.argtypes = [vp, u64, u32, i32, i32, i32, vp, vp, vp, vp, vp, vp, i64] + [vp] * 17
+    L.tm_sample_events.argtypes = [vp, u64, u32, i32, i32, i32, vp, vp, vp, vp, vp, vp, i64] + [vp] * 15
     L.tm_weights_create.argtypes = [i32, i32, i32, C.c_int, C.POINTER(vp)]
     L.tm_weights_pack.argtypes = [vp, C.POINTER(vp), vp]
     L.tm_weights_free.argtypes = [vp]

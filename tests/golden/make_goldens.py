@@ -348,7 +348,7 @@ def case_uslegis():
 
 
 def case_null():
-    CTX.update(seed=0)
+    CTX.update(seed=0, split=px.SPLIT_NULL)
     d = ref_null.get_null_distribution("uslegis_sampled")
     with open(os.path.join(HERE, "null_uslegis.json"), "w") as fh:
         json.dump({"seed": 0, "data": "uslegis_sampled", "N": 30,
@@ -412,7 +412,7 @@ def case_encoder():
     res = {"ts_cut": ts_cut, "batch_idx": batch_idx}
     for name, (nf, ef, seed) in feats.items():
         torch.manual_seed(seed)
-        CTX.update(seed=0)
+        CTX.update(seed=0, split=px.SPLIT_NULL)
         ex = TempME(_Base(nf, ef), base_model_type="tgn", data="uslegis_sampled", out_dim=40, hid_dim=64,
                     temp=0.07, if_cat_feature=True, dropout_p=0.1, device=torch.device("cpu"))
         ex.eval()

@@ -121,3 +121,37 @@ def test_uslegis_pipeline(mode):
         split = px.SPLIT_TEST
     for N, n_ev in ((20, 32), (30, 12)):
         _check_pipeline(g, z, f"{mode}_N{N}_", 0, split, N, 3, src, dst, ts, eidx, z[f"{mode}_sampler_dst"], n_ev)
+
+
+def test_null_model_oracle():
+    """utils/null_model.py:13-128 restated over the C oracle: keyed endpoint shuffle, random.seed(2023)
+    masks on the unshuffled columns, 500 test events x 3 sides with one walk per slot."""
+    import random
+    ref = json.load(open(os.path.join(G, "null_uslegis.json")))
+    g_df = pd.read_csv(os.path.join(G, "data", "ml_uslegis_sampled.csv"))
+    val_time, test_time = list(np.quantile(g_df.ts, [0.70, 0.85]))
+    ts_l, e_l = g_df.ts.values, g_df.idx.values
+    perm = px.keyed_permutation(len(ts_l), ref["seed"])
+    src_l, dst_l = g_df.u.values[perm], g_df.i.values[perm]
+    rnd = random.Random(2023)
+    total = set(np.unique(np.hstack([g_df.u.values, g_df.i.values])))
+    late = ts_l > val_time
+    mask = set(rnd.sample(list(set(src_l[late]).union(set(dst_l[late]))), int(0.1 * len(total))))
+    ms, md = g_df.u.map(lambda x: x in mask).values, g_df.i.map(lambda x: x in mask).values
+    tr = (ts_l <= val_time) * ((1 - ms) * (1 - md) > 0)
+    va, te = (ts_l <= test_time) * (ts_l > val_time), ts_l > test_time
+    pool = np.unique(np.concatenate([dst_l[tr], dst_l[va], dst_l[te]]))
+    g = orc.OracleGraph(src_l, dst_l, e_l, ts_l, int(max(src_l.max(), dst_l.max())) + 1)
+    n, N = 500, ref["N"]
+    o = orc.event_pipeline(g, ref["seed"], px.SPLIT_NULL, N, 1, src_l[te][:n], dst_l[te][:n], ts_l[te][:n],
+                           e_l[te][:n], np.arange(n), pool)
+    an = np.zeros((n * 3 * N, 3), np.int32)
+    # categories back to anony codes, then the null-model binning (key order of null_model.py:90)
+    codes = [(2, 1), (2, 2), (2, 3), (2, 0), (3, 1), (3, 3), (3, 2), (3, 0), (1, 3), (1, 2), (1, 1), (1, 0)]
+    c = o["cat"].reshape(-1)
+    an[:, 0] = 1
+    an[:, 1] = [codes[x][0] for x in c]
+    an[:, 2] = [codes[x][1] for x in c]
+    _, hist = orc.cat_hist(an, null_order=True)
+    dist = {str(k + 1): int(hist[k]) / (500 * 3 * N) for k in range(12)}
+    assert dist == ref["dist"]
