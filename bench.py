@@ -54,7 +54,7 @@ def sampling_bytes_per_event(N, M):
     return 3 * (khop + walks)
 
 
-def cpu_baseline(g, rows, events, pool, N, M, B, seed, sd, budget_s=12.0, max_batches=8):
+def cpu_baseline(g, rows, events, pool, N, M, B, seed, sd, budget_s=12.0, max_batches=400):
     """The oracle port (C sampler + torch-fp32 encoder) on the host cores, bounded sample."""
     from oracle import encoder_ref as er
     from oracle import oracle as orc
