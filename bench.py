@@ -43,6 +43,7 @@ def flops_model(de, dn, h, N, M):
     per_pos_gate = (de + dn) * h + h * (h // 2) + h // 2
     W = N * M
     return dict(gcn_kernel=2 * per_pos_gcn * 3, head_kernel=2 * per_walk_head, explain_kernel=2 * per_pos_gate * 3,
+                gate_per_edge=2 * per_pos_gate,
                 per_walk=2 * (3 * per_pos_gcn + per_walk_head + 3 * per_pos_gate), W=W)
 
 
@@ -171,7 +172,8 @@ def main():
         units = {"events_kernel": ("hbm", sampling_bytes_per_event(N, M) * E),
                  "gcn_kernel": ("mfma", fm["gcn_kernel"] * 3 * E * W),
                  "head_kernel": ("mfma", fm["head_kernel"] * 3 * E * W),
-                 "explain_kernel": ("mfma", fm["explain_kernel"] * 3 * E * W)}
+                 "explain_kernel": ("mfma", fm["explain_kernel"] * 3 * E * W),
+                 "gate_table_kernel": ("mfma", fm["gate_per_edge"] * (g["eidx"].max() + 1))}
         kernels = {}
         for name, (ms, cnt) in prof.items():
             avg_ms = ms / max(cnt, 1)

@@ -152,6 +152,19 @@ int tm_edge_importance(const tm_weights *w, const float *e_feat, int32_t n_group
                        const int32_t *sub1_eid, const int32_t *sub2_node, const int32_t *sub2_eid, float *out_h1,
                        float *out_h2, void *stream);
 
+/* Dependency-gate table (explainer_new.py:367-386 evaluated once per edge id): out_gf[e] =
+ * 0.5 + 0.5*sigmoid(depMLP([e_feat[e] | cos(t_e * basis_freq + phase)])) for e in [0, max_eid],
+ * t_e the edge's timestamp in g (as f32).  TM_E_UNSUPPORTED if an edge id carries several
+ * timestamps in g (then use tm_edge_importance). */
+int tm_edge_gate_table(const tm_weights *w, const tm_graph *g, const float *e_feat, float *out_gf, void *stream);
+
+/* tm_edge_importance driven by a gate table (n_ids entries): bit-identical outputs, no per-walk
+ * gate MLP.  *err_flag (nullable) is set if a walk edge id is outside the table. */
+int tm_edge_importance_tab(const float *gf, int32_t n_ids, int32_t n_groups, int32_t B, int32_t W, int32_t N,
+                           const int32_t *eid3, const float *imp, const int32_t *sub1_node, const int32_t *sub1_eid,
+                           const int32_t *sub2_node, const int32_t *sub2_eid, float *out_h1, float *out_h2,
+                           int32_t *err_flag, void *stream);
+
 /* ---------------------------------------------------------------- per-kernel timing
  * tm_profile_enable(1) clears and starts recording a HIP event pair around every kernel
  * launch, on that launch's stream; tm_profile_sync() waits and aggregates, returning the

@@ -33,7 +33,7 @@ EXPORTS = (
     "tm_last_error", "tm_version", "tm_graph_build", "tm_graph_free", "tm_graph_info", "tm_graph_export",
     "tm_sample_khop", "tm_sample_walks", "tm_neg_sample", "tm_perm_keys", "tm_motif_hist", "tm_edge_counts",
     "tm_sample_events", "tm_weights_create", "tm_weights_pack", "tm_weights_free", "tm_encoder_workspace_bytes",
-    "tm_encoder_fwd", "tm_edge_importance", "tm_profile_enable", "tm_profile_sync", "tm_profile_entry",
+    "tm_encoder_fwd", "tm_edge_importance", "tm_edge_gate_table", "tm_edge_importance_tab", "tm_profile_enable", "tm_profile_sync", "tm_profile_entry",
 )
 
 
@@ -71,6 +71,8 @@ def _sig(L):
     L.tm_encoder_workspace_bytes.argtypes = [vp, i64]
     L.tm_encoder_fwd.argtypes = [vp, vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.tm_edge_importance.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.tm_edge_gate_table.argtypes = [vp, vp, vp, vp, vp]
+    L.tm_edge_importance_tab.argtypes = [vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.tm_profile_enable.argtypes = [C.c_int]
     L.tm_profile_entry.argtypes = [C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(i64)]
     for name in EXPORTS:

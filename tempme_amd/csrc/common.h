@@ -58,6 +58,8 @@ struct DevGraph {
     const Rec *rec;         // [n_entries]
     const EdgeEnds *ends;   // [max_eid+1]
     const Pair *pair;       // [n_entries]
+    const double *ets;      // [max_eid+1] timestamp of each edge id (0 for absent ids)
+    int32_t ts_unique;      // every record of an edge id carries the same timestamp
 };
 
 // ------------------------------------------------------------------ Philox4x32-10
@@ -140,6 +142,7 @@ struct tm_graph {
     tmk::Rec *d_rec;
     tmk::EdgeEnds *d_ends;
     tmk::Pair *d_pair;
+    double *d_ets;
     // host copies (export)
     int64_t *h_off;
     int32_t *h_ngh, *h_eid, *h_dict;

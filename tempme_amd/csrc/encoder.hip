@@ -41,37 +41,56 @@ struct EncW {
 };
 
 // ------------------------------------------------------------------ MFMA tile GEMM
-// out[16mt.., 16nt..] = X[rows][ldx] (LDS) * W^T for tiles t = wave*2, wave*2+1, ... ; the
-// epilogue gets (mt, nt, acc) with acc[r] = D[4*(lane>>4)+r][lane&15].
-template <class Epi>
-__device__ __forceinline__ void gemm(const float *X, int ldx, const Lin &L, int MT, Epi epi) {
+// out[16mt.., 16nt..] = X[16*MT rows][ldx] (LDS) * W^T (packed, streamed from L2).
+// Each wave owns column tiles nt = wave, wave + nw, ... and sweeps all MT row tiles for
+// them, two column tiles at a time: per 16-deep K step it loads 2 weight fragments (the
+// next step's are prefetched into registers) and MT activation fragments (ds_read_b128)
+// and issues 8*MT MFMAs.  The epilogue gets (mt, nt, acc) with acc[r] = D[4*(lane>>4)+r][lane&15].
+template <int MT, class Epi>
+__device__ __forceinline__ void gemm(const float *X, int ldx, const Lin &L, Epi epi) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int arow = lane & 15, akoff = 4 * (lane >> 4);
-    const int T = MT * L.nt, nq = L.nq;
-    for (int t = wave * 2; t < T; t += nw * 2) {
-        const int t1 = t + 1;
-        const bool has1 = t1 < T;
-        const int mt0 = t / L.nt, nt0 = t % L.nt, mt1 = has1 ? t1 / L.nt : mt0, nt1 = has1 ? t1 % L.nt : nt0;
-        floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-        const float *xa0 = X + (mt0 * 16 + arow) * ldx + akoff;
-        const float *xa1 = X + (mt1 * 16 + arow) * ldx + akoff;
-        const float4 *wb0 = L.w + (size_t)nt0 * nq * 64 + lane;
-        const float4 *wb1 = L.w + (size_t)nt1 * nq * 64 + lane;
-        for (int q = 0; q < nq; ++q) {
-            const float4 b0 = wb0[q * 64], b1 = wb1[q * 64];
-            const float4 a0 = *reinterpret_cast<const float4 *>(xa0 + 16 * q);
-            const float4 a1 = *reinterpret_cast<const float4 *>(xa1 + 16 * q);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, b0.x, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, b1.x, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, b0.y, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, b1.y, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, b0.z, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, b1.z, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, b0.w, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, b1.w, acc1, 0, 0, 0);
+    const int nq = L.nq;
+    for (int nt0 = wave; nt0 < L.nt; nt0 += 2 * nw) {
+        const int nt1 = nt0 + nw;
+        const bool has1 = nt1 < L.nt;
+        floatx4 acc0[MT], acc1[MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+            acc0[m] = floatx4{0.f, 0.f, 0.f, 0.f};
+            acc1[m] = floatx4{0.f, 0.f, 0.f, 0.f};
         }
-        epi(mt0, nt0, acc0);
-        if (has1) epi(mt1, nt1, acc1);
+        const float4 *wb0 = L.w + (size_t)nt0 * nq * 64 + lane;
+        const float4 *wb1 = L.w + (size_t)(has1 ? nt1 : nt0) * nq * 64 + lane;
+        const float *xa = X + arow * ldx + akoff;
+        float4 b0 = wb0[0], b1 = wb1[0];
+        for (int q = 0; q < nq; ++q) {
+            float4 n0 = b0, n1 = b1;
+            if (q + 1 < nq) {
+                n0 = wb0[(q + 1) * 64];
+                n1 = wb1[(q + 1) * 64];
+            }
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                const float4 a = *reinterpret_cast<const float4 *>(xa + m * 16 * ldx + 16 * q);
+                acc0[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b0.x, acc0[m], 0, 0, 0);
+                acc1[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b1.x, acc1[m], 0, 0, 0);
+                acc0[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b0.y, acc0[m], 0, 0, 0);
+                acc1[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b1.y, acc1[m], 0, 0, 0);
+                acc0[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b0.z, acc0[m], 0, 0, 0);
+                acc1[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b1.z, acc1[m], 0, 0, 0);
+                acc0[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b0.w, acc0[m], 0, 0, 0);
+                acc1[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b1.w, acc1[m], 0, 0, 0);
+            }
+            b0 = n0;
+            b1 = n1;
+        }
+#pragma unroll
+        for (int m = 0; m < MT; ++m) epi(m, nt0, acc0[m]);
+        if (has1) {
+#pragma unroll
+            for (int m = 0; m < MT; ++m) epi(m, nt1, acc1[m]);
+        }
     }
 }
 
@@ -165,7 +184,7 @@ __global__ void __launch_bounds__(256) gcn_kernel(EncW P, int64_t n_rows, const 
     }
     __syncthreads();
     // L = lin_event(X); A = x_s + relu(x_t + L); B = x_t + relu(x_s + L)
-    gemm(X, ldx, P.ev, 2, [&](int mt, int nt, floatx4 acc) {
+    gemm<2>(X, ldx, P.ev, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) {
             const int row = erow(mt, r);
@@ -181,12 +200,12 @@ __global__ void __launch_bounds__(256) gcn_kernel(EncW P, int64_t n_rows, const 
         }
     });
     __syncthreads();
-    gemm(AB, ldab, P.g1, 4, [&](int mt, int nt, floatx4 acc) {
+    gemm<4>(AB, ldab, P.g1, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) H[erow(mt, r) * ldh + c] = relu(acc[r] + P.g1.b[c]);
     });
     __syncthreads();
-    gemm(H, ldh, P.g2, 4, [&](int mt, int nt, floatx4 acc) {
+    gemm<4>(H, ldh, P.g2, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) {
             const int row = erow(mt, r);
@@ -237,7 +256,7 @@ __global__ void __launch_bounds__(256) head_kernel(EncW P, int64_t n_walks, int6
     }
     if (tid < TILE_ROWS) s_cat[tid] = (w0 + tid < n_walks) ? cat[w0 + tid] : -1;
     __syncthreads();
-    gemm(T, LD, P.w2, 4, [&](int mt, int nt, floatx4 acc) {
+    gemm<4>(T, LD, P.w2, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) Q[erow(mt, r) * LD + c] = acc[r] + P.w2.b[c];
     });
@@ -250,7 +269,7 @@ __global__ void __launch_bounds__(256) head_kernel(EncW P, int64_t n_walks, int6
         *reinterpret_cast<float4 *>(S + w * LD + 4 * c4) = v;
     }
     __syncthreads();
-    gemm(S, LD, P.w1, 2, [&](int mt, int nt, floatx4 acc) {
+    gemm<2>(S, LD, P.w1, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) Pp[erow(mt, r) * LD + c] = acc[r] + P.w1.b[c];
     });
@@ -283,13 +302,13 @@ __global__ void __launch_bounds__(256) head_kernel(EncW P, int64_t n_walks, int6
         Pp[w * LD + c] = S[w * LD + c] + o;
     }
     __syncthreads();
-    gemm(Pp, LD, P.a1, 2, [&](int mt, int nt, floatx4 acc) {
+    gemm<2>(Pp, LD, P.a1, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) H1[erow(mt, r) * LDH + c] = relu(acc[r] + P.a1.b[c]);
     });
     __syncthreads();
     // X = [attention MLP out | one-hot(cat)]
-    gemm(H1, LDH, P.a2, 2, [&](int mt, int nt, floatx4 acc) {
+    gemm<2>(H1, LDH, P.a2, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) X[erow(mt, r) * LDM + c] = acc[r] + P.a2.b[c];
     });
@@ -298,12 +317,12 @@ __global__ void __launch_bounds__(256) head_kernel(EncW P, int64_t n_walks, int6
         X[w * LDM + HID + c] = (c < 12 && s_cat[w] == c) ? 1.f : 0.f;
     }
     __syncthreads();
-    gemm(X, LDM, P.m1, 2, [&](int mt, int nt, floatx4 acc) {
+    gemm<2>(X, LDM, P.m1, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) M1[erow(mt, r) * LDM + c] = c < P.m1.nout ? relu(acc[r] + P.m1.b[c]) : 0.f;
     });
     __syncthreads();
-    gemm(M1, LDM, P.m2, 2, [&](int mt, int nt, floatx4 acc) {
+    gemm<2>(M1, LDM, P.m2, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) M2[erow(mt, r) * LDH + c] = relu(acc[r] + P.m2.b[c]);
     });
@@ -370,12 +389,12 @@ __global__ void __launch_bounds__(256) explain_kernel(EncW P, int32_t W, int32_t
             X[r * ldx + c] = v;
         }
         __syncthreads();
-        gemm(X, ldx, P.d1, 2, [&](int mt, int nt, floatx4 acc) {
+        gemm<2>(X, ldx, P.d1, [&](int mt, int nt, floatx4 acc) {
             const int c = ecol(nt);
             for (int r = 0; r < 4; ++r) G1[erow(mt, r) * ldg + c] = relu(acc[r] + P.d1.b[c]);
         });
         __syncthreads();
-        gemm(G1, ldg, P.d2, 2, [&](int mt, int nt, floatx4 acc) {
+        gemm<2>(G1, ldg, P.d2, [&](int mt, int nt, floatx4 acc) {
             const int c = ecol(nt);
             for (int r = 0; r < 4; ++r) G2[erow(mt, r) * ldg2 + c] = relu(acc[r] + P.d2.b[c]);
         });
@@ -418,6 +437,113 @@ __global__ void __launch_bounds__(256) explain_kernel(EncW P, int32_t W, int32_t
             const int32_t k = hkey[h];
             if (k == key) {
                 p = __uint_as_float(hval[h]);
+                break;
+            }
+            if (k == -1) break;
+            h = (h + 1) & (hsize - 1);
+        }
+        const float a = fmaxf(p * 10.f, 1.f), b = fmaxf((1.f - p) * 10.f, 1.f);
+        const float v = nd == 0 ? 0.f : a / (a + b);
+        if (h1) out1[o] = v;
+        else out2[o] = v;
+    }
+}
+
+// ------------------------------------------------------------------ per-edge dependency gate table
+// The dependency gate (:367-386) is a function of (E[e], t) only, and every record of an edge id
+// carries the edge's single timestamp, so gf(e) = 0.5 + 0.5*sigmoid(depMLP([E[e] | cos(t_e*w+phi)]))
+// is computed once per edge id per call instead of once per walk position.
+__global__ void __launch_bounds__(256) gate_table_kernel(EncW P, int32_t n_ids, const double *__restrict__ ets,
+                                                         const float *__restrict__ e_feat, float *__restrict__ gf) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int de = P.de, kdep = P.kdep, kd16 = r16(kdep), ldx = kd16 + 8, ldg = HID + 8, ldg2 = HID / 2 + 8;
+    float *X = smem, *G1 = X + TILE_ROWS * ldx, *G2 = G1 + TILE_ROWS * ldg;
+    const int tid = threadIdx.x;
+    const int32_t e0 = blockIdx.x * TILE_ROWS;
+    for (int i = tid; i < TILE_ROWS * kd16; i += blockDim.x) {
+        const int r = i / kd16, c = i % kd16;
+        const int32_t e = e0 + r;
+        float v = 0.f;
+        if (e < n_ids) {
+            if (c < de) v = e_feat[(int64_t)e * de + c];
+            else if (c < kdep) v = time_cos((float)ets[e], P.freq[c - de], P.phase[c - de]);
+        }
+        X[r * ldx + c] = v;
+    }
+    __syncthreads();
+    gemm<2>(X, ldx, P.d1, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) G1[erow(mt, r) * ldg + c] = relu(acc[r] + P.d1.b[c]);
+    });
+    __syncthreads();
+    gemm<2>(G1, ldg, P.d2, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) G2[erow(mt, r) * ldg2 + c] = relu(acc[r] + P.d2.b[c]);
+    });
+    __syncthreads();
+    const int r = tid >> 3, sub = tid & 7;
+    float s = 0.f;
+    for (int c = sub; c < HID / 2; c += 8) s += G2[r * ldg2 + c] * P.d3w[c];
+    s += __shfl_xor(s, 1, 8);
+    s += __shfl_xor(s, 2, 8);
+    s += __shfl_xor(s, 4, 8);
+    if (sub == 0 && e0 + r < n_ids) {
+        const float z = s + P.d3b[0];
+        gf[e0 + r] = 0.5f + 0.5f * (1.f / (1.f + expf(-z)));
+    }
+}
+
+// retrieve_edge_imp_node with the gate table: per (group, event) the LDS hash keeps, per edge id,
+// the max graphlet importance of the walks through it; edge_imp = that max * gf(e), which equals
+// max_w(imp_w * gf(e)) bit for bit (rounding is monotone).
+__global__ void __launch_bounds__(256) explain_tab_kernel(int32_t W, int32_t N, int32_t hbits, int32_t n_ids,
+                                                          const float *__restrict__ gf,
+                                                          const int32_t *__restrict__ eid3,
+                                                          const float *__restrict__ imp,
+                                                          const int32_t *__restrict__ sub1_node,
+                                                          const int32_t *__restrict__ sub1_eid,
+                                                          const int32_t *__restrict__ sub2_node,
+                                                          const int32_t *__restrict__ sub2_eid, float *__restrict__ out1,
+                                                          float *__restrict__ out2, int32_t *err) {
+    extern __shared__ __attribute__((aligned(16))) int32_t hkey[];
+    const int hsize = 1 << hbits;
+    uint32_t *hval = reinterpret_cast<uint32_t *>(hkey + hsize);
+    const int64_t ge = blockIdx.x;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < hsize; i += blockDim.x) {
+        hkey[i] = -1;
+        hval[i] = 0u;
+    }
+    __syncthreads();
+    const int32_t *e3 = eid3 + ge * (int64_t)W * 3;
+    for (int r = tid; r < 3 * W; r += blockDim.x) {
+        const int32_t key = e3[r];
+        const float v = imp[ge * W + r / 3];
+        uint32_t h = hash_eid(key) >> (32 - hbits);
+        while (true) {
+            const int32_t prev = atomicCAS(&hkey[h], -1, key);
+            if (prev == -1 || prev == key) break;
+            h = (h + 1) & (hsize - 1);
+        }
+        atomicMax(&hval[h], __float_as_uint(v));
+    }
+    __syncthreads();
+    const int n1 = N, n2 = N * N;
+    for (int i = tid; i < n1 + n2; i += blockDim.x) {
+        const bool h1 = i < n1;
+        const int64_t o = h1 ? ge * n1 + i : ge * n2 + (i - n1);
+        const int32_t key = h1 ? sub1_eid[o] : sub2_eid[o];
+        const int32_t nd = h1 ? sub1_node[o] : sub2_node[o];
+        uint32_t h = hash_eid(key) >> (32 - hbits);
+        float p = 0.f;
+        while (true) {
+            const int32_t k = hkey[h];
+            if (k == key) {
+                if (key < 0 || key >= n_ids) {
+                    if (err) atomicCAS(err, 0, TM_E_ARG);
+                } else {
+                    p = __uint_as_float(hval[h]) * gf[key];
+                }
                 break;
             }
             if (k == -1) break;
@@ -563,6 +689,45 @@ extern "C" int tm_weights_free(tm_weights *w) {
 extern "C" int64_t tm_encoder_workspace_bytes(const tm_weights *w, int64_t n_walks) {
     (void)w;
     return n_walks * 3 * 2 * HID * (int64_t)sizeof(float) + (n_walks + 64) * (int64_t)sizeof(float) + 256;
+}
+
+static size_t gate_lds(const EncW &P) {
+    return sizeof(float) * (TILE_ROWS * (r16(P.kdep) + 8) + TILE_ROWS * (HID + 8) + TILE_ROWS * (HID / 2 + 8));
+}
+
+extern "C" int tm_edge_gate_table(const tm_weights *w, const tm_graph *g, const float *e_feat, float *out_gf,
+                                  void *stream) {
+    if (!w || !g || !e_feat || !out_gf) return fail(TM_E_ARG, "tm_edge_gate_table: bad arguments");
+    if (!g->d.ts_unique)
+        return fail(TM_E_UNSUPPORTED, "tm_edge_gate_table: an edge id carries several timestamps; use tm_edge_importance");
+    const int32_t n = g->d.max_eid + 1;
+    hipEvent_t pe = prof_begin(S_(stream));
+    gate_table_kernel<<<dim3((n + TILE_ROWS - 1) / TILE_ROWS), 256, gate_lds(w->P), S_(stream)>>>(w->P, n, g->d.ets,
+                                                                                                e_feat, out_gf);
+    TM_CHECK_LAUNCH();
+    prof_end("gate_table_kernel", S_(stream), pe);
+    return TM_OK;
+}
+
+extern "C" int tm_edge_importance_tab(const float *gf, int32_t n_ids, int32_t n_groups, int32_t B, int32_t W,
+                                      int32_t N, const int32_t *eid3, const float *imp, const int32_t *sub1_node,
+                                      const int32_t *sub1_eid, const int32_t *sub2_node, const int32_t *sub2_eid,
+                                      float *out_h1, float *out_h2, int32_t *err_flag, void *stream) {
+    if (n_groups < 0 || B < 0 || W <= 0 || N <= 0 || n_ids <= 0)
+        return fail(TM_E_ARG, "tm_edge_importance_tab: bad arguments");
+    const int64_t rows = (int64_t)n_groups * B;
+    if (rows == 0) return TM_OK;
+    if (!gf || !eid3 || !imp || !sub1_node || !sub1_eid || !sub2_node || !sub2_eid || !out_h1 || !out_h2)
+        return fail(TM_E_ARG, "tm_edge_importance_tab: NULL pointer");
+    int hbits = 6;
+    while ((1 << hbits) < 2 * 3 * W) ++hbits;
+    if (hbits > 14) return fail(TM_E_UNSUPPORTED, "tm_edge_importance_tab: too many walks per event");
+    hipEvent_t pe = prof_begin(S_(stream));
+    explain_tab_kernel<<<dim3((unsigned)rows), 256, 2 * sizeof(int32_t) * (1u << hbits), S_(stream)>>>(
+        W, N, hbits, n_ids, gf, eid3, imp, sub1_node, sub1_eid, sub2_node, sub2_eid, out_h1, out_h2, err_flag);
+    TM_CHECK_LAUNCH();
+    prof_end("explain_tab_kernel", S_(stream), pe);
+    return TM_OK;
 }
 
 static size_t gcn_lds(const EncW &P) {

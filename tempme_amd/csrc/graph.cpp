@@ -28,6 +28,7 @@ static void free_graph(tm_graph *g) {
     if (g->d_rec) (void)hipFree(g->d_rec);
     if (g->d_ends) (void)hipFree(g->d_ends);
     if (g->d_pair) (void)hipFree(g->d_pair);
+    if (g->d_ets) (void)hipFree(g->d_ets);
     delete[] g->h_off;
     delete[] g->h_ngh;
     delete[] g->h_eid;
@@ -65,6 +66,17 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
     std::vector<Pair> pair(nn);
     std::vector<EdgeEnds> ends((size_t)max_eid + 1, EdgeEnds{-1, 0, -1, 0});
     std::vector<int32_t> off32(n_nodes + 1);
+    std::vector<double> ets((size_t)max_eid + 1, 0.0);
+    std::vector<char> seen((size_t)max_eid + 1, 0);
+    int32_t ts_unique = 1;
+    for (int64_t i = 0; i < n; ++i) {
+        if (!seen[eid[i]]) {
+            seen[eid[i]] = 1;
+            ets[eid[i]] = ts[i];
+        } else if (!(ets[eid[i]] == ts[i])) {
+            ts_unique = 0;
+        }
+    }
 
     std::vector<int64_t> idx;
     std::unordered_map<int32_t, int32_t> dict;
@@ -145,6 +157,8 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
     e = e ? e : hipMalloc(&g->d_rec, sizeof(Rec) * nn);
     e = e ? e : hipMalloc(&g->d_ends, sizeof(EdgeEnds) * ends.size());
     e = e ? e : hipMalloc(&g->d_pair, sizeof(Pair) * nn);
+    e = e ? e : hipMalloc(&g->d_ets, sizeof(double) * ets.size());
+    e = e ? e : hipMemcpy(g->d_ets, ets.data(), sizeof(double) * ets.size(), hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(g->d_off, off32.data(), sizeof(int32_t) * (n_nodes + 1), hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(g->d_rec, rec.data(), sizeof(Rec) * nn, hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(g->d_ends, ends.data(), sizeof(EdgeEnds) * ends.size(), hipMemcpyHostToDevice);
@@ -154,7 +168,7 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
         free_graph(g);
         return fail(TM_E_HIP, std::string("tm_graph_build: ") + hipGetErrorString(e));
     }
-    g->d = DevGraph{n_nodes, max_eid, n, g->d_off, g->d_rec, g->d_ends, g->d_pair};
+    g->d = DevGraph{n_nodes, max_eid, n, g->d_off, g->d_rec, g->d_ends, g->d_pair, g->d_ets, ts_unique};
     *out = g;
     return TM_OK;
 }

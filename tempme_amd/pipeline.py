@@ -38,6 +38,7 @@ class ExplainPipeline:
         self.ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         self.h1 = torch.empty(max(3 * E * N, 1), dtype=torch.float32, device=dev)
         self.h2 = torch.empty(max(3 * E * N * N, 1), dtype=torch.float32, device=dev)
+        self.gf = torch.empty(self.graph.max_eid + 1, dtype=torch.float32, device=dev)
         self._E = E
 
     def sample(self, src, dst, ts, eidx, event_ids):
@@ -55,11 +56,19 @@ class ExplainPipeline:
         return self.imp
 
     def explain(self):
+        """retrieve_explanation(training=False) for all groups: per-edge gate table (once per call),
+        then the table-driven scatter-max / gather / Beta-mean / mask kernel."""
         E, B, W, N = self._E, self.B, self.W, self.N
         G = 3 * (E // B)
         b = self.buf
-        self.ex.edge_importance(b.eid3, b.ts3, self.imp, b.sub1_node, b.sub1_eid, b.sub2_node, b.sub2_eid, G, B, W,
-                                N, out1=self.h1, out2=self.h2)
+        dev = self.dev
+        _, et = self.ex.feature_tables()
+        L.check(L.lib().tm_edge_gate_table(self.ex.packed_weights(), self.graph.handle, L.ptr(et), L.ptr(self.gf),
+                                           L.stream_ptr(dev)), "tm_edge_gate_table")
+        L.check(L.lib().tm_edge_importance_tab(L.ptr(self.gf), self.gf.numel(), G, B, W, N, L.ptr(b.eid3),
+                                               L.ptr(self.imp), L.ptr(b.sub1_node), L.ptr(b.sub1_eid),
+                                               L.ptr(b.sub2_node), L.ptr(b.sub2_eid), L.ptr(self.h1), L.ptr(self.h2),
+                                               L.ptr(b.err), L.stream_ptr(dev)), "tm_edge_importance_tab")
         return self.h1, self.h2
 
     def run(self, src, dst, ts, eidx, event_ids):

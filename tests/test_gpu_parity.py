@@ -286,3 +286,29 @@ def test_pipeline_full_size_vs_oracle(tm):
         np.testing.assert_allclose(h(h1[s, sl]), e0.numpy(), rtol=RTOL, atol=ATOL)
         np.testing.assert_allclose(h(h2[s, sl]), e1.numpy(), rtol=RTOL, atol=ATOL)
     assert W == imp.shape[-1]
+
+
+def test_gate_table_path_bitwise_equals_per_walk_path(tm):
+    """tm_edge_importance_tab (gate once per edge id, max before the gate multiply) must equal the
+    per-walk-position path (tm_edge_importance, the reference's order of operations) bit for bit."""
+    from tempme_amd.pipeline import ExplainPipeline
+    from tempme_amd.workload import enron_like, split
+    g = enron_like(n_nodes=120, n_edges=6000, node_feat="uniform", seed=9)
+    (src, dst, ts, eidx), rows, pool = split(g)
+    dev = torch.device("cuda", 0)
+    f = _finder(tm, g["src"][rows], g["dst"][rows], g["eidx"][rows], g["ts"][rows], g["n_nodes"], seed=2)
+    torch.manual_seed(1)
+    ex = tm.TempME(_Base(g["n_feat"], g["e_feat"], dev), "tgn", "x", 40, 64, device=dev,
+                   null_model={k: 1 / 12 for k in range(1, 13)}).to(dev).eval()
+    N, B, E = 20, 50, 200
+    pipe = ExplainPipeline(ex, f.graph, torch.from_numpy(pool), N, 3, B, seed=2)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a[:E], dtype=dt)).to(dev)  # noqa: E731
+    imp, h1, h2 = pipe.run(t(src, np.int32), t(dst, np.int32), t(ts, np.float64), t(eidx, np.int32),
+                           torch.arange(E, dtype=torch.int32, device=dev))
+    b = pipe.buf
+    o1, o2 = ex.edge_importance(b.eid3, b.ts3, pipe.imp, b.sub1_node, b.sub1_eid, b.sub2_node, b.sub2_eid,
+                                3 * E // B, B, N * 3, N)
+    torch.cuda.synchronize()
+    pipe.check_errors()
+    assert torch.equal(o1[:3 * E * N].view(3, E, N), h1)
+    assert torch.equal(o2[:3 * E * N * N].view(3, E, N * N), h2)
