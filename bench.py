@@ -42,7 +42,10 @@ def flops_model(de, dn, h, N, M):
     per_walk_head = 3 * (2 * h) ** 2 + (2 * h) * h + h * h + (h + 12) ** 2 + (h + 12) * h + h + 2 * 2 * h
     per_pos_gate = (de + dn) * h + h * (h // 2) + h // 2
     W = N * M
+    # walk_kernel executes position 2 once per hop-1 slot (shared by the M walks of the slot)
+    exec_walk = 2 * ((2 + 1.0 / M) * per_pos_gcn + per_walk_head - (1 - 1.0 / M) * (2 * h) ** 2)
     return dict(gcn_kernel=2 * per_pos_gcn * 3, head_kernel=2 * per_walk_head, explain_kernel=2 * per_pos_gate * 3,
+                walk_kernel=2 * (3 * per_pos_gcn + per_walk_head), walk_kernel_executed=exec_walk,
                 gate_per_edge=2 * per_pos_gate,
                 per_walk=2 * (3 * per_pos_gcn + per_walk_head + 3 * per_pos_gate), W=W)
 
@@ -173,7 +176,9 @@ def main():
                  "gcn_kernel": ("mfma", fm["gcn_kernel"] * 3 * E * W),
                  "head_kernel": ("mfma", fm["head_kernel"] * 3 * E * W),
                  "explain_kernel": ("mfma", fm["explain_kernel"] * 3 * E * W),
-                 "gate_table_kernel": ("mfma", fm["gate_per_edge"] * (g["eidx"].max() + 1))}
+                 "gate_table_kernel": ("mfma", fm["gate_per_edge"] * (g["eidx"].max() + 1)),
+                 "walk_kernel": ("mfma", fm["walk_kernel"] * 3 * E * W)}
+        executed = {"walk_kernel": fm["walk_kernel_executed"] * 3 * E * W}
         kernels = {}
         for name, (ms, cnt) in prof.items():
             avg_ms = ms / max(cnt, 1)
@@ -187,6 +192,9 @@ def main():
                     ach = work / (avg_ms * 1e-3) / 1e12
                     ent.update(bound="mfma", achieved=round(ach, 2), unit="TFLOP/s",
                                frac=round(ach / FP32_MFMA_PEAK_TF, 4))
+                    if name in executed:
+                        ex_tf = executed[name] / (avg_ms * 1e-3) / 1e12
+                        ent.update(executed_tflops=round(ex_tf, 2), executed_frac=round(ex_tf / FP32_MFMA_PEAK_TF, 4))
             kernels[name] = ent
         dom = max((k for k in kernels if "bound" in kernels[k]), key=lambda k: kernels[k]["avg_ms"])
         d = kernels[dom]

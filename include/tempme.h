@@ -138,10 +138,13 @@ int64_t tm_encoder_workspace_bytes(const tm_weights *w, int64_t n_walks);
 /* TempME.forward (explainer_new.py:174-201), eval, for n_groups groups of B*W walks each
  * (one group = one reference call: one side of one batch; the attention's time std is
  * batch-global per group, :828).  Walk arrays are [G,B,W,...]; cut [G,B] (f64, event time);
- * cnt [G,B,W,3,3] f32.  out_imp [G,B,W] (graphlet importance, sigmoid output). */
+ * cnt [G,B,W,3,3] f32.  out_imp [G,B,W] (graphlet importance, sigmoid output).
+ * M = walks per hop-1 slot as find_k_walks lays them out (walks w and w' share position 2 iff
+ * w/M == w'/M, graph.py:283-289); position 2 is then encoded once per slot.  M = 1 is always safe. */
 int tm_encoder_fwd(const tm_weights *w, const float *n_feat, const float *e_feat, int32_t n_groups, int32_t B,
-                   int32_t W, const int32_t *node6, const int32_t *eid3, const float *ts3, const int32_t *cat,
-                   const double *cut, const float *cnt, void *workspace, float *out_imp, void *stream);
+                   int32_t W, int32_t M, const int32_t *node6, const int32_t *eid3, const float *ts3,
+                   const int32_t *cat, const double *cut, const float *cnt, void *workspace, float *out_imp,
+                   void *stream);
 
 /* retrieve_edge_imp_node, eval (explainer_new.py:354-406, :420-430) for each of the G*B
  * (group, event) rows: dependency gate, walk->edge scatter-max, gather at the subgraph eids,

@@ -69,7 +69,7 @@ def _sig(L):
     L.tm_weights_free.argtypes = [vp]
     L.tm_encoder_workspace_bytes.restype = i64
     L.tm_encoder_workspace_bytes.argtypes = [vp, i64]
-    L.tm_encoder_fwd.argtypes = [vp, vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.tm_encoder_fwd.argtypes = [vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.tm_edge_importance.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.tm_edge_gate_table.argtypes = [vp, vp, vp, vp, vp]
     L.tm_edge_importance_tab.argtypes = [vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]

@@ -449,6 +449,303 @@ __global__ void __launch_bounds__(256) explain_kernel(EncW P, int32_t W, int32_t
     }
 }
 
+// ------------------------------------------------------------------ fused register-resident walk encoder
+// Weights are the MFMA A operand (16 output features per tile, packed as above); activations are
+// the B operand with one walk position per column: lane l holds features 16q + 4(l>>4) + {0..3} of
+// column l&15.  The D tile of one layer is then exactly the B fragment of K-step q = tile of the
+// next layer, so the whole chain stays in registers.  A wave owns 16 hop-1 slots (columns):
+// position 2 (shared by the M walks of a slot: same e1, t1, v1, root, edge counts, dt = 0) is
+// encoded once per slot, positions 0/1 once per walk.
+// out[t] = W tile t * x  over the flattened (t, q) sequence, weights prefetched PF steps ahead in
+// a rotating register buffer; sched_barrier pins each step so the loads stay PF steps ahead instead
+// of being hoisted (which would need NTO*NQ registers).
+constexpr int PF = 6;
+
+#define TM_W_ADDR(i) ((((i) / NQ) * nq + ((i) % NQ)) * 64)
+
+// The lane index laundered through an opaque asm: loads addressed with it cannot be hoisted out of
+// the pass loop by LICM (hoisting every loop-invariant weight/bias load costs ~300 registers).
+__device__ __forceinline__ int lane_id() {
+    int l = threadIdx.x & 63;
+    asm volatile("" : "+v"(l));
+    return l;
+}
+
+template <int NTO, int NQ>
+__device__ __forceinline__ void rgemm(const Lin &L, const floatx4 (&x)[NQ], floatx4 (&o)[NTO]) {
+    const float4 *wp = L.w + lane_id();
+    const int nq = L.nq;
+    constexpr int N = NTO * NQ, D = PF < N ? PF : N;
+#pragma unroll
+    for (int t = 0; t < NTO; ++t) o[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float4 buf[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) buf[i] = wp[TM_W_ADDR(i)];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const int t = i / NQ, q = i % NQ;
+        const float4 w = buf[i % D];
+        if (i + D < N) buf[i % D] = wp[TM_W_ADDR(i + D)];
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, x[q].x, o[t], 0, 0, 0);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, x[q].y, o[t], 0, 0, 0);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, x[q].z, o[t], 0, 0, 0);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, x[q].w, o[t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// two column sets through the same weights (one weight load feeds both)
+template <int NTO, int NQ>
+__device__ __forceinline__ void rgemm2(const Lin &L, const floatx4 (&x)[NQ], const floatx4 (&y)[NQ],
+                                       floatx4 (&o)[NTO], floatx4 (&p)[NTO]) {
+    const float4 *wp = L.w + lane_id();
+    const int nq = L.nq;
+    constexpr int N = NTO * NQ, D = PF < N ? PF : N;
+#pragma unroll
+    for (int t = 0; t < NTO; ++t) {
+        o[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+        p[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    float4 buf[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) buf[i] = wp[TM_W_ADDR(i)];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const int t = i / NQ, q = i % NQ;
+        const float4 w = buf[i % D];
+        if (i + D < N) buf[i % D] = wp[TM_W_ADDR(i + D)];
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, x[q].x, o[t], 0, 0, 0);
+        p[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, y[q].x, p[t], 0, 0, 0);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, x[q].y, o[t], 0, 0, 0);
+        p[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, y[q].y, p[t], 0, 0, 0);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, x[q].z, o[t], 0, 0, 0);
+        p[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, y[q].z, p[t], 0, 0, 0);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, x[q].w, o[t], 0, 0, 0);
+        p[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, y[q].w, p[t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+__device__ __forceinline__ float4 bias4(const float *b, int t) {
+    return *reinterpret_cast<const float4 *>(b + 16 * t + 4 * (lane_id() >> 4));
+}
+
+struct WalkArgs {
+    EncW P;
+    int64_t n_slots;      // total hop-1 slots = n_event_groups * (W / M)
+    int32_t W, M, BW;     // walks per event-group, walks per slot, walks per std group (B*W)
+    const float *n_feat, *e_feat;
+    const int32_t *node6, *eid3, *cat;
+    const float *ts3, *cnt, *stdv;
+    const double *cut;
+    float *out;
+};
+
+// one walk position for the 16 columns of this wave -> F = [U_s | U_t] (8 tiles, B layout)
+template <int NQE, int NTD>
+__device__ __forceinline__ void encode_position(const WalkArgs &a, int64_t gw, bool valid, int p, floatx4 (&F)[8]) {
+    const EncW &P = a.P;
+    const int g = lane_id() >> 4;
+    const int de = P.de, dn = P.dn, kev = P.kev;
+    int32_t e = 0, ns = 0, nt = 0;
+    float dt = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f;
+    if (valid) {
+        e = a.eid3[gw * 3 + p];
+        ns = a.node6[gw * 6 + 2 * p];
+        nt = a.node6[gw * 6 + 2 * p + 1];
+        dt = a.ts3[gw * 3 + 2] - a.ts3[gw * 3 + p];   // relative to walk position 2 (:326)
+        c0 = a.cnt[gw * 9 + p * 3 + 0];
+        c1 = a.cnt[gw * 9 + p * 3 + 1];
+        c2 = a.cnt[gw * 9 + p * 3 + 2];
+    }
+    // event features [E(e) | cnt | cos(dt * w + phi)] in B layout, 4 per lane per K step
+    floatx4 x[NQE];
+#pragma unroll
+    for (int q = 0; q < NQE; ++q) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int k = 16 * q + 4 * g + s;
+            float v = 0.f;
+            if (k < de) v = a.e_feat[(int64_t)e * de + k];
+            else if (k < de + 3) v = (k == de) ? c0 : (k == de + 1) ? c1 : c2;
+            else if (k < kev) v = time_cos(dt, P.freq[k - de - 3], P.phase[k - de - 3]);
+            x[q][s] = v;
+        }
+    }
+    floatx4 L[NTD];
+    rgemm<NTD, NQE>(P.ev, x, L);
+    // A = x_s + relu(x_t + L), B = x_t + relu(x_s + L)   (event_gcn :93-96, lin_event shared)
+    floatx4 A[NTD], Bv[NTD];
+#pragma unroll
+    for (int t = 0; t < NTD; ++t) {
+        const float4 b = bias4(P.ev.b, t);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int f = 16 * t + 4 * g + r;
+            float av = 0.f, bvv = 0.f;
+            if (f < dn) {
+                const float l = L[t][r] + (r == 0 ? b.x : r == 1 ? b.y : r == 2 ? b.z : b.w);
+                const float xs = a.n_feat[(int64_t)ns * dn + f], xt = a.n_feat[(int64_t)nt * dn + f];
+                av = xs + relu(xt + l);
+                bvv = xt + relu(xs + l);
+            }
+            A[t][r] = av;
+            Bv[t][r] = bvv;
+        }
+    }
+    floatx4 Hs[4], Ht[4];
+    rgemm2<4, NTD>(P.g1, A, Bv, Hs, Ht);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const float4 b = bias4(P.g1.b, t);
+        Hs[t] = floatx4{relu(Hs[t][0] + b.x), relu(Hs[t][1] + b.y), relu(Hs[t][2] + b.z), relu(Hs[t][3] + b.w)};
+        Ht[t] = floatx4{relu(Ht[t][0] + b.x), relu(Ht[t][1] + b.y), relu(Ht[t][2] + b.z), relu(Ht[t][3] + b.w)};
+    }
+    floatx4 Us[4], Ut[4];
+    rgemm2<4, 4>(P.g2, Hs, Ht, Us, Ut);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const float4 b = bias4(P.g2.b, t);
+        F[t] = floatx4{Us[t][0] + b.x, Us[t][1] + b.y, Us[t][2] + b.z, Us[t][3] + b.w};
+        F[4 + t] = floatx4{Ut[t][0] + b.x, Ut[t][1] + b.y, Ut[t][2] + b.z, Ut[t][3] + b.w};
+    }
+}
+
+// sum over the 4 lane groups sharing a column (lanes l, l^16, l^32, l^48)
+__device__ __forceinline__ float col_sum(float v) {
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    return v;
+}
+
+// attention head + final MLP for the 16 walks of this wave (Q1 in registers, F2/Wp/Q0 in the stash)
+__device__ __forceinline__ void walk_head(const WalkArgs &a, int64_t gw, int64_t eg, bool valid,
+                                          const floatx4 (&sF2)[8][64], const floatx4 (&sWp)[8][64],
+                                          const floatx4 (&Q0)[8], const floatx4 (&Q1)[8]) {
+    const EncW &P = a.P;
+    const int lane = threadIdx.x & 63, g = lane_id() >> 4;
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        const floatx4 wp = sWp[t][lane];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            s0 += wp[r] * Q0[t][r];
+            s1 += wp[r] * Q1[t][r];
+        }
+    }
+    s0 = col_sum(s0);
+    s1 = col_sum(s1);
+    float tw0 = 0.f, tw1 = 0.f;
+    int32_t c = -1;
+    if (valid) {
+        const float cu = (float)a.cut[eg];
+        const float sd = a.stdv[gw / a.BW] + 1e-6f;
+        tw0 = expf(-fabsf(cu - a.ts3[gw * 3 + 0]) / sd);
+        tw1 = expf(-fabsf(cu - a.ts3[gw * 3 + 1]) / sd);
+        c = a.cat[gw];
+    }
+    // scores * (1.0 - 0.3 + 0.3 * time_weight) (:835-836), softmax over the 2 targets
+    s0 *= __fadd_rn(0.7f, __fmul_rn(0.3f, tw0));
+    s1 *= __fadd_rn(0.7f, __fmul_rn(0.3f, tw1));
+    const float mx = fmaxf(s0, s1), e0 = expf(s0 - mx), e1 = expf(s1 - mx), sum = e0 + e1;
+    const float al0 = e0 / sum, al1 = e1 / sum;
+    floatx4 O[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        const floatx4 f2 = sF2[t][lane];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) O[t][r] = f2[r] + (al0 * Q0[t][r] + al1 * Q1[t][r]);
+    }
+    floatx4 H1[4];
+    rgemm<4, 8>(P.a1, O, H1);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const float4 b = bias4(P.a1.b, t);
+        H1[t] = floatx4{relu(H1[t][0] + b.x), relu(H1[t][1] + b.y), relu(H1[t][2] + b.z), relu(H1[t][3] + b.w)};
+    }
+    floatx4 X5[5];
+    {
+        floatx4 H2[4];
+        rgemm<4, 4>(P.a2, H1, H2);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const float4 b = bias4(P.a2.b, t);
+            X5[t] = floatx4{H2[t][0] + b.x, H2[t][1] + b.y, H2[t][2] + b.z, H2[t][3] + b.w};
+        }
+        // one-hot category in features 64..75 (compute_catogory_feautres :308-315)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) X5[4][r] = (c == 4 * g + r) ? 1.f : 0.f;
+    }
+    floatx4 M1[5];
+    rgemm<5, 5>(P.m1, X5, M1);
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+        const float4 b = bias4(P.m1.b, t);
+        M1[t] = floatx4{relu(M1[t][0] + b.x), relu(M1[t][1] + b.y), relu(M1[t][2] + b.z), relu(M1[t][3] + b.w)};
+    }
+    floatx4 M2[4];
+    rgemm<4, 5>(P.m2, M1, M2);
+    float z = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const float4 b = bias4(P.m2.b, t);
+        const float4 w3 = *reinterpret_cast<const float4 *>(P.m3w + 16 * t + 4 * g);
+        z += relu(M2[t][0] + b.x) * w3.x + relu(M2[t][1] + b.y) * w3.y + relu(M2[t][2] + b.z) * w3.z +
+             relu(M2[t][3] + b.w) * w3.w;
+    }
+    z = col_sum(z) + P.m3b[0];
+    if (valid && g == 0) a.out[gw] = 1.f / (1.f + expf(-z));
+}
+
+template <int NQE, int NTD>
+__global__ void __launch_bounds__(256) walk_kernel(WalkArgs a) {
+    const EncW &P = a.P;
+    const int lane = threadIdx.x & 63, col = lane & 15;
+    const int64_t unit = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t gs = unit * 16 + col;                 // this column's hop-1 slot
+    const bool valid = gs < a.n_slots;
+    const int32_t NS = a.W / a.M;
+    const int64_t eg = valid ? gs / NS : 0;             // (group, event) row
+    const int32_t j = valid ? (int32_t)(gs % NS) : 0;
+    if (unit * 16 >= a.n_slots) return;                 // whole wave idle (wave-uniform)
+    // per-wave LDS stash: the slot's position-2 features and their W1 projection (16 KB per wave)
+    __shared__ floatx4 stash[4][2][8][64];
+    floatx4(&sF2)[8][64] = stash[threadIdx.x >> 6][0];
+    floatx4(&sWp)[8][64] = stash[threadIdx.x >> 6][1];
+    floatx4 Q0[8];                                      // W2(position 0), carried to the position-1 pass
+    const int n_pass = 1 + 2 * a.M;
+    // pass 0: position 2 once per slot (walk j*M carries it); then per walk m: position 0, position 1
+#pragma nounroll
+    for (int pass = 0; pass < n_pass; ++pass) {
+        const int m = pass == 0 ? 0 : (pass - 1) >> 1;
+        const int p = pass == 0 ? 2 : ((pass - 1) & 1);
+        const int64_t gw = eg * a.W + (int64_t)j * a.M + m;
+        floatx4 F[8];
+        encode_position<NQE, NTD>(a, gw, valid, p, F);
+        floatx4 Y[8];
+        rgemm<8, 8>(p == 2 ? P.w1 : P.w2, F, Y);
+        const float *bb = p == 2 ? P.w1.b : P.w2.b;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const float4 b = bias4(bb, t);
+            Y[t] = floatx4{Y[t][0] + b.x, Y[t][1] + b.y, Y[t][2] + b.z, Y[t][3] + b.w};
+        }
+        if (p == 2) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                sF2[t][lane] = F[t];
+                sWp[t][lane] = Y[t];
+            }
+        } else if (p == 0) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) Q0[t] = Y[t];
+        } else {
+            walk_head(a, gw, eg, valid, sF2, sWp, Q0, Y);
+        }
+    }
+}
+
 // ------------------------------------------------------------------ per-edge dependency gate table
 // The dependency gate (:367-386) is a function of (E[e], t) only, and every record of an edge id
 // carries the edge's single timestamp, so gf(e) = 0.5 + 0.5*sigmoid(depMLP([E[e] | cos(t_e*w+phi)]))
@@ -736,11 +1033,17 @@ static size_t gcn_lds(const EncW &P) {
 }
 static size_t head_lds() { return sizeof(float) * (4 * TILE_ROWS * (2 * HID + 8)); }
 
+template <int NQE>
+static void launch_walk(const WalkArgs &a, unsigned blocks, hipStream_t s) {
+    walk_kernel<NQE, 11><<<dim3(blocks), 256, 0, s>>>(a);
+}
+
 extern "C" int tm_encoder_fwd(const tm_weights *w, const float *n_feat, const float *e_feat, int32_t n_groups,
-                              int32_t B, int32_t W, const int32_t *node6, const int32_t *eid3, const float *ts3,
-                              const int32_t *cat, const double *cut, const float *cnt, void *workspace,
-                              float *out_imp, void *stream) {
-    if (!w || n_groups < 0 || B < 0 || W < 0) return fail(TM_E_ARG, "tm_encoder_fwd: bad arguments");
+                              int32_t B, int32_t W, int32_t M, const int32_t *node6, const int32_t *eid3,
+                              const float *ts3, const int32_t *cat, const double *cut, const float *cnt,
+                              void *workspace, float *out_imp, void *stream) {
+    if (!w || n_groups < 0 || B < 0 || W < 0 || M <= 0) return fail(TM_E_ARG, "tm_encoder_fwd: bad arguments");
+    if (W % M) return fail(TM_E_SHAPE, "tm_encoder_fwd: W must be a multiple of M (walks per hop-1 slot)");
     const int64_t n_walks = (int64_t)n_groups * B * W;
     if (n_walks == 0) return TM_OK;
     if (!n_feat || !e_feat || !node6 || !eid3 || !ts3 || !cat || !cut || !cnt || !workspace || !out_imp)
@@ -755,6 +1058,22 @@ extern "C" int tm_encoder_fwd(const tm_weights *w, const float *n_feat, const fl
     std_kernel<<<dim3(n_groups), 256, 0, s>>>(B, W, cut, ts3, stdv);
     TM_CHECK_LAUNCH();
     prof_end("std_kernel", s, pe);
+    const int nqe = r16(P.kev) / 16, ntd = r16(P.dn) / 16;
+    if (ntd == 11 && nqe >= 11 && nqe <= 14) {
+        // fused register-resident path
+        const int64_t n_slots = n_walks / M;
+        const int64_t units = (n_slots + 15) / 16;
+        WalkArgs a{P, n_slots, W, M, B * W, n_feat, e_feat, node6, eid3, cat, ts3, cnt, stdv, cut, out_imp};
+        const unsigned blocks = (unsigned)((units + 3) / 4);
+        pe = prof_begin(s);
+        if (nqe == 11) launch_walk<11>(a, blocks, s);
+        else if (nqe == 12) launch_walk<12>(a, blocks, s);
+        else if (nqe == 13) launch_walk<13>(a, blocks, s);
+        else launch_walk<14>(a, blocks, s);
+        TM_CHECK_LAUNCH();
+        prof_end("walk_kernel", s, pe);
+        return TM_OK;
+    }
     const int64_t n_rows = n_walks * 3;
     pe = prof_begin(s);
     gcn_kernel<<<dim3((unsigned)((n_rows + TILE_ROWS - 1) / TILE_ROWS)), 256, lds_g, s>>>(

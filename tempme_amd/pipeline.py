@@ -52,7 +52,8 @@ class ExplainPipeline:
         G = 3 * (E // B)
         b = self.buf
         cut = ts.repeat(3).contiguous()
-        self.ex.encoder_fwd(b.node6, b.eid3, b.ts3, b.cat, cut, b.cnt, G, B, W, out=self.imp, workspace=self.ws)
+        self.ex.encoder_fwd(b.node6, b.eid3, b.ts3, b.cat, cut, b.cnt, G, B, W, out=self.imp, workspace=self.ws,
+                            M=self.M)
         return self.imp
 
     def explain(self):
