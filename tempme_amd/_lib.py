@@ -15,7 +15,8 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libtempme_hip.so")
+# TEMPME_LIB: an alternative in-tree build of the same library (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("TEMPME_LIB") or os.path.join(_HERE, "lib", "libtempme_hip.so")
 
 TM_OK = 0
 TM_E_EDGE_NOT_IN_LIST = -1

@@ -459,7 +459,7 @@ __global__ void __launch_bounds__(256) explain_kernel(EncW P, int32_t W, int32_t
 // out[t] = W tile t * x  over the flattened (t, q) sequence, weights prefetched PF steps ahead in
 // a rotating register buffer; sched_barrier pins each step so the loads stay PF steps ahead instead
 // of being hoisted (which would need NTO*NQ registers).
-constexpr int PF = 6;
+constexpr int PF = 3;
 
 #define TM_W_ADDR(i) ((((i) / NQ) * nq + ((i) % NQ)) * 64)
 
@@ -474,7 +474,7 @@ __device__ __forceinline__ int lane_id() {
 template <int NTO, int NQ>
 __device__ __forceinline__ void rgemm(const Lin &L, const floatx4 (&x)[NQ], floatx4 (&o)[NTO]) {
     const float4 *wp = L.w + lane_id();
-    const int nq = L.nq;
+    constexpr int nq = NQ;   // == L.nq: fragment offsets are immediates
     constexpr int N = NTO * NQ, D = PF < N ? PF : N;
 #pragma unroll
     for (int t = 0; t < NTO; ++t) o[t] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -499,7 +499,7 @@ template <int NTO, int NQ>
 __device__ __forceinline__ void rgemm2(const Lin &L, const floatx4 (&x)[NQ], const floatx4 (&y)[NQ],
                                        floatx4 (&o)[NTO], floatx4 (&p)[NTO]) {
     const float4 *wp = L.w + lane_id();
-    const int nq = L.nq;
+    constexpr int nq = NQ;
     constexpr int N = NTO * NQ, D = PF < N ? PF : N;
 #pragma unroll
     for (int t = 0; t < NTO; ++t) {
@@ -526,8 +526,51 @@ __device__ __forceinline__ void rgemm2(const Lin &L, const floatx4 (&x)[NQ], con
     }
 }
 
-__device__ __forceinline__ float4 bias4(const float *b, int t) {
-    return *reinterpret_cast<const float4 *>(b + 16 * t + 4 * (lane_id() >> 4));
+// Per-workgroup LDS table of the small per-feature vectors the walk kernel reads in its epilogues:
+// every bias (zero padded to its tiles), the last MLP row, and the time encoder's frequency and phase
+// laid out on the event-feature axis k (zero outside the time block), so the per-lane reads in the
+// feature generation and the epilogues are ds_reads (broadcast within a lane group), not L2 loads
+// whose latency a dependent epilogue would wait for in every layer.
+template <int NQE, int NTD>
+struct WalkConsts {
+    static constexpr int XW = 0, XP = XW + 16 * NQE, EV = XP + 16 * NQE, G1 = EV + 16 * NTD, G2 = G1 + HID,
+                         W1 = G2 + HID, W2 = W1 + 2 * HID, A1 = W2 + 2 * HID, A2 = A1 + HID, M1 = A2 + HID,
+                         M2 = M1 + 80, M3 = M2 + HID, SIZE = M3 + HID;
+};
+
+template <int NQE, int NTD>
+__device__ __forceinline__ void load_consts(const EncW &P, float *cs) {
+    using C = WalkConsts<NQE, NTD>;
+    for (int i = threadIdx.x; i < C::SIZE; i += blockDim.x) {
+        float v;
+        if (i < C::EV) {
+            const int k = i < C::XP ? i : i - C::XP, ti = k - P.de - 3;
+            v = (ti >= 0 && ti < P.dn) ? (i < C::XP ? P.freq[ti] : P.phase[ti]) : 0.f;
+        } else if (i < C::G1) v = P.ev.b[i - C::EV];
+        else if (i < C::G2) v = P.g1.b[i - C::G1];
+        else if (i < C::W1) v = P.g2.b[i - C::G2];
+        else if (i < C::W2) v = P.w1.b[i - C::W1];
+        else if (i < C::A1) v = P.w2.b[i - C::W2];
+        else if (i < C::A2) v = P.a1.b[i - C::A1];
+        else if (i < C::M1) v = P.a2.b[i - C::A2];
+        else if (i < C::M2) v = P.m1.b[i - C::M1];
+        else if (i < C::M3) v = P.m2.b[i - C::M2];
+        else v = P.m3w[i - C::M3];
+        cs[i] = v;
+    }
+}
+
+// this lane's 4 entries of tile t of an LDS vector
+__device__ __forceinline__ float4 lds4(const float *v, int t) {
+    return *reinterpret_cast<const float4 *>(v + 16 * t + 4 * ((threadIdx.x & 63) >> 4));
+}
+
+__device__ __forceinline__ floatx4 add4(const floatx4 &a, const float4 &b) {
+    return floatx4{a[0] + b.x, a[1] + b.y, a[2] + b.z, a[3] + b.w};
+}
+
+__device__ __forceinline__ floatx4 relu_add4(const floatx4 &a, const float4 &b) {
+    return floatx4{relu(a[0] + b.x), relu(a[1] + b.y), relu(a[2] + b.z), relu(a[3] + b.w)};
 }
 
 struct WalkArgs {
@@ -541,9 +584,54 @@ struct WalkArgs {
     float *out;
 };
 
-// one walk position for the 16 columns of this wave -> F = [U_s | U_t] (8 tiles, B layout)
+// Phase timing (debug builds only, -DTM_STAMPS; tools_stamps.py): s_memtime deltas of lane 0 per
+// pass type accumulated for workgroups 512..1023 (past the first dispatch round).
+#ifdef TM_STAMPS
+__device__ unsigned long long g_st[3][10];
+#define TM_STAMP(k)                                 \
+    do {                                            \
+        __builtin_amdgcn_sched_barrier(0);          \
+        T[k] = __builtin_amdgcn_s_memtime();        \
+        __builtin_amdgcn_sched_barrier(0);          \
+    } while (0)
+#else
+#define TM_STAMP(k) (void)T
+#endif
+
+constexpr int EQ_MAX = 4;   // edge features span at most 4 K steps (de <= 64, checked on the host)
+
+// K step q of the event features x[k] = [E(e) | cnt | cos(dt * w + phi)] (:176-179, TimeEncode :45-59)
 template <int NQE, int NTD>
-__device__ __forceinline__ void encode_position(const WalkArgs &a, int64_t gw, bool valid, int p, floatx4 (&F)[8]) {
+__device__ __forceinline__ floatx4 gen_x(int q, const float *cs, const float (&ef)[EQ_MAX][4], int g, int de, int kev,
+                                         float dt, float c0, float c1, float c2) {
+    using C = WalkConsts<NQE, NTD>;
+    floatx4 xq;
+    const float4 w4 = lds4(cs + C::XW, q), p4 = lds4(cs + C::XP, q);
+    const float wv[4] = {w4.x, w4.y, w4.z, w4.w}, pv[4] = {p4.x, p4.y, p4.z, p4.w};
+    const int qe = q < EQ_MAX ? q : 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int k = 16 * q + 4 * g + s;
+        float v;
+        if (16 * q + 16 <= de) v = ef[qe][s];
+        else {
+            v = (k < kev) ? time_cos(dt, wv[s], pv[s]) : 0.f;
+            if (k < de + 3) v = (k == de) ? c0 : (k == de + 1) ? c1 : c2;
+            if (k < de) v = ef[qe][s];
+        }
+        xq[s] = v;
+    }
+    return xq;
+}
+
+// one walk position for the 16 columns of this wave -> F = [U_s | U_t] (8 tiles, B layout).
+// lin_event runs K-outer ((q, t) fragment order): the event features of K step q+1 are generated
+// while step q's MFMAs run, only L and two x fragments are live, and the node-feature rows of tile q
+// (float4 gathers, dn % 4 == 0) are issued during step q so they have landed when the GEMM ends.
+template <int NQE, int NTD>
+__device__ __forceinline__ void encode_position(const WalkArgs &a, const float *cs, int64_t gw, bool valid, int p,
+                                                floatx4 (&F)[8], unsigned long long (&T)[10]) {
+    using C = WalkConsts<NQE, NTD>;
     const EncW &P = a.P;
     const int g = lane_id() >> 4;
     const int de = P.de, dn = P.dn, kev = P.kev;
@@ -558,56 +646,89 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, int64_t gw, b
         c1 = a.cnt[gw * 9 + p * 3 + 1];
         c2 = a.cnt[gw * 9 + p * 3 + 2];
     }
-    // event features [E(e) | cnt | cos(dt * w + phi)] in B layout, 4 per lane per K step
-    floatx4 x[NQE];
+    // edge-feature part of x: unconditional (clamped) loads, all in flight together
+    float ef[EQ_MAX][4];
+    const float *erow = a.e_feat + (int64_t)e * de;
 #pragma unroll
-    for (int q = 0; q < NQE; ++q) {
+    for (int q = 0; q < EQ_MAX; ++q)
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const int k = 16 * q + 4 * g + s;
-            float v = 0.f;
-            if (k < de) v = a.e_feat[(int64_t)e * de + k];
-            else if (k < de + 3) v = (k == de) ? c0 : (k == de + 1) ? c1 : c2;
-            else if (k < kev) v = time_cos(dt, P.freq[k - de - 3], P.phase[k - de - 3]);
-            x[q][s] = v;
+            ef[q][s] = (16 * q < de) ? erow[k < de ? k : de - 1] : 0.f;
+        }
+    const float4 *nrow_s = reinterpret_cast<const float4 *>(a.n_feat + (int64_t)ns * dn);
+    const float4 *nrow_t = reinterpret_cast<const float4 *>(a.n_feat + (int64_t)nt * dn);
+    float4 xs[NTD], xt[NTD];
+    floatx4 L[NTD];
+#pragma unroll
+    for (int t = 0; t < NTD; ++t) L[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    TM_STAMP(1);
+    {
+        const float4 *wp = P.ev.w + lane_id();
+        constexpr int nq = NQE;
+        constexpr int N = NTD * NQE, D = PF;
+        float4 buf[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i) buf[i] = wp[((i % NTD) * nq + i / NTD) * 64];
+        floatx4 xq = gen_x<NQE, NTD>(0, cs, ef, g, de, kev, dt, c0, c1, c2);
+#pragma unroll
+        for (int q = 0; q < NQE; ++q) {
+            if (false) {
+                const int f4 = 4 * q + g < dn / 4 ? 4 * q + g : dn / 4 - 1;   // clamped; masked below
+                xs[q] = nrow_s[f4];
+                xt[q] = nrow_t[f4];
+            }
+            floatx4 xn = xq;
+            if (q + 1 < NQE) xn = gen_x<NQE, NTD>(q + 1, cs, ef, g, de, kev, dt, c0, c1, c2);
+#pragma unroll
+            for (int t = 0; t < NTD; ++t) {
+                const int i = q * NTD + t;
+                const float4 w = buf[i % D];
+                if (i + D < N) buf[i % D] = wp[(((i + D) % NTD) * nq + (i + D) / NTD) * 64];
+                L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, xq.x, L[t], 0, 0, 0);
+                L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, xq.y, L[t], 0, 0, 0);
+                L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, xq.z, L[t], 0, 0, 0);
+                L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, xq.w, L[t], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            xq = xn;
         }
     }
-    floatx4 L[NTD];
-    rgemm<NTD, NQE>(P.ev, x, L);
+    TM_STAMP(2);
     // A = x_s + relu(x_t + L), B = x_t + relu(x_s + L)   (event_gcn :93-96, lin_event shared)
     floatx4 A[NTD], Bv[NTD];
 #pragma unroll
     for (int t = 0; t < NTD; ++t) {
-        const float4 b = bias4(P.ev.b, t);
+        const float4 b = lds4(cs + C::EV, t);
+        const float bv[4] = {b.x, b.y, b.z, b.w};
+        { const int f4 = 4 * t + g < dn / 4 ? 4 * t + g : dn / 4 - 1; xs[t] = nrow_s[f4]; xt[t] = nrow_t[f4]; }
+        const float sv[4] = {xs[t].x, xs[t].y, xs[t].z, xs[t].w}, tv[4] = {xt[t].x, xt[t].y, xt[t].z, xt[t].w};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int f = 16 * t + 4 * g + r;
-            float av = 0.f, bvv = 0.f;
-            if (f < dn) {
-                const float l = L[t][r] + (r == 0 ? b.x : r == 1 ? b.y : r == 2 ? b.z : b.w);
-                const float xs = a.n_feat[(int64_t)ns * dn + f], xt = a.n_feat[(int64_t)nt * dn + f];
-                av = xs + relu(xt + l);
-                bvv = xt + relu(xs + l);
-            }
-            A[t][r] = av;
-            Bv[t][r] = bvv;
+            const bool in = 16 * t + 4 * g + r < dn;
+            const float l = L[t][r] + bv[r];
+            A[t][r] = in ? sv[r] + relu(tv[r] + l) : 0.f;
+            Bv[t][r] = in ? tv[r] + relu(sv[r] + l) : 0.f;
         }
     }
     floatx4 Hs[4], Ht[4];
+    TM_STAMP(3);
     rgemm2<4, NTD>(P.g1, A, Bv, Hs, Ht);
+    TM_STAMP(4);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        const float4 b = bias4(P.g1.b, t);
-        Hs[t] = floatx4{relu(Hs[t][0] + b.x), relu(Hs[t][1] + b.y), relu(Hs[t][2] + b.z), relu(Hs[t][3] + b.w)};
-        Ht[t] = floatx4{relu(Ht[t][0] + b.x), relu(Ht[t][1] + b.y), relu(Ht[t][2] + b.z), relu(Ht[t][3] + b.w)};
+        const float4 b = lds4(cs + C::G1, t);
+        Hs[t] = relu_add4(Hs[t], b);
+        Ht[t] = relu_add4(Ht[t], b);
     }
     floatx4 Us[4], Ut[4];
     rgemm2<4, 4>(P.g2, Hs, Ht, Us, Ut);
+    TM_STAMP(5);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        const float4 b = bias4(P.g2.b, t);
-        F[t] = floatx4{Us[t][0] + b.x, Us[t][1] + b.y, Us[t][2] + b.z, Us[t][3] + b.w};
-        F[4 + t] = floatx4{Ut[t][0] + b.x, Ut[t][1] + b.y, Ut[t][2] + b.z, Ut[t][3] + b.w};
+        const float4 b = lds4(cs + C::G2, t);
+        F[t] = add4(Us[t], b);
+        F[4 + t] = add4(Ut[t], b);
     }
 }
 
@@ -618,10 +739,18 @@ __device__ __forceinline__ float col_sum(float v) {
     return v;
 }
 
+// per-walk scalars of the head, loaded at the start of the position-1 pass
+struct HeadIn {
+    float cu, sd, t0, t1;
+    int32_t c;
+};
+
 // attention head + final MLP for the 16 walks of this wave (Q1 in registers, F2/Wp/Q0 in the stash)
-__device__ __forceinline__ void walk_head(const WalkArgs &a, int64_t gw, int64_t eg, bool valid,
+template <int NQE, int NTD>
+__device__ __forceinline__ void walk_head(const WalkArgs &a, const float *cs, int64_t gw, bool valid, const HeadIn &hi,
                                           const floatx4 (&sF2)[8][64], const floatx4 (&sWp)[8][64],
                                           const floatx4 (&Q0)[8], const floatx4 (&Q1)[8]) {
+    using C = WalkConsts<NQE, NTD>;
     const EncW &P = a.P;
     const int lane = threadIdx.x & 63, g = lane_id() >> 4;
     float s0 = 0.f, s1 = 0.f;
@@ -637,13 +766,9 @@ __device__ __forceinline__ void walk_head(const WalkArgs &a, int64_t gw, int64_t
     s0 = col_sum(s0);
     s1 = col_sum(s1);
     float tw0 = 0.f, tw1 = 0.f;
-    int32_t c = -1;
     if (valid) {
-        const float cu = (float)a.cut[eg];
-        const float sd = a.stdv[gw / a.BW] + 1e-6f;
-        tw0 = expf(-fabsf(cu - a.ts3[gw * 3 + 0]) / sd);
-        tw1 = expf(-fabsf(cu - a.ts3[gw * 3 + 1]) / sd);
-        c = a.cat[gw];
+        tw0 = expf(-fabsf(hi.cu - hi.t0) / hi.sd);
+        tw1 = expf(-fabsf(hi.cu - hi.t1) / hi.sd);
     }
     // scores * (1.0 - 0.3 + 0.3 * time_weight) (:835-836), softmax over the 2 targets
     s0 *= __fadd_rn(0.7f, __fmul_rn(0.3f, tw0));
@@ -660,46 +785,38 @@ __device__ __forceinline__ void walk_head(const WalkArgs &a, int64_t gw, int64_t
     floatx4 H1[4];
     rgemm<4, 8>(P.a1, O, H1);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        const float4 b = bias4(P.a1.b, t);
-        H1[t] = floatx4{relu(H1[t][0] + b.x), relu(H1[t][1] + b.y), relu(H1[t][2] + b.z), relu(H1[t][3] + b.w)};
-    }
+    for (int t = 0; t < 4; ++t) H1[t] = relu_add4(H1[t], lds4(cs + C::A1, t));
     floatx4 X5[5];
     {
         floatx4 H2[4];
         rgemm<4, 4>(P.a2, H1, H2);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const float4 b = bias4(P.a2.b, t);
-            X5[t] = floatx4{H2[t][0] + b.x, H2[t][1] + b.y, H2[t][2] + b.z, H2[t][3] + b.w};
-        }
+        for (int t = 0; t < 4; ++t) X5[t] = add4(H2[t], lds4(cs + C::A2, t));
         // one-hot category in features 64..75 (compute_catogory_feautres :308-315)
+        const int32_t c = valid ? hi.c : -1;
 #pragma unroll
         for (int r = 0; r < 4; ++r) X5[4][r] = (c == 4 * g + r) ? 1.f : 0.f;
     }
     floatx4 M1[5];
     rgemm<5, 5>(P.m1, X5, M1);
 #pragma unroll
-    for (int t = 0; t < 5; ++t) {
-        const float4 b = bias4(P.m1.b, t);
-        M1[t] = floatx4{relu(M1[t][0] + b.x), relu(M1[t][1] + b.y), relu(M1[t][2] + b.z), relu(M1[t][3] + b.w)};
-    }
+    for (int t = 0; t < 5; ++t) M1[t] = relu_add4(M1[t], lds4(cs + C::M1, t));
     floatx4 M2[4];
     rgemm<4, 5>(P.m2, M1, M2);
     float z = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        const float4 b = bias4(P.m2.b, t);
-        const float4 w3 = *reinterpret_cast<const float4 *>(P.m3w + 16 * t + 4 * g);
-        z += relu(M2[t][0] + b.x) * w3.x + relu(M2[t][1] + b.y) * w3.y + relu(M2[t][2] + b.z) * w3.z +
-             relu(M2[t][3] + b.w) * w3.w;
+        const floatx4 h = relu_add4(M2[t], lds4(cs + C::M2, t));
+        const float4 w3 = lds4(cs + C::M3, t);
+        z += h[0] * w3.x + h[1] * w3.y + h[2] * w3.z + h[3] * w3.w;
     }
     z = col_sum(z) + P.m3b[0];
     if (valid && g == 0) a.out[gw] = 1.f / (1.f + expf(-z));
 }
 
 template <int NQE, int NTD>
-__global__ void __launch_bounds__(256) walk_kernel(WalkArgs a) {
+__global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
+    using C = WalkConsts<NQE, NTD>;
     const EncW &P = a.P;
     const int lane = threadIdx.x & 63, col = lane & 15;
     const int64_t unit = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -708,9 +825,14 @@ __global__ void __launch_bounds__(256) walk_kernel(WalkArgs a) {
     const int32_t NS = a.W / a.M;
     const int64_t eg = valid ? gs / NS : 0;             // (group, event) row
     const int32_t j = valid ? (int32_t)(gs % NS) : 0;
-    if (unit * 16 >= a.n_slots) return;                 // whole wave idle (wave-uniform)
-    // per-wave LDS stash: the slot's position-2 features and their W1 projection (16 KB per wave)
+    // LDS: per-wave stash of the slot's position-2 features and their W1 projection (16 KB per wave),
+    // then the constant table
     __shared__ floatx4 stash[4][2][8][64];
+    __shared__ float4 cs4[(C::SIZE + 3) / 4];
+    float *cs = reinterpret_cast<float *>(cs4);
+    load_consts<NQE, NTD>(P, cs);
+    __syncthreads();
+    if (unit * 16 >= a.n_slots) return;                 // whole wave idle (wave-uniform)
     floatx4(&sF2)[8][64] = stash[threadIdx.x >> 6][0];
     floatx4(&sWp)[8][64] = stash[threadIdx.x >> 6][1];
     floatx4 Q0[8];                                      // W2(position 0), carried to the position-1 pass
@@ -721,16 +843,25 @@ __global__ void __launch_bounds__(256) walk_kernel(WalkArgs a) {
         const int m = pass == 0 ? 0 : (pass - 1) >> 1;
         const int p = pass == 0 ? 2 : ((pass - 1) & 1);
         const int64_t gw = eg * a.W + (int64_t)j * a.M + m;
-        floatx4 F[8];
-        encode_position<NQE, NTD>(a, gw, valid, p, F);
-        floatx4 Y[8];
-        rgemm<8, 8>(p == 2 ? P.w1 : P.w2, F, Y);
-        const float *bb = p == 2 ? P.w1.b : P.w2.b;
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            const float4 b = bias4(bb, t);
-            Y[t] = floatx4{Y[t][0] + b.x, Y[t][1] + b.y, Y[t][2] + b.z, Y[t][3] + b.w};
+        HeadIn hi{0.f, 1.f, 0.f, 0.f, -1};
+        if (p == 1 && valid) {                           // issued early, consumed by the head
+            hi.cu = (float)a.cut[eg];
+            hi.sd = a.stdv[gw / a.BW] + 1e-6f;
+            hi.t0 = a.ts3[gw * 3 + 0];
+            hi.t1 = a.ts3[gw * 3 + 1];
+            hi.c = a.cat[gw];
         }
+        floatx4 F[8];
+        unsigned long long T[10];
+        TM_STAMP(0);
+        encode_position<NQE, NTD>(a, cs, gw, valid, p, F, T);
+        floatx4 Y[8];
+        TM_STAMP(6);
+        rgemm<8, 8>(p == 2 ? P.w1 : P.w2, F, Y);
+        TM_STAMP(7);
+        const float *bb = cs + (p == 2 ? C::W1 : C::W2);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) Y[t] = add4(Y[t], lds4(bb, t));
         if (p == 2) {
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
@@ -741,8 +872,15 @@ __global__ void __launch_bounds__(256) walk_kernel(WalkArgs a) {
 #pragma unroll
             for (int t = 0; t < 8; ++t) Q0[t] = Y[t];
         } else {
-            walk_head(a, gw, eg, valid, sF2, sWp, Q0, Y);
+            walk_head<NQE, NTD>(a, cs, gw, valid, hi, sF2, sWp, Q0, Y);
         }
+        TM_STAMP(8);
+#ifdef TM_STAMPS
+        if (lane == 0 && blockIdx.x >= 512 && blockIdx.x < 1024) {
+            for (int k = 0; k < 8; ++k) atomicAdd(&g_st[p][k], T[k + 1] - T[k]);
+            atomicAdd(&g_st[p][8], 1ull);
+        }
+#endif
     }
 }
 
@@ -1059,7 +1197,7 @@ extern "C" int tm_encoder_fwd(const tm_weights *w, const float *n_feat, const fl
     TM_CHECK_LAUNCH();
     prof_end("std_kernel", s, pe);
     const int nqe = r16(P.kev) / 16, ntd = r16(P.dn) / 16;
-    if (ntd == 11 && nqe >= 11 && nqe <= 14) {
+    if (ntd == 11 && nqe >= 11 && nqe <= 14 && P.de <= 16 * EQ_MAX && P.dn % 4 == 0) {
         // fused register-resident path
         const int64_t n_slots = n_walks / M;
         const int64_t units = (n_slots + 15) / 16;
@@ -1111,3 +1249,10 @@ extern "C" int tm_edge_importance(const tm_weights *w, const float *e_feat, int3
     prof_end("explain_kernel", S_(stream), pe);
     return TM_OK;
 }
+
+#ifdef TM_STAMPS
+extern "C" int tm_debug_stamps(unsigned long long *host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(tmk::g_st), sizeof(unsigned long long) * 30, 0,
+                                    hipMemcpyDeviceToHost);
+}
+#endif

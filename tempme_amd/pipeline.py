@@ -82,4 +82,5 @@ class ExplainPipeline:
             self.h2[:3 * E * N * N].view(3, E, N * N)
 
     def check_errors(self):
-        L.raise_device_error(int(self.buf.err.item()), "ExplainPipeline")
+        if getattr(self, "buf", None) is not None:   # nothing sampled yet: nothing to report
+            L.raise_device_error(int(self.buf.err.item()), "ExplainPipeline")

@@ -21,6 +21,35 @@ for s in "$@"; do
         bench) step bench 600 python bench.py --steps 10 --warmup 2 ;;
         benchq) step bench 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
         prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+        pmc)
+            B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline"
+            i=0
+            for ctr in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
+                       "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU" \
+                       "TCC_HIT_sum TCC_MISS_sum" "FETCH_SIZE" "WRITE_SIZE" \
+                       "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_SALU"; do
+                i=$((i+1))
+                step pmc$i 400 rocprofv3 --kernel-trace --pmc $ctr -d gpurun_out/pmc$i -o run --output-format csv -- $B
+            done ;;
+        ablate)
+            for ab in 0 1 2 4 7 0; do
+                TEMPME_ABLATE=$ab step ablate$ab 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline
+                grep -o '"walk_kernel": {"avg_ms": [0-9.]*' gpurun_out/ablate$ab.log
+            done ;;
+        ab)  # interleaved A/B timing of every tempme_amd/lib/ab/*.so variant (two rounds)
+            for r in 1 2; do
+                for so in tempme_amd/lib/ab/*.so; do
+                    n=$(basename "$so" .so)
+                    TEMPME_LIB="$PWD/$so" step ab_${n}_$r 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline
+                    echo "$n round $r: $(grep -o '"walk_kernel": {"avg_ms": [0-9.]*' gpurun_out/ab_${n}_$r.log)" | tee -a gpurun_out/ab.txt
+                done
+            done ;;
+        stamps)  # phase stamps of every -DTM_STAMPS build in tempme_amd/lib/ab/
+            for so in tempme_amd/lib/ab/*.so; do
+                n=$(basename "$so" .so)
+                TEMPME_LIB="$PWD/$so" step stamps_$n 300 python tools_stamps.py
+                { echo "== $n: $(grep -o '"walk_kernel": {"avg_ms": [0-9.]*' gpurun_out/stamps_$n.log)"; grep -E "^(slot|walk) " gpurun_out/stamps_$n.log; } | tee -a gpurun_out/stamps.txt
+            done ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done
