@@ -7,7 +7,7 @@ import json
 import sys
 from collections import defaultdict
 
-root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
+root = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else "gpurun_out"
 acc = defaultdict(lambda: defaultdict(list))
 for f in sorted(glob.glob(f"{root}/pmc*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
@@ -26,3 +26,15 @@ for k, d in acc.items():
     if "FETCH_SIZE" in x:
         x["hbm_read_bytes_x2"] = x["FETCH_SIZE"] * 1024 * 2
 print(json.dumps(out, indent=1))
+# --traffic FILE: per-launch HBM bytes (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM) keyed by
+# the kernel names bench.py reports, read by bench.py for roofline.traffic
+if "--traffic" in sys.argv:
+    dest = sys.argv[sys.argv.index("--traffic") + 1]
+    tr = {}
+    for k, x in out.items():
+        if "FETCH_SIZE" in x and "WRITE_SIZE" in x:
+            short = k.replace("tmk::", "").split("<")[0]
+            tr[short] = int(round(x["FETCH_SIZE"] * 1024 * 2 + x["WRITE_SIZE"] * 1024))
+    with open(dest, "w") as fh:
+        json.dump(tr, fh, indent=1)
+    print("wrote", dest, tr)
