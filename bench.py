@@ -116,6 +116,7 @@ def main():
     import tempme_amd as tm
     from tempme_amd import _lib as L
     from tempme_amd.pipeline import ExplainPipeline
+    from tempme_amd.sharding import max_over_ranks, shard_events
     from tempme_amd.workload import enron_like, split
 
     N, M, B = args.n_degree, 3, args.batch_size
@@ -138,12 +139,12 @@ def main():
 
     # inputs for every step resident in HBM before timing: events cycle through the test split
     n_steps = args.warmup + args.steps
-    n_test = len(src)
-    gidx = [((np.arange(E) + (k * world + rank) * E) % n_test) for k in range(n_steps)]
     to = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)  # noqa: E731
-    inputs = [(to(src[i], np.int32), to(dst[i], np.int32), to(ts[i], np.float64), to(eidx[i], np.int32),
-               to((np.arange(E, dtype=np.int64) + (k * world + rank) * E).astype(np.uint32).view(np.int32), np.int32))
-              for k, i in enumerate(gidx)]
+    inputs = []
+    for k in range(n_steps):
+        i, ev = shard_events(k, rank, world, E, len(src))
+        inputs.append((to(src[i], np.int32), to(dst[i], np.int32), to(ts[i], np.float64), to(eidx[i], np.int32),
+                       to(ev.view(np.int32), np.int32)))
 
     for k in range(args.warmup):
         pipe.run(*inputs[k])
@@ -164,10 +165,7 @@ def main():
     prof = L.profile_read()
     L.profile_enable(False)
     pipe.check_errors()
-    if dist:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = max_over_ranks(el, dist, dev)
 
     if rank == 0:
         fm = flops_model(g["e_feat"].shape[1], g["n_feat"].shape[1], 64, N, M)

@@ -1,0 +1,114 @@
+"""N>1 path on CPU (gloo, world_size 2): event sharding, keyed-RNG shard independence, max-over-ranks.
+
+The GPU path shards exactly like this (bench.py --gpus N); here the per-rank work is the oracle's
+event pipeline (test infrastructure), which follows the same RNG contract as the HIP kernels."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tempme_amd.sharding import max_over_ranks, shard_events
+
+
+def test_shards_disjoint_and_contiguous():
+    for world in (1, 2, 4, 8):
+        per, n = 7, 23
+        for step in range(3):
+            ids = np.concatenate([shard_events(step, r, world, per, n)[1] for r in range(world)]).astype(np.int64)
+            first = step * world * per
+            assert np.array_equal(ids, np.arange(first, first + world * per))
+            rows = np.concatenate([shard_events(step, r, world, per, n)[0] for r in range(world)])
+            assert np.array_equal(rows, ids % n)
+
+
+def test_shard_events_rejects_bad_args():
+    with pytest.raises(ValueError):
+        shard_events(0, 2, 2, 4, 10)
+    with pytest.raises(ValueError):
+        shard_events(0, 0, 1, 4, 0)
+
+
+def test_max_over_ranks_without_group():
+    assert max_over_ranks(3.5) == 3.5
+
+
+def _graph():
+    rng = np.random.default_rng(7)
+    V, E = 40, 600
+    src = rng.integers(1, V, E)
+    dst = rng.integers(1, V, E)
+    ts = np.sort(rng.integers(0, 400, E)).astype(np.float64)
+    eidx = np.arange(1, E + 1)
+    return V, src, dst, ts, eidx
+
+
+def _run_events(rows, ev, N=4, M=2):
+    from oracle import oracle as O
+    V, src, dst, ts, eidx = _graph()
+    cut = len(src) * 3 // 4
+    g = O.OracleGraph(src, dst, eidx, ts, V)   # events' own edges are in the graph (temp_exp_main.py)
+    test = slice(cut, None)
+    s, d, t, e = src[test][rows], dst[test][rows], ts[test][rows], eidx[test][rows]
+    o = O.event_pipeline(g, 11, 1, N, M, s, d, t, e, ev, np.unique(dst), n_threads=1)
+    return {k: v for k, v in o.items() if k != "hist"}
+
+
+def _worker(rank, world, port, per, steps, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _work(rank, world, per, steps, q)
+    except Exception as exc:  # surface the failure instead of a queue timeout
+        q.put(repr(exc))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _work(rank, world, per, steps, q):
+    n_test = len(_graph()[1]) - len(_graph()[1]) * 3 // 4
+    outs = []
+    for step in range(steps):
+        rows, ev = shard_events(step, rank, world, per, n_test)
+        outs.append(_run_events(rows, ev))
+    dist.barrier()
+    el = max_over_ranks(1.0 + rank, dist)          # per-rank "elapsed" -> max over ranks
+    gathered = [None] * world
+    dist.all_gather_object(gathered, outs)
+    if rank == 0:
+        q.put((el, gathered))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_gloo_two_ranks_match_single_process():
+    world, per, steps = 2, 6, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, per, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    assert not isinstance(res, str), res
+    el, gathered = res
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert el == 2.0
+    n_test = len(_graph()[1]) - len(_graph()[1]) * 3 // 4
+    for step in range(steps):
+        # one process over the step's whole block of events == the ranks' shards, concatenated
+        rows = np.arange(step * world * per, (step + 1) * world * per)
+        full = _run_events(rows % n_test, rows.astype(np.uint32))
+        for k, v in full.items():
+            got = np.concatenate([gathered[r][step][k] for r in range(world)])
+            assert np.array_equal(got, v), k
