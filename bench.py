@@ -42,8 +42,11 @@ def flops_model(de, dn, h, N, M):
     per_walk_head = 3 * (2 * h) ** 2 + (2 * h) * h + h * h + (h + 12) ** 2 + (h + 12) * h + h + 2 * 2 * h
     per_pos_gate = (de + dn) * h + h * (h // 2) + h // 2
     W = N * M
-    # walk_kernel executes position 2 once per hop-1 slot (shared by the M walks of the slot)
-    exec_walk = 2 * ((2 + 1.0 / M) * per_pos_gcn + per_walk_head - (1 - 1.0 / M) * (2 * h) ** 2)
+    # walk_kernel executes position 2 once per hop-1 slot (shared by the M walks of the slot), and
+    # there the all-time-feature K steps of lin_event (dt = 0: constant) are folded into a bias
+    qt = (de + 3 + 15) // 16
+    exec_walk = 2 * ((2 + 1.0 / M) * per_pos_gcn + per_walk_head - (1 - 1.0 / M) * (2 * h) ** 2
+                     - max(kev - 16 * qt, 0) * dn / M)
     return dict(gcn_kernel=2 * per_pos_gcn * 3, head_kernel=2 * per_walk_head, explain_kernel=2 * per_pos_gate * 3,
                 walk_kernel=2 * (3 * per_pos_gcn + per_walk_head), walk_kernel_executed=exec_walk,
                 gate_per_edge=2 * per_pos_gate,

@@ -38,6 +38,10 @@ struct EncW {
     int de, dn, kev, kdep;
     Lin ev, g1, g2, w1, w2, a1, a2, m1, m2, d1, d2;
     const float *m3w, *m3b, *d3w, *d3b, *freq, *phase;
+    // lin_event bias plus the K steps q >= qt (all time features) at dt = 0: walk position 2 is
+    // relative to itself, so those steps are the constant cos(phase) (walk_kernel's slot pass)
+    const float *evc;
+    int qt;
 };
 
 // ------------------------------------------------------------------ MFMA tile GEMM
@@ -556,7 +560,8 @@ __device__ __forceinline__ void rgemm2(const Lin &L, const floatx4 (&x)[NQ], con
 // whose latency a dependent epilogue would wait for in every layer.
 template <int NQE, int NTD>
 struct WalkConsts {
-    static constexpr int XW = 0, XP = XW + 16 * NQE, EV = XP + 16 * NQE, G1 = EV + 16 * NTD, G2 = G1 + HID,
+    static constexpr int XW = 0, XP = XW + 16 * NQE, EV = XP + 16 * NQE, EVC = EV + 16 * NTD, G1 = EVC + 16 * NTD,
+                         G2 = G1 + HID,
                          W1 = G2 + HID, W2 = W1 + 2 * HID, A1 = W2 + 2 * HID, A2 = A1 + HID, M1 = A2 + HID,
                          M2 = M1 + 80, M3 = M2 + HID, SIZE = M3 + HID;
 };
@@ -569,7 +574,8 @@ __device__ __forceinline__ void load_consts(const EncW &P, float *cs) {
         if (i < C::EV) {
             const int k = i < C::XP ? i : i - C::XP, ti = k - P.de - 3;
             v = (ti >= 0 && ti < P.dn) ? (i < C::XP ? P.freq[ti] : P.phase[ti]) : 0.f;
-        } else if (i < C::G1) v = P.ev.b[i - C::EV];
+        } else if (i < C::EVC) v = P.ev.b[i - C::EV];
+        else if (i < C::G1) v = P.evc[i - C::EVC];
         else if (i < C::G2) v = P.g1.b[i - C::G1];
         else if (i < C::W1) v = P.g2.b[i - C::G2];
         else if (i < C::W2) v = P.w1.b[i - C::W1];
@@ -649,8 +655,9 @@ __device__ __forceinline__ floatx4 gen_x(int q, const float *cs, const float (&e
 
 // one walk position for the 16 columns of this wave -> F = [U_s | U_t] (8 tiles, B layout).
 // lin_event runs K-outer ((q, t) fragment order): the event features of K step q+1 are generated
-// while step q's MFMAs run, only L and two x fragments are live, and the node-feature rows of tile q
-// (float4 gathers, dn % 4 == 0) are issued during step q so they have landed when the GEMM ends.
+// while step q's MFMAs run and only L and two x fragments are live.  Node-feature rows are float4
+// gathers (dn % 4 == 0) in the epilogue, unconditional with a clamped index (issuing them during the
+// GEMM keeps 88 more registers live and costs the second wave per SIMD).
 template <int NQE, int NTD>
 __device__ __forceinline__ void encode_position(const WalkArgs &a, const float *cs, int64_t gw, bool valid, int p,
                                                 floatx4 (&F)[8], unsigned long long (&T)[10]) {
@@ -694,27 +701,25 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, const float *
 #pragma unroll
         for (int i = 0; i < D; ++i) buf[i] = wp[((i % NTD) * nq + i / NTD) * 64];
         floatx4 xq = gen_x<NQE, NTD>(0, cs, ef, g, de, kev, dt, c0, c1, c2);
+        const int qend = p == 2 ? P.qt : NQE;            // slot pass: steps >= qt folded into evc
 #pragma unroll
         for (int q = 0; q < NQE; ++q) {
-            if (false) {
-                const int f4 = 4 * q + g < dn / 4 ? 4 * q + g : dn / 4 - 1;   // clamped; masked below
-                xs[q] = nrow_s[f4];
-                xt[q] = nrow_t[f4];
-            }
-            floatx4 xn = xq;
-            if (q + 1 < NQE) xn = gen_x<NQE, NTD>(q + 1, cs, ef, g, de, kev, dt, c0, c1, c2);
+            if (q < qend) {                               // wave-uniform (a break would stop the unrolling)
+                floatx4 xn = xq;
+                if (q + 1 < NQE) xn = gen_x<NQE, NTD>(q + 1, cs, ef, g, de, kev, dt, c0, c1, c2);
 #pragma unroll
-            for (int t = 0; t < NTD; ++t) {
-                const int i = q * NTD + t;
-                const float4 w = buf[i % D];
-                if (i + D < N) buf[i % D] = wp[(((i + D) % NTD) * nq + (i + D) / NTD) * 64];
-                L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, xq.x, L[t], 0, 0, 0);
-                L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, xq.y, L[t], 0, 0, 0);
-                L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, xq.z, L[t], 0, 0, 0);
-                L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, xq.w, L[t], 0, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
+                for (int t = 0; t < NTD; ++t) {
+                    const int i = q * NTD + t;
+                    const float4 w = buf[i % D];
+                    if (i + D < N) buf[i % D] = wp[(((i + D) % NTD) * nq + (i + D) / NTD) * 64];
+                    L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, xq.x, L[t], 0, 0, 0);
+                    L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, xq.y, L[t], 0, 0, 0);
+                    L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, xq.z, L[t], 0, 0, 0);
+                    L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, xq.w, L[t], 0, 0, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                xq = xn;
             }
-            xq = xn;
         }
     }
     TM_STAMP(2);
@@ -722,9 +727,11 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, const float *
     floatx4 A[NTD], Bv[NTD];
 #pragma unroll
     for (int t = 0; t < NTD; ++t) {
-        const float4 b = lds4(cs + C::EV, t);
+        const float4 b = lds4(cs + (p == 2 ? C::EVC : C::EV), t);
         const float bv[4] = {b.x, b.y, b.z, b.w};
-        { const int f4 = 4 * t + g < dn / 4 ? 4 * t + g : dn / 4 - 1; xs[t] = nrow_s[f4]; xt[t] = nrow_t[f4]; }
+        const int f4 = 4 * t + g < dn / 4 ? 4 * t + g : dn / 4 - 1;   // clamped; masked below
+        xs[t] = nrow_s[f4];
+        xt[t] = nrow_t[f4];
         const float sv[4] = {xs[t].x, xs[t].y, xs[t].z, xs[t].w}, tv[4] = {xt[t].x, xt[t].y, xt[t].z, xt[t].w};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1092,6 +1099,7 @@ extern "C" int tm_weights_create(int32_t de, int32_t dn, int32_t h, int device, 
     const size_t d3b = total; total += 4;
     const size_t fq = total; total += r16(dn);
     const size_t ph = total; total += r16(dn);
+    const size_t evc = total; total += r16(dn);
     int prev = 0;
     (void)hipGetDevice(&prev);
     if (hipSetDevice(device) != hipSuccess || hipMalloc(&w->buf, total * sizeof(float)) != hipSuccess ||
@@ -1113,8 +1121,23 @@ extern "C" int tm_weights_create(int32_t de, int32_t dn, int32_t h, int device, 
     P.d3b = w->buf + d3b;
     P.freq = w->buf + fq;
     P.phase = w->buf + ph;
+    P.evc = w->buf + evc;
+    P.qt = (de + 3 + 15) / 16;
     *out = w;
     return TM_OK;
+}
+
+// evc[f] = b[f] + sum_{k >= 16 qt} W[f][k] * cos(0 * w + phi)  (fp64 sum, one rounding)
+__global__ void evc_kernel(const float *__restrict__ W, const float *__restrict__ b, const float *__restrict__ phase,
+                           int de, int dn, int kev, int qt, float *__restrict__ out) {
+    for (int f = threadIdx.x; f < r16(dn); f += blockDim.x) {
+        double acc = 0.0;
+        if (f < dn) {
+            acc = b[f];
+            for (int k = 16 * qt; k < kev; ++k) acc += (double)W[(int64_t)f * kev + k] * (double)cos_rd(phase[k - de - 3]);
+        }
+        out[f] = (float)acc;
+    }
 }
 
 extern "C" int tm_weights_pack(tm_weights *w, const float *const *t, void *stream) {
@@ -1133,6 +1156,7 @@ extern "C" int tm_weights_pack(tm_weights *w, const float *const *t, void *strea
     copy_pad_kernel<<<dim3(1), 256, 0, s>>>(t[25], 1, 4, const_cast<float *>(w->P.d3b));
     copy_pad_kernel<<<dim3(1), 256, 0, s>>>(t[26], w->dn, r16(w->dn), const_cast<float *>(w->P.freq));
     copy_pad_kernel<<<dim3(1), 256, 0, s>>>(t[27], w->dn, r16(w->dn), const_cast<float *>(w->P.phase));
+    evc_kernel<<<dim3(1), 256, 0, s>>>(t[0], t[1], t[27], w->de, w->dn, w->P.kev, w->P.qt, const_cast<float *>(w->P.evc));
     TM_CHECK_LAUNCH();
     return TM_OK;
 }
