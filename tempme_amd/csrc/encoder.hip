@@ -628,6 +628,41 @@ __device__ unsigned long long g_st[3][10];
 #endif
 
 constexpr int EQ_MAX = 4;   // edge features span at most 4 K steps (de <= 64, checked on the host)
+static_assert(EQ_MAX == 4, "load_ef holds 4 K steps");
+
+// per-position scalars of one pass (walk row gw, position p): edge, its two endpoints, the time
+// offset to position 2 (:326) and the three edge counts; loaded one pass ahead of their use
+struct PosIn {
+    int32_t e, ns, nt;
+    float dt, c0, c1, c2;
+};
+
+__device__ __forceinline__ PosIn load_pos(const WalkArgs &a, int64_t gw, int p, bool valid) {
+    PosIn r{0, 0, 0, 0.f, 0.f, 0.f, 0.f};
+    if (valid) {
+        r.e = a.eid3[gw * 3 + p];
+        r.ns = a.node6[gw * 6 + 2 * p];
+        r.nt = a.node6[gw * 6 + 2 * p + 1];
+        r.dt = a.ts3[gw * 3 + 2] - a.ts3[gw * 3 + p];
+        r.c0 = a.cnt[gw * 9 + p * 3 + 0];
+        r.c1 = a.cnt[gw * 9 + p * 3 + 1];
+        r.c2 = a.cnt[gw * 9 + p * 3 + 2];
+    }
+    return r;
+}
+
+// edge-feature part of x: unconditional (clamped) loads, all in flight together
+__device__ __forceinline__ void load_ef(const WalkArgs &a, int32_t e, float (&ef)[4][4]) {
+    const int g = lane_id() >> 4, de = a.P.de;
+    const float *erow = a.e_feat + (int64_t)e * de;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int k = 16 * q + 4 * g + s;
+            ef[q][s] = (16 * q < de) ? erow[k < de ? k : de - 1] : 0.f;
+        }
+}
 
 // K step q of the event features x[k] = [E(e) | cnt | cos(dt * w + phi)] (:176-179, TimeEncode :45-59)
 template <int NQE, int NTD>
@@ -659,33 +694,15 @@ __device__ __forceinline__ floatx4 gen_x(int q, const float *cs, const float (&e
 // gathers (dn % 4 == 0) in the epilogue, unconditional with a clamped index (issuing them during the
 // GEMM keeps 88 more registers live and costs the second wave per SIMD).
 template <int NQE, int NTD>
-__device__ __forceinline__ void encode_position(const WalkArgs &a, const float *cs, int64_t gw, bool valid, int p,
-                                                floatx4 (&F)[8], unsigned long long (&T)[10]) {
+__device__ __forceinline__ void encode_position(const WalkArgs &a, const float *cs, const PosIn &pi,
+                                                const float (&ef)[EQ_MAX][4], int p, floatx4 (&F)[8],
+                                                unsigned long long (&T)[10]) {
     using C = WalkConsts<NQE, NTD>;
     const EncW &P = a.P;
     const int g = lane_id() >> 4;
     const int de = P.de, dn = P.dn, kev = P.kev;
-    int32_t e = 0, ns = 0, nt = 0;
-    float dt = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f;
-    if (valid) {
-        e = a.eid3[gw * 3 + p];
-        ns = a.node6[gw * 6 + 2 * p];
-        nt = a.node6[gw * 6 + 2 * p + 1];
-        dt = a.ts3[gw * 3 + 2] - a.ts3[gw * 3 + p];   // relative to walk position 2 (:326)
-        c0 = a.cnt[gw * 9 + p * 3 + 0];
-        c1 = a.cnt[gw * 9 + p * 3 + 1];
-        c2 = a.cnt[gw * 9 + p * 3 + 2];
-    }
-    // edge-feature part of x: unconditional (clamped) loads, all in flight together
-    float ef[EQ_MAX][4];
-    const float *erow = a.e_feat + (int64_t)e * de;
-#pragma unroll
-    for (int q = 0; q < EQ_MAX; ++q)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int k = 16 * q + 4 * g + s;
-            ef[q][s] = (16 * q < de) ? erow[k < de ? k : de - 1] : 0.f;
-        }
+    const int32_t ns = pi.ns, nt = pi.nt;
+    const float dt = pi.dt, c0 = pi.c0, c1 = pi.c1, c2 = pi.c2;
     const float4 *nrow_s = reinterpret_cast<const float4 *>(a.n_feat + (int64_t)ns * dn);
     const float4 *nrow_t = reinterpret_cast<const float4 *>(a.n_feat + (int64_t)nt * dn);
     float4 xs[NTD], xt[NTD];
@@ -867,6 +884,9 @@ __global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
     floatx4(&sWp)[8][64] = stash[threadIdx.x >> 6][1];
     floatx4 Q0[8];                                      // W2(position 0), carried to the position-1 pass
     const int n_pass = 1 + 2 * a.M;
+    PosIn cur = load_pos(a, eg * a.W + (int64_t)j * a.M, 2, valid);
+    float ef[EQ_MAX][4];
+    load_ef(a, cur.e, ef);
     // pass 0: position 2 once per slot (walk j*M carries it); then per walk m: position 0, position 1
 #pragma nounroll
     for (int pass = 0; pass < n_pass; ++pass) {
@@ -881,10 +901,16 @@ __global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
             hi.t1 = a.ts3[gw * 3 + 1];
             hi.c = a.cat[gw];
         }
+        // next pass's scalars now; its edge features once this pass's lin_event is done
+        const int pn = pass + 1 < n_pass ? ((pass & 1) == 0 ? 0 : 1) : 0;
+        const int64_t gwn = eg * a.W + (int64_t)j * a.M + (pass >> 1);
+        const PosIn nxt = load_pos(a, gwn, pn, valid && pass + 1 < n_pass);
         floatx4 F[8];
         unsigned long long T[10];
         TM_STAMP(0);
-        encode_position<NQE, NTD>(a, cs, gw, valid, p, F, T);
+        encode_position<NQE, NTD>(a, cs, cur, ef, p, F, T);
+        load_ef(a, nxt.e, ef);
+        cur = nxt;
         floatx4 Y[8];
         TM_STAMP(6);
         rgemm<8, 8>(p == 2 ? P.w1 : P.w2, F, Y);
