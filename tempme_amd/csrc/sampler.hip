@@ -306,8 +306,11 @@ __global__ void __launch_bounds__(256) edge_counts_kernel(const int32_t *__restr
 }
 
 // ------------------------------------------------------------------ fused per-(event, side) sampler
-// One 256-thread workgroup per (event, side): hop 1 -> hop 2 -> step 2 -> step 3 -> category ->
-// edge counts, intermediates in LDS.  Side 0/1: root = src/dst, e_idx path (data_preprocess.py:114,
+// One wave per (event, side): hop 1 -> hop 2 -> step 2 -> step 3 -> category -> edge counts,
+// intermediates in LDS sized to N and M.  The walk steps are chains of dependent L2 lookups (cut
+// lengths, pair-index binary searches, record gathers), so the kernel is latency-bound: a single-wave
+// workgroup with ~3 KB of LDS (N=20) lets 32 (event, side)s run per CU, where a 256-thread workgroup
+// with N=64-sized arrays allowed 6 and left 3 of its 4 waves idle in the walk phase.  Side 0/1: root = src/dst, e_idx path (data_preprocess.py:114,
 // :118); side 2: root = negative dst, time path (:122).
 struct EventArgs {
     DevGraph g;
@@ -332,15 +335,21 @@ struct EventArgs {
     int32_t *err;
 };
 
-__global__ void __launch_bounds__(256) events_kernel(EventArgs a) {
-    __shared__ int32_t h1n[kMaxN], h1e[kMaxN];
-    __shared__ float h1t[kMaxN];
-    __shared__ uint32_t d2[kMaxN * kMaxN];
-    __shared__ int32_t c2[kMaxN];
-    __shared__ int32_t weid[kMaxN * kMaxM * 3];
-    __shared__ unsigned int bins[12];
+// LDS of one (event, side): hop-1 row, hop-2 draws, hop-2 cut lengths, walk edge ids, histogram
+__host__ __device__ inline size_t events_lds_bytes(int32_t N, int32_t M) {
+    return sizeof(int32_t) * ((size_t)3 * N + (size_t)N * N + N + (size_t)N * M * 3 + 12);
+}
+
+__global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
+    extern __shared__ int32_t ev_lds[];
+    const int32_t N = a.N, M = a.M, W = N * M;
+    int32_t *h1n = ev_lds, *h1e = h1n + N;
+    float *h1t = reinterpret_cast<float *>(h1e + N);
+    uint32_t *d2 = reinterpret_cast<uint32_t *>(h1e + 2 * N);
+    int32_t *c2 = reinterpret_cast<int32_t *>(d2 + N * N), *weid = c2 + N;
+    unsigned int *bins = reinterpret_cast<unsigned int *>(weid + W * 3);
     const DevGraph &g = a.g;
-    const int32_t e = blockIdx.x, s = blockIdx.y, N = a.N, M = a.M, W = N * M, tid = threadIdx.x;
+    const int32_t e = blockIdx.x, s = blockIdx.y, tid = threadIdx.x;
     const uint32_t ev = a.event_ids[e];
     const Key key = make_key(a.seed, a.split, (uint32_t)(s + 1));
     if (tid < 12) bins[tid] = 0;
@@ -544,7 +553,7 @@ extern "C" int tm_sample_events(const tm_graph *g, uint64_t seed, uint32_t split
                 dst_list, (uint32_t)n_dst, dst_fake, sub1_node, sub1_eid, sub1_ts, sub2_node, sub2_eid, sub2_ts,
                 node6,    eid3,     ts3,       cat,       cnt,      hist12,   err_flag};
     hipEvent_t pe = prof_begin(S(stream));
-    events_kernel<<<dim3(n_events, 3), 256, 0, S(stream)>>>(a);
+    events_kernel<<<dim3(n_events, 3), 64, events_lds_bytes(N, M), S(stream)>>>(a);
     TM_CHECK_LAUNCH();
     prof_end("events_kernel", S(stream), pe);
     return TM_OK;

@@ -41,7 +41,7 @@ for s in "$@"; do
                 for so in tempme_amd/lib/ab/*.so; do
                     n=$(basename "$so" .so)
                     TEMPME_LIB="$PWD/$so" step ab_${n}_$r 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline
-                    echo "$n round $r: $(grep -o '"walk_kernel": {"avg_ms": [0-9.]*' gpurun_out/ab_${n}_$r.log)" | tee -a gpurun_out/ab.txt
+                    echo "$n round $r: $(grep -o '"walk_kernel": {"avg_ms": [0-9.]*' gpurun_out/ab_${n}_$r.log) $(grep -o '"events_kernel": {"avg_ms": [0-9.]*' gpurun_out/ab_${n}_$r.log) $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_${n}_$r.log)" | tee -a gpurun_out/ab.txt
                 done
             done ;;
         stamps)  # phase stamps of every -DTM_STAMPS build in tempme_amd/lib/ab/
