@@ -39,7 +39,7 @@ __device__ __forceinline__ void rgemm(const float4 *w, const floatx4 (&x)[NQ], f
 }
 
 // EPI 0: none (just pass D through), 1: bias (LDS) + relu
-template <int D, int MODE, int EPI>
+template <int D, int MODE, int EPI, int U = 1>
 __global__ void __launch_bounds__(256, 2) chain_kernel(const float4 *w, int iters, float *out) {
     extern __shared__ float bias[];   // dynamic size sets blocks per CU (occupancy)
     if (threadIdx.x < 128) bias[threadIdx.x] = 0.001f * threadIdx.x;
@@ -49,12 +49,23 @@ __global__ void __launch_bounds__(256, 2) chain_kernel(const float4 *w, int iter
     for (int q = 0; q < 8; ++q) x[q] = floatx4{1e-3f * q, 1e-3f, 2e-3f, 3e-3f};
     const int g = threadIdx.x & 63 >> 4;
 #pragma nounroll
-    for (int it = 0; it < iters; ++it) {
+    for (int it = 0; it < iters; it += U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
         floatx4 y[8];
-        rgemm<8, 8, D, MODE>(w + (it & 3) * 64 * 64, x, y);
+        rgemm<8, 8, D, MODE>(w + ((it + u) & 3) * 64 * 64, x, y);
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
-            if (EPI) {
+            if (EPI == 2 && t == 0) {
+                // VALU block: 4 independent chains x 64 dependent FMAs (256 VALU) per layer
+                float a0 = y[0][0], a1 = y[0][1], a2 = y[0][2], a3 = y[0][3];
+#pragma unroll
+                for (int r = 0; r < 64; ++r) {
+                    a0 = __builtin_fmaf(a0, 0.999f, 1e-3f); a1 = __builtin_fmaf(a1, 0.999f, 1e-3f);
+                    a2 = __builtin_fmaf(a2, 0.999f, 1e-3f); a3 = __builtin_fmaf(a3, 0.999f, 1e-3f);
+                }
+                x[0] = floatx4{a0, a1, a2, a3};
+            } else if (EPI) {
                 const float4 b = *reinterpret_cast<const float4 *>(bias + 16 * t + 4 * g);
                 x[t] = floatx4{fmaxf(y[t][0] + b.x, 0.f), fmaxf(y[t][1] + b.y, 0.f), fmaxf(y[t][2] + b.z, 0.f),
                                fmaxf(y[t][3] + b.w, 0.f)};
@@ -63,23 +74,24 @@ __global__ void __launch_bounds__(256, 2) chain_kernel(const float4 *w, int iter
             }
         }
     }
+    }
     float s = 0.f;
 #pragma unroll
     for (int q = 0; q < 8; ++q) s += x[q][0] + x[q][1] + x[q][2] + x[q][3];
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
-template <int D, int MODE, int EPI>
+template <int D, int MODE, int EPI, int U = 1>
 static void run(const char *name, const float4 *w, float *out, int blocks, int iters, int lds = 64 * 1024) {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    hipFuncSetAttribute((const void *)chain_kernel<D, MODE, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    chain_kernel<D, MODE, EPI><<<blocks, 256, lds>>>(w, iters, out);
+    hipFuncSetAttribute((const void *)chain_kernel<D, MODE, EPI, U>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    chain_kernel<D, MODE, EPI, U><<<blocks, 256, lds>>>(w, iters, out);
     hipDeviceSynchronize();
     hipEventRecord(a);
     const int reps = 5;
-    for (int r = 0; r < reps; ++r) chain_kernel<D, MODE, EPI><<<blocks, 256, lds>>>(w, iters, out);
+    for (int r = 0; r < reps; ++r) chain_kernel<D, MODE, EPI, U><<<blocks, 256, lds>>>(w, iters, out);
     hipEventRecord(b);
     hipEventSynchronize(b);
     float ms;
@@ -105,6 +117,10 @@ int main() {
     run<3, 1, 1>("D3 pairs epi", w, out, blocks, iters);
     run<6, 0, 1>("D6 tmajor epi", w, out, blocks, iters);
     run<1, 0, 1>("D1 tmajor epi", w, out, blocks, iters);
+    run<3, 0, 2>("D3 tmajor valu256 2w", w, out, blocks, iters);
+    run<3, 0, 2>("D3 tmajor valu256 1w", w, out, blocks, iters, 100 * 1024);
+    run<3, 0, 2>("D3 tmajor valu256 4w", w, out, blocks, iters, 32 * 1024);
+    run<3, 1, 2>("D3 pairs valu256 2w", w, out, blocks, iters);
     run<3, 0, 1>("D3 tmajor epi 1 wave/SIMD", w, out, blocks, iters, 100 * 1024);
     run<3, 0, 1>("D3 tmajor epi 4 waves/SIMD", w, out, blocks, iters, 32 * 1024);
     run<3, 1, 1>("D3 pairs epi 4 waves/SIMD", w, out, blocks, iters, 32 * 1024);

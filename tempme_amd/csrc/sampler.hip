@@ -66,6 +66,38 @@ __device__ __forceinline__ int32_t kth_of_two(const Pair *p1, int32_t n1, const 
     return a > b ? a : b;
 }
 
+// K independent pair_lb searches advanced together: every halving issues all K loads (unconditional,
+// clamped) before any compare, so the K searches cost one round trip per level.  u < 0: empty (0).
+template <int K>
+__device__ __forceinline__ void pair_lb_multi(const DevGraph &g, const int32_t (&u)[K], const int32_t (&x)[K],
+                                              const int32_t (&p)[K], int32_t (&out)[K]) {
+    int32_t lo[K], hi[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        lo[k] = u[k] >= 0 ? g.off[u[k]] : 0;
+        hi[k] = u[k] >= 0 ? g.off[u[k] + 1] : 0;
+    }
+    while (true) {
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < K; ++k) any |= lo[k] < hi[k];
+        if (!any) break;
+        Pair q[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) q[k] = g.pair[lo[k] < hi[k] ? (lo[k] + hi[k]) >> 1 : 0];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (lo[k] < hi[k]) {
+                const int32_t mid = (lo[k] + hi[k]) >> 1;
+                if (q[k].ngh < x[k] || (q[k].ngh == x[k] && q[k].pos < p[k])) lo[k] = mid + 1;
+                else hi[k] = mid;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) out[k] = lo[k];
+}
+
 struct Step3 {
     int32_t src, ngh, eid;
     float ts;
@@ -90,18 +122,20 @@ __device__ Step3 final_step(const DevGraph &g, Key key, uint32_t ev, uint32_t w,
     const int32_t ca = final_len(g, a_node, e2), cb = final_len(g, b_node, e2);
     int32_t na, nb, lb1 = 0, n1 = 0, lb2 = 0, n2 = 0, lbb = 0;
     if (filt) {
-        if (ca > 0) {
-            lb1 = pair_lb(g, a_node, a1, 0);
-            n1 = pair_lb(g, a_node, a1, ca) - lb1;
-            lb2 = pair_lb(g, a_node, a2, 0);
-            n2 = pair_lb(g, a_node, a2, ca) - lb2;
-        }
+        // the six lower bounds of the filtered counts, searched in lockstep (one dependent L2 round
+        // trip per halving for all six instead of six sequential searches)
+        const int32_t ua = (ca > 0) ? a_node : -1, ub = (cb > 0) ? b_node : -1;
+        const int32_t us[6] = {ua, ua, ua, ua, ub, ub}, xs[6] = {a1, a1, a2, a2, bf, bf},
+                      ps[6] = {0, ca, 0, ca, 0, cb};
+        int32_t lb[6];
+        pair_lb_multi<6>(g, us, xs, ps, lb);
+        n1 = lb[1] - lb[0];
+        n2 = lb[3] - lb[2];
+        nb = lb[5] - lb[4];
+        lb1 = lb[0];
+        lb2 = lb[2];
+        lbb = lb[4];
         na = n1 + n2;
-        nb = 0;
-        if (cb > 0) {
-            lbb = pair_lb(g, b_node, bf, 0);
-            nb = pair_lb(g, b_node, bf, cb) - lbb;
-        }
     } else {
         na = ca;
         nb = cb;
@@ -337,7 +371,7 @@ struct EventArgs {
 
 // LDS of one (event, side): hop-1 row, hop-2 draws, hop-2 cut lengths, walk edge ids, histogram
 __host__ __device__ inline size_t events_lds_bytes(int32_t N, int32_t M) {
-    return sizeof(int32_t) * ((size_t)3 * N + (size_t)N * N + N + (size_t)N * M * 3 + 12);
+    return sizeof(int32_t) * ((size_t)3 * N + (size_t)N * N + 2 * N + (size_t)N * M * 3 + 12);
 }
 
 __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
@@ -346,7 +380,7 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
     int32_t *h1n = ev_lds, *h1e = h1n + N;
     float *h1t = reinterpret_cast<float *>(h1e + N);
     uint32_t *d2 = reinterpret_cast<uint32_t *>(h1e + 2 * N);
-    int32_t *c2 = reinterpret_cast<int32_t *>(d2 + N * N), *weid = c2 + N;
+    int32_t *c2 = reinterpret_cast<int32_t *>(d2 + N * N), *o2 = c2 + N, *weid = o2 + N;
     unsigned int *bins = reinterpret_cast<unsigned int *>(weid + W * 3);
     const DevGraph &g = a.g;
     const int32_t e = blockIdx.x, s = blockIdx.y, tid = threadIdx.x;
@@ -386,31 +420,49 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
     }
     __syncthreads();
     // ---- hop 2 (N rows x N draws; e_idx path, graph.py:247-250)
-    if (tid < N) c2[tid] = find_before_len(g, h1n[tid], false, 0.0, h1e[tid], a.err);
+    if (tid < N) {
+        c2[tid] = find_before_len(g, h1n[tid], false, 0.0, h1e[tid], a.err);
+        const int32_t v = h1n[tid];
+        o2[tid] = (v >= 0 && v < g.n_nodes) ? g.off[v] : 0;   // record offset of the hop-2 row's node
+    }
     __syncthreads();
     for (int32_t x = tid; x < N * N; x += blockDim.x) {
         const int32_t j = x / N, k = x % N, c = c2[j];
         d2[x] = c > 0 ? (uint32_t)draw(key, 2, ev, j, k, c) : 0xFFFFFFFFu;
     }
     __syncthreads();
-    for (int32_t x = tid; x < N * N; x += blockDim.x) {
-        const int32_t j = x / N, k = x % N, c = c2[j];
-        const uint32_t d = d2[x];
-        int32_t rank = 0;
-        for (int32_t i = 0; i < N; ++i) {
-            const uint32_t di = d2[j * N + i];
-            rank += (di < d) || (i < k && di == d);
+    // 4 rows of draws per lane per round: ranks from LDS, then the 4 record gathers issued together
+    // (unconditional, index 0 when the row is empty) before any output is stored
+    constexpr int HB = 4;
+    for (int32_t x0 = 0; x0 < N * N; x0 += HB * 64) {
+        int32_t slot[HB], idx[HB];
+        bool ok[HB];
+#pragma unroll
+        for (int u = 0; u < HB; ++u) {
+            const int32_t x = x0 + u * 64 + tid;
+            const int32_t j = x < N * N ? x / N : 0, k = x % N, c = x < N * N ? c2[j] : 0;
+            const uint32_t d = x < N * N ? d2[x] : 0u;
+            int32_t rank = 0;
+            if (c > 0)
+                for (int32_t i = 0; i < N; ++i) {
+                    const uint32_t di = d2[j * N + i];
+                    rank += (di < d) || (i < k && di == d);
+                }
+            ok[u] = c > 0 && g.n_entries > 0;
+            slot[u] = c > 0 ? j * N + rank : x;
+            idx[u] = ok[u] ? o2[j] + (int32_t)d : 0;
         }
-        int32_t n_ = 0, e_ = 0, slot = x;
-        float t_ = 0.f;
-        if (c > 0) {
-            const Rec rc = g.rec[g.off[h1n[j]] + (int32_t)d];
-            n_ = rc.ngh; e_ = rc.eid; t_ = (float)rc.ts; slot = j * N + rank;
+        Rec rc[HB];
+#pragma unroll
+        for (int u = 0; u < HB; ++u) rc[u] = g.n_entries > 0 ? g.rec[idx[u]] : Rec{0, 0, 0.0};
+#pragma unroll
+        for (int u = 0; u < HB; ++u) {
+            if (x0 + u * 64 + tid >= N * N) continue;
+            const int64_t o = se * N * N + slot[u];
+            a.sub2_node[o] = ok[u] ? rc[u].ngh : 0;
+            a.sub2_eid[o] = ok[u] ? rc[u].eid : 0;
+            a.sub2_ts[o] = ok[u] ? (float)rc[u].ts : 0.f;
         }
-        const int64_t o = se * N * N + slot;
-        a.sub2_node[o] = n_;
-        a.sub2_eid[o] = e_;
-        a.sub2_ts[o] = t_;
     }
     // ---- steps 2 + 3, one thread per walk
     for (int32_t w = tid; w < W; w += blockDim.x) {
