@@ -498,21 +498,33 @@ __device__ __forceinline__ int lane_id() {
     return l;
 }
 
+// Weight fragments are read with buffer loads: the fragment's byte offset is a compile-time SGPR
+// operand (s_mov, scalar pipe) instead of a 64-bit VGPR address add per fragment.  The lane offset
+// goes through lane_id() so the loads stay inside the pass loop.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wrsrc(const float4 *w) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float4 *>(w), (short)0, 0x7fffffff, 0x00020000);
+}
+
+__device__ __forceinline__ float4 wload(__amdgpu_buffer_rsrc_t r, int vo, int f4) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, f4 * 16, 0));
+}
+
 template <int NTO, int NQ>
 __device__ __forceinline__ void rgemm(const Lin &L, const floatx4 (&x)[NQ], floatx4 (&o)[NTO]) {
-    const float4 *wp = L.w + lane_id();
+    const auto wr = wrsrc(L.w);
+    const int vo = lane_id() * 16;
     constexpr int nq = NQ;   // == L.nq: fragment offsets are immediates
     constexpr int N = NTO * NQ, D = PF < N ? PF : N;
 #pragma unroll
     for (int t = 0; t < NTO; ++t) o[t] = floatx4{0.f, 0.f, 0.f, 0.f};
     float4 buf[D];
 #pragma unroll
-    for (int i = 0; i < D; ++i) buf[i] = wp[TM_W_ADDR(i)];
+    for (int i = 0; i < D; ++i) buf[i] = wload(wr, vo, TM_W_ADDR(i));
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         const int t = i / NQ, q = i % NQ;
         const float4 w = buf[i % D];
-        if (i + D < N) buf[i % D] = wp[TM_W_ADDR(i + D)];
+        if (i + D < N) buf[i % D] = wload(wr, vo, TM_W_ADDR(i + D));
         o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, x[q].x, o[t], 0, 0, 0);
         o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, x[q].y, o[t], 0, 0, 0);
         o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, x[q].z, o[t], 0, 0, 0);
@@ -525,7 +537,8 @@ __device__ __forceinline__ void rgemm(const Lin &L, const floatx4 (&x)[NQ], floa
 template <int NTO, int NQ>
 __device__ __forceinline__ void rgemm2(const Lin &L, const floatx4 (&x)[NQ], const floatx4 (&y)[NQ],
                                        floatx4 (&o)[NTO], floatx4 (&p)[NTO]) {
-    const float4 *wp = L.w + lane_id();
+    const auto wr = wrsrc(L.w);
+    const int vo = lane_id() * 16;
     constexpr int nq = NQ;
     constexpr int N = NTO * NQ, D = PF < N ? PF : N;
 #pragma unroll
@@ -535,12 +548,12 @@ __device__ __forceinline__ void rgemm2(const Lin &L, const floatx4 (&x)[NQ], con
     }
     float4 buf[D];
 #pragma unroll
-    for (int i = 0; i < D; ++i) buf[i] = wp[TM_W_ADDR(i)];
+    for (int i = 0; i < D; ++i) buf[i] = wload(wr, vo, TM_W_ADDR(i));
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         const int t = i / NQ, q = i % NQ;
         const float4 w = buf[i % D];
-        if (i + D < N) buf[i % D] = wp[TM_W_ADDR(i + D)];
+        if (i + D < N) buf[i % D] = wload(wr, vo, TM_W_ADDR(i + D));
         o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, x[q].x, o[t], 0, 0, 0);
         p[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, y[q].x, p[t], 0, 0, 0);
         o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, x[q].y, o[t], 0, 0, 0);
@@ -711,12 +724,13 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, const float *
     for (int t = 0; t < NTD; ++t) L[t] = floatx4{0.f, 0.f, 0.f, 0.f};
     TM_STAMP(1);
     {
-        const float4 *wp = P.ev.w + lane_id();
+        const auto wr = wrsrc(P.ev.w);
+        const int vo = lane_id() * 16;
         constexpr int nq = NQE;
         constexpr int N = NTD * NQE, D = PF;
         float4 buf[D];
 #pragma unroll
-        for (int i = 0; i < D; ++i) buf[i] = wp[((i % NTD) * nq + i / NTD) * 64];
+        for (int i = 0; i < D; ++i) buf[i] = wload(wr, vo, ((i % NTD) * nq + i / NTD) * 64);
         floatx4 xq = gen_x<NQE, NTD>(0, cs, ef, g, de, kev, dt, c0, c1, c2);
         const int qend = p == 2 ? P.qt : NQE;            // slot pass: steps >= qt folded into evc
 #pragma unroll
@@ -728,7 +742,7 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, const float *
                 for (int t = 0; t < NTD; ++t) {
                     const int i = q * NTD + t;
                     const float4 w = buf[i % D];
-                    if (i + D < N) buf[i % D] = wp[(((i + D) % NTD) * nq + (i + D) / NTD) * 64];
+                    if (i + D < N) buf[i % D] = wload(wr, vo, (((i + D) % NTD) * nq + (i + D) / NTD) * 64);
                     L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, xq.x, L[t], 0, 0, 0);
                     L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, xq.y, L[t], 0, 0, 0);
                     L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, xq.z, L[t], 0, 0, 0);

@@ -374,7 +374,22 @@ __host__ __device__ inline size_t events_lds_bytes(int32_t N, int32_t M) {
     return sizeof(int32_t) * ((size_t)3 * N + (size_t)N * N + 2 * N + (size_t)N * M * 3 + 12);
 }
 
+// Phase timing (debug builds only, -DTM_STAMPS): s_memtime deltas of lane 0 for events 2000..3999
+#ifdef TM_STAMPS
+__device__ unsigned long long g_est[8];
+#define TM_EST(k)                                   \
+    do {                                            \
+        __builtin_amdgcn_sched_barrier(0);          \
+        T[k] = __builtin_amdgcn_s_memtime();        \
+        __builtin_amdgcn_sched_barrier(0);          \
+    } while (0)
+#else
+#define TM_EST(k) (void)T
+#endif
+
 __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
+    unsigned long long T[8];
+    TM_EST(0);
     extern __shared__ int32_t ev_lds[];
     const int32_t N = a.N, M = a.M, W = N * M;
     int32_t *h1n = ev_lds, *h1e = h1n + N;
@@ -419,6 +434,7 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
         }
     }
     __syncthreads();
+    TM_EST(1);
     // ---- hop 2 (N rows x N draws; e_idx path, graph.py:247-250)
     if (tid < N) {
         c2[tid] = find_before_len(g, h1n[tid], false, 0.0, h1e[tid], a.err);
@@ -426,6 +442,7 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
         o2[tid] = (v >= 0 && v < g.n_nodes) ? g.off[v] : 0;   // record offset of the hop-2 row's node
     }
     __syncthreads();
+    TM_EST(2);
     for (int32_t x = tid; x < N * N; x += blockDim.x) {
         const int32_t j = x / N, k = x % N, c = c2[j];
         d2[x] = c > 0 ? (uint32_t)draw(key, 2, ev, j, k, c) : 0xFFFFFFFFu;
@@ -464,6 +481,7 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
             a.sub2_ts[o] = ok[u] ? (float)rc[u].ts : 0.f;
         }
     }
+    TM_EST(3);
     // ---- steps 2 + 3, one thread per walk
     for (int32_t w = tid; w < W; w += blockDim.x) {
         const int32_t j = w / M, m = w % M;
@@ -481,7 +499,15 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
         weid[w * 3 + 0] = s3.eid; weid[w * 3 + 1] = s2.eid; weid[w * 3 + 2] = e1;
     }
     __syncthreads();
+    TM_EST(4);
     edge_counts_group(weid, W, a.cnt + se * W * 9);
+    TM_EST(5);
+#ifdef TM_STAMPS
+    if (tid == 0 && e >= 2000 && e < 4000) {
+        for (int k = 0; k < 5; ++k) atomicAdd(&g_est[k], T[k + 1] - T[k]);
+        atomicAdd(&g_est[7], 1ull);
+    }
+#endif
     if (tid < 12 && bins[tid]) atomicAdd(&a.hist[tid], (unsigned long long)bins[tid]);
 }
 
@@ -610,3 +636,10 @@ extern "C" int tm_sample_events(const tm_graph *g, uint64_t seed, uint32_t split
     prof_end("events_kernel", S(stream), pe);
     return TM_OK;
 }
+
+#ifdef TM_STAMPS
+extern "C" int tm_debug_event_stamps(unsigned long long *host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(tmk::g_est), sizeof(unsigned long long) * 8, 0,
+                                    hipMemcpyDeviceToHost);
+}
+#endif

@@ -1,13 +1,19 @@
-"""Debug: run bench.py once under a stamping walk_kernel build (TEMPME_LIB=.../stamp.so) and print the
-average cycles per phase per pass type (s_memtime deltas of lane 0, blocks 512..1023)."""
+"""Debug: run bench.py once under a -DTM_STAMPS build (TEMPME_LIB=tempme_amd/lib/ab/<name>.so) and print
+the average cycles per phase of events_kernel (per (event, side)) and of walk_kernel per pass type
+(s_memtime deltas of lane 0)."""
 import ctypes as C
 import runpy
 import sys
 
-sys.argv = ["bench.py", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"]
+sys.argv = ["bench.py", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
 runpy.run_path("bench.py", run_name="__main__")
 from tempme_amd import _lib  # noqa: E402
 
+ev = (C.c_ulonglong * 8)()
+assert _lib.lib().tm_debug_event_stamps(ev) == 0
+n = max(1, ev[7])
+print("events_kernel n=%d" % ev[7], " ".join("%s=%.0f" % (nm, ev[k] / n) for k, nm in
+                                             enumerate(["hop1", "hop2_cuts", "hop2", "walks", "edge_counts"])))
 buf = (C.c_ulonglong * 30)()
 assert _lib.lib().tm_debug_stamps(buf) == 0
 names = ["issue", "xgen+ev_gemm", "A/B+gather", "g1", "g2+ep", "F ep", "W gemm", "head/stash"]
