@@ -669,12 +669,21 @@ __device__ __forceinline__ void load_ef(const WalkArgs &a, int32_t e, float (&ef
     const int g = lane_id() >> 4, de = a.P.de;
     const float *erow = a.e_feat + (int64_t)e * de;
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < 4; ++q) {
+        if ((de & 3) == 0 && 16 * q + 16 <= de) {         // whole K step inside the row: one float4
+            const float4 v = *reinterpret_cast<const float4 *>(erow + 16 * q + 4 * g);
+            ef[q][0] = v.x;
+            ef[q][1] = v.y;
+            ef[q][2] = v.z;
+            ef[q][3] = v.w;
+        } else {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int k = 16 * q + 4 * g + s;
-            ef[q][s] = (16 * q < de) ? erow[k < de ? k : de - 1] : 0.f;
+            for (int s = 0; s < 4; ++s) {
+                const int k = 16 * q + 4 * g + s;
+                ef[q][s] = (16 * q < de) ? erow[k < de ? k : de - 1] : 0.f;
+            }
         }
+    }
 }
 
 // K step q of the event features x[k] = [E(e) | cnt | cos(dt * w + phi)] (:176-179, TimeEncode :45-59)
@@ -760,7 +769,9 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, const float *
     for (int t = 0; t < NTD; ++t) {
         const float4 b = lds4(cs + (p == 2 ? C::EVC : C::EV), t);
         const float bv[4] = {b.x, b.y, b.z, b.w};
-        const int f4 = 4 * t + g < dn / 4 ? 4 * t + g : dn / 4 - 1;   // clamped; masked below
+        // tiles below the last are inside the row (dispatch: 160 < dn <= 176), so their offsets are
+        // immediates on one row address; the last tile's index is clamped and masked below
+        const int f4 = (t < NTD - 1) ? 4 * t + g : min(4 * t + g, dn / 4 - 1);
         xs[t] = nrow_s[f4];
         xt[t] = nrow_t[f4];
         const float sv[4] = {xs[t].x, xs[t].y, xs[t].z, xs[t].w}, tv[4] = {xt[t].x, xt[t].y, xt[t].z, xt[t].w};
