@@ -39,18 +39,23 @@ __device__ __forceinline__ int32_t find_before_len(const DevGraph &g, int32_t u,
     return l;
 }
 
-// cut of find_before_walk (graph.py:171-176): missing e_idx -> 0
-__device__ __forceinline__ int32_t walk_len(const DevGraph &g, int32_t u, int32_t e) {
-    if (!(u > 0) || u >= g.n_nodes) return 0;
-    int32_t l = edge_len(g, u, e);
-    return l < 0 ? 0 : l;
-}
-
-// cut of get_final_step (graph.py:357, :366, ...): None -> whole list ([:None] leak)
-__device__ __forceinline__ int32_t final_len(const DevGraph &g, int32_t u, int32_t e) {
-    if (!(u > 0) || u >= g.n_nodes) return 0;
-    int32_t l = edge_len(g, u, e);
-    return l < 0 ? deg(g, u) : l;
+// bisect_left over node u's timestamps by the whole wave (all 64 lanes call it, the result is
+// uniform): each round tests 64 evenly spaced records and keeps the gap holding the answer, so a
+// list of up to 4096 records costs two dependent loads instead of twelve.
+__device__ int32_t bisect_ts_wave(const DevGraph &g, int32_t u, double x) {
+    const int32_t s = g.off[u], lane = threadIdx.x & 63;
+    int32_t lo = 0, hi = g.off[u + 1] - s;
+    while (hi - lo > 64) {
+        const int32_t stride = (hi - lo + 63) / 64, q = lo + lane * stride;
+        const bool lt = q < hi && g.rec[s + q].ts < x;
+        const int32_t c = __popcll(__ballot(lt));        // sorted: the samples below x are a prefix
+        const int32_t nlo = c > 0 ? lo + (c - 1) * stride + 1 : lo;
+        hi = min(hi, lo + c * stride);
+        lo = nlo;
+    }
+    const int32_t q = lo + lane;
+    const bool lt = q < hi && g.rec[s + q].ts < x;
+    return lo + __popcll(__ballot(lt));
 }
 
 // rank-th smallest position of the union of two sorted, disjoint position lists
@@ -67,16 +72,11 @@ __device__ __forceinline__ int32_t kth_of_two(const Pair *p1, int32_t n1, const 
 }
 
 // K independent pair_lb searches advanced together: every halving issues all K loads (unconditional,
-// clamped) before any compare, so the K searches cost one round trip per level.  u < 0: empty (0).
+// clamped) before any compare, so the K searches cost one round trip per level.
+// [lo, hi) = the owner node's range in the pair index (empty: no search).
 template <int K>
-__device__ __forceinline__ void pair_lb_multi(const DevGraph &g, const int32_t (&u)[K], const int32_t (&x)[K],
-                                              const int32_t (&p)[K], int32_t (&out)[K]) {
-    int32_t lo[K], hi[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        lo[k] = u[k] >= 0 ? g.off[u[k]] : 0;
-        hi[k] = u[k] >= 0 ? g.off[u[k] + 1] : 0;
-    }
+__device__ __forceinline__ void pair_lb_multi(const DevGraph &g, int32_t (&lo)[K], int32_t (&hi)[K],
+                                              const int32_t (&x)[K], const int32_t (&p)[K], int32_t (&out)[K]) {
     while (true) {
         bool any = false;
 #pragma unroll
@@ -119,16 +119,24 @@ __device__ Step3 final_step(const DevGraph &g, Key key, uint32_t ev, uint32_t w,
     } else {
         code = 1; a_node = tgt1; b_node = tgt2; filt = false;
     }
-    const int32_t ca = final_len(g, a_node, e2), cb = final_len(g, b_node, e2);
+    // everything the cut lengths and the record offsets need, loaded together up front:
+    // final_len (graph.py:357, :366): node 0 / out of range -> 0; e2 not in the node's dict -> whole list
+    const bool va = a_node > 0 && a_node < g.n_nodes, vb = b_node > 0 && b_node < g.n_nodes;
+    const EdgeEnds x2 = (e2 >= 0 && e2 <= g.max_eid) ? g.ends[e2] : EdgeEnds{-1, 0, -1, 0};
+    const int32_t oa0 = va ? g.off[a_node] : 0, oa1 = va ? g.off[a_node + 1] : 0;
+    const int32_t ob0 = vb ? g.off[b_node] : 0, ob1 = vb ? g.off[b_node + 1] : 0;
+    const int32_t ca = !va ? 0 : x2.node_a == a_node ? x2.len_a : x2.node_b == a_node ? x2.len_b : oa1 - oa0;
+    const int32_t cb = !vb ? 0 : x2.node_a == b_node ? x2.len_a : x2.node_b == b_node ? x2.len_b : ob1 - ob0;
     int32_t na, nb, lb1 = 0, n1 = 0, lb2 = 0, n2 = 0, lbb = 0;
     if (filt) {
         // the six lower bounds of the filtered counts, searched in lockstep (one dependent L2 round
         // trip per halving for all six instead of six sequential searches)
-        const int32_t ua = (ca > 0) ? a_node : -1, ub = (cb > 0) ? b_node : -1;
-        const int32_t us[6] = {ua, ua, ua, ua, ub, ub}, xs[6] = {a1, a1, a2, a2, bf, bf},
-                      ps[6] = {0, ca, 0, ca, 0, cb};
+        const bool sa = ca > 0, sb = cb > 0;
+        int32_t lo[6] = {sa ? oa0 : 0, sa ? oa0 : 0, sa ? oa0 : 0, sa ? oa0 : 0, sb ? ob0 : 0, sb ? ob0 : 0};
+        int32_t hi[6] = {sa ? oa1 : 0, sa ? oa1 : 0, sa ? oa1 : 0, sa ? oa1 : 0, sb ? ob1 : 0, sb ? ob1 : 0};
+        const int32_t xs[6] = {a1, a1, a2, a2, bf, bf}, ps[6] = {0, ca, 0, ca, 0, cb};
         int32_t lb[6];
-        pair_lb_multi<6>(g, us, xs, ps, lb);
+        pair_lb_multi<6>(g, lo, hi, xs, ps, lb);
         n1 = lb[1] - lb[0];
         n2 = lb[3] - lb[2];
         nb = lb[5] - lb[4];
@@ -147,12 +155,12 @@ __device__ Step3 final_step(const DevGraph &g, Key key, uint32_t ev, uint32_t w,
     if (r < na) {
         o.src = a_node;
         int32_t pos = filt ? kth_of_two(g.pair + lb1, n1, g.pair + lb2, n2, r) : r;
-        ent = g.off[a_node] + pos;
+        ent = oa0 + pos;
     } else {
         o.src = b_node;
         int32_t rr = r - na;
         int32_t pos = filt ? g.pair[lbb + rr].pos : rr;
-        ent = g.off[b_node] + pos;
+        ent = ob0 + pos;
     }
     const Rec rc = g.rec[ent];
     o.ngh = rc.ngh;
@@ -194,7 +202,13 @@ struct Step2 {
 __device__ __forceinline__ Step2 next_step(const DevGraph &g, Key key, uint32_t ev, uint32_t slot, int32_t M,
                                            int32_t m, int32_t u, int32_t v1, int32_t e1) {
     Step2 o{0, 0, 0, 0.f};
-    const int32_t cu = walk_len(g, u, e1), cv = walk_len(g, v1, e1), tot = cu + cv;
+    // walk_len (graph.py:171-176) for both owners from one EdgeEnds load; offsets loaded alongside
+    const bool vu = u > 0 && u < g.n_nodes, vv = v1 > 0 && v1 < g.n_nodes;
+    const EdgeEnds x1 = (e1 >= 0 && e1 <= g.max_eid) ? g.ends[e1] : EdgeEnds{-1, 0, -1, 0};
+    const int32_t ou = vu ? g.off[u] : 0, ov = vv ? g.off[v1] : 0;
+    const int32_t lu = x1.node_a == u ? x1.len_a : x1.node_b == u ? x1.len_b : -1;
+    const int32_t lv = x1.node_a == v1 ? x1.len_a : x1.node_b == v1 ? x1.len_b : -1;
+    const int32_t cu = (vu && lu > 0) ? lu : 0, cv = (vv && lv > 0) ? lv : 0, tot = cu + cv;
     if (tot == 0) return o;
     uint32_t dv[kMaxM];
 #pragma unroll
@@ -211,10 +225,10 @@ __device__ __forceinline__ Step2 next_step(const DevGraph &g, Key key, uint32_t 
     int32_t ent;
     if (x < cu) {
         o.src = u;
-        ent = g.off[u] + x;
+        ent = ou + x;
     } else {
         o.src = v1;
-        ent = g.off[v1] + (x - cu);
+        ent = ov + (x - cu);
     }
     const Rec rc = g.rec[ent];
     o.ngh = rc.ngh;
@@ -314,19 +328,29 @@ __global__ void __launch_bounds__(256) hist_kernel(const int32_t *__restrict__ a
     if (threadIdx.x < 12 && bins[threadIdx.x]) atomicAdd(&hist[threadIdx.x], (unsigned long long)bins[threadIdx.x]);
 }
 
-// new_edge_info for one group of W walks: eids staged in LDS, each (w,p) counts its id per column q
+// new_edge_info for one group of W walks (eids staged in LDS): thread w counts, for each of its
+// 3 ids, the walks holding that id in column q.  Every thread reads the same walk w2 at a time
+// (LDS broadcast), so a walk costs 3 reads and 9 compares instead of 9 reads per (w, p).
 __device__ __forceinline__ void edge_counts_group(const int32_t *e_lds, int32_t W, float *out) {
-    for (int32_t wp = threadIdx.x; wp < W * 3; wp += blockDim.x) {
-        const int32_t x = e_lds[wp];
-        int32_t c0 = 0, c1 = 0, c2 = 0;
+    for (int32_t w0 = 0; w0 < W; w0 += blockDim.x) {
+        const int32_t w = w0 + threadIdx.x;
+        int32_t x[3], c[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+#pragma unroll
+        for (int p = 0; p < 3; ++p) x[p] = w < W ? e_lds[w * 3 + p] : 0;
         for (int32_t w2 = 0; w2 < W; ++w2) {
-            c0 += e_lds[w2 * 3 + 0] == x;
-            c1 += e_lds[w2 * 3 + 1] == x;
-            c2 += e_lds[w2 * 3 + 2] == x;
+            const int32_t y0 = e_lds[w2 * 3 + 0], y1 = e_lds[w2 * 3 + 1], y2 = e_lds[w2 * 3 + 2];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                c[p][0] += x[p] == y0;
+                c[p][1] += x[p] == y1;
+                c[p][2] += x[p] == y2;
+            }
         }
-        out[wp * 3 + 0] = (float)c0;
-        out[wp * 3 + 1] = (float)c1;
-        out[wp * 3 + 2] = (float)c2;
+        if (w < W)
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) out[(w * 3 + p) * 3 + q] = (float)c[p][q];
     }
 }
 
@@ -411,7 +435,9 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
     const int64_t se = (int64_t)s * a.E + e;
     // ---- hop 1 (one row, N draws), lanes of wave 0
     if (tid < 64) {
-        const int32_t c = find_before_len(g, u, s == 2, a.ts[e], a.eidx ? a.eidx[e] : 0, tid == 0 ? a.err : nullptr);
+        int32_t c;
+        if (s == 2 && u >= 0 && u < g.n_nodes) c = bisect_ts_wave(g, u, a.ts[e]);   // time path, whole wave
+        else c = find_before_len(g, u, s == 2, a.ts[e], a.eidx ? a.eidx[e] : 0, tid == 0 ? a.err : nullptr);
         uint32_t d = 0xFFFFFFFFu;
         if (c > 0 && tid < N) d = (uint32_t)draw(key, 1, ev, 0, tid, c);
         int32_t rank = 0;
