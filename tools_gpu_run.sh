@@ -20,7 +20,7 @@ for s in "$@"; do
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) step bench 600 python bench.py --steps 10 --warmup 2 ;;
         benchq) step bench 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
-        prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+        prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --no-cpu-baseline ;;
         pmc)
             B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline"
             i=0
