@@ -50,6 +50,20 @@ struct __attribute__((aligned(8))) Pair {
     int32_t pos;
 };
 
+// (node, neighbour) -> the block [start, end) of that neighbour's entries in the node's pair-index
+// range: open addressing, linear probing, u = -1 marks an empty slot, capacity a power of two.
+struct __attribute__((aligned(16))) PairBlk {
+    int32_t u, x, start, end;
+};
+
+__host__ __device__ inline uint32_t pblk_hash(int32_t u, int32_t x) {
+    uint32_t h = (uint32_t)u * 0x9E3779B1u ^ ((uint32_t)x + 0x7F4A7C15u) * 0x85EBCA77u;
+    h ^= h >> 15;
+    h *= 0x2C1B3C6Du;
+    h ^= h >> 12;
+    return h;
+}
+
 struct DevGraph {
     int32_t n_nodes;
     int32_t max_eid;
@@ -60,11 +74,16 @@ struct DevGraph {
     const Pair *pair;       // [n_entries]
     const double *ets;      // [max_eid+1] timestamp of each edge id (0 for absent ids)
     int32_t ts_unique;      // every record of an edge id carries the same timestamp
+    const PairBlk *pblk;    // [pblk_mask+1] (node, neighbour) block table
+    uint32_t pblk_mask;
 };
 
 // ------------------------------------------------------------------ Philox4x32-10
-__device__ __forceinline__ uint32_t philox_word(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
-                                                uint32_t k1, uint32_t w) {
+// all four output words of one Philox4x32-10 block
+__device__ __forceinline__ uint4 philox4(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+    // key schedule in VGPRs: with a uniform key the compiler otherwise keeps all 20 round keys of
+    // every key live in SGPRs, which spills the kernels' scalar state through v_readlane
+    asm volatile("" : "+v"(k0), "+v"(k1));
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         if (r) {
@@ -79,7 +98,13 @@ __device__ __forceinline__ uint32_t philox_word(uint32_t c0, uint32_t c1, uint32
         c2 = n2;
         c3 = lo0;
     }
-    return w == 0 ? c0 : w == 1 ? c1 : w == 2 ? c2 : c3;
+    return make_uint4(c0, c1, c2, c3);
+}
+
+__device__ __forceinline__ uint32_t philox_word(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                                uint32_t k1, uint32_t w) {
+    const uint4 r = philox4(c0, c1, c2, c3, k0, k1);
+    return w == 0 ? r.x : w == 1 ? r.y : w == 2 ? r.z : r.w;
 }
 
 struct Key {
@@ -88,6 +113,16 @@ struct Key {
 
 __host__ __device__ inline Key make_key(uint64_t seed, uint32_t split, uint32_t side) {
     return Key{(uint32_t)seed, (uint32_t)(seed >> 32), (split << 16) | (side << 8)};
+}
+
+// the draw of word u for [0, high)
+__device__ __forceinline__ int32_t scale_draw(uint32_t u, uint32_t high) {
+    return (int32_t)(((uint64_t)u * (uint64_t)high) >> 32);
+}
+
+// the four words of block (stage, event, row, j >> 2): draws j = 4*(j>>2) .. +3 of the contract
+__device__ __forceinline__ uint4 draw_block(Key k, uint32_t stage, uint32_t event, uint32_t row, uint32_t jb) {
+    return philox4(event, k.tagbase | stage, row, jb, k.k0, k.k1);
 }
 
 // draw in [0, high) for (stage, event, row, j)
@@ -143,6 +178,7 @@ struct tm_graph {
     tmk::EdgeEnds *d_ends;
     tmk::Pair *d_pair;
     double *d_ets;
+    tmk::PairBlk *d_pblk;
     // host copies (export)
     int64_t *h_off;
     int32_t *h_ngh, *h_eid, *h_dict;

@@ -29,6 +29,7 @@ static void free_graph(tm_graph *g) {
     if (g->d_ends) (void)hipFree(g->d_ends);
     if (g->d_pair) (void)hipFree(g->d_pair);
     if (g->d_ets) (void)hipFree(g->d_ets);
+    if (g->d_pblk) (void)hipFree(g->d_pblk);
     delete[] g->h_off;
     delete[] g->h_ngh;
     delete[] g->h_eid;
@@ -146,6 +147,23 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
     g->h_off[n_nodes] = n;
     off32[n_nodes] = (int32_t)n;
 
+    // (node, neighbour) block table over the pair index, load factor <= 1/2
+    int64_t n_blocks = 0;
+    for (int32_t u = 0; u < n_nodes; ++u)
+        for (int64_t i = off32[u]; i < off32[u + 1]; ++i) n_blocks += (i == off32[u] || pair[i].ngh != pair[i - 1].ngh);
+    uint32_t cap = 16;
+    while ((int64_t)cap < 2 * n_blocks) cap <<= 1;
+    std::vector<PairBlk> pblk(cap, PairBlk{-1, 0, 0, 0});
+    for (int32_t u = 0; u < n_nodes; ++u)
+        for (int64_t i = off32[u]; i < off32[u + 1];) {
+            int64_t j = i + 1;
+            while (j < off32[u + 1] && pair[j].ngh == pair[i].ngh) ++j;
+            uint32_t h = pblk_hash(u, pair[i].ngh) & (cap - 1);
+            while (pblk[h].u != -1) h = (h + 1) & (cap - 1);
+            pblk[h] = PairBlk{u, pair[i].ngh, (int32_t)i, (int32_t)j};
+            i = j;
+        }
+
     int prev = 0;
     if (hipGetDevice(&prev) != hipSuccess) prev = 0;
     if (hipSetDevice(device) != hipSuccess) {
@@ -158,6 +176,8 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
     e = e ? e : hipMalloc(&g->d_ends, sizeof(EdgeEnds) * ends.size());
     e = e ? e : hipMalloc(&g->d_pair, sizeof(Pair) * nn);
     e = e ? e : hipMalloc(&g->d_ets, sizeof(double) * ets.size());
+    e = e ? e : hipMalloc(&g->d_pblk, sizeof(PairBlk) * cap);
+    e = e ? e : hipMemcpy(g->d_pblk, pblk.data(), sizeof(PairBlk) * cap, hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(g->d_ets, ets.data(), sizeof(double) * ets.size(), hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(g->d_off, off32.data(), sizeof(int32_t) * (n_nodes + 1), hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(g->d_rec, rec.data(), sizeof(Rec) * nn, hipMemcpyHostToDevice);
@@ -168,7 +188,8 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
         free_graph(g);
         return fail(TM_E_HIP, std::string("tm_graph_build: ") + hipGetErrorString(e));
     }
-    g->d = DevGraph{n_nodes, max_eid, n, g->d_off, g->d_rec, g->d_ends, g->d_pair, g->d_ets, ts_unique};
+    g->d = DevGraph{n_nodes, max_eid, n, g->d_off, g->d_rec, g->d_ends, g->d_pair, g->d_ets, ts_unique, g->d_pblk,
+                    cap - 1};
     *out = g;
     return TM_OK;
 }

@@ -71,31 +71,63 @@ __device__ __forceinline__ int32_t kth_of_two(const Pair *p1, int32_t n1, const 
     return a > b ? a : b;
 }
 
-// K independent pair_lb searches advanced together: every halving issues all K loads (unconditional,
-// clamped) before any compare, so the K searches cost one round trip per level.
-// [lo, hi) = the owner node's range in the pair index (empty: no search).
+// K (node, neighbour) block lookups in lockstep (u < 0: empty block)
 template <int K>
-__device__ __forceinline__ void pair_lb_multi(const DevGraph &g, int32_t (&lo)[K], int32_t (&hi)[K],
-                                              const int32_t (&x)[K], const int32_t (&p)[K], int32_t (&out)[K]) {
+__device__ __forceinline__ void pair_blocks(const DevGraph &g, const int32_t (&u)[K], const int32_t (&x)[K],
+                                            int32_t (&st)[K], int32_t (&en)[K]) {
+    uint32_t h[K];
+    bool live[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        live[k] = u[k] >= 0;
+        h[k] = pblk_hash(u[k], x[k]) & g.pblk_mask;
+        st[k] = en[k] = 0;
+    }
+    while (true) {
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < K; ++k) any |= live[k];
+        if (!any) break;
+        PairBlk b[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) b[k] = g.pblk[h[k]];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (!live[k]) continue;
+            if (b[k].u == u[k] && b[k].x == x[k]) {
+                st[k] = b[k].start;
+                en[k] = b[k].end;
+                live[k] = false;
+            } else if (b[k].u == -1) {
+                live[k] = false;
+            } else {
+                h[k] = (h[k] + 1) & g.pblk_mask;
+            }
+        }
+    }
+}
+
+// K lower bounds "first entry of [lo, hi) with pos >= p" in lockstep (entries sorted by pos)
+template <int K>
+__device__ __forceinline__ void pos_lb_multi(const DevGraph &g, int32_t (&lo)[K], int32_t (&hi)[K],
+                                             const int32_t (&p)[K]) {
     while (true) {
         bool any = false;
 #pragma unroll
         for (int k = 0; k < K; ++k) any |= lo[k] < hi[k];
         if (!any) break;
-        Pair q[K];
+        int32_t q[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) q[k] = g.pair[lo[k] < hi[k] ? (lo[k] + hi[k]) >> 1 : 0];
+        for (int k = 0; k < K; ++k) q[k] = g.pair[lo[k] < hi[k] ? (lo[k] + hi[k]) >> 1 : 0].pos;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             if (lo[k] < hi[k]) {
                 const int32_t mid = (lo[k] + hi[k]) >> 1;
-                if (q[k].ngh < x[k] || (q[k].ngh == x[k] && q[k].pos < p[k])) lo[k] = mid + 1;
+                if (q[k] < p[k]) lo[k] = mid + 1;
                 else hi[k] = mid;
             }
         }
     }
-#pragma unroll
-    for (int k = 0; k < K; ++k) out[k] = lo[k];
 }
 
 struct Step3 {
@@ -129,20 +161,22 @@ __device__ Step3 final_step(const DevGraph &g, Key key, uint32_t ev, uint32_t w,
     const int32_t cb = !vb ? 0 : x2.node_a == b_node ? x2.len_a : x2.node_b == b_node ? x2.len_b : ob1 - ob0;
     int32_t na, nb, lb1 = 0, n1 = 0, lb2 = 0, n2 = 0, lbb = 0;
     if (filt) {
-        // the six lower bounds of the filtered counts, searched in lockstep (one dependent L2 round
-        // trip per halving for all six instead of six sequential searches)
+        // filtered counts: the (node, neighbour) block of each of the three neighbours from the block
+        // table (its start is the (x, 0) lower bound), then the entries before the cut inside each
+        // block; the three lookups and the three in-block searches each run in lockstep
         const bool sa = ca > 0, sb = cb > 0;
-        int32_t lo[6] = {sa ? oa0 : 0, sa ? oa0 : 0, sa ? oa0 : 0, sa ? oa0 : 0, sb ? ob0 : 0, sb ? ob0 : 0};
-        int32_t hi[6] = {sa ? oa1 : 0, sa ? oa1 : 0, sa ? oa1 : 0, sa ? oa1 : 0, sb ? ob1 : 0, sb ? ob1 : 0};
-        const int32_t xs[6] = {a1, a1, a2, a2, bf, bf}, ps[6] = {0, ca, 0, ca, 0, cb};
-        int32_t lb[6];
-        pair_lb_multi<6>(g, lo, hi, xs, ps, lb);
-        n1 = lb[1] - lb[0];
-        n2 = lb[3] - lb[2];
-        nb = lb[5] - lb[4];
-        lb1 = lb[0];
-        lb2 = lb[2];
-        lbb = lb[4];
+        const int32_t us[3] = {sa ? a_node : -1, sa ? a_node : -1, sb ? b_node : -1}, xs[3] = {a1, a2, bf};
+        int32_t st[3], en[3];
+        pair_blocks<3>(g, us, xs, st, en);
+        int32_t lo[3] = {st[0], st[1], st[2]}, hi[3] = {en[0], en[1], en[2]};
+        const int32_t ps[3] = {ca, ca, cb};
+        pos_lb_multi<3>(g, lo, hi, ps);
+        n1 = lo[0] - st[0];
+        n2 = lo[1] - st[1];
+        nb = lo[2] - st[2];
+        lb1 = st[0];
+        lb2 = st[1];
+        lbb = st[2];
         na = n1 + n2;
     } else {
         na = ca;
@@ -211,8 +245,11 @@ __device__ __forceinline__ Step2 next_step(const DevGraph &g, Key key, uint32_t 
     const int32_t cu = (vu && lu > 0) ? lu : 0, cv = (vv && lv > 0) ? lv : 0, tot = cu + cv;
     if (tot == 0) return o;
     uint32_t dv[kMaxM];
+    const uint4 b0 = draw_block(key, TM_STAGE_STEP2, ev, slot, 0);          // draws 0..3 of the slot
+    const uint4 b1 = M > 4 ? draw_block(key, TM_STAGE_STEP2, ev, slot, 1) : b0;
+    const uint32_t words[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-    for (int k = 0; k < kMaxM; ++k) dv[k] = k < M ? (uint32_t)draw(key, TM_STAGE_STEP2, ev, slot, k, tot) : 0xFFFFFFFFu;
+    for (int k = 0; k < kMaxM; ++k) dv[k] = k < M ? (uint32_t)scale_draw(words[k], tot) : 0xFFFFFFFFu;
     uint32_t sel = 0;
 #pragma unroll
     for (int k = 0; k < kMaxM; ++k) {
@@ -393,6 +430,13 @@ struct EventArgs {
     int32_t *err;
 };
 
+template <class T>
+__device__ __forceinline__ T *vptr(T *p) {
+    uint64_t v = reinterpret_cast<uint64_t>(p);
+    asm volatile("" : "+v"(v));
+    return reinterpret_cast<T *>(v);
+}
+
 // LDS of one (event, side): hop-1 row, hop-2 draws, hop-2 cut lengths, walk edge ids, histogram
 __host__ __device__ inline size_t events_lds_bytes(int32_t N, int32_t M) {
     return sizeof(int32_t) * ((size_t)3 * N + (size_t)N * N + 2 * N + (size_t)N * M * 3 + 12);
@@ -422,6 +466,15 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
     int32_t *c2 = reinterpret_cast<int32_t *>(d2 + N * N), *o2 = c2 + N, *weid = o2 + N;
     unsigned int *bins = reinterpret_cast<unsigned int *>(weid + W * 3);
     const DevGraph &g = a.g;
+    // output pointers live in VGPRs (vptr): kept as uniform SGPR pairs next to the graph and input
+    // pointers they overflow the scalar file and spill through v_readlane in every phase
+    int32_t *const o_dst_fake = vptr(a.dst_fake), *const o_sub1_node = vptr(a.sub1_node),
+                  *const o_sub1_eid = vptr(a.sub1_eid), *const o_sub2_node = vptr(a.sub2_node),
+                  *const o_sub2_eid = vptr(a.sub2_eid), *const o_node6 = vptr(a.node6), *const o_eid3 = vptr(a.eid3),
+                  *const o_cat = vptr(a.cat);
+    float *const o_sub1_ts = vptr(a.sub1_ts), *const o_sub2_ts = vptr(a.sub2_ts), *const o_ts3 = vptr(a.ts3),
+                *const o_cnt = vptr(a.cnt);
+    unsigned long long *const o_hist = vptr(a.hist);
     const int32_t e = blockIdx.x, s = blockIdx.y, tid = threadIdx.x;
     const uint32_t ev = a.event_ids[e];
     const Key key = make_key(a.seed, a.split, (uint32_t)(s + 1));
@@ -431,7 +484,7 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
     if (s == 0) u = a.src[e];
     else if (s == 1) u = a.dst[e];
     else u = a.dst_list[draw(make_key(a.seed, a.split, TM_SIDE_NONE), TM_STAGE_NEG, ev, 0, 1, a.n_dst)];
-    if (s == 2 && tid == 0) a.dst_fake[e] = u;
+    if (s == 2 && tid == 0) o_dst_fake[e] = u;
     const int64_t se = (int64_t)s * a.E + e;
     // ---- hop 1 (one row, N draws), lanes of wave 0
     if (tid < 64) {
@@ -454,9 +507,9 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
                 n_ = rc.ngh; e_ = rc.eid; t_ = (float)rc.ts; slot = rank;
             }
             h1n[slot] = n_; h1e[slot] = e_; h1t[slot] = t_;
-            a.sub1_node[se * N + slot] = n_;
-            a.sub1_eid[se * N + slot] = e_;
-            a.sub1_ts[se * N + slot] = t_;
+            o_sub1_node[se * N + slot] = n_;
+            o_sub1_eid[se * N + slot] = e_;
+            o_sub1_ts[se * N + slot] = t_;
         }
     }
     __syncthreads();
@@ -469,9 +522,17 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
     }
     __syncthreads();
     TM_EST(2);
-    for (int32_t x = tid; x < N * N; x += blockDim.x) {
-        const int32_t j = x / N, k = x % N, c = c2[j];
-        d2[x] = c > 0 ? (uint32_t)draw(key, 2, ev, j, k, c) : 0xFFFFFFFFu;
+    // one Philox block per 4 draws of a row
+    const int32_t NB = (N + 3) >> 2;
+    for (int32_t x = tid; x < N * NB; x += blockDim.x) {
+        const int32_t j = x / NB, kb = x % NB, c = c2[j];
+        const uint4 b = draw_block(key, 2, ev, j, kb);
+        const uint32_t wv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const int32_t k = 4 * kb + w;
+            if (k < N) d2[j * N + k] = c > 0 ? (uint32_t)scale_draw(wv[w], c) : 0xFFFFFFFFu;
+        }
     }
     __syncthreads();
     // 4 rows of draws per lane per round: ranks from LDS, then the 4 record gathers issued together
@@ -502,9 +563,9 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
         for (int u = 0; u < HB; ++u) {
             if (x0 + u * 64 + tid >= N * N) continue;
             const int64_t o = se * N * N + slot[u];
-            a.sub2_node[o] = ok[u] ? rc[u].ngh : 0;
-            a.sub2_eid[o] = ok[u] ? rc[u].eid : 0;
-            a.sub2_ts[o] = ok[u] ? (float)rc[u].ts : 0.f;
+            o_sub2_node[o] = ok[u] ? rc[u].ngh : 0;
+            o_sub2_eid[o] = ok[u] ? rc[u].eid : 0;
+            o_sub2_ts[o] = ok[u] ? (float)rc[u].ts : 0.f;
         }
     }
     TM_EST(3);
@@ -515,18 +576,18 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
         const Step2 s2 = next_step(g, key, ev, j, M, m, u, v1, e1);
         const Step3 s3 = final_step(g, key, ev, w, u, v1, s2.src, s2.ngh, s2.eid);
         const int64_t o = se * W + w;
-        int32_t *nd = a.node6 + o * 6;
+        int32_t *nd = o_node6 + o * 6;
         nd[0] = s3.src; nd[1] = s3.ngh; nd[2] = s2.src; nd[3] = s2.ngh; nd[4] = u; nd[5] = v1;
-        a.eid3[o * 3 + 0] = s3.eid; a.eid3[o * 3 + 1] = s2.eid; a.eid3[o * 3 + 2] = e1;
-        a.ts3[o * 3 + 0] = s3.ts; a.ts3[o * 3 + 1] = s2.ts; a.ts3[o * 3 + 2] = h1t[j];
+        o_eid3[o * 3 + 0] = s3.eid; o_eid3[o * 3 + 1] = s2.eid; o_eid3[o * 3 + 2] = e1;
+        o_ts3[o * 3 + 0] = s3.ts; o_ts3[o * 3 + 1] = s2.ts; o_ts3[o * 3 + 2] = h1t[j];
         const int32_t c = cat_of(s3.code, s3.t, 0);
-        a.cat[o] = c;
+        o_cat[o] = c;
         if (c >= 0) atomicAdd(&bins[c], 1u);
         weid[w * 3 + 0] = s3.eid; weid[w * 3 + 1] = s2.eid; weid[w * 3 + 2] = e1;
     }
     __syncthreads();
     TM_EST(4);
-    edge_counts_group(weid, W, a.cnt + se * W * 9);
+    edge_counts_group(weid, W, o_cnt + se * W * 9);
     TM_EST(5);
 #ifdef TM_STAMPS
     if (tid == 0 && e >= 2000 && e < 4000) {
@@ -534,7 +595,7 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
         atomicAdd(&g_est[7], 1ull);
     }
 #endif
-    if (tid < 12 && bins[tid]) atomicAdd(&a.hist[tid], (unsigned long long)bins[tid]);
+    if (tid < 12 && bins[tid]) atomicAdd(&o_hist[tid], (unsigned long long)bins[tid]);
 }
 
 }  // namespace tmk
