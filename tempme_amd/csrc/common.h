@@ -11,6 +11,9 @@ namespace tmk {
 void set_error(const std::string &msg);
 int fail(int code, const std::string &msg);
 
+// library-internal device scratch per (device, stream), grown on demand (scratch.cpp); nullptr on failure
+void *scratch(size_t bytes, hipStream_t stream);
+
 // per-kernel HIP-event timing (prof.cpp); no-ops unless tm_profile_enable(1)
 hipEvent_t prof_begin(hipStream_t s);
 void prof_end(const char *name, hipStream_t s, hipEvent_t a);

@@ -352,7 +352,7 @@ __global__ void perm_keys_kernel(Key key, int64_t n, uint32_t *__restrict__ out)
 }
 
 __global__ void __launch_bounds__(256) hist_kernel(const int32_t *__restrict__ anony3, int64_t n, int null_order,
-                                                   int32_t *__restrict__ cat, unsigned long long *__restrict__ hist) {
+                                                   int32_t *__restrict__ cat, uint32_t *__restrict__ bins_out) {
     __shared__ unsigned int bins[12];
     if (threadIdx.x < 12) bins[threadIdx.x] = 0;
     __syncthreads();
@@ -362,7 +362,7 @@ __global__ void __launch_bounds__(256) hist_kernel(const int32_t *__restrict__ a
         if (c >= 0) atomicAdd(&bins[c], 1u);
     }
     __syncthreads();
-    if (threadIdx.x < 12 && bins[threadIdx.x]) atomicAdd(&hist[threadIdx.x], (unsigned long long)bins[threadIdx.x]);
+    if (threadIdx.x < 12) bins_out[blockIdx.x * 12 + threadIdx.x] = bins[threadIdx.x];   // hist_reduce_kernel
 }
 
 // new_edge_info for one group of W walks (eids staged in LDS): thread w counts, for each of its
@@ -427,6 +427,7 @@ struct EventArgs {
     int32_t *cat;
     float *cnt;
     unsigned long long *hist;
+    uint32_t *bins_out;     // [3 * E][12] per-(event, side) motif bins, reduced by hist_reduce_kernel
     int32_t *err;
 };
 
@@ -435,6 +436,32 @@ __device__ __forceinline__ T *vptr(T *p) {
     uint64_t v = reinterpret_cast<uint64_t>(p);
     asm volatile("" : "+v"(v));
     return reinterpret_cast<T *>(v);
+}
+
+// hist[k] += sum over the n_groups rows of bins[row][k].  252 threads (21 per category) stride over
+// the flat array by a multiple of 12, so each thread always sums one category; one atomic per
+// category per workgroup.
+constexpr int kReduceThreads = 252;
+
+__global__ void __launch_bounds__(kReduceThreads) hist_reduce_kernel(const uint32_t *__restrict__ bins,
+                                                                     int64_t n_groups,
+                                                                     unsigned long long *__restrict__ hist) {
+    __shared__ unsigned long long red[kReduceThreads];
+    unsigned long long acc = 0;
+    const int64_t n = n_groups * 12;
+    for (int64_t i = (int64_t)blockIdx.x * kReduceThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kReduceThreads)
+        acc += bins[i];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x < 12) {
+        unsigned long long t = 0;
+        for (int j = threadIdx.x; j < kReduceThreads; j += 12) t += red[j];
+        if (t) atomicAdd(&hist[threadIdx.x], t);
+    }
+}
+
+static inline unsigned reduce_blocks(int64_t n_groups) {
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>(64, (n_groups * 12 + 4095) / 4096));
 }
 
 // LDS of one (event, side): hop-1 row, hop-2 draws, hop-2 cut lengths, walk edge ids, histogram
@@ -474,7 +501,7 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
                   *const o_cat = vptr(a.cat);
     float *const o_sub1_ts = vptr(a.sub1_ts), *const o_sub2_ts = vptr(a.sub2_ts), *const o_ts3 = vptr(a.ts3),
                 *const o_cnt = vptr(a.cnt);
-    unsigned long long *const o_hist = vptr(a.hist);
+    uint32_t *const o_bins = vptr(a.bins_out);
     const int32_t e = blockIdx.x, s = blockIdx.y, tid = threadIdx.x;
     const uint32_t ev = a.event_ids[e];
     const Key key = make_key(a.seed, a.split, (uint32_t)(s + 1));
@@ -595,7 +622,9 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
         atomicAdd(&g_est[7], 1ull);
     }
 #endif
-    if (tid < 12 && bins[tid]) atomicAdd(&o_hist[tid], (unsigned long long)bins[tid]);
+    // per-(event, side) bins, summed by hist_reduce_kernel: 12 same-address device-scope atomics from
+    // each of the 3E workgroups serialized on one line and cost the kernel 40 % of its time
+    if (tid < 12) o_bins[se * 12 + tid] = bins[tid];
 }
 
 }  // namespace tmk
@@ -685,7 +714,11 @@ extern "C" int tm_motif_hist(const int32_t *anony3, int64_t n, int32_t null_orde
     if (n == 0) return TM_OK;
     if (!anony3) return fail(TM_E_ARG, "tm_motif_hist: NULL anony");
     const int64_t blocks = std::min<int64_t>((n + 255) / 256, 2048);
-    hist_kernel<<<dim3((unsigned)blocks), 256, 0, S(stream)>>>(anony3, n, null_order, out_cat, hist12);
+    uint32_t *bins = static_cast<uint32_t *>(scratch(sizeof(uint32_t) * 12 * (size_t)blocks, S(stream)));
+    if (!bins) return fail(TM_E_HIP, "tm_motif_hist: scratch allocation failed");
+    hist_kernel<<<dim3((unsigned)blocks), 256, 0, S(stream)>>>(anony3, n, null_order, out_cat, bins);
+    TM_CHECK_LAUNCH();
+    hist_reduce_kernel<<<dim3(reduce_blocks(blocks)), kReduceThreads, 0, S(stream)>>>(bins, blocks, hist12);
     TM_CHECK_LAUNCH();
     return TM_OK;
 }
@@ -714,13 +747,20 @@ extern "C" int tm_sample_events(const tm_graph *g, uint64_t seed, uint32_t split
     if (!src || !dst || !ts || !eidx || !event_ids || !dst_list || !dst_fake || !sub1_node || !sub1_eid ||
         !sub1_ts || !sub2_node || !sub2_eid || !sub2_ts || !node6 || !eid3 || !ts3 || !cat || !cnt || !hist12)
         return fail(TM_E_ARG, "tm_sample_events: NULL pointer");
+    uint32_t *bins = static_cast<uint32_t *>(scratch(sizeof(uint32_t) * 12 * 3 * (size_t)n_events, S(stream)));
+    if (!bins) return fail(TM_E_HIP, "tm_sample_events: scratch allocation failed");
     EventArgs a{g->d,     seed,     split,     N,         M,        n_events, src,  dst,   eidx, ts,     event_ids,
                 dst_list, (uint32_t)n_dst, dst_fake, sub1_node, sub1_eid, sub1_ts, sub2_node, sub2_eid, sub2_ts,
-                node6,    eid3,     ts3,       cat,       cnt,      hist12,   err_flag};
+                node6,    eid3,     ts3,       cat,       cnt,      hist12,   bins,     err_flag};
     hipEvent_t pe = prof_begin(S(stream));
     events_kernel<<<dim3(n_events, 3), 64, events_lds_bytes(N, M), S(stream)>>>(a);
     TM_CHECK_LAUNCH();
     prof_end("events_kernel", S(stream), pe);
+    pe = prof_begin(S(stream));
+    hist_reduce_kernel<<<dim3(reduce_blocks(3 * (int64_t)n_events)), kReduceThreads, 0, S(stream)>>>(
+        bins, 3 * (int64_t)n_events, hist12);
+    TM_CHECK_LAUNCH();
+    prof_end("hist_reduce_kernel", S(stream), pe);
     return TM_OK;
 }
 

@@ -5,10 +5,10 @@ set -e
 cd "$(dirname "$0")"
 name=$1; enc=$2
 out=ab_src/$name; mkdir -p "$out" tempme_amd/lib/ab
-cp tempme_amd/csrc/*.h tempme_amd/csrc/graph.cpp tempme_amd/csrc/prof.cpp tempme_amd/csrc/sampler.hip "$out/"
+cp tempme_amd/csrc/*.h tempme_amd/csrc/*.cpp tempme_amd/csrc/sampler.hip "$out/"
 cp "$enc" "$out/encoder.hip"
 F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -mcode-object-version=5 -Wno-unused-result -Iinclude $EXTRA"
-for s in graph.cpp prof.cpp sampler.hip encoder.hip; do /opt/rocm/bin/hipcc $F -x hip -c "$out/$s" -o "$out/$s.o" & done
+for s in $(cd "$out" && ls *.cpp *.hip); do /opt/rocm/bin/hipcc $F -x hip -c "$out/$s" -o "$out/$s.o" & done
 wait
 /opt/rocm/bin/hipcc $F -shared -o "tempme_amd/lib/ab/$name.so" "$out"/*.o
 rm -rf "$out"; rmdir ab_src 2>/dev/null || true
