@@ -374,6 +374,7 @@ __device__ __forceinline__ void edge_counts_group(const int32_t *e_lds, int32_t 
         int32_t x[3], c[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
 #pragma unroll
         for (int p = 0; p < 3; ++p) x[p] = w < W ? e_lds[w * 3 + p] : 0;
+#pragma unroll 4
         for (int32_t w2 = 0; w2 < W; ++w2) {
             const int32_t y0 = e_lds[w2 * 3 + 0], y1 = e_lds[w2 * 3 + 1], y2 = e_lds[w2 * 3 + 2];
 #pragma unroll
@@ -566,22 +567,31 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
     // (unconditional, index 0 when the row is empty) before any output is stored
     constexpr int HB = 4;
     for (int32_t x0 = 0; x0 < N * N; x0 += HB * 64) {
-        int32_t slot[HB], idx[HB];
+        int32_t slot[HB], idx[HB], jr[HB], kr[HB], rank[HB];
+        uint32_t dr[HB];
         bool ok[HB];
 #pragma unroll
         for (int u = 0; u < HB; ++u) {
             const int32_t x = x0 + u * 64 + tid;
-            const int32_t j = x < N * N ? x / N : 0, k = x % N, c = x < N * N ? c2[j] : 0;
-            const uint32_t d = x < N * N ? d2[x] : 0u;
-            int32_t rank = 0;
-            if (c > 0)
-                for (int32_t i = 0; i < N; ++i) {
-                    const uint32_t di = d2[j * N + i];
-                    rank += (di < d) || (i < k && di == d);
-                }
+            jr[u] = x < N * N ? x / N : 0;
+            kr[u] = x % N;
+            dr[u] = x < N * N ? d2[x] : 0u;
+            rank[u] = 0;
+        }
+        // the 4 rows' comparisons interleaved, 4 columns per iteration: 16 LDS reads in flight
+#pragma unroll 4
+        for (int32_t i = 0; i < N; ++i)
+#pragma unroll
+            for (int u = 0; u < HB; ++u) {
+                const uint32_t di = d2[jr[u] * N + i];
+                rank[u] += (di < dr[u]) || (i < kr[u] && di == dr[u]);
+            }
+#pragma unroll
+        for (int u = 0; u < HB; ++u) {
+            const int32_t x = x0 + u * 64 + tid, c = x < N * N ? c2[jr[u]] : 0;
             ok[u] = c > 0 && g.n_entries > 0;
-            slot[u] = c > 0 ? j * N + rank : x;
-            idx[u] = ok[u] ? o2[j] + (int32_t)d : 0;
+            slot[u] = c > 0 ? jr[u] * N + rank[u] : x;
+            idx[u] = ok[u] ? o2[jr[u]] + (int32_t)dr[u] : 0;
         }
         Rec rc[HB];
 #pragma unroll
