@@ -233,16 +233,24 @@ struct Step2 {
     float ts;
 };
 
-__device__ __forceinline__ Step2 next_step(const DevGraph &g, Key key, uint32_t ev, uint32_t slot, int32_t M,
-                                           int32_t m, int32_t u, int32_t v1, int32_t e1) {
-    Step2 o{0, 0, 0, 0.f};
-    // walk_len (graph.py:171-176) for both owners from one EdgeEnds load; offsets loaded alongside
+// candidate cut lengths and record offsets of step 2 for one hop-1 slot (shared by its M walks):
+// walk_len (graph.py:171-176) of root u and of v1 from one EdgeEnds load
+struct Step2Cuts {
+    int32_t cu, cv, ou, ov;
+};
+
+__device__ __forceinline__ Step2Cuts step2_cuts(const DevGraph &g, int32_t u, int32_t v1, int32_t e1) {
     const bool vu = u > 0 && u < g.n_nodes, vv = v1 > 0 && v1 < g.n_nodes;
     const EdgeEnds x1 = (e1 >= 0 && e1 <= g.max_eid) ? g.ends[e1] : EdgeEnds{-1, 0, -1, 0};
-    const int32_t ou = vu ? g.off[u] : 0, ov = vv ? g.off[v1] : 0;
     const int32_t lu = x1.node_a == u ? x1.len_a : x1.node_b == u ? x1.len_b : -1;
     const int32_t lv = x1.node_a == v1 ? x1.len_a : x1.node_b == v1 ? x1.len_b : -1;
-    const int32_t cu = (vu && lu > 0) ? lu : 0, cv = (vv && lv > 0) ? lv : 0, tot = cu + cv;
+    return Step2Cuts{(vu && lu > 0) ? lu : 0, (vv && lv > 0) ? lv : 0, vu ? g.off[u] : 0, vv ? g.off[v1] : 0};
+}
+
+__device__ __forceinline__ Step2 next_step(const DevGraph &g, Key key, uint32_t ev, uint32_t slot, int32_t M,
+                                           int32_t m, int32_t u, int32_t v1, const Step2Cuts &sc) {
+    Step2 o{0, 0, 0, 0.f};
+    const int32_t cu = sc.cu, cv = sc.cv, ou = sc.ou, ov = sc.ov, tot = cu + cv;
     if (tot == 0) return o;
     uint32_t dv[kMaxM];
     const uint4 b0 = draw_block(key, TM_STAGE_STEP2, ev, slot, 0);          // draws 0..3 of the slot
@@ -327,7 +335,7 @@ __global__ void __launch_bounds__(256) walks_kernel(DevGraph g, Key key, int32_t
     const uint32_t ev = event_ids[b];
     const int32_t u = root[b], v1 = h1n[b * N + j], e1 = h1e[b * N + j];
     const float t1 = h1t[b * N + j];
-    const Step2 s2 = next_step(g, key, ev, j, M, m, u, v1, e1);
+    const Step2 s2 = next_step(g, key, ev, j, M, m, u, v1, step2_cuts(g, u, v1, e1));
     const Step3 s3 = final_step(g, key, ev, w, u, v1, s2.src, s2.ngh, s2.eid);
     int32_t *nd = node6 + i * 6;
     nd[0] = s3.src; nd[1] = s3.ngh; nd[2] = s2.src; nd[3] = s2.ngh; nd[4] = u; nd[5] = v1;
@@ -467,7 +475,8 @@ static inline unsigned reduce_blocks(int64_t n_groups) {
 
 // LDS of one (event, side): hop-1 row, hop-2 draws, hop-2 cut lengths, walk edge ids, histogram
 __host__ __device__ inline size_t events_lds_bytes(int32_t N, int32_t M) {
-    return sizeof(int32_t) * ((size_t)3 * N + (size_t)N * N + 2 * N + (size_t)N * M * 3 + 12);
+    return sizeof(int32_t) * ((size_t)3 * N + (size_t)N * N + 2 * N + (size_t)N * M * 3 + 12) +
+           sizeof(Step2Cuts) * (size_t)N;
 }
 
 // Phase timing (debug builds only, -DTM_STAMPS): s_memtime deltas of lane 0 for events 2000..3999
@@ -493,6 +502,7 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
     uint32_t *d2 = reinterpret_cast<uint32_t *>(h1e + 2 * N);
     int32_t *c2 = reinterpret_cast<int32_t *>(d2 + N * N), *o2 = c2 + N, *weid = o2 + N;
     unsigned int *bins = reinterpret_cast<unsigned int *>(weid + W * 3);
+    Step2Cuts *s2c = reinterpret_cast<Step2Cuts *>(bins + 12);
     const DevGraph &g = a.g;
     // output pointers live in VGPRs (vptr): kept as uniform SGPR pairs next to the graph and input
     // pointers they overflow the scalar file and spill through v_readlane in every phase
@@ -547,6 +557,7 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
         c2[tid] = find_before_len(g, h1n[tid], false, 0.0, h1e[tid], a.err);
         const int32_t v = h1n[tid];
         o2[tid] = (v >= 0 && v < g.n_nodes) ? g.off[v] : 0;   // record offset of the hop-2 row's node
+        s2c[tid] = step2_cuts(g, u, v, h1e[tid]);            // step 2 of the slot's M walks
     }
     __syncthreads();
     TM_EST(2);
@@ -610,7 +621,7 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
     for (int32_t w = tid; w < W; w += blockDim.x) {
         const int32_t j = w / M, m = w % M;
         const int32_t v1 = h1n[j], e1 = h1e[j];
-        const Step2 s2 = next_step(g, key, ev, j, M, m, u, v1, e1);
+        const Step2 s2 = next_step(g, key, ev, j, M, m, u, v1, s2c[j]);
         const Step3 s3 = final_step(g, key, ev, w, u, v1, s2.src, s2.ngh, s2.eid);
         const int64_t o = se * W + w;
         int32_t *nd = o_node6 + o * 6;
