@@ -53,6 +53,53 @@ def flops_model(de, dn, h, N, M):
                 per_walk=2 * (3 * per_pos_gcn + per_walk_head + 3 * per_pos_gate), W=W)
 
 
+def khop_bytes_per_event(N):
+    """SURVEY.md §8(d) compulsory traffic of the k-hop kernel (a1-a4) alone, per target event (3 sides)."""
+    return 3 * ((N + N * N) * 16 + (N + N * N) * 12 + (1 + N) * 32)
+
+
+def khop_alone(pipe, inputs, steps, N):
+    """The (a) kernel measured alone (the >= 50 % HBM target applies to it): 2-hop
+    sampling of the three sides of the same events through tm_sample_khop (src and dst on the e_idx
+    path, the pipeline's fake dst on the time path), HIP-event timed per call."""
+    from tempme_amd import _lib as L
+    g = pipe.graph
+    E = int(inputs[0][0].numel())
+    dev = inputs[0][0].device
+    tot = E * (N + N * N)
+    on = torch.empty(tot, dtype=torch.int32, device=dev)
+    oe = torch.empty_like(on)
+    ot = torch.empty(tot, dtype=torch.float32, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    st = L.stream_ptr(dev)
+
+    def one(src, dst, ts, eidx, ev):
+        pipe.sample(src, dst, ts, eidx, ev)          # fake dst of these events (not timed below)
+        fake = pipe.buf.dst_fake
+        sides = ((L.SIDE_SRC, src, eidx), (L.SIDE_TGT, dst, eidx), (L.SIDE_BGD, fake, None))
+        return sides
+
+    plans = [one(*inp) for inp in inputs[:steps]]
+    torch.cuda.synchronize()
+    L.profile_enable(True)
+    for k, sides in enumerate(plans):
+        _, _, ts, _, ev = inputs[k]
+        for side, root, ei in sides:
+            L.check(L.lib().tm_sample_khop(g.handle, L.TmRng(pipe.seed, pipe.split, side), 2, N, E, L.ptr(root),
+                                           L.ptr(ts), L.ptr(ei), L.ptr(ev), L.ptr(on), L.ptr(oe), L.ptr(ot),
+                                           L.ptr(err), st), "tm_sample_khop")
+    torch.cuda.synchronize()
+    prof = L.profile_read()
+    L.profile_enable(False)
+    L.raise_device_error(int(err.item()), "khop_alone")
+    ms, cnt = prof["khop_kernel"]
+    per_step_ms = ms / len(plans)
+    ach = khop_bytes_per_event(N) * E / (per_step_ms * 1e-3) / 1e9
+    return {"kernel": "khop_kernel (tm_sample_khop, 2 hops x 3 sides)", "avg_ms": round(per_step_ms, 4),
+            "launches": cnt, "bound": "hbm", "achieved": round(ach, 1), "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_event": khop_bytes_per_event(N)}
+
+
 def sampling_bytes_per_event(N, M):
     """SURVEY.md §8(d) compulsory-traffic model for (a)+(b), per target event (3 sides)."""
     W = N * M
@@ -219,6 +266,7 @@ def main():
                           "events_per_step_per_gpu": E, "parallelism": f"dp{world} (whole batches per rank)"},
                "roofline": roof, "kernels": kernels,
                "sampling_roofline": kernels.get("events_kernel")}
+        out["khop_roofline"] = khop_alone(pipe, inputs, min(args.steps, 5), N)
         if world == 1 and not args.no_cpu_baseline:
             sd = {k: v.detach().cpu() for k, v in ex.state_dict().items()}
             out["cpu_baseline"] = cpu_baseline(g, rows, (src, dst, ts, eidx), pool, N, M, B, args.seed, sd)

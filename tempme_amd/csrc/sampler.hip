@@ -282,42 +282,76 @@ __device__ __forceinline__ Step2 next_step(const DevGraph &g, Key key, uint32_t 
     return o;
 }
 
-// ------------------------------------------------------------------ k-hop: one row per L-lane group
-// Each lane j < N draws one index; its slot in the np.sort order is its rank among the
-// row's draws (ties by lane), found with shuffles inside the group.
-template <int L>
+// ------------------------------------------------------------------ k-hop: one Philox block per thread
+// A workgroup takes R = 256 / NB rows (NB = ceil(N/4) Philox blocks per row).  Each thread computes
+// ONE Philox block = 4 consecutive draws of its row (the contract's counter (row, j>>2), word j&3),
+// so a wave covers 256 draws instead of 64 lanes x 1; the row's cut length and record offset are
+// looked up once per row, the draws go to LDS, and each thread ranks its 4 draws against the row
+// (np.sort order, ties by draw index) and gathers their records.
 __global__ void __launch_bounds__(256) khop_kernel(DevGraph g, Key key, uint32_t stage, int32_t N, int64_t rows,
                                                    int64_t rows_per_event, const int32_t *__restrict__ root,
                                                    const double *__restrict__ cut, const int32_t *__restrict__ eidx,
-                                                   int time_path, const float *__restrict__ tin,
-                                                   const uint32_t *__restrict__ event_ids, int32_t *__restrict__ on,
-                                                   int32_t *__restrict__ oe, float *__restrict__ ot, int32_t *err) {
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t r = gid / L;
-    const int j = threadIdx.x & (L - 1);
-    if (r >= rows) return;
-    const int32_t u = root[r];
-    const int32_t c = find_before_len(g, u, time_path, time_path ? cut[r] : 0.0, time_path ? 0 : eidx[r], j == 0 ? err : nullptr);
-    (void)tin;
-    uint32_t d = 0xFFFFFFFFu;
-    if (c > 0 && j < N) d = (uint32_t)draw(key, stage, event_ids[r / rows_per_event], (uint32_t)(r % rows_per_event), j, c);
-    int32_t rank = 0;
-    for (int k = 0; k < N; ++k) {
-        uint32_t dk = __shfl(d, k, L);
-        rank += (dk < d) || (k < j && dk == d);
+                                                   int time_path, const uint32_t *__restrict__ event_ids,
+                                                   int32_t *__restrict__ on, int32_t *__restrict__ oe,
+                                                   float *__restrict__ ot, int32_t *err) {
+    extern __shared__ uint32_t kh_lds[];
+    const int32_t NB = (N + 3) >> 2, R = 256 / NB;
+    int32_t *rc = reinterpret_cast<int32_t *>(kh_lds), *ro = rc + R;   // per row: cut length, record offset
+    uint32_t *dd = kh_lds + 2 * R;                                     // [R][N] draws
+    const int64_t r0 = (int64_t)blockIdx.x * R;
+    const int tid = threadIdx.x;
+    if (tid < R) {
+        const int64_t r = r0 + tid;
+        int32_t c = 0, o = 0;
+        if (r < rows) {
+            const int32_t u = root[r];
+            c = find_before_len(g, u, time_path, time_path ? cut[r] : 0.0, time_path ? 0 : eidx[r], err);
+            o = (c > 0) ? g.off[u] : 0;
+        }
+        rc[tid] = c;
+        ro[tid] = o;
     }
-    if (j >= N) return;
-    const int64_t o = r * N + rank;
-    if (c == 0) {
-        on[r * N + j] = 0;
-        oe[r * N + j] = 0;
-        ot[r * N + j] = 0.f;
-        return;
+    __syncthreads();
+    const int32_t lr = tid / NB, kb = tid % NB;
+    const int64_t r = r0 + lr;
+    const bool act = lr < R && r < rows;
+    uint32_t d[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    int32_t c = 0;
+    if (act) {
+        c = rc[lr];
+        if (c > 0) {
+            const uint4 b = draw_block(key, stage, event_ids[r / rows_per_event], (uint32_t)(r % rows_per_event), kb);
+            d[0] = scale_draw(b.x, c);
+            d[1] = scale_draw(b.y, c);
+            d[2] = scale_draw(b.z, c);
+            d[3] = scale_draw(b.w, c);
+        }
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+            if (4 * kb + w < N) dd[lr * N + 4 * kb + w] = d[w];
     }
-    const Rec rc = g.rec[g.off[u] + (int32_t)d];
-    on[o] = rc.ngh;
-    oe[o] = rc.eid;
-    ot[o] = (float)rc.ts;
+    __syncthreads();
+    if (!act) return;
+    int32_t rank[4] = {0, 0, 0, 0};
+    if (c > 0)
+        for (int32_t i = 0; i < N; ++i) {
+            const uint32_t di = dd[lr * N + i];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) rank[w] += (di < d[w]) || (i < 4 * kb + w && di == d[w]);
+        }
+    Rec rec[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+        rec[w] = (c > 0 && 4 * kb + w < N) ? g.rec[ro[lr] + (int32_t)d[w]] : Rec{0, 0, 0.0};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const int32_t k = 4 * kb + w;
+        if (k >= N) break;
+        const int64_t o = r * N + (c > 0 ? rank[w] : k);
+        on[o] = rec[w].ngh;
+        oe[o] = rec[w].eid;
+        ot[o] = (float)rec[w].ts;
+    }
 }
 
 // ------------------------------------------------------------------ walks: one thread per walk
@@ -663,23 +697,18 @@ extern "C" int tm_sample_khop(const tm_graph *g, tm_rng rng, int32_t k, int32_t 
     if (!root || !event_ids || !out_node || !out_eid || !out_ts || (!eidx && !cut))
         return fail(TM_E_ARG, "tm_sample_khop: NULL pointer");
     const Key key = make_key(rng.seed, rng.split, rng.side);
+    hipEvent_t pe = prof_begin(S(stream));
     int64_t rows = B, rpe = 1, off = 0;
     const int32_t *rn = root, *re = eidx;
     for (int32_t h = 1; h <= k; ++h) {
         const bool tp = (h == 1 && eidx == nullptr);
         int32_t *on = out_node + off, *oe = out_eid + off;
         float *ot = out_ts + off;
-        const int L = N <= 8 ? 8 : N <= 16 ? 16 : N <= 32 ? 32 : 64;
-        const int64_t threads = rows * L;
-        const dim3 grid((unsigned)((threads + 255) / 256));
-#define KH(LL)                                                                                                  \
-    khop_kernel<LL><<<grid, 256, 0, S(stream)>>>(g->d, key, (uint32_t)h, N, rows, rpe, rn, cut, re, tp ? 1 : 0, \
-                                                 nullptr, event_ids, on, oe, ot, err_flag)
-        if (L == 8) KH(8);
-        else if (L == 16) KH(16);
-        else if (L == 32) KH(32);
-        else KH(64);
-#undef KH
+        const int32_t NB = (N + 3) / 4, R = 256 / NB;
+        const dim3 grid((unsigned)((rows + R - 1) / R));
+        const size_t lds = sizeof(uint32_t) * ((size_t)2 * R + (size_t)R * N);
+        khop_kernel<<<grid, 256, lds, S(stream)>>>(g->d, key, (uint32_t)h, N, rows, rpe, rn, cut, re, tp ? 1 : 0,
+                                                   event_ids, on, oe, ot, err_flag);
         TM_CHECK_LAUNCH();
         rn = on;
         re = oe;
@@ -688,6 +717,7 @@ extern "C" int tm_sample_khop(const tm_graph *g, tm_rng rng, int32_t k, int32_t 
         rpe *= N;
         if (rows > ((int64_t)1 << 40)) return fail(TM_E_UNSUPPORTED, "tm_sample_khop: too many rows");
     }
+    prof_end("khop_kernel", S(stream), pe);   // all hops of one call
     return TM_OK;
 }
 
