@@ -355,6 +355,131 @@ __global__ void __launch_bounds__(256) khop_kernel(DevGraph g, Key key, uint32_t
 }
 
 // ------------------------------------------------------------------ walks: one thread per walk
+// ------------------------------------------------------------------ 2-hop fused: hop 1 and hop 2 in one launch
+// find_k_hop(2, ...) as the reference calls it: a workgroup takes EPB roots, samples their hop-1 rows
+// (kept in LDS), looks up the hop-2 rows' cut lengths and offsets once per row, then draws, ranks and
+// gathers the EPB*N hop-2 rows -- one launch, and no hop-1 -> hop-2 round trip through HBM.
+// Same Philox-block-per-thread scheme as khop_kernel.
+__host__ __device__ inline int32_t khop2_epb(int32_t N) {
+    const int32_t e = 4096 / (N * N);
+    return e < 1 ? 1 : e > 8 ? 8 : e;
+}
+
+__host__ __device__ inline size_t khop2_lds_bytes(int32_t N) {
+    const size_t epb = khop2_epb(N), rows2 = epb * N;
+    return sizeof(int32_t) * (3 * epb + epb * N + 2 * rows2 + 2 * rows2 + rows2 * N);
+}
+
+// one level: ranks of thread (row lr, block kb)'s 4 draws among the row's N draws in dd, then the
+// record gathers and the stores at (row base + rank)
+__device__ __forceinline__ void khop_emit(const DevGraph &g, int32_t N, const uint32_t *dd, int32_t lr, int32_t kb,
+                                          const uint32_t (&d)[4], int32_t c, int32_t o, int64_t obase,
+                                          int32_t *__restrict__ on, int32_t *__restrict__ oe,
+                                          float *__restrict__ ot, int32_t *h_n, int32_t *h_e) {
+    int32_t rank[4] = {0, 0, 0, 0};
+    if (c > 0)
+        for (int32_t i = 0; i < N; ++i) {
+            const uint32_t di = dd[lr * N + i];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) rank[w] += (di < d[w]) || (i < 4 * kb + w && di == d[w]);
+        }
+    Rec rec[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) rec[w] = (c > 0 && 4 * kb + w < N) ? g.rec[o + (int32_t)d[w]] : Rec{0, 0, 0.0};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const int32_t k = 4 * kb + w;
+        if (k >= N) break;
+        const int32_t slot = c > 0 ? rank[w] : k;
+        on[obase + slot] = rec[w].ngh;
+        oe[obase + slot] = rec[w].eid;
+        ot[obase + slot] = (float)rec[w].ts;
+        if (h_n) {
+            h_n[lr * N + slot] = rec[w].ngh;
+            h_e[lr * N + slot] = rec[w].eid;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t N, int32_t B,
+                                                    const int32_t *__restrict__ root, const double *__restrict__ cut,
+                                                    const int32_t *__restrict__ eidx,
+                                                    const uint32_t *__restrict__ event_ids, int32_t *__restrict__ on,
+                                                    int32_t *__restrict__ oe, float *__restrict__ ot, int32_t *err) {
+    extern __shared__ uint32_t k2_lds[];
+    const int32_t EPB = khop2_epb(N), NB = (N + 3) >> 2, R2 = EPB * N;
+    int32_t *c1 = reinterpret_cast<int32_t *>(k2_lds), *o1 = c1 + EPB;
+    uint32_t *ev1 = reinterpret_cast<uint32_t *>(o1 + EPB), *d1 = ev1 + EPB;
+    int32_t *h1n = reinterpret_cast<int32_t *>(d1 + EPB * N), *h1e = h1n + R2, *c2 = h1e + R2, *o2 = c2 + R2;
+    uint32_t *d2 = reinterpret_cast<uint32_t *>(o2 + R2);
+    const int32_t e0 = blockIdx.x * EPB, ne = min(EPB, B - e0), tid = threadIdx.x;
+    const bool time_path = eidx == nullptr;
+    // hop-1 rows
+    if (tid < ne) {
+        const int32_t u = root[e0 + tid];
+        const int32_t c = find_before_len(g, u, time_path, time_path ? cut[e0 + tid] : 0.0,
+                                          time_path ? 0 : eidx[e0 + tid], err);
+        c1[tid] = c;
+        o1[tid] = c > 0 ? g.off[u] : 0;
+        ev1[tid] = event_ids[e0 + tid];
+    }
+    __syncthreads();
+    if (tid < ne * NB) {
+        const int32_t lr = tid / NB, kb = tid % NB, c = c1[lr];
+        uint32_t d[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+        if (c > 0) {
+            const uint4 b = draw_block(key, 1, ev1[lr], 0, kb);
+            d[0] = scale_draw(b.x, c);
+            d[1] = scale_draw(b.y, c);
+            d[2] = scale_draw(b.z, c);
+            d[3] = scale_draw(b.w, c);
+        }
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+            if (4 * kb + w < N) d1[lr * N + 4 * kb + w] = d[w];
+    }
+    __syncthreads();
+    if (tid < ne * NB) {
+        const int32_t lr = tid / NB, kb = tid % NB;
+        uint32_t d[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) d[w] = 4 * kb + w < N ? d1[lr * N + 4 * kb + w] : 0xFFFFFFFFu;
+        khop_emit(g, N, d1, lr, kb, d, c1[lr], o1[lr], (int64_t)(e0 + lr) * N, on, oe, ot, h1n, h1e);
+    }
+    __syncthreads();
+    // hop-2 rows (e_idx path, graph.py:247-250): cut length and record offset once per row
+    for (int32_t x = tid; x < ne * N; x += blockDim.x) {
+        const int32_t v = h1n[x];
+        const int32_t c = find_before_len(g, v, false, 0.0, h1e[x], err);
+        c2[x] = c;
+        o2[x] = c > 0 ? g.off[v] : 0;
+    }
+    __syncthreads();
+    for (int32_t x = tid; x < ne * N * NB; x += blockDim.x) {
+        const int32_t lr = x / NB, kb = x % NB, c = c2[lr];
+        uint32_t d[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+        if (c > 0) {
+            const uint4 b = draw_block(key, 2, ev1[lr / N], (uint32_t)(lr % N), kb);
+            d[0] = scale_draw(b.x, c);
+            d[1] = scale_draw(b.y, c);
+            d[2] = scale_draw(b.z, c);
+            d[3] = scale_draw(b.w, c);
+        }
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+            if (4 * kb + w < N) d2[lr * N + 4 * kb + w] = d[w];
+    }
+    __syncthreads();
+    const int64_t base2 = (int64_t)B * N + (int64_t)e0 * N * N;
+    for (int32_t x = tid; x < ne * N * NB; x += blockDim.x) {
+        const int32_t lr = x / NB, kb = x % NB;
+        uint32_t d[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) d[w] = 4 * kb + w < N ? d2[lr * N + 4 * kb + w] : 0xFFFFFFFFu;
+        khop_emit(g, N, d2, lr, kb, d, c2[lr], o2[lr], base2 + (int64_t)lr * N, on, oe, ot, nullptr, nullptr);
+    }
+}
+
 __global__ void __launch_bounds__(256) walks_kernel(DevGraph g, Key key, int32_t N, int32_t M, int64_t n_walks,
                                                     const int32_t *__restrict__ root, const int32_t *__restrict__ h1n,
                                                     const int32_t *__restrict__ h1e, const float *__restrict__ h1t,
@@ -698,6 +823,14 @@ extern "C" int tm_sample_khop(const tm_graph *g, tm_rng rng, int32_t k, int32_t 
         return fail(TM_E_ARG, "tm_sample_khop: NULL pointer");
     const Key key = make_key(rng.seed, rng.split, rng.side);
     hipEvent_t pe = prof_begin(S(stream));
+    if (k == 2) {
+        const int32_t epb = khop2_epb(N);
+        khop2_kernel<<<dim3((unsigned)((B + epb - 1) / epb)), 256, khop2_lds_bytes(N), S(stream)>>>(
+            g->d, key, N, B, root, cut, eidx, event_ids, out_node, out_eid, out_ts, err_flag);
+        TM_CHECK_LAUNCH();
+        prof_end("khop_kernel", S(stream), pe);
+        return TM_OK;
+    }
     int64_t rows = B, rpe = 1, off = 0;
     const int32_t *rn = root, *re = eidx;
     for (int32_t h = 1; h <= k; ++h) {
