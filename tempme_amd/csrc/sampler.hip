@@ -361,43 +361,40 @@ __global__ void __launch_bounds__(256) khop_kernel(DevGraph g, Key key, uint32_t
 // gathers the EPB*N hop-2 rows -- one launch, and no hop-1 -> hop-2 round trip through HBM.
 // Same Philox-block-per-thread scheme as khop_kernel.
 __host__ __device__ inline int32_t khop2_epb(int32_t N) {
-    const int32_t e = 4096 / (N * N);
+    const int32_t e = 1200 / (N * N);
     return e < 1 ? 1 : e > 8 ? 8 : e;
 }
 
 __host__ __device__ inline size_t khop2_lds_bytes(int32_t N) {
     const size_t epb = khop2_epb(N), rows2 = epb * N;
-    return sizeof(int32_t) * (3 * epb + epb * N + 2 * rows2 + 2 * rows2 + rows2 * N);
+    return sizeof(int32_t) * (3 * epb + epb * N + 3 * rows2 + 2 * rows2 + rows2 * N + 3 * rows2 * N);
 }
 
-// one level: ranks of thread (row lr, block kb)'s 4 draws among the row's N draws in dd, then the
-// record gathers and the stores at (row base + rank)
+// one level: record gathers of thread (row lr, block kb)'s 4 draws and their ranks among the row's N
+// draws in dd; results staged in LDS at (row, rank) so the workgroup writes its output range coalesced
 __device__ __forceinline__ void khop_emit(const DevGraph &g, int32_t N, const uint32_t *dd, int32_t lr, int32_t kb,
-                                          const uint32_t (&d)[4], int32_t c, int32_t o, int64_t obase,
-                                          int32_t *__restrict__ on, int32_t *__restrict__ oe,
-                                          float *__restrict__ ot, int32_t *h_n, int32_t *h_e) {
+                                          const uint32_t (&d)[4], int32_t c, int32_t o, int32_t *sn, int32_t *se,
+                                          float *st) {
+    // record gathers first (independent of the ranks), then the rank loop under their latency
+    Rec rec[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) rec[w] = (c > 0 && 4 * kb + w < N) ? g.rec[o + (int32_t)d[w]] : Rec{0, 0, 0.0};
     int32_t rank[4] = {0, 0, 0, 0};
     if (c > 0)
+#pragma unroll 4
         for (int32_t i = 0; i < N; ++i) {
             const uint32_t di = dd[lr * N + i];
 #pragma unroll
             for (int w = 0; w < 4; ++w) rank[w] += (di < d[w]) || (i < 4 * kb + w && di == d[w]);
         }
-    Rec rec[4];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) rec[w] = (c > 0 && 4 * kb + w < N) ? g.rec[o + (int32_t)d[w]] : Rec{0, 0, 0.0};
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
         const int32_t k = 4 * kb + w;
         if (k >= N) break;
-        const int32_t slot = c > 0 ? rank[w] : k;
-        on[obase + slot] = rec[w].ngh;
-        oe[obase + slot] = rec[w].eid;
-        ot[obase + slot] = (float)rec[w].ts;
-        if (h_n) {
-            h_n[lr * N + slot] = rec[w].ngh;
-            h_e[lr * N + slot] = rec[w].eid;
-        }
+        const int32_t slot = lr * N + (c > 0 ? rank[w] : k);
+        sn[slot] = rec[w].ngh;
+        se[slot] = rec[w].eid;
+        st[slot] = (float)rec[w].ts;
     }
 }
 
@@ -411,7 +408,10 @@ __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t
     int32_t *c1 = reinterpret_cast<int32_t *>(k2_lds), *o1 = c1 + EPB;
     uint32_t *ev1 = reinterpret_cast<uint32_t *>(o1 + EPB), *d1 = ev1 + EPB;
     int32_t *h1n = reinterpret_cast<int32_t *>(d1 + EPB * N), *h1e = h1n + R2, *c2 = h1e + R2, *o2 = c2 + R2;
-    uint32_t *d2 = reinterpret_cast<uint32_t *>(o2 + R2);
+    float *h1t = reinterpret_cast<float *>(o2 + R2);
+    uint32_t *d2 = reinterpret_cast<uint32_t *>(h1t + R2);
+    int32_t *s2n = reinterpret_cast<int32_t *>(d2 + R2 * N), *s2e = s2n + R2 * N;
+    float *s2t = reinterpret_cast<float *>(s2e + R2 * N);
     const int32_t e0 = blockIdx.x * EPB, ne = min(EPB, B - e0), tid = threadIdx.x;
     const bool time_path = eidx == nullptr;
     // hop-1 rows
@@ -444,9 +444,15 @@ __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t
         uint32_t d[4];
 #pragma unroll
         for (int w = 0; w < 4; ++w) d[w] = 4 * kb + w < N ? d1[lr * N + 4 * kb + w] : 0xFFFFFFFFu;
-        khop_emit(g, N, d1, lr, kb, d, c1[lr], o1[lr], (int64_t)(e0 + lr) * N, on, oe, ot, h1n, h1e);
+        khop_emit(g, N, d1, lr, kb, d, c1[lr], o1[lr], h1n, h1e, h1t);
     }
     __syncthreads();
+    for (int32_t x = tid; x < ne * N; x += blockDim.x) {                 // hop-1 rows, coalesced
+        const int64_t o = (int64_t)e0 * N + x;
+        on[o] = h1n[x];
+        oe[o] = h1e[x];
+        ot[o] = h1t[x];
+    }
     // hop-2 rows (e_idx path, graph.py:247-250): cut length and record offset once per row
     for (int32_t x = tid; x < ne * N; x += blockDim.x) {
         const int32_t v = h1n[x];
@@ -476,7 +482,13 @@ __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t
         uint32_t d[4];
 #pragma unroll
         for (int w = 0; w < 4; ++w) d[w] = 4 * kb + w < N ? d2[lr * N + 4 * kb + w] : 0xFFFFFFFFu;
-        khop_emit(g, N, d2, lr, kb, d, c2[lr], o2[lr], base2 + (int64_t)lr * N, on, oe, ot, nullptr, nullptr);
+        khop_emit(g, N, d2, lr, kb, d, c2[lr], o2[lr], s2n, s2e, s2t);
+    }
+    __syncthreads();
+    for (int32_t x = tid; x < ne * N * N; x += blockDim.x) {             // hop-2 rows, coalesced
+        on[base2 + x] = s2n[x];
+        oe[base2 + x] = s2e[x];
+        ot[base2 + x] = s2t[x];
     }
 }
 
