@@ -380,13 +380,27 @@ __device__ __forceinline__ void khop_emit(const DevGraph &g, int32_t N, const ui
 #pragma unroll
     for (int w = 0; w < 4; ++w) rec[w] = (c > 0 && 4 * kb + w < N) ? g.rec[o + (int32_t)d[w]] : Rec{0, 0, 0.0};
     int32_t rank[4] = {0, 0, 0, 0};
-    if (c > 0)
-#pragma unroll 4
-        for (int32_t i = 0; i < N; ++i) {
-            const uint32_t di = dd[lr * N + i];
+    if (c > 0) {
+        if ((N & 3) == 0) {                              // row start 16-B aligned: 4 draws per LDS read
+            const uint4 *row = reinterpret_cast<const uint4 *>(dd + lr * N);
+            for (int32_t i4 = 0; i4 < (N >> 2); ++i4) {
+                const uint4 q = row[i4];
+                const uint32_t qv[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-            for (int w = 0; w < 4; ++w) rank[w] += (di < d[w]) || (i < 4 * kb + w && di == d[w]);
+                for (int v = 0; v < 4; ++v) {
+                    const int32_t i = 4 * i4 + v;
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) rank[w] += (qv[v] < d[w]) || (i < 4 * kb + w && qv[v] == d[w]);
+                }
+            }
+        } else {
+            for (int32_t i = 0; i < N; ++i) {
+                const uint32_t di = dd[lr * N + i];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) rank[w] += (di < d[w]) || (i < 4 * kb + w && di == d[w]);
+            }
         }
+    }
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
         const int32_t k = 4 * kb + w;
@@ -405,13 +419,14 @@ __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t
                                                     int32_t *__restrict__ oe, float *__restrict__ ot, int32_t *err) {
     extern __shared__ uint32_t k2_lds[];
     const int32_t EPB = khop2_epb(N), NB = (N + 3) >> 2, R2 = EPB * N;
-    int32_t *c1 = reinterpret_cast<int32_t *>(k2_lds), *o1 = c1 + EPB;
-    uint32_t *ev1 = reinterpret_cast<uint32_t *>(o1 + EPB), *d1 = ev1 + EPB;
-    int32_t *h1n = reinterpret_cast<int32_t *>(d1 + EPB * N), *h1e = h1n + R2, *c2 = h1e + R2, *o2 = c2 + R2;
-    float *h1t = reinterpret_cast<float *>(o2 + R2);
-    uint32_t *d2 = reinterpret_cast<uint32_t *>(h1t + R2);
-    int32_t *s2n = reinterpret_cast<int32_t *>(d2 + R2 * N), *s2e = s2n + R2 * N;
+    // draw rows first so each row starts 16-B aligned when N % 4 == 0 (uint4 reads in khop_emit)
+    uint32_t *d2 = k2_lds, *d1 = d2 + R2 * N;
+    int32_t *s2n = reinterpret_cast<int32_t *>(d1 + EPB * N), *s2e = s2n + R2 * N;
     float *s2t = reinterpret_cast<float *>(s2e + R2 * N);
+    int32_t *h1n = reinterpret_cast<int32_t *>(s2t + R2 * N), *h1e = h1n + R2, *c2 = h1e + R2, *o2 = c2 + R2;
+    float *h1t = reinterpret_cast<float *>(o2 + R2);
+    int32_t *c1 = reinterpret_cast<int32_t *>(h1t + R2), *o1 = c1 + EPB;
+    uint32_t *ev1 = reinterpret_cast<uint32_t *>(o1 + EPB);
     const int32_t e0 = blockIdx.x * EPB, ne = min(EPB, B - e0), tid = threadIdx.x;
     const bool time_path = eidx == nullptr;
     // hop-1 rows
@@ -420,7 +435,7 @@ __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t
         const int32_t c = find_before_len(g, u, time_path, time_path ? cut[e0 + tid] : 0.0,
                                           time_path ? 0 : eidx[e0 + tid], err);
         c1[tid] = c;
-        o1[tid] = c > 0 ? g.off[u] : 0;
+        o1[tid] = (u >= 0 && u < g.n_nodes) ? g.off[u] : 0;   // issued alongside the cut lookup
         ev1[tid] = event_ids[e0 + tid];
     }
     __syncthreads();
@@ -456,9 +471,8 @@ __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t
     // hop-2 rows (e_idx path, graph.py:247-250): cut length and record offset once per row
     for (int32_t x = tid; x < ne * N; x += blockDim.x) {
         const int32_t v = h1n[x];
-        const int32_t c = find_before_len(g, v, false, 0.0, h1e[x], err);
-        c2[x] = c;
-        o2[x] = c > 0 ? g.off[v] : 0;
+        c2[x] = find_before_len(g, v, false, 0.0, h1e[x], err);
+        o2[x] = (v >= 0 && v < g.n_nodes) ? g.off[v] : 0;
     }
     __syncthreads();
     for (int32_t x = tid; x < ne * N * NB; x += blockDim.x) {
