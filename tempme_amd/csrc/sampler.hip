@@ -360,18 +360,21 @@ __global__ void __launch_bounds__(256) khop_kernel(DevGraph g, Key key, uint32_t
 // (kept in LDS), looks up the hop-2 rows' cut lengths and offsets once per row, then draws, ranks and
 // gathers the EPB*N hop-2 rows -- one launch, and no hop-1 -> hop-2 round trip through HBM.
 // Same Philox-block-per-thread scheme as khop_kernel.
+// roots per workgroup: ~one hop-2 Philox block per thread, so the launch is about one round of
+// resident workgroups (each is a chain of dependent lookups; a second round doubles the time)
 __host__ __device__ inline int32_t khop2_epb(int32_t N) {
-    const int32_t e = 1200 / (N * N);
+    const int32_t e = 1600 / (N * N);
     return e < 1 ? 1 : e > 8 ? 8 : e;
 }
 
 __host__ __device__ inline size_t khop2_lds_bytes(int32_t N) {
     const size_t epb = khop2_epb(N), rows2 = epb * N;
-    return sizeof(int32_t) * (3 * epb + epb * N + 3 * rows2 + 2 * rows2 + rows2 * N + 3 * rows2 * N);
+    return sizeof(int32_t) * (3 * epb + epb * N + 3 * rows2 + 2 * rows2 + rows2 * N);
 }
 
 // one level: record gathers of thread (row lr, block kb)'s 4 draws and their ranks among the row's N
 // draws in dd; results staged in LDS at (row, rank) so the workgroup writes its output range coalesced
+template <bool kStage>
 __device__ __forceinline__ void khop_emit(const DevGraph &g, int32_t N, const uint32_t *dd, int32_t lr, int32_t kb,
                                           const uint32_t (&d)[4], int32_t c, int32_t o, int32_t *sn, int32_t *se,
                                           float *st) {
@@ -405,7 +408,8 @@ __device__ __forceinline__ void khop_emit(const DevGraph &g, int32_t N, const ui
     for (int w = 0; w < 4; ++w) {
         const int32_t k = 4 * kb + w;
         if (k >= N) break;
-        const int32_t slot = lr * N + (c > 0 ? rank[w] : k);
+        // kStage: (row, rank) in LDS; else sn/se/st already point at this row's output
+        const int32_t slot = (kStage ? lr * N : 0) + (c > 0 ? rank[w] : k);
         sn[slot] = rec[w].ngh;
         se[slot] = rec[w].eid;
         st[slot] = (float)rec[w].ts;
@@ -421,9 +425,7 @@ __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t
     const int32_t EPB = khop2_epb(N), NB = (N + 3) >> 2, R2 = EPB * N;
     // draw rows first so each row starts 16-B aligned when N % 4 == 0 (uint4 reads in khop_emit)
     uint32_t *d2 = k2_lds, *d1 = d2 + R2 * N;
-    int32_t *s2n = reinterpret_cast<int32_t *>(d1 + EPB * N), *s2e = s2n + R2 * N;
-    float *s2t = reinterpret_cast<float *>(s2e + R2 * N);
-    int32_t *h1n = reinterpret_cast<int32_t *>(s2t + R2 * N), *h1e = h1n + R2, *c2 = h1e + R2, *o2 = c2 + R2;
+    int32_t *h1n = reinterpret_cast<int32_t *>(d1 + EPB * N), *h1e = h1n + R2, *c2 = h1e + R2, *o2 = c2 + R2;
     float *h1t = reinterpret_cast<float *>(o2 + R2);
     int32_t *c1 = reinterpret_cast<int32_t *>(h1t + R2), *o1 = c1 + EPB;
     uint32_t *ev1 = reinterpret_cast<uint32_t *>(o1 + EPB);
@@ -459,7 +461,7 @@ __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t
         uint32_t d[4];
 #pragma unroll
         for (int w = 0; w < 4; ++w) d[w] = 4 * kb + w < N ? d1[lr * N + 4 * kb + w] : 0xFFFFFFFFu;
-        khop_emit(g, N, d1, lr, kb, d, c1[lr], o1[lr], h1n, h1e, h1t);
+        khop_emit<true>(g, N, d1, lr, kb, d, c1[lr], o1[lr], h1n, h1e, h1t);
     }
     __syncthreads();
     for (int32_t x = tid; x < ne * N; x += blockDim.x) {                 // hop-1 rows, coalesced
@@ -496,13 +498,8 @@ __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t
         uint32_t d[4];
 #pragma unroll
         for (int w = 0; w < 4; ++w) d[w] = 4 * kb + w < N ? d2[lr * N + 4 * kb + w] : 0xFFFFFFFFu;
-        khop_emit(g, N, d2, lr, kb, d, c2[lr], o2[lr], s2n, s2e, s2t);
-    }
-    __syncthreads();
-    for (int32_t x = tid; x < ne * N * N; x += blockDim.x) {             // hop-2 rows, coalesced
-        on[base2 + x] = s2n[x];
-        oe[base2 + x] = s2e[x];
-        ot[base2 + x] = s2t[x];
+        const int64_t ob = base2 + (int64_t)lr * N;
+        khop_emit<false>(g, N, d2, lr, kb, d, c2[lr], o2[lr], on + ob, oe + ob, ot + ob);
     }
 }
 
