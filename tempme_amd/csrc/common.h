@@ -81,6 +81,15 @@ struct DevGraph {
     uint32_t pblk_mask;
 };
 
+// A uniform pointer moved into VGPRs: kernels with many pointer arguments otherwise overflow the
+// scalar register file and spill it through v_readlane/v_writelane in their loops.
+template <class T>
+__device__ __forceinline__ T *vptr(T *p) {
+    uint64_t v = reinterpret_cast<uint64_t>(p);
+    asm volatile("" : "+v"(v));
+    return reinterpret_cast<T *>(v);
+}
+
 // ------------------------------------------------------------------ Philox4x32-10
 // all four output words of one Philox4x32-10 block
 __device__ __forceinline__ uint4 philox4(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {

@@ -374,7 +374,7 @@ __host__ __device__ inline size_t khop2_lds_bytes(int32_t N) {
 
 // one level: record gathers of thread (row lr, block kb)'s 4 draws and their ranks among the row's N
 // draws in dd; results staged in LDS at (row, rank) so the workgroup writes its output range coalesced
-template <bool kStage>
+template <bool kStage, bool keyed>
 __device__ __forceinline__ void khop_emit(const DevGraph &g, int32_t N, const uint32_t *dd, int32_t lr, int32_t kb,
                                           const uint32_t (&d)[4], int32_t c, int32_t o, int32_t *sn, int32_t *se,
                                           float *st) {
@@ -383,7 +383,27 @@ __device__ __forceinline__ void khop_emit(const DevGraph &g, int32_t N, const ui
 #pragma unroll
     for (int w = 0; w < 4; ++w) rec[w] = (c > 0 && 4 * kb + w < N) ? g.rec[o + (int32_t)d[w]] : Rec{0, 0, 0.0};
     int32_t rank[4] = {0, 0, 0, 0};
-    if (c > 0) {
+    if (keyed && c > 0) {
+        // dd holds (draw << 6 | index): unique keys, so the np.sort rank (ties by index) is one compare
+        uint32_t my[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) my[w] = (d[w] << 6) | (uint32_t)(4 * kb + w);
+        const uint4 *row = reinterpret_cast<const uint4 *>(dd + lr * N);
+        if ((N & 3) == 0) {
+            for (int32_t i4 = 0; i4 < (N >> 2); ++i4) {
+                const uint4 q = row[i4];
+#pragma unroll
+                for (int w = 0; w < 4; ++w)
+                    rank[w] += (q.x < my[w]) + (q.y < my[w]) + (q.z < my[w]) + (q.w < my[w]);
+            }
+        } else {
+            for (int32_t i = 0; i < N; ++i) {
+                const uint32_t q = dd[lr * N + i];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) rank[w] += q < my[w];
+            }
+        }
+    } else if (!keyed && c > 0) {
         if ((N & 3) == 0) {                              // row start 16-B aligned: 4 draws per LDS read
             const uint4 *row = reinterpret_cast<const uint4 *>(dd + lr * N);
             for (int32_t i4 = 0; i4 < (N >> 2); ++i4) {
@@ -416,6 +436,7 @@ __device__ __forceinline__ void khop_emit(const DevGraph &g, int32_t N, const ui
     }
 }
 
+template <bool keyed>
 __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t N, int32_t B,
                                                     const int32_t *__restrict__ root, const double *__restrict__ cut,
                                                     const int32_t *__restrict__ eidx,
@@ -431,6 +452,9 @@ __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t
     uint32_t *ev1 = reinterpret_cast<uint32_t *>(o1 + EPB);
     const int32_t e0 = blockIdx.x * EPB, ne = min(EPB, B - e0), tid = threadIdx.x;
     const bool time_path = eidx == nullptr;
+    on = vptr(on);   // output pointers in VGPRs (scalar file pressure, see events_kernel)
+    oe = vptr(oe);
+    ot = vptr(ot);
     // hop-1 rows
     if (tid < ne) {
         const int32_t u = root[e0 + tid];
@@ -453,15 +477,18 @@ __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t
         }
 #pragma unroll
         for (int w = 0; w < 4; ++w)
-            if (4 * kb + w < N) d1[lr * N + 4 * kb + w] = d[w];
+            if (4 * kb + w < N) d1[lr * N + 4 * kb + w] = keyed ? (d[w] << 6) | (uint32_t)(4 * kb + w) : d[w];
     }
     __syncthreads();
     if (tid < ne * NB) {
         const int32_t lr = tid / NB, kb = tid % NB;
         uint32_t d[4];
 #pragma unroll
-        for (int w = 0; w < 4; ++w) d[w] = 4 * kb + w < N ? d1[lr * N + 4 * kb + w] : 0xFFFFFFFFu;
-        khop_emit<true>(g, N, d1, lr, kb, d, c1[lr], o1[lr], h1n, h1e, h1t);
+        for (int w = 0; w < 4; ++w) {
+            const uint32_t v = 4 * kb + w < N ? d1[lr * N + 4 * kb + w] : 0xFFFFFFFFu;
+            d[w] = keyed ? v >> 6 : v;
+        }
+        khop_emit<true, keyed>(g, N, d1, lr, kb, d, c1[lr], o1[lr], h1n, h1e, h1t);
     }
     __syncthreads();
     for (int32_t x = tid; x < ne * N; x += blockDim.x) {                 // hop-1 rows, coalesced
@@ -489,7 +516,7 @@ __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t
         }
 #pragma unroll
         for (int w = 0; w < 4; ++w)
-            if (4 * kb + w < N) d2[lr * N + 4 * kb + w] = d[w];
+            if (4 * kb + w < N) d2[lr * N + 4 * kb + w] = keyed ? (d[w] << 6) | (uint32_t)(4 * kb + w) : d[w];
     }
     __syncthreads();
     const int64_t base2 = (int64_t)B * N + (int64_t)e0 * N * N;
@@ -497,9 +524,12 @@ __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t
         const int32_t lr = x / NB, kb = x % NB;
         uint32_t d[4];
 #pragma unroll
-        for (int w = 0; w < 4; ++w) d[w] = 4 * kb + w < N ? d2[lr * N + 4 * kb + w] : 0xFFFFFFFFu;
+        for (int w = 0; w < 4; ++w) {
+            const uint32_t v = 4 * kb + w < N ? d2[lr * N + 4 * kb + w] : 0xFFFFFFFFu;
+            d[w] = keyed ? v >> 6 : v;
+        }
         const int64_t ob = base2 + (int64_t)lr * N;
-        khop_emit<false>(g, N, d2, lr, kb, d, c2[lr], o2[lr], on + ob, oe + ob, ot + ob);
+        khop_emit<false, keyed>(g, N, d2, lr, kb, d, c2[lr], o2[lr], on + ob, oe + ob, ot + ob);
     }
 }
 
@@ -621,13 +651,6 @@ struct EventArgs {
     uint32_t *bins_out;     // [3 * E][12] per-(event, side) motif bins, reduced by hist_reduce_kernel
     int32_t *err;
 };
-
-template <class T>
-__device__ __forceinline__ T *vptr(T *p) {
-    uint64_t v = reinterpret_cast<uint64_t>(p);
-    asm volatile("" : "+v"(v));
-    return reinterpret_cast<T *>(v);
-}
 
 // hist[k] += sum over the n_groups rows of bins[row][k].  252 threads (21 per category) stride over
 // the flat array by a multiple of 12, so each thread always sums one category; one atomic per
@@ -848,8 +871,15 @@ extern "C" int tm_sample_khop(const tm_graph *g, tm_rng rng, int32_t k, int32_t 
     hipEvent_t pe = prof_begin(S(stream));
     if (k == 2) {
         const int32_t epb = khop2_epb(N);
-        khop2_kernel<<<dim3((unsigned)((B + epb - 1) / epb)), 256, khop2_lds_bytes(N), S(stream)>>>(
-            g->d, key, N, B, root, cut, eidx, event_ids, out_node, out_eid, out_ts, err_flag);
+        // a draw is < its row's cut <= n_entries: below 2^26 it packs with its index into one sort key
+        const dim3 grid((unsigned)((B + epb - 1) / epb));
+        if (g->d.n_entries < ((int64_t)1 << 26))
+            khop2_kernel<true><<<grid, 256, khop2_lds_bytes(N), S(stream)>>>(g->d, key, N, B, root, cut, eidx, event_ids,
+                                                                              out_node, out_eid, out_ts, err_flag);
+        else
+            khop2_kernel<false><<<grid, 256, khop2_lds_bytes(N), S(stream)>>>(g->d, key, N, B, root, cut, eidx,
+                                                                               event_ids, out_node, out_eid, out_ts,
+                                                                               err_flag);
         TM_CHECK_LAUNCH();
         prof_end("khop_kernel", S(stream), pe);
         return TM_OK;
