@@ -102,8 +102,11 @@ __device__ __forceinline__ uint4 philox4(uint32_t c0, uint32_t c1, uint32_t c2, 
             k0 += 0x9E3779B9u;
             k1 += 0xBB67AE85u;
         }
-        uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-        uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        // one 32x32->64 multiply (v_mad_u64_u32) per product instead of separate mul_hi and mul_lo:
+        // integer multiplies are quarter rate and dominate the round
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
         uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
         c0 = n0;
         c1 = lo1;
