@@ -164,11 +164,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # one process per GPU; TEMPME_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks
+    # sharing the GPUs there are (ranks map to local_rank % device_count)
+    backend = os.environ.get("TEMPME_DIST_BACKEND", "nccl")
+    dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(dev)
 
     import tempme_amd as tm
@@ -223,7 +229,7 @@ def main():
     prof = L.profile_read()
     L.profile_enable(False)
     pipe.check_errors()
-    el = max_over_ranks(el, dist, dev)
+    el = max_over_ranks(el, dist, dev if backend == "nccl" else "cpu")
 
     if rank == 0:
         fm = flops_model(g["e_feat"].shape[1], g["n_feat"].shape[1], 64, N, M)

@@ -50,6 +50,9 @@ for s in "$@"; do
                 TEMPME_LIB="$PWD/$so" step stamps_$n 300 python tools_stamps.py
                 { echo "== $n: $(grep -o '"walk_kernel": {"avg_ms": [0-9.]*' gpurun_out/stamps_$n.log)"; grep -E "^(slot|walk) " gpurun_out/stamps_$n.log; } | tee -a gpurun_out/stamps.txt
             done ;;
+        dist2)  # multi-rank rehearsal on one GPU: 2 ranks, gloo barrier/all-reduce, both on cuda:0
+            TEMPME_DIST_BACKEND=gloo step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+                --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu-baseline ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done
