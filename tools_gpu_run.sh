@@ -53,6 +53,8 @@ for s in "$@"; do
         dist2)  # multi-rank rehearsal on one GPU: 2 ranks, gloo barrier/all-reduce, both on cuda:0
             TEMPME_DIST_BACKEND=gloo step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu-baseline ;;
+        n30) step bench_n30 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --n-degree 30 ;;
+        a3) step bench_a3 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --alpha 3.0 ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done
