@@ -697,6 +697,7 @@ __device__ unsigned long long g_est[8];
 #define TM_EST(k) (void)T
 #endif
 
+template <bool keyed>
 __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
     unsigned long long T[8];
     TM_EST(0);
@@ -775,7 +776,9 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
             const int32_t k = 4 * kb + w;
-            if (k < N) d2[j * N + k] = c > 0 ? (uint32_t)scale_draw(wv[w], c) : 0xFFFFFFFFu;
+            // keyed: (draw << 6 | index), unique, so the np.sort rank is one compare (see khop2_kernel)
+            const uint32_t dv = (uint32_t)scale_draw(wv[w], c);
+            if (k < N) d2[j * N + k] = c > 0 ? (keyed ? (dv << 6) | (uint32_t)k : dv) : 0xFFFFFFFFu;
         }
     }
     __syncthreads();
@@ -800,8 +803,12 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
 #pragma unroll
             for (int u = 0; u < HB; ++u) {
                 const uint32_t di = d2[jr[u] * N + i];
-                rank[u] += (di < dr[u]) || (i < kr[u] && di == dr[u]);
+                if (keyed) rank[u] += di < dr[u];
+                else rank[u] += (di < dr[u]) || (i < kr[u] && di == dr[u]);
             }
+        if (keyed)
+#pragma unroll
+            for (int u = 0; u < HB; ++u) dr[u] >>= 6;                  // back to the draw
 #pragma unroll
         for (int u = 0; u < HB; ++u) {
             const int32_t x = x0 + u * 64 + tid, c = x < N * N ? c2[jr[u]] : 0;
@@ -990,7 +997,10 @@ extern "C" int tm_sample_events(const tm_graph *g, uint64_t seed, uint32_t split
                 dst_list, (uint32_t)n_dst, dst_fake, sub1_node, sub1_eid, sub1_ts, sub2_node, sub2_eid, sub2_ts,
                 node6,    eid3,     ts3,       cat,       cnt,      hist12,   bins,     err_flag};
     hipEvent_t pe = prof_begin(S(stream));
-    events_kernel<<<dim3(n_events, 3), 64, events_lds_bytes(N, M), S(stream)>>>(a);
+    if (g->d.n_entries < ((int64_t)1 << 26))
+        events_kernel<true><<<dim3(n_events, 3), 64, events_lds_bytes(N, M), S(stream)>>>(a);
+    else
+        events_kernel<false><<<dim3(n_events, 3), 64, events_lds_bytes(N, M), S(stream)>>>(a);
     TM_CHECK_LAUNCH();
     prof_end("events_kernel", S(stream), pe);
     pe = prof_begin(S(stream));
