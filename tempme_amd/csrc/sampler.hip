@@ -11,6 +11,8 @@
 // dwordx4 gather; e_idx -> position is an O(1) per-edge table (EdgeEnds); the filtered
 // step-3 candidate sets of get_final_step are counted and indexed through a per-node
 // (neighbor, position)-sorted pair index with binary searches instead of O(deg) scans.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace tmk {
@@ -866,6 +868,12 @@ using namespace tmk;
 
 static inline hipStream_t S(void *s) { return (hipStream_t)s; }
 
+// keyed one-compare ranks need draw << 6 to fit 32 bits: draws are < n_entries.  TEMPME_FORCE_UNKEYED
+// (tests) selects the two-compare kernels on any graph.
+static inline bool use_keyed(const tm_graph *g) {
+    return g->d.n_entries < ((int64_t)1 << 26) && !std::getenv("TEMPME_FORCE_UNKEYED");
+}
+
 extern "C" int tm_sample_khop(const tm_graph *g, tm_rng rng, int32_t k, int32_t N, int32_t B, const int32_t *root,
                               const double *cut, const int32_t *eidx, const uint32_t *event_ids, int32_t *out_node,
                               int32_t *out_eid, float *out_ts, int32_t *err_flag, void *stream) {
@@ -880,7 +888,7 @@ extern "C" int tm_sample_khop(const tm_graph *g, tm_rng rng, int32_t k, int32_t 
         const int32_t epb = khop2_epb(N);
         // a draw is < its row's cut <= n_entries: below 2^26 it packs with its index into one sort key
         const dim3 grid((unsigned)((B + epb - 1) / epb));
-        if (g->d.n_entries < ((int64_t)1 << 26))
+        if (use_keyed(g))
             khop2_kernel<true><<<grid, 256, khop2_lds_bytes(N), S(stream)>>>(g->d, key, N, B, root, cut, eidx, event_ids,
                                                                               out_node, out_eid, out_ts, err_flag);
         else
@@ -997,7 +1005,7 @@ extern "C" int tm_sample_events(const tm_graph *g, uint64_t seed, uint32_t split
                 dst_list, (uint32_t)n_dst, dst_fake, sub1_node, sub1_eid, sub1_ts, sub2_node, sub2_eid, sub2_ts,
                 node6,    eid3,     ts3,       cat,       cnt,      hist12,   bins,     err_flag};
     hipEvent_t pe = prof_begin(S(stream));
-    if (g->d.n_entries < ((int64_t)1 << 26))
+    if (use_keyed(g))
         events_kernel<true><<<dim3(n_events, 3), 64, events_lds_bytes(N, M), S(stream)>>>(a);
     else
         events_kernel<false><<<dim3(n_events, 3), 64, events_lds_bytes(N, M), S(stream)>>>(a);

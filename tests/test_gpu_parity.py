@@ -312,3 +312,83 @@ def test_gate_table_path_bitwise_equals_per_walk_path(tm):
     pipe.check_errors()
     assert torch.equal(o1[:3 * E * N].view(3, E, N), h1)
     assert torch.equal(o2[:3 * E * N * N].view(3, E, N * N), h2)
+
+
+def _pareto_finder(tm, seed=4, **kw):
+    from tempme_amd.workload import enron_like, split
+    g = enron_like(seed=seed, **kw)
+    (src, dst, ts, eidx), rows, pool = split(g)
+    f = _finder(tm, g["src"][rows], g["dst"][rows], g["eidx"][rows], g["ts"][rows], g["n_nodes"], seed=seed)
+    return g, rows, (src, dst, ts, eidx), pool, f
+
+
+@pytest.mark.parametrize("N", [7, 20, 30, 64])
+def test_khop2_fused_equals_per_level_and_oracle(tm, N):
+    """find_k_hop(2) runs the fused 2-hop kernel, find_k_hop(3) the per-level kernel: their first two
+    hops share the RNG keys and must be identical, on both the e_idx path and the time path; and
+    both equal the C oracle."""
+    g, rows, (src, dst, ts, eidx), pool, f = _pareto_finder(tm)
+    B = 96
+    ev = 1000 + np.arange(B)
+    for side, ei in ((px.SIDE_SRC, eidx[:B]), (px.SIDE_BGD, None)):
+        two = f.find_k_hop(2, src[:B], ts[:B], N, e_idx_l=ei, event_ids=ev, side=side)
+        three = f.find_k_hop(3, src[:B], ts[:B], N, e_idx_l=ei, event_ids=ev, side=side)
+        for h in range(2):
+            for a in range(3):
+                assert np.array_equal(two[a][h], three[a][h]), (side, h, a)
+    og = orc.OracleGraph(g["src"][rows], g["dst"][rows], g["eidx"][rows], g["ts"][rows], g["n_nodes"])
+    o = orc.khop(og, f.seed, f.split, px.SIDE_SRC, 2, N, src[:B], ts[:B], eidx[:B], ev)
+    two = f.find_k_hop(2, src[:B], ts[:B], N, e_idx_l=eidx[:B], event_ids=ev, side=px.SIDE_SRC)
+    for h in range(2):
+        for a in range(3):
+            assert np.array_equal(two[a][h].reshape(-1), np.asarray(o[a][h]).reshape(-1)), (h, a)
+
+
+def test_unkeyed_kernels_equal_keyed(tm, monkeypatch):
+    """The one-compare keyed rank kernels (graphs < 2^26 entries) and the two-compare kernels must
+    give identical samples (TEMPME_FORCE_UNKEYED selects the latter)."""
+    from tempme_amd.preprocess import sample_events
+    g, rows, (src, dst, ts, eidx), pool, f = _pareto_finder(tm, seed=6)
+    dev = f.device
+    E, N = 200, 20
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a[:E], dtype=dt)).to(dev)  # noqa: E731
+    args = (f.graph, 3, px.SPLIT_TEST, N, 3, t(src, np.int32), t(dst, np.int32), t(ts, np.float64),
+            t(eidx, np.int32), torch.arange(E, dtype=torch.int32, device=dev), torch.from_numpy(pool).to(dev))
+    a = sample_events(*args)
+    ka = f.find_k_hop(2, src[:E], ts[:E], N, e_idx_l=eidx[:E], event_ids=np.arange(E), side=px.SIDE_TGT)
+    monkeypatch.setenv("TEMPME_FORCE_UNKEYED", "1")
+    b = sample_events(*args)
+    kb = f.find_k_hop(2, src[:E], ts[:E], N, e_idx_l=eidx[:E], event_ids=np.arange(E), side=px.SIDE_TGT)
+    for name in ("dst_fake", "node6", "eid3", "ts3", "cat", "cnt", "hist", "sub1_node", "sub1_eid", "sub1_ts",
+                 "sub2_node", "sub2_eid", "sub2_ts"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    for x, y in zip(ka, kb):
+        for h in range(2):
+            assert np.array_equal(x[h], y[h])
+
+
+@pytest.mark.parametrize("N,alpha", [(30, 1.2), (20, 3.0)])
+def test_pipeline_other_configs_vs_oracle(tm, N, alpha):
+    """Sampling bit-exact vs the C oracle at N=30 and at Pareto alpha=3 (bench's other configs)."""
+    from tempme_amd.pipeline import ExplainPipeline
+    g, rows, (src, dst, ts, eidx), pool, f = _pareto_finder(tm, seed=7, alpha=alpha, node_feat="uniform")
+    dev = f.device
+    torch.manual_seed(0)
+    ex = tm.TempME(_Base(g["n_feat"], g["e_feat"], dev), "tgn", "enron_sampled", 40, 64, device=dev,
+                   null_model={k: 1 / 12 for k in range(1, 13)}).to(dev).eval()
+    B, E = 100, 200
+    pipe = ExplainPipeline(ex, f.graph, torch.from_numpy(pool), N, 3, B, seed=7, split=px.SPLIT_TEST)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a[:E], dtype=dt)).to(dev)  # noqa: E731
+    imp, h1, h2 = pipe.run(t(src, np.int32), t(dst, np.int32), t(ts, np.float64), t(eidx, np.int32),
+                           torch.arange(E, dtype=torch.int32, device=dev))
+    torch.cuda.synchronize()
+    pipe.check_errors()
+    og = orc.OracleGraph(g["src"][rows], g["dst"][rows], g["eidx"][rows], g["ts"][rows], g["n_nodes"])
+    o = orc.event_pipeline(og, 7, px.SPLIT_TEST, N, 3, src[:E], dst[:E], ts[:E], eidx[:E], np.arange(E), pool, 8)
+    b = pipe.buf
+    h = lambda x: x.cpu().numpy()  # noqa: E731
+    for name in ("node6", "eid3", "ts3", "cat", "sub1_node", "sub1_eid", "sub2_node", "sub2_eid"):
+        assert np.array_equal(h(getattr(b, name)).swapaxes(0, 1), o[name]), name
+    assert np.array_equal(h(b.cnt).swapaxes(0, 1).astype(np.int32), o["cnt"])
+    x = h(imp)
+    assert np.isfinite(x).all() and (x >= 0).all() and (x <= 1).all()
