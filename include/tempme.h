@@ -168,6 +168,57 @@ int tm_edge_importance_tab(const float *gf, int32_t n_ids, int32_t n_groups, int
                            const int32_t *sub2_node, const int32_t *sub2_eid, float *out_h1, float *out_h2,
                            int32_t *err_flag, void *stream);
 
+/* ---------------------------------------------------------------- TGN base model (consumer of the path)
+ * One temporal-attention layer of the base TGN's embedding_update_layer
+ * (TGN/modules/embedding_module.py:356-393 -> TemporalAttentionLayer :181-216 ->
+ * MultiHeadAttention :52-86 -> ScaledDotProductAttention :16-32), the part that touches every
+ * neighbour: per source row r and head h
+ *     s_j = (qf[r,h] . key[r,j]) / temperature,   s_j = -1e10 where mask_node[m,j] == 0
+ *     z[r,h] = sum_j softmax(s)_j * ew[m,j] * key[r,j]
+ * with key[r,j] = [node feature (d_node) | edge feature (d_edge) | cos(dt[r,j]*time_w + time_b) (d_time)]
+ * built on the fly (never materialised) and m = (r*n_head + h) % rows when head_major_rows
+ * (the reference pairs rows with mask/explain-weight rows through .repeat(n_head,1,1),
+ * embedding_module.py:74-75 and :211-212), else m = r.
+ * The caller supplies qf[r,h] = (W_k,h^T W_q,h) query[r] and applies (fc W_v,h) to z: the
+ * per-neighbour key/value projections of the reference fold into one per-row projection on each
+ * side (same result up to fp32 reassociation; DESIGN.md "TGN contrast"). */
+typedef struct {
+    int32_t rows, n_ngh, n_head;
+    int32_t d_node, d_edge, d_time;       /* d_key = d_node + d_edge + d_time <= 512 */
+    int32_t node_rows, edge_rows;         /* table sizes when gathered (index checks) */
+    int32_t head_major_rows;              /* 1 = the reference's row pairing (see above) */
+    int32_t seg_rows;                     /* > 0: rows are independent batches of seg_rows rows and the
+                                             pairing runs inside each (m = base + ((r-base)*n_head+h) % seg) */
+    float temperature;                    /* sqrt(d_key), embedding_module.py:51 */
+    const float *node_tab;                /* node_idx != NULL: [node_rows, d_node] table; else dense [rows*n_ngh, d_node] */
+    const int32_t *node_idx;              /* [rows*n_ngh] or NULL */
+    const float *edge_tab;                /* edge_idx != NULL: [edge_rows, d_edge] table; else dense [rows*n_ngh, d_edge] */
+    const int32_t *edge_idx;              /* [rows*n_ngh] or NULL */
+    const float *dt;                      /* [rows*n_ngh] time deltas (f32, as the reference casts them) */
+    const float *time_w, *time_b;         /* [d_time] TimeEncode Linear(1, d) weight and bias */
+    const int32_t *mask_node;             /* [rows*n_ngh]; 0 = padding (masked) */
+    const float *ew;                      /* [rows*n_ngh] explanation weights or NULL (= 1) */
+    const float *qf;                      /* [rows, n_head*d_key] folded queries */
+    int32_t *err_flag;                    /* nullable device flag: set to TM_E_ARG on an out-of-range index */
+} tm_tgn_attn;
+
+/* forward: z [rows, n_head*d_key], stats [rows, n_head, 2] (softmax max and sum, for the backward) */
+int tm_tgn_attn_fwd(const tm_tgn_attn *a, float *z, float *stats, void *stream);
+/* backward given gz = dL/dz: d_ew_parts [rows*n_head, n_ngh] holds the contribution of pair
+ * q = r*n_head + h to d ew[m(q), j] (the caller sums the n_head contributions of each row);
+ * d_node (nullable; dense node_tab only) [rows*n_ngh, d_node] = dL/d node feature. */
+int tm_tgn_attn_bwd(const tm_tgn_attn *a, const float *stats, const float *gz, float *d_ew_parts, float *d_node,
+                    void *stream);
+
+/* threshold_test masking (temp_exp_main.py:153-181, tgn branch): for group g and row r,
+ * sel = torch.topk(imp[r], k_of_group[g], largest=False).indices as the reference computes it on the
+ * CPU -- the index set std::nth_element (or std::partial_sort when 64*k <= n) leaves in front of
+ * the (value, index) pairs, ATen TopKImpl.h, so ties resolve exactly as there -- and
+ * node_out[g, r, :] = node_in[r, :] with node_out[g, r, sel] = 0 (np.put_along_axis(..., 0)).
+ * imp [rows, n] f32, node_in [rows, n] int32, node_out [n_groups, rows, n]; n <= 4096. */
+int tm_mask_least_important(const float *imp, int32_t rows, int32_t n, const int32_t *k_of_group, int32_t n_groups,
+                            const int32_t *node_in, int32_t *node_out, void *stream);
+
 /* ---------------------------------------------------------------- per-kernel timing
  * tm_profile_enable(1) clears and starts recording a HIP event pair around every kernel
  * launch, on that launch's stream; tm_profile_sync() waits and aggregates, returning the

@@ -34,12 +34,25 @@ EXPORTS = (
     "tm_last_error", "tm_version", "tm_graph_build", "tm_graph_free", "tm_graph_info", "tm_graph_export",
     "tm_sample_khop", "tm_sample_walks", "tm_neg_sample", "tm_perm_keys", "tm_motif_hist", "tm_edge_counts",
     "tm_sample_events", "tm_weights_create", "tm_weights_pack", "tm_weights_free", "tm_encoder_workspace_bytes",
-    "tm_encoder_fwd", "tm_edge_importance", "tm_edge_gate_table", "tm_edge_importance_tab", "tm_profile_enable", "tm_profile_sync", "tm_profile_entry",
+    "tm_encoder_fwd", "tm_edge_importance", "tm_edge_gate_table", "tm_edge_importance_tab", "tm_tgn_attn_fwd",
+    "tm_tgn_attn_bwd", "tm_mask_least_important", "tm_profile_enable", "tm_profile_sync", "tm_profile_entry",
 )
 
 
 class TmRng(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("split", C.c_uint32), ("side", C.c_uint32)]
+
+
+class TgnAttn(C.Structure):
+    """tm_tgn_attn (include/tempme.h)."""
+    _fields_ = [("rows", C.c_int32), ("n_ngh", C.c_int32), ("n_head", C.c_int32),
+                ("d_node", C.c_int32), ("d_edge", C.c_int32), ("d_time", C.c_int32),
+                ("node_rows", C.c_int32), ("edge_rows", C.c_int32), ("head_major_rows", C.c_int32),
+                ("seg_rows", C.c_int32),
+                ("temperature", C.c_float),
+                ("node_tab", C.c_void_p), ("node_idx", C.c_void_p), ("edge_tab", C.c_void_p),
+                ("edge_idx", C.c_void_p), ("dt", C.c_void_p), ("time_w", C.c_void_p), ("time_b", C.c_void_p),
+                ("mask_node", C.c_void_p), ("ew", C.c_void_p), ("qf", C.c_void_p), ("err_flag", C.c_void_p)]
 
 
 class TempMEError(RuntimeError):
@@ -74,6 +87,9 @@ def _sig(L):
     L.tm_edge_importance.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.tm_edge_gate_table.argtypes = [vp, vp, vp, vp, vp]
     L.tm_edge_importance_tab.argtypes = [vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.tm_tgn_attn_fwd.argtypes = [C.POINTER(TgnAttn), vp, vp, vp]
+    L.tm_tgn_attn_bwd.argtypes = [C.POINTER(TgnAttn), vp, vp, vp, vp, vp]
+    L.tm_mask_least_important.argtypes = [vp, i32, i32, vp, i32, vp, vp, vp]
     L.tm_profile_enable.argtypes = [C.c_int]
     L.tm_profile_entry.argtypes = [C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(i64)]
     for name in EXPORTS:

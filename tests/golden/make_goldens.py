@@ -70,7 +70,9 @@ def _scatter(src, index, dim=-1, out=None, dim_size=None, reduce="sum"):
 
 tsc.scatter = _scatter
 sys.modules["torch_scatter"] = tsc
-sys.modules["turtle"] = types.ModuleType("turtle")
+_turtle = types.ModuleType("turtle")
+_turtle.pos = _turtle.position = None     # names imported (unused) by TGN/tgn.py:2, embedding_module.py:1
+sys.modules["turtle"] = _turtle
 
 
 class _FakeH5File:
@@ -371,21 +373,10 @@ USED_PREFIXES = ("event_conv.", "attention.W1.", "attention.W2.", "attention.MLP
                  "edge_dependency_gcn.", "time_encoder.")
 
 
-def case_encoder():
-    from models.explainer_new import TempME
+def _enc_batch(n_deg=20, bsz=32):
+    """The first `bsz` test events of uslegis_pipeline.npz through the reference's own H5 pack
+    loader (data_preprocess.py:393-404 layout, batch_loader.py:120-242)."""
     pipe = np.load(os.path.join(HERE, "uslegis_pipeline.npz"))
-    n_deg, bsz = 20, 32
-    e_raw = np.load(os.path.join(REF, "processed", "ml_uslegis_sampled.npy"))
-    n_raw = np.load(os.path.join(REF, "processed", "ml_uslegis_sampled_node.npy"))
-    # the shipped edge table has 8832 rows for idx 1..8832 (sampling/sample_dataset.py:110-111);
-    # pad one zero row so every idx is addressable
-    e_pad = np.vstack([e_raw, np.zeros((1, e_raw.shape[1]))])
-    rs = np.random.RandomState(5)
-    feats = {
-        "uslegis": (n_raw, e_pad, 0),
-        "synth": (rs.uniform(0, 1, (n_raw.shape[0], 172)), rs.uniform(0, 1, (e_pad.shape[0], 32)), 1),
-    }
-    # rebuild the H5 pack layout the reference loads (data_preprocess.py:393-404, batch_loader.py:120-201)
     st = {}
     for side in ("src", "tgt", "bgd"):
         for h in (0, 1):
@@ -406,9 +397,30 @@ def case_encoder():
     pack = load_subgraph_margin(args, _FakeH5File("enc_pack"))
     edge = pipe[f"test_N{n_deg}_edge"].astype(np.float64)
     batch_idx = np.arange(bsz)
-    sg_s, sg_t, sg_b, w_s, w_t, w_b, dst_fake = get_item(pack, batch_idx)
-    e_s, e_t, e_b = get_item_edge(edge, batch_idx)
+    items = get_item(pack, batch_idx)
+    edges = get_item_edge(edge, batch_idx)
     ts_cut = pipe["test_ts"][:bsz].astype(np.float64)
+    return pipe, items, edges, ts_cut, batch_idx
+
+
+def _uslegis_feats():
+    e_raw = np.load(os.path.join(REF, "processed", "ml_uslegis_sampled.npy"))
+    n_raw = np.load(os.path.join(REF, "processed", "ml_uslegis_sampled_node.npy"))
+    # the shipped edge table has 8832 rows for idx 1..8832 (sampling/sample_dataset.py:110-111);
+    # pad one zero row so every idx is addressable
+    e_pad = np.vstack([e_raw, np.zeros((1, e_raw.shape[1]))])
+    rs = np.random.RandomState(5)
+    return {
+        "uslegis": (n_raw, e_pad, 0),
+        "synth": (rs.uniform(0, 1, (n_raw.shape[0], 172)), rs.uniform(0, 1, (e_pad.shape[0], 32)), 1),
+    }
+
+
+def case_encoder():
+    from models.explainer_new import TempME
+    n_deg, bsz = 20, 32
+    feats = _uslegis_feats()
+    pipe, (sg_s, sg_t, sg_b, w_s, w_t, w_b, dst_fake), (e_s, e_t, e_b), ts_cut, batch_idx = _enc_batch(n_deg, bsz)
     res = {"ts_cut": ts_cut, "batch_idx": batch_idx}
     for name, (nf, ef, seed) in feats.items():
         torch.manual_seed(seed)
@@ -436,8 +448,129 @@ def case_encoder():
     save_npz("encoder_uslegis.npz", **res)
 
 
+
+def load_ref_function(relpath, name, **ns):
+    """One FunctionDef of a reference module whose body cannot be imported (temp_exp_main.py
+    parses argv and loads checkpoints at module level); line numbers kept."""
+    path = os.path.join(REF, relpath)
+    tree = ast.parse(open(path).read(), path)
+    fn = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == name]
+    ns.setdefault("__name__", "golden_" + name)
+    exec(compile(ast.Module(body=fn, type_ignores=[]), path, "exec"), ns)
+    return ns[name]
+
+
+TGN_SEEDS = {"uslegis": 11, "synth": 12}
+TGN_RATIOS = [0.01, 0.02, 0.04, 0.06, 0.08, 0.10, 0.12, 0.14, 0.16, 0.18, 0.2, 0.22, 0.24, 0.26, 0.28, 0.30]
+TGN_MSG_NODES = (3, 17, 42, 100, 101)
+
+
+def tgn_perturbation(name, n_nodes, dim, raw_dim):
+    """Memory state, last_update, TimeEncode bias and stored raw messages put on the random-init
+    base model so that memory (tgn.py:104-108), the time-encoder bias and the message path of
+    get_updated_memory (tgn.py:237-248) are all exercised.  Committed as data."""
+    rng = np.random.default_rng(TGN_SEEDS[name])
+    out = {
+        "memory": rng.normal(0, 0.5, (n_nodes, dim)).astype(np.float32),
+        "last_update": np.floor(rng.uniform(0, 10, n_nodes)).astype(np.float32),
+        "time_bias": rng.normal(0, 0.5, dim).astype(np.float32),
+        "msg_nodes": np.array(TGN_MSG_NODES, dtype=np.int64),
+        # two messages per node; the "last" aggregator keeps the second (message_aggregator.py:40-46)
+        "msg_raw": rng.normal(0, 1.0, (len(TGN_MSG_NODES), 2, raw_dim)).astype(np.float32),
+        "msg_ts": np.floor(rng.uniform(0, 12, (len(TGN_MSG_NODES), 2))).astype(np.float32),
+    }
+    return out
+
+
+def case_tgn():
+    """Base TGN contrast (TGN/tgn.py:201-218) with and without TempME explanation weights, with
+    explicit edge features (embedding_update_attr), and threshold_test (temp_exp_main.py:153-272)."""
+    from TGN.tgn import TGN
+    from sklearn.metrics import average_precision_score, roc_auc_score
+    import math
+    threshold_test = load_ref_function("temp_exp_main.py", "threshold_test", math=math, np=np, torch=torch,
+                                       average_precision_score=average_precision_score,
+                                       roc_auc_score=roc_auc_score)
+    enc = np.load(os.path.join(HERE, "encoder_uslegis.npz"))
+    n_deg, bsz = 20, 32
+    pipe, (sg_s, sg_t, sg_b, _, _, _, dst_fake), _, ts_cut, _ = _enc_batch(n_deg, bsz)
+    src, dst = pipe["test_src"][:bsz], pipe["test_dst"][:bsz]
+    e_l = pipe["test_eidx"][:bsz]
+    res = {}
+    for name, (nf, ef, _) in _uslegis_feats().items():
+        torch.manual_seed(TGN_SEEDS[name])
+        # learn_base.py:175-176 with its defaults (--n_layer 3, --n_head 2, --drop_out 0.5)
+        base = TGN(nf, ef, n_neighbors=n_deg, device=torch.device("cpu"), n_layers=3, n_heads=2, dropout=0.5)
+        base.forbidden_memory_update = True       # temp_exp_main.py:703-704
+        base.eval()
+        for k, v in base.state_dict().items():
+            v = v.detach().double()
+            res[f"{name}_sd_{k}"] = np.array([v.sum().item(), v.abs().sum().item(), (v * v).sum().item()])
+        dim = base.n_node_features
+        raw_dim = 2 * dim + base.n_edge_features + dim
+        pert = tgn_perturbation(name, base.n_nodes, dim, raw_dim)
+        with torch.no_grad():
+            base.memory.memory.data.copy_(torch.from_numpy(pert["memory"]))
+            base.memory.last_update.data.copy_(torch.from_numpy(pert["last_update"]))
+            base.time_encoder.w.bias.data.copy_(torch.from_numpy(pert["time_bias"]))
+        for i, nd in enumerate(pert["msg_nodes"]):
+            base.memory.messages[int(nd)] = [(torch.from_numpy(pert["msg_raw"][i, m]),
+                                              torch.tensor(pert["msg_ts"][i, m])) for m in range(2)]
+        for k, v in pert.items():
+            res[f"{name}_pert_{k}"] = v
+        expl = [torch.from_numpy(enc[f"{name}_expl0"]), torch.from_numpy(enc[f"{name}_expl1"])]
+        rng = np.random.default_rng(100 + TGN_SEEDS[name])
+        ew_rand = [rng.uniform(0, 1, tuple(e.shape)).astype(np.float32) for e in expl]
+        ew_rand[0][rng.uniform(0, 1, ew_rand[0].shape) < 0.2] = 0.0
+        res[f"{name}_ew_rand0"], res[f"{name}_ew_rand1"] = ew_rand
+        with torch.no_grad():
+            upd_mem, _ = base.get_updated_memory(list(range(base.n_nodes)), base.memory.messages)
+            res[f"{name}_updated_memory"] = upd_mem.numpy()
+            pos_o, neg_o = base.contrast(src, dst, dst_fake, ts_cut, e_l, sg_s, sg_t, sg_b)
+            pos_e, neg_e = base.contrast(src, dst, dst_fake, ts_cut, e_l, sg_s, sg_t, sg_b, explain_weights=expl)
+            pos_r, neg_r = base.contrast(src, dst, dst_fake, ts_cut, e_l, sg_s, sg_t, sg_b,
+                                         explain_weights=[torch.from_numpy(x) for x in ew_rand])
+        res[f"{name}_ori"] = torch.cat([pos_o, neg_o]).numpy()
+        res[f"{name}_expl"] = torch.cat([pos_e, neg_e]).numpy()
+        res[f"{name}_rand"] = torch.cat([pos_r, neg_r]).numpy()
+        if name == "uslegis":
+            ea = [x.numpy() for x in base.retrieve_edge_features(sg_s, sg_t, sg_b)]
+            ea = [(x + rng.normal(0, 0.25, x.shape)).astype(np.float32) for x in ea]
+            res[f"{name}_edge_attr0"], res[f"{name}_edge_attr1"] = ea
+            with torch.no_grad():
+                pos_a, neg_a = base.contrast(src, dst, dst_fake, ts_cut, e_l, sg_s, sg_t, sg_b, explain_weights=expl,
+                                             edge_attr=[torch.from_numpy(x) for x in ea])
+            res[f"{name}_attr"] = torch.cat([pos_a, neg_a]).numpy()
+
+        # threshold_test, capturing every masked-subgraph contrast it makes
+        y_ori = torch.where(torch.cat([pos_o, neg_o]).sigmoid() > 0.5, 1., 0.).view(-1, 1)
+        calls = []
+        orig = base.contrast
+
+        def capture(*a, **k):
+            out = orig(*a, **k)
+            calls.append((np.concatenate(a[5][0], axis=1) == 0, np.concatenate(a[6][0], axis=1) == 0,
+                          np.concatenate(a[7][0], axis=1) == 0, torch.cat(out).numpy()))
+            return out
+        base.contrast = capture
+
+        class A:
+            pass
+        args = A()
+        args.ratios, args.base_type, args.n_degree, args.bs = TGN_RATIOS, "tgn", n_deg, bsz
+        metrics = threshold_test(args, expl, base, src, dst, dst_fake, ts_cut, e_l, pos_o, neg_o, y_ori,
+                                 sg_s, sg_t, sg_b)
+        base.contrast = orig
+        res[f"{name}_thr_metrics"] = np.array([float(m) for m in metrics])
+        res[f"{name}_thr_logits"] = np.stack([c[3] for c in calls])
+        res[f"{name}_thr_zero_bits"] = np.packbits(np.stack([np.concatenate(c[:3], axis=0) for c in calls]))
+        print(name, "ori", float(res[f"{name}_ori"].mean()), "expl", float(res[f"{name}_expl"].mean()),
+              "thr", res[f"{name}_thr_metrics"])
+    res["ratios"] = np.array(TGN_RATIOS)
+    save_npz("tgn_uslegis.npz", **res)
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["kats", "small", "uslegis", "null", "encoder"]
+    which = sys.argv[1:] or ["kats", "small", "uslegis", "null", "encoder", "tgn"]
     if "kats" in which:
         case_kats()
     if "small" in which:
@@ -448,3 +581,5 @@ if __name__ == "__main__":
         case_null()
     if "encoder" in which:
         case_encoder()
+    if "tgn" in which:
+        case_tgn()
