@@ -1,0 +1,122 @@
+"""Explainer training-step throughput (BASELINE.json configs[3]: full Enron + TGN,
+target-edge batches sharded across GPUs with one RCCL gradient all-reduce per step).
+
+    python bench_train.py [--gpus N --steps K --warmup W --n-degree 20 --batch-size 100]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench_train.py --gpus N
+
+One step = temp_exp_main.py:593-632 for one batch of `--batch-size` target events per GPU: base
+contrast without explanation (no grad), TempME forward x3 (training mode: dropout, Beta rsample),
+retrieve_explanation, contrast with explanation weights, BCE + 0.5 KL, backward, gradient all-reduce,
+Adam.  The pack (k-hop subgraphs, walks, categories, edge counts of every training event) is sampled
+on the device before timing, as the reference samples it offline (processed/data_preprocess.py).
+Prints one JSON line (rank 0); value = trained target edges per second over all ranks.
+"""
+import argparse
+import json
+import os
+import time
+
+import numpy as np
+import torch
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch-size", type=int, default=100, help="temp_exp_main --bs")
+    ap.add_argument("--n-degree", type=int, default=20)
+    ap.add_argument("--alpha", type=float, default=1.2)
+    ap.add_argument("--seed", type=int, default=0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("TEMPME_DIST_BACKEND", "nccl")
+    dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
+    torch.cuda.set_device(dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+
+    import tempme_amd as tm
+    from tempme_amd import _lib as L
+    from tempme_amd.preprocess import sample_events
+    from tempme_amd.sharding import max_over_ranks
+    from tempme_amd.tgn import TGN
+    from tempme_amd.train import GradAllReduce, batch_from_pack, epoch_spans, train_step
+    from tempme_amd.workload import enron_like, split
+
+    N, M, B = args.n_degree, 3, args.batch_size
+    g = enron_like(n_nodes=184, n_edges=125235, alpha=args.alpha, seed=args.seed)     # full Enron shape
+    (src, dst, ts, eidx), rows, pool = split(g, mode="train")
+    finder = tm.NeighborFinder.from_edges(g["src"][rows], g["dst"][rows], g["eidx"][rows], g["ts"][rows],
+                                          g["n_nodes"], device=dev, seed=args.seed, split=tm.SPLIT_TRAIN)
+    to = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)  # noqa: E731
+    s_d, d_d, t_d, e_d = to(src, np.int32), to(dst, np.int32), to(ts, np.float64), to(eidx, np.int32)
+    ev = torch.arange(len(src), dtype=torch.int32, device=dev)
+    buf = sample_events(finder.graph, args.seed, tm.SPLIT_TRAIN, N, M, s_d, d_d, t_d, e_d, ev,
+                        to(pool, np.int32))
+
+    torch.manual_seed(args.seed)          # identical replicas on every rank
+    base = TGN(g["n_feat"], g["e_feat"], n_neighbors=N, device=dev, n_layers=2, n_heads=2, dropout=0.1)
+    base.forbidden_memory_update = True
+    base = base.to(dev).eval()
+    ex = tm.TempME(base, "tgn", "enron", out_dim=40, hid_dim=64, device=dev,
+                   null_model={k: 1.0 / 12 for k in range(1, 13)}).to(dev)
+    opt = torch.optim.Adam(ex.parameters(), lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0)
+    sync = GradAllReduce(ex)
+    ex.train()
+
+    n_steps = args.warmup + args.steps
+    gen = torch.Generator().manual_seed(args.seed)
+    spans = []
+    while len(spans) < n_steps:
+        perm = torch.randperm(len(src) - 1, generator=gen).to(dev)
+        spans += [(perm, a, b) for a, b in epoch_spans(len(src) - 1, B, rank, world)]
+    batches = [batch_from_pack(buf, s_d, d_d, t_d, e_d, perm[a:b]) for perm, a, b in spans[:n_steps]]
+
+    for k in range(args.warmup):
+        train_step(ex, base, opt, batches[k], grad_sync=sync)
+    torch.cuda.synchronize()
+    base.check_errors()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    L.profile_enable(True)
+    t0 = time.perf_counter()
+    outs = [train_step(ex, base, opt, batches[k], grad_sync=sync) for k in range(args.warmup, n_steps)]
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    prof = L.profile_read()
+    L.profile_enable(False)
+    el = max_over_ranks(el, dist, dev if backend == "nccl" else "cpu")
+    losses = [float(o["loss"]) for o in outs]
+    if rank == 0:
+        edges = sum(len(batches[k]) for k in range(args.warmup, n_steps)) * world
+        out = {"metric": "trained target-edges/sec (explainer training step, TGN + full-Enron-shaped graph)",
+               "value": round(edges / el, 2), "unit": "edges/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+               "data": "synthetic (seeded Enron-shaped graph V=184 E=125,235, random-init TGN and TempME)",
+               "config": {"workload": "configs[3]: full Enron + TGN explainer training step", "n_degree": N,
+                          "batch_size": B, "train_events": int(len(src)), "parallelism": f"dp{world}",
+                          "grad_bucket_floats": sum(p.numel() for p in ex.parameters() if p.grad is not None)},
+               "loss_first_last": [round(losses[0], 5), round(losses[-1], 5)],
+               "kernels": {k: {"avg_ms": round(ms / max(c, 1), 4), "launches": c} for k, (ms, c) in prof.items()}}
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -151,6 +151,11 @@ class TempME(nn.Module):
     def _dev(self):
         return L.require_device(self.device)
 
+    def _needs_autograd(self):
+        """Training mode, or a forward whose result must carry gradients to the explainer's
+        parameters (temp_exp_main.py:605-631): the autograd formulation runs then."""
+        return self.training or (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()))
+
     def _hip_ok(self):
         return (self.use_temporal_guidance and self.use_dependency_aware_sampling and self.if_cat
                 and self.hid_dim == 64)
@@ -224,7 +229,7 @@ class TempME(nn.Module):
         dev = self._dev()
         B, W = np.shape(edge_idx)[0], np.shape(edge_idx)[1]
         assert np.shape(edge_identify)[-1] == 3 and np.shape(edge_idx)[-1] == 3, "event_dim mismatch (:180)"
-        if self.training or not self._hip_ok():
+        if self._needs_autograd() or not self._hip_ok():
             return self._forward_torch(walks, cut_time_l, edge_identify)
         out = self.encoder_fwd(_to(node_idx, dev, torch.int32).contiguous(), _to(edge_idx, dev, torch.int32).contiguous(),
                                _to(time_idx, dev, torch.float32).contiguous(),

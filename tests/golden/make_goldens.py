@@ -482,10 +482,31 @@ def tgn_perturbation(name, n_nodes, dim, raw_dim):
     return out
 
 
+def tgn_base(name, nf, ef, n_deg):
+    """The seeded reference TGN of case_tgn with its committed perturbation applied."""
+    from TGN.tgn import TGN
+    torch.manual_seed(TGN_SEEDS[name])
+    # learn_base.py:175-176 with its defaults (--n_layer 3, --n_head 2, --drop_out 0.5)
+    base = TGN(nf, ef, n_neighbors=n_deg, device=torch.device("cpu"), n_layers=3, n_heads=2, dropout=0.5)
+    base.forbidden_memory_update = True       # temp_exp_main.py:703-704
+    base.eval()
+    sd0 = {k: v.detach().clone() for k, v in base.state_dict().items()}
+    dim = base.n_node_features
+    raw_dim = 2 * dim + base.n_edge_features + dim
+    pert = tgn_perturbation(name, base.n_nodes, dim, raw_dim)
+    with torch.no_grad():
+        base.memory.memory.data.copy_(torch.from_numpy(pert["memory"]))
+        base.memory.last_update.data.copy_(torch.from_numpy(pert["last_update"]))
+        base.time_encoder.w.bias.data.copy_(torch.from_numpy(pert["time_bias"]))
+    for i, nd in enumerate(pert["msg_nodes"]):
+        base.memory.messages[int(nd)] = [(torch.from_numpy(pert["msg_raw"][i, m]),
+                                          torch.tensor(pert["msg_ts"][i, m])) for m in range(2)]
+    return base, sd0, pert
+
+
 def case_tgn():
     """Base TGN contrast (TGN/tgn.py:201-218) with and without TempME explanation weights, with
     explicit edge features (embedding_update_attr), and threshold_test (temp_exp_main.py:153-272)."""
-    from TGN.tgn import TGN
     from sklearn.metrics import average_precision_score, roc_auc_score
     import math
     threshold_test = load_ref_function("temp_exp_main.py", "threshold_test", math=math, np=np, torch=torch,
@@ -498,24 +519,10 @@ def case_tgn():
     e_l = pipe["test_eidx"][:bsz]
     res = {}
     for name, (nf, ef, _) in _uslegis_feats().items():
-        torch.manual_seed(TGN_SEEDS[name])
-        # learn_base.py:175-176 with its defaults (--n_layer 3, --n_head 2, --drop_out 0.5)
-        base = TGN(nf, ef, n_neighbors=n_deg, device=torch.device("cpu"), n_layers=3, n_heads=2, dropout=0.5)
-        base.forbidden_memory_update = True       # temp_exp_main.py:703-704
-        base.eval()
-        for k, v in base.state_dict().items():
-            v = v.detach().double()
+        base, sd0, pert = tgn_base(name, nf, ef, n_deg)
+        for k, v in sd0.items():
+            v = v.double()
             res[f"{name}_sd_{k}"] = np.array([v.sum().item(), v.abs().sum().item(), (v * v).sum().item()])
-        dim = base.n_node_features
-        raw_dim = 2 * dim + base.n_edge_features + dim
-        pert = tgn_perturbation(name, base.n_nodes, dim, raw_dim)
-        with torch.no_grad():
-            base.memory.memory.data.copy_(torch.from_numpy(pert["memory"]))
-            base.memory.last_update.data.copy_(torch.from_numpy(pert["last_update"]))
-            base.time_encoder.w.bias.data.copy_(torch.from_numpy(pert["time_bias"]))
-        for i, nd in enumerate(pert["msg_nodes"]):
-            base.memory.messages[int(nd)] = [(torch.from_numpy(pert["msg_raw"][i, m]),
-                                              torch.tensor(pert["msg_ts"][i, m])) for m in range(2)]
         for k, v in pert.items():
             res[f"{name}_pert_{k}"] = v
         expl = [torch.from_numpy(enc[f"{name}_expl0"]), torch.from_numpy(enc[f"{name}_expl1"])]
@@ -569,8 +576,55 @@ def case_tgn():
     res["ratios"] = np.array(TGN_RATIOS)
     save_npz("tgn_uslegis.npz", **res)
 
+
+def case_train():
+    """One deterministic iteration of the explainer training loop (temp_exp_main.py:584-632) with the
+    reference TempME on the reference TGN: Explainer.eval() (dropout off) and if_bern=False (Beta mean),
+    so loss, gradients and the Adam step are reproducible.  Stores the losses, every gradient that
+    reaches the explainer and the parameter update of the Adam step."""
+    from models.explainer_new import TempME
+    n_deg, bsz = 20, 32
+    pipe, (sg_s, sg_t, sg_b, w_s, w_t, w_b, dst_fake), (e_s, e_t, e_b), ts_cut, _ = _enc_batch(n_deg, bsz)
+    src, dst = pipe["test_src"][:bsz], pipe["test_dst"][:bsz]
+    e_l = pipe["test_eidx"][:bsz]
+    res = {}
+    for name, (nf, ef, seed) in _uslegis_feats().items():
+        base, _, _ = tgn_base(name, nf, ef, n_deg)
+        torch.manual_seed(seed)
+        CTX.update(seed=0, split=px.SPLIT_NULL)
+        ex = TempME(base, base_model_type="tgn", data="uslegis_sampled", out_dim=40, hid_dim=64, temp=0.07,
+                    if_cat_feature=True, dropout_p=0.1, device=torch.device("cpu"))
+        opt = torch.optim.Adam(ex.parameters(), lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0)
+        criterion = torch.nn.BCEWithLogitsLoss()
+        p0 = {k: v.detach().clone() for k, v in ex.named_parameters()}
+        ex.eval()
+        with torch.no_grad():
+            pos_o, neg_o = base.contrast(src, dst, dst_fake, ts_cut, e_l, sg_s, sg_t, sg_b)
+            y_ori = torch.where(torch.cat([pos_o, neg_o], dim=0).sigmoid() > 0.5, 1., 0.).view(-1, 1)
+        opt.zero_grad()
+        g_s, g_t, g_b = ex(w_s, ts_cut, e_s), ex(w_t, ts_cut, e_t), ex(w_b, ts_cut, e_b)
+        expl = ex.retrieve_explanation(sg_s, g_s, w_s, sg_t, g_t, w_t, sg_b, g_b, w_b, training=False)
+        pos, neg = base.contrast(src, dst, dst_fake, ts_cut, e_l, sg_s, sg_t, sg_b, explain_weights=expl)
+        pred_loss = criterion(torch.cat([pos, neg], dim=0), y_ori)
+        kl = ex.kl_loss(g_s, w_s, target=0.3) + ex.kl_loss(g_t, w_t, target=0.3) + ex.kl_loss(g_b, w_b, target=0.3)
+        loss = pred_loss + 0.5 * kl
+        loss.backward()
+        opt.step()
+        res[f"{name}_losses"] = np.array([loss.item(), pred_loss.item(), kl.item()])
+        res[f"{name}_logits"] = torch.cat([pos, neg]).detach().numpy()
+        n_grad = 0
+        for k, v in ex.named_parameters():
+            if v.grad is None:
+                continue
+            n_grad += v.numel()
+            res[f"{name}_grad_{k}"] = v.grad.numpy().astype(np.float32)
+            if name == "uslegis":
+                res[f"{name}_upd_{k}"] = (v.detach() - p0[k]).numpy().astype(np.float32)
+        print(name, "loss", res[f"{name}_losses"], "params with grad", n_grad)
+    save_npz("train_uslegis.npz", **res)
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["kats", "small", "uslegis", "null", "encoder", "tgn"]
+    which = sys.argv[1:] or ["kats", "small", "uslegis", "null", "encoder", "tgn", "train"]
     if "kats" in which:
         case_kats()
     if "small" in which:
@@ -583,3 +637,5 @@ if __name__ == "__main__":
         case_encoder()
     if "tgn" in which:
         case_tgn()
+    if "train" in which:
+        case_train()

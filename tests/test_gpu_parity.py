@@ -229,7 +229,8 @@ def test_encoder_matches_reference_goldens(tm, case):
     for s in SIDES:
         x = d[s]
         w = (x["node"], x["eid"], x["ts"], x["cat"], x["marg"])
-        imp = ex(w, d["ts_cut"], x["cnt"])
+        with torch.no_grad():        # eval_one_epoch scores under no_grad (temp_exp_main.py:446-452)
+            imp = ex(w, d["ts_cut"], x["cnt"])
         np.testing.assert_allclose(imp.cpu().numpy(), x["imp"], rtol=RTOL, atol=ATOL)
         imps.append(imp)
         subs.append((x["sub_node"], x["sub_eid"], x["sub_ts"]))

@@ -1,0 +1,88 @@
+"""GPU parity of the explainer training step (temp_exp_main.py:584-632) against one
+deterministic iteration of the reference (tests/golden/train_uslegis.npz, make_goldens.py case_train:
+reference TempME on the reference TGN, Explainer.eval(), if_bern=False, Adam lr 1e-3): losses,
+logits, every gradient that reaches the explainer (115,554 values at uslegis dims) and the Adam
+update.  The stochastic configuration (dropout, Beta rsample) is checked for shape and finiteness."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import tgn_inputs as TI
+from tests.encoder_inputs import SIDES, load as load_enc
+
+pytestmark = pytest.mark.gpu
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+EX_SEEDS = {"uslegis": 0, "synth": 1}
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a HIP device")
+    return torch.device("cuda", 0)
+
+
+def _setup(case, dev):
+    from tempme_amd import TempME
+    from tempme_amd.train import Batch
+    base = TI.build_model(case).to(dev)
+    enc = load_enc(case)
+    torch.manual_seed(EX_SEEDS[case])
+    ex = TempME(base, "tgn", "uslegis_sampled", out_dim=40, hid_dim=64, temp=0.07, if_cat_feature=True,
+                dropout_p=0.1, device=dev, null_model={k + 1: float(v) for k, v in enumerate(enc["null"])})
+    missing, unexpected = ex.load_state_dict(enc["sd"], strict=False)
+    assert not unexpected
+    ex = ex.to(dev)
+    d = TI.load_batch()
+    walks = [(enc[s]["node"], enc[s]["eid"], enc[s]["ts"], enc[s]["cat"], enc[s]["marg"]) for s in SIDES]
+    batch = Batch(d["src"], d["dst"], d["ts_cut"], d["e_idx"], d["fake"], [d["sg_" + s] for s in SIDES], walks,
+                  [enc[s]["cnt"] for s in SIDES])
+    opt = torch.optim.Adam(ex.parameters(), lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0)
+    return base, ex, batch, opt
+
+
+@pytest.mark.parametrize("case", ["uslegis", "synth"])
+def test_train_step_matches_reference(dev, case):
+    from tempme_amd.train import train_step
+    g = np.load(os.path.join(G, "train_uslegis.npz"))
+    base, ex, batch, opt = _setup(case, dev)
+    p0 = {k: v.detach().clone() for k, v in ex.named_parameters()}
+    ex.eval()
+    out = train_step(ex, base, opt, batch, beta=0.5, prior_p=0.3, if_bern=False)
+    got = np.array([out["loss"].item(), out["pred_loss"].item(), out["kl_loss"].item()])
+    np.testing.assert_allclose(got, g[f"{case}_losses"], rtol=1e-5, atol=1e-6)
+    logits = torch.cat([out["pos_logit"], out["neg_logit"]]).cpu().numpy()
+    np.testing.assert_allclose(logits, g[f"{case}_logits"], atol=2e-5, rtol=1e-5)
+    ref_keys = {k[len(case) + 6:] for k in g.files if k.startswith(f"{case}_grad_")}
+    got_keys = {k for k, v in ex.named_parameters() if v.grad is not None}
+    assert got_keys == ref_keys
+    for k, v in ex.named_parameters():
+        if k not in ref_keys:
+            continue
+        gr = g[f"{case}_grad_{k}"].astype(np.float64)
+        ga = v.grad.detach().cpu().numpy().astype(np.float64)
+        scale = np.abs(gr).max()
+        assert np.linalg.norm(ga - gr) <= 2e-4 * np.linalg.norm(gr) + 1e-9, k
+        assert np.abs(ga - gr).max() <= 1e-8 + 2e-4 * scale, k
+        if f"{case}_upd_{k}" in g.files:
+            upd = (v.detach() - p0[k]).cpu().numpy()
+            ref = g[f"{case}_upd_{k}"]
+            sure = np.abs(gr) > max(1e-3 * scale, 1e-7)      # Adam's first step is ~lr*sign(g)
+            np.testing.assert_allclose(upd[sure], ref[sure], atol=2e-6, rtol=1e-3, err_msg=k)
+
+
+def test_stochastic_train_step_runs(dev):
+    from tempme_amd.train import train_step
+    base, ex, batch, opt = _setup("uslegis", dev)
+    ex.train()
+    before = {k: v.detach().clone() for k, v in ex.named_parameters()}
+    out = train_step(ex, base, opt, batch, if_bern=True)
+    assert torch.isfinite(out["loss"]).item()
+    n_grad = sum(v.grad.numel() for v in ex.parameters() if v.grad is not None)
+    assert n_grad == 115554
+    changed = sum(int((v.detach() != before[k]).any()) for k, v in ex.named_parameters())
+    assert changed > 0
+    assert all(p.grad is None for p in base.parameters())

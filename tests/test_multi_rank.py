@@ -112,3 +112,68 @@ def test_gloo_two_ranks_match_single_process():
         for k, v in full.items():
             got = np.concatenate([gathered[r][step][k] for r in range(world)])
             assert np.array_equal(got, v), k
+
+
+# ------------------------------------------------------------------ explainer gradient all-reduce (a15)
+def test_epoch_spans_deal_whole_batches():
+    from tempme_amd.train import epoch_spans
+    one = epoch_spans(1000, 100)
+    assert one[0] == (0, 100) and one[-1] == (900, 999)          # temp_exp_main.py:584-590 bounds
+    for world in (2, 4, 8):
+        per = [epoch_spans(1000, 100, r, world) for r in range(world)]
+        assert len({len(p) for p in per}) == 1                     # same number of all-reduced steps
+        got = sorted(sp for p in per for sp in p)
+        assert got == one[:len(one) - len(one) % world]
+
+
+def _grad_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tempme_amd.train import GradAllReduce
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(torch.nn.Linear(5, 7), torch.nn.ReLU(), torch.nn.Linear(7, 1),
+                                  torch.nn.Linear(3, 3))                  # last layer gets no gradient
+        opt = torch.optim.Adam(net.parameters(), lr=1e-2)
+        sync = GradAllReduce(net)
+        for step in range(3):
+            x = torch.randn(4, 5, generator=torch.Generator().manual_seed(100 * step + rank))
+            opt.zero_grad()
+            net[2](net[1](net[0](x))).pow(2).mean().backward()
+            local = [p.grad.clone() if p.grad is not None else None for p in net.parameters()]
+            sync()
+            synced = [p.grad.clone() if p.grad is not None else None for p in net.parameters()]
+            opt.step()
+            gl = [None] * world
+            dist.all_gather_object(gl, local)
+            if rank == 0:
+                for i, s in enumerate(synced):
+                    if s is None:
+                        assert all(g[i] is None for g in gl)
+                        continue
+                    torch.testing.assert_close(s, sum(g[i] for g in gl) / world)
+        params = [None] * world
+        dist.all_gather_object(params, [p.detach().clone() for p in net.parameters()])
+        if rank == 0:
+            for a, b in zip(params[0], params[1]):
+                assert torch.equal(a, b)                                  # replicas stay identical
+            q.put("ok")
+    except Exception as exc:
+        q.put(repr(exc))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_all_reduce_two_ranks():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grad_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == "ok", res
+    assert all(p.exitcode == 0 for p in procs)

@@ -17,7 +17,7 @@ step() {  # step <name> <timeout_s> <cmd...>
 for s in "$@"; do
     case $s in
         tests) step pytest_gpu 900 python -m pytest tests -x -q -m gpu ;;
-        tgn) step pytest_tgn 600 python -m pytest tests/test_gpu_tgn.py -x -q -m gpu ;;
+        tgn) step pytest_tgn 600 python -m pytest tests/test_gpu_tgn.py tests/test_gpu_train.py -x -q -m gpu ;;
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) step bench 600 python bench.py --steps 10 --warmup 2 ;;
         benchq) step bench 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
@@ -54,6 +54,10 @@ for s in "$@"; do
         dist2)  # multi-rank rehearsal on one GPU: 2 ranks, gloo barrier/all-reduce, both on cuda:0
             TEMPME_DIST_BACKEND=gloo step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu-baseline ;;
+        train) step bench_train 600 python bench_train.py --steps 10 --warmup 2 ;;
+        train2)  # 2-rank rehearsal of the gradient all-reduce on one GPU (gloo)
+            TEMPME_DIST_BACKEND=gloo step bench_train2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+                --master-addr 127.0.0.1 --master-port 29512 bench_train.py --gpus 2 --steps 5 --warmup 1 ;;
         n30) step bench_n30 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --n-degree 30 ;;
         a3) step bench_a3 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --alpha 3.0 ;;
         *) echo "unknown step $s"; exit 2 ;;
