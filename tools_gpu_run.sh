@@ -54,6 +54,7 @@ for s in "$@"; do
         dist2)  # multi-rank rehearsal on one GPU: 2 ranks, gloo barrier/all-reduce, both on cuda:0
             TEMPME_DIST_BACKEND=gloo step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu-baseline ;;
+        proftrain) step rocprof_train 600 rocprofv3 --kernel-trace --stats -d gpurun_out/proftrain -o run --output-format csv -- python bench_train.py --steps 10 --warmup 2 ;;
         train) step bench_train 600 python bench_train.py --steps 10 --warmup 2 ;;
         train2)  # 2-rank rehearsal of the gradient all-reduce on one GPU (gloo)
             TEMPME_DIST_BACKEND=gloo step bench_train2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
