@@ -1,5 +1,5 @@
-"""Fidelity evaluation of an explanation on the base TGN: ``threshold_test``
-(temp_exp_main.py:153-272, tgn branch) on the HIP device.
+"""Fidelity evaluation of an explanation on the base model: ``threshold_test``
+(temp_exp_main.py:153-272, tgn and graphmixer branches) on the HIP device.
 
 For each sparsity ratio the reference keeps the top ``ceil(ratio * (N + N^2))`` subgraph entries by
 explanation score, zeroes the node ids of the rest (torch.topk(largest=False) + np.put_along_axis),
@@ -21,11 +21,13 @@ from . import _lib as L
 from .tgn import _as_dev
 
 
-def _masked_nodes(explanation, subgraphs, N, ratios, dev):
-    """[G, 3B, N+N^2] int32 node records with the least important entries of each ratio set to 0."""
-    ne = N + N * N
-    imp = torch.cat([explanation[0], explanation[1]], dim=1).to(dev, torch.float32).contiguous()
-    nodes = torch.cat([torch.cat([_as_dev(sg[0][0], dev, torch.int32), _as_dev(sg[0][1], dev, torch.int32)], dim=1)
+def _masked_nodes(explanation, subgraphs, N, ratios, dev, hops=2):
+    """[G, 3B, ne] int32 node records with the least important entries of each ratio set to 0;
+    hops=2: [hop-1 | hop-2] records, ne = N + N^2 (tgn / tgat branches); hops=1: hop-1 records,
+    ne = N (graphmixer branch)."""
+    ne = N + N * N if hops == 2 else N
+    imp = torch.cat(list(explanation[:hops]), dim=1).to(dev, torch.float32).contiguous()
+    nodes = torch.cat([torch.cat([_as_dev(sg[0][h], dev, torch.int32) for h in range(hops)], dim=1)
                        for sg in subgraphs], dim=0).contiguous()
     rows = nodes.shape[0]
     if imp.shape != (rows, ne):
@@ -62,14 +64,36 @@ def masked_contrast(base_model, explanation, src_l_cut, dst_l_cut, dst_l_fake, t
     return score[:, :B], score[:, B:]
 
 
+def masked_contrast_graphmixer(base_model, explanation, src_l_cut, dst_l_cut, dst_l_fake, ts_l_cut, subgraph_src,
+                               subgraph_tgt, subgraph_bgd, n_degree, ratios):
+    """graphmixer branch (temp_exp_main.py:186-206): hop-1 records masked, all ratios in one batch."""
+    dev = base_model._dev()
+    B, N, G = len(src_l_cut), n_degree, len(ratios)
+    sgs = (subgraph_src, subgraph_tgt, subgraph_bgd)
+    masked = _masked_nodes(explanation, sgs, N, ratios, dev, hops=1).reshape(G * 3 * B, N)
+    roots = torch.cat([_as_dev(x, dev, torch.long).reshape(-1) for x in (src_l_cut, dst_l_cut, dst_l_fake)])
+    cut = _as_dev(ts_l_cut, dev, torch.float64).reshape(-1).repeat(3 * G)
+
+    def rep(i, dtype):
+        return torch.cat([_as_dev(sg[i][0], dev, dtype) for sg in sgs], dim=0).repeat(G, 1)
+    emb = base_model.node_embeddings(roots.repeat(G), cut, masked, rep(1, torch.long), rep(2, torch.float64))
+    emb = emb.view(G, 3, B, -1)
+    s, d, n = emb[:, 0], emb[:, 1], emb[:, 2]
+    x1 = torch.cat([s, s], dim=1).reshape(G * 2 * B, -1)
+    x2 = torch.cat([d, n], dim=1).reshape(G * 2 * B, -1)
+    score = base_model.affinity(x1, x2).view(G, 2 * B)
+    return score[:, :B], score[:, B:]
+
+
 def threshold_test(args, explanation, base_model, src_l_cut, dst_l_cut, dst_l_fake, ts_l_cut, e_l_cut,
                    pos_out_ori, neg_out_ori, y_ori, subgraph_src, subgraph_tgt, subgraph_bgd):
     """temp_exp_main.py:153-272 -> (aps_AUC, auc_AUC, acc_AUC, fid_prob_AUC, fid_logit_AUC)."""
-    if args.base_type != "tgn":
-        raise NotImplementedError(f"threshold_test for base_type {args.base_type!r}: only the TGN branch is built")
+    fns = {"tgn": masked_contrast, "graphmixer": masked_contrast_graphmixer}
+    if args.base_type not in fns:
+        raise NotImplementedError(f"threshold_test for base_type {args.base_type!r}: tgn and graphmixer are built")
     with torch.no_grad():
-        pos, neg = masked_contrast(base_model, explanation, src_l_cut, dst_l_cut, dst_l_fake, ts_l_cut, subgraph_src,
-                                   subgraph_tgt, subgraph_bgd, args.n_degree, list(args.ratios))
+        pos, neg = fns[args.base_type](base_model, explanation, src_l_cut, dst_l_cut, dst_l_fake, ts_l_cut,
+                                       subgraph_src, subgraph_tgt, subgraph_bgd, args.n_degree, list(args.ratios))
         po = pos_out_ori.reshape(1, -1).to(pos.device, torch.float32)
         no = neg_out_ori.reshape(1, -1).to(pos.device, torch.float32)
         fid_prob = torch.cat([pos.sigmoid() - po.sigmoid(), no.sigmoid() - neg.sigmoid()], dim=1).mean(1)

@@ -623,8 +623,80 @@ def case_train():
         print(name, "loss", res[f"{name}_losses"], "params with grad", n_grad)
     save_npz("train_uslegis.npz", **res)
 
+
+GM_SEEDS = {"uslegis": 21, "synth": 22}
+
+
+def case_graphmixer():
+    """Base GraphMixer contrast (GraphM/graphmixer.py:106-239) without / with the TempME hop-1
+    explanation, with random weights, with explicit edge features, and threshold_test's graphmixer
+    branch (temp_exp_main.py:186-206) with every masked contrast captured."""
+    from GraphM.graphmixer import GraphMixer
+    from sklearn.metrics import average_precision_score, roc_auc_score
+    import math
+    threshold_test = load_ref_function("temp_exp_main.py", "threshold_test", math=math, np=np, torch=torch,
+                                       average_precision_score=average_precision_score,
+                                       roc_auc_score=roc_auc_score)
+    enc = np.load(os.path.join(HERE, "encoder_uslegis.npz"))
+    n_deg, bsz = 20, 32
+    pipe, (sg_s, sg_t, sg_b, _, _, _, dst_fake), _, ts_cut, _ = _enc_batch(n_deg, bsz)
+    src, dst = pipe["test_src"][:bsz], pipe["test_dst"][:bsz]
+    e_l = pipe["test_eidx"][:bsz]
+    res = {}
+    for name, (nf, ef, _) in _uslegis_feats().items():
+        torch.manual_seed(GM_SEEDS[name])
+        # learn_base.py:178-180 with its defaults (--n_layer 3, --drop_out 0.5)
+        base = GraphMixer(nf, ef, n_neighbors=n_deg, device=torch.device("cpu"), num_tokens=n_deg, num_layers=3,
+                          dropout=0.5)
+        base.eval()
+        for k, v in base.state_dict().items():
+            v = v.detach().double()
+            res[f"{name}_sd_{k}"] = np.array([v.sum().item(), v.abs().sum().item(), (v * v).sum().item()])
+        expl = [torch.from_numpy(enc[f"{name}_expl0"])]
+        rng = np.random.default_rng(200 + GM_SEEDS[name])
+        ew_rand = rng.uniform(0, 1, tuple(expl[0].shape)).astype(np.float32)
+        ew_rand[rng.uniform(0, 1, ew_rand.shape) < 0.2] = 0.0
+        res[f"{name}_ew_rand"] = ew_rand
+        with torch.no_grad():
+            pos_o, neg_o = base.contrast(src, dst, dst_fake, ts_cut, e_l, sg_s, sg_t, sg_b)
+            pos_e, neg_e = base.contrast(src, dst, dst_fake, ts_cut, e_l, sg_s, sg_t, sg_b, explain_weights=expl)
+            pos_r, neg_r = base.contrast(src, dst, dst_fake, ts_cut, e_l, sg_s, sg_t, sg_b,
+                                         explain_weights=[torch.from_numpy(ew_rand)])
+            ea = base.retrieve_edge_features(sg_s, sg_t, sg_b).numpy()
+            ea = (ea + rng.normal(0, 0.25, ea.shape)).astype(np.float32)
+            pos_a, neg_a = base.contrast(src, dst, dst_fake, ts_cut, e_l, sg_s, sg_t, sg_b, explain_weights=expl,
+                                         edge_attr=torch.from_numpy(ea))
+        res[f"{name}_edge_attr"] = ea
+        for tag, (p, n) in (("ori", (pos_o, neg_o)), ("expl", (pos_e, neg_e)), ("rand", (pos_r, neg_r)),
+                            ("attr", (pos_a, neg_a))):
+            res[f"{name}_{tag}"] = torch.cat([p, n]).numpy()
+        y_ori = torch.where(torch.cat([pos_o, neg_o]).sigmoid() > 0.5, 1., 0.).view(-1, 1)
+        calls = []
+        orig = base.contrast
+
+        def capture(*a, **k):
+            out = orig(*a, **k)
+            calls.append((np.concatenate([a[5][0][0], a[6][0][0], a[7][0][0]], axis=0) == 0, torch.cat(out).numpy()))
+            return out
+        base.contrast = capture
+
+        class A:
+            pass
+        args = A()
+        args.ratios, args.base_type, args.n_degree, args.bs = TGN_RATIOS, "graphmixer", n_deg, bsz
+        metrics = threshold_test(args, expl, base, src, dst, dst_fake, ts_cut, e_l, pos_o, neg_o, y_ori,
+                                 sg_s, sg_t, sg_b)
+        base.contrast = orig
+        res[f"{name}_thr_metrics"] = np.array([float(m) for m in metrics])
+        res[f"{name}_thr_logits"] = np.stack([c[1] for c in calls])
+        res[f"{name}_thr_zero_bits"] = np.packbits(np.stack([c[0] for c in calls]))
+        print(name, "ori", float(res[f"{name}_ori"].mean()), "expl", float(res[f"{name}_expl"].mean()),
+              "thr", res[f"{name}_thr_metrics"])
+    res["ratios"] = np.array(TGN_RATIOS)
+    save_npz("graphmixer_uslegis.npz", **res)
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["kats", "small", "uslegis", "null", "encoder", "tgn", "train"]
+    which = sys.argv[1:] or ["kats", "small", "uslegis", "null", "encoder", "tgn", "train", "graphmixer"]
     if "kats" in which:
         case_kats()
     if "small" in which:
@@ -639,3 +711,5 @@ if __name__ == "__main__":
         case_tgn()
     if "train" in which:
         case_train()
+    if "graphmixer" in which:
+        case_graphmixer()
