@@ -1,0 +1,235 @@
+"""The reference's on-disk handoff between preprocessing and the explainer loop.
+
+Files (processed/data_preprocess.py:139-143, :393-404, :416-419):
+
+* ``{data}_{mode}.h5``      subgraph_{src,tgt,bgd}_0 [n, 3N] (node | eid | ts), subgraph_*_1 [n, 3N^2],
+                            walks_{src,tgt,bgd} [n, W, 15] (6 node, 3 eid, 3 ts, 3 anony), dst_fake [n]
+* ``{data}_{mode}_cat.h5``  the same subgraphs and dst_fake, walks_*_new [n, W, 14] (6 node, 3 eid, 3 ts,
+                            cat id, marginal) instead of walks_*
+* ``{data}_{mode}_edge.npy`` [3, n, W, 3, 3] edge-occurrence counts
+
+every array float64, as the reference's h5py round trip leaves them.  Readers mirror
+utils/batch_loader.py: ``load_subgraph`` (:45-116), ``load_subgraph_margin`` (:119-197), ``get_item``
+(:200-235), ``get_item_edge`` (:238-242) -- same argument order, same tuple nesting, same dtypes
+(``.astype(int)`` on node/eid/cat columns, float64 ts / marginal).
+
+Container: HDF5 through h5py when it is importable; this image has no h5py (nor libhdf5), so the
+writer then stores the same dataset names / shapes / dtypes in an ``.npz`` container under the
+reference's file name.  ``open_pack`` sniffs the magic bytes, so either container reads back, and
+``file[name][:]`` (what the reference's loaders do) works on both.
+
+``DevicePack`` is the MI355X side: a pack (from a file or from ``preprocess.pre_processing`` /
+``sample_events`` output) uploaded once into the side-major device layout of
+``preprocess.EventBuffers``, which ``train.batch_from_pack`` and the scoring pipeline slice without
+host round trips.
+"""
+import os
+import zipfile
+
+import numpy as np
+import torch
+
+from .preprocess import SIDES, EventBuffers, anony_from_cat
+
+SUBGRAPH_KEYS = tuple(f"subgraph_{s}_{h}" for s in SIDES for h in (0, 1))
+RAW_KEYS = SUBGRAPH_KEYS + tuple(f"walks_{s}" for s in SIDES) + ("dst_fake",)       # data_preprocess.py:139
+CAT_KEYS = SUBGRAPH_KEYS + tuple(f"walks_{s}_new" for s in SIDES) + ("dst_fake",)   # :393-402
+_HDF5_MAGIC = b"\x89HDF\r\n\x1a\n"
+
+
+def _h5py():
+    try:
+        import h5py
+        return h5py
+    except ImportError:
+        return None
+
+
+def write_pack(path, arrays, keys=None):
+    """hf.create_dataset(name, data=...) for every key (data_preprocess.py:139-143), float64."""
+    keys = tuple(arrays) if keys is None else keys
+    missing = [k for k in keys if k not in arrays]
+    if missing:
+        raise KeyError(f"pack is missing {missing}")
+    data = {k: np.asarray(arrays[k], dtype=np.float64) for k in keys}
+    h5 = _h5py()
+    if h5 is not None:
+        with h5.File(path, "w") as hf:
+            for k in keys:
+                hf.create_dataset(k, data=data[k])
+        return path
+    with open(path, "wb") as fh:              # keep the reference's file name (np.savez would add .npz)
+        np.savez(fh, **data)
+    return path
+
+
+class _NpzPack:
+    """h5py.File-like read view of an .npz pack: ``f[name][:]``, ``keys()``, ``close()``, context manager."""
+
+    def __init__(self, path):
+        self._z = np.load(path, allow_pickle=False)
+
+    def __getitem__(self, k):
+        return self._z[k]
+
+    def __contains__(self, k):
+        return k in self._z.files
+
+    def keys(self):
+        return list(self._z.files)
+
+    def close(self):
+        self._z.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def open_pack(path, mode="r"):
+    """``h5py.File(path, 'r')`` of temp_exp_main.py:705-706 for either container."""
+    if mode != "r":
+        raise ValueError("open_pack is read-only; use write_pack")
+    with open(path, "rb") as fh:
+        magic = fh.read(8)
+    if magic == _HDF5_MAGIC:
+        h5 = _h5py()
+        if h5 is None:
+            raise ImportError(f"{path} is HDF5 and h5py is not importable here")
+        return h5.File(path, "r")
+    if magic[:2] == b"PK" and zipfile.is_zipfile(path):
+        return _NpzPack(path)
+    raise ValueError(f"{path}: neither an HDF5 nor an npz pack")
+
+
+def _split_cols(a, n):
+    return a[..., 0:n], a[..., n:2 * n], a[..., 2 * n:3 * n]
+
+
+def _subgraph(file, side, n_degree, batch_id=None):
+    recs = ([], [], [])
+    for h, width in ((0, n_degree), (1, n_degree ** 2)):
+        a = file[f"subgraph_{side}_{h}"][:]
+        if batch_id is not None:
+            a = a[batch_id]
+        for r, c in zip(recs, _split_cols(a, width)):
+            r.append(c)
+    return recs
+
+
+def load_subgraph(args, file, batch_id):
+    """utils/batch_loader.py:45-116: one batch of a ``{data}_{mode}.h5`` pack (raw walks, anony codes)."""
+    subs = [_subgraph(file, s, args.n_degree, batch_id) for s in SIDES]
+    walks = []
+    for s in SIDES:
+        w = file[f"walks_{s}"][:][batch_id]
+        walks.append((w[:, :, :6].astype(int), w[:, :, 6:9].astype(int), w[:, :, 9:12], w[:, :, 12:15].astype(int)))
+    return (*subs, *walks)
+
+
+def load_subgraph_margin(args, file):
+    """utils/batch_loader.py:119-197: the whole ``{data}_{mode}_cat.h5`` pack ->
+    (subgraph_src, subgraph_tgt, subgraph_bgd, walks_src, walks_tgt, walks_bgd, dst_fake)."""
+    subs = [_subgraph(file, s, args.n_degree) for s in SIDES]
+    walks = []
+    for s in SIDES:
+        w = file[f"walks_{s}_new"][:]
+        walks.append((w[:, :, :6].astype(int), w[:, :, 6:9].astype(int), w[:, :, 9:12], w[:, :, 12:13].astype(int),
+                      w[:, :, 13:14]))
+    return (*subs, *walks, file["dst_fake"][:])
+
+
+def get_item(input_pack, batch_id):
+    """utils/batch_loader.py:200-235."""
+    *subs, ws, wt, wb, dst_fake = input_pack
+    out = []
+    for node_records, eidx_records, t_records in subs:
+        out.append(([i[batch_id] for i in node_records], [i[batch_id] for i in eidx_records],
+                    [i[batch_id] for i in t_records]))
+    for w in (ws, wt, wb):
+        out.append(tuple(item[batch_id] for item in w))
+    out.append(dst_fake[batch_id])
+    return tuple(out)
+
+
+def get_item_edge(edge_features, batch_id):
+    """utils/batch_loader.py:238-242: [3, n, W, 3, 3] -> (src_edge, tgt_edge, bgd_edge)."""
+    e = edge_features[:, batch_id, :, :, :]
+    return e[0], e[1], e[2]
+
+
+# ---------------------------------------------------------------------------------- device side
+def buffers_to_arrays(buf, n=None):
+    """EventBuffers (device, side-major) -> the float64 arrays of both H5 files and the edge .npy:
+    (raw dict of ``{data}_{mode}.h5``, cat dict of ``{data}_{mode}_cat.h5``, edge [3, n, W, 3, 3])."""
+    n = buf.E if n is None else n
+    h = lambda t: t[:, :n].cpu().numpy()  # noqa: E731
+    raw = {"dst_fake": buf.dst_fake[:n].cpu().numpy().astype(np.float64)}
+    cat_d = {"dst_fake": raw["dst_fake"]}
+    cat = h(buf.cat)
+    freq = np.bincount(cat.reshape(-1), minlength=12).astype(np.float64) / max(cat.size, 1)  # marginal :180-208
+    an = anony_from_cat(cat)
+    s1 = [h(buf.sub1_node), h(buf.sub1_eid), h(buf.sub1_ts)]
+    s2 = [h(buf.sub2_node), h(buf.sub2_eid), h(buf.sub2_ts)]
+    n6, e3, t3 = h(buf.node6), h(buf.eid3), h(buf.ts3)
+    for s, side in enumerate(SIDES):
+        raw[f"subgraph_{side}_0"] = cat_d[f"subgraph_{side}_0"] = np.concatenate(
+            [x[s] for x in s1], -1).astype(np.float64)
+        raw[f"subgraph_{side}_1"] = cat_d[f"subgraph_{side}_1"] = np.concatenate(
+            [x[s] for x in s2], -1).astype(np.float64)
+        base = np.concatenate([n6[s], e3[s], t3[s]], -1).astype(np.float64)
+        raw[f"walks_{side}"] = np.concatenate([base, an[s]], -1)
+        cat_d[f"walks_{side}_new"] = np.concatenate([base, cat[s][..., None], freq[cat[s]][..., None]], -1)
+    return raw, cat_d, h(buf.cnt).astype(np.float64)
+
+
+def write_split(buf, out_dir, data, mode, n=None):
+    """The three files data_preprocess.py:364-420 writes for one (data, MODE), from one sample_events
+    launch's EventBuffers.  Returns their paths."""
+    raw, cat_d, edge = buffers_to_arrays(buf, n)
+    p_raw = write_pack(os.path.join(out_dir, f"{data}_{mode}.h5"), raw, RAW_KEYS)
+    p_cat = write_pack(os.path.join(out_dir, f"{data}_{mode}_cat.h5"), cat_d, CAT_KEYS)
+    p_edge = os.path.join(out_dir, f"{data}_{mode}_edge.npy")
+    np.save(p_edge, edge)
+    return p_raw, p_cat, p_edge
+
+
+class DevicePack(EventBuffers):
+    """A ``_cat.h5`` pack + ``_edge.npy`` resident on the device in EventBuffers' layout
+    ([3, n, ...] int32 / float32), i.e. what ``load_subgraph_margin`` + ``get_item`` + ``get_item_edge``
+    hand the training loop, without per-batch host copies."""
+
+    def __init__(self, file, edge, n_degree, device, walks_per_slot=3):
+        dst_fake = np.asarray(file["dst_fake"][:])
+        n, N = int(dst_fake.shape[0]), int(n_degree)
+        w0 = np.asarray(file["walks_src_new"][:])
+        if w0.shape[1] % N:
+            raise AssertionError(f"walks per side {w0.shape[1]} is not a multiple of n_degree {N}")
+        super().__init__(n, N, w0.shape[1] // N if w0.shape[1] else walks_per_slot, device)
+        edge = np.asarray(edge)
+        if edge.shape != (3, n, self.W, 3, 3):
+            raise AssertionError(f"edge counts {edge.shape} != (3, {n}, {self.W}, 3, 3)")
+        i32 = lambda a: torch.from_numpy(np.ascontiguousarray(a).astype(np.int32))  # noqa: E731
+        f32 = lambda a: torch.from_numpy(np.ascontiguousarray(a).astype(np.float32))  # noqa: E731
+        self.dst_fake.copy_(i32(dst_fake))
+        for s, side in enumerate(SIDES):
+            for h, (nd, ed, td) in ((0, (self.sub1_node, self.sub1_eid, self.sub1_ts)),
+                                    (1, (self.sub2_node, self.sub2_eid, self.sub2_ts))):
+                x, y, z = _split_cols(np.asarray(file[f"subgraph_{side}_{h}"][:]), N ** (h + 1))
+                nd[s].copy_(i32(x))
+                ed[s].copy_(i32(y))
+                td[s].copy_(f32(z))
+            w = np.asarray(w0 if s == 0 else file[f"walks_{side}_new"][:])
+            self.node6[s].copy_(i32(w[:, :, :6]))
+            self.eid3[s].copy_(i32(w[:, :, 6:9]))
+            self.ts3[s].copy_(f32(w[:, :, 9:12]))
+            self.cat[s].copy_(i32(w[:, :, 12]))
+            self.cnt[s].copy_(f32(edge[s]))
+        self.hist.copy_(torch.bincount(self.cat.reshape(-1).long().cpu(), minlength=12))
+
+    @classmethod
+    def from_files(cls, cat_path, edge_path, n_degree, device):
+        with open_pack(cat_path) as f:
+            return cls(f, np.load(edge_path, allow_pickle=False), n_degree, device)
