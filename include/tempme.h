@@ -146,6 +146,52 @@ int tm_encoder_fwd(const tm_weights *w, const float *n_feat, const float *e_feat
                    const int32_t *cat, const double *cut, const float *cnt, void *workspace, float *out_imp,
                    void *stream);
 
+/* ---------------------------------------------------------------- encoder training (device)
+ * Training forward of TempME.forward (explainer_new.py:174-201) with dropout active: drop (nullable
+ * = eval) holds uint8 keep-masks [n_walks][144]: columns 0..1 the attention weights alpha (:839),
+ * 2..65 attention.MLP's hidden layer (:780), 66..141 MLP's hidden layer (:122); kept values are
+ * scaled by drop_scale = 1/(1-p).  `workspace` (tm_encoder_workspace_bytes) keeps the event_gcn
+ * outputs F for tm_encoder_bwd.  Replaces the autograd forward of temp_exp_main.py:605-607. */
+int tm_encoder_train_fwd(const tm_weights *w, const float *n_feat, const float *e_feat, int32_t n_groups, int32_t B,
+                         int32_t W, const int32_t *node6, const int32_t *eid3, const float *ts3, const int32_t *cat,
+                         const double *cut, const float *cnt, const uint8_t *drop, float drop_scale, void *workspace,
+                         float *out_imp, void *stream);
+
+/* Buffers of tm_encoder_bwd (caller-allocated device memory; n = n_walks, R = 3n walk positions,
+ * KE = kev rounded up to 16 (kev = de + 3 + dn), DN = dn rounded up to 16).  Each layer's
+ * (d pre-activation, input) row pair is written so the weight gradients are dW = dY^T X over all rows
+ * and the bias gradients sum(dY) (the caller runs those GEMMs / reductions).  Padding columns are 0. */
+typedef struct {
+    float *imp;    /* [n] recomputed forward output (nullable) */
+    float *dlogit; /* [n]            MLP.5:       dW = dlogit^T M2 */
+    float *M2;     /* [n][64] */
+    float *dM2;    /* [n][64]        MLP.3:       dW = dM2^T M1d[:, :76] */
+    float *M1d;    /* [n][80] */
+    float *dM1;    /* [n][80]        MLP.0:       dW = dM1[:, :76]^T X[:, :76] */
+    float *X;      /* [n][80] */
+    float *dY2;    /* [n][64]        attention.MLP.3: dW = dY2^T H1d */
+    float *H1d;    /* [n][64] */
+    float *dH1;    /* [n][64]        attention.MLP.0: dW = dH1^T O */
+    float *O;      /* [n][128] */
+    float *dP;     /* [n][128]       attention.W1: dW = dP^T F[:, 2] */
+    float *dQ;     /* [2][n][128]    attention.W2: dW = dQ[0]^T F[:, 0] + dQ[1]^T F[:, 1] */
+    float *dF;     /* [n][3][128]    d event_gcn outputs */
+    float *ev;     /* [R][KE]        lin_event:   dW = dlev[:, :dn]^T ev[:, :kev] */
+    float *AB;     /* [R][2][DN]     event_conv.MLP.0: dW = dZ^T AB (2R rows) */
+    float *H;      /* [R][2][64]     event_conv.MLP.2: dW = dF^T H (2R rows of 64) */
+    float *dZ;     /* [R][2][64] */
+    float *dlev;   /* [R][DN] */
+    float *g;      /* [R][DN]        time encoder: d phase = sum_rows g, d basis_freq = dt^T g */
+    float *dt;     /* [R] */
+} tm_encoder_grad_io;
+
+/* Backward of tm_encoder_train_fwd given d_imp [n] = dL/d out_imp, with the same inputs, masks and
+ * workspace: recomputes each tile's forward and writes the buffers above. */
+int tm_encoder_bwd(const tm_weights *w, const float *n_feat, const float *e_feat, int32_t n_groups, int32_t B,
+                   int32_t W, const int32_t *node6, const int32_t *eid3, const float *ts3, const int32_t *cat,
+                   const double *cut, const float *cnt, const uint8_t *drop, float drop_scale, const void *workspace,
+                   const float *d_imp, const tm_encoder_grad_io *io, void *stream);
+
 /* retrieve_edge_imp_node, eval (explainer_new.py:354-406, :420-430) for each of the G*B
  * (group, event) rows: dependency gate, walk->edge scatter-max, gather at the subgraph eids,
  * Beta mean, node==0 mask.  sub1_* [G,B,N], sub2_* [G,B,N*N]; out_h1 [G,B,N], out_h2 [G,B,N*N]

@@ -6,7 +6,8 @@ Functional restatement (no nn.Module) of models/explainer_new.py:
   TemporalAwareAttention  :789-846   (batch-global unbiased std of |cut - t|)
   retrieve_edge_imp_node  :354-406   (dependency gate, scatter-max walk->edge, gather, Beta mean, mask)
   kl_loss                 :432-453   (empirical prior; null vector in null-model key order)
-Eval semantics only (dropout = identity, Beta mean instead of rsample).
+Eval semantics (dropout = identity, Beta mean instead of rsample); forward() also takes explicit dropout
+keep-masks so the training forward / backward can be checked with autograd through this restatement.
 Pinned against tests/golden/encoder_uslegis.npz (outputs of the reference module).
 """
 import numpy as np
@@ -19,23 +20,31 @@ def _lin(sd, name, x):
 
 
 def time_encode(sd, t):
-    """TimeEncode.forward: cos(t * basis_freq + phase) in fp32 (explainer_new.py:51-59)."""
-    m = t.unsqueeze(-1) * sd["time_encoder.basis_freq"]
-    m = m + sd["time_encoder.phase"]
-    return torch.cos(m)
+    """TimeEncode.forward: cos(t * basis_freq + phase) with the argument rounded in fp32 as the reference
+    computes it (explainer_new.py:51-59); the cosine in the weights' dtype (fp64 gradient references)."""
+    w, ph = sd["time_encoder.basis_freq"], sd["time_encoder.phase"]
+    m = t.float().unsqueeze(-1) * w.float()
+    m = m + ph.float()
+    return torch.cos(m.to(w.dtype))
 
 
-def forward(sd, n_feat, e_feat, node, eid, ts, cat, cut, edge_count):
-    """graphlet importance [B, W, 1] for one side (explainer_new.py:174-201)."""
+def forward(sd, n_feat, e_feat, node, eid, ts, cat, cut, edge_count, drop=None, scale=1.0):
+    """graphlet importance [B, W, 1] for one side (explainer_new.py:174-201).  drop: optional keep-masks
+    [B, W, 144] of the training forward's three dropouts (alpha :839 -> cols 0..1, attention.MLP hidden :780
+    -> 2..65, MLP hidden :122 -> 66..141), kept values scaled by `scale` (training-mode parity).
+    Computes in the dtype of sd's tensors (fp32, or fp64 for gradient references)."""
     node = torch.as_tensor(np.asarray(node), dtype=torch.long)
     eid = torch.as_tensor(np.asarray(eid), dtype=torch.long)
     t = torch.as_tensor(np.asarray(ts, dtype=np.float64)).float()
     cut = torch.as_tensor(np.asarray(cut, dtype=np.float64)).float()
     cnt = torch.as_tensor(np.asarray(edge_count, dtype=np.float64)).float()
+    dty = sd["event_conv.lin_event.weight"].dtype
+    n_feat, e_feat, cnt = n_feat.to(dty), e_feat.to(dty), cnt.to(dty)
+    keep = None if drop is None else torch.as_tensor(np.asarray(drop)).to(dty) * scale
     B, W = eid.shape[0], eid.shape[1]
     ef = e_feat[eid]                                             # [B,W,3,de]
     dt = t[:, :, 2:3] - t                                        # relative to position 2
-    tf = time_encode(sd, dt.reshape(B, -1)).reshape(B, W, 3, -1)
+    tf = time_encode(sd, dt.reshape(B, -1).to(dty)).reshape(B, W, 3, -1)
     ev = torch.cat([ef, cnt, tf], dim=-1)
     xs = n_feat[node[:, :, [0, 2, 4]]]
     xt = n_feat[node[:, :, [1, 3, 5]]]
@@ -52,14 +61,21 @@ def forward(sd, n_feat, e_feat, node, eid, ts, cat, cut, edge_count):
     wq = _lin(sd, "attention.W2", tgt)                           # [B,W,2,2h]
     scores = (wp.unsqueeze(2) * wq).sum(-1)                      # [B,W,2]
     diff = torch.abs(cut.view(B, 1, 1) - t[:, :, :2])
-    tw = torch.exp(-diff / (diff.std() + 1e-6))
+    tw = torch.exp(-diff / (diff.std() + 1e-6)).to(dty)
     scores = scores * (1.0 - 0.3 + 0.3 * tw)
     alpha = torch.softmax(scores, dim=-1)
+    if keep is not None:
+        alpha = alpha * keep[..., 0:2]
     out = src + (alpha.unsqueeze(-1) * wq).sum(2)
-    out = _lin(sd, "attention.MLP.3", torch.relu(_lin(sd, "attention.MLP.0", out)))
-    oh = F.one_hot(torch.as_tensor(np.asarray(cat), dtype=torch.long).reshape(B, W), 12).float()
+    hid = torch.relu(_lin(sd, "attention.MLP.0", out))
+    if keep is not None:
+        hid = hid * keep[..., 2:66]
+    out = _lin(sd, "attention.MLP.3", hid)
+    oh = F.one_hot(torch.as_tensor(np.asarray(cat), dtype=torch.long).reshape(B, W), 12).to(dty)
     x = torch.cat([out, oh], dim=-1)
     x = torch.relu(_lin(sd, "MLP.0", x))
+    if keep is not None:
+        x = x * keep[..., 66:142]
     x = torch.relu(_lin(sd, "MLP.3", x))
     return torch.sigmoid(_lin(sd, "MLP.5", x))
 

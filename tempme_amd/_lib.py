@@ -34,7 +34,7 @@ EXPORTS = (
     "tm_last_error", "tm_version", "tm_graph_build", "tm_graph_free", "tm_graph_info", "tm_graph_export",
     "tm_sample_khop", "tm_sample_walks", "tm_neg_sample", "tm_perm_keys", "tm_motif_hist", "tm_edge_counts",
     "tm_sample_events", "tm_weights_create", "tm_weights_pack", "tm_weights_free", "tm_encoder_workspace_bytes",
-    "tm_encoder_fwd", "tm_edge_importance", "tm_edge_gate_table", "tm_edge_importance_tab", "tm_tgn_attn_fwd",
+    "tm_encoder_fwd", "tm_encoder_train_fwd", "tm_encoder_bwd", "tm_edge_importance", "tm_edge_gate_table", "tm_edge_importance_tab", "tm_tgn_attn_fwd",
     "tm_tgn_attn_bwd", "tm_mask_least_important", "tm_profile_enable", "tm_profile_sync", "tm_profile_entry",
 )
 
@@ -53,6 +53,15 @@ class TgnAttn(C.Structure):
                 ("node_tab", C.c_void_p), ("node_idx", C.c_void_p), ("edge_tab", C.c_void_p),
                 ("edge_idx", C.c_void_p), ("dt", C.c_void_p), ("time_w", C.c_void_p), ("time_b", C.c_void_p),
                 ("mask_node", C.c_void_p), ("ew", C.c_void_p), ("qf", C.c_void_p), ("err_flag", C.c_void_p)]
+
+
+GRAD_IO_FIELDS = ("imp", "dlogit", "M2", "dM2", "M1d", "dM1", "X", "dY2", "H1d", "dH1", "O", "dP", "dQ", "dF",
+                  "ev", "AB", "H", "dZ", "dlev", "g", "dt")
+
+
+class EncoderGradIO(C.Structure):
+    """tm_encoder_grad_io (include/tempme.h)."""
+    _fields_ = [(n, C.c_void_p) for n in GRAD_IO_FIELDS]
 
 
 class TempMEError(RuntimeError):
@@ -84,6 +93,9 @@ def _sig(L):
     L.tm_encoder_workspace_bytes.restype = i64
     L.tm_encoder_workspace_bytes.argtypes = [vp, i64]
     L.tm_encoder_fwd.argtypes = [vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.tm_encoder_train_fwd.argtypes = [vp, vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, C.c_float, vp, vp, vp]
+    L.tm_encoder_bwd.argtypes = [vp, vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, C.c_float, vp, vp,
+                                 C.POINTER(EncoderGradIO), vp]
     L.tm_edge_importance.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.tm_edge_gate_table.argtypes = [vp, vp, vp, vp, vp]
     L.tm_edge_importance_tab.argtypes = [vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]

@@ -17,95 +17,9 @@
 // activations staged in LDS (row stride K16+8 floats: conflict-free ds_read_b128).
 #include <vector>
 
-#include "common.h"
-
-typedef float floatx4 __attribute__((ext_vector_type(4)));
+#include "encoder_common.h"
 
 namespace tmk {
-
-constexpr int HID = 64;   // hid_dim supported by this build (reference default --hid_dim 64)
-constexpr int TILE_ROWS = 32;
-
-__host__ __device__ constexpr int r16(int x) { return (x + 15) & ~15; }
-
-struct Lin {
-    const float4 *w;  // packed [nt][nq][64 lanes] float4
-    const float *b;   // [nt*16] zero padded
-    int nt, nq, nout, k;
-};
-
-struct EncW {
-    int de, dn, kev, kdep;
-    Lin ev, g1, g2, w1, w2, a1, a2, m1, m2, d1, d2;
-    const float *m3w, *m3b, *d3w, *d3b, *freq, *phase;
-    // lin_event bias plus the K steps q >= qt (all time features) at dt = 0: walk position 2 is
-    // relative to itself, so those steps are the constant cos(phase) (walk_kernel's slot pass)
-    const float *evc;
-    int qt;
-};
-
-// ------------------------------------------------------------------ MFMA tile GEMM
-// out[16mt.., 16nt..] = X[16*MT rows][ldx] (LDS) * W^T (packed, streamed from L2).
-// Each wave owns column tiles nt = wave, wave + nw, ... and sweeps all MT row tiles for
-// them, two column tiles at a time: per 16-deep K step it loads 2 weight fragments (the
-// next step's are prefetched into registers) and MT activation fragments (ds_read_b128)
-// and issues 8*MT MFMAs.  The epilogue gets (mt, nt, acc) with acc[r] = D[4*(lane>>4)+r][lane&15].
-template <int MT, class Epi>
-__device__ __forceinline__ void gemm(const float *X, int ldx, const Lin &L, Epi epi) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    const int arow = lane & 15, akoff = 4 * (lane >> 4);
-    const int nq = L.nq;
-    for (int nt0 = wave; nt0 < L.nt; nt0 += 2 * nw) {
-        const int nt1 = nt0 + nw;
-        const bool has1 = nt1 < L.nt;
-        floatx4 acc0[MT], acc1[MT];
-#pragma unroll
-        for (int m = 0; m < MT; ++m) {
-            acc0[m] = floatx4{0.f, 0.f, 0.f, 0.f};
-            acc1[m] = floatx4{0.f, 0.f, 0.f, 0.f};
-        }
-        const float4 *wb0 = L.w + (size_t)nt0 * nq * 64 + lane;
-        const float4 *wb1 = L.w + (size_t)(has1 ? nt1 : nt0) * nq * 64 + lane;
-        const float *xa = X + arow * ldx + akoff;
-        float4 b0 = wb0[0], b1 = wb1[0];
-        for (int q = 0; q < nq; ++q) {
-            float4 n0 = b0, n1 = b1;
-            if (q + 1 < nq) {
-                n0 = wb0[(q + 1) * 64];
-                n1 = wb1[(q + 1) * 64];
-            }
-#pragma unroll
-            for (int m = 0; m < MT; ++m) {
-                const float4 a = *reinterpret_cast<const float4 *>(xa + m * 16 * ldx + 16 * q);
-                acc0[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b0.x, acc0[m], 0, 0, 0);
-                acc1[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b1.x, acc1[m], 0, 0, 0);
-                acc0[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b0.y, acc0[m], 0, 0, 0);
-                acc1[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b1.y, acc1[m], 0, 0, 0);
-                acc0[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b0.z, acc0[m], 0, 0, 0);
-                acc1[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b1.z, acc1[m], 0, 0, 0);
-                acc0[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b0.w, acc0[m], 0, 0, 0);
-                acc1[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b1.w, acc1[m], 0, 0, 0);
-            }
-            b0 = n0;
-            b1 = n1;
-        }
-#pragma unroll
-        for (int m = 0; m < MT; ++m) epi(m, nt0, acc0[m]);
-        if (has1) {
-#pragma unroll
-            for (int m = 0; m < MT; ++m) epi(m, nt1, acc1[m]);
-        }
-    }
-}
-
-__device__ __forceinline__ int erow(int mt, int r) { return mt * 16 + 4 * ((threadIdx.x & 63) >> 4) + r; }
-__device__ __forceinline__ int ecol(int nt) { return nt * 16 + (threadIdx.x & 15); }
-
-// cos(t * w + phi) with the multiply and add rounded separately, as torch does
-// (TimeEncode.forward, explainer_new.py:56-58); never contracted into an fma.
-__device__ __forceinline__ float time_cos(float t, float w, float phi) { return cos_rd(__fadd_rn(__fmul_rn(t, w), phi)); }
-
-__device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
 
 // ------------------------------------------------------------------ std over |cut - t| per group
 __global__ void __launch_bounds__(256) std_kernel(int32_t B, int32_t W, const double *__restrict__ cut,
@@ -224,7 +138,9 @@ __global__ void __launch_bounds__(256) gcn_kernel(EncW P, int64_t n_rows, const 
 __global__ void __launch_bounds__(256) head_kernel(EncW P, int64_t n_walks, int64_t walks_per_group, int32_t W,
                                                    const float *__restrict__ F, const float *__restrict__ ts3,
                                                    const double *__restrict__ cut, const int32_t *__restrict__ cat,
-                                                   const float *__restrict__ stdv, float *__restrict__ out) {
+                                                   const float *__restrict__ stdv, float *__restrict__ out,
+                                                   const uint8_t *__restrict__ drop = nullptr, float dscale = 1.f) {
+    // drop (training forward, nullable): keep-masks [n_walks][DROP_COLS]; kept values are scaled by dscale
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int D2 = 2 * HID, LD = D2 + 8, LDM = r16(HID + 12) + 8, LDH = HID + 8;
     float *T = smem;                  // [64][LD]  positions 0,1 (rows p*32 + w)  -> later S, P
@@ -295,8 +211,14 @@ __global__ void __launch_bounds__(256) head_kernel(EncW P, int64_t n_walks, int6
     if (tid < TILE_ROWS) {
         const float s0 = s_score[2 * tid], s1 = s_score[2 * tid + 1], mx = fmaxf(s0, s1);
         const float e0 = expf(s0 - mx), e1 = expf(s1 - mx), sum = e0 + e1;
-        s_alpha[2 * tid] = e0 / sum;
-        s_alpha[2 * tid + 1] = e1 / sum;
+        float a0 = e0 / sum, a1 = e1 / sum;
+        if (drop) {   // alpha = self.dropout(alpha)  (:839)
+            const uint8_t *dm = drop + (w0 + tid < n_walks ? w0 + tid : 0) * DROP_COLS + DROP_A;
+            a0 = dm[0] ? a0 * dscale : 0.f;
+            a1 = dm[1] ? a1 * dscale : 0.f;
+        }
+        s_alpha[2 * tid] = a0;
+        s_alpha[2 * tid + 1] = a1;
     }
     __syncthreads();
     // O = src + alpha . Wq   (into Pp)
@@ -308,7 +230,13 @@ __global__ void __launch_bounds__(256) head_kernel(EncW P, int64_t n_walks, int6
     __syncthreads();
     gemm<2>(Pp, LD, P.a1, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
-        for (int r = 0; r < 4; ++r) H1[erow(mt, r) * LDH + c] = relu(acc[r] + P.a1.b[c]);
+        for (int r = 0; r < 4; ++r) {
+            const int row = erow(mt, r);
+            float v = relu(acc[r] + P.a1.b[c]);
+            if (drop && !drop[(w0 + row < n_walks ? w0 + row : 0) * DROP_COLS + DROP_H + c]) v = 0.f;
+            else if (drop) v *= dscale;
+            H1[row * LDH + c] = v;
+        }
     });
     __syncthreads();
     // X = [attention MLP out | one-hot(cat)]
@@ -323,7 +251,12 @@ __global__ void __launch_bounds__(256) head_kernel(EncW P, int64_t n_walks, int6
     __syncthreads();
     gemm<2>(X, LDM, P.m1, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
-        for (int r = 0; r < 4; ++r) M1[erow(mt, r) * LDM + c] = c < P.m1.nout ? relu(acc[r] + P.m1.b[c]) : 0.f;
+        for (int r = 0; r < 4; ++r) {
+            const int row = erow(mt, r);
+            float v = c < P.m1.nout ? relu(acc[r] + P.m1.b[c]) : 0.f;
+            if (drop && c < P.m1.nout) v = drop[(w0 + row < n_walks ? w0 + row : 0) * DROP_COLS + DROP_M + c] ? v * dscale : 0.f;
+            M1[row * LDM + c] = v;
+        }
     });
     __syncthreads();
     gemm<2>(M1, LDM, P.m2, [&](int mt, int nt, floatx4 acc) {
@@ -1070,22 +1003,6 @@ __global__ void copy_pad_kernel(const float *__restrict__ src, int n, int npad, 
 
 using namespace tmk;
 
-struct tm_weights {
-    int device;
-    int de, dn, h;
-    float *buf;
-    size_t n_floats;
-    EncW P;
-    // per linear: raw tensor index, nout, k
-    struct Spec {
-        Lin *lin;
-        int wi, nout, k;
-    };
-    std::vector<Spec> specs;
-    std::vector<std::pair<int, float **>> vecs;
-};
-
-static inline hipStream_t S_(void *s) { return (hipStream_t)s; }
 
 extern "C" int tm_weights_create(int32_t de, int32_t dn, int32_t h, int device, tm_weights **out) {
     if (!out || de <= 0 || dn <= 0) return fail(TM_E_ARG, "tm_weights_create: bad arguments");
@@ -1151,6 +1068,11 @@ extern "C" int tm_weights_create(int32_t de, int32_t dn, int32_t h, int device, 
     P.phase = w->buf + ph;
     P.evc = w->buf + evc;
     P.qt = (de + 3 + 15) / 16;
+    if (int rc = train_packs_create(w)) {
+        (void)hipFree(w->buf);
+        delete w;
+        return rc;
+    }
     *out = w;
     return TM_OK;
 }
@@ -1185,6 +1107,7 @@ extern "C" int tm_weights_pack(tm_weights *w, const float *const *t, void *strea
     copy_pad_kernel<<<dim3(1), 256, 0, s>>>(t[26], w->dn, r16(w->dn), const_cast<float *>(w->P.freq));
     copy_pad_kernel<<<dim3(1), 256, 0, s>>>(t[27], w->dn, r16(w->dn), const_cast<float *>(w->P.phase));
     evc_kernel<<<dim3(1), 256, 0, s>>>(t[0], t[1], t[27], w->de, w->dn, w->P.kev, w->P.qt, const_cast<float *>(w->P.evc));
+    train_packs_fill(w, t, s);
     TM_CHECK_LAUNCH();
     return TM_OK;
 }
@@ -1192,6 +1115,7 @@ extern "C" int tm_weights_pack(tm_weights *w, const float *const *t, void *strea
 extern "C" int tm_weights_free(tm_weights *w) {
     if (!w) return TM_OK;
     if (w->buf) (void)hipFree(w->buf);
+    train_packs_free(w);
     delete w;
     return TM_OK;
 }
@@ -1296,6 +1220,41 @@ extern "C" int tm_encoder_fwd(const tm_weights *w, const float *n_feat, const fl
     pe = prof_begin(s);
     head_kernel<<<dim3((unsigned)((n_walks + TILE_ROWS - 1) / TILE_ROWS)), 256, lds_h, s>>>(
         P, n_walks, (int64_t)B * W, W, F, ts3, cut, cat, stdv, out_imp);
+    TM_CHECK_LAUNCH();
+    prof_end("head_kernel", s, pe);
+    return TM_OK;
+}
+
+// Training forward (explainer_new.py:174-201 with dropout active): the LDS-tiled kernels, keeping
+// F [n_walks*3, 2h] and the per-group std in `workspace` for tm_encoder_bwd.  drop nullable (eval).
+extern "C" int tm_encoder_train_fwd(const tm_weights *w, const float *n_feat, const float *e_feat, int32_t n_groups,
+                                    int32_t B, int32_t W, const int32_t *node6, const int32_t *eid3, const float *ts3,
+                                    const int32_t *cat, const double *cut, const float *cnt, const uint8_t *drop,
+                                    float drop_scale, void *workspace, float *out_imp, void *stream) {
+    if (!w || n_groups < 0 || B < 0 || W < 0) return fail(TM_E_ARG, "tm_encoder_train_fwd: bad arguments");
+    const int64_t n_walks = (int64_t)n_groups * B * W;
+    if (n_walks == 0) return TM_OK;
+    if (!n_feat || !e_feat || !node6 || !eid3 || !ts3 || !cat || !cut || !cnt || !workspace || !out_imp)
+        return fail(TM_E_ARG, "tm_encoder_train_fwd: NULL pointer");
+    const EncW &P = w->P;
+    const size_t lds_g = gcn_lds(P), lds_h = head_lds();
+    if (lds_g > 160 * 1024) return fail(TM_E_UNSUPPORTED, "tm_encoder_train_fwd: feature dims too large for LDS tile");
+    hipStream_t s = S_(stream);
+    float *F = reinterpret_cast<float *>(workspace);
+    float *stdv = F + n_walks * 3 * 2 * HID;
+    hipEvent_t pe = prof_begin(s);
+    std_kernel<<<dim3(n_groups), 256, 0, s>>>(B, W, cut, ts3, stdv);
+    TM_CHECK_LAUNCH();
+    prof_end("std_kernel", s, pe);
+    const int64_t n_rows = n_walks * 3;
+    pe = prof_begin(s);
+    gcn_kernel<<<dim3((unsigned)((n_rows + TILE_ROWS - 1) / TILE_ROWS)), 256, lds_g, s>>>(
+        P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, F);
+    TM_CHECK_LAUNCH();
+    prof_end("gcn_kernel", s, pe);
+    pe = prof_begin(s);
+    head_kernel<<<dim3((unsigned)((n_walks + TILE_ROWS - 1) / TILE_ROWS)), 256, lds_h, s>>>(
+        P, n_walks, (int64_t)B * W, W, F, ts3, cut, cat, stdv, out_imp, drop, drop_scale);
     TM_CHECK_LAUNCH();
     prof_end("head_kernel", s, pe);
     return TM_OK;

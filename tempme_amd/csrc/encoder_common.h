@@ -1,0 +1,136 @@
+// Encoder internals shared by encoder.hip (scoring) and encoder_train.hip (training forward/backward).
+#pragma once
+#include <vector>
+
+#include "common.h"
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+namespace tmk {
+
+constexpr int HID = 64;   // hid_dim supported by this build (reference default --hid_dim 64)
+constexpr int TILE_ROWS = 32;
+
+__host__ __device__ constexpr int r16(int x) { return (x + 15) & ~15; }
+
+struct Lin {
+    const float4 *w;  // packed [nt][nq][64 lanes] float4
+    const float *b;   // [nt*16] zero padded
+    int nt, nq, nout, k;
+};
+
+struct EncW {
+    int de, dn, kev, kdep;
+    Lin ev, g1, g2, w1, w2, a1, a2, m1, m2, d1, d2;
+    const float *m3w, *m3b, *d3w, *d3b, *freq, *phase;
+    // lin_event bias plus the K steps q >= qt (all time features) at dt = 0: walk position 2 is
+    // relative to itself, so those steps are the constant cos(phase) (walk_kernel's slot pass)
+    const float *evc;
+    int qt;
+};
+
+// ------------------------------------------------------------------ MFMA tile GEMM
+// out[16mt.., 16nt..] = X[16*MT rows][ldx] (LDS) * W^T (packed, streamed from L2).
+// Each wave owns column tiles nt = wave, wave + nw, ... and sweeps all MT row tiles for
+// them, two column tiles at a time: per 16-deep K step it loads 2 weight fragments (the
+// next step's are prefetched into registers) and MT activation fragments (ds_read_b128)
+// and issues 8*MT MFMAs.  The epilogue gets (mt, nt, acc) with acc[r] = D[4*(lane>>4)+r][lane&15].
+template <int MT, class Epi>
+__device__ __forceinline__ void gemm(const float *X, int ldx, const Lin &L, Epi epi) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int arow = lane & 15, akoff = 4 * (lane >> 4);
+    const int nq = L.nq;
+    for (int nt0 = wave; nt0 < L.nt; nt0 += 2 * nw) {
+        const int nt1 = nt0 + nw;
+        const bool has1 = nt1 < L.nt;
+        floatx4 acc0[MT], acc1[MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+            acc0[m] = floatx4{0.f, 0.f, 0.f, 0.f};
+            acc1[m] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+        const float4 *wb0 = L.w + (size_t)nt0 * nq * 64 + lane;
+        const float4 *wb1 = L.w + (size_t)(has1 ? nt1 : nt0) * nq * 64 + lane;
+        const float *xa = X + arow * ldx + akoff;
+        float4 b0 = wb0[0], b1 = wb1[0];
+        for (int q = 0; q < nq; ++q) {
+            float4 n0 = b0, n1 = b1;
+            if (q + 1 < nq) {
+                n0 = wb0[(q + 1) * 64];
+                n1 = wb1[(q + 1) * 64];
+            }
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                const float4 a = *reinterpret_cast<const float4 *>(xa + m * 16 * ldx + 16 * q);
+                acc0[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b0.x, acc0[m], 0, 0, 0);
+                acc1[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b1.x, acc1[m], 0, 0, 0);
+                acc0[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b0.y, acc0[m], 0, 0, 0);
+                acc1[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b1.y, acc1[m], 0, 0, 0);
+                acc0[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b0.z, acc0[m], 0, 0, 0);
+                acc1[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b1.z, acc1[m], 0, 0, 0);
+                acc0[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b0.w, acc0[m], 0, 0, 0);
+                acc1[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b1.w, acc1[m], 0, 0, 0);
+            }
+            b0 = n0;
+            b1 = n1;
+        }
+#pragma unroll
+        for (int m = 0; m < MT; ++m) epi(m, nt0, acc0[m]);
+        if (has1) {
+#pragma unroll
+            for (int m = 0; m < MT; ++m) epi(m, nt1, acc1[m]);
+        }
+    }
+}
+
+__device__ __forceinline__ int erow(int mt, int r) { return mt * 16 + 4 * ((threadIdx.x & 63) >> 4) + r; }
+__device__ __forceinline__ int ecol(int nt) { return nt * 16 + (threadIdx.x & 15); }
+
+// cos(t * w + phi) with the multiply and add rounded separately, as torch does
+// (TimeEncode.forward, explainer_new.py:56-58); never contracted into an fma.
+__device__ __forceinline__ float time_cos(float t, float w, float phi) { return cos_rd(__fadd_rn(__fmul_rn(t, w), phi)); }
+
+__device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
+
+// Transposed weight packs for the backward's data-gradient GEMMs (dX = dY W = dY (W^T)^T), same
+// fragment format as the forward packs; no biases.  evT holds only lin_event's time-feature columns.
+struct EncWT {
+    Lin evT, g1T, g2T, w1T, w2T, a1T, a2T, m1T, m2T;
+};
+
+// Dropout keep-masks of the training forward, uint8 [n_walks][DROP_COLS]: attention weights alpha
+// (TemporalAwareAttention.dropout, explainer_new.py:839), the attention MLP's hidden layer (:780) and
+// the final MLP's hidden layer (:122); 1 = kept (scaled by 1/(1-p)), 0 = dropped.
+constexpr int DROP_A = 0, DROP_H = 2, DROP_M = DROP_H + HID, DROP_COLS = 144;
+static_assert(DROP_M + HID + 12 <= DROP_COLS, "dropout mask columns");
+
+}  // namespace tmk
+
+using tmk::Lin;
+using tmk::EncW;
+
+struct tm_weights {
+    int device;
+    int de, dn, h;
+    float *buf;
+    size_t n_floats;
+    EncW P;
+    // per linear: raw tensor index, nout, k
+    struct Spec {
+        Lin *lin;
+        int wi, nout, k;
+    };
+    std::vector<Spec> specs;
+    std::vector<std::pair<int, float **>> vecs;
+    // training: transposed packs (encoder_train.hip)
+    tmk::EncWT T;
+    float *tbuf = nullptr;
+    size_t t_floats = 0;
+};
+
+// encoder_train.hip: allocate / fill the transposed packs (called by tm_weights_create / _pack / _free)
+int train_packs_create(tm_weights *w);
+void train_packs_fill(tm_weights *w, const float *const *t, hipStream_t s);
+void train_packs_free(tm_weights *w);
+
+static inline hipStream_t S_(void *s) { return (hipStream_t)s; }

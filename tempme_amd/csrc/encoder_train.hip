@@ -1,0 +1,577 @@
+// TempME motif encoder, training: backward kernels on gfx950.
+//
+// Reference (dharunm236/TempME): the explainer's training step temp_exp_main.py:605-632 back-propagates
+// through TempME.forward (models/explainer_new.py:174-201: event features, event_gcn x2 :79-96,
+// TemporalAwareAttention :789-846 with dropout on alpha :839 and in its MLP :780, the category one-hot
+// and MLP :122-125 with dropout, sigmoid).  The reference leaves that to autograd; here the forward
+// runs gcn_kernel + head_kernel (encoder.hip, dropout keep-masks applied in the head) and the backward
+// is two LDS-tiled MFMA kernels that recompute the forward of their tile and run its chain rule:
+//
+//   head_bwd_kernel  per 32 walks: attention + MLP head forward again (from the stored F rows), then
+//                    d imp -> d logit -> MLP -> one-hot split -> attention MLP -> softmax / temporal
+//                    scaling -> W1 / W2 -> dF [walk][position][2h]
+//   gcn_bwd_kernel   per 32 walk positions: event features, lin_event, both event_gcn branches again,
+//                    then dF -> MLP.2 -> ReLU -> MLP.0 -> the two ReLU branches -> d lin_event ->
+//                    d time features -> (-sin) for the time encoder's frequency / phase
+//
+// Every data-gradient GEMM (dX = dY W) runs on MFMA against transposed weight packs (EncWT, packed
+// alongside the forward packs).  Each kernel also writes, per layer, the (dY, X) row pairs of its tile;
+// the weight gradients dW = dY^T X are then plain tall-skinny library GEMMs over all rows (hipBLASLt,
+// issued by the host wrapper), and bias gradients the column sums of dY.
+#include "encoder_common.h"
+
+namespace tmk {
+
+// ------------------------------------------------------------------ transposed weight packs
+// packed element (o, c) of job j = src[o * so + c * sc]  (same fragment order as pack_kernel)
+struct PackJob {
+    const float *src;
+    float *dst;
+    int32_t so, sc, nout, k, nt, nq;
+    int64_t begin;
+};
+constexpr int MAX_PACK_JOBS = 12;
+struct PackJobs {
+    PackJob j[MAX_PACK_JOBS];
+    int32_t n;
+    int64_t total;
+};
+
+__global__ void pack_jobs_kernel(PackJobs J) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < J.total; i += (int64_t)gridDim.x * blockDim.x) {
+        int b = 0;
+        while (b + 1 < J.n && i >= J.j[b + 1].begin) ++b;
+        const PackJob &p = J.j[b];
+        const int64_t e = i - p.begin;
+        const int s = e & 3, l = (e >> 2) & 63;
+        const int64_t tq = e >> 8;
+        const int q = (int)(tq % p.nq), t = (int)(tq / p.nq);
+        const int o = 16 * t + (l & 15), c = 16 * q + 4 * (l >> 4) + s;
+        p.dst[e] = (o < p.nout && c < p.k) ? p.src[(int64_t)o * p.so + (int64_t)c * p.sc] : 0.f;
+    }
+}
+
+// ------------------------------------------------------------------ head backward
+struct HeadBwdOut {
+    float *imp;     // [n]          recomputed sigmoid output (nullable)
+    float *dlogit;  // [n]          d logit                         (MLP.5: with M2)
+    float *M2;      // [n][64]      relu(MLP.3 ...)
+    float *dM2;     // [n][64]      d MLP.3 pre-activation          (with M1d)
+    float *M1d;     // [n][80]      dropout(relu(MLP.0 x))
+    float *dM1;     // [n][80]      d MLP.0 pre-activation          (with X)
+    float *X;       // [n][80]      [attention out | one-hot(cat)]
+    float *dY2;     // [n][64]      d attention.MLP.3 output        (with H1d)
+    float *H1d;     // [n][64]      dropout(relu(attention.MLP.0 O))
+    float *dH1;     // [n][64]      d attention.MLP.0 pre-activation (with O)
+    float *O;       // [n][128]     src + sum alpha' Wq
+    float *dP;      // [n][128]     d W1(src)                       (with F[:, 2])
+    float *dQ;      // [2][n][128]  d W2(tgt_k)                     (with F[:, k])
+    float *dF;      // [n][3][128]  d [U_s | U_t] per walk position
+};
+
+__global__ void __launch_bounds__(256) head_bwd_kernel(EncW P, EncWT T, int64_t n_walks, int64_t walks_per_group,
+                                                       int32_t W, const float *__restrict__ F,
+                                                       const float *__restrict__ ts3, const double *__restrict__ cut,
+                                                       const int32_t *__restrict__ cat, const float *__restrict__ stdv,
+                                                       const uint8_t *__restrict__ drop, float dscale,
+                                                       const float *__restrict__ d_imp, HeadBwdOut o) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int D2 = 2 * HID, LD = D2 + 8, LDH = HID + 8, KM = r16(HID + 12), LDM = KM + 8;
+    float *Qb = smem;              // [64][LD]  W2(F0 | F1)            -> dQ
+    float *Wp = Qb + 64 * LD;      // [32][LD]  W1(F2)                 -> dP      (Wp..Ob: F0|F1 staging)
+    float *Ob = Wp + 32 * LD;      // [32][LD]  F2 -> O                -> dO
+    float *H1 = Ob + 32 * LD;      // [32][LDH] H1d                    -> dH1
+    float *Xb = H1 + 32 * LDH;     // [32][LDM] X                      -> dY2
+    float *M1 = Xb + 32 * LDM;     // [32][LDM] M1d                    -> dM1
+    float *M2 = M1 + 32 * LDM;     // [32][LDH] M2                     -> dM2
+    __shared__ float s_mult[64], s_score[64], s_alpha[64], s_alphad[64], s_dsr[64], s_dl[32];
+    __shared__ int32_t s_cat[32];
+    const int64_t w0 = (int64_t)blockIdx.x * TILE_ROWS;
+    const int tid = threadIdx.x;
+    const float kscale = drop ? dscale : 1.f;   // d(dropout(relu(z)))/dz where the output is > 0
+    auto valid = [&](int w) { return w0 + w < n_walks; };
+    auto keep = [&](int w, int col) -> float {
+        if (!drop) return 1.f;
+        return (valid(w) && drop[(w0 + w) * DROP_COLS + col]) ? dscale : 0.f;
+    };
+
+    // ---- forward again: Q = W2 [F0; F1], Wp = W1 F2, scores, softmax, dropout, O
+    float *Tb = Wp;
+    for (int i = tid; i < 2 * TILE_ROWS * (D2 / 4); i += blockDim.x) {
+        const int row = i / (D2 / 4), c4 = i % (D2 / 4), p = row / TILE_ROWS, w = row % TILE_ROWS;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (valid(w)) v = reinterpret_cast<const float4 *>(F + ((w0 + w) * 3 + p) * D2)[c4];
+        *reinterpret_cast<float4 *>(Tb + row * LD + 4 * c4) = v;
+    }
+    if (tid < 2 * TILE_ROWS) {
+        const int w = tid >> 1, p = tid & 1;
+        float tw = 0.f;
+        if (valid(w)) {
+            const int64_t gw = w0 + w, g = gw / walks_per_group, b = (gw % walks_per_group) / W;
+            const float c = (float)cut[g * (walks_per_group / W) + b];
+            tw = expf(-fabsf(c - ts3[gw * 3 + p]) / (stdv[g] + 1e-6f));
+        }
+        s_mult[tid] = __fadd_rn(0.7f, __fmul_rn(0.3f, tw));   // 1.0 - 0.3 + 0.3 * time_weight (:835-836)
+    }
+    if (tid < TILE_ROWS) s_cat[tid] = valid(tid) ? cat[w0 + tid] : -1;
+    __syncthreads();
+    gemm<4>(Tb, LD, P.w2, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) Qb[erow(mt, r) * LD + c] = acc[r] + P.w2.b[c];
+    });
+    __syncthreads();
+    for (int i = tid; i < TILE_ROWS * (D2 / 4); i += blockDim.x) {
+        const int w = i / (D2 / 4), c4 = i % (D2 / 4);
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (valid(w)) v = reinterpret_cast<const float4 *>(F + ((w0 + w) * 3 + 2) * D2)[c4];
+        *reinterpret_cast<float4 *>(Ob + w * LD + 4 * c4) = v;
+    }
+    __syncthreads();
+    gemm<2>(Ob, LD, P.w1, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) Wp[erow(mt, r) * LD + c] = acc[r] + P.w1.b[c];
+    });
+    __syncthreads();
+    {
+        const int pair = tid >> 2, sub = tid & 3, w = pair >> 1, p = pair & 1;
+        float s = 0.f;
+        for (int c = sub; c < D2; c += 4) s += Wp[w * LD + c] * Qb[(p * TILE_ROWS + w) * LD + c];
+        s += __shfl_xor(s, 1, 4);
+        s += __shfl_xor(s, 2, 4);
+        if (sub == 0) s_score[pair] = s * s_mult[pair];
+    }
+    __syncthreads();
+    if (tid < TILE_ROWS) {
+        const float s0 = s_score[2 * tid], s1 = s_score[2 * tid + 1], mx = fmaxf(s0, s1);
+        const float e0 = expf(s0 - mx), e1 = expf(s1 - mx), sum = e0 + e1;
+        const float a0 = e0 / sum, a1 = e1 / sum;
+        s_alpha[2 * tid] = a0;
+        s_alpha[2 * tid + 1] = a1;
+        s_alphad[2 * tid] = a0 * keep(tid, DROP_A);
+        s_alphad[2 * tid + 1] = a1 * keep(tid, DROP_A + 1);
+    }
+    __syncthreads();
+    for (int i = tid; i < TILE_ROWS * D2; i += blockDim.x) {
+        const int w = i / D2, c = i % D2;
+        const float a = s_alphad[2 * w] * Qb[w * LD + c] + s_alphad[2 * w + 1] * Qb[(TILE_ROWS + w) * LD + c];
+        const float v = Ob[w * LD + c] + a;
+        Ob[w * LD + c] = v;
+        if (valid(w)) o.O[(w0 + w) * D2 + c] = v;
+    }
+    __syncthreads();
+    gemm<2>(Ob, LD, P.a1, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) {
+            const int row = erow(mt, r);
+            const float v = relu(acc[r] + P.a1.b[c]) * keep(row, DROP_H + c);
+            H1[row * LDH + c] = v;
+            if (valid(row)) o.H1d[(w0 + row) * HID + c] = v;
+        }
+    });
+    __syncthreads();
+    gemm<2>(H1, LDH, P.a2, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) Xb[erow(mt, r) * LDM + c] = acc[r] + P.a2.b[c];
+    });
+    for (int i = tid; i < TILE_ROWS * 16; i += blockDim.x) {
+        const int w = i >> 4, c = i & 15;
+        Xb[w * LDM + HID + c] = (c < 12 && s_cat[w] == c) ? 1.f : 0.f;
+    }
+    __syncthreads();
+    for (int i = tid; i < TILE_ROWS * KM; i += blockDim.x) {
+        const int w = i / KM, c = i % KM;
+        if (valid(w)) o.X[(w0 + w) * KM + c] = Xb[w * LDM + c];
+    }
+    gemm<2>(Xb, LDM, P.m1, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) {
+            const int row = erow(mt, r);
+            const float v = c < P.m1.nout ? relu(acc[r] + P.m1.b[c]) * keep(row, DROP_M + c) : 0.f;
+            M1[row * LDM + c] = v;
+            if (valid(row)) o.M1d[(w0 + row) * KM + c] = v;
+        }
+    });
+    __syncthreads();
+    gemm<2>(M1, LDM, P.m2, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) {
+            const int row = erow(mt, r);
+            const float v = relu(acc[r] + P.m2.b[c]);
+            M2[row * LDH + c] = v;
+            if (valid(row)) o.M2[(w0 + row) * HID + c] = v;
+        }
+    });
+    __syncthreads();
+    {
+        const int w = tid >> 3, sub = tid & 7;
+        float s = 0.f;
+        for (int c = sub; c < HID; c += 8) s += M2[w * LDH + c] * P.m3w[c];
+        s += __shfl_xor(s, 1, 8);
+        s += __shfl_xor(s, 2, 8);
+        s += __shfl_xor(s, 4, 8);
+        if (sub == 0) {
+            float dl = 0.f;
+            if (valid(w)) {
+                const float y = 1.f / (1.f + expf(-(s + P.m3b[0])));
+                dl = d_imp[w0 + w] * (1.f - y) * y;   // sigmoid backward
+                if (o.imp) o.imp[w0 + w] = y;
+                o.dlogit[w0 + w] = dl;
+            }
+            s_dl[w] = dl;
+        }
+    }
+    __syncthreads();
+
+    // ---- backward through the MLP head
+    for (int i = tid; i < TILE_ROWS * HID; i += blockDim.x) {
+        const int w = i / HID, c = i % HID;
+        const float v = M2[w * LDH + c] > 0.f ? s_dl[w] * P.m3w[c] : 0.f;
+        M2[w * LDH + c] = v;
+        if (valid(w)) o.dM2[(w0 + w) * HID + c] = v;
+    }
+    __syncthreads();
+    gemm<2>(M2, LDH, T.m2T, [&](int mt, int nt, floatx4 acc) {   // d M1d = dM2 P3
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) {
+            const int row = erow(mt, r);
+            const float v = (c < P.m1.nout && M1[row * LDM + c] > 0.f) ? acc[r] * kscale : 0.f;
+            M1[row * LDM + c] = v;
+            if (valid(row)) o.dM1[(w0 + row) * KM + c] = v;
+        }
+    });
+    __syncthreads();
+    gemm<2>(M1, LDM, T.m1T, [&](int mt, int nt, floatx4 acc) {   // d X = dM1 P0; keep the attention part
+        const int c = ecol(nt);
+        if (c < HID) {
+            for (int r = 0; r < 4; ++r) {
+                const int row = erow(mt, r);
+                Xb[row * LDM + c] = acc[r];
+                if (valid(row)) o.dY2[(w0 + row) * HID + c] = acc[r];
+            }
+        }
+    });
+    __syncthreads();
+    gemm<2>(Xb, LDM, T.a2T, [&](int mt, int nt, floatx4 acc) {   // d H1d = dY2 A3
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) {
+            const int row = erow(mt, r);
+            const float v = H1[row * LDH + c] > 0.f ? acc[r] * kscale : 0.f;
+            H1[row * LDH + c] = v;
+            if (valid(row)) o.dH1[(w0 + row) * HID + c] = v;
+        }
+    });
+    __syncthreads();
+    gemm<2>(H1, LDH, T.a1T, [&](int mt, int nt, floatx4 acc) {   // d O = dH1 A0
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) Ob[erow(mt, r) * LD + c] = acc[r];
+    });
+    __syncthreads();
+    {   // d alpha'_k = dO . Wq_k
+        const int pair = tid >> 2, sub = tid & 3, w = pair >> 1, p = pair & 1;
+        float s = 0.f;
+        for (int c = sub; c < D2; c += 4) s += Ob[w * LD + c] * Qb[(p * TILE_ROWS + w) * LD + c];
+        s += __shfl_xor(s, 1, 4);
+        s += __shfl_xor(s, 2, 4);
+        if (sub == 0) s_score[pair] = s;
+    }
+    __syncthreads();
+    if (tid < TILE_ROWS) {   // dropout, softmax and temporal-scaling backward
+        const float a0 = s_alpha[2 * tid], a1 = s_alpha[2 * tid + 1];
+        const float g0 = s_score[2 * tid] * keep(tid, DROP_A), g1 = s_score[2 * tid + 1] * keep(tid, DROP_A + 1);
+        const float dot = g0 * a0 + g1 * a1;
+        s_dsr[2 * tid] = (g0 - dot) * a0 * s_mult[2 * tid];
+        s_dsr[2 * tid + 1] = (g1 - dot) * a1 * s_mult[2 * tid + 1];
+    }
+    __syncthreads();
+    for (int i = tid; i < TILE_ROWS * D2; i += blockDim.x) {
+        const int w = i / D2, c = i % D2;
+        const float q0 = Qb[w * LD + c], q1 = Qb[(TILE_ROWS + w) * LD + c], wp = Wp[w * LD + c], dO = Ob[w * LD + c];
+        const float ds0 = s_dsr[2 * w], ds1 = s_dsr[2 * w + 1];
+        const float dq0 = s_alphad[2 * w] * dO + ds0 * wp, dq1 = s_alphad[2 * w + 1] * dO + ds1 * wp;
+        const float dp = ds0 * q0 + ds1 * q1;
+        Qb[w * LD + c] = dq0;
+        Qb[(TILE_ROWS + w) * LD + c] = dq1;
+        Wp[w * LD + c] = dp;
+        if (valid(w)) {
+            o.dQ[(w0 + w) * D2 + c] = dq0;
+            o.dQ[(n_walks + w0 + w) * D2 + c] = dq1;
+            o.dP[(w0 + w) * D2 + c] = dp;
+        }
+    }
+    __syncthreads();
+    gemm<4>(Qb, LD, T.w2T, [&](int mt, int nt, floatx4 acc) {   // dF0, dF1 = dQ W2
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) {
+            const int row = erow(mt, r), p = row / TILE_ROWS, w = row % TILE_ROWS;
+            if (valid(w)) o.dF[((w0 + w) * 3 + p) * D2 + c] = acc[r];
+        }
+    });
+    gemm<2>(Wp, LD, T.w1T, [&](int mt, int nt, floatx4 acc) {   // dF2 = dO + dP W1
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) {
+            const int row = erow(mt, r);
+            if (valid(row)) o.dF[((w0 + row) * 3 + 2) * D2 + c] = acc[r] + Ob[row * LD + c];
+        }
+    });
+}
+
+// ------------------------------------------------------------------ event_gcn backward
+struct GcnBwdOut {
+    float *ev;    // [R][kev16]     event features                    (lin_event: with dlev)
+    float *AB;    // [R][2][dn16]   [x_s + relu(a) | x_t + relu(b)]     (MLP.0: with dZ)
+    float *H;     // [R][2][64]     relu(MLP.0 .)                       (MLP.2: with dF)
+    float *dZ;    // [R][2][64]     d MLP.0 pre-activation
+    float *dlev;  // [R][dn16]      d lin_event output
+    float *g;     // [R][dn16]      d time feature * -sin(dt w + phi)   (phase: sum; freq: dt^T g)
+    float *dt;    // [R]            dt of the row (relative to walk position 2)
+};
+
+__global__ void __launch_bounds__(256) gcn_bwd_kernel(EncW P, EncWT T, int64_t n_rows, const float *__restrict__ n_feat,
+                                                      const float *__restrict__ e_feat,
+                                                      const int32_t *__restrict__ node6, const int32_t *__restrict__ eid3,
+                                                      const float *__restrict__ ts3, const float *__restrict__ cnt,
+                                                      const float *__restrict__ dF, GcnBwdOut o) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int de = P.de, dn = P.dn, kev = P.kev, kev16 = r16(kev), dn16 = r16(dn);
+    const int ldx = kev16 + 8, ldab = dn16 + 8, ldh = HID + 8;
+    const int xsz = max(TILE_ROWS * ldx, 2 * TILE_ROWS * ldh);
+    float *X = smem;                                     // [32][ldx]  event features -> dU [64][ldh]
+    float *dU = X;
+    float *AB = X + xsz;                                 // [64][ldab] hs rows 0..31, ht rows 32..63 -> d lev
+    float *Hb = AB + 2 * TILE_ROWS * ldab;               // [64][ldh]  z = relu(MLP.0 .) -> dZ
+    uint8_t *MK = reinterpret_cast<uint8_t *>(Hb + 2 * TILE_ROWS * ldh);   // [64][dn16] relu masks of a / b
+    __shared__ int32_t s_eid[TILE_ROWS], s_ns[TILE_ROWS], s_nt[TILE_ROWS];
+    __shared__ float s_dt[TILE_ROWS], s_cnt[TILE_ROWS * 3];
+    const int64_t row0 = (int64_t)blockIdx.x * TILE_ROWS;
+    const int tid = threadIdx.x;
+    auto valid = [&](int r) { return row0 + r < n_rows; };
+    if (tid < TILE_ROWS) {
+        const int64_t r = row0 + tid;
+        if (r < n_rows) {
+            const int64_t w = r / 3;
+            const int p = (int)(r % 3);
+            s_eid[tid] = eid3[w * 3 + p];
+            s_ns[tid] = node6[w * 6 + 2 * p];
+            s_nt[tid] = node6[w * 6 + 2 * p + 1];
+            s_dt[tid] = ts3[w * 3 + 2] - ts3[w * 3 + p];
+            for (int q = 0; q < 3; ++q) s_cnt[tid * 3 + q] = cnt[w * 9 + p * 3 + q];
+            o.dt[r] = s_dt[tid];
+        } else {
+            s_eid[tid] = 0; s_ns[tid] = 0; s_nt[tid] = 0; s_dt[tid] = 0.f;
+            for (int q = 0; q < 3; ++q) s_cnt[tid * 3 + q] = 0.f;
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < TILE_ROWS * kev16; i += blockDim.x) {
+        const int r = i / kev16, c = i % kev16;
+        float v = 0.f;
+        if (valid(r)) {
+            if (c < de) v = e_feat[(int64_t)s_eid[r] * de + c];
+            else if (c < de + 3) v = s_cnt[r * 3 + (c - de)];
+            else if (c < kev) v = time_cos(s_dt[r], P.freq[c - de - 3], P.phase[c - de - 3]);
+            o.ev[(row0 + r) * kev16 + c] = v;
+        }
+        X[r * ldx + c] = v;
+    }
+    __syncthreads();
+    gemm<2>(X, ldx, P.ev, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) {
+            const int row = erow(mt, r);
+            float hs = 0.f, ht = 0.f;
+            uint8_t ma = 0, mb = 0;
+            if (c < dn) {
+                const float L = acc[r] + P.ev.b[c];
+                const float xs = n_feat[(int64_t)s_ns[row] * dn + c], xt = n_feat[(int64_t)s_nt[row] * dn + c];
+                const float a = xt + L, b = xs + L;
+                hs = xs + relu(a);
+                ht = xt + relu(b);
+                ma = a > 0.f;
+                mb = b > 0.f;
+            }
+            AB[row * ldab + c] = hs;
+            AB[(row + TILE_ROWS) * ldab + c] = ht;
+            MK[row * dn16 + c] = ma;
+            MK[(row + TILE_ROWS) * dn16 + c] = mb;
+            if (valid(row)) {
+                o.AB[((row0 + row) * 2) * dn16 + c] = hs;
+                o.AB[((row0 + row) * 2 + 1) * dn16 + c] = ht;
+            }
+        }
+    });
+    __syncthreads();
+    for (int i = tid; i < 2 * TILE_ROWS * HID; i += blockDim.x) {   // dU: d U_s rows 0..31, d U_t rows 32..63
+        const int row = i / HID, c = i % HID, r = row % TILE_ROWS, half = row / TILE_ROWS;
+        dU[row * ldh + c] = valid(r) ? dF[(row0 + r) * (2 * HID) + half * HID + c] : 0.f;
+    }
+    gemm<4>(AB, ldab, P.g1, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) {
+            const int row = erow(mt, r), rr = row % TILE_ROWS, half = row / TILE_ROWS;
+            const float v = relu(acc[r] + P.g1.b[c]);
+            Hb[row * ldh + c] = v;
+            if (valid(rr)) o.H[((row0 + rr) * 2 + half) * HID + c] = v;
+        }
+    });
+    __syncthreads();
+    gemm<4>(dU, ldh, T.g2T, [&](int mt, int nt, floatx4 acc) {   // dZ = (dU M2) * [z > 0]
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) {
+            const int row = erow(mt, r), rr = row % TILE_ROWS, half = row / TILE_ROWS;
+            const float v = Hb[row * ldh + c] > 0.f ? acc[r] : 0.f;
+            Hb[row * ldh + c] = v;
+            if (valid(rr)) o.dZ[((row0 + rr) * 2 + half) * HID + c] = v;
+        }
+    });
+    __syncthreads();
+    // d lev = (dZ_s M0) * [a > 0] + (dZ_t M0) * [b > 0]; rows r and r + 32 of one column land in the same
+    // lane (row tiles mt and mt + 2, in that order), so the sum needs no synchronisation.
+    float *DL = AB;
+    gemm<4>(Hb, ldh, T.g1T, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) {
+            const int row = erow(mt, r);
+            const float v = MK[row * dn16 + c] ? acc[r] : 0.f;
+            if (mt < 2) {
+                DL[row * ldab + c] = v;
+            } else {
+                const int rr = row - TILE_ROWS;
+                const float s = DL[rr * ldab + c] + v;
+                DL[rr * ldab + c] = s;
+                if (valid(rr)) o.dlev[(row0 + rr) * dn16 + c] = s;
+            }
+        }
+    });
+    __syncthreads();
+    gemm<2>(DL, ldab, T.evT, [&](int mt, int nt, floatx4 acc) {   // d time features -> * -sin(dt w + phi)
+        const int j = ecol(nt);
+        for (int r = 0; r < 4; ++r) {
+            const int row = erow(mt, r);
+            if (!valid(row)) continue;
+            float gv = 0.f;
+            if (j < dn) gv = -acc[r] * sinf(__fadd_rn(__fmul_rn(s_dt[row], P.freq[j]), P.phase[j]));
+            o.g[(row0 + row) * dn16 + j] = gv;
+        }
+    });
+}
+
+}  // namespace tmk
+
+using namespace tmk;
+
+// ------------------------------------------------------------------ host side
+int train_packs_create(tm_weights *w) {
+    const int de = w->de, dn = w->dn, h = w->h, h2 = 2 * h, hm = h + 12, kev = de + 3 + dn;
+    (void)kev;
+    struct D {
+        Lin *lin;
+        int nout, k;
+    } ds[] = {{&w->T.evT, dn, dn}, {&w->T.g1T, dn, h}, {&w->T.g2T, h, h},   {&w->T.w1T, h2, h2}, {&w->T.w2T, h2, h2},
+              {&w->T.a1T, h2, h},  {&w->T.a2T, h, h},  {&w->T.m1T, hm, hm}, {&w->T.m2T, hm, h}};
+    size_t total = 0;
+    std::vector<size_t> off;
+    for (auto &d : ds) {
+        d.lin->nt = r16(d.nout) / 16;
+        d.lin->nq = r16(d.k) / 16;
+        d.lin->nout = d.nout;
+        d.lin->k = d.k;
+        d.lin->b = nullptr;
+        off.push_back(total);
+        total += (size_t)d.lin->nt * d.lin->nq * 256;
+    }
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (hipSetDevice(w->device) != hipSuccess || hipMalloc(&w->tbuf, total * sizeof(float)) != hipSuccess ||
+        hipMemset(w->tbuf, 0, total * sizeof(float)) != hipSuccess) {
+        (void)hipSetDevice(prev);
+        w->tbuf = nullptr;
+        return fail(TM_E_HIP, "tm_weights_create: allocation of the transposed packs failed");
+    }
+    (void)hipSetDevice(prev);
+    w->t_floats = total;
+    for (size_t i = 0; i < off.size(); ++i) ds[i].lin->w = reinterpret_cast<const float4 *>(w->tbuf + off[i]);
+    return TM_OK;
+}
+
+void train_packs_fill(tm_weights *w, const float *const *t, hipStream_t s) {
+    const int de = w->de, dn = w->dn, h = w->h, h2 = 2 * h, hm = h + 12, kev = de + 3 + dn;
+    // job: packed (o, c) = src[o * so + c * sc]; transposed packs of W[nout][k]: so = 1, sc = k
+    struct J {
+        const Lin *lin;
+        const float *src;
+        int so, sc;
+    } js[] = {{&w->T.evT, t[0] + de + 3, 1, kev}, {&w->T.g1T, t[2], 1, dn}, {&w->T.g2T, t[4], 1, h},
+              {&w->T.w1T, t[6], 1, h2},           {&w->T.w2T, t[8], 1, h2}, {&w->T.a1T, t[10], 1, h2},
+              {&w->T.a2T, t[12], 1, h},           {&w->T.m1T, t[14], 1, hm}, {&w->T.m2T, t[16], 1, hm}};
+    PackJobs P{};
+    int64_t total = 0;
+    P.n = 0;
+    for (auto &j : js) {
+        PackJob &p = P.j[P.n++];
+        p.src = j.src;
+        p.dst = const_cast<float *>(reinterpret_cast<const float *>(j.lin->w));
+        p.so = j.so;
+        p.sc = j.sc;
+        p.nout = j.lin->nout;
+        p.k = j.lin->k;
+        p.nt = j.lin->nt;
+        p.nq = j.lin->nq;
+        p.begin = total;
+        total += (int64_t)p.nt * p.nq * 256;
+    }
+    P.total = total;
+    pack_jobs_kernel<<<dim3(128), 256, 0, s>>>(P);
+}
+
+void train_packs_free(tm_weights *w) {
+    if (w->tbuf) (void)hipFree(w->tbuf);
+    w->tbuf = nullptr;
+}
+
+static size_t head_bwd_lds() {
+    constexpr int D2 = 2 * HID, LD = D2 + 8, LDH = HID + 8, LDM = r16(HID + 12) + 8;
+    return sizeof(float) * (128 * LD + 2 * TILE_ROWS * LDH + 2 * TILE_ROWS * LDM);
+}
+static size_t gcn_bwd_lds(const EncW &P) {
+    const int ldx = r16(P.kev) + 8, ldab = r16(P.dn) + 8, ldh = HID + 8;
+    const size_t xsz = std::max(TILE_ROWS * ldx, 2 * TILE_ROWS * ldh);
+    return sizeof(float) * (xsz + 2 * TILE_ROWS * ldab + 2 * TILE_ROWS * ldh) + 2 * TILE_ROWS * r16(P.dn);
+}
+
+extern "C" int tm_encoder_bwd(const tm_weights *w, const float *n_feat, const float *e_feat, int32_t n_groups,
+                              int32_t B, int32_t W, const int32_t *node6, const int32_t *eid3, const float *ts3,
+                              const int32_t *cat, const double *cut, const float *cnt, const uint8_t *drop,
+                              float drop_scale, const void *workspace, const float *d_imp, const tm_encoder_grad_io *io,
+                              void *stream) {
+    if (!w || !io || n_groups < 0 || B < 0 || W < 0) return fail(TM_E_ARG, "tm_encoder_bwd: bad arguments");
+    const int64_t n_walks = (int64_t)n_groups * B * W;
+    if (n_walks == 0) return TM_OK;
+    if (!n_feat || !e_feat || !node6 || !eid3 || !ts3 || !cat || !cut || !cnt || !workspace || !d_imp)
+        return fail(TM_E_ARG, "tm_encoder_bwd: NULL pointer");
+    if (!io->dlogit || !io->M2 || !io->dM2 || !io->M1d || !io->dM1 || !io->X || !io->dY2 || !io->H1d || !io->dH1 ||
+        !io->O || !io->dP || !io->dQ || !io->dF || !io->ev || !io->AB || !io->H || !io->dZ || !io->dlev || !io->g ||
+        !io->dt)
+        return fail(TM_E_ARG, "tm_encoder_bwd: NULL output buffer");
+    if (!w->tbuf) return fail(TM_E_ARG, "tm_encoder_bwd: weights have no transposed packs");
+    const EncW &P = w->P;
+    const size_t lh = head_bwd_lds(), lg = gcn_bwd_lds(P);
+    if (lh > 160 * 1024 || lg > 160 * 1024) return fail(TM_E_UNSUPPORTED, "tm_encoder_bwd: LDS budget exceeded");
+    hipStream_t s = S_(stream);
+    const float *F = reinterpret_cast<const float *>(workspace);
+    const float *stdv = F + n_walks * 3 * 2 * HID;
+    HeadBwdOut ho{io->imp, io->dlogit, io->M2, io->dM2, io->M1d, io->dM1, io->X, io->dY2, io->H1d, io->dH1, io->O,
+                  io->dP,  io->dQ,     io->dF};
+    hipEvent_t pe = prof_begin(s);
+    head_bwd_kernel<<<dim3((unsigned)((n_walks + TILE_ROWS - 1) / TILE_ROWS)), 256, lh, s>>>(
+        P, w->T, n_walks, (int64_t)B * W, W, F, ts3, cut, cat, stdv, drop, drop_scale, d_imp, ho);
+    TM_CHECK_LAUNCH();
+    prof_end("head_bwd_kernel", s, pe);
+    const int64_t n_rows = n_walks * 3;
+    GcnBwdOut go{io->ev, io->AB, io->H, io->dZ, io->dlev, io->g, io->dt};
+    pe = prof_begin(s);
+    gcn_bwd_kernel<<<dim3((unsigned)((n_rows + TILE_ROWS - 1) / TILE_ROWS)), 256, lg, s>>>(
+        P, w->T, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, io->dF, go);
+    TM_CHECK_LAUNCH();
+    prof_end("gcn_bwd_kernel", s, pe);
+    return TM_OK;
+}

@@ -222,6 +222,91 @@ class TempME(nn.Module):
                                            L.ptr(out1), L.ptr(out2), L.stream_ptr(dev)), "retrieve_edge_imp_node")
         return out1, out2
 
+    # ------------------------------------------------------------------ HIP training path (f3)
+    def _encoder_params(self):
+        """The 22 tensors TempME.forward reads (tm_weights order minus the dependency gate)."""
+        at, ec, m = self.attention, self.event_conv, self.MLP
+        ts = []
+        for mod in (ec.lin_event, ec.MLP[0], ec.MLP[2], at.W1, at.W2, at.MLP[0], at.MLP[3], m[0], m[3], m[5]):
+            ts += [mod.weight, mod.bias]
+        return ts + [self.time_encoder.basis_freq, self.time_encoder.phase]
+
+    def dropout_masks(self, n_walks):
+        """Keep-masks of the three dropouts TempME.forward applies in training (explainer_new.py:839 alpha,
+        :780 attention.MLP hidden, :122 MLP hidden), uint8 [n_walks, 144] from torch's device RNG, or
+        None when they are inactive (eval mode or p = 0)."""
+        p = self.dropout_p
+        if not self.training or p <= 0:
+            return None, 1.0
+        dev = self._dev()
+        return torch.empty(n_walks, 144, dtype=torch.uint8, device=dev).bernoulli_(1.0 - p), 1.0 / (1.0 - p)
+
+    def forward_groups(self, node6, eid3, ts3, cat, cut, cnt, n_groups, B, W, drop=None, drop_scale=1.0,
+                       use_module_dropout=True):
+        """TempME.forward for n_groups independent reference calls at once (e.g. the src/tgt/bgd sides
+        of one batch; the attention's time std is per group) with gradients to the encoder's weights:
+        tm_encoder_train_fwd forward, tm_encoder_bwd + weight-gradient GEMMs backward.  Inputs are device
+        tensors shaped [G,B,W,...]; returns [G*B*W] graphlet importance."""
+        dev = self._dev()
+        if drop is None and use_module_dropout:
+            drop, drop_scale = self.dropout_masks(n_groups * B * W)
+        args = (node6.to(dev, torch.int32).contiguous(), eid3.to(dev, torch.int32).contiguous(),
+                ts3.to(dev, torch.float32).contiguous(), cat.to(dev, torch.int32).contiguous(),
+                cut.to(dev, torch.float64).contiguous(), cnt.to(dev, torch.float32).contiguous(),
+                int(n_groups), int(B), int(W))
+        return _EncoderFn.apply(self, args, drop, float(drop_scale), *self._encoder_params())
+
+    def _train_fwd(self, args, drop, drop_scale):
+        node6, eid3, ts3, cat, cut, cnt, G, B, W = args
+        dev = self._dev()
+        nt, et = self.feature_tables()
+        n = G * B * W
+        out = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+        ws = torch.empty(L.lib().tm_encoder_workspace_bytes(self.packed_weights(), n), dtype=torch.uint8, device=dev)
+        L.check(L.lib().tm_encoder_train_fwd(self.packed_weights(), L.ptr(nt), L.ptr(et), G, B, W, L.ptr(node6),
+                                             L.ptr(eid3), L.ptr(ts3), L.ptr(cat), L.ptr(cut), L.ptr(cnt), L.ptr(drop),
+                                             drop_scale, L.ptr(ws), L.ptr(out), L.stream_ptr(dev)),
+                "TempME.forward (training)")
+        return out[:n], ws
+
+    def _train_bwd(self, args, drop, drop_scale, ws, d_imp):
+        node6, eid3, ts3, cat, cut, cnt, G, B, W = args
+        dev = self._dev()
+        nt, et = self.feature_tables()
+        n = G * B * W
+        R = 3 * n
+        de, dn, h = self.edge_dim, self.node_dim, self.hid_dim
+        kev = de + 3 + dn
+        KE, DN, KM = -(-kev // 16) * 16, -(-dn // 16) * 16, -(-(h + 12) // 16) * 16
+        e = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
+        b = dict(imp=None, dlogit=e(n), M2=e(n, h), dM2=e(n, h), M1d=e(n, KM), dM1=e(n, KM), X=e(n, KM), dY2=e(n, h),
+                 H1d=e(n, h), dH1=e(n, h), O=e(n, 2 * h), dP=e(n, 2 * h), dQ=e(2, n, 2 * h), dF=e(n, 3, 2 * h),
+                 ev=e(R, KE), AB=e(R, 2, DN), H=e(R, 2, h), dZ=e(R, 2, h), dlev=e(R, DN), g=e(R, DN), dt=e(R))
+        io = L.EncoderGradIO(*[None if b[k] is None else b[k].data_ptr() for k in L.GRAD_IO_FIELDS])
+        d_imp = d_imp.to(dev, torch.float32).contiguous()
+        L.check(L.lib().tm_encoder_bwd(self.packed_weights(), L.ptr(nt), L.ptr(et), G, B, W, L.ptr(node6),
+                                       L.ptr(eid3), L.ptr(ts3), L.ptr(cat), L.ptr(cut), L.ptr(cnt), L.ptr(drop),
+                                       drop_scale, L.ptr(ws), L.ptr(d_imp), L.C.byref(io), L.stream_ptr(dev)),
+                "TempME.forward backward")
+        F = ws[:n * 3 * 2 * h * 4].view(torch.float32).view(n, 3, 2 * h)
+        hm = h + 12
+        dlev, g = b["dlev"][:, :dn], b["g"][:, :dn]
+        dZ, dU = b["dZ"].view(2 * R, h), b["dF"].view(2 * R, h)
+        dQ, dP = b["dQ"], b["dP"]
+        dM1, dM2 = b["dM1"][:, :hm], b["dM2"]
+        gW2 = torch.addmm(dQ[0].t() @ F[:, 0], dQ[1].t(), F[:, 1])
+        return (dlev.t() @ b["ev"][:, :kev], dlev.sum(0),
+                dZ.t() @ b["AB"].view(2 * R, DN)[:, :dn], dZ.sum(0),
+                dU.t() @ b["H"].view(2 * R, h), dU.sum(0),
+                dP.t() @ F[:, 2], dP.sum(0),
+                gW2, dQ.sum((0, 1)),
+                b["dH1"].t() @ b["O"], b["dH1"].sum(0),
+                b["dY2"].t() @ b["H1d"], b["dY2"].sum(0),
+                dM1.t() @ b["X"][:, :hm], dM1.sum(0),
+                dM2.t() @ b["M1d"][:, :hm], dM2.sum(0),
+                b["dlogit"].view(1, n) @ b["M2"], b["dlogit"].sum().view(1),
+                b["dt"].view(1, R) @ g, g.sum(0))
+
     # ------------------------------------------------------------------ reference API
     def forward(self, walks, cut_time_l, edge_identify):
         """explainer_new.py:174-201 -> [bsz, n_walks, 1]."""
@@ -229,8 +314,13 @@ class TempME(nn.Module):
         dev = self._dev()
         B, W = np.shape(edge_idx)[0], np.shape(edge_idx)[1]
         assert np.shape(edge_identify)[-1] == 3 and np.shape(edge_idx)[-1] == 3, "event_dim mismatch (:180)"
-        if self._needs_autograd() or not self._hip_ok():
+        if not self._hip_ok():
             return self._forward_torch(walks, cut_time_l, edge_identify)
+        if self._needs_autograd():
+            out = self.forward_groups(_to(node_idx, dev, torch.int32), _to(edge_idx, dev, torch.int32),
+                                      _to(time_idx, dev, torch.float32), _to(cat_feat, dev, torch.int32).reshape(B, W),
+                                      _to(cut_time_l, dev, torch.float64), _to(edge_identify, dev, torch.float32), 1, B, W)
+            return out.view(B, W, 1)
         out = self.encoder_fwd(_to(node_idx, dev, torch.int32).contiguous(), _to(edge_idx, dev, torch.int32).contiguous(),
                                _to(time_idx, dev, torch.float32).contiguous(),
                                _to(cat_feat, dev, torch.int32).reshape(B, W).contiguous(),
@@ -357,3 +447,19 @@ class _Packed:
         if self.h is not None and L._lib is not None:
             L._lib.tm_weights_free(self.h)
             self.h = None
+
+
+class _EncoderFn(torch.autograd.Function):
+    """TempME.forward with its backward on the HIP kernels (tm_encoder_train_fwd / tm_encoder_bwd)."""
+
+    @staticmethod
+    def forward(ctx, ex, args, drop, drop_scale, *params):
+        out, ws = ex._train_fwd(args, drop, drop_scale)
+        ctx.ex, ctx.args, ctx.drop, ctx.drop_scale, ctx.ws = ex, args, drop, drop_scale, ws
+        return out
+
+    @staticmethod
+    def backward(ctx, d_imp):
+        grads = ctx.ex._train_bwd(ctx.args, ctx.drop, ctx.drop_scale, ctx.ws, d_imp)
+        ctx.ws = None
+        return (None, None, None, None, *grads)

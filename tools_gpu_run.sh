@@ -17,6 +17,7 @@ step() {  # step <name> <timeout_s> <cmd...>
 for s in "$@"; do
     case $s in
         tests) step pytest_gpu 900 python -m pytest tests -x -q -m gpu ;;
+        f3) step pytest_f3 600 python -u -m pytest tests/test_gpu_encoder_train.py tests/test_gpu_train.py tests/test_gpu_pack.py -x -v --timeout 300 -m gpu ;;
         tgn) step pytest_tgn 600 python -m pytest tests/test_gpu_tgn.py tests/test_gpu_train.py tests/test_gpu_graphmixer.py -x -q -m gpu ;;
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) step bench 600 python bench.py --steps 10 --warmup 2 ;;
