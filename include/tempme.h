@@ -192,6 +192,16 @@ int tm_encoder_bwd(const tm_weights *w, const float *n_feat, const float *e_feat
                    const double *cut, const float *cnt, const uint8_t *drop, float drop_scale, const void *workspace,
                    const float *d_imp, const tm_encoder_grad_io *io, void *stream);
 
+/* Weight gradients of the encoder from tm_encoder_bwd's buffers (io, same n_groups/B/W) and the
+ * training forward's workspace: grads = 22 DEVICE pointers, written (not accumulated), in the tm_weights
+ * order without the dependency gate: lin_event w/b, event_conv.MLP.0 w/b, .MLP.2 w/b, attention.W1 w/b,
+ * .W2 w/b, .MLP.0 w/b, .MLP.3 w/b, MLP.0 w/b, MLP.3 w/b, MLP.5 w/b, time_encoder.basis_freq, .phase.
+ * dW = dY^T X over all rows, computed as per-chunk MFMA partials plus one fixed-order reduce
+ * (deterministic). */
+#define TM_N_ENC_GRADS 22
+int tm_encoder_wgrad(const tm_weights *w, int32_t n_groups, int32_t B, int32_t W, const tm_encoder_grad_io *io,
+                     const void *workspace, float *const *grads, void *stream);
+
 /* retrieve_edge_imp_node, eval (explainer_new.py:354-406, :420-430) for each of the G*B
  * (group, event) rows: dependency gate, walk->edge scatter-max, gather at the subgraph eids,
  * Beta mean, node==0 mask.  sub1_* [G,B,N], sub2_* [G,B,N*N]; out_h1 [G,B,N], out_h2 [G,B,N*N]

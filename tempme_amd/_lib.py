@@ -34,7 +34,8 @@ EXPORTS = (
     "tm_last_error", "tm_version", "tm_graph_build", "tm_graph_free", "tm_graph_info", "tm_graph_export",
     "tm_sample_khop", "tm_sample_walks", "tm_neg_sample", "tm_perm_keys", "tm_motif_hist", "tm_edge_counts",
     "tm_sample_events", "tm_weights_create", "tm_weights_pack", "tm_weights_free", "tm_encoder_workspace_bytes",
-    "tm_encoder_fwd", "tm_encoder_train_fwd", "tm_encoder_bwd", "tm_edge_importance", "tm_edge_gate_table", "tm_edge_importance_tab", "tm_tgn_attn_fwd",
+    "tm_encoder_fwd", "tm_encoder_train_fwd", "tm_encoder_bwd",
+    "tm_encoder_wgrad", "tm_edge_importance", "tm_edge_gate_table", "tm_edge_importance_tab", "tm_tgn_attn_fwd",
     "tm_tgn_attn_bwd", "tm_mask_least_important", "tm_profile_enable", "tm_profile_sync", "tm_profile_entry",
 )
 
@@ -96,6 +97,7 @@ def _sig(L):
     L.tm_encoder_train_fwd.argtypes = [vp, vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, C.c_float, vp, vp, vp]
     L.tm_encoder_bwd.argtypes = [vp, vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, C.c_float, vp, vp,
                                  C.POINTER(EncoderGradIO), vp]
+    L.tm_encoder_wgrad.argtypes = [vp, i32, i32, i32, C.POINTER(EncoderGradIO), vp, C.POINTER(vp), vp]
     L.tm_edge_importance.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.tm_edge_gate_table.argtypes = [vp, vp, vp, vp, vp]
     L.tm_edge_importance_tab.argtypes = [vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]

@@ -983,21 +983,8 @@ __global__ void __launch_bounds__(256) explain_tab_kernel(int32_t W, int32_t N, 
 }
 
 // ------------------------------------------------------------------ weight packing
-// packed[((nt*nq + q)*64 + l)*4 + s] = W[16nt + (l&15)][16q + 4(l>>4) + s]
-__global__ void pack_kernel(const float *__restrict__ W, int nout, int k, int nt, int nq, float *__restrict__ out) {
-    const int64_t n = (int64_t)nt * nq * 256;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int s = i & 3, l = (i >> 2) & 63;
-        const int64_t tq = i >> 8;
-        const int q = (int)(tq % nq), t = (int)(tq / nq);
-        const int o = 16 * t + (l & 15), c = 16 * q + 4 * (l >> 4) + s;
-        out[i] = (o < nout && c < k) ? W[(int64_t)o * k + c] : 0.f;
-    }
-}
-
-__global__ void copy_pad_kernel(const float *__restrict__ src, int n, int npad, float *__restrict__ dst) {
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < npad; i += gridDim.x * blockDim.x) dst[i] = i < n ? src[i] : 0.f;
-}
+// packed[((nt*nq + q)*64 + l)*4 + s] = W[16nt + (l&15)][16q + 4(l>>4) + s]; all packs (and the slot
+// pass's folded bias evc) are written by pack_all_weights (encoder_train.hip) in one launch.
 
 }  // namespace tmk
 
@@ -1077,37 +1064,12 @@ extern "C" int tm_weights_create(int32_t de, int32_t dn, int32_t h, int device, 
     return TM_OK;
 }
 
-// evc[f] = b[f] + sum_{k >= 16 qt} W[f][k] * cos(0 * w + phi)  (fp64 sum, one rounding)
-__global__ void evc_kernel(const float *__restrict__ W, const float *__restrict__ b, const float *__restrict__ phase,
-                           int de, int dn, int kev, int qt, float *__restrict__ out) {
-    for (int f = threadIdx.x; f < r16(dn); f += blockDim.x) {
-        double acc = 0.0;
-        if (f < dn) {
-            acc = b[f];
-            for (int k = 16 * qt; k < kev; ++k) acc += (double)W[(int64_t)f * kev + k] * (double)cos_rd(phase[k - de - 3]);
-        }
-        out[f] = (float)acc;
-    }
-}
-
 extern "C" int tm_weights_pack(tm_weights *w, const float *const *t, void *stream) {
     if (!w || !t) return fail(TM_E_ARG, "tm_weights_pack: bad arguments");
     for (int i = 0; i < TM_N_WEIGHTS; ++i)
         if (!t[i]) return fail(TM_E_ARG, "tm_weights_pack: NULL tensor " + std::to_string(i));
     hipStream_t s = S_(stream);
-    for (auto &sp : w->specs) {
-        Lin *l = sp.lin;
-        pack_kernel<<<dim3(64), 256, 0, s>>>(t[sp.wi], sp.nout, sp.k, l->nt, l->nq, const_cast<float *>(reinterpret_cast<const float *>(l->w)));
-        copy_pad_kernel<<<dim3(1), 256, 0, s>>>(t[sp.wi + 1], sp.nout, l->nt * 16, const_cast<float *>(l->b));
-    }
-    copy_pad_kernel<<<dim3(1), 256, 0, s>>>(t[18], w->h, 64, const_cast<float *>(w->P.m3w));
-    copy_pad_kernel<<<dim3(1), 256, 0, s>>>(t[19], 1, 4, const_cast<float *>(w->P.m3b));
-    copy_pad_kernel<<<dim3(1), 256, 0, s>>>(t[24], w->h / 2, 64, const_cast<float *>(w->P.d3w));
-    copy_pad_kernel<<<dim3(1), 256, 0, s>>>(t[25], 1, 4, const_cast<float *>(w->P.d3b));
-    copy_pad_kernel<<<dim3(1), 256, 0, s>>>(t[26], w->dn, r16(w->dn), const_cast<float *>(w->P.freq));
-    copy_pad_kernel<<<dim3(1), 256, 0, s>>>(t[27], w->dn, r16(w->dn), const_cast<float *>(w->P.phase));
-    evc_kernel<<<dim3(1), 256, 0, s>>>(t[0], t[1], t[27], w->de, w->dn, w->P.kev, w->P.qt, const_cast<float *>(w->P.evc));
-    train_packs_fill(w, t, s);
+    pack_all_weights(w, t, s);
     TM_CHECK_LAUNCH();
     return TM_OK;
 }

@@ -128,9 +128,9 @@ struct tm_weights {
     size_t t_floats = 0;
 };
 
-// encoder_train.hip: allocate / fill the transposed packs (called by tm_weights_create / _pack / _free)
+// encoder_train.hip: transposed packs (tm_weights_create / _free) and the one-launch packing of every tensor
 int train_packs_create(tm_weights *w);
-void train_packs_fill(tm_weights *w, const float *const *t, hipStream_t s);
+void pack_all_weights(tm_weights *w, const float *const *t, hipStream_t s);   // every pack, one launch (+ evc)
 void train_packs_free(tm_weights *w);
 
 static inline hipStream_t S_(void *s) { return (hipStream_t)s; }

@@ -16,21 +16,24 @@
 //
 // Every data-gradient GEMM (dX = dY W) runs on MFMA against transposed weight packs (EncWT, packed
 // alongside the forward packs).  Each kernel also writes, per layer, the (dY, X) row pairs of its tile;
-// the weight gradients dW = dY^T X are then plain tall-skinny library GEMMs over all rows (hipBLASLt,
-// issued by the host wrapper), and bias gradients the column sums of dY.
+// wgrad_partial_kernel + wgrad_reduce_kernel then form every weight gradient dW = dY^T X (and bias
+// gradient, a column of ones appended to X) over all rows in two launches (tm_encoder_wgrad).
 #include "encoder_common.h"
 
 namespace tmk {
 
-// ------------------------------------------------------------------ transposed weight packs
-// packed element (o, c) of job j = src[o * so + c * sc]  (same fragment order as pack_kernel)
+// ------------------------------------------------------------------ weight packing (one launch)
+// Every packed tensor of tm_weights -- the forward fragment packs, the transposed packs of the backward
+// and the zero-padded bias / vector copies -- is one job of a single launch (the training step repacks
+// after every optimizer step).  Fragment job: packed element (o, c) = src[o * so + c * sc] in
+// the fragment order the MFMA tiles read (see EncW / gemm); copy job (nt = 0): dst[i] = i < nout ? src[i] : 0 for i < k (k = padded length).
 struct PackJob {
     const float *src;
     float *dst;
     int32_t so, sc, nout, k, nt, nq;
     int64_t begin;
 };
-constexpr int MAX_PACK_JOBS = 12;
+constexpr int MAX_PACK_JOBS = 40;
 struct PackJobs {
     PackJob j[MAX_PACK_JOBS];
     int32_t n;
@@ -43,12 +46,29 @@ __global__ void pack_jobs_kernel(PackJobs J) {
         while (b + 1 < J.n && i >= J.j[b + 1].begin) ++b;
         const PackJob &p = J.j[b];
         const int64_t e = i - p.begin;
+        if (p.nt == 0) {
+            p.dst[e] = e < p.nout ? p.src[e] : 0.f;
+            continue;
+        }
         const int s = e & 3, l = (e >> 2) & 63;
         const int64_t tq = e >> 8;
         const int q = (int)(tq % p.nq), t = (int)(tq / p.nq);
         const int o = 16 * t + (l & 15), c = 16 * q + 4 * (l >> 4) + s;
         p.dst[e] = (o < p.nout && c < p.k) ? p.src[(int64_t)o * p.so + (int64_t)c * p.sc] : 0.f;
     }
+}
+
+// evc[f] = b[f] + sum_{k >= 16 qt} W[f][k] * cos(0 * w + phi): one wave per output feature, fp64
+// partial sums combined in a fixed butterfly order, one rounding to fp32 (walk_kernel's slot pass)
+__global__ void __launch_bounds__(64) evc_par_kernel(const float *__restrict__ W, const float *__restrict__ b,
+                                                     const float *__restrict__ phase, int de, int dn, int kev, int qt,
+                                                     float *__restrict__ out) {
+    const int f = blockIdx.x, lane = threadIdx.x;
+    double acc = 0.0;
+    if (f < dn)
+        for (int k = 16 * qt + lane; k < kev; k += 64) acc += (double)W[(int64_t)f * kev + k] * (double)cos_rd(phase[k - de - 3]);
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) out[f] = f < dn ? (float)(acc + (double)b[f]) : 0.f;
 }
 
 // ------------------------------------------------------------------ head backward
@@ -455,6 +475,99 @@ __global__ void __launch_bounds__(256) gcn_bwd_kernel(EncW P, EncWT T, int64_t n
     });
 }
 
+
+// ------------------------------------------------------------------ weight gradients: dW = dY^T X over rows
+// One launch computes every weight / bias gradient of the encoder from the (dY, X) row pairs the two
+// backward kernels wrote: job j covers a 64 x 64 block of dW_j (its bias gradient = a virtual column of
+// ones appended to X) over CHUNK rows; the workgroup stages 64-row slabs of dY and X in LDS and each
+// wave runs a 16 x 64 strip on MFMA (k = rows), then stores its partial block.  A second launch sums
+// the partials of every output element in a fixed order (deterministic; no atomics).
+constexpr int WG_CHUNK = 1024, WG_LDS_LD = 80, MAX_WG_JOBS = 14, MAX_WG_TGTS = 12;
+struct WgJob {
+    const float *y, *x;
+    int32_t ldy, ldx, O, I, bias, OB, IB, R;
+    int64_t wg_begin, part_begin;
+};
+struct WgTarget {
+    float *w, *b;
+    int32_t O, I, bias, j0, nj;
+    int64_t out_begin;
+};
+struct WgPlan {
+    WgJob job[MAX_WG_JOBS];
+    WgTarget tgt[MAX_WG_TGTS];
+    int32_t njob, ntgt;
+    int64_t total_wg, total_out;
+};
+
+__global__ void __launch_bounds__(256) wgrad_partial_kernel(WgPlan P, float *__restrict__ part) {
+    __shared__ __attribute__((aligned(16))) float Ys[64 * WG_LDS_LD], Xs[64 * WG_LDS_LD];
+    const int64_t bid = blockIdx.x;
+    int j = 0;
+    while (j + 1 < P.njob && bid >= P.job[j + 1].wg_begin) ++j;
+    const WgJob &J = P.job[j];
+    const int64_t local = bid - J.wg_begin;
+    const int nb = J.OB * J.IB;
+    const int chunk = (int)(local / nb), tb = (int)(local % nb), ob = tb / J.IB, ib = tb % J.IB;
+    const int o0 = ob * 64, i0 = ib * 64;
+    const int r_begin = chunk * WG_CHUNK, r_end = min(J.R, r_begin + WG_CHUNK);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, m = lane & 15;
+    floatx4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int r0 = r_begin; r0 < r_end; r0 += 64) {
+        for (int e = tid; e < 64 * 64; e += 256) {
+            const int row = e >> 6, col = e & 63, r = r0 + row;
+            const bool rv = r < r_end;
+            const int o = o0 + col, i = i0 + col;
+            Ys[row * WG_LDS_LD + col] = (rv && o < J.O) ? J.y[(int64_t)r * J.ldy + o] : 0.f;
+            float xv = 0.f;
+            if (rv) {
+                if (i < J.I) xv = J.x[(int64_t)r * J.ldx + i];
+                else if (J.bias && i == J.I) xv = 1.f;
+            }
+            Xs[row * WG_LDS_LD + col] = xv;
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int s = 0; s < 16; ++s) {
+            const float a = Ys[(4 * s + g) * WG_LDS_LD + 16 * wave + m];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float b = Xs[(4 * s + g) * WG_LDS_LD + 16 * t + m];
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+    float *out = part + J.part_begin + local * 4096;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[(16 * wave + 4 * g + r) * 64 + 16 * t + m] = acc[t][r];
+}
+
+__global__ void wgrad_reduce_kernel(WgPlan P, const float *__restrict__ part) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < P.total_out; e += (int64_t)gridDim.x * blockDim.x) {
+        int t = 0;
+        while (t + 1 < P.ntgt && e >= P.tgt[t + 1].out_begin) ++t;
+        const WgTarget &T = P.tgt[t];
+        const int ia = T.I + T.bias;
+        const int64_t le = e - T.out_begin;
+        const int o = (int)(le / ia), i = (int)(le % ia);
+        float s = 0.f;
+        for (int jj = 0; jj < T.nj; ++jj) {
+            const WgJob &J = P.job[T.j0 + jj];
+            const int nchunk = (J.R + WG_CHUNK - 1) / WG_CHUNK, nb = J.OB * J.IB;
+            const int tb = (o / 64) * J.IB + i / 64;
+            const float *p = part + J.part_begin + (int64_t)tb * 4096 + (o % 64) * 64 + (i % 64);
+            for (int c = 0; c < nchunk; ++c) s += p[(int64_t)c * nb * 4096];
+        }
+        if (i < T.I) T.w[(int64_t)o * T.I + i] = s;
+        else T.b[o] = s;
+    }
+}
+
 }  // namespace tmk
 
 using namespace tmk;
@@ -493,34 +606,56 @@ int train_packs_create(tm_weights *w) {
     return TM_OK;
 }
 
-void train_packs_fill(tm_weights *w, const float *const *t, hipStream_t s) {
+void pack_all_weights(tm_weights *w, const float *const *t, hipStream_t s) {
     const int de = w->de, dn = w->dn, h = w->h, h2 = 2 * h, hm = h + 12, kev = de + 3 + dn;
-    // job: packed (o, c) = src[o * so + c * sc]; transposed packs of W[nout][k]: so = 1, sc = k
-    struct J {
-        const Lin *lin;
-        const float *src;
-        int so, sc;
-    } js[] = {{&w->T.evT, t[0] + de + 3, 1, kev}, {&w->T.g1T, t[2], 1, dn}, {&w->T.g2T, t[4], 1, h},
-              {&w->T.w1T, t[6], 1, h2},           {&w->T.w2T, t[8], 1, h2}, {&w->T.a1T, t[10], 1, h2},
-              {&w->T.a2T, t[12], 1, h},           {&w->T.m1T, t[14], 1, hm}, {&w->T.m2T, t[16], 1, hm}};
     PackJobs P{};
     int64_t total = 0;
-    P.n = 0;
-    for (auto &j : js) {
+    auto frag = [&](const Lin &lin, const float *src, int so, int sc) {
         PackJob &p = P.j[P.n++];
-        p.src = j.src;
-        p.dst = const_cast<float *>(reinterpret_cast<const float *>(j.lin->w));
-        p.so = j.so;
-        p.sc = j.sc;
-        p.nout = j.lin->nout;
-        p.k = j.lin->k;
-        p.nt = j.lin->nt;
-        p.nq = j.lin->nq;
+        p.src = src;
+        p.dst = const_cast<float *>(reinterpret_cast<const float *>(lin.w));
+        p.so = so;
+        p.sc = sc;
+        p.nout = lin.nout;
+        p.k = lin.k;
+        p.nt = lin.nt;
+        p.nq = lin.nq;
         p.begin = total;
         total += (int64_t)p.nt * p.nq * 256;
+    };
+    auto copy = [&](const float *src, const float *dst, int n, int npad) {
+        PackJob &p = P.j[P.n++];
+        p.src = src;
+        p.dst = const_cast<float *>(dst);
+        p.nout = n;
+        p.k = npad;
+        p.nt = 0;
+        p.begin = total;
+        total += npad;
+    };
+    for (auto &sp : w->specs) {           // forward packs of W[nout][k] and their biases
+        frag(*sp.lin, t[sp.wi], sp.k, 1);
+        copy(t[sp.wi + 1], sp.lin->b, sp.nout, sp.lin->nt * 16);
     }
+    copy(t[18], w->P.m3w, h, 64);
+    copy(t[19], w->P.m3b, 1, 4);
+    copy(t[24], w->P.d3w, h / 2, 64);
+    copy(t[25], w->P.d3b, 1, 4);
+    copy(t[26], w->P.freq, dn, r16(dn));
+    copy(t[27], w->P.phase, dn, r16(dn));
+    // transposed packs of W[nout][k] (so = 1, sc = k); evT takes lin_event's time-feature columns only
+    frag(w->T.evT, t[0] + de + 3, 1, kev);
+    frag(w->T.g1T, t[2], 1, dn);
+    frag(w->T.g2T, t[4], 1, h);
+    frag(w->T.w1T, t[6], 1, h2);
+    frag(w->T.w2T, t[8], 1, h2);
+    frag(w->T.a1T, t[10], 1, h2);
+    frag(w->T.a2T, t[12], 1, h);
+    frag(w->T.m1T, t[14], 1, hm);
+    frag(w->T.m2T, t[16], 1, hm);
     P.total = total;
-    pack_jobs_kernel<<<dim3(128), 256, 0, s>>>(P);
+    pack_jobs_kernel<<<dim3((unsigned)std::min<int64_t>((total + 255) / 256, 1024)), 256, 0, s>>>(P);
+    evc_par_kernel<<<dim3(r16(dn)), 64, 0, s>>>(t[0], t[1], t[27], de, dn, kev, w->P.qt, const_cast<float *>(w->P.evc));
 }
 
 void train_packs_free(tm_weights *w) {
@@ -573,5 +708,84 @@ extern "C" int tm_encoder_bwd(const tm_weights *w, const float *n_feat, const fl
         P, w->T, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, io->dF, go);
     TM_CHECK_LAUNCH();
     prof_end("gcn_bwd_kernel", s, pe);
+    return TM_OK;
+}
+
+extern "C" int tm_encoder_wgrad(const tm_weights *w, int32_t n_groups, int32_t B, int32_t W,
+                                const tm_encoder_grad_io *io, const void *workspace, float *const *grads,
+                                void *stream) {
+    if (!w || !io || !workspace || !grads || n_groups < 0 || B < 0 || W < 0)
+        return fail(TM_E_ARG, "tm_encoder_wgrad: bad arguments");
+    for (int i = 0; i < TM_N_ENC_GRADS; ++i)
+        if (!grads[i]) return fail(TM_E_ARG, "tm_encoder_wgrad: NULL gradient " + std::to_string(i));
+    const int64_t n64 = (int64_t)n_groups * B * W;
+    if (n64 * 3 * 2 > INT32_MAX) return fail(TM_E_UNSUPPORTED, "tm_encoder_wgrad: too many walks per call");
+    const int n = (int)n64, R = 3 * n, h = w->h, h2 = 2 * h, hm = h + 12;
+    const int dn = w->dn, kev = w->P.kev, KE = r16(kev), DN = r16(dn), KM = r16(hm);
+    const float *F = reinterpret_cast<const float *>(workspace);
+    struct JD {
+        const float *y, *x;
+        int ldy, ldx, O, I, bias, R;
+    } jd[] = {
+        {io->dlev, io->ev, DN, KE, dn, kev, 1, R},            // lin_event
+        {io->dZ, io->AB, h, DN, h, dn, 1, 2 * R},             // event_conv.MLP.0
+        {io->dF, io->H, h, h, h, h, 1, 2 * R},                // event_conv.MLP.2
+        {io->dP, F + 2 * h2, h2, 3 * h2, h2, h2, 1, n},       // attention.W1 (x = F[:, 2])
+        {io->dQ, F, h2, 3 * h2, h2, h2, 1, n},                // attention.W2, position 0
+        {io->dQ + (int64_t)n * h2, F + h2, h2, 3 * h2, h2, h2, 1, n},   // position 1
+        {io->dH1, io->O, h, h2, h, h2, 1, n},                 // attention.MLP.0
+        {io->dY2, io->H1d, h, h, h, h, 1, n},                 // attention.MLP.3
+        {io->dM1, io->X, KM, KM, hm, hm, 1, n},               // MLP.0
+        {io->dM2, io->M1d, h, KM, h, hm, 1, n},               // MLP.3
+        {io->dlogit, io->M2, 1, h, 1, h, 1, n},               // MLP.5
+        {io->g, io->dt, DN, 1, dn, 1, 1, R},                  // time encoder: freq (x = dt), phase (ones)
+    };
+    // targets: (first job, job count, weight grad index, bias grad index)
+    const int tg[][4] = {{0, 1, 0, 1}, {1, 1, 2, 3}, {2, 1, 4, 5}, {3, 1, 6, 7}, {4, 2, 8, 9}, {6, 1, 10, 11},
+                         {7, 1, 12, 13}, {8, 1, 14, 15}, {9, 1, 16, 17}, {10, 1, 18, 19}, {11, 1, 20, 21}};
+    WgPlan P{};
+    P.njob = (int)(sizeof(jd) / sizeof(jd[0]));
+    int64_t wg = 0, pb = 0;
+    for (int j = 0; j < P.njob; ++j) {
+        WgJob &J = P.job[j];
+        const JD &d = jd[j];
+        J.y = d.y; J.x = d.x; J.ldy = d.ldy; J.ldx = d.ldx; J.O = d.O; J.I = d.I; J.R = d.R;
+        J.bias = 1;   // W2's two jobs both carry the ones column: its bias gradient sums dQ over both positions
+        J.OB = (d.O + 63) / 64;
+        J.IB = (d.I + 1 + 63) / 64;
+        J.wg_begin = wg;
+        J.part_begin = pb;
+        const int64_t nchunk = (d.R + WG_CHUNK - 1) / WG_CHUNK;
+        wg += nchunk * J.OB * J.IB;
+        pb += nchunk * J.OB * J.IB * 4096;
+    }
+    P.total_wg = wg;
+    P.ntgt = (int)(sizeof(tg) / sizeof(tg[0]));
+    int64_t ob = 0;
+    for (int t = 0; t < P.ntgt; ++t) {
+        WgTarget &T = P.tgt[t];
+        T.j0 = tg[t][0];
+        T.nj = tg[t][1];
+        T.w = grads[tg[t][2]];
+        T.b = grads[tg[t][3]];
+        T.O = jd[T.j0].O;
+        T.I = jd[T.j0].I;
+        T.bias = 1;
+        T.out_begin = ob;
+        ob += (int64_t)T.O * (T.I + 1);
+    }
+    P.total_out = ob;
+    if (wg == 0) return TM_OK;
+    hipStream_t s = S_(stream);
+    float *part = reinterpret_cast<float *>(scratch((size_t)pb * sizeof(float), s));
+    if (!part) return fail(TM_E_HIP, "tm_encoder_wgrad: scratch allocation failed");
+    hipEvent_t pe = prof_begin(s);
+    wgrad_partial_kernel<<<dim3((unsigned)wg), 256, 0, s>>>(P, part);
+    TM_CHECK_LAUNCH();
+    prof_end("wgrad_partial_kernel", s, pe);
+    pe = prof_begin(s);
+    wgrad_reduce_kernel<<<dim3((unsigned)std::min<int64_t>((ob + 255) / 256, 1024)), 256, 0, s>>>(P, part);
+    TM_CHECK_LAUNCH();
+    prof_end("wgrad_reduce_kernel", s, pe);
     return TM_OK;
 }

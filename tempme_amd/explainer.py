@@ -169,12 +169,13 @@ class TempME(nn.Module):
             ts += [mod.weight, mod.bias]
         return ts + [self.time_encoder.basis_freq, self.time_encoder.phase]
 
-    def packed_weights(self):
-        """tm_weights handle, re-packed whenever a parameter changed (version counters)."""
+    def packed_weights(self, force=False):
+        """tm_weights handle, re-packed whenever a parameter changed (version counters) or when forced
+        (a step captured as a HIP graph must record its repack launch: GraphedTrainStep)."""
         dev = self._dev()
         ws = self._weight_list()
         key = tuple((w.data_ptr(), w._version) for w in ws)
-        if self._packed is None or self._packed_key != key:
+        if self._packed is None or self._packed_key != key or force:
             if self._packed is None:
                 h = L.C.c_void_p()
                 L.check(L.lib().tm_weights_create(self.edge_dim, self.node_dim, self.hid_dim, dev.index,
@@ -288,24 +289,11 @@ class TempME(nn.Module):
                                        L.ptr(eid3), L.ptr(ts3), L.ptr(cat), L.ptr(cut), L.ptr(cnt), L.ptr(drop),
                                        drop_scale, L.ptr(ws), L.ptr(d_imp), L.C.byref(io), L.stream_ptr(dev)),
                 "TempME.forward backward")
-        F = ws[:n * 3 * 2 * h * 4].view(torch.float32).view(n, 3, 2 * h)
-        hm = h + 12
-        dlev, g = b["dlev"][:, :dn], b["g"][:, :dn]
-        dZ, dU = b["dZ"].view(2 * R, h), b["dF"].view(2 * R, h)
-        dQ, dP = b["dQ"], b["dP"]
-        dM1, dM2 = b["dM1"][:, :hm], b["dM2"]
-        gW2 = torch.addmm(dQ[0].t() @ F[:, 0], dQ[1].t(), F[:, 1])
-        return (dlev.t() @ b["ev"][:, :kev], dlev.sum(0),
-                dZ.t() @ b["AB"].view(2 * R, DN)[:, :dn], dZ.sum(0),
-                dU.t() @ b["H"].view(2 * R, h), dU.sum(0),
-                dP.t() @ F[:, 2], dP.sum(0),
-                gW2, dQ.sum((0, 1)),
-                b["dH1"].t() @ b["O"], b["dH1"].sum(0),
-                b["dY2"].t() @ b["H1d"], b["dY2"].sum(0),
-                dM1.t() @ b["X"][:, :hm], dM1.sum(0),
-                dM2.t() @ b["M1d"][:, :hm], dM2.sum(0),
-                b["dlogit"].view(1, n) @ b["M2"], b["dlogit"].sum().view(1),
-                b["dt"].view(1, R) @ g, g.sum(0))
+        grads = [torch.empty_like(p, memory_format=torch.contiguous_format) for p in self._encoder_params()]
+        gp = (L.C.c_void_p * len(grads))(*[t.data_ptr() for t in grads])
+        L.check(L.lib().tm_encoder_wgrad(self.packed_weights(), G, B, W, L.C.byref(io), L.ptr(ws), gp,
+                                         L.stream_ptr(dev)), "TempME.forward weight gradients")
+        return tuple(grads)
 
     # ------------------------------------------------------------------ reference API
     def forward(self, walks, cut_time_l, edge_identify):
@@ -360,8 +348,17 @@ class TempME(nn.Module):
         alpha = torch.clamp(prob * 10, min=1.0)
         beta = torch.clamp((1 - prob) * 10, min=1.0)
         if training:
-            return torch.distributions.Beta(alpha, beta).rsample()
+            # validate_args=False: the argument check is a host sync (the values are valid by construction)
+            return torch.distributions.Beta(alpha, beta, validate_args=False).rsample()
         return alpha / (alpha + beta)
+
+    def _null_vec(self, device):
+        """torch.tensor(list(null_model.values())) on the device, built once (no per-step host copy)."""
+        key = (tuple(self.null_model.items()), str(device))
+        if getattr(self, "_null_key", None) != key:
+            self._null_dev = torch.tensor(list(self.null_model.values())).to(device)
+            self._null_key = key
+        return self._null_dev
 
     def kl_loss(self, prob, walks, target=0.3):
         """explainer_new.py:432-453."""
@@ -369,7 +366,7 @@ class TempME(nn.Module):
         prob = torch.clamp(prob, 1e-6, 1 - 1e-6)
         if self.prior == "empirical":
             s = torch.mean(prob, dim=1)
-            null = torch.tensor(list(self.null_model.values())).to(prob.device)
+            null = self._null_vec(prob.device)
             num_cat = len(self.null_model.keys())
             cat = _to(cat_feat, prob.device, torch.long).reshape(prob.shape[0], -1, 1)
             emp = torch.zeros(prob.shape[0], num_cat, 1, device=prob.device, dtype=prob.dtype)
@@ -424,7 +421,9 @@ class TempME(nn.Module):
         i1 = _to(eidx_record[1], dev, torch.long)
         B = graphlet_imp.shape[0]
         ew = _to(walks[1], dev, torch.long).reshape(B, -1)
-        n_e = int(max(ew.max(), i0.max(), i1.max()) + 1)
+        # dense width: the reference sizes it by the batch's largest edge id (a host sync, :362); every id
+        # indexes the edge-feature table, so its row count bounds them and gives the same values
+        n_e = self.edge_raw_embed.weight.shape[0]
         wimp = graphlet_imp.repeat(1, 1, 3).view(B, -1)
         if self.use_dependency_aware_sampling:
             tw = _to(walks[2], dev, torch.float32).reshape(B, -1)

@@ -28,9 +28,12 @@ SIDES = ("src", "tgt", "bgd")
 class Batch:
     """One reference batch (get_item + get_item_edge, utils/batch_loader.py:203-242) as device tensors."""
 
-    def __init__(self, src, dst, ts, e_idx, fake, subgraphs, walks, edges):
+    def __init__(self, src, dst, ts, e_idx, fake, subgraphs, walks, edges, stacked=None):
         self.src, self.dst, self.ts, self.e_idx, self.fake = src, dst, ts, e_idx, fake
         self.subgraphs, self.walks, self.edges = subgraphs, walks, edges
+        # (node6 [3,B,W,6], eid3, ts3, cat [3,B,W], cnt [3,B,W,3,3]) device tensors: the three sides of the
+        # batch stacked, so the explainer encodes them in one call (per-side walks are views of these)
+        self.stacked = stacked
 
     def __len__(self):
         return int(self.src.shape[0])
@@ -39,17 +42,43 @@ class Batch:
 def batch_from_pack(buf, src, dst, ts, e_idx, rows):
     """Rows ``rows`` (device int64 index, or a slice) of a sampled pack (preprocess.EventBuffers,
     side-major [3, E, ...]) and of the event arrays."""
-    def take(x, s=None):
-        x = x if s is None else x[s]
-        return x[rows] if isinstance(rows, slice) else x.index_select(0, rows)
+    def take(x, dim=0):
+        return x[(slice(None),) * dim + (rows,)] if isinstance(rows, slice) else x.index_select(dim, rows)
+    node6, eid3, ts3, cat, cnt = (take(buf.node6, 1), take(buf.eid3, 1), take(buf.ts3, 1), take(buf.cat, 1),
+                                  take(buf.cnt, 1))
+    s1 = [take(buf.sub1_node, 1), take(buf.sub1_eid, 1), take(buf.sub1_ts, 1)]
+    s2 = [take(buf.sub2_node, 1), take(buf.sub2_eid, 1), take(buf.sub2_ts, 1)]
     subgraphs, walks, edges = [], [], []
     for s in range(3):
-        subgraphs.append(([take(buf.sub1_node, s), take(buf.sub2_node, s)],
-                          [take(buf.sub1_eid, s), take(buf.sub2_eid, s)],
-                          [take(buf.sub1_ts, s), take(buf.sub2_ts, s)]))
-        walks.append((take(buf.node6, s), take(buf.eid3, s), take(buf.ts3, s), take(buf.cat, s).unsqueeze(-1), None))
-        edges.append(take(buf.cnt, s))
-    return Batch(take(src), take(dst), take(ts), take(e_idx), take(buf.dst_fake), subgraphs, walks, edges)
+        subgraphs.append(([s1[0][s], s2[0][s]], [s1[1][s], s2[1][s]], [s1[2][s], s2[2][s]]))
+        walks.append((node6[s], eid3[s], ts3[s], cat[s].unsqueeze(-1), None))
+        edges.append(cnt[s])
+    return Batch(take(src), take(dst), take(ts), take(e_idx), take(buf.dst_fake), subgraphs, walks, edges,
+                 stacked=(node6, eid3, ts3, cat, cnt))
+
+
+def _as_dev(x, dev, dtype):
+    if isinstance(x, torch.Tensor):
+        return x.to(dev, dtype)
+    return torch.from_numpy(np.ascontiguousarray(x)).to(dev, dtype)
+
+
+def encode_sides(explainer, batch):
+    """TempME.forward for the src / tgt / bgd walks of one batch (temp_exp_main.py:605-607).  On the HIP
+    path the three sides go through ONE forward_groups call (one std group per side, exactly as three
+    separate calls); returns the three [B, W, 1] importance tensors."""
+    if not explainer._hip_ok():
+        return [explainer(w, batch.ts, e) for w, e in zip(batch.walks, batch.edges)]
+    dev = explainer._dev()
+    if batch.stacked is None:
+        st = lambda k, dt: torch.stack([_as_dev(w[k], dev, dt) for w in batch.walks])  # noqa: E731
+        cnt = torch.stack([_as_dev(e, dev, torch.float32) for e in batch.edges])
+        batch.stacked = (st(0, torch.int32), st(1, torch.int32), st(2, torch.float32), st(3, torch.int32), cnt)
+    node6, eid3, ts3, cat, cnt = batch.stacked
+    G, B, W = node6.shape[0], node6.shape[1], node6.shape[2]
+    cut = _as_dev(batch.ts, dev, torch.float64).reshape(1, B).expand(G, B)
+    imp = explainer.forward_groups(node6, eid3, ts3, cat.reshape(G, B, W), cut, cnt, G, B, W)
+    return list(imp.view(G, B, W, 1).unbind(0))
 
 
 class GradAllReduce:
@@ -87,16 +116,13 @@ def train_step(explainer, base_model, optimizer, batch, *, beta=0.5, prior_p=0.3
     criterion = criterion or torch.nn.BCEWithLogitsLoss()
     sg_s, sg_t, sg_b = batch.subgraphs
     w_s, w_t, w_b = batch.walks
-    e_s, e_t, e_b = batch.edges
     with torch.no_grad():
         pos_out_ori, neg_out_ori = base_model.contrast(batch.src, batch.dst, batch.fake, batch.ts, batch.e_idx,
                                                        sg_s, sg_t, sg_b)
         y_pred = torch.cat([pos_out_ori, neg_out_ori], dim=0).sigmoid()
         y_ori = torch.where(y_pred > 0.5, 1., 0.).view(y_pred.size(0), 1)
     optimizer.zero_grad()
-    g_s = explainer(w_s, batch.ts, e_s)
-    g_t = explainer(w_t, batch.ts, e_t)
-    g_b = explainer(w_b, batch.ts, e_b)
+    g_s, g_t, g_b = encode_sides(explainer, batch)
     explanation = explainer.retrieve_explanation(sg_s, g_s, w_s, sg_t, g_t, w_t, sg_b, g_b, w_b, training=if_bern)
     pos_logit, neg_logit = base_model.contrast(batch.src, batch.dst, batch.fake, batch.ts, batch.e_idx, sg_s, sg_t,
                                                sg_b, explain_weights=explanation)
@@ -112,6 +138,48 @@ def train_step(explainer, base_model, optimizer, batch, *, beta=0.5, prior_p=0.3
     return dict(loss=loss.detach(), pred_loss=pred_loss.detach(), kl_loss=kl_loss.detach(),
                 pos_logit=pos_logit.detach(), neg_logit=neg_logit.detach(), pos_out_ori=pos_out_ori,
                 neg_out_ori=neg_out_ori, y_ori=y_ori)
+
+
+class GraphedTrainStep:
+    """``train_step`` on one fixed batch shape captured once as a HIP graph and replayed per batch.
+
+    The step launches ~1,000 kernels (the base model's contrast forward/backward, the explainer's
+    encoder and explanation, losses, Adam); replaying a captured graph removes their host-side launch
+    cost.  Each call copies the batch's rows into a static index buffer and replays: the pack slice,
+    every kernel and the optimizer step run on the device with no host synchronisation.  Needs an
+    optimizer built with ``capturable=True`` and no host-side collectives (gloo) inside the step; the
+    first ``len(warmup_rows)`` batches are run eagerly on the capture stream first (they are real
+    training steps).  Returns the static output dict of ``train_step`` (overwritten by every call)."""
+
+    def __init__(self, explainer, base_model, optimizer, buf, src, dst, ts, e_idx, warmup_rows, **kw):
+        dev = src.device
+        self.args = (explainer, base_model, optimizer, buf, src, dst, ts, e_idx)
+        self.kw = kw
+        self.rows = torch.empty_like(warmup_rows[0])
+        self.stream = torch.cuda.Stream(device=dev)
+        self.stream.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(self.stream):
+            for r in warmup_rows:
+                self.rows.copy_(r)
+                self._body()
+        torch.cuda.current_stream(dev).wait_stream(self.stream)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=self.stream):
+            self.out = self._body()
+
+    def _body(self):
+        ex, base, opt, buf, src, dst, ts, e_idx = self.args
+        batch = batch_from_pack(buf, src, dst, ts, e_idx, self.rows)
+        ex.packed_weights(force=True)     # the replayed step repacks the weights Adam just updated
+        return train_step(ex, base, opt, batch, **self.kw)
+
+    def __call__(self, rows):
+        self.rows.copy_(rows)
+        self.graph.replay()
+        # the replay updated the parameters without bumping their version counters: drop the explainer's
+        # pack key so an eager call after this one repacks instead of using the pre-update pack
+        self.args[0]._packed_key = None
+        return self.out
 
 
 def step_metrics(out):
