@@ -158,7 +158,13 @@ def main():
     ap.add_argument("--alpha", type=float, default=1.2)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--config", type=int, default=1, choices=(1, 2, 4),
+                    help="BASELINE.json configs[i] workload: 1 = enron_sampled + TGN, N=20 (the headline); "
+                         "2 = full Enron shape (E=125,235), N=20; 4 = synthetic 1M-edge graph, de=dn=172, "
+                         "Pareto 1.5, N=30 (the HBM stress case)")
     args = ap.parse_args()
+    if args.config == 4 and args.n_degree == 20:
+        args.n_degree = 30
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -185,7 +191,19 @@ def main():
 
     N, M, B = args.n_degree, 3, args.batch_size
     E = args.batches * B
-    g = enron_like(alpha=args.alpha, seed=args.seed)
+    if args.config == 1:
+        g = enron_like(alpha=args.alpha, seed=args.seed)
+        workload = ("configs[1]: enron_sampled-shaped synthetic graph (V=183, E=18,780, "
+                    f"Pareto {args.alpha}) + TGN explainer scoring, n_degree={args.n_degree}")
+    elif args.config == 2:
+        g = enron_like(n_nodes=184, n_edges=125235, alpha=args.alpha, seed=args.seed)
+        workload = (f"configs[2]: full-Enron-shaped synthetic graph (V=184, E=125,235, Pareto {args.alpha}), "
+                    f"TempME encoder + explanation, n_degree={args.n_degree}")
+    else:
+        g = enron_like(n_nodes=100000, n_edges=1000000, alpha=1.5, de=172, dn=172, seed=args.seed,
+                       node_feat="uniform")
+        workload = ("configs[4]: synthetic 1M-edge temporal graph (V=100,000, Pareto 1.5, de=dn=172 U(0,1) "
+                    f"features), TempME explanation scoring, n_degree={args.n_degree}")
     (src, dst, ts, eidx), rows, pool = split(g)
     finder = tm.NeighborFinder.from_edges(g["src"][rows], g["dst"][rows], g["eidx"][rows], g["ts"][rows],
                                           g["n_nodes"], device=dev, seed=args.seed, split=tm.SPLIT_TEST)
@@ -273,9 +291,8 @@ def main():
         out = {"metric": METRIC, "value": round(total / el, 2), "unit": "edges/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
-               "data": "synthetic (seeded enron_sampled-shaped graph, random-init TempME weights)",
-               "config": {"workload": "configs[1]: enron_sampled-shaped synthetic graph (V=183, E=18,780, "
-                                      f"Pareto {args.alpha}) + TGN explainer scoring, n_degree={N}",
+               "data": "synthetic (seeded graph of the config's shape, random-init TempME weights)",
+               "config": {"workload": workload,
                           "n_degree": N, "walks_per_slot": M, "batch_size": B, "batches_per_step_per_gpu": args.batches,
                           "events_per_step_per_gpu": E, "parallelism": f"dp{world} (whole batches per rank)"},
                "roofline": roof, "kernels": kernels,

@@ -620,12 +620,45 @@ __device__ __forceinline__ floatx4 gen_x(int q, const float *cs, const float (&e
     return xq;
 }
 
+// gen_x for the streamed-edge-feature variant: e4 = this lane's 4 edge features of K step q
+template <int NQE, int NTD>
+__device__ __forceinline__ floatx4 gen_x_s(int q, const float *cs, const float4 &e4, int g, int de, int kev, float dt,
+                                           float c0, float c1, float c2) {
+    using C = WalkConsts<NQE, NTD>;
+    floatx4 xq;
+    const float4 w4 = lds4(cs + C::XW, q), p4 = lds4(cs + C::XP, q);
+    const float wv[4] = {w4.x, w4.y, w4.z, w4.w}, pv[4] = {p4.x, p4.y, p4.z, p4.w}, ev[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int k = 16 * q + 4 * g + s;
+        float v;
+        if (16 * q + 16 <= de) v = ev[s];
+        else {
+            v = (k < kev) ? time_cos(dt, wv[s], pv[s]) : 0.f;
+            if (k < de + 3) v = (k == de) ? c0 : (k == de + 1) ? c1 : c2;
+            if (k < de) v = ev[s];
+        }
+        xq[s] = v;
+    }
+    return xq;
+}
+
+// this lane's float4 of K step q of an edge-feature row (de % 4 == 0): clamped unconditional load,
+// zero outside the row
+__device__ __forceinline__ float4 ef_step(const float4 *erow4, int q, int g, int de) {
+    const int i = 4 * q + g, n4 = de >> 2;
+    const float4 v = erow4[i < n4 ? i : n4 - 1];
+    return i < n4 ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 // one walk position for the 16 columns of this wave -> F = [U_s | U_t] (8 tiles, B layout).
 // lin_event runs K-outer ((q, t) fragment order): the event features of K step q+1 are generated
 // while step q's MFMAs run and only L and two x fragments are live.  Node-feature rows are float4
 // gathers (dn % 4 == 0) in the epilogue, unconditional with a clamped index (issuing them during the
 // GEMM keeps 88 more registers live and costs the second wave per SIMD).
-template <int NQE, int NTD>
+// SEF (streamed edge features, EQ_MAX*16 < de <= 176): ef holds K steps 0 and 1 (loaded during the
+// previous pass); step q + 2's float4 is loaded while step q's MFMAs run.
+template <int NQE, int NTD, bool SEF>
 __device__ __forceinline__ void encode_position(const WalkArgs &a, const float *cs, const PosIn &pi,
                                                 const float (&ef)[EQ_MAX][4], int p, floatx4 (&F)[8],
                                                 unsigned long long (&T)[10]) {
@@ -650,13 +683,26 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, const float *
         float4 buf[D];
 #pragma unroll
         for (int i = 0; i < D; ++i) buf[i] = wload(wr, vo, ((i % NTD) * nq + i / NTD) * 64);
-        floatx4 xq = gen_x<NQE, NTD>(0, cs, ef, g, de, kev, dt, c0, c1, c2);
+        const float4 *erow4 = reinterpret_cast<const float4 *>(a.e_feat + (int64_t)pi.e * de);
+        float4 ring[2];
+        if constexpr (SEF) {
+            ring[0] = make_float4(ef[0][0], ef[0][1], ef[0][2], ef[0][3]);
+            ring[1] = make_float4(ef[1][0], ef[1][1], ef[1][2], ef[1][3]);
+        }
+        floatx4 xq = SEF ? gen_x_s<NQE, NTD>(0, cs, ring[0], g, de, kev, dt, c0, c1, c2)
+                         : gen_x<NQE, NTD>(0, cs, ef, g, de, kev, dt, c0, c1, c2);
         const int qend = p == 2 ? P.qt : NQE;            // slot pass: steps >= qt folded into evc
 #pragma unroll
         for (int q = 0; q < NQE; ++q) {
             if (q < qend) {                               // wave-uniform (a break would stop the unrolling)
                 floatx4 xn = xq;
-                if (q + 1 < NQE) xn = gen_x<NQE, NTD>(q + 1, cs, ef, g, de, kev, dt, c0, c1, c2);
+                float4 e2 = make_float4(0.f, 0.f, 0.f, 0.f);
+                if constexpr (SEF) {
+                    if (q + 2 < NQE && 16 * (q + 2) < de) e2 = ef_step(erow4, q + 2, g, de);
+                    if (q + 1 < NQE) xn = gen_x_s<NQE, NTD>(q + 1, cs, ring[(q + 1) & 1], g, de, kev, dt, c0, c1, c2);
+                } else {
+                    if (q + 1 < NQE) xn = gen_x<NQE, NTD>(q + 1, cs, ef, g, de, kev, dt, c0, c1, c2);
+                }
 #pragma unroll
                 for (int t = 0; t < NTD; ++t) {
                     const int i = q * NTD + t;
@@ -668,6 +714,7 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, const float *
                     L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, xq.w, L[t], 0, 0, 0);
                     __builtin_amdgcn_sched_barrier(0);
                 }
+                if constexpr (SEF) ring[q & 1] = e2;
                 xq = xn;
             }
         }
@@ -796,7 +843,7 @@ __device__ __forceinline__ void walk_head(const WalkArgs &a, const float *cs, in
     if (valid && g == 0) a.out[gw] = 1.f / (1.f + expf(-z));
 }
 
-template <int NQE, int NTD>
+template <int NQE, int NTD, bool SEF = false>
 __global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
     using C = WalkConsts<NQE, NTD>;
     const EncW &P = a.P;
@@ -843,7 +890,7 @@ __global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
         floatx4 F[8];
         unsigned long long T[10];
         TM_STAMP(0);
-        encode_position<NQE, NTD>(a, cs, cur, ef, p, F, T);
+        encode_position<NQE, NTD, SEF>(a, cs, cur, ef, p, F, T);
         load_ef(a, nxt.e, ef);
         cur = nxt;
         floatx4 Y[8];
@@ -1132,9 +1179,9 @@ static size_t gcn_lds(const EncW &P) {
 }
 static size_t head_lds() { return sizeof(float) * (4 * TILE_ROWS * (2 * HID + 8)); }
 
-template <int NQE>
+template <int NQE, bool SEF = false>
 static void launch_walk(const WalkArgs &a, unsigned blocks, hipStream_t s) {
-    walk_kernel<NQE, 11><<<dim3(blocks), 256, 0, s>>>(a);
+    walk_kernel<NQE, 11, SEF><<<dim3(blocks), 256, 0, s>>>(a);
 }
 
 extern "C" int tm_encoder_fwd(const tm_weights *w, const float *n_feat, const float *e_feat, int32_t n_groups,
@@ -1158,14 +1205,20 @@ extern "C" int tm_encoder_fwd(const tm_weights *w, const float *n_feat, const fl
     TM_CHECK_LAUNCH();
     prof_end("std_kernel", s, pe);
     const int nqe = r16(P.kev) / 16, ntd = r16(P.dn) / 16;
-    if (ntd == 11 && nqe >= 11 && nqe <= 14 && P.de <= 16 * EQ_MAX && P.dn % 4 == 0) {
+    const bool narrow = nqe >= 11 && nqe <= 14 && P.de <= 16 * EQ_MAX;
+    // wide edge features (e.g. BASELINE configs[4]: de = dn = 172): streamed per K step
+    const bool wide = (nqe == 21 || nqe == 22) && P.de > 16 * EQ_MAX && P.de % 4 == 0;
+    if (ntd == 11 && P.dn % 4 == 0 && (narrow || wide)) {
         // fused register-resident path
         const int64_t n_slots = n_walks / M;
         const int64_t units = (n_slots + 15) / 16;
         WalkArgs a{P, n_slots, W, M, B * W, n_feat, e_feat, node6, eid3, cat, ts3, cnt, stdv, cut, out_imp};
         const unsigned blocks = (unsigned)((units + 3) / 4);
         pe = prof_begin(s);
-        if (nqe == 11) launch_walk<11>(a, blocks, s);
+        if (wide) {
+            if (nqe == 21) launch_walk<21, true>(a, blocks, s);
+            else launch_walk<22, true>(a, blocks, s);
+        } else if (nqe == 11) launch_walk<11>(a, blocks, s);
         else if (nqe == 12) launch_walk<12>(a, blocks, s);
         else if (nqe == 13) launch_walk<13>(a, blocks, s);
         else launch_walk<14>(a, blocks, s);

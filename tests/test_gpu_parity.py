@@ -393,3 +393,34 @@ def test_pipeline_other_configs_vs_oracle(tm, N, alpha):
     assert np.array_equal(h(b.cnt).swapaxes(0, 1).astype(np.int32), o["cnt"])
     x = h(imp)
     assert np.isfinite(x).all() and (x >= 0).all() and (x <= 1).all()
+
+
+def test_pipeline_wide_edge_features_vs_oracle(tm):
+    """BASELINE configs[4] shapes (de = dn = 172, N = 30): the walk kernel's streamed-edge-feature
+    instance (lin_event over 22 K steps) vs the torch-fp32 oracle on sampled walks."""
+    from tempme_amd.pipeline import ExplainPipeline
+    from tempme_amd.workload import enron_like, split
+    g = enron_like(n_nodes=300, n_edges=6000, alpha=1.5, de=172, dn=172, node_feat="uniform", seed=11)
+    (src, dst, ts, eidx), rows, pool = split(g)
+    dev = torch.device("cuda", 0)
+    f = _finder(tm, g["src"][rows], g["dst"][rows], g["eidx"][rows], g["ts"][rows], g["n_nodes"], seed=3)
+    torch.manual_seed(1)
+    ex = tm.TempME(_Base(g["n_feat"], g["e_feat"], dev), "tgn", "synth", 40, 64, device=dev,
+                   null_model={k: 1 / 12 for k in range(1, 13)}).to(dev).eval()
+    N, B, E = 30, 20, 40
+    pipe = ExplainPipeline(ex, f.graph, torch.from_numpy(pool), N, 3, B, seed=3, split=px.SPLIT_TEST)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a[:E], dtype=dt)).to(dev)  # noqa: E731
+    imp, h1, h2 = pipe.run(t(src, np.int32), t(dst, np.int32), t(ts, np.float64), t(eidx, np.int32),
+                           torch.arange(E, dtype=torch.int32, device=dev))
+    torch.cuda.synchronize()
+    pipe.check_errors()
+    b = pipe.buf
+    h = lambda x: x.cpu().numpy()  # noqa: E731
+    sd = {k: v.detach().cpu() for k, v in ex.state_dict().items()}
+    nf, ef = torch.from_numpy(g["n_feat"]), torch.from_numpy(g["e_feat"])
+    for bi in range(E // B):
+        sl = slice(bi * B, (bi + 1) * B)
+        for s in range(3):
+            ref = er.forward(sd, nf, ef, h(b.node6[s, sl]), h(b.eid3[s, sl]), h(b.ts3[s, sl]), h(b.cat[s, sl]),
+                             ts[sl], h(b.cnt[s, sl]).astype(np.float64))
+            np.testing.assert_allclose(h(imp[s, sl]), ref.numpy()[..., 0], rtol=RTOL, atol=ATOL)
