@@ -202,6 +202,54 @@ int tm_encoder_bwd(const tm_weights *w, const float *n_feat, const float *e_feat
 int tm_encoder_wgrad(const tm_weights *w, int32_t n_groups, int32_t B, int32_t W, const tm_encoder_grad_io *io,
                      const void *workspace, float *const *grads, void *stream);
 
+/* Generic weight-gradient reduction (the launches tm_encoder_wgrad uses): job j contributes
+ * dY_j^T X_j over its R rows (dY [R][ldy] with O used columns, X [R][ldx] with I used columns);
+ * target t writes w [O][I] = the sum over jobs first_job .. first_job+n_jobs-1 (same O, I) and
+ * b [O] = the column sums of their dY.  Deterministic (fixed-order chunk reduction). */
+typedef struct {
+    const float *dy, *x;
+    int32_t ldy, ldx, O, I, R;
+} tm_wgrad_job;
+typedef struct {
+    float *w, *b;
+    int32_t first_job, n_jobs;
+} tm_wgrad_target;
+int tm_wgrad(const tm_wgrad_job *jobs, int32_t n_jobs, const tm_wgrad_target *targets, int32_t n_targets,
+             void *stream);
+
+/* retrieve_edge_imp_node in training (explainer_new.py:354-406 with dropout in the dependency gate,
+ * :367-386) up to the gathered scatter-max values: p1 [G,B,N] and p2 [G,B,N^2] are the per-edge maxima
+ * of imp * (0.5 + 0.5 sigmoid(gate)) gathered at the subgraph edge ids BEFORE beta_sample and the
+ * padding mask (the caller applies those, :395-404).  keep1 [R][64] / keep2 [R][32] (R = G*B*3W walk
+ * positions; nullable = eval) are the keep-masks of the gate's Dropout(1.5p) and Dropout(p), kept
+ * values scaled by scale1 / scale2.  io receives the activations the backward needs. */
+typedef struct {
+    float *X;      /* [R][KD] gate input [E[e] | cos(t w + phi)], KD = de + dn rounded up to 16 */
+    float *G1;     /* [R][64] dropout(relu(edge_dependency_gcn.0 X)) */
+    float *G2;     /* [R][32] dropout(relu(edge_dependency_gcn.3 G1)) */
+    float *z;      /* [R]     gate logit (edge_dependency_gcn.6 G2) */
+    float *gate;   /* [R]     0.5 + 0.5 sigmoid(z) */
+    float *d_gate; /* [R]     backward: dL/d gate */
+    float *dz;     /* [R]     backward: .6:  dW = dz^T G2 */
+    float *dG2;    /* [R][32] backward: .3:  dW = dG2^T G1 */
+    float *dG1;    /* [R][64] backward: .0:  dW = dG1^T X[:, :de+dn] */
+    float *g;      /* [R][DN] backward: time encoder: d phase = sum g, d basis_freq = t^T g */
+    float *t;      /* [R]     walk event times (f32) */
+} tm_explain_grad_io;
+int tm_explain_train_fwd(const tm_weights *w, const float *e_feat, int32_t n_groups, int32_t B, int32_t W, int32_t N,
+                         const int32_t *eid3, const float *ts3, const float *imp, const int32_t *sub1_eid,
+                         const int32_t *sub2_eid, const uint8_t *keep1, const uint8_t *keep2, float scale1,
+                         float scale2, const tm_explain_grad_io *io, float *p1, float *p2, void *stream);
+/* Backward given dp1 / dp2: d_imp [G,B,W] (the scatter-max gradient is split evenly among tied walk
+ * positions, as torch's scatter_reduce amax backward does) and the gate's weight gradients
+ * grads = 8 DEVICE pointers: edge_dependency_gcn.0 w/b, .3 w/b, .6 w/b, time_encoder.basis_freq, .phase
+ * (written, not accumulated). */
+int tm_explain_train_bwd(const tm_weights *w, int32_t n_groups, int32_t B, int32_t W, int32_t N, const int32_t *eid3,
+                         const float *ts3, const float *imp, const int32_t *sub1_eid, const int32_t *sub2_eid,
+                         const uint8_t *keep1, const uint8_t *keep2, float scale1, float scale2, const float *dp1,
+                         const float *dp2, const tm_explain_grad_io *io, float *d_imp, float *const *grads,
+                         void *stream);
+
 /* retrieve_edge_imp_node, eval (explainer_new.py:354-406, :420-430) for each of the G*B
  * (group, event) rows: dependency gate, walk->edge scatter-max, gather at the subgraph eids,
  * Beta mean, node==0 mask.  sub1_* [G,B,N], sub2_* [G,B,N*N]; out_h1 [G,B,N], out_h2 [G,B,N*N]

@@ -119,3 +119,28 @@ def kl_loss(imp, cat, null_vec, target=0.3):
     null = target * torch.as_tensor(np.asarray(null_vec), dtype=torch.float32).reshape(-1, 12)
     return ((1 - s) * torch.log((1 - s) / (1 - target + 1e-6) + 1e-6)
             + emp * torch.log(emp / (null + 1e-6) + 1e-6)).mean()
+
+
+def edge_importance_train(sd, e_feat, imp, walk_eid, walk_ts, sub_eid, keep1=None, keep2=None, sc1=1.0, sc2=1.0):
+    """retrieve_edge_imp_node up to the gathered scatter-max (explainer_new.py:354-393), with explicit keep-masks
+    for edge_dependency_gcn's two dropouts ([B, 3W, h] / [B, 3W, h/2]); autograd-able in the weights' dtype.
+    Returns (p1 [B, N], p2 [B, N^2]) before beta_sample and the padding mask."""
+    dty = sd["edge_dependency_gcn.0.weight"].dtype
+    B = imp.shape[0]
+    ew = torch.as_tensor(np.asarray(walk_eid), dtype=torch.long).reshape(B, -1)
+    tw = torch.as_tensor(np.asarray(walk_ts, dtype=np.float64)).float().reshape(B, -1)
+    wimp = imp.repeat(1, 1, 3).view(B, -1)
+    g = torch.cat([e_feat.to(dty)[ew], time_encode(sd, tw)], dim=-1)
+    g = torch.relu(_lin(sd, "edge_dependency_gcn.0", g))
+    if keep1 is not None:
+        g = g * (torch.as_tensor(np.asarray(keep1)).to(dty) * sc1)
+    g = torch.relu(_lin(sd, "edge_dependency_gcn.3", g))
+    if keep2 is not None:
+        g = g * (torch.as_tensor(np.asarray(keep2)).to(dty) * sc2)
+    g = _lin(sd, "edge_dependency_gcn.6", g).squeeze(-1)
+    wimp = wimp * (0.5 + 0.5 * torch.sigmoid(g))
+    i0 = torch.as_tensor(np.asarray(sub_eid[0]), dtype=torch.long)
+    i1 = torch.as_tensor(np.asarray(sub_eid[1]), dtype=torch.long)
+    n_e = int(max(ew.max(), i0.max(), i1.max()) + 1)
+    dense = torch.zeros(B, n_e, dtype=wimp.dtype).scatter_reduce(-1, ew, wimp, "amax", include_self=False)
+    return torch.gather(dense, -1, i0), torch.gather(dense, -1, i1)

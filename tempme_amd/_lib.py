@@ -34,9 +34,10 @@ EXPORTS = (
     "tm_last_error", "tm_version", "tm_graph_build", "tm_graph_free", "tm_graph_info", "tm_graph_export",
     "tm_sample_khop", "tm_sample_walks", "tm_neg_sample", "tm_perm_keys", "tm_motif_hist", "tm_edge_counts",
     "tm_sample_events", "tm_weights_create", "tm_weights_pack", "tm_weights_free", "tm_encoder_workspace_bytes",
-    "tm_encoder_fwd", "tm_encoder_train_fwd", "tm_encoder_bwd",
-    "tm_encoder_wgrad", "tm_edge_importance", "tm_edge_gate_table", "tm_edge_importance_tab", "tm_tgn_attn_fwd",
-    "tm_tgn_attn_bwd", "tm_mask_least_important", "tm_profile_enable", "tm_profile_sync", "tm_profile_entry",
+    "tm_encoder_fwd", "tm_encoder_train_fwd", "tm_encoder_bwd", "tm_encoder_wgrad", "tm_wgrad",
+    "tm_explain_train_fwd", "tm_explain_train_bwd", "tm_edge_importance", "tm_edge_gate_table",
+    "tm_edge_importance_tab", "tm_tgn_attn_fwd", "tm_tgn_attn_bwd", "tm_mask_least_important", "tm_profile_enable",
+    "tm_profile_sync", "tm_profile_entry",
 )
 
 
@@ -63,6 +64,23 @@ GRAD_IO_FIELDS = ("imp", "dlogit", "M2", "dM2", "M1d", "dM1", "X", "dY2", "H1d",
 class EncoderGradIO(C.Structure):
     """tm_encoder_grad_io (include/tempme.h)."""
     _fields_ = [(n, C.c_void_p) for n in GRAD_IO_FIELDS]
+
+
+EXPL_IO_FIELDS = ("X", "G1", "G2", "z", "gate", "d_gate", "dz", "dG2", "dG1", "g", "t")
+
+
+class ExplainGradIO(C.Structure):
+    """tm_explain_grad_io (include/tempme.h)."""
+    _fields_ = [(n, C.c_void_p) for n in EXPL_IO_FIELDS]
+
+
+class WgradJob(C.Structure):
+    _fields_ = [("dy", C.c_void_p), ("x", C.c_void_p), ("ldy", C.c_int32), ("ldx", C.c_int32), ("O", C.c_int32),
+                ("I", C.c_int32), ("R", C.c_int32)]
+
+
+class WgradTarget(C.Structure):
+    _fields_ = [("w", C.c_void_p), ("b", C.c_void_p), ("first_job", C.c_int32), ("n_jobs", C.c_int32)]
 
 
 class TempMEError(RuntimeError):
@@ -98,6 +116,11 @@ def _sig(L):
     L.tm_encoder_bwd.argtypes = [vp, vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, C.c_float, vp, vp,
                                  C.POINTER(EncoderGradIO), vp]
     L.tm_encoder_wgrad.argtypes = [vp, i32, i32, i32, C.POINTER(EncoderGradIO), vp, C.POINTER(vp), vp]
+    L.tm_wgrad.argtypes = [C.POINTER(WgradJob), i32, C.POINTER(WgradTarget), i32, vp]
+    L.tm_explain_train_fwd.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, C.c_float, C.c_float,
+                                       C.POINTER(ExplainGradIO), vp, vp, vp]
+    L.tm_explain_train_bwd.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, C.c_float, C.c_float, vp, vp,
+                                       C.POINTER(ExplainGradIO), vp, C.POINTER(vp), vp]
     L.tm_edge_importance.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.tm_edge_gate_table.argtypes = [vp, vp, vp, vp, vp]
     L.tm_edge_importance_tab.argtypes = [vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]

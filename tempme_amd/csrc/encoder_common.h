@@ -96,6 +96,7 @@ __device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
 // fragment format as the forward packs; no biases.  evT holds only lin_event's time-feature columns.
 struct EncWT {
     Lin evT, g1T, g2T, w1T, w2T, a1T, a2T, m1T, m2T;
+    Lin d1T, d2T;   // dependency gate: d1T holds only the time-feature columns of edge_dependency_gcn.0
 };
 
 // Dropout keep-masks of the training forward, uint8 [n_walks][DROP_COLS]: attention weights alpha

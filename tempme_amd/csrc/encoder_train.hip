@@ -568,6 +568,254 @@ __global__ void wgrad_reduce_kernel(WgPlan P, const float *__restrict__ part) {
     }
 }
 
+
+// ------------------------------------------------------------------ explanation (training)
+// retrieve_edge_imp_node with the dependency gate in training mode (explainer_new.py:354-406):
+//   gate_train_fwd_kernel   per 32 walk positions: X = [E[e] | cos(t w + phi)], gate MLP with its two
+//                           dropouts, z, gate = 0.5 + 0.5 sigmoid(z); keeps X, G1, G2 for the backward
+//   explain_train_kernel    per (group, event): LDS hash scatter-max of imp_w * gate over the walk edge
+//                           ids, gathered at the subgraph edge ids -> p (before beta_sample / mask)
+//   explain_train_bwd_kernel per (group, event): d p -> d dense (scatter-add) -> split evenly among the
+//                           tied maxima -> d imp (sum over a walk's 3 positions), d gate
+//   gate_train_bwd_kernel   per 32 positions: d gate -> d z -> .6 -> relu/dropout -> .3 -> relu/dropout
+//                           -> d time features -> * -sin(t w + phi)
+struct ExplIO {
+    float *X, *G1, *G2, *z, *gate, *d_gate, *dz, *dG2, *dG1, *g, *t;
+};
+
+__global__ void __launch_bounds__(256) gate_train_fwd_kernel(EncW P, int64_t n_rows, const float *__restrict__ e_feat,
+                                                             const int32_t *__restrict__ eid3,
+                                                             const float *__restrict__ ts3,
+                                                             const uint8_t *__restrict__ keep1,
+                                                             const uint8_t *__restrict__ keep2, float sc1, float sc2,
+                                                             ExplIO o) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int H2 = HID / 2;
+    const int de = P.de, kdep = P.kdep, kd16 = r16(kdep), ldx = kd16 + 8, ldg = HID + 8, ldg2 = H2 + 8;
+    float *X = smem, *G1 = X + TILE_ROWS * ldx, *G2 = G1 + TILE_ROWS * ldg;
+    __shared__ int32_t s_e[TILE_ROWS];
+    __shared__ float s_t[TILE_ROWS];
+    const int64_t r0 = (int64_t)blockIdx.x * TILE_ROWS;
+    const int tid = threadIdx.x;
+    auto valid = [&](int r) { return r0 + r < n_rows; };
+    if (tid < TILE_ROWS) {
+        s_e[tid] = valid(tid) ? eid3[r0 + tid] : 0;
+        s_t[tid] = valid(tid) ? ts3[r0 + tid] : 0.f;    // raw event time (:371)
+        if (valid(tid)) o.t[r0 + tid] = s_t[tid];
+    }
+    __syncthreads();
+    for (int i = tid; i < TILE_ROWS * kd16; i += blockDim.x) {
+        const int r = i / kd16, c = i % kd16;
+        float v = 0.f;
+        if (valid(r)) {
+            if (c < de) v = e_feat[(int64_t)s_e[r] * de + c];
+            else if (c < kdep) v = time_cos(s_t[r], P.freq[c - de], P.phase[c - de]);
+            o.X[(r0 + r) * kd16 + c] = v;
+        }
+        X[r * ldx + c] = v;
+    }
+    __syncthreads();
+    gemm<2>(X, ldx, P.d1, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) {
+            const int row = erow(mt, r);
+            float v = relu(acc[r] + P.d1.b[c]);
+            if (keep1) v = (valid(row) && keep1[(r0 + row) * HID + c]) ? v * sc1 : 0.f;
+            G1[row * ldg + c] = v;
+            if (valid(row)) o.G1[(r0 + row) * HID + c] = v;
+        }
+    });
+    __syncthreads();
+    gemm<2>(G1, ldg, P.d2, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) {
+            const int row = erow(mt, r);
+            float v = relu(acc[r] + P.d2.b[c]);
+            if (keep2) v = (valid(row) && keep2[(r0 + row) * H2 + c]) ? v * sc2 : 0.f;
+            G2[row * ldg2 + c] = v;
+            if (valid(row)) o.G2[(r0 + row) * H2 + c] = v;
+        }
+    });
+    __syncthreads();
+    const int r = tid >> 3, sub = tid & 7;
+    float sv = 0.f;
+    for (int c = sub; c < H2; c += 8) sv += G2[r * ldg2 + c] * P.d3w[c];
+    sv += __shfl_xor(sv, 1, 8);
+    sv += __shfl_xor(sv, 2, 8);
+    sv += __shfl_xor(sv, 4, 8);
+    if (sub == 0 && valid(r)) {
+        const float z = sv + P.d3b[0];
+        o.z[r0 + r] = z;
+        o.gate[r0 + r] = 0.5f + 0.5f * (1.f / (1.f + expf(-z)));
+    }
+}
+
+// open-addressing LDS hash of one event's walk edge ids -> max of imp_w * gate (float bits; values > 0)
+__device__ __forceinline__ void expl_hash_build(int nrow, const int32_t *e3, const float *imp_ev, const float *gate_ev,
+                                                int hbits, int32_t *hkey, uint32_t *hval) {
+    const int hsize = 1 << hbits;
+    for (int i = threadIdx.x; i < hsize; i += blockDim.x) {
+        hkey[i] = -1;
+        hval[i] = 0u;
+    }
+    __syncthreads();
+    for (int r = threadIdx.x; r < nrow; r += blockDim.x) {
+        const int32_t key = e3[r];
+        const float v = imp_ev[r / 3] * gate_ev[r];
+        uint32_t hh = ((uint32_t)key * 0x9E3779B1u) >> (32 - hbits);
+        while (true) {
+            const int32_t prev = atomicCAS(&hkey[hh], -1, key);
+            if (prev == -1 || prev == key) break;
+            hh = (hh + 1) & (hsize - 1);
+        }
+        atomicMax(&hval[hh], __float_as_uint(v));
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ int expl_hash_find(int32_t key, int hbits, const int32_t *hkey) {
+    const int hsize = 1 << hbits;
+    uint32_t hh = ((uint32_t)key * 0x9E3779B1u) >> (32 - hbits);
+    while (true) {
+        const int32_t k = hkey[hh];
+        if (k == key) return (int)hh;
+        if (k == -1) return -1;
+        hh = (hh + 1) & (hsize - 1);
+    }
+}
+
+__global__ void __launch_bounds__(256) explain_train_kernel(int32_t W, int32_t N, int32_t hbits,
+                                                            const int32_t *__restrict__ eid3,
+                                                            const float *__restrict__ imp,
+                                                            const float *__restrict__ gate,
+                                                            const int32_t *__restrict__ sub1_eid,
+                                                            const int32_t *__restrict__ sub2_eid,
+                                                            float *__restrict__ p1, float *__restrict__ p2) {
+    extern __shared__ __attribute__((aligned(16))) int32_t hkey[];
+    uint32_t *hval = reinterpret_cast<uint32_t *>(hkey + (1 << hbits));
+    const int64_t ge = blockIdx.x;
+    const int nrow = 3 * W;
+    expl_hash_build(nrow, eid3 + ge * nrow, imp + ge * W, gate + ge * nrow, hbits, hkey, hval);
+    const int n1 = N, n2 = N * N;
+    for (int i = threadIdx.x; i < n1 + n2; i += blockDim.x) {
+        const bool h1 = i < n1;
+        const int64_t o = h1 ? ge * n1 + i : ge * n2 + (i - n1);
+        const int hh = expl_hash_find(h1 ? sub1_eid[o] : sub2_eid[o], hbits, hkey);
+        const float p = hh >= 0 ? __uint_as_float(hval[hh]) : 0.f;   // ids no walk passes through: 0
+        if (h1) p1[o] = p;
+        else p2[o] = p;
+    }
+}
+
+__global__ void __launch_bounds__(256) explain_train_bwd_kernel(int32_t W, int32_t N, int32_t hbits,
+                                                                const int32_t *__restrict__ eid3,
+                                                                const float *__restrict__ imp,
+                                                                const float *__restrict__ gate,
+                                                                const int32_t *__restrict__ sub1_eid,
+                                                                const int32_t *__restrict__ sub2_eid,
+                                                                const float *__restrict__ dp1,
+                                                                const float *__restrict__ dp2,
+                                                                float *__restrict__ d_imp, float *__restrict__ d_gate) {
+    extern __shared__ __attribute__((aligned(16))) int32_t hkey[];
+    const int hsize = 1 << hbits;
+    uint32_t *hval = reinterpret_cast<uint32_t *>(hkey + hsize);
+    int32_t *hcnt = reinterpret_cast<int32_t *>(hval + hsize);
+    float *hd = reinterpret_cast<float *>(hcnt + hsize);
+    const int64_t ge = blockIdx.x;
+    const int nrow = 3 * W;
+    const int32_t *e3 = eid3 + ge * nrow;
+    const float *imp_ev = imp + ge * W, *gate_ev = gate + ge * nrow;
+    for (int i = threadIdx.x; i < hsize; i += blockDim.x) {
+        hcnt[i] = 0;
+        hd[i] = 0.f;
+    }
+    expl_hash_build(nrow, e3, imp_ev, gate_ev, hbits, hkey, hval);
+    // number of positions attaining each maximum; d dense[e] = sum of d p over the slots gathering e
+    for (int r = threadIdx.x; r < nrow; r += blockDim.x) {
+        const int hh = expl_hash_find(e3[r], hbits, hkey);
+        if (__float_as_uint(imp_ev[r / 3] * gate_ev[r]) == hval[hh]) atomicAdd(&hcnt[hh], 1);
+    }
+    const int n1 = N, n2 = N * N;
+    for (int i = threadIdx.x; i < n1 + n2; i += blockDim.x) {
+        const bool h1 = i < n1;
+        const int64_t o = h1 ? ge * n1 + i : ge * n2 + (i - n1);
+        const int hh = expl_hash_find(h1 ? sub1_eid[o] : sub2_eid[o], hbits, hkey);
+        if (hh >= 0) atomicAdd(&hd[hh], h1 ? dp1[o] : dp2[o]);
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w < W; w += blockDim.x) {
+        const float iw = imp_ev[w];
+        float di = 0.f;
+        for (int k = 0; k < 3; ++k) {
+            const int r = 3 * w + k;
+            const int hh = expl_hash_find(e3[r], hbits, hkey);
+            const float gt = gate_ev[r];
+            float dv = 0.f;
+            if (__float_as_uint(iw * gt) == hval[hh]) dv = hd[hh] / (float)hcnt[hh];
+            di += dv * gt;
+            d_gate[ge * nrow + r] = dv * iw;
+        }
+        d_imp[ge * W + w] = di;
+    }
+}
+
+__global__ void __launch_bounds__(256) gate_train_bwd_kernel(EncW P, EncWT T, int64_t n_rows, const uint8_t *keep1,
+                                                             const uint8_t *keep2, float sc1, float sc2, ExplIO o) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int H2 = HID / 2;
+    const int dn = P.dn, dn16 = r16(dn), ldg = HID + 8, ldg2 = H2 + 8;
+    float *G1 = smem, *G2 = G1 + TILE_ROWS * ldg;
+    __shared__ float s_dz[TILE_ROWS], s_t[TILE_ROWS];
+    const int64_t r0 = (int64_t)blockIdx.x * TILE_ROWS;
+    const int tid = threadIdx.x;
+    auto valid = [&](int r) { return r0 + r < n_rows; };
+    const float k1 = keep1 ? sc1 : 1.f, k2 = keep2 ? sc2 : 1.f;
+    if (tid < TILE_ROWS) {
+        float dz = 0.f, t = 0.f;
+        if (valid(tid)) {
+            const float sg = 1.f / (1.f + expf(-o.z[r0 + tid]));
+            dz = o.d_gate[r0 + tid] * 0.5f * (1.f - sg) * sg;   // gate = 0.5 + 0.5 sigmoid(z)
+            t = o.t[r0 + tid];
+            o.dz[r0 + tid] = dz;
+        }
+        s_dz[tid] = dz;
+        s_t[tid] = t;
+    }
+    for (int i = tid; i < TILE_ROWS * HID; i += blockDim.x) {
+        const int r = i / HID, c = i % HID;
+        G1[r * ldg + c] = valid(r) ? o.G1[(r0 + r) * HID + c] : 0.f;
+    }
+    __syncthreads();
+    for (int i = tid; i < TILE_ROWS * H2; i += blockDim.x) {   // dG2 = dz d3 * [G2 > 0] * keep
+        const int r = i / H2, c = i % H2;
+        const float g2 = valid(r) ? o.G2[(r0 + r) * H2 + c] : 0.f;
+        const float v = g2 > 0.f ? s_dz[r] * P.d3w[c] * k2 : 0.f;
+        G2[r * ldg2 + c] = v;
+        if (valid(r)) o.dG2[(r0 + r) * H2 + c] = v;
+    }
+    __syncthreads();
+    gemm<2>(G2, ldg2, T.d2T, [&](int mt, int nt, floatx4 acc) {   // dG1 = (dG2 W.3) * [G1 > 0] * keep
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) {
+            const int row = erow(mt, r);
+            const float v = G1[row * ldg + c] > 0.f ? acc[r] * k1 : 0.f;
+            G1[row * ldg + c] = v;
+            if (valid(row)) o.dG1[(r0 + row) * HID + c] = v;
+        }
+    });
+    __syncthreads();
+    gemm<2>(G1, ldg, T.d1T, [&](int mt, int nt, floatx4 acc) {   // d time features -> * -sin(t w + phi)
+        const int j = ecol(nt);
+        for (int r = 0; r < 4; ++r) {
+            const int row = erow(mt, r);
+            if (!valid(row)) continue;
+            float gv = 0.f;
+            if (j < dn) gv = -acc[r] * sinf(__fadd_rn(__fmul_rn(s_t[row], P.freq[j]), P.phase[j]));
+            o.g[(r0 + row) * dn16 + j] = gv;
+        }
+    });
+}
+
 }  // namespace tmk
 
 using namespace tmk;
@@ -580,7 +828,8 @@ int train_packs_create(tm_weights *w) {
         Lin *lin;
         int nout, k;
     } ds[] = {{&w->T.evT, dn, dn}, {&w->T.g1T, dn, h}, {&w->T.g2T, h, h},   {&w->T.w1T, h2, h2}, {&w->T.w2T, h2, h2},
-              {&w->T.a1T, h2, h},  {&w->T.a2T, h, h},  {&w->T.m1T, hm, hm}, {&w->T.m2T, hm, h}};
+              {&w->T.a1T, h2, h},  {&w->T.a2T, h, h},  {&w->T.m1T, hm, hm}, {&w->T.m2T, hm, h},
+              {&w->T.d1T, dn, h},  {&w->T.d2T, h, h / 2}};
     size_t total = 0;
     std::vector<size_t> off;
     for (auto &d : ds) {
@@ -653,6 +902,8 @@ void pack_all_weights(tm_weights *w, const float *const *t, hipStream_t s) {
     frag(w->T.a2T, t[12], 1, h);
     frag(w->T.m1T, t[14], 1, hm);
     frag(w->T.m2T, t[16], 1, hm);
+    frag(w->T.d1T, t[20] + de, 1, de + dn);
+    frag(w->T.d2T, t[22], 1, h);
     P.total = total;
     pack_jobs_kernel<<<dim3((unsigned)std::min<int64_t>((total + 255) / 256, 1024)), 256, 0, s>>>(P);
     evc_par_kernel<<<dim3(r16(dn)), 64, 0, s>>>(t[0], t[1], t[27], de, dn, kev, w->P.qt, const_cast<float *>(w->P.evc));
@@ -711,6 +962,77 @@ extern "C" int tm_encoder_bwd(const tm_weights *w, const float *n_feat, const fl
     return TM_OK;
 }
 
+// Shared driver of the weight-gradient launches: jobs (dY, X, rows) and targets (dW, db, job range).
+static int run_wgrad(const tm_wgrad_job *jobs, int njob, const tm_wgrad_target *tgts, int ntgt, hipStream_t s,
+                     const char *what) {
+    if (njob <= 0 || njob > MAX_WG_JOBS || ntgt <= 0 || ntgt > MAX_WG_TGTS)
+        return fail(TM_E_ARG, std::string(what) + ": job / target count out of range");
+    WgPlan P{};
+    P.njob = njob;
+    int64_t wg = 0, pb = 0;
+    for (int j = 0; j < njob; ++j) {
+        const tm_wgrad_job &d = jobs[j];
+        if (!d.dy || !d.x || d.O <= 0 || d.I <= 0 || d.R < 0 || d.ldy < d.O || d.ldx < d.I)
+            return fail(TM_E_ARG, std::string(what) + ": bad job " + std::to_string(j));
+        WgJob &J = P.job[j];
+        J.y = d.dy; J.x = d.x; J.ldy = d.ldy; J.ldx = d.ldx; J.O = d.O; J.I = d.I; J.R = d.R;
+        J.bias = 1;   // a column of ones: every job adds its dY column sums to its target's bias gradient
+        J.OB = (d.O + 63) / 64;
+        J.IB = (d.I + 1 + 63) / 64;
+        J.wg_begin = wg;
+        J.part_begin = pb;
+        const int64_t nchunk = (d.R + WG_CHUNK - 1) / WG_CHUNK;
+        wg += nchunk * J.OB * J.IB;
+        pb += nchunk * J.OB * J.IB * 4096;
+    }
+    P.total_wg = wg;
+    P.ntgt = ntgt;
+    int64_t ob = 0;
+    for (int t = 0; t < ntgt; ++t) {
+        const tm_wgrad_target &d = tgts[t];
+        if (!d.w || !d.b || d.first_job < 0 || d.n_jobs <= 0 || d.first_job + d.n_jobs > njob)
+            return fail(TM_E_ARG, std::string(what) + ": bad target " + std::to_string(t));
+        WgTarget &T = P.tgt[t];
+        T.j0 = d.first_job;
+        T.nj = d.n_jobs;
+        T.w = d.w;
+        T.b = d.b;
+        T.O = jobs[T.j0].O;
+        T.I = jobs[T.j0].I;
+        for (int j = T.j0; j < T.j0 + T.nj; ++j)
+            if (jobs[j].O != T.O || jobs[j].I != T.I)
+                return fail(TM_E_ARG, std::string(what) + ": jobs of one target differ in shape");
+        T.bias = 1;
+        T.out_begin = ob;
+        ob += (int64_t)T.O * (T.I + 1);
+    }
+    P.total_out = ob;
+    if (wg == 0) {   // no rows: every gradient is zero
+        for (int t = 0; t < ntgt; ++t) {
+            TM_HIP(hipMemsetAsync(P.tgt[t].w, 0, sizeof(float) * P.tgt[t].O * P.tgt[t].I, s));
+            TM_HIP(hipMemsetAsync(P.tgt[t].b, 0, sizeof(float) * P.tgt[t].O, s));
+        }
+        return TM_OK;
+    }
+    float *part = reinterpret_cast<float *>(scratch((size_t)pb * sizeof(float), s));
+    if (!part) return fail(TM_E_HIP, std::string(what) + ": scratch allocation failed");
+    hipEvent_t pe = prof_begin(s);
+    wgrad_partial_kernel<<<dim3((unsigned)wg), 256, 0, s>>>(P, part);
+    TM_CHECK_LAUNCH();
+    prof_end("wgrad_partial_kernel", s, pe);
+    pe = prof_begin(s);
+    wgrad_reduce_kernel<<<dim3((unsigned)std::min<int64_t>((ob + 255) / 256, 1024)), 256, 0, s>>>(P, part);
+    TM_CHECK_LAUNCH();
+    prof_end("wgrad_reduce_kernel", s, pe);
+    return TM_OK;
+}
+
+extern "C" int tm_wgrad(const tm_wgrad_job *jobs, int32_t n_jobs, const tm_wgrad_target *targets, int32_t n_targets,
+                        void *stream) {
+    if (!jobs || !targets) return fail(TM_E_ARG, "tm_wgrad: NULL arguments");
+    return run_wgrad(jobs, n_jobs, targets, n_targets, S_(stream), "tm_wgrad");
+}
+
 extern "C" int tm_encoder_wgrad(const tm_weights *w, int32_t n_groups, int32_t B, int32_t W,
                                 const tm_encoder_grad_io *io, const void *workspace, float *const *grads,
                                 void *stream) {
@@ -723,69 +1045,109 @@ extern "C" int tm_encoder_wgrad(const tm_weights *w, int32_t n_groups, int32_t B
     const int n = (int)n64, R = 3 * n, h = w->h, h2 = 2 * h, hm = h + 12;
     const int dn = w->dn, kev = w->P.kev, KE = r16(kev), DN = r16(dn), KM = r16(hm);
     const float *F = reinterpret_cast<const float *>(workspace);
-    struct JD {
-        const float *y, *x;
-        int ldy, ldx, O, I, bias, R;
-    } jd[] = {
-        {io->dlev, io->ev, DN, KE, dn, kev, 1, R},            // lin_event
-        {io->dZ, io->AB, h, DN, h, dn, 1, 2 * R},             // event_conv.MLP.0
-        {io->dF, io->H, h, h, h, h, 1, 2 * R},                // event_conv.MLP.2
-        {io->dP, F + 2 * h2, h2, 3 * h2, h2, h2, 1, n},       // attention.W1 (x = F[:, 2])
-        {io->dQ, F, h2, 3 * h2, h2, h2, 1, n},                // attention.W2, position 0
-        {io->dQ + (int64_t)n * h2, F + h2, h2, 3 * h2, h2, h2, 1, n},   // position 1
-        {io->dH1, io->O, h, h2, h, h2, 1, n},                 // attention.MLP.0
-        {io->dY2, io->H1d, h, h, h, h, 1, n},                 // attention.MLP.3
-        {io->dM1, io->X, KM, KM, hm, hm, 1, n},               // MLP.0
-        {io->dM2, io->M1d, h, KM, h, hm, 1, n},               // MLP.3
-        {io->dlogit, io->M2, 1, h, 1, h, 1, n},               // MLP.5
-        {io->g, io->dt, DN, 1, dn, 1, 1, R},                  // time encoder: freq (x = dt), phase (ones)
+    const tm_wgrad_job jobs[] = {
+        {io->dlev, io->ev, DN, KE, dn, kev, R},            // lin_event
+        {io->dZ, io->AB, h, DN, h, dn, 2 * R},             // event_conv.MLP.0
+        {io->dF, io->H, h, h, h, h, 2 * R},                // event_conv.MLP.2
+        {io->dP, F + 2 * h2, h2, 3 * h2, h2, h2, n},       // attention.W1 (x = F[:, 2])
+        {io->dQ, F, h2, 3 * h2, h2, h2, n},                // attention.W2, position 0
+        {io->dQ + (int64_t)n * h2, F + h2, h2, 3 * h2, h2, h2, n},   // position 1
+        {io->dH1, io->O, h, h2, h, h2, n},                 // attention.MLP.0
+        {io->dY2, io->H1d, h, h, h, h, n},                 // attention.MLP.3
+        {io->dM1, io->X, KM, KM, hm, hm, n},               // MLP.0
+        {io->dM2, io->M1d, h, KM, h, hm, n},               // MLP.3
+        {io->dlogit, io->M2, 1, h, 1, h, n},               // MLP.5
+        {io->g, io->dt, DN, 1, dn, 1, R},                  // time encoder: freq (x = dt), phase (ones)
     };
-    // targets: (first job, job count, weight grad index, bias grad index)
-    const int tg[][4] = {{0, 1, 0, 1}, {1, 1, 2, 3}, {2, 1, 4, 5}, {3, 1, 6, 7}, {4, 2, 8, 9}, {6, 1, 10, 11},
-                         {7, 1, 12, 13}, {8, 1, 14, 15}, {9, 1, 16, 17}, {10, 1, 18, 19}, {11, 1, 20, 21}};
-    WgPlan P{};
-    P.njob = (int)(sizeof(jd) / sizeof(jd[0]));
-    int64_t wg = 0, pb = 0;
-    for (int j = 0; j < P.njob; ++j) {
-        WgJob &J = P.job[j];
-        const JD &d = jd[j];
-        J.y = d.y; J.x = d.x; J.ldy = d.ldy; J.ldx = d.ldx; J.O = d.O; J.I = d.I; J.R = d.R;
-        J.bias = 1;   // W2's two jobs both carry the ones column: its bias gradient sums dQ over both positions
-        J.OB = (d.O + 63) / 64;
-        J.IB = (d.I + 1 + 63) / 64;
-        J.wg_begin = wg;
-        J.part_begin = pb;
-        const int64_t nchunk = (d.R + WG_CHUNK - 1) / WG_CHUNK;
-        wg += nchunk * J.OB * J.IB;
-        pb += nchunk * J.OB * J.IB * 4096;
-    }
-    P.total_wg = wg;
-    P.ntgt = (int)(sizeof(tg) / sizeof(tg[0]));
-    int64_t ob = 0;
-    for (int t = 0; t < P.ntgt; ++t) {
-        WgTarget &T = P.tgt[t];
-        T.j0 = tg[t][0];
-        T.nj = tg[t][1];
-        T.w = grads[tg[t][2]];
-        T.b = grads[tg[t][3]];
-        T.O = jd[T.j0].O;
-        T.I = jd[T.j0].I;
-        T.bias = 1;
-        T.out_begin = ob;
-        ob += (int64_t)T.O * (T.I + 1);
-    }
-    P.total_out = ob;
-    if (wg == 0) return TM_OK;
+    const tm_wgrad_target tgts[] = {{grads[0], grads[1], 0, 1},   {grads[2], grads[3], 1, 1},
+                                    {grads[4], grads[5], 2, 1},   {grads[6], grads[7], 3, 1},
+                                    {grads[8], grads[9], 4, 2},   {grads[10], grads[11], 6, 1},
+                                    {grads[12], grads[13], 7, 1}, {grads[14], grads[15], 8, 1},
+                                    {grads[16], grads[17], 9, 1}, {grads[18], grads[19], 10, 1},
+                                    {grads[20], grads[21], 11, 1}};
+    return run_wgrad(jobs, (int)(sizeof(jobs) / sizeof(jobs[0])), tgts, (int)(sizeof(tgts) / sizeof(tgts[0])),
+                     S_(stream), "tm_encoder_wgrad");
+}
+
+static int expl_hbits(int W) {
+    int hb = 6;
+    while ((1 << hb) < 2 * 3 * W) ++hb;
+    return hb;
+}
+
+extern "C" int tm_explain_train_fwd(const tm_weights *w, const float *e_feat, int32_t n_groups, int32_t B, int32_t W,
+                                    int32_t N, const int32_t *eid3, const float *ts3, const float *imp,
+                                    const int32_t *sub1_eid, const int32_t *sub2_eid, const uint8_t *keep1,
+                                    const uint8_t *keep2, float scale1, float scale2, const tm_explain_grad_io *io,
+                                    float *p1, float *p2, void *stream) {
+    if (!w || !io || n_groups < 0 || B < 0 || W <= 0 || N <= 0) return fail(TM_E_ARG, "tm_explain_train_fwd: bad arguments");
+    const int64_t rows = (int64_t)n_groups * B;
+    if (rows == 0) return TM_OK;
+    if (!e_feat || !eid3 || !ts3 || !imp || !sub1_eid || !sub2_eid || !p1 || !p2 || !io->X || !io->G1 || !io->G2 ||
+        !io->z || !io->gate || !io->t)
+        return fail(TM_E_ARG, "tm_explain_train_fwd: NULL pointer");
+    const int hb = expl_hbits(W);
+    if (hb > 12) return fail(TM_E_UNSUPPORTED, "tm_explain_train_fwd: too many walks per event");
+    const EncW &P = w->P;
     hipStream_t s = S_(stream);
-    float *part = reinterpret_cast<float *>(scratch((size_t)pb * sizeof(float), s));
-    if (!part) return fail(TM_E_HIP, "tm_encoder_wgrad: scratch allocation failed");
+    const int64_t R = rows * 3 * W;
+    ExplIO o{io->X, io->G1, io->G2, io->z, io->gate, io->d_gate, io->dz, io->dG2, io->dG1, io->g, io->t};
+    const size_t lds = sizeof(float) * (TILE_ROWS * (r16(P.kdep) + 8) + TILE_ROWS * (HID + 8) + TILE_ROWS * (HID / 2 + 8));
     hipEvent_t pe = prof_begin(s);
-    wgrad_partial_kernel<<<dim3((unsigned)wg), 256, 0, s>>>(P, part);
+    gate_train_fwd_kernel<<<dim3((unsigned)((R + TILE_ROWS - 1) / TILE_ROWS)), 256, lds, s>>>(
+        P, R, e_feat, eid3, ts3, keep1, keep2, scale1, scale2, o);
     TM_CHECK_LAUNCH();
-    prof_end("wgrad_partial_kernel", s, pe);
+    prof_end("gate_train_fwd_kernel", s, pe);
     pe = prof_begin(s);
-    wgrad_reduce_kernel<<<dim3((unsigned)std::min<int64_t>((ob + 255) / 256, 1024)), 256, 0, s>>>(P, part);
+    explain_train_kernel<<<dim3((unsigned)rows), 256, 2 * sizeof(int32_t) * (1u << hb), s>>>(
+        W, N, hb, eid3, imp, io->gate, sub1_eid, sub2_eid, p1, p2);
     TM_CHECK_LAUNCH();
-    prof_end("wgrad_reduce_kernel", s, pe);
+    prof_end("explain_train_kernel", s, pe);
     return TM_OK;
+}
+
+extern "C" int tm_explain_train_bwd(const tm_weights *w, int32_t n_groups, int32_t B, int32_t W, int32_t N,
+                                    const int32_t *eid3, const float *ts3, const float *imp, const int32_t *sub1_eid,
+                                    const int32_t *sub2_eid, const uint8_t *keep1, const uint8_t *keep2, float scale1,
+                                    float scale2, const float *dp1, const float *dp2, const tm_explain_grad_io *io,
+                                    float *d_imp, float *const *grads, void *stream) {
+    (void)ts3;
+    if (!w || !io || !grads || n_groups < 0 || B < 0 || W <= 0 || N <= 0)
+        return fail(TM_E_ARG, "tm_explain_train_bwd: bad arguments");
+    for (int i = 0; i < 8; ++i)
+        if (!grads[i]) return fail(TM_E_ARG, "tm_explain_train_bwd: NULL gradient " + std::to_string(i));
+    const int64_t rows = (int64_t)n_groups * B;
+    if (!eid3 || !imp || !sub1_eid || !sub2_eid || !dp1 || !dp2 || !d_imp || !io->X || !io->G1 || !io->G2 ||
+        !io->z || !io->gate || !io->d_gate || !io->dz || !io->dG2 || !io->dG1 || !io->g || !io->t)
+        return fail(TM_E_ARG, "tm_explain_train_bwd: NULL pointer");
+    const int64_t R64 = rows * 3 * W;
+    if (R64 > INT32_MAX) return fail(TM_E_UNSUPPORTED, "tm_explain_train_bwd: too many walk positions");
+    const int hb = expl_hbits(W);
+    if (hb > 12) return fail(TM_E_UNSUPPORTED, "tm_explain_train_bwd: too many walks per event");
+    const EncW &P = w->P;
+    hipStream_t s = S_(stream);
+    ExplIO o{io->X, io->G1, io->G2, io->z, io->gate, io->d_gate, io->dz, io->dG2, io->dG1, io->g, io->t};
+    if (rows > 0) {
+        hipEvent_t pe = prof_begin(s);
+        explain_train_bwd_kernel<<<dim3((unsigned)rows), 256, 4 * sizeof(int32_t) * (1u << hb), s>>>(
+            W, N, hb, eid3, imp, io->gate, sub1_eid, sub2_eid, dp1, dp2, d_imp, io->d_gate);
+        TM_CHECK_LAUNCH();
+        prof_end("explain_train_bwd_kernel", s, pe);
+        const size_t lds = sizeof(float) * (TILE_ROWS * (HID + 8) + TILE_ROWS * (HID / 2 + 8));
+        pe = prof_begin(s);
+        gate_train_bwd_kernel<<<dim3((unsigned)((R64 + TILE_ROWS - 1) / TILE_ROWS)), 256, lds, s>>>(
+            P, w->T, R64, keep1, keep2, scale1, scale2, o);
+        TM_CHECK_LAUNCH();
+        prof_end("gate_train_bwd_kernel", s, pe);
+    }
+    const int R = (int)R64, h = w->h, dn = w->dn, kdep = P.kdep;
+    const tm_wgrad_job jobs[] = {
+        {io->dG1, io->X, h, r16(kdep), h, kdep, R},        // edge_dependency_gcn.0
+        {io->dG2, io->G1, h / 2, h, h / 2, h, R},          // .3
+        {io->dz, io->G2, 1, h / 2, 1, h / 2, R},           // .6
+        {io->g, io->t, r16(dn), 1, dn, 1, R},              // time encoder: freq (x = t), phase (ones)
+    };
+    const tm_wgrad_target tgts[] = {{grads[0], grads[1], 0, 1}, {grads[2], grads[3], 1, 1}, {grads[4], grads[5], 2, 1},
+                                    {grads[6], grads[7], 3, 1}};
+    return run_wgrad(jobs, 4, tgts, 4, s, "tm_explain_train_bwd");
 }

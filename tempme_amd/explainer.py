@@ -295,6 +295,79 @@ class TempME(nn.Module):
                                          L.stream_ptr(dev)), "TempME.forward weight gradients")
         return tuple(grads)
 
+    def _gate_params(self):
+        d = self.edge_dependency_gcn
+        return [d[0].weight, d[0].bias, d[3].weight, d[3].bias, d[6].weight, d[6].bias,
+                self.time_encoder.basis_freq, self.time_encoder.phase]
+
+    def gate_dropout_masks(self, n_pos):
+        """Keep-masks of edge_dependency_gcn's Dropout(1.5p) [n_pos, h] and Dropout(p) [n_pos, h/2]
+        (explainer_new.py:136-140) from torch's device RNG, or None in eval mode."""
+        p = self.dropout_p
+        if not self.training or p <= 0:
+            return None, None, 1.0, 1.0
+        dev = self._dev()
+        p1 = min(1.5 * p, 1.0)
+        k1 = torch.empty(n_pos, self.hid_dim, dtype=torch.uint8, device=dev).bernoulli_(1.0 - p1)
+        k2 = torch.empty(n_pos, self.hid_dim // 2, dtype=torch.uint8, device=dev).bernoulli_(1.0 - p)
+        return k1, k2, (1.0 / (1.0 - p1) if p1 < 1 else 0.0), 1.0 / (1.0 - p)
+
+    def explain_groups(self, imp, eid3, ts3, s1n, s1e, s2n, s2e, n_groups, B, W, N, training, masks=None):
+        """retrieve_edge_imp_node (explainer_new.py:354-406) for n_groups calls at once with gradients to
+        imp and the dependency gate: tm_explain_train_fwd / _bwd up to the gathered maxima, then
+        beta_sample and the padding mask in torch ops (the rsample gradient is torch's).  imp
+        [G,B,W]; returns hop-1 [G,B,N] and hop-2 [G,B,N^2]."""
+        dev = self._dev()
+        if masks is None:
+            masks = self.gate_dropout_masks(n_groups * B * 3 * W)
+        args = (eid3.to(dev, torch.int32).contiguous(), ts3.to(dev, torch.float32).contiguous(),
+                s1e.to(dev, torch.int32).contiguous(), s2e.to(dev, torch.int32).contiguous(), masks,
+                int(n_groups), int(B), int(W), int(N))
+        p1, p2 = _ExplainFn.apply(self, args, imp.reshape(-1).to(dev, torch.float32).contiguous(),
+                                  *self._gate_params())
+        e1 = self.beta_sample(p1.view(n_groups, B, N), training)
+        e2 = self.beta_sample(p2.view(n_groups, B, N * N), training)
+        e1 = e1.masked_fill(s1n.to(dev).view(n_groups, B, N) == 0, 0)
+        e2 = e2.masked_fill(s2n.to(dev).view(n_groups, B, N * N) == 0, 0)
+        return e1, e2
+
+    def _expl_io(self, R):
+        dev = self._dev()
+        h, dn = self.hid_dim, self.node_dim
+        KD, DN = -(-(self.edge_dim + dn) // 16) * 16, -(-dn // 16) * 16
+        e = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
+        b = dict(X=e(R, KD), G1=e(R, h), G2=e(R, h // 2), z=e(R), gate=e(R), d_gate=e(R), dz=e(R), dG2=e(R, h // 2),
+                 dG1=e(R, h), g=e(R, DN), t=e(R))
+        return b, L.ExplainGradIO(*[b[k].data_ptr() for k in L.EXPL_IO_FIELDS])
+
+    def _explain_fwd(self, args, imp):
+        eid3, ts3, s1e, s2e, (k1, k2, sc1, sc2), G, B, W, N = args
+        dev = self._dev()
+        _, et = self.feature_tables()
+        b, io = self._expl_io(G * B * 3 * W)
+        p1 = torch.empty(max(G * B * N, 1), dtype=torch.float32, device=dev)
+        p2 = torch.empty(max(G * B * N * N, 1), dtype=torch.float32, device=dev)
+        L.check(L.lib().tm_explain_train_fwd(self.packed_weights(), L.ptr(et), G, B, W, N, L.ptr(eid3), L.ptr(ts3),
+                                             L.ptr(imp), L.ptr(s1e), L.ptr(s2e), L.ptr(k1), L.ptr(k2), sc1, sc2,
+                                             L.C.byref(io), L.ptr(p1), L.ptr(p2), L.stream_ptr(dev)),
+                "retrieve_edge_imp_node (training)")
+        return p1[:G * B * N], p2[:G * B * N * N], (b, io)
+
+    def _explain_bwd(self, args, imp, bufs, dp1, dp2):
+        eid3, ts3, s1e, s2e, (k1, k2, sc1, sc2), G, B, W, N = args
+        dev = self._dev()
+        b, io = bufs
+        d_imp = torch.empty(max(G * B * W, 1), dtype=torch.float32, device=dev)
+        grads = [torch.empty_like(p, memory_format=torch.contiguous_format) for p in self._gate_params()]
+        gp = (L.C.c_void_p * len(grads))(*[t.data_ptr() for t in grads])
+        dp1 = dp1.to(dev, torch.float32).contiguous()
+        dp2 = dp2.to(dev, torch.float32).contiguous()
+        L.check(L.lib().tm_explain_train_bwd(self.packed_weights(), G, B, W, N, L.ptr(eid3), L.ptr(ts3), L.ptr(imp),
+                                             L.ptr(s1e), L.ptr(s2e), L.ptr(k1), L.ptr(k2), sc1, sc2, L.ptr(dp1),
+                                             L.ptr(dp2), L.C.byref(io), L.ptr(d_imp), gp, L.stream_ptr(dev)),
+                "retrieve_edge_imp_node backward")
+        return d_imp[:G * B * W], grads
+
     # ------------------------------------------------------------------ reference API
     def forward(self, walks, cut_time_l, edge_identify):
         """explainer_new.py:174-201 -> [bsz, n_walks, 1]."""
@@ -320,8 +393,16 @@ class TempME(nn.Module):
         """explainer_new.py:354-406 -> (hop-1 [B,N], hop-2 [B,N^2])."""
         node_record, eidx_record, _ = subgraph
         dev = self._dev()
-        if training or graphlet_imp.requires_grad or not self._hip_ok():
+        if not self._hip_ok():
             return self._edge_imp_torch(subgraph, graphlet_imp, walks, training)
+        if training or (graphlet_imp.requires_grad and torch.is_grad_enabled()) or self._needs_autograd():
+            B, N = np.shape(node_record[0])[0], np.shape(node_record[0])[1]
+            W = np.shape(walks[1])[1]
+            e0, e1 = self.explain_groups(graphlet_imp.reshape(1, B, W), _to(walks[1], dev, torch.int32),
+                                         _to(walks[2], dev, torch.float32), _to(node_record[0], dev, torch.int32),
+                                         _to(eidx_record[0], dev, torch.int32), _to(node_record[1], dev, torch.int32),
+                                         _to(eidx_record[1], dev, torch.int32), 1, B, W, N, training)
+            return e0.view(B, N), e1.view(B, N * N)
         B, N = np.shape(node_record[0])[0], np.shape(node_record[0])[1]
         W = np.shape(walks[1])[1]
         o1, o2 = self.edge_importance(_to(walks[1], dev, torch.int32).contiguous(),
@@ -462,3 +543,21 @@ class _EncoderFn(torch.autograd.Function):
         grads = ctx.ex._train_bwd(ctx.args, ctx.drop, ctx.drop_scale, ctx.ws, d_imp)
         ctx.ws = None
         return (None, None, None, None, *grads)
+
+
+class _ExplainFn(torch.autograd.Function):
+    """retrieve_edge_imp_node's gate + scatter-max + gather (training) on the HIP kernels."""
+
+    @staticmethod
+    def forward(ctx, ex, args, imp, *params):
+        p1, p2, bufs = ex._explain_fwd(args, imp)
+        ctx.ex, ctx.args, ctx.bufs = ex, args, bufs
+        ctx.save_for_backward(imp)
+        return p1, p2
+
+    @staticmethod
+    def backward(ctx, dp1, dp2):
+        (imp,) = ctx.saved_tensors
+        d_imp, grads = ctx.ex._explain_bwd(ctx.args, imp, ctx.bufs, dp1, dp2)
+        ctx.bufs = None
+        return (None, None, d_imp, *grads)

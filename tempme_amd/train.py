@@ -110,6 +110,29 @@ class GradAllReduce:
             off += g.numel()
 
 
+def explain_sides(explainer, batch, imps, training):
+    """Explainer.retrieve_explanation(sg_src, imp_src, walks_src, ..., training) (temp_exp_main.py:608-609);
+    on the HIP path the three sides run as one explain_groups call.  Returns the reference's list
+    [hop-1 [3B, N], hop-2 [3B, N^2]] (hop-1 only for non-TGN bases)."""
+    if not explainer._hip_ok() or batch.stacked is None:
+        (sg_s, sg_t, sg_b), (w_s, w_t, w_b) = batch.subgraphs, batch.walks
+        return explainer.retrieve_explanation(sg_s, imps[0], w_s, sg_t, imps[1], w_t, sg_b, imps[2], w_b,
+                                              training=training)
+    dev = explainer._dev()
+    node6, eid3, ts3, cat, cnt = batch.stacked
+    G, B, W = eid3.shape[0], eid3.shape[1], eid3.shape[2]
+    s1n = torch.stack([_as_dev(sg[0][0], dev, torch.int32) for sg in batch.subgraphs])
+    s1e = torch.stack([_as_dev(sg[1][0], dev, torch.int32) for sg in batch.subgraphs])
+    s2n = torch.stack([_as_dev(sg[0][1], dev, torch.int32) for sg in batch.subgraphs])
+    s2e = torch.stack([_as_dev(sg[1][1], dev, torch.int32) for sg in batch.subgraphs])
+    N = s1n.shape[-1]
+    imp = torch.stack([x.reshape(B, W) for x in imps])
+    e1, e2 = explainer.explain_groups(imp, eid3, ts3, s1n, s1e, s2n, s2e, G, B, W, N, training)
+    if explainer.base_type == "tgn":
+        return [e1.reshape(G * B, N), e2.reshape(G * B, N * N)]
+    return [e1.reshape(G * B, N)]
+
+
 def train_step(explainer, base_model, optimizer, batch, *, beta=0.5, prior_p=0.3, if_bern=True, criterion=None,
                grad_sync=None):
     """temp_exp_main.py:593-632 for one batch; returns the step's tensors (no host sync)."""
@@ -123,7 +146,7 @@ def train_step(explainer, base_model, optimizer, batch, *, beta=0.5, prior_p=0.3
         y_ori = torch.where(y_pred > 0.5, 1., 0.).view(y_pred.size(0), 1)
     optimizer.zero_grad()
     g_s, g_t, g_b = encode_sides(explainer, batch)
-    explanation = explainer.retrieve_explanation(sg_s, g_s, w_s, sg_t, g_t, w_t, sg_b, g_b, w_b, training=if_bern)
+    explanation = explain_sides(explainer, batch, (g_s, g_t, g_b), if_bern)
     pos_logit, neg_logit = base_model.contrast(batch.src, batch.dst, batch.fake, batch.ts, batch.e_idx, sg_s, sg_t,
                                                sg_b, explain_weights=explanation)
     pred = torch.cat([pos_logit, neg_logit], dim=0)

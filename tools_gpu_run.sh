@@ -17,7 +17,7 @@ step() {  # step <name> <timeout_s> <cmd...>
 for s in "$@"; do
     case $s in
         tests) step pytest_gpu 900 python -m pytest tests -x -q -m gpu ;;
-        f3) step pytest_f3 600 python -u -m pytest tests/test_gpu_encoder_train.py tests/test_gpu_train.py tests/test_gpu_pack.py -x -v --timeout 300 -m gpu ;;
+        f3) step pytest_f3 600 python -u -m pytest tests/test_gpu_encoder_train.py tests/test_gpu_explain_train.py tests/test_gpu_train.py tests/test_gpu_pack.py -x -v --timeout 300 -m gpu ;;
         tgn) step pytest_tgn 600 python -m pytest tests/test_gpu_tgn.py tests/test_gpu_train.py tests/test_gpu_graphmixer.py -x -q -m gpu ;;
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) step bench 600 python bench.py --steps 10 --warmup 2 ;;
@@ -61,6 +61,7 @@ for s in "$@"; do
             TEMPME_DIST_BACKEND=gloo step bench_train2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                 --master-addr 127.0.0.1 --master-port 29512 bench_train.py --gpus 2 --steps 5 --warmup 1 ;;
         n30) step bench_n30 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --n-degree 30 ;;
+        phases) step phases 300 python tools_train_phases.py ;;
         c2) step bench_c2 600 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config 2 ;;
         c4) step bench_c4 900 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config 4 ;;
         a3) step bench_a3 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --alpha 3.0 ;;
