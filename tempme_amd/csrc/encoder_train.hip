@@ -485,7 +485,7 @@ __global__ void __launch_bounds__(256) gcn_bwd_kernel(EncW P, EncWT T, int64_t n
 constexpr int WG_CHUNK = 1024, WG_LDS_LD = 80, MAX_WG_JOBS = 14, MAX_WG_TGTS = 12;
 struct WgJob {
     const float *y, *x;
-    int32_t ldy, ldx, O, I, bias, OB, IB, R;
+    int32_t ldy, ldx, O, I, bias, OB, IB, R, vec;
     int64_t wg_begin, part_begin;
 };
 struct WgTarget {
@@ -500,8 +500,53 @@ struct WgPlan {
     int64_t total_wg, total_out;
 };
 
+// slab staging: 64 rows x 64 columns of dY (cols o0..) and X (cols i0.., the ones column at I), one
+// float4 per (thread, k) when the job's rows are 16-byte aligned (vec), else scalars
+struct Slab {
+    float4 y[4], x[4];
+};
+
+__device__ __forceinline__ float4 ld_cols(const float *p, int64_t row_off, int c0, int ncol, bool vec, bool ones,
+                                          bool rv) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (!rv) return v;
+    float e[4] = {0.f, 0.f, 0.f, 0.f};
+    if (vec && c0 + 3 < ncol) {
+        v = *reinterpret_cast<const float4 *>(p + row_off + c0);
+        e[0] = v.x; e[1] = v.y; e[2] = v.z; e[3] = v.w;
+    } else {
+        for (int k = 0; k < 4; ++k)
+            if (c0 + k < ncol) e[k] = p[row_off + c0 + k];
+    }
+    if (ones)
+        for (int k = 0; k < 4; ++k)
+            if (c0 + k == ncol) e[k] = 1.f;
+    return make_float4(e[0], e[1], e[2], e[3]);
+}
+
+__device__ __forceinline__ void slab_load(const WgJob &J, int r0, int r_end, int o0, int i0, Slab &sl) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int e = tid + 256 * k, row = e >> 4, c = (e & 15) * 4, r = r0 + row;
+        const bool rv = r < r_end;
+        sl.y[k] = ld_cols(J.y, (int64_t)r * J.ldy, o0 + c, J.O, J.vec, false, rv);
+        sl.x[k] = ld_cols(J.x, (int64_t)r * J.ldx, i0 + c, J.I, J.vec, J.bias != 0, rv);
+    }
+}
+
+__device__ __forceinline__ void slab_store(const Slab &sl, float *Ys, float *Xs) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int e = tid + 256 * k, row = e >> 4, c = (e & 15) * 4;
+        *reinterpret_cast<float4 *>(Ys + row * WG_LDS_LD + c) = sl.y[k];
+        *reinterpret_cast<float4 *>(Xs + row * WG_LDS_LD + c) = sl.x[k];
+    }
+}
+
 __global__ void __launch_bounds__(256) wgrad_partial_kernel(WgPlan P, float *__restrict__ part) {
-    __shared__ __attribute__((aligned(16))) float Ys[64 * WG_LDS_LD], Xs[64 * WG_LDS_LD];
+    __shared__ __attribute__((aligned(16))) float Ys[2][64 * WG_LDS_LD], Xs[2][64 * WG_LDS_LD];
     const int64_t bid = blockIdx.x;
     int j = 0;
     while (j + 1 < P.njob && bid >= P.job[j + 1].wg_begin) ++j;
@@ -515,30 +560,28 @@ __global__ void __launch_bounds__(256) wgrad_partial_kernel(WgPlan P, float *__r
     floatx4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // double-buffered: slab k+1 is loaded into registers while slab k's MFMAs run from LDS
+    Slab sl;
+    slab_load(J, r_begin, r_end, o0, i0, sl);
+    slab_store(sl, Ys[0], Xs[0]);
+    __syncthreads();
+    int buf = 0;
     for (int r0 = r_begin; r0 < r_end; r0 += 64) {
-        for (int e = tid; e < 64 * 64; e += 256) {
-            const int row = e >> 6, col = e & 63, r = r0 + row;
-            const bool rv = r < r_end;
-            const int o = o0 + col, i = i0 + col;
-            Ys[row * WG_LDS_LD + col] = (rv && o < J.O) ? J.y[(int64_t)r * J.ldy + o] : 0.f;
-            float xv = 0.f;
-            if (rv) {
-                if (i < J.I) xv = J.x[(int64_t)r * J.ldx + i];
-                else if (J.bias && i == J.I) xv = 1.f;
-            }
-            Xs[row * WG_LDS_LD + col] = xv;
-        }
-        __syncthreads();
+        const bool more = r0 + 64 < r_end;
+        if (more) slab_load(J, r0 + 64, r_end, o0, i0, sl);
+        const float *Y = Ys[buf], *X = Xs[buf];
 #pragma unroll 4
         for (int s = 0; s < 16; ++s) {
-            const float a = Ys[(4 * s + g) * WG_LDS_LD + 16 * wave + m];
+            const float a = Y[(4 * s + g) * WG_LDS_LD + 16 * wave + m];
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
-                const float b = Xs[(4 * s + g) * WG_LDS_LD + 16 * t + m];
+                const float b = X[(4 * s + g) * WG_LDS_LD + 16 * t + m];
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
             }
         }
+        if (more) slab_store(sl, Ys[buf ^ 1], Xs[buf ^ 1]);
         __syncthreads();
+        buf ^= 1;
     }
     float *out = part + J.part_begin + local * 4096;
 #pragma unroll
@@ -977,6 +1020,9 @@ static int run_wgrad(const tm_wgrad_job *jobs, int njob, const tm_wgrad_target *
         WgJob &J = P.job[j];
         J.y = d.dy; J.x = d.x; J.ldy = d.ldy; J.ldx = d.ldx; J.O = d.O; J.I = d.I; J.R = d.R;
         J.bias = 1;   // a column of ones: every job adds its dY column sums to its target's bias gradient
+        // float4 staging when both row arrays are 16-byte aligned row by row
+        J.vec = (d.ldy % 4 == 0 && d.ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(d.dy) & 15) == 0 &&
+                 (reinterpret_cast<uintptr_t>(d.x) & 15) == 0) ? 1 : 0;
         J.OB = (d.O + 63) / 64;
         J.IB = (d.I + 1 + 63) / 64;
         J.wg_begin = wg;
