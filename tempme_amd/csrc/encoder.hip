@@ -338,11 +338,7 @@ __global__ void __launch_bounds__(256) explain_kernel(EncW P, int32_t W, int32_t
         __syncthreads();
         {
             const int r = tid >> 3, sub = tid & 7;
-            float s = 0.f;
-            for (int c = sub; c < HID / 2; c += 8) s += G2[r * ldg2 + c] * P.d3w[c];
-            s += __shfl_xor(s, 1, 8);
-            s += __shfl_xor(s, 2, 8);
-            s += __shfl_xor(s, 4, 8);
+            const float s = gate_logit_lds(G2 + r * ldg2, P.d3w, sub);
             const int gr = c0 + r;
             if (sub == 0 && gr < nrow) {
                 const float z = s + P.d3b[0];
@@ -955,15 +951,65 @@ __global__ void __launch_bounds__(256) gate_table_kernel(EncW P, int32_t n_ids, 
     });
     __syncthreads();
     const int r = tid >> 3, sub = tid & 7;
-    float s = 0.f;
-    for (int c = sub; c < HID / 2; c += 8) s += G2[r * ldg2 + c] * P.d3w[c];
-    s += __shfl_xor(s, 1, 8);
-    s += __shfl_xor(s, 2, 8);
-    s += __shfl_xor(s, 4, 8);
+    const float s = gate_logit_lds(G2 + r * ldg2, P.d3w, sub);
     if (sub == 0 && e0 + r < n_ids) {
         const float z = s + P.d3b[0];
         gf[e0 + r] = 0.5f + 0.5f * (1.f / (1.f + expf(-z)));
     }
+}
+
+// Register-resident gate table: one wave = 16 edge ids (MFMA columns), the gate MLP's weights as the
+// A operand (walk_kernel's layout), X = [E[e] | cos(t_e w + phi)] generated straight into the B
+// fragments, G1 -> G2 -> logit chained in registers.  NQ = K steps of X (de + dn rounded up / 16).
+template <int NQ>
+__global__ void __launch_bounds__(256) gate_reg_kernel(EncW P, int32_t n_ids, const double *__restrict__ ets,
+                                                       const float *__restrict__ e_feat, float *__restrict__ gf) {
+    const int lane = threadIdx.x & 63, col = lane & 15, g = lane_id() >> 4;
+    const int64_t e = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + col;
+    if (((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 >= n_ids) return;   // wave-uniform
+    const bool valid = e < n_ids;
+    const int64_t ec = valid ? e : 0;
+    const int de = P.de, kdep = P.kdep;
+    const float t = (float)ets[ec];
+    const float *erow = e_feat + ec * de;
+    floatx4 X[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        if ((de & 3) == 0 && 16 * q + 16 <= de) {     // whole K step inside the edge-feature row
+            const float4 v = *reinterpret_cast<const float4 *>(erow + 16 * q + 4 * g);
+            X[q] = floatx4{v.x, v.y, v.z, v.w};
+        } else {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int k = 16 * q + 4 * g + s;
+                float v = 0.f;
+                if (k < de) v = erow[k];
+                else if (k < kdep) v = time_cos(t, P.freq[k - de], P.phase[k - de]);
+                X[q][s] = v;
+            }
+        }
+    }
+    floatx4 G1[4];
+    rgemm<4, NQ>(P.d1, X, G1);
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) G1[tt] = relu_add4(G1[tt], *reinterpret_cast<const float4 *>(P.d1.b + 16 * tt + 4 * g));
+    floatx4 G2[2];
+    rgemm<2, 4>(P.d2, G1, G2);
+    // this lane group's part of the logit in gate_part's order (features 16t + 4g + r), then
+    // (part0 + part1) + (part2 + part3) across the lane groups, exactly as gate_logit_lds sums it
+    float z = 0.f;
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+        const float4 b = *reinterpret_cast<const float4 *>(P.d2.b + 16 * tt + 4 * g);
+        const float4 w3 = *reinterpret_cast<const float4 *>(P.d3w + 16 * tt + 4 * g);
+        const float bb[4] = {b.x, b.y, b.z, b.w}, ww[4] = {w3.x, w3.y, w3.z, w3.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) z = __builtin_fmaf(relu(G2[tt][r] + bb[r]), ww[r], z);
+    }
+    z += __shfl_xor(z, 16);
+    z += __shfl_xor(z, 32);
+    z += P.d3b[0];
+    if (valid && g == 0) gf[e] = 0.5f + 0.5f * (1.f / (1.f + expf(-z)));
 }
 
 // retrieve_edge_imp_node with the gate table: per (group, event) the LDS hash keeps, per edge id,
@@ -1145,8 +1191,19 @@ extern "C" int tm_edge_gate_table(const tm_weights *w, const tm_graph *g, const 
         return fail(TM_E_UNSUPPORTED, "tm_edge_gate_table: an edge id carries several timestamps; use tm_edge_importance");
     const int32_t n = g->d.max_eid + 1;
     hipEvent_t pe = prof_begin(S_(stream));
-    gate_table_kernel<<<dim3((n + TILE_ROWS - 1) / TILE_ROWS), 256, gate_lds(w->P), S_(stream)>>>(w->P, n, g->d.ets,
-                                                                                                e_feat, out_gf);
+    const int nq = w->P.d1.nq;
+    const unsigned rblocks = (unsigned)((n + 63) / 64);
+    if (w->P.d2.nq == 4 && w->P.d1.nt == 4 && w->P.d2.nt == 2) {   // hid_dim 64: register-resident path
+        if (nq == 11) gate_reg_kernel<11><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf);
+        else if (nq == 12) gate_reg_kernel<12><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf);
+        else if (nq == 13) gate_reg_kernel<13><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf);
+        else if (nq == 22) gate_reg_kernel<22><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf);
+        else gate_table_kernel<<<dim3((n + TILE_ROWS - 1) / TILE_ROWS), 256, gate_lds(w->P), S_(stream)>>>(
+            w->P, n, g->d.ets, e_feat, out_gf);
+    } else {
+        gate_table_kernel<<<dim3((n + TILE_ROWS - 1) / TILE_ROWS), 256, gate_lds(w->P), S_(stream)>>>(w->P, n, g->d.ets,
+                                                                                                    e_feat, out_gf);
+    }
     TM_CHECK_LAUNCH();
     prof_end("gate_table_kernel", S_(stream), pe);
     return TM_OK;

@@ -92,6 +92,26 @@ __device__ __forceinline__ float time_cos(float t, float w, float phi) { return 
 
 __device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
 
+// The dependency gate's logit d3 . G2 over its h/2 = 32 features in ONE fixed order, shared by the
+// LDS-tiled kernels and the register-resident gate_reg_kernel so their gates agree bit for bit:
+// part k (k = 0..3) is an fma chain over features 16t + 4k + r (t = 0, 1; r = 0..3) and
+// z = (part0 + part1) + (part2 + part3).
+__device__ __forceinline__ float gate_part(const float *g2, const float *w3, int k) {
+    float p = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) p = __builtin_fmaf(g2[16 * t + 4 * k + r], w3[16 * t + 4 * k + r], p);
+    return p;
+}
+// LDS form: 8 lanes per row (sub = lane & 7), the row's relu'd G2 at g2; the result in every lane
+__device__ __forceinline__ float gate_logit_lds(const float *g2, const float *w3, int sub) {
+    float v = sub < 4 ? gate_part(g2, w3, sub) : 0.f;
+    v += __shfl_xor(v, 1, 8);
+    v += __shfl_xor(v, 2, 8);
+    return v;
+}
+
 // Transposed weight packs for the backward's data-gradient GEMMs (dX = dY W = dY (W^T)^T), same
 // fragment format as the forward packs; no biases.  evT holds only lin_event's time-feature columns.
 struct EncWT {

@@ -681,11 +681,7 @@ __global__ void __launch_bounds__(256) gate_train_fwd_kernel(EncW P, int64_t n_r
     });
     __syncthreads();
     const int r = tid >> 3, sub = tid & 7;
-    float sv = 0.f;
-    for (int c = sub; c < H2; c += 8) sv += G2[r * ldg2 + c] * P.d3w[c];
-    sv += __shfl_xor(sv, 1, 8);
-    sv += __shfl_xor(sv, 2, 8);
-    sv += __shfl_xor(sv, 4, 8);
+    const float sv = gate_logit_lds(G2 + r * ldg2, P.d3w, sub);
     if (sub == 0 && valid(r)) {
         const float z = sv + P.d3b[0];
         o.z[r0 + r] = z;

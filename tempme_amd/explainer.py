@@ -395,7 +395,7 @@ class TempME(nn.Module):
         dev = self._dev()
         if not self._hip_ok():
             return self._edge_imp_torch(subgraph, graphlet_imp, walks, training)
-        if training or (graphlet_imp.requires_grad and torch.is_grad_enabled()) or self._needs_autograd():
+        if training or (graphlet_imp.requires_grad and torch.is_grad_enabled()):
             B, N = np.shape(node_record[0])[0], np.shape(node_record[0])[1]
             W = np.shape(walks[1])[1]
             e0, e1 = self.explain_groups(graphlet_imp.reshape(1, B, W), _to(walks[1], dev, torch.int32),
