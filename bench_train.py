@@ -30,7 +30,9 @@ def main():
     ap.add_argument("--alpha", type=float, default=1.2)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-graph", action="store_true", help="launch every kernel from the host each step "
-                    "instead of replaying the step captured as a HIP graph")
+                    "instead of replaying the step captured as a HIP graph (the default with one GPU)")
+    ap.add_argument("--graph", action="store_true", help="capture the step as a HIP graph with several ranks "
+                    "too (the RCCL all-reduce is then captured inside the graph)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -72,7 +74,7 @@ def main():
     base = base.to(dev).eval()
     ex = tm.TempME(base, "tgn", "enron", out_dim=40, hid_dim=64, device=dev,
                    null_model={k: 1.0 / 12 for k in range(1, 13)}).to(dev)
-    use_graph = not args.no_graph and (world == 1 or backend == "nccl")
+    use_graph = not args.no_graph and (world == 1 or (args.graph and backend == "nccl"))
     opt = torch.optim.Adam(ex.parameters(), lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0,
                            capturable=use_graph)
     sync = GradAllReduce(ex)
