@@ -249,23 +249,28 @@ __device__ __forceinline__ Step2Cuts step2_cuts(const DevGraph &g, int32_t u, in
     return Step2Cuts{(vu && lu > 0) ? lu : 0, (vv && lv > 0) ? lv : 0, vu ? g.off[u] : 0, vv ? g.off[v1] : 0};
 }
 
+// MC > 0: M is the compile-time constant MC (3 for the walks, 1 for the null model) and the rank of
+// each draw is MC x MC compares; MC = 0: any M <= kMaxM, padded to kMaxM.
+template <int MC = 0>
 __device__ __forceinline__ Step2 next_step(const DevGraph &g, Key key, uint32_t ev, uint32_t slot, int32_t M,
                                            int32_t m, int32_t u, int32_t v1, const Step2Cuts &sc) {
+    constexpr int MX = MC > 0 ? MC : kMaxM;
+    if (MC > 0) M = MC;
     Step2 o{0, 0, 0, 0.f};
     const int32_t cu = sc.cu, cv = sc.cv, ou = sc.ou, ov = sc.ov, tot = cu + cv;
     if (tot == 0) return o;
-    uint32_t dv[kMaxM];
+    uint32_t dv[MX];
     const uint4 b0 = draw_block(key, TM_STAGE_STEP2, ev, slot, 0);          // draws 0..3 of the slot
-    const uint4 b1 = M > 4 ? draw_block(key, TM_STAGE_STEP2, ev, slot, 1) : b0;
+    const uint4 b1 = (MX > 4 && M > 4) ? draw_block(key, TM_STAGE_STEP2, ev, slot, 1) : b0;
     const uint32_t words[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-    for (int k = 0; k < kMaxM; ++k) dv[k] = k < M ? (uint32_t)scale_draw(words[k], tot) : 0xFFFFFFFFu;
+    for (int k = 0; k < MX; ++k) dv[k] = k < M ? (uint32_t)scale_draw(words[k], tot) : 0xFFFFFFFFu;
     uint32_t sel = 0;
 #pragma unroll
-    for (int k = 0; k < kMaxM; ++k) {
+    for (int k = 0; k < MX; ++k) {
         int32_t rank = 0;
 #pragma unroll
-        for (int i = 0; i < kMaxM; ++i) rank += (dv[i] < dv[k]) || (i < k && dv[i] == dv[k]);
+        for (int i = 0; i < MX; ++i) rank += (dv[i] < dv[k]) || (i < k && dv[i] == dv[k]);
         if (k < M && rank == m) sel = dv[k];
     }
     const int32_t x = (int32_t)sel;
@@ -680,9 +685,40 @@ static inline unsigned reduce_blocks(int64_t n_groups) {
     return (unsigned)std::max<int64_t>(1, std::min<int64_t>(64, (n_groups * 12 + 4095) / 4096));
 }
 
-// LDS of one (event, side): hop-1 row, hop-2 draws, hop-2 cut lengths, walk edge ids, histogram
+// new_edge_info's counts through an LDS hash table (one wave per group): the distinct edge ids of a
+// group are at most N (hop-1 column) + 2W, so a table of >= 1.75x that many slots keeps linear probing
+// short.  Each slot holds the id and its three per-column counts packed 10 bits each (W <= 512).
+__host__ __device__ inline int32_t ecnt_slots(int32_t N, int32_t W) {
+    int32_t s = 64;
+    while (s * 4 < 7 * (N + 2 * W)) s *= 2;
+    return s;
+}
+__device__ __forceinline__ uint32_t ecnt_hash(int32_t x, uint32_t mask) { return ((uint32_t)x * 2654435761u >> 7) & mask; }
+
+// count column q of id x (ids >= 0; empty slot = -1)
+__device__ __forceinline__ void ecnt_insert(int32_t *keys, uint32_t *cnts, uint32_t mask, int32_t x, int q) {
+    uint32_t h = ecnt_hash(x, mask);
+    while (true) {
+        const int32_t prev = atomicCAS(&keys[h], -1, x);
+        if (prev == -1 || prev == x) break;
+        h = (h + 1) & mask;
+    }
+    atomicAdd(&cnts[h], 1u << (10 * q));
+}
+__device__ __forceinline__ uint32_t ecnt_lookup(const int32_t *keys, const uint32_t *cnts, uint32_t mask, int32_t x) {
+    uint32_t h = ecnt_hash(x, mask);
+    while (keys[h] != x) h = (h + 1) & mask;
+    return cnts[h];
+}
+
+// LDS of one (event, side): hop-1 row, hop-2 draws (reused as the edge-count table once hop 2 is
+// done), hop-2 cut lengths, walk edge ids, histogram
+__host__ __device__ inline size_t events_d2_bytes(int32_t N, int32_t M) {
+    const size_t d2 = sizeof(uint32_t) * (size_t)N * N, tab = sizeof(int32_t) * 2 * (size_t)ecnt_slots(N, N * M);
+    return d2 > tab ? d2 : tab;
+}
 __host__ __device__ inline size_t events_lds_bytes(int32_t N, int32_t M) {
-    return sizeof(int32_t) * ((size_t)3 * N + (size_t)N * N + 2 * N + (size_t)N * M * 3 + 12) +
+    return sizeof(int32_t) * ((size_t)3 * N + 2 * N + (size_t)N * M * 3 + 12) + events_d2_bytes(N, M) +
            sizeof(Step2Cuts) * (size_t)N;
 }
 
@@ -699,7 +735,7 @@ __device__ unsigned long long g_est[8];
 #define TM_EST(k) (void)T
 #endif
 
-template <bool keyed>
+template <bool keyed, int MC>
 __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
     unsigned long long T[8];
     TM_EST(0);
@@ -708,7 +744,8 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
     int32_t *h1n = ev_lds, *h1e = h1n + N;
     float *h1t = reinterpret_cast<float *>(h1e + N);
     uint32_t *d2 = reinterpret_cast<uint32_t *>(h1e + 2 * N);
-    int32_t *c2 = reinterpret_cast<int32_t *>(d2 + N * N), *o2 = c2 + N, *weid = o2 + N;
+    int32_t *c2 = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(d2) + events_d2_bytes(N, M)), *o2 = c2 + N,
+            *weid = o2 + N;
     unsigned int *bins = reinterpret_cast<unsigned int *>(weid + W * 3);
     Step2Cuts *s2c = reinterpret_cast<Step2Cuts *>(bins + 12);
     const DevGraph &g = a.g;
@@ -831,11 +868,21 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
         }
     }
     TM_EST(3);
-    // ---- steps 2 + 3, one thread per walk
+    // hop 2 is done with the draws: their LDS becomes the edge-count table
+    const uint32_t tmask = (uint32_t)ecnt_slots(N, W) - 1;
+    int32_t *tkeys = reinterpret_cast<int32_t *>(d2);
+    uint32_t *tcnt = reinterpret_cast<uint32_t *>(tkeys + tmask + 1);
+    __syncthreads();
+    for (int32_t i = tid; i <= (int32_t)tmask; i += blockDim.x) {
+        tkeys[i] = -1;
+        tcnt[i] = 0;
+    }
+    __syncthreads();
+    // ---- steps 2 + 3, one thread per walk; each walk's three ids counted into the table
     for (int32_t w = tid; w < W; w += blockDim.x) {
         const int32_t j = w / M, m = w % M;
         const int32_t v1 = h1n[j], e1 = h1e[j];
-        const Step2 s2 = next_step(g, key, ev, j, M, m, u, v1, s2c[j]);
+        const Step2 s2 = next_step<MC>(g, key, ev, j, M, m, u, v1, s2c[j]);
         const Step3 s3 = final_step(g, key, ev, w, u, v1, s2.src, s2.ngh, s2.eid);
         const int64_t o = se * W + w;
         int32_t *nd = o_node6 + o * 6;
@@ -846,10 +893,22 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
         o_cat[o] = c;
         if (c >= 0) atomicAdd(&bins[c], 1u);
         weid[w * 3 + 0] = s3.eid; weid[w * 3 + 1] = s2.eid; weid[w * 3 + 2] = e1;
+        ecnt_insert(tkeys, tcnt, tmask, s3.eid, 0);
+        ecnt_insert(tkeys, tcnt, tmask, s2.eid, 1);
+        ecnt_insert(tkeys, tcnt, tmask, e1, 2);
     }
     __syncthreads();
     TM_EST(4);
-    edge_counts_group(weid, W, o_cnt + se * W * 9);
+    // new_edge_info (data_preprocess.py:327-343): count of walk w's id p in column q
+    float *const oc = o_cnt + se * W * 9;
+    for (int32_t w = tid; w < W; w += blockDim.x) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const uint32_t c = ecnt_lookup(tkeys, tcnt, tmask, weid[w * 3 + p]);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) oc[(w * 3 + p) * 3 + q] = (float)((c >> (10 * q)) & 1023u);
+        }
+    }
     TM_EST(5);
 #ifdef TM_STAMPS
     if (tid == 0 && e >= 2000 && e < 4000) {
@@ -1005,10 +1064,19 @@ extern "C" int tm_sample_events(const tm_graph *g, uint64_t seed, uint32_t split
                 dst_list, (uint32_t)n_dst, dst_fake, sub1_node, sub1_eid, sub1_ts, sub2_node, sub2_eid, sub2_ts,
                 node6,    eid3,     ts3,       cat,       cnt,      hist12,   bins,     err_flag};
     hipEvent_t pe = prof_begin(S(stream));
-    if (use_keyed(g))
-        events_kernel<true><<<dim3(n_events, 3), 64, events_lds_bytes(N, M), S(stream)>>>(a);
-    else
-        events_kernel<false><<<dim3(n_events, 3), 64, events_lds_bytes(N, M), S(stream)>>>(a);
+    const size_t lds = events_lds_bytes(N, M);
+    const dim3 grid(n_events, 3);
+    const bool kd = use_keyed(g);
+    if (M == 3) {
+        if (kd) events_kernel<true, 3><<<grid, 64, lds, S(stream)>>>(a);
+        else events_kernel<false, 3><<<grid, 64, lds, S(stream)>>>(a);
+    } else if (M == 1) {
+        if (kd) events_kernel<true, 1><<<grid, 64, lds, S(stream)>>>(a);
+        else events_kernel<false, 1><<<grid, 64, lds, S(stream)>>>(a);
+    } else {
+        if (kd) events_kernel<true, 0><<<grid, 64, lds, S(stream)>>>(a);
+        else events_kernel<false, 0><<<grid, 64, lds, S(stream)>>>(a);
+    }
     TM_CHECK_LAUNCH();
     prof_end("events_kernel", S(stream), pe);
     pe = prof_begin(S(stream));
