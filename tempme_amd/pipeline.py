@@ -84,3 +84,47 @@ class ExplainPipeline:
     def check_errors(self):
         if getattr(self, "buf", None) is not None:   # nothing sampled yet: nothing to report
             L.raise_device_error(int(self.buf.err.item()), "ExplainPipeline")
+
+
+class PipelinedExplainer:
+    """``depth`` ExplainPipelines in flight on ``depth`` streams (call k on stream k % depth, each
+    with its own buffers), for a serving loop over many calls: call k+1's sampling overlaps call k's
+    encoder kernel, and call k's explanation overlaps call k+1's encoder.  The encoders themselves
+    are chained by an event (each waits for the previous call's encoder) so they never share the
+    GPU with each other: the MFMA-bound kernel keeps the whole chip, the latency-bound sampling and
+    explanation kernels run in its shadow.
+
+    ``submit`` returns the call's (imp, hop-1, hop-2) device tensors and the stream they are produced
+    on (a pipeline stream, not the caller's: ``torch.cuda.current_stream().wait_stream(stream)``
+    before using them there); they are overwritten by call k + depth, so consume them first."""
+
+    def __init__(self, explainer, graph, dst_list, N, M=3, B=100, seed=0, split=L.SPLIT_TEST, depth=2):
+        dev = graph.device
+        self.depth = max(1, int(depth))
+        self.pipes = [ExplainPipeline(explainer, graph, dst_list, N, M, B, seed, split) for _ in range(self.depth)]
+        self.streams = [torch.cuda.Stream(device=dev) for _ in range(self.depth)]
+        self._k = 0
+        self._enc_done = None
+
+    def submit(self, src, dst, ts, eidx, event_ids):
+        i = self._k % self.depth
+        p, st = self.pipes[i], self.streams[i]
+        ready = torch.cuda.Event()                      # the inputs, produced on the caller's stream
+        ready.record(torch.cuda.current_stream(st.device))
+        with torch.cuda.stream(st):
+            st.wait_event(ready)
+            p.sample(src, dst, ts, eidx, event_ids)
+            if self._enc_done is not None:
+                st.wait_event(self._enc_done)
+            p.encode(ts)
+            self._enc_done = torch.cuda.Event()
+            self._enc_done.record(st)
+            p.explain()
+        self._k += 1
+        E, N, W = p._E, p.N, p.W
+        return (p.imp[:3 * E * W].view(3, E, W), p.h1[:3 * E * N].view(3, E, N),
+                p.h2[:3 * E * N * N].view(3, E, N * N)), st
+
+    def check_errors(self):
+        for p in self.pipes:
+            p.check_errors()

@@ -424,3 +424,39 @@ def test_pipeline_wide_edge_features_vs_oracle(tm):
             ref = er.forward(sd, nf, ef, h(b.node6[s, sl]), h(b.eid3[s, sl]), h(b.ts3[s, sl]), h(b.cat[s, sl]),
                              ts[sl], h(b.cnt[s, sl]).astype(np.float64))
             np.testing.assert_allclose(h(imp[s, sl]), ref.numpy()[..., 0], rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.parametrize("depth", [2, 3])
+def test_pipelined_explainer_equals_single_stream(tm, depth):
+    """PipelinedExplainer (calls in flight on several streams, encoders chained by events) returns,
+    call for call, exactly what ExplainPipeline returns for the same inputs on one stream."""
+    from tempme_amd.pipeline import ExplainPipeline, PipelinedExplainer
+    from tempme_amd.workload import enron_like, split
+    g = enron_like(n_nodes=120, n_edges=6000, node_feat="uniform", seed=4)
+    (src, dst, ts, eidx), rows, pool = split(g)
+    dev = torch.device("cuda", 0)
+    f = _finder(tm, g["src"][rows], g["dst"][rows], g["eidx"][rows], g["ts"][rows], g["n_nodes"], seed=3)
+    torch.manual_seed(2)
+    ex = tm.TempME(_Base(g["n_feat"], g["e_feat"], dev), "tgn", "x", 40, 64, device=dev,
+                   null_model={k: 1 / 12 for k in range(1, 13)}).to(dev).eval()
+    N, B, E, calls = 20, 50, 150, 5
+    t = lambda a, dt, k: torch.from_numpy(np.ascontiguousarray(a[k * E:(k + 1) * E], dtype=dt)).to(dev)  # noqa: E731
+    ins = [(t(src, np.int32, k), t(dst, np.int32, k), t(ts, np.float64, k), t(eidx, np.int32, k),
+            torch.arange(k * E, (k + 1) * E, dtype=torch.int32, device=dev)) for k in range(calls)]
+    one = ExplainPipeline(ex, f.graph, torch.from_numpy(pool), N, 3, B, seed=3)
+    want = []
+    for x in ins:
+        want.append([o.clone() for o in one.run(*x)])
+    torch.cuda.synchronize()
+    one.check_errors()
+    fl = PipelinedExplainer(ex, f.graph, torch.from_numpy(pool), N, 3, B, seed=3, depth=depth)
+    got = []
+    for x in ins:
+        outs, st = fl.submit(*x)
+        with torch.cuda.stream(st):
+            got.append([o.clone() for o in outs])      # before call k + depth reuses the buffers
+    torch.cuda.synchronize()
+    fl.check_errors()
+    for k in range(calls):
+        for a, b in zip(want[k], got[k]):
+            assert torch.equal(a, b), k
