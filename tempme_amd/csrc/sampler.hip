@@ -776,10 +776,13 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
         else c = find_before_len(g, u, s == 2, a.ts[e], a.eidx ? a.eidx[e] : 0, tid == 0 ? a.err : nullptr);
         uint32_t d = 0xFFFFFFFFu;
         if (c > 0 && tid < N) d = (uint32_t)draw(key, 1, ev, 0, tid, c);
+        // rank among the row's N draws (np.sort order, ties by index): lane k's draw read into a scalar
+        // register (v_readlane, k is wave-uniform) instead of a ds_bpermute round trip per k
+        const uint32_t dkey = keyed ? (d << 6) | (uint32_t)tid : d;   // unique keys: one compare
         int32_t rank = 0;
         for (int k = 0; k < N; ++k) {
-            uint32_t dk = __shfl(d, k, 64);
-            rank += (dk < d) || (k < tid && dk == d);
+            const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)dkey, k);
+            rank += keyed ? (dk < dkey) : ((dk < d) || (k < tid && dk == d));
         }
         if (tid < N) {
             int32_t n_ = 0, e_ = 0;

@@ -460,3 +460,27 @@ def test_pipelined_explainer_equals_single_stream(tm, depth):
     for k in range(calls):
         for a, b in zip(want[k], got[k]):
             assert torch.equal(a, b), k
+
+
+@pytest.mark.parametrize("N,M", [(64, 8), (7, 5), (30, 1), (12, 2)])
+def test_fused_events_sizes_vs_oracle(tm, N, M):
+    """The fused sampler at the largest supported shape (N=64, M=8: W=512 walks per group, edge-count
+    fields at their widest) and at walks-per-slot values outside the specialised M=3 / M=1 kernels,
+    bit-exact vs the C oracle (every sampled field, categories, edge counts, histogram)."""
+    from tempme_amd.preprocess import sample_events
+    g, rows, (src, dst, ts, eidx), pool, f = _pareto_finder(tm, seed=13, alpha=1.2, node_feat="uniform")
+    dev = f.device
+    E = 24
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a[:E], dtype=dt)).to(dev)  # noqa: E731
+    b = sample_events(f.graph, 13, px.SPLIT_TEST, N, M, t(src, np.int32), t(dst, np.int32), t(ts, np.float64),
+                      t(eidx, np.int32), torch.arange(E, dtype=torch.int32, device=dev),
+                      torch.from_numpy(np.asarray(pool, np.int32)).to(dev))
+    og = orc.OracleGraph(g["src"][rows], g["dst"][rows], g["eidx"][rows], g["ts"][rows], g["n_nodes"])
+    o = orc.event_pipeline(og, 13, px.SPLIT_TEST, N, M, src[:E], dst[:E], ts[:E], eidx[:E], np.arange(E), pool, 8)
+    h = lambda x: x.cpu().numpy()  # noqa: E731
+    assert np.array_equal(h(b.dst_fake[:E]), o["dst_fake"])
+    for name in ("node6", "eid3", "ts3", "cat", "sub1_node", "sub1_eid", "sub1_ts", "sub2_node", "sub2_eid",
+                 "sub2_ts"):
+        assert np.array_equal(h(getattr(b, name)).swapaxes(0, 1), o[name]), name
+    assert np.array_equal(h(b.cnt).swapaxes(0, 1).astype(np.int32), o["cnt"])
+    assert np.array_equal(h(b.hist).astype(np.uint64), o["hist"])
