@@ -35,8 +35,10 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
 FP32_MFMA_PEAK_TF = 157.3      # MI355X_MICROARCH.md: FP32 matrix (spec)
 
 
-def flops_model(de, dn, h, N, M):
-    """Algorithmic MACs per unit for each encoder kernel."""
+def flops_model(de, dn, h, N, M, etab=False):
+    """Algorithmic MACs per unit for each encoder kernel.  ``etab``: the
+    pipeline's edge table (lin_event's de x dn edge part once per edge id in the gate-table launch,
+    not per executed walk position)."""
     kev = de + 3 + dn
     per_pos_gcn = kev * dn + 2 * (dn * h + h * h)                       # lin_event + event_gcn MLP x2
     per_walk_head = 3 * (2 * h) ** 2 + (2 * h) * h + h * h + (h + 12) ** 2 + (h + 12) * h + h + 2 * 2 * h
@@ -47,9 +49,11 @@ def flops_model(de, dn, h, N, M):
     qt = (de + 3 + 15) // 16
     exec_walk = 2 * ((2 + 1.0 / M) * per_pos_gcn + per_walk_head - (1 - 1.0 / M) * (2 * h) ** 2
                      - max(kev - 16 * qt, 0) * dn / M)
+    if etab:
+        exec_walk -= 2 * (2 + 1.0 / M) * de * dn
     return dict(gcn_kernel=2 * per_pos_gcn * 3, head_kernel=2 * per_walk_head, explain_kernel=2 * per_pos_gate * 3,
                 walk_kernel=2 * (3 * per_pos_gcn + per_walk_head), walk_kernel_executed=exec_walk,
-                gate_per_edge=2 * per_pos_gate,
+                gate_per_edge=2 * per_pos_gate + (2 * de * dn if etab else 0),
                 per_walk=2 * (3 * per_pos_gcn + per_walk_head + 3 * per_pos_gate), W=W)
 
 
@@ -158,6 +162,8 @@ def main():
     ap.add_argument("--alpha", type=float, default=1.2)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-edge-table", action="store_true",
+                    help="lin_event's edge-feature product per walk position instead of per edge id")
     ap.add_argument("--streams", type=int, default=1,
                     help="steps in flight (PipelinedExplainer): step k runs on stream k %% S with its own "
                          "buffers, so its sampling and explanation kernels overlap the neighbouring steps' "
@@ -223,13 +229,15 @@ def main():
                    null_model={k: 1.0 / 12 for k in range(1, 13)}).to(dev).eval()
     S = max(1, args.streams)
     if S == 1:
-        pipe = ExplainPipeline(ex, finder.graph, torch.from_numpy(pool), N, M, B, seed=args.seed)
+        pipe = ExplainPipeline(ex, finder.graph, torch.from_numpy(pool), N, M, B, seed=args.seed,
+                               edge_table=not args.no_edge_table)
         pipes = [pipe]
 
         def run_step(k):
             pipe.run(*inputs[k])
     else:
-        flight = PipelinedExplainer(ex, finder.graph, torch.from_numpy(pool), N, M, B, seed=args.seed, depth=S)
+        flight = PipelinedExplainer(ex, finder.graph, torch.from_numpy(pool), N, M, B, seed=args.seed, depth=S,
+                                    edge_table=not args.no_edge_table)
         pipes = flight.pipes
         pipe = pipes[0]
 
@@ -269,7 +277,7 @@ def main():
     el = max_over_ranks(el, dist, dev if backend == "nccl" else "cpu")
 
     if rank == 0:
-        fm = flops_model(g["e_feat"].shape[1], g["n_feat"].shape[1], 64, N, M)
+        fm = flops_model(g["e_feat"].shape[1], g["n_feat"].shape[1], 64, N, M, etab=pipe.etab is not None)
         W = fm["W"]
         units = {"events_kernel": ("hbm", sampling_bytes_per_event(N, M) * E),
                  "gcn_kernel": ("mfma", fm["gcn_kernel"] * 3 * E * W),

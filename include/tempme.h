@@ -146,6 +146,17 @@ int tm_encoder_fwd(const tm_weights *w, const float *n_feat, const float *e_feat
                    const int32_t *cat, const double *cut, const float *cnt, void *workspace, float *out_imp,
                    void *stream);
 
+/* tm_encoder_fwd with lin_event's edge-feature product taken from a per-edge-id table (etab from
+ * tm_edge_tables, [n_ids][tm_edge_table_cols] f32; every eid3 entry must be < n_ids): the
+ * event_conv linear (explainer_new.py:79-96) over [E(e) | cnt | cos] is split as
+ * W[:, :de] E(e) (table) + W[:, de:] [cnt | cos] (walk kernel), a re-association of the same sum
+ * (outputs within the 1e-5 contract, not bit-identical to tm_encoder_fwd).  etab = NULL is
+ * tm_encoder_fwd; TM_E_UNSUPPORTED if the encoder dims have no table mode (tm_edge_table_cols == 0). */
+int tm_encoder_fwd_tab(const tm_weights *w, const float *n_feat, const float *e_feat, const float *etab,
+                       int32_t n_groups, int32_t B, int32_t W, int32_t M, const int32_t *node6, const int32_t *eid3,
+                       const float *ts3, const int32_t *cat, const double *cut, const float *cnt, void *workspace,
+                       float *out_imp, void *stream);
+
 /* ---------------------------------------------------------------- encoder training (device)
  * Training forward of TempME.forward (explainer_new.py:174-201) with dropout active: drop (nullable
  * = eval) holds uint8 keep-masks [n_walks][144]: columns 0..1 the attention weights alpha (:839),
@@ -264,6 +275,15 @@ int tm_edge_importance(const tm_weights *w, const float *e_feat, int32_t n_group
  * t_e the edge's timestamp in g (as f32).  TM_E_UNSUPPORTED if an edge id carries several
  * timestamps in g (then use tm_edge_importance). */
 int tm_edge_gate_table(const tm_weights *w, const tm_graph *g, const float *e_feat, float *out_gf, void *stream);
+
+/* Row width of the walk kernel's edge table for these encoder dims (176), or 0 if it has none. */
+int tm_edge_table_cols(const tm_weights *w);
+
+/* tm_edge_gate_table plus (out_etab non-NULL) the edge table of tm_encoder_fwd_tab, in one launch
+ * over the edge ids [0, max_eid]: out_etab[e][k] = sum_{j < de} lin_event.W[k][j] * e_feat[e][j]
+ * (k < dn; columns dn..cols-1 are 0).  out_etab [max_eid + 1][tm_edge_table_cols(w)]. */
+int tm_edge_tables(const tm_weights *w, const tm_graph *g, const float *e_feat, float *out_gf, float *out_etab,
+                   void *stream);
 
 /* tm_edge_importance driven by a gate table (n_ids entries): bit-identical outputs, no per-walk
  * gate MLP.  *err_flag (nullable) is set if a walk edge id is outside the table. */

@@ -415,11 +415,12 @@ __device__ __forceinline__ float4 wload(__amdgpu_buffer_rsrc_t r, int vo, int f4
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, f4 * 16, 0));
 }
 
-template <int NTO, int NQ>
+// NQL = the pack's K steps (L.nq); NQ <= NQL of them are multiplied (the leading ones)
+template <int NTO, int NQ, int NQL = NQ>
 __device__ __forceinline__ void rgemm(const Lin &L, const floatx4 (&x)[NQ], floatx4 (&o)[NTO]) {
     const auto wr = wrsrc(L.w);
     const int vo = lane_id() * 16;
-    constexpr int nq = NQ;   // == L.nq: fragment offsets are immediates
+    constexpr int nq = NQL;   // == L.nq: fragment offsets are immediates
     constexpr int N = NTO * NQ, D = PF < N ? PF : N;
 #pragma unroll
     for (int t = 0; t < NTO; ++t) o[t] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -530,6 +531,7 @@ struct WalkArgs {
     const float *ts3, *cnt, *stdv;
     const double *cut;
     float *out;
+    const float *etab;    // [n_ids][16*NTD] lin_event's edge-feature part per edge id (walk_kernel Q0 > 0)
 };
 
 // Phase timing (debug builds only, -DTM_STAMPS; tools_stamps.py): s_memtime deltas of lane 0 per
@@ -593,7 +595,7 @@ __device__ __forceinline__ void load_ef(const WalkArgs &a, int32_t e, float (&ef
 }
 
 // K step q of the event features x[k] = [E(e) | cnt | cos(dt * w + phi)] (:176-179, TimeEncode :45-59)
-template <int NQE, int NTD>
+template <int NQE, int NTD, bool ETAB = false>
 __device__ __forceinline__ floatx4 gen_x(int q, const float *cs, const float (&ef)[EQ_MAX][4], int g, int de, int kev,
                                          float dt, float c0, float c1, float c2) {
     using C = WalkConsts<NQE, NTD>;
@@ -605,11 +607,11 @@ __device__ __forceinline__ floatx4 gen_x(int q, const float *cs, const float (&e
     for (int s = 0; s < 4; ++s) {
         const int k = 16 * q + 4 * g + s;
         float v;
-        if (16 * q + 16 <= de) v = ef[qe][s];
+        if (!ETAB && 16 * q + 16 <= de) v = ef[qe][s];
         else {
             v = (k < kev) ? time_cos(dt, wv[s], pv[s]) : 0.f;
             if (k < de + 3) v = (k == de) ? c0 : (k == de + 1) ? c1 : c2;
-            if (k < de) v = ef[qe][s];
+            if (k < de) v = ETAB ? 0.f : ef[qe][s];      // table mode: the edge part comes from etab
         }
         xq[s] = v;
     }
@@ -647,6 +649,19 @@ __device__ __forceinline__ float4 ef_step(const float4 *erow4, int q, int g, int
     return i < n4 ? v : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+// table mode: this lane's 4 features of each of the 11 output tiles of edge e's table row (loaded a
+// pass ahead, as load_ef does for the plain mode's edge features)
+#define ETAB_N(q0) ((q0) > 0 ? 11 : 1)
+template <int Q0>
+__device__ __forceinline__ void load_et(const WalkArgs &a, int32_t e, float4 (&et)[ETAB_N(Q0)]) {
+    if constexpr (Q0 > 0) {
+        const float4 *trow = reinterpret_cast<const float4 *>(a.etab + (int64_t)e * 176);
+        const int g = lane_id() >> 4;
+#pragma unroll
+        for (int t = 0; t < 11; ++t) et[t] = trow[4 * t + g];
+    }
+}
+
 // one walk position for the 16 columns of this wave -> F = [U_s | U_t] (8 tiles, B layout).
 // lin_event runs K-outer ((q, t) fragment order): the event features of K step q+1 are generated
 // while step q's MFMAs run and only L and two x fragments are live.  Node-feature rows are float4
@@ -654,10 +669,15 @@ __device__ __forceinline__ float4 ef_step(const float4 *erow4, int q, int g, int
 // GEMM keeps 88 more registers live and costs the second wave per SIMD).
 // SEF (streamed edge features, EQ_MAX*16 < de <= 176): ef holds K steps 0 and 1 (loaded during the
 // previous pass); step q + 2's float4 is loaded while step q's MFMAs run.
-template <int NQE, int NTD, bool SEF>
+// Q0 > 0 (edge table): K steps < Q0 hold only edge features, whose product with lin_event's weights
+// is the per-edge-id row etab[e] (computed once per call with the gate table); the loop starts at
+// step Q0 with the edge lanes of step Q0 zeroed, and the epilogue adds the row.
+template <int NQE, int NTD, bool SEF, int Q0 = 0>
 __device__ __forceinline__ void encode_position(const WalkArgs &a, const float *cs, const PosIn &pi,
-                                                const float (&ef)[EQ_MAX][4], int p, floatx4 (&F)[8],
-                                                unsigned long long (&T)[10]) {
+                                                const float (&ef)[EQ_MAX][4], const float4 (&et)[ETAB_N(Q0)], int p,
+                                                floatx4 (&F)[8], unsigned long long (&T)[10]) {
+    constexpr bool ETAB = Q0 > 0;
+    static_assert(!(ETAB && SEF), "table mode replaces the streamed edge features");
     using C = WalkConsts<NQE, NTD>;
     const EncW &P = a.P;
     const int g = lane_id() >> 4;
@@ -675,10 +695,10 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, const float *
         const auto wr = wrsrc(P.ev.w);
         const int vo = lane_id() * 16;
         constexpr int nq = NQE;
-        constexpr int N = NTD * NQE, D = PF;
+        constexpr int N = NTD * (NQE - Q0), D = PF;
         float4 buf[D];
 #pragma unroll
-        for (int i = 0; i < D; ++i) buf[i] = wload(wr, vo, ((i % NTD) * nq + i / NTD) * 64);
+        for (int i = 0; i < D; ++i) buf[i] = wload(wr, vo, ((i % NTD) * nq + Q0 + i / NTD) * 64);
         const float4 *erow4 = reinterpret_cast<const float4 *>(a.e_feat + (int64_t)pi.e * de);
         float4 ring[2];
         if constexpr (SEF) {
@@ -686,10 +706,10 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, const float *
             ring[1] = make_float4(ef[1][0], ef[1][1], ef[1][2], ef[1][3]);
         }
         floatx4 xq = SEF ? gen_x_s<NQE, NTD>(0, cs, ring[0], g, de, kev, dt, c0, c1, c2)
-                         : gen_x<NQE, NTD>(0, cs, ef, g, de, kev, dt, c0, c1, c2);
+                         : gen_x<NQE, NTD, ETAB>(Q0, cs, ef, g, de, kev, dt, c0, c1, c2);
         const int qend = p == 2 ? P.qt : NQE;            // slot pass: steps >= qt folded into evc
 #pragma unroll
-        for (int q = 0; q < NQE; ++q) {
+        for (int q = Q0; q < NQE; ++q) {
             if (q < qend) {                               // wave-uniform (a break would stop the unrolling)
                 floatx4 xn = xq;
                 float4 e2 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -697,13 +717,13 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, const float *
                     if (q + 2 < NQE && 16 * (q + 2) < de) e2 = ef_step(erow4, q + 2, g, de);
                     if (q + 1 < NQE) xn = gen_x_s<NQE, NTD>(q + 1, cs, ring[(q + 1) & 1], g, de, kev, dt, c0, c1, c2);
                 } else {
-                    if (q + 1 < NQE) xn = gen_x<NQE, NTD>(q + 1, cs, ef, g, de, kev, dt, c0, c1, c2);
+                    if (q + 1 < NQE) xn = gen_x<NQE, NTD, ETAB>(q + 1, cs, ef, g, de, kev, dt, c0, c1, c2);
                 }
 #pragma unroll
                 for (int t = 0; t < NTD; ++t) {
-                    const int i = q * NTD + t;
+                    const int i = (q - Q0) * NTD + t;
                     const float4 w = buf[i % D];
-                    if (i + D < N) buf[i % D] = wload(wr, vo, (((i + D) % NTD) * nq + (i + D) / NTD) * 64);
+                    if (i + D < N) buf[i % D] = wload(wr, vo, (((i + D) % NTD) * nq + Q0 + (i + D) / NTD) * 64);
                     L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, xq.x, L[t], 0, 0, 0);
                     L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, xq.y, L[t], 0, 0, 0);
                     L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, xq.z, L[t], 0, 0, 0);
@@ -721,7 +741,13 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, const float *
 #pragma unroll
     for (int t = 0; t < NTD; ++t) {
         const float4 b = lds4(cs + (p == 2 ? C::EVC : C::EV), t);
-        const float bv[4] = {b.x, b.y, b.z, b.w};
+        float bv[4] = {b.x, b.y, b.z, b.w};
+        if constexpr (ETAB) {
+            bv[0] += et[t].x;
+            bv[1] += et[t].y;
+            bv[2] += et[t].z;
+            bv[3] += et[t].w;
+        }
         // tiles below the last are inside the row (dispatch: 160 < dn <= 176), so their offsets are
         // immediates on one row address; the last tile's index is clamped and masked below
         const int f4 = (t < NTD - 1) ? 4 * t + g : min(4 * t + g, dn / 4 - 1);
@@ -839,7 +865,7 @@ __device__ __forceinline__ void walk_head(const WalkArgs &a, const float *cs, in
     if (valid && g == 0) a.out[gw] = 1.f / (1.f + expf(-z));
 }
 
-template <int NQE, int NTD, bool SEF = false>
+template <int NQE, int NTD, bool SEF = false, int QE0 = 0>
 __global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
     using C = WalkConsts<NQE, NTD>;
     const EncW &P = a.P;
@@ -863,8 +889,10 @@ __global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
     floatx4 Q0[8];                                      // W2(position 0), carried to the position-1 pass
     const int n_pass = 1 + 2 * a.M;
     PosIn cur = load_pos(a, eg * a.W + (int64_t)j * a.M, 2, valid);
-    float ef[EQ_MAX][4];
-    load_ef(a, cur.e, ef);
+    float ef[EQ_MAX][4] = {};
+    float4 et[ETAB_N(QE0)];
+    if constexpr (QE0 == 0) load_ef(a, cur.e, ef);
+    else load_et<QE0>(a, cur.e, et);
     // pass 0: position 2 once per slot (walk j*M carries it); then per walk m: position 0, position 1
 #pragma nounroll
     for (int pass = 0; pass < n_pass; ++pass) {
@@ -886,8 +914,9 @@ __global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
         floatx4 F[8];
         unsigned long long T[10];
         TM_STAMP(0);
-        encode_position<NQE, NTD, SEF>(a, cs, cur, ef, p, F, T);
-        load_ef(a, nxt.e, ef);
+        encode_position<NQE, NTD, SEF, QE0>(a, cs, cur, ef, et, p, F, T);
+        if constexpr (QE0 == 0) load_ef(a, nxt.e, ef);
+        else load_et<QE0>(a, nxt.e, et);
         cur = nxt;
         floatx4 Y[8];
         TM_STAMP(6);
@@ -961,9 +990,13 @@ __global__ void __launch_bounds__(256) gate_table_kernel(EncW P, int32_t n_ids, 
 // Register-resident gate table: one wave = 16 edge ids (MFMA columns), the gate MLP's weights as the
 // A operand (walk_kernel's layout), X = [E[e] | cos(t_e w + phi)] generated straight into the B
 // fragments, G1 -> G2 -> logit chained in registers.  NQ = K steps of X (de + dn rounded up / 16).
-template <int NQ>
+// NQX > 0: the same edge-feature fragments also give the walk kernel's edge table, etab[e] =
+// lin_event.W[:, :de] . E[e] (16 * 11 features, no bias), from lin_event's pack (NQL K steps): the
+// first NQX K steps with the lanes past de zeroed.
+template <int NQ, int NQX = 0, int NQL = 1>
 __global__ void __launch_bounds__(256) gate_reg_kernel(EncW P, int32_t n_ids, const double *__restrict__ ets,
-                                                       const float *__restrict__ e_feat, float *__restrict__ gf) {
+                                                       const float *__restrict__ e_feat, float *__restrict__ gf,
+                                                       float *__restrict__ etab = nullptr) {
     const int lane = threadIdx.x & 63, col = lane & 15, g = lane_id() >> 4;
     const int64_t e = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + col;
     if (((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 >= n_ids) return;   // wave-uniform
@@ -987,6 +1020,20 @@ __global__ void __launch_bounds__(256) gate_reg_kernel(EncW P, int32_t n_ids, co
                 else if (k < kdep) v = time_cos(t, P.freq[k - de], P.phase[k - de]);
                 X[q][s] = v;
             }
+        }
+    }
+    if constexpr (NQX > 0) {
+        floatx4 XE[NQX], ET[11];
+#pragma unroll
+        for (int q = 0; q < NQX; ++q) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) XE[q][s] = (16 * q + 4 * g + s < de) ? X[q][s] : 0.f;
+        }
+        rgemm<11, NQX, NQL>(P.ev, XE, ET);
+        if (valid) {
+            float4 *row = reinterpret_cast<float4 *>(etab + e * 176);
+#pragma unroll
+            for (int t = 0; t < 11; ++t) row[4 * t + g] = make_float4(ET[t][0], ET[t][1], ET[t][2], ET[t][3]);
         }
     }
     floatx4 G1[4];
@@ -1184,16 +1231,45 @@ static size_t gate_lds(const EncW &P) {
     return sizeof(float) * (TILE_ROWS * (r16(P.kdep) + 8) + TILE_ROWS * (HID + 8) + TILE_ROWS * (HID / 2 + 8));
 }
 
+// lin_event's K steps before the first one holding a count or time feature (= de / 16), when the
+// fused walk kernel has a table-mode instance for these dims (de = 32..47 with 11..14 K steps, as
+// Enron's 32; de = 160..175 with 21..22, as BASELINE configs[4]'s 172), else 0
+static int etab_q0(const EncW &P) {
+    const int nqe = r16(P.kev) / 16, ntd = r16(P.dn) / 16, q0 = P.de / 16;
+    if (ntd != 11 || P.dn % 4 || P.ev.nt != 11 || P.ev.nq != nqe || P.d1.nt != 4 || P.d2.nq != 4 || P.d2.nt != 2)
+        return 0;
+    if (q0 == 2 && nqe >= 11 && nqe <= 14 && P.d1.nq == 13) return 2;
+    if (q0 == 10 && (nqe == 21 || nqe == 22) && P.d1.nq == 22) return 10;
+    return 0;
+}
+
+extern "C" int tm_edge_table_cols(const tm_weights *w) { return (w && etab_q0(w->P) > 0) ? 176 : 0; }
+
 extern "C" int tm_edge_gate_table(const tm_weights *w, const tm_graph *g, const float *e_feat, float *out_gf,
                                   void *stream) {
-    if (!w || !g || !e_feat || !out_gf) return fail(TM_E_ARG, "tm_edge_gate_table: bad arguments");
+    return tm_edge_tables(w, g, e_feat, out_gf, nullptr, stream);
+}
+
+extern "C" int tm_edge_tables(const tm_weights *w, const tm_graph *g, const float *e_feat, float *out_gf,
+                              float *out_etab, void *stream) {
+    if (!w || !g || !e_feat || !out_gf) return fail(TM_E_ARG, "tm_edge_tables: bad arguments");
+    const int q0 = etab_q0(w->P);
+    if (out_etab && q0 == 0) return fail(TM_E_UNSUPPORTED, "tm_edge_tables: no edge table for these encoder dims");
     if (!g->d.ts_unique)
         return fail(TM_E_UNSUPPORTED, "tm_edge_gate_table: an edge id carries several timestamps; use tm_edge_importance");
     const int32_t n = g->d.max_eid + 1;
     hipEvent_t pe = prof_begin(S_(stream));
     const int nq = w->P.d1.nq;
     const unsigned rblocks = (unsigned)((n + 63) / 64);
-    if (w->P.d2.nq == 4 && w->P.d1.nt == 4 && w->P.d2.nt == 2) {   // hid_dim 64: register-resident path
+    if (out_etab) {   // one launch: gate table and edge table from the same edge-feature fragments
+        const int nqe = w->P.ev.nq;
+        if (q0 == 2 && nqe == 11) gate_reg_kernel<13, 3, 11><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf, out_etab);
+        else if (q0 == 2 && nqe == 12) gate_reg_kernel<13, 3, 12><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf, out_etab);
+        else if (q0 == 2 && nqe == 13) gate_reg_kernel<13, 3, 13><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf, out_etab);
+        else if (q0 == 2) gate_reg_kernel<13, 3, 14><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf, out_etab);
+        else if (nqe == 21) gate_reg_kernel<22, 11, 21><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf, out_etab);
+        else gate_reg_kernel<22, 11, 22><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf, out_etab);
+    } else if (w->P.d2.nq == 4 && w->P.d1.nt == 4 && w->P.d2.nt == 2) {   // hid_dim 64: register-resident path
         if (nq == 11) gate_reg_kernel<11><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf);
         else if (nq == 12) gate_reg_kernel<12><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf);
         else if (nq == 13) gate_reg_kernel<13><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf);
@@ -1236,15 +1312,23 @@ static size_t gcn_lds(const EncW &P) {
 }
 static size_t head_lds() { return sizeof(float) * (4 * TILE_ROWS * (2 * HID + 8)); }
 
-template <int NQE, bool SEF = false>
+template <int NQE, bool SEF = false, int Q0 = 0>
 static void launch_walk(const WalkArgs &a, unsigned blocks, hipStream_t s) {
-    walk_kernel<NQE, 11, SEF><<<dim3(blocks), 256, 0, s>>>(a);
+    walk_kernel<NQE, 11, SEF, Q0><<<dim3(blocks), 256, 0, s>>>(a);
 }
 
 extern "C" int tm_encoder_fwd(const tm_weights *w, const float *n_feat, const float *e_feat, int32_t n_groups,
                               int32_t B, int32_t W, int32_t M, const int32_t *node6, const int32_t *eid3,
                               const float *ts3, const int32_t *cat, const double *cut, const float *cnt,
                               void *workspace, float *out_imp, void *stream) {
+    return tm_encoder_fwd_tab(w, n_feat, e_feat, nullptr, n_groups, B, W, M, node6, eid3, ts3, cat, cut, cnt,
+                              workspace, out_imp, stream);
+}
+
+extern "C" int tm_encoder_fwd_tab(const tm_weights *w, const float *n_feat, const float *e_feat, const float *etab,
+                                  int32_t n_groups, int32_t B, int32_t W, int32_t M, const int32_t *node6,
+                                  const int32_t *eid3, const float *ts3, const int32_t *cat, const double *cut,
+                                  const float *cnt, void *workspace, float *out_imp, void *stream) {
     if (!w || n_groups < 0 || B < 0 || W < 0 || M <= 0) return fail(TM_E_ARG, "tm_encoder_fwd: bad arguments");
     if (W % M) return fail(TM_E_SHAPE, "tm_encoder_fwd: W must be a multiple of M (walks per hop-1 slot)");
     const int64_t n_walks = (int64_t)n_groups * B * W;
@@ -1261,6 +1345,7 @@ extern "C" int tm_encoder_fwd(const tm_weights *w, const float *n_feat, const fl
     std_kernel<<<dim3(n_groups), 256, 0, s>>>(B, W, cut, ts3, stdv);
     TM_CHECK_LAUNCH();
     prof_end("std_kernel", s, pe);
+    if (etab && etab_q0(P) == 0) return fail(TM_E_UNSUPPORTED, "tm_encoder_fwd_tab: no edge table for these dims");
     const int nqe = r16(P.kev) / 16, ntd = r16(P.dn) / 16;
     const bool narrow = nqe >= 11 && nqe <= 14 && P.de <= 16 * EQ_MAX;
     // wide edge features (e.g. BASELINE configs[4]: de = dn = 172): streamed per K step
@@ -1269,10 +1354,19 @@ extern "C" int tm_encoder_fwd(const tm_weights *w, const float *n_feat, const fl
         // fused register-resident path
         const int64_t n_slots = n_walks / M;
         const int64_t units = (n_slots + 15) / 16;
-        WalkArgs a{P, n_slots, W, M, B * W, n_feat, e_feat, node6, eid3, cat, ts3, cnt, stdv, cut, out_imp};
+        WalkArgs a{P, n_slots, W, M, B * W, n_feat, e_feat, node6, eid3, cat, ts3, cnt, stdv, cut, out_imp, etab};
         const unsigned blocks = (unsigned)((units + 3) / 4);
+        const int q0 = etab ? etab_q0(P) : 0;
         pe = prof_begin(s);
-        if (wide) {
+        if (q0 == 2) {        // edge table: lin_event from K step 2
+            if (nqe == 11) launch_walk<11, false, 2>(a, blocks, s);
+            else if (nqe == 12) launch_walk<12, false, 2>(a, blocks, s);
+            else if (nqe == 13) launch_walk<13, false, 2>(a, blocks, s);
+            else launch_walk<14, false, 2>(a, blocks, s);
+        } else if (q0 == 10) {   // edge table: lin_event from K step 10 (no streamed edge features)
+            if (nqe == 21) launch_walk<21, false, 10>(a, blocks, s);
+            else launch_walk<22, false, 10>(a, blocks, s);
+        } else if (wide) {
             if (nqe == 21) launch_walk<21, true>(a, blocks, s);
             else launch_walk<22, true>(a, blocks, s);
         } else if (nqe == 11) launch_walk<11>(a, blocks, s);

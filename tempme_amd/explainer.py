@@ -196,9 +196,11 @@ class TempME(nn.Module):
             self._tables_key = key
         return self._n_tab, self._e_tab
 
-    def encoder_fwd(self, node6, eid3, ts3, cat, cut, cnt, n_groups, B, W, out=None, workspace=None, M=1):
+    def encoder_fwd(self, node6, eid3, ts3, cat, cut, cnt, n_groups, B, W, out=None, workspace=None, M=1,
+                    etab=None):
         """tm_encoder_fwd on device tensors (int32 node6 [G,B,W,6], eid3, f32 ts3, int32 cat [G,B,W],
-        f64 cut [G,B], f32 cnt [G,B,W,3,3]) -> f32 [G,B,W]."""
+        f64 cut [G,B], f32 cnt [G,B,W,3,3]) -> f32 [G,B,W].  ``etab``: the per-edge-id table of
+        tm_edge_tables (tm_encoder_fwd_tab: lin_event's edge-feature product read, not recomputed)."""
         dev = self._dev()
         nt, et = self.feature_tables()
         n_walks = n_groups * B * W
@@ -207,9 +209,10 @@ class TempME(nn.Module):
         if workspace is None:
             nbytes = L.lib().tm_encoder_workspace_bytes(self.packed_weights(), n_walks)
             workspace = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        L.check(L.lib().tm_encoder_fwd(self.packed_weights(), L.ptr(nt), L.ptr(et), n_groups, B, W, M, L.ptr(node6),
-                                       L.ptr(eid3), L.ptr(ts3), L.ptr(cat), L.ptr(cut), L.ptr(cnt),
-                                       L.ptr(workspace), L.ptr(out), L.stream_ptr(dev)), "TempME.forward")
+        L.check(L.lib().tm_encoder_fwd_tab(self.packed_weights(), L.ptr(nt), L.ptr(et),
+                                           None if etab is None else L.ptr(etab), n_groups, B, W, M, L.ptr(node6),
+                                           L.ptr(eid3), L.ptr(ts3), L.ptr(cat), L.ptr(cut), L.ptr(cnt),
+                                           L.ptr(workspace), L.ptr(out), L.stream_ptr(dev)), "TempME.forward")
         return out
 
     def edge_importance(self, eid3, ts3, imp, s1n, s1e, s2n, s2e, n_groups, B, W, N, out1=None, out2=None):

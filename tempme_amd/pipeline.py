@@ -4,9 +4,10 @@ One call = what temp_exp_main.py's eval loop does per batch for ``E / B`` batche
 ``B`` events (sampling as data_preprocess.py:106-134, TempME.forward x3,
 retrieve_explanation(training=False)), without host round trips:
 
-    tm_sample_events   fake dst, 2-hop subgraphs x3, walks x3, categories, edge counts
-    tm_encoder_fwd     graphlet importance for the 3 * E/B groups (one std per group)
-    tm_edge_importance explanation weights hop-1 [3, E, N] and hop-2 [3, E, N^2]
+    tm_sample_events        fake dst, 2-hop subgraphs x3, walks x3, categories, edge counts
+    tm_edge_tables          per edge id: the dependency gate and lin_event's edge-feature product
+    tm_encoder_fwd_tab      graphlet importance for the 3 * E/B groups (one std per group)
+    tm_edge_importance_tab  explanation weights hop-1 [3, E, N] and hop-2 [3, E, N^2]
 
 Outputs are side-major: rows [s, b*B:(b+1)*B] of batch b are the reference's
 ``retrieve_explanation`` rows [s*B:(s+1)*B].
@@ -18,8 +19,12 @@ from .preprocess import EventBuffers, sample_events
 
 
 class ExplainPipeline:
-    def __init__(self, explainer, graph, dst_list, N, M=3, B=100, seed=0, split=L.SPLIT_TEST):
+    def __init__(self, explainer, graph, dst_list, N, M=3, B=100, seed=0, split=L.SPLIT_TEST, edge_table=True):
+        """``edge_table=False`` keeps lin_event's edge-feature product inside the walk kernel
+        (tm_encoder_fwd, bit-identical to the drop-in TempME.forward) instead of reading it from the
+        per-edge-id table (a re-association of the same sum, within the 1e-5 contract)."""
         self.ex = explainer
+        self.edge_table = bool(edge_table)
         self.graph = graph
         self.dev = graph.device
         self.dst_list = dst_list.to(self.dev, torch.int32).contiguous()
@@ -39,6 +44,8 @@ class ExplainPipeline:
         self.h1 = torch.empty(max(3 * E * N, 1), dtype=torch.float32, device=dev)
         self.h2 = torch.empty(max(3 * E * N * N, 1), dtype=torch.float32, device=dev)
         self.gf = torch.empty(self.graph.max_eid + 1, dtype=torch.float32, device=dev)
+        cols = L.lib().tm_edge_table_cols(self.ex.packed_weights()) if self.edge_table else 0
+        self.etab = torch.empty((self.graph.max_eid + 1, cols), dtype=torch.float32, device=dev) if cols else None
         self._E = E
 
     def sample(self, src, dst, ts, eidx, event_ids):
@@ -53,19 +60,24 @@ class ExplainPipeline:
         b = self.buf
         cut = ts.repeat(3).contiguous()
         self.ex.encoder_fwd(b.node6, b.eid3, b.ts3, b.cat, cut, b.cnt, G, B, W, out=self.imp, workspace=self.ws,
-                            M=self.M)
+                            M=self.M, etab=self.etab)
         return self.imp
 
+    def tables(self):
+        """Once per call, per edge id of the graph: the dependency gate (retrieve_edge_imp_node's
+        depMLP, explainer_new.py:367-386) and, when the encoder has a table mode, lin_event's
+        edge-feature product (event_gcn, :79-96) -- one launch, the edge features read once."""
+        _, et = self.ex.feature_tables()
+        L.check(L.lib().tm_edge_tables(self.ex.packed_weights(), self.graph.handle, L.ptr(et), L.ptr(self.gf),
+                                       L.ptr(self.etab), L.stream_ptr(self.dev)), "tm_edge_tables")
+
     def explain(self):
-        """retrieve_explanation(training=False) for all groups: per-edge gate table (once per call),
-        then the table-driven scatter-max / gather / Beta-mean / mask kernel."""
+        """retrieve_explanation(training=False) for all groups: the table-driven scatter-max / gather /
+        Beta-mean / mask kernel (gate table from ``tables``)."""
         E, B, W, N = self._E, self.B, self.W, self.N
         G = 3 * (E // B)
         b = self.buf
         dev = self.dev
-        _, et = self.ex.feature_tables()
-        L.check(L.lib().tm_edge_gate_table(self.ex.packed_weights(), self.graph.handle, L.ptr(et), L.ptr(self.gf),
-                                           L.stream_ptr(dev)), "tm_edge_gate_table")
         L.check(L.lib().tm_edge_importance_tab(L.ptr(self.gf), self.gf.numel(), G, B, W, N, L.ptr(b.eid3),
                                                L.ptr(self.imp), L.ptr(b.sub1_node), L.ptr(b.sub1_eid),
                                                L.ptr(b.sub2_node), L.ptr(b.sub2_eid), L.ptr(self.h1), L.ptr(self.h2),
@@ -75,6 +87,7 @@ class ExplainPipeline:
     def run(self, src, dst, ts, eidx, event_ids):
         """Returns (imp [3,E,W], hop-1 weights [3,E,N], hop-2 weights [3,E,N^2]) device tensors."""
         self.sample(src, dst, ts, eidx, event_ids)
+        self.tables()
         self.encode(ts)
         self.explain()
         E, N, W = self._E, self.N, self.W
@@ -98,10 +111,12 @@ class PipelinedExplainer:
     on (a pipeline stream, not the caller's: ``torch.cuda.current_stream().wait_stream(stream)``
     before using them there); they are overwritten by call k + depth, so consume them first."""
 
-    def __init__(self, explainer, graph, dst_list, N, M=3, B=100, seed=0, split=L.SPLIT_TEST, depth=2):
+    def __init__(self, explainer, graph, dst_list, N, M=3, B=100, seed=0, split=L.SPLIT_TEST, depth=2,
+                 edge_table=True):
         dev = graph.device
         self.depth = max(1, int(depth))
-        self.pipes = [ExplainPipeline(explainer, graph, dst_list, N, M, B, seed, split) for _ in range(self.depth)]
+        self.pipes = [ExplainPipeline(explainer, graph, dst_list, N, M, B, seed, split, edge_table)
+                      for _ in range(self.depth)]
         self.streams = [torch.cuda.Stream(device=dev) for _ in range(self.depth)]
         self._k = 0
         self._enc_done = None
@@ -114,6 +129,7 @@ class PipelinedExplainer:
         with torch.cuda.stream(st):
             st.wait_event(ready)
             p.sample(src, dst, ts, eidx, event_ids)
+            p.tables()
             if self._enc_done is not None:
                 st.wait_event(self._enc_done)
             p.encode(ts)

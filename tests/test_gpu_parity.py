@@ -484,3 +484,42 @@ def test_fused_events_sizes_vs_oracle(tm, N, M):
         assert np.array_equal(h(getattr(b, name)).swapaxes(0, 1), o[name]), name
     assert np.array_equal(h(b.cnt).swapaxes(0, 1).astype(np.int32), o["cnt"])
     assert np.array_equal(h(b.hist).astype(np.uint64), o["hist"])
+
+
+@pytest.mark.parametrize("de", [32, 172])
+def test_edge_table_path(tm, de):
+    """tm_edge_tables' edge table = lin_event.W[:, :de] E[e] (fp64 reference, 1e-5), zero past dn;
+    the pipeline's table mode (lin_event's edge part read per edge id) agrees with the per-walk
+    product (edge_table=False, the drop-in TempME.forward arithmetic) within the 1e-5 contract, and
+    its gate table is unchanged."""
+    from tempme_amd.pipeline import ExplainPipeline
+    from tempme_amd.workload import enron_like, split
+    g = enron_like(n_nodes=150, n_edges=5000, alpha=1.5, de=de, dn=172, node_feat="uniform", seed=21)
+    (src, dst, ts, eidx), rows, pool = split(g)
+    dev = torch.device("cuda", 0)
+    f = _finder(tm, g["src"][rows], g["dst"][rows], g["eidx"][rows], g["ts"][rows], g["n_nodes"], seed=6)
+    torch.manual_seed(3)
+    ex = tm.TempME(_Base(g["n_feat"], g["e_feat"], dev), "tgn", "x", 40, 64, device=dev,
+                   null_model={k: 1 / 12 for k in range(1, 13)}).to(dev).eval()
+    N, B, E = 20 if de == 32 else 30, 50, 100
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a[:E], dtype=dt)).to(dev)  # noqa: E731
+    args = (t(src, np.int32), t(dst, np.int32), t(ts, np.float64), t(eidx, np.int32),
+            torch.arange(E, dtype=torch.int32, device=dev))
+    pt = ExplainPipeline(ex, f.graph, torch.from_numpy(pool), N, 3, B, seed=6)
+    pp = ExplainPipeline(ex, f.graph, torch.from_numpy(pool), N, 3, B, seed=6, edge_table=False)
+    a = [x.clone() for x in pt.run(*args)]
+    b = [x.clone() for x in pp.run(*args)]
+    torch.cuda.synchronize()
+    pt.check_errors()
+    pp.check_errors()
+    assert pt.etab is not None and pp.etab is None
+    w = ex.event_conv.lin_event.weight.detach().double().cpu()
+    ef = torch.from_numpy(g["e_feat"]).double()[:pt.etab.shape[0]]
+    want = ef @ w[:, :de].T
+    got = pt.etab.double().cpu()
+    np.testing.assert_allclose(got[:, :172].numpy(), want.numpy(), rtol=1e-5, atol=1e-6)
+    assert (got[:, 172:] == 0).all()
+    assert torch.equal(pt.gf, pp.gf)
+    np.testing.assert_allclose(a[0].cpu().numpy(), b[0].cpu().numpy(), rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(a[1].cpu().numpy(), b[1].cpu().numpy(), rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(a[2].cpu().numpy(), b[2].cpu().numpy(), rtol=RTOL, atol=ATOL)
