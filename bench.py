@@ -49,10 +49,14 @@ def flops_model(de, dn, h, N, M, etab=False):
     qt = (de + 3 + 15) // 16
     exec_walk = 2 * ((2 + 1.0 / M) * per_pos_gcn + per_walk_head - (1 - 1.0 / M) * (2 * h) ** 2
                      - max(kev - 16 * qt, 0) * dn / M)
+    walk = 2 * (3 * per_pos_gcn + per_walk_head)
     if etab:
+        # the per-position edge-feature product (de x dn MACs) is done per edge id by the table
+        # launch: the walk kernel is credited with the rest of the SURVEY model only
         exec_walk -= 2 * (2 + 1.0 / M) * de * dn
+        walk -= 2 * 3 * de * dn
     return dict(gcn_kernel=2 * per_pos_gcn * 3, head_kernel=2 * per_walk_head, explain_kernel=2 * per_pos_gate * 3,
-                walk_kernel=2 * (3 * per_pos_gcn + per_walk_head), walk_kernel_executed=exec_walk,
+                walk_kernel=walk, walk_kernel_executed=exec_walk,
                 gate_per_edge=2 * per_pos_gate + (2 * de * dn if etab else 0),
                 per_walk=2 * (3 * per_pos_gcn + per_walk_head + 3 * per_pos_gate), W=W)
 
