@@ -61,6 +61,24 @@ def flops_model(de, dn, h, N, M, etab=False):
                 per_walk=2 * (3 * per_pos_gcn + per_walk_head + 3 * per_pos_gate), W=W)
 
 
+def aux_rows(finder, src, dst, ts, eidx, pool, graph_build_ms):
+    """SURVEY §8 rows outside the per-step unit, timed once (not part of ``value``): a1 the CSR build
+    (NeighborFinder.__init__: host sort + per-edge tables + upload) and a11 the null model's sampling
+    and counting (utils/null_model.py pre_processing + statistic: 500 events, num_neighbors 30, one
+    walk per slot), which the reference spends 2.7-3.2 s on per TempME construction."""
+    from tempme_amd.batch_loader import RandEdgeSampler
+    from tempme_amd.null_model import null_counts
+    from tempme_amd import _lib as L
+    sampler = RandEdgeSampler((pool,), (pool,), seed=0, split=L.SPLIT_NULL, device=finder.device)
+    null_counts(finder, sampler, src, dst, ts, eidx, 30)          # warm-up (allocations)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    cnt = null_counts(finder, sampler, src, dst, ts, eidx, 30)
+    null_ms = (time.perf_counter() - t0) * 1e3
+    return {"graph_build_ms": round(graph_build_ms, 2), "graph_entries": int(finder.graph.n_entries),
+            "null_model_ms": round(null_ms, 3), "null_model_walks": int(cnt.sum())}
+
+
 def khop_bytes_per_event(N):
     """SURVEY.md §8(d) compulsory traffic of the k-hop kernel (a1-a4) alone, per target event (3 sides)."""
     return 3 * ((N + N * N) * 16 + (N + N * N) * 12 + (1 + N) * 32)
@@ -219,8 +237,13 @@ def main():
         workload = ("configs[4]: synthetic 1M-edge temporal graph (V=100,000, Pareto 1.5, de=dn=172 U(0,1) "
                     f"features), TempME explanation scoring, n_degree={args.n_degree}")
     (src, dst, ts, eidx), rows, pool = split(g)
+    torch.zeros(1, device=dev)                     # device context and allocator up before timing the build
+    torch.cuda.synchronize()
+    tb = time.perf_counter()
     finder = tm.NeighborFinder.from_edges(g["src"][rows], g["dst"][rows], g["eidx"][rows], g["ts"][rows],
                                           g["n_nodes"], device=dev, seed=args.seed, split=tm.SPLIT_TEST)
+    torch.cuda.synchronize()
+    graph_build_ms = (time.perf_counter() - tb) * 1e3
 
     class Base:
         n_feat_th = torch.from_numpy(g["n_feat"])
@@ -347,6 +370,7 @@ def main():
                                         "achieved": round(ach, 1), "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                                         "measured": "one step in flight (not overlapped), after the timed region"}
         out["khop_roofline"] = khop_alone(pipe, inputs, min(args.steps, 5), N, group=8)
+        out["aux"] = aux_rows(finder, src, dst, ts, eidx, pool, graph_build_ms)
         if world == 1 and not args.no_cpu_baseline:
             sd = {k: v.detach().cpu() for k, v in ex.state_dict().items()}
             out["cpu_baseline"] = cpu_baseline(g, rows, (src, dst, ts, eidx), pool, N, M, B, args.seed, sd)
