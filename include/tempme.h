@@ -261,6 +261,13 @@ int tm_explain_train_bwd(const tm_weights *w, int32_t n_groups, int32_t B, int32
                          const float *dp2, const tm_explain_grad_io *io, float *d_imp, float *const *grads,
                          void *stream);
 
+/* kl_loss, prior='empirical' (explainer_new.py:432-448) of n_groups groups (one reference call each:
+ * prob [G,B,W] graphlet importance, cat [G,B,W] category ids 0..11, null12 the null vector in key order,
+ * target the prior): partial [G*B] = each event's share of its group's loss (the step's KL term is
+ * their sum) and dprob [G,B,W] = d(sum over groups)/d prob, clamp included.  fp64 inside. */
+int tm_kl_loss(const float *prob, const int32_t *cat, const float *null12, float target, int32_t n_groups, int32_t B,
+               int32_t W, float *partial, float *dprob, void *stream);
+
 /* retrieve_edge_imp_node, eval (explainer_new.py:354-406, :420-430) for each of the G*B
  * (group, event) rows: dependency gate, walk->edge scatter-max, gather at the subgraph eids,
  * Beta mean, node==0 mask.  sub1_* [G,B,N], sub2_* [G,B,N*N]; out_h1 [G,B,N], out_h2 [G,B,N*N]

@@ -35,9 +35,9 @@ EXPORTS = (
     "tm_sample_khop", "tm_sample_walks", "tm_neg_sample", "tm_perm_keys", "tm_motif_hist", "tm_edge_counts",
     "tm_sample_events", "tm_weights_create", "tm_weights_pack", "tm_weights_free", "tm_encoder_workspace_bytes",
     "tm_encoder_fwd", "tm_encoder_fwd_tab", "tm_encoder_train_fwd", "tm_encoder_bwd", "tm_encoder_wgrad", "tm_wgrad",
-    "tm_explain_train_fwd", "tm_explain_train_bwd", "tm_edge_importance", "tm_edge_gate_table",
-    "tm_edge_table_cols", "tm_edge_tables",    "tm_edge_importance_tab", "tm_tgn_attn_fwd", "tm_tgn_attn_bwd", "tm_mask_least_important", "tm_profile_enable",
-    "tm_profile_sync", "tm_profile_entry",
+    "tm_explain_train_fwd", "tm_explain_train_bwd", "tm_kl_loss", "tm_edge_importance", "tm_edge_gate_table",
+    "tm_edge_table_cols", "tm_edge_tables", "tm_edge_importance_tab", "tm_tgn_attn_fwd", "tm_tgn_attn_bwd",
+    "tm_mask_least_important", "tm_profile_enable", "tm_profile_sync", "tm_profile_entry",
 )
 
 
@@ -123,6 +123,7 @@ def _sig(L):
                                        C.POINTER(ExplainGradIO), vp, C.POINTER(vp), vp]
     L.tm_edge_importance.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.tm_edge_gate_table.argtypes = [vp, vp, vp, vp, vp]
+    L.tm_kl_loss.argtypes = [vp, vp, vp, C.c_float, i32, i32, i32, vp, vp, vp]
     L.tm_edge_table_cols.argtypes = [vp]
     L.tm_edge_tables.argtypes = [vp, vp, vp, vp, vp, vp]
     L.tm_encoder_fwd_tab.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]

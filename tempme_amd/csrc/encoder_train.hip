@@ -1193,3 +1193,90 @@ extern "C" int tm_explain_train_bwd(const tm_weights *w, int32_t n_groups, int32
                                     {grads[6], grads[7], 3, 1}};
     return run_wgrad(jobs, 4, tgts, 4, s, "tm_explain_train_bwd");
 }
+
+// ------------------------------------------------------------------ kl_loss, prior = 'empirical'
+// explainer_new.py:432-448 for the G groups of one step (the reference's three per-side calls, summed):
+// per (group g, event b) one wave computes, in fp64,
+//   p = clamp(prob, 1e-6, 1-1e-6);  s = mean_w p;  m_k = mean_{w: cat=k} p  (0 for an empty category)
+//   A = (1-s) log((1-s)/(1-target+1e-6) + 1e-6),  E_k = s m_k log(s m_k/(target null_k + 1e-6) + 1e-6)
+// and the event's share of the group's .mean() over the broadcast [B, 12]: (A + mean_k E_k) / B,
+// plus d(sum over groups)/d prob for its W walks (zero where the clamp is active), so the loss and
+// its whole backward are a few launches instead of ~150 small ones.
+__global__ void __launch_bounds__(64) kl_loss_kernel(int32_t B, int32_t W, const float *__restrict__ prob,
+                                                     const int32_t *__restrict__ cat,
+                                                     const float *__restrict__ null12, float target,
+                                                     float *__restrict__ partial, float *__restrict__ dprob) {
+    __shared__ double ssum[64], bins[12], dcat[12];
+    __shared__ int cnts[12];
+    const int tid = threadIdx.x;
+    const int64_t row = blockIdx.x;                 // group * B + event
+    const float *p = prob + row * W;
+    const int32_t *c = cat + row * W;
+    if (tid < 12) {
+        bins[tid] = 0.0;
+        cnts[tid] = 0;
+    }
+    __syncthreads();
+    double acc = 0.0;
+    for (int w = tid; w < W; w += 64) {
+        const double v = fmin(fmax((double)p[w], 1e-6), 1.0 - 1e-6);
+        acc += v;
+        const int k = c[w];
+        if (k >= 0 && k < 12) {
+            atomicAdd(&bins[k], v);
+            atomicAdd(&cnts[k], 1);
+        }
+    }
+    ssum[tid] = acc;
+    __syncthreads();
+    for (int o = 32; o > 0; o >>= 1) {
+        if (tid < o) ssum[tid] += ssum[tid + o];
+        __syncthreads();
+    }
+    const double s = ssum[0] / W;
+    const double c1 = 1.0 - (double)target + 1e-6;
+    const double u = (1.0 - s) / c1 + 1e-6;
+    // per-category value and d/d(emp_k), lanes 0..11
+    double ek = 0.0, dek = 0.0, mk = 0.0;
+    if (tid < 12) {
+        mk = cnts[tid] ? bins[tid] / cnts[tid] : 0.0;
+        const double emp = s * mk, nk = (double)target * (double)null12[tid] + 1e-6, v = emp / nk + 1e-6;
+        ek = emp * log(v);
+        dek = log(v) + emp / (v * nk);
+    }
+    double se = ek, sdm = dek * mk;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+        se += __shfl_xor(se, o, 16);
+        sdm += __shfl_xor(sdm, o, 16);
+    }
+    se = __shfl(se, 0);
+    sdm = __shfl(sdm, 0);
+    const double a = (1.0 - s) * log(u), dads = -log(u) - (1.0 - s) / (u * c1);
+    if (tid == 0) partial[row] = (float)((a + se / 12.0) / B);
+    // d/dp_w = (1/W) [dA/ds / B + sum_k dE_k/demp_k m_k / (12 B)] + dE_{c(w)}/demp s / (12 B n_{c(w)})
+    const double base = (dads / B + sdm / (12.0 * B)) / W;
+    if (tid < 12) dcat[tid] = cnts[tid] ? dek * s / (12.0 * B * cnts[tid]) : 0.0;
+    __syncthreads();
+    for (int w = tid; w < W; w += 64) {
+        const float pw = p[w];
+        const int k = c[w];
+        double g = base + ((k >= 0 && k < 12) ? dcat[k] : 0.0);
+        if (!(pw >= 1e-6f && pw <= 1.f - 1e-6f)) g = 0.0;      // clamp's backward
+        dprob[row * W + w] = (float)g;
+    }
+}
+
+extern "C" int tm_kl_loss(const float *prob, const int32_t *cat, const float *null12, float target, int32_t n_groups,
+                          int32_t B, int32_t W, float *partial, float *dprob, void *stream) {
+    if (n_groups < 0 || B < 0 || W <= 0) return fail(TM_E_ARG, "tm_kl_loss: bad arguments");
+    if (n_groups == 0 || B == 0) return TM_OK;
+    if (!prob || !cat || !null12 || !partial || !dprob) return fail(TM_E_ARG, "tm_kl_loss: NULL pointer");
+    hipStream_t s = S_(stream);
+    hipEvent_t pe = prof_begin(s);
+    kl_loss_kernel<<<dim3((unsigned)((int64_t)n_groups * B)), 64, 0, s>>>(B, W, prob, cat, null12, target, partial,
+                                                                          dprob);
+    TM_CHECK_LAUNCH();
+    prof_end("kl_loss_kernel", s, pe);
+    return TM_OK;
+}

@@ -462,6 +462,16 @@ class TempME(nn.Module):
         return (prob * torch.log(prob / target + 1e-6)
                 + (1 - prob) * torch.log((1 - prob) / (1 - target + 1e-6) + 1e-6)).mean()
 
+    def kl_loss_groups(self, prob, cat, target=0.3):
+        """sum_g kl_loss(prob[g], walks with categories cat[g]) for G groups at once (the training step's
+        three per-side calls, temp_exp_main.py:618-620) on the HIP path: prob [G,B,W] (autograd input),
+        cat [G,B,W] int.  prior='empirical' only (the reference default); value and gradient from
+        tm_kl_loss (fp64 inside), within 1e-5 of the per-side torch formulation."""
+        if self.prior != "empirical" or not self._hip_ok():
+            return sum(self.kl_loss(prob[g].unsqueeze(-1), (None, None, None, cat[g], None), target=target)
+                       for g in range(prob.shape[0]))
+        return _KLFn.apply(prob, cat, self._null_vec(prob.device), float(target))
+
     # ------------------------------------------------------------------ autograd formulation (training)
     def _forward_torch(self, walks, cut_time_l, edge_identify):
         node_idx, edge_idx, time_idx, cat_feat, _ = walks
@@ -546,6 +556,29 @@ class _EncoderFn(torch.autograd.Function):
         grads = ctx.ex._train_bwd(ctx.args, ctx.drop, ctx.drop_scale, ctx.ws, d_imp)
         ctx.ws = None
         return (None, None, None, None, *grads)
+
+
+class _KLFn(torch.autograd.Function):
+    """kl_loss of G groups summed: per-event shares and d/d prob from one tm_kl_loss launch."""
+
+    @staticmethod
+    def forward(ctx, prob, cat, null12, target):
+        G, B, W = prob.shape
+        dev = prob.device
+        p = prob.detach().to(torch.float32).contiguous()
+        c = cat.to(dev, torch.int32).contiguous()
+        nv = null12.to(dev, torch.float32).contiguous()
+        partial = torch.empty(max(G * B, 1), dtype=torch.float32, device=dev)
+        dprob = torch.empty((G, B, W), dtype=torch.float32, device=dev)
+        L.check(L.lib().tm_kl_loss(L.ptr(p), L.ptr(c), L.ptr(nv), float(target), G, B, W, L.ptr(partial),
+                                   L.ptr(dprob), L.stream_ptr(dev)), "kl_loss")
+        ctx.save_for_backward(dprob)
+        return partial[:G * B].sum()
+
+    @staticmethod
+    def backward(ctx, g):
+        (dprob,) = ctx.saved_tensors
+        return dprob * g, None, None, None
 
 
 class _ExplainFn(torch.autograd.Function):

@@ -151,8 +151,14 @@ def train_step(explainer, base_model, optimizer, batch, *, beta=0.5, prior_p=0.3
                                                sg_b, explain_weights=explanation)
     pred = torch.cat([pos_logit, neg_logit], dim=0)
     pred_loss = criterion(pred, y_ori)
-    kl_loss = (explainer.kl_loss(g_s, w_s, target=prior_p) + explainer.kl_loss(g_t, w_t, target=prior_p)
-               + explainer.kl_loss(g_b, w_b, target=prior_p))
+    if batch.stacked is not None and explainer._hip_ok() and explainer.prior == "empirical":
+        # the three per-side kl_loss calls as one tm_kl_loss launch (value and gradient)
+        B, W = g_s.shape[0], g_s.shape[1]
+        prob = torch.stack([g.reshape(B, W) for g in (g_s, g_t, g_b)])
+        kl_loss = explainer.kl_loss_groups(prob, batch.stacked[3].reshape(3, B, W), target=prior_p)
+    else:
+        kl_loss = (explainer.kl_loss(g_s, w_s, target=prior_p) + explainer.kl_loss(g_t, w_t, target=prior_p)
+                   + explainer.kl_loss(g_b, w_b, target=prior_p))
     loss = pred_loss + beta * kl_loss
     loss.backward()
     if grad_sync is not None:

@@ -74,6 +74,32 @@ def test_train_step_matches_reference(dev, case):
             np.testing.assert_allclose(upd[sure], ref[sure], atol=2e-6, rtol=1e-3, err_msg=k)
 
 
+@pytest.mark.parametrize("W", [60, 90])
+def test_kl_loss_groups_matches_per_side(dev, W):
+    """tm_kl_loss (three per-side kl_loss calls as one launch) = the torch formulation of kl_loss
+    (explainer_new.py:432-448) summed over the sides: value and d/d prob within 1e-5, including
+    probabilities clamped at 1e-6 / 1-1e-6 (zero gradient there), empty categories and W > 64."""
+    from tempme_amd import TempME
+    base = TI.build_model("uslegis").to(dev)
+    torch.manual_seed(0)
+    ex = TempME(base, "tgn", "uslegis_sampled", out_dim=40, hid_dim=64, device=dev,
+                null_model={k: (k + 1.0) / 90 for k in range(1, 13)}).to(dev)
+    gen = torch.Generator().manual_seed(W)
+    G, B = 3, 37
+    prob = torch.rand(G, B, W, generator=gen, dtype=torch.float64).float()
+    prob[0, 0, :5] = 1.0            # sigmoid saturated: clamped
+    prob[1, 2, :3] = 0.0
+    cat = torch.randint(0, 9, (G, B, W), generator=gen, dtype=torch.int32)   # categories 9..11 empty
+    p1 = prob.clone().to(dev).requires_grad_(True)
+    p2 = prob.clone().to(dev).requires_grad_(True)
+    a = ex.kl_loss_groups(p1, cat.to(dev), target=0.3)
+    b = sum(ex.kl_loss(p2[g].unsqueeze(-1), (None, None, None, cat[g].to(dev), None), target=0.3) for g in range(G))
+    a.backward()
+    b.backward()
+    np.testing.assert_allclose(a.item(), b.item(), rtol=1e-5)
+    np.testing.assert_allclose(p1.grad.cpu().numpy(), p2.grad.cpu().numpy(), rtol=1e-4, atol=1e-9)
+
+
 def test_stochastic_train_step_runs(dev):
     from tempme_amd.train import train_step
     base, ex, batch, opt = _setup("uslegis", dev)
