@@ -119,6 +119,19 @@ int tm_sample_events(const tm_graph *g, uint64_t seed, uint32_t split, int32_t N
                      float *sub2_ts, int32_t *node6, int32_t *eid3, float *ts3, int32_t *cat, float *cnt,
                      unsigned long long *hist12, int32_t *err_flag, void *stream);
 
+/* Batch slice of a device-resident pack (utils/batch_loader.py get_item / get_item_edge,
+ * :203-242): for each job, dst[side][r] = src[side][rows[r]] (row_bytes per row, a multiple of 4;
+ * side strides in bytes; rows[r] checked against src_rows, *err_flag (nullable) set if outside).
+ * Up to 24 jobs in one launch. */
+typedef struct {
+    const void *src;
+    void *dst;
+    int64_t row_bytes, src_side_stride, dst_side_stride, src_rows;
+    int32_t sides, reserved;
+} tm_gather_job;
+int tm_gather_rows(const tm_gather_job *jobs, int32_t n_jobs, const int64_t *rows, int64_t n_rows, int32_t *err_flag,
+                   void *stream);
+
 /* ---------------------------------------------------------------- encoder (device)
  * Weights: the 28 fp32 tensors of TempME (models/explainer_new.py:103-171), row-major as
  * nn.Linear stores them, in this order (DEVICE pointers):

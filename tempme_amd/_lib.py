@@ -33,7 +33,8 @@ N_WEIGHTS = 28
 EXPORTS = (
     "tm_last_error", "tm_version", "tm_graph_build", "tm_graph_free", "tm_graph_info", "tm_graph_export",
     "tm_sample_khop", "tm_sample_walks", "tm_neg_sample", "tm_perm_keys", "tm_motif_hist", "tm_edge_counts",
-    "tm_sample_events", "tm_weights_create", "tm_weights_pack", "tm_weights_free", "tm_encoder_workspace_bytes",
+    "tm_sample_events", "tm_gather_rows", "tm_weights_create", "tm_weights_pack", "tm_weights_free",
+    "tm_encoder_workspace_bytes",
     "tm_encoder_fwd", "tm_encoder_fwd_tab", "tm_encoder_train_fwd", "tm_encoder_bwd", "tm_encoder_wgrad", "tm_wgrad",
     "tm_explain_train_fwd", "tm_explain_train_bwd", "tm_kl_loss", "tm_edge_importance", "tm_edge_gate_table",
     "tm_edge_table_cols", "tm_edge_tables", "tm_edge_importance_tab", "tm_tgn_attn_fwd", "tm_tgn_attn_bwd",
@@ -77,6 +78,11 @@ class ExplainGradIO(C.Structure):
 class WgradJob(C.Structure):
     _fields_ = [("dy", C.c_void_p), ("x", C.c_void_p), ("ldy", C.c_int32), ("ldx", C.c_int32), ("O", C.c_int32),
                 ("I", C.c_int32), ("R", C.c_int32)]
+
+
+class GatherJob(C.Structure):
+    _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("row_bytes", C.c_int64), ("src_side_stride", C.c_int64),
+                ("dst_side_stride", C.c_int64), ("src_rows", C.c_int64), ("sides", C.c_int32), ("reserved", C.c_int32)]
 
 
 class WgradTarget(C.Structure):
@@ -123,6 +129,7 @@ def _sig(L):
                                        C.POINTER(ExplainGradIO), vp, C.POINTER(vp), vp]
     L.tm_edge_importance.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.tm_edge_gate_table.argtypes = [vp, vp, vp, vp, vp]
+    L.tm_gather_rows.argtypes = [C.POINTER(GatherJob), i32, vp, i64, vp, vp]
     L.tm_kl_loss.argtypes = [vp, vp, vp, C.c_float, i32, i32, i32, vp, vp, vp]
     L.tm_edge_table_cols.argtypes = [vp]
     L.tm_edge_tables.argtypes = [vp, vp, vp, vp, vp, vp]

@@ -449,16 +449,37 @@ class TGN(nn.Module):
         x = torch.cat([h, src_feat], dim=1)
         return F.linear(F.relu(F.linear(x, lw["m1w"], lw["m1b"])), lw["m2w"], lw["m2b"])
 
-    def node_embeddings(self, nodes, eids, times, cut_time, explain_weights=None, edge_attr=None, n_segments=1):
+    def node_embeddings(self, nodes, eids, times, cut_time, explain_weights=None, edge_attr=None, n_segments=1,
+                        prepared=None):
         """embedding_update(_attr) + embedding_update_layer (embedding_module.py:314-393) for
         nodes = [n0 [R1], n1 [R1,N], n2 [R1,N^2]], eids/times = [hop1, hop2] -> [R1, d].
         n_segments > 1 stacks independent contrast batches (R1 = n_segments * 3B rows): every row
-        gives the same result as in its own call (the head-major pairing stays inside its batch)."""
+        gives the same result as in its own call (the head-major pairing stays inside its batch).
+        ``prepared``: the output of ``_prep_inputs`` for these inputs (built once when the same
+        subgraphs go through several contrasts, as the training step's two do)."""
         if self.use_memory and not self.forbidden_memory_update:
             raise NotImplementedError("stateful memory updates inside contrast (tgn.py:167-199) are not part of "
                                       "this build; set forbidden_memory_update=True as temp_exp_main.py:704 does")
         pk = self._pack()
+        x = prepared if prepared is not None else self._prep_inputs(nodes, eids, times, cut_time, edge_attr, n_segments)
+        R1, N, seg1 = x["R1"], x["N"], x["seg1"]
         dev = pk["dev"]
+        ew1 = ew2 = None
+        if explain_weights is not None:
+            ew1 = explain_weights[0].to(dev, torch.float32).reshape(R1, N).contiguous()
+            ew2 = explain_weights[1].to(dev, torch.float32).reshape(R1 * N, N).contiguous()
+        tab = pk["tab"]
+        # layer 0 (attention_models[0]): hop-1 nodes attend over their hop-2 neighbours
+        y0 = self._layer(pk, 0, tab[x["n1l"]], R1 * N, N, x["n2f"], None, x["e2"], x["ed2"], x["dt2"], x["n2f"],
+                         ew2, seg1 * N)
+        # layer 1 (attention_models[1]): roots attend over the hop-1 embeddings
+        y1 = self._layer(pk, 1, tab[x["n0"]], R1, N, None, y0.contiguous(), x["e1"], x["ed1"], x["dt1"], x["n1f"],
+                         ew1, seg1)
+        return y1
+
+    def _prep_inputs(self, nodes, eids, times, cut_time, edge_attr=None, n_segments=1):
+        """node_embeddings' index, time-offset and edge-attribute tensors (retrieve_time_features etc.)."""
+        dev = self._dev()
         i32 = torch.int32
         n0 = _as_dev(nodes[0], dev, torch.long).reshape(-1)
         R1 = n0.shape[0]
@@ -485,18 +506,9 @@ class TGN(nn.Module):
             e1 = e2 = None
             ed1 = _as_dev(edge_attr[0], dev, torch.float32).reshape(R1 * N, -1).contiguous()
             ed2 = _as_dev(edge_attr[1], dev, torch.float32).reshape(R1 * N * N, -1).contiguous()
-        ew1 = ew2 = None
-        if explain_weights is not None:
-            ew1 = explain_weights[0].to(dev, torch.float32).reshape(R1, N).contiguous()
-            ew2 = explain_weights[1].to(dev, torch.float32).reshape(R1 * N, N).contiguous()
-        tab = pk["tab"]
-        # layer 0 (attention_models[0]): hop-1 nodes attend over their hop-2 neighbours
-        y0 = self._layer(pk, 0, tab[n1.reshape(-1).long()], R1 * N, N, n2.reshape(-1).contiguous(), None,
-                         e2, ed2, dt2.reshape(-1), n2.reshape(-1).contiguous(), ew2, seg1 * N)
-        # layer 1 (attention_models[1]): roots attend over the hop-1 embeddings
-        y1 = self._layer(pk, 1, tab[n0], R1, N, None, y0.contiguous(), e1, ed1, dt1.reshape(-1),
-                         n1.reshape(-1).contiguous(), ew1, seg1)
-        return y1
+        return dict(R1=R1, N=N, seg1=seg1, n0=n0, n1l=n1.reshape(-1).long(), n1f=n1.reshape(-1).contiguous(),
+                    n2f=n2.reshape(-1).contiguous(), dt1=dt1.reshape(-1), dt2=dt2.reshape(-1), e1=e1, e2=e2,
+                    ed1=ed1, ed2=ed2)
 
     def check_errors(self):
         """Raise if a kernel saw an out-of-range node or edge index (synchronises)."""
@@ -507,9 +519,20 @@ class TGN(nn.Module):
 
     # -------------------------------------------------------------- reference API
     def get_node_emb(self, src_idx, tgt_idx, bgd_idx, cut_time, e_idx, subgraph_src, subgraph_tgt, subgraph_bgd,
-                     explain_weights=None, edge_attr=None):
+                     explain_weights=None, edge_attr=None, prepared=None):
         """tgn.py:99-199 -> (source, destination, negative) embeddings [B, d] each."""
         B = len(src_idx)
+        if prepared is None:
+            prepared = self.prepare_contrast(src_idx, tgt_idx, bgd_idx, cut_time, subgraph_src, subgraph_tgt,
+                                             subgraph_bgd, edge_attr)
+        emb = self.node_embeddings(None, None, None, None, explain_weights, edge_attr, prepared=prepared)
+        return emb[:B], emb[B:2 * B], emb[2 * B:]
+
+    def prepare_contrast(self, src_idx, tgt_idx, bgd_idx, cut_time, subgraph_src, subgraph_tgt, subgraph_bgd,
+                         edge_attr=None):
+        """The inputs contrast derives from its batch (the three sides' roots and subgraphs
+        concatenated, time offsets), built once: the training step's two contrasts of the same batch
+        (without and with explanation weights, temp_exp_main.py:597, :611) share them."""
         dev = self._dev()
         roots = torch.cat([_as_dev(x, dev, torch.long).reshape(-1) for x in (src_idx, tgt_idx, bgd_idx)])
 
@@ -518,8 +541,7 @@ class TGN(nn.Module):
         nodes = [roots, cat(0, 0, torch.int32), cat(0, 1, torch.int32)]
         eids = [cat(1, 0, torch.int32), cat(1, 1, torch.int32)] if edge_attr is None else [None, None]
         times = [cat(2, 0, torch.float64), cat(2, 1, torch.float64)]
-        emb = self.node_embeddings(nodes, eids, times, cut_time, explain_weights, edge_attr)
-        return emb[:B], emb[B:2 * B], emb[2 * B:]
+        return self._prep_inputs(nodes, eids, times, cut_time, edge_attr)
 
     def affinity(self, x1, x2):
         pk = self._pack()
@@ -527,11 +549,12 @@ class TGN(nn.Module):
         return F.linear(h, pk["a2w"], pk["a2b"])
 
     def contrast(self, src_idx, tgt_idx, bgd_idx, cut_time, e_idx, subgraph_src, subgraph_tgt, subgraph_bgd,
-                 explain_weights=None, edge_attr=None):
-        """tgn.py:201-218 -> (pos_score [B,1], neg_score [B,1])."""
+                 explain_weights=None, edge_attr=None, prepared=None):
+        """tgn.py:201-218 -> (pos_score [B,1], neg_score [B,1]).  ``prepared``: prepare_contrast's
+        output for these same inputs (optional, shared by several contrasts of one batch)."""
         B = len(src_idx)
         s, d, n = self.get_node_emb(src_idx, tgt_idx, bgd_idx, cut_time, e_idx, subgraph_src, subgraph_tgt,
-                                    subgraph_bgd, explain_weights, edge_attr)
+                                    subgraph_bgd, explain_weights, edge_attr, prepared=prepared)
         score = self.affinity(torch.cat([s, s], dim=0), torch.cat([d, n])).squeeze(dim=0)
         return score[:B], score[B:]
 

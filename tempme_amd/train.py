@@ -22,6 +22,8 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from . import _lib as L
+
 SIDES = ("src", "tgt", "bgd")
 
 
@@ -39,22 +41,56 @@ class Batch:
         return int(self.src.shape[0])
 
 
+def _gather_pack(arrays, rows):
+    """index_select(dim, rows) of every (tensor, dim) in ``arrays`` (dim 1 for the side-major pack
+    arrays, 0 for the event arrays) as ONE tm_gather_rows launch; rows a device int64 tensor."""
+    outs, jobs = [], []
+    n = int(rows.numel())
+    for x, dim in arrays:
+        shape = list(x.shape)
+        shape[dim] = n
+        o = torch.empty(shape, dtype=x.dtype, device=x.device)
+        row_elems = int(np.prod(x.shape[dim + 1:])) if x.dim() > dim + 1 else 1
+        sides = int(x.shape[0]) if dim == 1 else 1
+        jobs.append(L.GatherJob(x.data_ptr(), o.data_ptr(), row_elems * x.element_size(),
+                                x.stride(0) * x.element_size() if dim == 1 else 0,
+                                o.stride(0) * o.element_size() if dim == 1 else 0, int(x.shape[dim]), sides, 0))
+        outs.append(o)
+    arr = (L.GatherJob * len(jobs))(*jobs)
+    L.check(L.lib().tm_gather_rows(arr, len(jobs), L.ptr(rows), n, None, L.stream_ptr(rows.device)),
+            "batch_from_pack")
+    return outs
+
+
 def batch_from_pack(buf, src, dst, ts, e_idx, rows):
     """Rows ``rows`` (device int64 index, or a slice) of a sampled pack (preprocess.EventBuffers,
-    side-major [3, E, ...]) and of the event arrays."""
+    side-major [3, E, ...]) and of the event arrays (one gather launch for all of them)."""
+    packed = [(buf.node6, 1), (buf.eid3, 1), (buf.ts3, 1), (buf.cat, 1), (buf.cnt, 1), (buf.sub1_node, 1),
+              (buf.sub1_eid, 1), (buf.sub1_ts, 1), (buf.sub2_node, 1), (buf.sub2_eid, 1), (buf.sub2_ts, 1),
+              (src, 0), (dst, 0), (ts, 0), (e_idx, 0), (buf.dst_fake, 0)]
+    if (not isinstance(rows, slice) and rows.is_cuda and rows.dtype == torch.int64
+            and all(x.is_contiguous() and x.is_cuda and x.element_size() % 4 == 0 for x, _ in packed)):
+        g = _gather_pack(packed, rows)
+        node6, eid3, ts3, cat, cnt = g[:5]
+        s1, s2 = g[5:8], g[8:11]
+        return _batch(g[11], g[12], g[13], g[14], g[15], node6, eid3, ts3, cat, cnt, s1, s2)
+
     def take(x, dim=0):
         return x[(slice(None),) * dim + (rows,)] if isinstance(rows, slice) else x.index_select(dim, rows)
     node6, eid3, ts3, cat, cnt = (take(buf.node6, 1), take(buf.eid3, 1), take(buf.ts3, 1), take(buf.cat, 1),
                                   take(buf.cnt, 1))
     s1 = [take(buf.sub1_node, 1), take(buf.sub1_eid, 1), take(buf.sub1_ts, 1)]
     s2 = [take(buf.sub2_node, 1), take(buf.sub2_eid, 1), take(buf.sub2_ts, 1)]
+    return _batch(take(src), take(dst), take(ts), take(e_idx), take(buf.dst_fake), node6, eid3, ts3, cat, cnt, s1, s2)
+
+
+def _batch(src, dst, ts, e_idx, fake, node6, eid3, ts3, cat, cnt, s1, s2):
     subgraphs, walks, edges = [], [], []
     for s in range(3):
         subgraphs.append(([s1[0][s], s2[0][s]], [s1[1][s], s2[1][s]], [s1[2][s], s2[2][s]]))
         walks.append((node6[s], eid3[s], ts3[s], cat[s].unsqueeze(-1), None))
         edges.append(cnt[s])
-    return Batch(take(src), take(dst), take(ts), take(e_idx), take(buf.dst_fake), subgraphs, walks, edges,
-                 stacked=(node6, eid3, ts3, cat, cnt))
+    return Batch(src, dst, ts, e_idx, fake, subgraphs, walks, edges, stacked=(node6, eid3, ts3, cat, cnt))
 
 
 def _as_dev(x, dev, dtype):
@@ -139,16 +175,22 @@ def train_step(explainer, base_model, optimizer, batch, *, beta=0.5, prior_p=0.3
     criterion = criterion or torch.nn.BCEWithLogitsLoss()
     sg_s, sg_t, sg_b = batch.subgraphs
     w_s, w_t, w_b = batch.walks
+    # the two contrasts of the batch (original and explained) share their derived inputs when the base
+    # model can prepare them (TGN: subgraph concatenations and time offsets built once per step)
+    kw = {}
+    if hasattr(base_model, "prepare_contrast"):
+        with torch.no_grad():
+            kw["prepared"] = base_model.prepare_contrast(batch.src, batch.dst, batch.fake, batch.ts, sg_s, sg_t, sg_b)
     with torch.no_grad():
         pos_out_ori, neg_out_ori = base_model.contrast(batch.src, batch.dst, batch.fake, batch.ts, batch.e_idx,
-                                                       sg_s, sg_t, sg_b)
+                                                       sg_s, sg_t, sg_b, **kw)
         y_pred = torch.cat([pos_out_ori, neg_out_ori], dim=0).sigmoid()
         y_ori = torch.where(y_pred > 0.5, 1., 0.).view(y_pred.size(0), 1)
     optimizer.zero_grad()
     g_s, g_t, g_b = encode_sides(explainer, batch)
     explanation = explain_sides(explainer, batch, (g_s, g_t, g_b), if_bern)
     pos_logit, neg_logit = base_model.contrast(batch.src, batch.dst, batch.fake, batch.ts, batch.e_idx, sg_s, sg_t,
-                                               sg_b, explain_weights=explanation)
+                                               sg_b, explain_weights=explanation, **kw)
     pred = torch.cat([pos_logit, neg_logit], dim=0)
     pred_loss = criterion(pred, y_ori)
     if batch.stacked is not None and explainer._hip_ok() and explainer.prior == "empirical":

@@ -100,6 +100,33 @@ def test_kl_loss_groups_matches_per_side(dev, W):
     np.testing.assert_allclose(p1.grad.cpu().numpy(), p2.grad.cpu().numpy(), rtol=1e-4, atol=1e-9)
 
 
+def test_batch_from_pack_gather_equals_index_select(dev):
+    """batch_from_pack's one-launch row gather (tm_gather_rows) = torch.index_select of every pack array."""
+    import tempme_amd as tm
+    from tempme_amd.preprocess import sample_events
+    from tempme_amd.train import batch_from_pack
+    from tempme_amd.workload import enron_like, split
+    g = enron_like(n_nodes=60, n_edges=2000, seed=8)
+    (src, dst, ts, eidx), rows, pool = split(g, mode="train")
+    f = tm.NeighborFinder.from_edges(g["src"][rows], g["dst"][rows], g["eidx"][rows], g["ts"][rows], g["n_nodes"],
+                                     device=dev, seed=1, split=tm.SPLIT_TRAIN)
+    to = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)  # noqa: E731
+    s_d, d_d, t_d, e_d = to(src, np.int32), to(dst, np.int32), to(ts, np.float64), to(eidx, np.int32)
+    buf = sample_events(f.graph, 1, tm.SPLIT_TRAIN, 8, 3, s_d, d_d, t_d, e_d,
+                        torch.arange(len(src), dtype=torch.int32, device=dev), to(pool, np.int32))
+    r = torch.randperm(len(src) - 1, generator=torch.Generator().manual_seed(0))[:37].to(dev)
+    b = batch_from_pack(buf, s_d, d_d, t_d, e_d, r)
+    sel = lambda x, dim: x.index_select(dim, r)  # noqa: E731
+    for got, want in zip(b.stacked, (sel(buf.node6, 1), sel(buf.eid3, 1), sel(buf.ts3, 1), sel(buf.cat, 1),
+                                     sel(buf.cnt, 1))):
+        assert torch.equal(got, want)
+    for s in range(3):
+        assert torch.equal(b.subgraphs[s][0][1], sel(buf.sub2_node, 1)[s])
+        assert torch.equal(b.subgraphs[s][2][0], sel(buf.sub1_ts, 1)[s])
+    for got, x in ((b.src, s_d), (b.dst, d_d), (b.ts, t_d), (b.e_idx, e_d), (b.fake, buf.dst_fake)):
+        assert torch.equal(got, sel(x, 0))
+
+
 def test_stochastic_train_step_runs(dev):
     from tempme_amd.train import train_step
     base, ex, batch, opt = _setup("uslegis", dev)
