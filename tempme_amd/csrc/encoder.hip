@@ -22,39 +22,42 @@
 namespace tmk {
 
 // ------------------------------------------------------------------ std over |cut - t| per group
-__global__ void __launch_bounds__(256) std_kernel(int32_t B, int32_t W, const double *__restrict__ cut,
-                                                  const float *__restrict__ ts3, float *__restrict__ std_out) {
-    __shared__ double red[256];
-    const int64_t g = blockIdx.x, n = (int64_t)B * W * 2;
-    const float *t = ts3 + g * (int64_t)B * W * 3;
+// sum over the workgroup (fixed order: wave butterflies, then the waves' partials in order)
+__device__ __forceinline__ double block_sum(double v, double *red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[wave] = v;
+    __syncthreads();
     double s = 0.0;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const int64_t w = i >> 1, b = w / W;
-        const float c = (float)cut[g * B + b];
-        s += (double)fabsf(c - t[w * 3 + (i & 1)]);
+    for (int k = 0; k < nw; ++k) s += red[k];
+    return s;
+}
+
+// one 1024-thread workgroup per group; thread w takes walk w's two |cut - t| values (int32 indexing)
+__global__ void __launch_bounds__(1024) std_kernel(int32_t B, int32_t W, const double *__restrict__ cut,
+                                                   const float *__restrict__ ts3, float *__restrict__ std_out) {
+    __shared__ double red[16];
+    const int64_t g = blockIdx.x;
+    const int32_t nw = B * W;
+    const int64_t n = (int64_t)nw * 2;
+    const float *t = ts3 + g * (int64_t)nw * 3;
+    const double *cg = cut + g * B;
+    double s = 0.0;
+    for (int32_t w = threadIdx.x; w < nw; w += blockDim.x) {
+        const float c = (float)cg[w / W];
+        s += (double)fabsf(c - t[w * 3]) + (double)fabsf(c - t[w * 3 + 1]);
     }
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int k = 128; k > 0; k >>= 1) {
-        if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
-        __syncthreads();
-    }
-    const double mean = red[0] / (double)n;
-    __syncthreads();
+    const double mean = block_sum(s, red) / (double)n;
     double v = 0.0;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const int64_t w = i >> 1, b = w / W;
-        const float c = (float)cut[g * B + b];
-        const double d = (double)fabsf(c - t[w * 3 + (i & 1)]) - mean;
-        v += d * d;
+    for (int32_t w = threadIdx.x; w < nw; w += blockDim.x) {
+        const float c = (float)cg[w / W];
+        const double d0 = (double)fabsf(c - t[w * 3]) - mean, d1 = (double)fabsf(c - t[w * 3 + 1]) - mean;
+        v += d0 * d0 + d1 * d1;
     }
-    red[threadIdx.x] = v;
-    __syncthreads();
-    for (int k = 128; k > 0; k >>= 1) {
-        if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) std_out[g] = n > 1 ? (float)sqrt(red[0] / (double)(n - 1)) : __builtin_nanf("");
+    const double var = block_sum(v, red);
+    if (threadIdx.x == 0) std_out[g] = n > 1 ? (float)sqrt(var / (double)(n - 1)) : __builtin_nanf("");
 }
 
 // ------------------------------------------------------------------ event_gcn: 32 walk-positions per block
@@ -1342,7 +1345,7 @@ extern "C" int tm_encoder_fwd_tab(const tm_weights *w, const float *n_feat, cons
     float *F = reinterpret_cast<float *>(workspace);
     float *stdv = F + n_walks * 3 * 2 * HID;
     hipEvent_t pe = prof_begin(s);
-    std_kernel<<<dim3(n_groups), 256, 0, s>>>(B, W, cut, ts3, stdv);
+    std_kernel<<<dim3(n_groups), 1024, 0, s>>>(B, W, cut, ts3, stdv);
     TM_CHECK_LAUNCH();
     prof_end("std_kernel", s, pe);
     if (etab && etab_q0(P) == 0) return fail(TM_E_UNSUPPORTED, "tm_encoder_fwd_tab: no edge table for these dims");
@@ -1409,7 +1412,7 @@ extern "C" int tm_encoder_train_fwd(const tm_weights *w, const float *n_feat, co
     float *F = reinterpret_cast<float *>(workspace);
     float *stdv = F + n_walks * 3 * 2 * HID;
     hipEvent_t pe = prof_begin(s);
-    std_kernel<<<dim3(n_groups), 256, 0, s>>>(B, W, cut, ts3, stdv);
+    std_kernel<<<dim3(n_groups), 1024, 0, s>>>(B, W, cut, ts3, stdv);
     TM_CHECK_LAUNCH();
     prof_end("std_kernel", s, pe);
     const int64_t n_rows = n_walks * 3;
