@@ -164,6 +164,95 @@ __global__ void __launch_bounds__(64 * ATT_WAVES) tgn_attn_fwd_kernel(tm_tgn_att
     }
 }
 
+// The same forward with the row's neighbours split over the workgroup's ATT_WAVES waves (wave w takes
+// j = w, w + 4, ...), each running its own online softmax; the partial states (max, normaliser,
+// weighted key sum) merge through LDS in wave order.  A row's neighbours are independent gathers, so
+// four waves keep four of them in flight where one wave walked the chain alone; the 300-row root
+// layer of a bs=100 contrast had only 300 waves for 1,024 SIMDs.
+template <int KPL>
+__global__ void __launch_bounds__(64 * ATT_WAVES) tgn_attn_fwd_split_kernel(tm_tgn_attn a, float *__restrict__ z,
+                                                                            float *__restrict__ stats) {
+    __shared__ float s_acc[ATT_WAVES][ATT_MAXH][KPL][64], s_m[ATT_WAVES][ATT_MAXH], s_l[ATT_WAVES][ATT_MAXH];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t r = blockIdx.x;
+    const int H = a.n_head, N = a.n_ngh, dk = a.d_node + a.d_edge + a.d_time;
+    const KeyLane<KPL> L = key_lane<KPL>(a, lane);
+    float q[ATT_MAXH][KPL], acc[ATT_MAXH][KPL], m[ATT_MAXH], l[ATT_MAXH];
+    int64_t mr[ATT_MAXH];
+#pragma unroll
+    for (int h = 0; h < ATT_MAXH; ++h) {
+        m[h] = -__builtin_inff();
+        l[h] = 0.f;
+        mr[h] = h < H ? pair_row(a, r, h) : 0;
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) {
+            const int c = lane + 64 * i;
+            q[h][i] = (h < H && c < dk) ? a.qf[(r * H + h) * dk + c] : 0.f;
+            acc[h][i] = 0.f;
+        }
+    }
+    for (int j = wv; j < N; j += ATT_WAVES) {
+        float k[KPL];
+        build_key<KPL>(a, L, r * N + j, k);
+#pragma unroll
+        for (int h = 0; h < ATT_MAXH; ++h) {
+            if (h < H) {
+                float p = 0.f;
+#pragma unroll
+                for (int i = 0; i < KPL; ++i) p = __builtin_fmaf(q[h][i], k[i], p);
+                float s = wave_sum(p) / a.temperature;
+                const int64_t ms = mr[h] * N + j;
+                if (a.mask_node[ms] == 0) s = -1e10f;
+                const float e = a.ew ? a.ew[ms] : 1.f;
+                const float mn = fmaxf(m[h], s);
+                const float sc = expf(m[h] - mn), w = expf(s - mn);
+                l[h] = l[h] * sc + w;
+                const float we = w * e;
+#pragma unroll
+                for (int i = 0; i < KPL; ++i) acc[h][i] = __builtin_fmaf(we, k[i], acc[h][i] * sc);
+                m[h] = mn;
+            }
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < ATT_MAXH; ++h) {
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) s_acc[wv][h][i][lane] = acc[h][i];
+        if (lane == 0) {
+            s_m[wv][h] = m[h];
+            s_l[wv][h] = l[h];
+        }
+    }
+    __syncthreads();
+    if (wv != 0) return;
+#pragma unroll
+    for (int h = 0; h < ATT_MAXH; ++h) {
+        if (h >= H) continue;
+        float M = s_m[0][h];
+#pragma unroll
+        for (int w = 1; w < ATT_WAVES; ++w) M = fmaxf(M, s_m[w][h]);
+        float Ls = 0.f, sc[ATT_WAVES];
+#pragma unroll
+        for (int w = 0; w < ATT_WAVES; ++w) {
+            sc[w] = s_l[w][h] > 0.f ? expf(s_m[w][h] - M) : 0.f;   // a wave with no neighbour adds nothing
+            Ls += s_l[w][h] * sc[w];
+        }
+        const float inv = 1.f / Ls;
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) {
+            float v = 0.f;
+#pragma unroll
+            for (int w = 0; w < ATT_WAVES; ++w) v = __builtin_fmaf(s_acc[w][h][i][lane], sc[w], v);
+            const int c = lane + 64 * i;
+            if (c < dk) z[(r * H + h) * dk + c] = v * inv;
+        }
+        if (lane == 0) {
+            stats[(r * H + h) * 2] = M;
+            stats[(r * H + h) * 2 + 1] = Ls;
+        }
+    }
+}
+
 // Backward of z[r,h] = sum_j p_j e_j k_j, p = softmax(s), s_j = qf_h.k_j / T (masked: constant):
 //   c_j = gz_h.k_j;  d e_j += p_j c_j;  S_h = sum_j p_j e_j c_j;  ds_j = p_j (e_j c_j - S_h) (0 if masked)
 //   d k_j = sum_h p_j e_j gz_h + (ds_j / T) qf_h        (node-feature columns only are written)
@@ -277,6 +366,10 @@ static int check_attn(const tm_tgn_attn *a, const char *who) {
 
 template <int KPL>
 static void launch_fwd(const tm_tgn_attn &a, float *z, float *stats, hipStream_t s) {
+    if (a.n_ngh >= ATT_WAVES) {   // one row per workgroup, its neighbours over the waves
+        tgn_attn_fwd_split_kernel<KPL><<<dim3((unsigned)a.rows), 64 * ATT_WAVES, 0, s>>>(a, z, stats);
+        return;
+    }
     const unsigned blocks = (unsigned)((a.rows + ATT_WAVES - 1) / ATT_WAVES);
     tgn_attn_fwd_kernel<KPL><<<dim3(blocks), 64 * ATT_WAVES, 0, s>>>(a, z, stats);
 }
