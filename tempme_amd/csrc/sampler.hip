@@ -367,10 +367,11 @@ __global__ void __launch_bounds__(256) khop_kernel(DevGraph g, Key key, uint32_t
 // (kept in LDS), looks up the hop-2 rows' cut lengths and offsets once per row, then draws, ranks and
 // gathers the EPB*N hop-2 rows -- one launch, and no hop-1 -> hop-2 round trip through HBM.
 // Same Philox-block-per-thread scheme as khop_kernel.
-// roots per workgroup: ~one hop-2 Philox block per thread, so the launch is about one round of
-// resident workgroups (each is a chain of dependent lookups; a second round doubles the time)
+// roots per workgroup: ~three hop-2 Philox blocks per thread (8 roots at N=20): each workgroup is a
+// chain of dependent lookups with barriers between the levels, and more rows per level keep more
+// gathers in flight per barrier (A/B at N=20: 2 / 4 / 8 / 16 roots -> 48 / 51 / 52 / 51 % of HBM)
 __host__ __device__ inline int32_t khop2_epb(int32_t N) {
-    const int32_t e = 1600 / (N * N);
+    const int32_t e = 3200 / (N * N);
     return e < 1 ? 1 : e > 8 ? 8 : e;
 }
 
