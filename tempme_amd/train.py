@@ -41,9 +41,10 @@ class Batch:
         return int(self.src.shape[0])
 
 
-def _gather_pack(arrays, rows):
+def _gather_pack(arrays, rows, err=None):
     """index_select(dim, rows) of every (tensor, dim) in ``arrays`` (dim 1 for the side-major pack
-    arrays, 0 for the event arrays) as ONE tm_gather_rows launch; rows a device int64 tensor."""
+    arrays, 0 for the event arrays) as ONE tm_gather_rows launch; rows a device int64 tensor; a row
+    outside an array sets the int32 device flag ``err`` (the pack's, raised by its check)."""
     outs, jobs = [], []
     n = int(rows.numel())
     for x, dim in arrays:
@@ -57,7 +58,7 @@ def _gather_pack(arrays, rows):
                                 o.stride(0) * o.element_size() if dim == 1 else 0, int(x.shape[dim]), sides, 0))
         outs.append(o)
     arr = (L.GatherJob * len(jobs))(*jobs)
-    L.check(L.lib().tm_gather_rows(arr, len(jobs), L.ptr(rows), n, None, L.stream_ptr(rows.device)),
+    L.check(L.lib().tm_gather_rows(arr, len(jobs), L.ptr(rows), n, L.ptr(err), L.stream_ptr(rows.device)),
             "batch_from_pack")
     return outs
 
@@ -70,7 +71,7 @@ def batch_from_pack(buf, src, dst, ts, e_idx, rows):
               (src, 0), (dst, 0), (ts, 0), (e_idx, 0), (buf.dst_fake, 0)]
     if (not isinstance(rows, slice) and rows.is_cuda and rows.dtype == torch.int64
             and all(x.is_contiguous() and x.is_cuda and x.element_size() % 4 == 0 for x, _ in packed)):
-        g = _gather_pack(packed, rows)
+        g = _gather_pack(packed, rows, getattr(buf, "err", None))
         node6, eid3, ts3, cat, cnt = g[:5]
         s1, s2 = g[5:8], g[8:11]
         return _batch(g[11], g[12], g[13], g[14], g[15], node6, eid3, ts3, cat, cnt, s1, s2)
