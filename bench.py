@@ -184,6 +184,8 @@ def main():
     ap.add_argument("--alpha", type=float, default=1.2)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: --batches is the whole step, split over the ranks (default: per rank)")
     ap.add_argument("--no-edge-table", action="store_true",
                     help="lin_event's edge-feature product per walk position instead of per edge id")
     ap.add_argument("--streams", type=int, default=1,
@@ -222,7 +224,13 @@ def main():
     from tempme_amd.workload import enron_like, split
 
     N, M, B = args.n_degree, 3, args.batch_size
-    E = args.batches * B
+    if args.strong:
+        # strong scaling: the step's args.batches reference batches are dealt over the ranks
+        if args.batches % world:
+            raise SystemExit(f"--strong needs --batches divisible by the {world} ranks")
+        E = args.batches // world * B
+    else:
+        E = args.batches * B
     if args.config == 1:
         g = enron_like(alpha=args.alpha, seed=args.seed)
         workload = ("configs[1]: enron_sampled-shaped synthetic graph (V=183, E=18,780, "
@@ -344,10 +352,11 @@ def main():
         total = world * args.steps * E
         out = {"metric": METRIC, "value": round(total / el, 2), "unit": "edges/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
-               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+               "higher_is_better": True, "scaling": "strong" if args.strong else "weak", "vs_baseline": None,
+               "dtype": "fp32",
                "data": "synthetic (seeded graph of the config's shape, random-init TempME weights)",
                "config": {"workload": workload,
-                          "n_degree": N, "walks_per_slot": M, "batch_size": B, "batches_per_step_per_gpu": args.batches,
+                          "n_degree": N, "walks_per_slot": M, "batch_size": B, "batches_per_step_per_gpu": E // B,
                           "events_per_step_per_gpu": E, "parallelism": f"dp{world} (whole batches per rank)",
                           "steps_in_flight": S},
                "roofline": roof, "kernels": kernels,
