@@ -125,6 +125,11 @@ def test_batch_from_pack_gather_equals_index_select(dev):
         assert torch.equal(b.subgraphs[s][2][0], sel(buf.sub1_ts, 1)[s])
     for got, x in ((b.src, s_d), (b.dst, d_d), (b.ts, t_d), (b.e_idx, e_d), (b.fake, buf.dst_fake)):
         assert torch.equal(got, sel(x, 0))
+    # a row outside the pack is not read; it flags the pack's error word (index_select would raise)
+    assert int(buf.err.item()) == 0
+    batch_from_pack(buf, s_d, d_d, t_d, e_d, torch.tensor([0, len(src) + 5], dtype=torch.int64, device=dev))
+    from tempme_amd import _lib as L
+    assert int(buf.err.item()) == L.TM_E_ARG
 
 
 def test_stochastic_train_step_runs(dev):
