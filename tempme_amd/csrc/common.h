@@ -93,9 +93,8 @@ __device__ __forceinline__ T *vptr(T *p) {
 // ------------------------------------------------------------------ Philox4x32-10
 // all four output words of one Philox4x32-10 block
 __device__ __forceinline__ uint4 philox4(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
-    // key schedule in VGPRs: with a uniform key the compiler otherwise keeps all 20 round keys of
-    // every key live in SGPRs, which spills the kernels' scalar state through v_readlane
-    asm volatile("" : "+v"(k0), "+v"(k1));
+    // a wave-uniform key stays in SGPRs and its schedule is scalar adds (the keyed sampler kernels
+    // fit it without spills; forcing the key into VGPRs cost 20 VALU per block: events_kernel 3 %)
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         if (r) {
