@@ -8,8 +8,10 @@ import sys
 from collections import defaultdict
 
 root = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else "gpurun_out"
+# --glob PAT: the pass directories (default pmc[0-9]* = the bench passes; tools_pmc_train.sh writes pmct*)
+pat = sys.argv[sys.argv.index("--glob") + 1] if "--glob" in sys.argv else "pmc[0-9]*"
 acc = defaultdict(lambda: defaultdict(list))
-for f in sorted(glob.glob(f"{root}/pmc*/run_counter_collection.csv")):
+for f in sorted(glob.glob(f"{root}/{pat}/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0].replace("void ", "")
         acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
