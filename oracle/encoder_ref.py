@@ -8,7 +8,8 @@ Functional restatement (no nn.Module) of models/explainer_new.py:
   kl_loss                 :432-453   (empirical prior; null vector in null-model key order)
 Eval semantics (dropout = identity, Beta mean instead of rsample); forward() also takes explicit dropout
 keep-masks so the training forward / backward can be checked with autograd through this restatement.
-Pinned against tests/golden/encoder_uslegis.npz (outputs of the reference module).
+Pinned against tests/golden/encoder_uslegis.npz and enron_goldens.npz (outputs of the reference module;
+the latter at Enron-scale timestamps and for the constructor variants).
 """
 import numpy as np
 import torch
@@ -28,8 +29,9 @@ def time_encode(sd, t):
     return torch.cos(m.to(w.dtype))
 
 
-def forward(sd, n_feat, e_feat, node, eid, ts, cat, cut, edge_count, drop=None, scale=1.0):
-    """graphlet importance [B, W, 1] for one side (explainer_new.py:174-201).  drop: optional keep-masks
+def forward(sd, n_feat, e_feat, node, eid, ts, cat, cut, edge_count, drop=None, scale=1.0, temporal=True):
+    """graphlet importance [B, W, 1] for one side (explainer_new.py:174-201).  temporal=False: the
+    plain ``Attention`` of use_temporal_guidance=False (explainer_new.py:12-43, no time scaling).  drop: optional keep-masks
     [B, W, 144] of the training forward's three dropouts (alpha :839 -> cols 0..1, attention.MLP hidden :780
     -> 2..65, MLP hidden :122 -> 66..141), kept values scaled by `scale` (training-mode parity).
     Computes in the dtype of sd's tensors (fp32, or fp64 for gradient references)."""
@@ -60,9 +62,10 @@ def forward(sd, n_feat, e_feat, node, eid, ts, cat, cut, edge_count, drop=None, 
     wp = _lin(sd, "attention.W1", src)                           # [B,W,2h]
     wq = _lin(sd, "attention.W2", tgt)                           # [B,W,2,2h]
     scores = (wp.unsqueeze(2) * wq).sum(-1)                      # [B,W,2]
-    diff = torch.abs(cut.view(B, 1, 1) - t[:, :, :2])
-    tw = torch.exp(-diff / (diff.std() + 1e-6)).to(dty)
-    scores = scores * (1.0 - 0.3 + 0.3 * tw)
+    if temporal:
+        diff = torch.abs(cut.view(B, 1, 1) - t[:, :, :2])
+        tw = torch.exp(-diff / (diff.std() + 1e-6)).to(dty)
+        scores = scores * (1.0 - 0.3 + 0.3 * tw)
     alpha = torch.softmax(scores, dim=-1)
     if keep is not None:
         alpha = alpha * keep[..., 0:2]
@@ -70,7 +73,8 @@ def forward(sd, n_feat, e_feat, node, eid, ts, cat, cut, edge_count, drop=None, 
     hid = torch.relu(_lin(sd, "attention.MLP.0", out))
     if keep is not None:
         hid = hid * keep[..., 2:66]
-    out = _lin(sd, "attention.MLP.3", hid)
+    # TemporalAwareAttention.MLP has a Dropout at index 2 (:777-782), Attention.MLP does not (:18)
+    out = _lin(sd, "attention.MLP.3" if "attention.MLP.3.weight" in sd else "attention.MLP.2", hid)
     oh = F.one_hot(torch.as_tensor(np.asarray(cat), dtype=torch.long).reshape(B, W), 12).to(dty)
     x = torch.cat([out, oh], dim=-1)
     x = torch.relu(_lin(sd, "MLP.0", x))
@@ -86,17 +90,19 @@ def beta_mean(p):
     return a / (a + b)
 
 
-def edge_importance(sd, e_feat, imp, walk_eid, walk_ts, sub_node, sub_eid):
-    """retrieve_edge_imp_node, eval (explainer_new.py:354-406).  sub_*: [hop1 [B,N], hop2 [B,N^2]]."""
+def edge_importance(sd, e_feat, imp, walk_eid, walk_ts, sub_node, sub_eid, dependency=True):
+    """retrieve_edge_imp_node, eval (explainer_new.py:354-406).  sub_*: [hop1 [B,N], hop2 [B,N^2]].
+    dependency=False: use_dependency_aware_sampling=False (no gate, :366-386 skipped)."""
     B = imp.shape[0]
     ew = torch.as_tensor(np.asarray(walk_eid), dtype=torch.long).reshape(B, -1)
     tw = torch.as_tensor(np.asarray(walk_ts, dtype=np.float64)).float().reshape(B, -1)
     wimp = imp.repeat(1, 1, 3).view(B, -1)
-    g = torch.cat([e_feat[ew], time_encode(sd, tw)], dim=-1)
-    g = torch.relu(_lin(sd, "edge_dependency_gcn.0", g))
-    g = torch.relu(_lin(sd, "edge_dependency_gcn.3", g))
-    g = _lin(sd, "edge_dependency_gcn.6", g).squeeze(-1)
-    wimp = wimp * (0.5 + 0.5 * torch.sigmoid(g))
+    if dependency:
+        g = torch.cat([e_feat[ew], time_encode(sd, tw)], dim=-1)
+        g = torch.relu(_lin(sd, "edge_dependency_gcn.0", g))
+        g = torch.relu(_lin(sd, "edge_dependency_gcn.3", g))
+        g = _lin(sd, "edge_dependency_gcn.6", g).squeeze(-1)
+        wimp = wimp * (0.5 + 0.5 * torch.sigmoid(g))
     i0 = torch.as_tensor(np.asarray(sub_eid[0]), dtype=torch.long)
     i1 = torch.as_tensor(np.asarray(sub_eid[1]), dtype=torch.long)
     n_e = int(max(ew.max(), i0.max(), i1.max()) + 1)

@@ -373,21 +373,20 @@ USED_PREFIXES = ("event_conv.", "attention.W1.", "attention.W2.", "attention.MLP
                  "edge_dependency_gcn.", "time_encoder.")
 
 
-def _enc_batch(n_deg=20, bsz=32):
-    """The first `bsz` test events of uslegis_pipeline.npz through the reference's own H5 pack
-    loader (data_preprocess.py:393-404 layout, batch_loader.py:120-242)."""
-    pipe = np.load(os.path.join(HERE, "uslegis_pipeline.npz"))
+def _pack_items(pipe, pre, n_deg, bsz, ts_key):
+    """The first `bsz` events of a packed pipeline golden (keys `pre` + ...) through the reference's
+    own H5 pack loader (data_preprocess.py:393-404 layout, batch_loader.py:120-242)."""
     st = {}
     for side in ("src", "tgt", "bgd"):
         for h in (0, 1):
-            p = f"test_N{n_deg}_subgraph_{side}_{h}"
+            p = f"{pre}subgraph_{side}_{h}"
             st[f"subgraph_{side}_{h}"] = np.concatenate(
                 [pipe[p + "_node"], pipe[p + "_eid"], pipe[p + "_ts"].astype(np.float64)], axis=1).astype(np.float64)
-        p = f"test_N{n_deg}_walks_{side}"
+        p = f"{pre}walks_{side}"
         st[f"walks_{side}_new"] = np.concatenate(
             [pipe[p + "_node"], pipe[p + "_eid"], pipe[p + "_ts"].astype(np.float64),
              pipe[p + "_cat"][..., None], pipe[p + "_marg"][..., None]], axis=-1).astype(np.float64)
-    st["dst_fake"] = pipe[f"test_N{n_deg}_dst_fake"].astype(np.float64)
+    st["dst_fake"] = pipe[f"{pre}dst_fake"].astype(np.float64)
     _FakeH5File.store["enc_pack"] = st
 
     class A:
@@ -395,11 +394,18 @@ def _enc_batch(n_deg=20, bsz=32):
     args = A()
     args.n_degree = n_deg
     pack = load_subgraph_margin(args, _FakeH5File("enc_pack"))
-    edge = pipe[f"test_N{n_deg}_edge"].astype(np.float64)
+    edge = pipe[f"{pre}edge"].astype(np.float64)
     batch_idx = np.arange(bsz)
     items = get_item(pack, batch_idx)
     edges = get_item_edge(edge, batch_idx)
-    ts_cut = pipe["test_ts"][:bsz].astype(np.float64)
+    ts_cut = pipe[ts_key][:bsz].astype(np.float64)
+    return items, edges, ts_cut, batch_idx
+
+
+def _enc_batch(n_deg=20, bsz=32):
+    """The first `bsz` test events of uslegis_pipeline.npz as TempME receives them."""
+    pipe = np.load(os.path.join(HERE, "uslegis_pipeline.npz"))
+    items, edges, ts_cut, batch_idx = _pack_items(pipe, f"test_N{n_deg}_", n_deg, bsz, "test_ts")
     return pipe, items, edges, ts_cut, batch_idx
 
 
@@ -460,7 +466,7 @@ def load_ref_function(relpath, name, **ns):
     return ns[name]
 
 
-TGN_SEEDS = {"uslegis": 11, "synth": 12}
+TGN_SEEDS = {"uslegis": 11, "synth": 12, "enron": 13}
 TGN_RATIOS = [0.01, 0.02, 0.04, 0.06, 0.08, 0.10, 0.12, 0.14, 0.16, 0.18, 0.2, 0.22, 0.24, 0.26, 0.28, 0.30]
 TGN_MSG_NODES = (3, 17, 42, 100, 101)
 
@@ -624,6 +630,147 @@ def case_train():
     save_npz("train_uslegis.npz", **res)
 
 
+# ----------------------------------------------------------------------------- Enron-scale case
+ENRON = dict(n_nodes=184, n_edges=125235, alpha=1.2, de=32, dn=172, seed=0, node_feat="uniform")
+ENRON_SETS = ((20, 100), (30, 32))          # (n_degree, events) of the test split
+ENRON_VARIANTS = {"base": {}, "notg": dict(use_temporal_guidance=False),
+                  "nodep": dict(use_dependency_aware_sampling=False), "h32": dict(hid_dim=32)}
+
+
+def enron_graph():
+    """Full-Enron-shaped synthetic graph of the bench (tempme_amd/workload.py enron_like: seeded
+    numpy RandomState, so it is regenerated bit for bit from its parameters; a checksum is stored)."""
+    from tempme_amd.workload import enron_like
+    return enron_like(**ENRON)
+
+
+def graph_checksum(g):
+    return np.array([int(g["src"].sum()), int((g["src"] * g["dst"]).sum() % (1 << 61)), int(g["ts"].sum()),
+                     float(g["e_feat"].astype(np.float64).sum()), float(g["n_feat"].astype(np.float64).sum())])
+
+
+def _enron_load_data(g, mode):
+    """The reference's own split code (data_preprocess.load_data, :24-76) on the synthetic graph: its
+    pd.read_csv is pointed at an in-memory frame of the edges (the CSV layout of processed/ml_*.csv)."""
+    import pandas
+    df = pandas.DataFrame({"u": g["src"], "i": g["dst"], "ts": g["ts"], "label": g["label"], "idx": g["eidx"]})
+    real = DP["pd"]
+    DP["pd"] = types.SimpleNamespace(read_csv=lambda path, *a, **k: df if path.endswith("ml_enron_synth.csv")
+                                     else real.read_csv(path, *a, **k))
+    try:
+        return DP["load_data"](mode=mode, data="enron_synth")
+    finally:
+        DP["pd"] = real
+
+
+def _explain_outputs(ex, items, edges, ts_cut):
+    """eval_one_epoch's scoring calls (temp_exp_main.py:446-452) plus the three kl_loss terms."""
+    sg_s, sg_t, sg_b, w_s, w_t, w_b, _ = items
+    e_s, e_t, e_b = edges
+    with torch.no_grad():
+        imp = [ex(w, ts_cut, e) for w, e in ((w_s, e_s), (w_t, e_t), (w_b, e_b))]
+        expl = ex.retrieve_explanation(sg_s, imp[0], w_s, sg_t, imp[1], w_t, sg_b, imp[2], w_b, training=False)
+        kl = [ex.kl_loss(p, w, target=0.3) for p, w in zip(imp, (w_s, w_t, w_b))]
+    return imp, expl, kl
+
+
+def _train_iteration(ex, base, src, dst, e_l, ts_cut, items, edges):
+    """temp_exp_main.py:605-632 with Explainer.eval() and if_bern=False (see case_train)."""
+    sg_s, sg_t, sg_b, w_s, w_t, w_b, dst_fake = items
+    e_s, e_t, e_b = edges
+    opt = torch.optim.Adam(ex.parameters(), lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0)
+    criterion = torch.nn.BCEWithLogitsLoss()
+    p0 = {k: v.detach().clone() for k, v in ex.named_parameters()}
+    ex.eval()
+    with torch.no_grad():
+        pos_o, neg_o = base.contrast(src, dst, dst_fake, ts_cut, e_l, sg_s, sg_t, sg_b)
+        y_ori = torch.where(torch.cat([pos_o, neg_o], dim=0).sigmoid() > 0.5, 1., 0.).view(-1, 1)
+    opt.zero_grad()
+    g_s, g_t, g_b = ex(w_s, ts_cut, e_s), ex(w_t, ts_cut, e_t), ex(w_b, ts_cut, e_b)
+    expl = ex.retrieve_explanation(sg_s, g_s, w_s, sg_t, g_t, w_t, sg_b, g_b, w_b, training=False)
+    pos, neg = base.contrast(src, dst, dst_fake, ts_cut, e_l, sg_s, sg_t, sg_b, explain_weights=expl)
+    pred_loss = criterion(torch.cat([pos, neg], dim=0), y_ori)
+    kl = ex.kl_loss(g_s, w_s, target=0.3) + ex.kl_loss(g_t, w_t, target=0.3) + ex.kl_loss(g_b, w_b, target=0.3)
+    loss = pred_loss + 0.5 * kl
+    loss.backward()
+    opt.step()
+    res = {"losses": np.array([loss.item(), pred_loss.item(), kl.item()]),
+           "logits": torch.cat([pos, neg]).detach().numpy()}
+    for k, v in ex.named_parameters():
+        if v.grad is None:
+            continue
+        res[f"grad_{k}"] = v.grad.numpy().astype(np.float32)
+        res[f"upd_{k}"] = (v.detach() - p0[k]).numpy().astype(np.float32)
+    return res
+
+
+def case_enron():
+    """Bench-regime goldens: the full-Enron-shaped graph (V=184, E=125,235,
+    ts in [0, 1e8)) through the reference's own load_data split, pre_processing, marginal and
+    calculate_edge at N=20 and N=30; the reference TempME at Enron dims (de=32, dn=172) scoring those
+    walks (forward x3, retrieve_explanation eval, kl_loss) for the default constructor and the
+    use_temporal_guidance=False / use_dependency_aware_sampling=False / hid_dim=32 variants; and one
+    deterministic training iteration on the reference TGN (as case_train)."""
+    from models.explainer_new import TempME
+    import time as _time
+    g = enron_graph()
+    t0 = _time.time()
+    sampler, src, dst, ts, label, eidx, finder = _enron_load_data(g, "test")
+    res = {"graph_checksum": graph_checksum(g), "graph_params": np.array(json.dumps(ENRON)),
+           "test_src": src.astype(np.int32), "test_dst": dst.astype(np.int32), "test_ts": ts.astype(np.float64),
+           "test_eidx": eidx.astype(np.int32), "test_sampler_dst": sampler.dst_list.astype(np.int32)}
+    print("enron: load_data", round(_time.time() - t0, 1), "s; test events", len(src))
+    for n_deg, n_ev in ENRON_SETS:
+        t0 = _time.time()
+        CTX.update(seed=0, event_base=0)
+        out = run_pipeline(finder, sampler, src, dst, ts, eidx, n_deg, n_ev, f"enron{n_deg}", px.SPLIT_TEST)
+        for k2, v in pack_pipeline(out).items():
+            res[f"test_N{n_deg}_{k2}"] = v
+        print(f"enron: N={n_deg} pipeline of {n_ev} events", round(_time.time() - t0, 1), "s")
+    nf, ef = g["n_feat"], g["e_feat"]
+    for n_deg, n_ev in ENRON_SETS:
+        items, edges, ts_cut, _ = _pack_items(res, f"test_N{n_deg}_", n_deg, n_ev, "test_ts")
+        for var, kw in ENRON_VARIANTS.items():
+            if n_deg == 30 and var != "base":
+                continue
+            tag = f"N{n_deg}_{var}"
+            torch.manual_seed(30 + len(tag))
+            CTX.update(seed=0, split=px.SPLIT_NULL)
+            ctor = dict(out_dim=40, hid_dim=64, temp=0.07, if_cat_feature=True, dropout_p=0.1,
+                        device=torch.device("cpu"))
+            ctor.update(kw)
+            ex = TempME(_Base(nf, ef), base_model_type="tgn", data="uslegis_sampled", **ctor)
+            ex.eval()
+            imp, expl, kl = _explain_outputs(ex, items, edges, ts_cut)
+            for k, v in ex.state_dict().items():
+                if k.startswith(USED_PREFIXES):
+                    res[f"{tag}_w_{k}"] = v.detach().numpy().astype(np.float32)
+            for s, v in zip(("src", "tgt", "bgd"), imp):
+                res[f"{tag}_imp_{s}"] = v.numpy()
+            res[f"{tag}_expl0"], res[f"{tag}_expl1"] = expl[0].numpy(), expl[1].numpy()
+            res[f"{tag}_kl"] = np.array([float(x) for x in kl])
+            print("enron", tag, "imp mean", [round(float(v.mean()), 6) for v in imp], "kl", [float(x) for x in kl])
+    res["null"] = np.array([v for _, v in sorted(ex.null_model.items())])
+    # one training iteration on the reference TGN at N=20 (the Enron+TGN training config, a15)
+    n_deg, n_ev = ENRON_SETS[0]
+    items, edges, ts_cut, _ = _pack_items(res, f"test_N{n_deg}_", n_deg, n_ev, "test_ts")
+    base, _, pert = tgn_base("enron", nf, ef, n_deg)
+    for k, v in pert.items():
+        res[f"train_pert_{k}"] = v
+    torch.manual_seed(40)
+    CTX.update(seed=0, split=px.SPLIT_NULL)
+    ex = TempME(base, base_model_type="tgn", data="uslegis_sampled", out_dim=40, hid_dim=64, temp=0.07,
+                if_cat_feature=True, dropout_p=0.1, device=torch.device("cpu"))
+    for k, v in ex.state_dict().items():
+        if k.startswith(USED_PREFIXES):
+            res[f"train_w_{k}"] = v.detach().numpy().astype(np.float32)
+    tr = _train_iteration(ex, base, src[:n_ev], dst[:n_ev], eidx[:n_ev], ts_cut, items, edges)
+    for k, v in tr.items():
+        res[f"train_{k}"] = v
+    print("enron train loss", tr["losses"])
+    save_npz("enron_goldens.npz", **res)
+
+
 GM_SEEDS = {"uslegis": 21, "synth": 22}
 
 
@@ -696,7 +843,7 @@ def case_graphmixer():
     save_npz("graphmixer_uslegis.npz", **res)
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["kats", "small", "uslegis", "null", "encoder", "tgn", "train", "graphmixer"]
+    which = sys.argv[1:] or ["kats", "small", "uslegis", "null", "encoder", "tgn", "train", "graphmixer", "enron"]
     if "kats" in which:
         case_kats()
     if "small" in which:
@@ -713,3 +860,5 @@ if __name__ == "__main__":
         case_train()
     if "graphmixer" in which:
         case_graphmixer()
+    if "enron" in which:
+        case_enron()

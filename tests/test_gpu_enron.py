@@ -1,0 +1,223 @@
+"""GPU parity in the bench regime: the HIP path through the C ABI on
+the full-Enron-shaped graph (V=184, E=125,235, timestamps in [0, 1e8)) against
+
+* outputs of the reference itself (tests/golden/enron_goldens.npz, make_goldens.py case_enron):
+  sampled fields / categories / marginals / edge counts bit-exact; TempME forward, retrieve_explanation
+  (eval) and kl_loss within rtol 1e-5 / atol 1e-6 for the default constructor and the
+  use_temporal_guidance=False / use_dependency_aware_sampling=False / hid_dim=32 variants, through both
+  the drop-in TempME surface and the bench's ExplainPipeline; one deterministic training iteration
+  (losses, logits, every gradient, the Adam update);
+* the C / torch-fp32 oracle at the bench shapes: 400 events of full Enron at N=20 and 200 events of the
+  1M-edge de=dn=172 graph at N=30 (configs[4]), every sampled field and count bit-exact, the encoder on
+  one reference batch per side.
+"""
+import numpy as np
+import pytest
+import torch
+
+import enron_inputs as EI
+from oracle import encoder_ref as er
+from oracle import oracle as orc
+from oracle import philox as px
+from tests.test_gpu_parity import _Base, _check_events
+
+pytestmark = pytest.mark.gpu
+
+RTOL, ATOL = 1e-5, 1e-6
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a HIP device")
+    return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def z():
+    return EI.golden()
+
+
+@pytest.fixture(scope="module")
+def g(z):
+    return EI.graph(z)
+
+
+@pytest.fixture(scope="module")
+def finder(dev, g):
+    import tempme_amd as tm
+    return tm.NeighborFinder.from_edges(g["src"], g["dst"], g["eidx"], g["ts"], g["n_nodes"], device=dev, seed=0,
+                                        split=px.SPLIT_TEST)
+
+
+def _explainer(dev, g, z, tag, **kw):
+    import tempme_amd as tm
+    ctor = dict(out_dim=40, hid_dim=64)
+    ctor.update(kw)
+    ex = tm.TempME(_Base(g["n_feat"], g["e_feat"], dev), "tgn", "enron", device=dev, null_model=EI.null(z), **ctor)
+    missing, unexpected = ex.load_state_dict(EI.weights(z, tag), strict=False)
+    assert not unexpected
+    return ex.to(dev).eval()
+
+
+@pytest.mark.parametrize("N", sorted(EI.SETS))
+def test_sampling_matches_reference_enron(finder, z, N):
+    _check_events(None, finder, z, f"test_N{N}_", 0, px.SPLIT_TEST, N, 3, z["test_src"], z["test_dst"],
+                  z["test_ts"], z["test_eidx"], z["test_sampler_dst"], EI.SETS[N])
+
+
+@pytest.mark.parametrize("tag", ["N20_base", "N20_notg", "N20_nodep", "N20_h32", "N30_base"])
+def test_dropin_tempme_matches_reference_enron(dev, g, z, tag):
+    """The drop-in surface as eval_one_epoch calls it (temp_exp_main.py:446-452): TempME.forward x3 from
+    the H5 pack's numpy arrays, retrieve_explanation(training=False), kl_loss."""
+    N, var = int(tag[1:3]), tag[4:]
+    ex = _explainer(dev, g, z, tag, **EI.VARIANTS[var])
+    d = EI.walks(z, N)
+    imps, subs, walks = [], [], []
+    for s in EI.SIDES:
+        x = d[s]
+        w = (x["node"], x["eid"], x["ts"], x["cat"], x["marg"])
+        with torch.no_grad():
+            imp = ex(w, d["ts_cut"], x["cnt"])
+        np.testing.assert_allclose(imp.cpu().numpy(), z[f"{tag}_imp_{s}"], rtol=RTOL, atol=ATOL, err_msg=s)
+        imps.append(imp)
+        subs.append((x["sub_node"], x["sub_eid"], x["sub_ts"]))
+        walks.append(w)
+    expl = ex.retrieve_explanation(subs[0], imps[0], walks[0], subs[1], imps[1], walks[1], subs[2], imps[2],
+                                   walks[2], training=False)
+    np.testing.assert_allclose(expl[0].detach().cpu().numpy(), z[f"{tag}_expl0"], rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(expl[1].detach().cpu().numpy(), z[f"{tag}_expl1"], rtol=RTOL, atol=ATOL)
+    for k in range(3):
+        kl = ex.kl_loss(imps[k], walks[k], target=0.3)
+        np.testing.assert_allclose(float(kl), z[f"{tag}_kl"][k], rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.parametrize("edge_table", [True, False])
+@pytest.mark.parametrize("N", sorted(EI.SETS))
+def test_pipeline_matches_reference_enron(dev, finder, g, z, N, edge_table):
+    """The bench's ExplainPipeline (one fused sampling launch, edge tables, table-mode encoder,
+    table-driven explanation) on the golden events = the reference's pre_processing -> TempME.forward x3
+    -> retrieve_explanation(eval) on the same events (one reference batch)."""
+    from tempme_amd.pipeline import ExplainPipeline
+    tag = f"N{N}_base"
+    ex = _explainer(dev, g, z, tag)
+    E = EI.SETS[N]
+    pipe = ExplainPipeline(ex, finder.graph, torch.from_numpy(z["test_sampler_dst"]), N, 3, E, seed=0,
+                           split=px.SPLIT_TEST, edge_table=edge_table)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a[:E], dtype=dt)).to(dev)  # noqa: E731
+    imp, h1, h2 = pipe.run(t(z["test_src"], np.int32), t(z["test_dst"], np.int32), t(z["test_ts"], np.float64),
+                           t(z["test_eidx"], np.int32), torch.arange(E, dtype=torch.int32, device=dev))
+    torch.cuda.synchronize()
+    pipe.check_errors()
+    for s_i, s in enumerate(EI.SIDES):
+        np.testing.assert_allclose(imp[s_i].cpu().numpy(), z[f"{tag}_imp_{s}"][..., 0], rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(h1.reshape(3 * E, N).cpu().numpy(), z[f"{tag}_expl0"], rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(h2.reshape(3 * E, N * N).cpu().numpy(), z[f"{tag}_expl1"], rtol=RTOL, atol=ATOL)
+
+
+def test_train_step_matches_reference_enron(dev, g, z):
+    """One deterministic iteration of the training loop (temp_exp_main.py:605-632, Explainer.eval(),
+    Beta mean) on the reference TGN at Enron dims and timestamps: losses, logits, every gradient that
+    reaches the explainer, and the Adam update."""
+    from tempme_amd import TempME
+    from tempme_amd.train import Batch, train_step
+    N, B = 20, EI.SETS[20]
+    base = EI.build_tgn(z, g).to(dev)
+    ex = TempME(base, "tgn", "enron", out_dim=40, hid_dim=64, temp=0.07, if_cat_feature=True, dropout_p=0.1,
+                device=dev, null_model=EI.null(z))
+    missing, unexpected = ex.load_state_dict(EI.weights(z, "train"), strict=False)
+    assert not unexpected
+    ex = ex.to(dev)
+    d = EI.walks(z, N)
+    pre = f"test_N{N}_"
+    sg = [tuple([z[pre + f"subgraph_{s}_{h}_{k}"][:B].astype(np.float64) for h in (0, 1)]
+                for k in ("node", "eid", "ts")) for s in EI.SIDES]
+    walks = [(d[s]["node"], d[s]["eid"], d[s]["ts"], d[s]["cat"], d[s]["marg"]) for s in EI.SIDES]
+    batch = Batch(z["test_src"][:B].astype(np.int64), z["test_dst"][:B].astype(np.int64), d["ts_cut"],
+                  z["test_eidx"][:B].astype(np.int64), z[pre + "dst_fake"][:B].astype(np.float64), sg, walks,
+                  [d[s]["cnt"] for s in EI.SIDES])
+    opt = torch.optim.Adam(ex.parameters(), lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0)
+    p0 = {k: v.detach().clone() for k, v in ex.named_parameters()}
+    ex.eval()
+    out = train_step(ex, base, opt, batch, beta=0.5, prior_p=0.3, if_bern=False)
+    got = np.array([out["loss"].item(), out["pred_loss"].item(), out["kl_loss"].item()])
+    np.testing.assert_allclose(got, z["train_losses"], rtol=1e-5, atol=1e-6)
+    logits = torch.cat([out["pos_logit"], out["neg_logit"]]).cpu().numpy()
+    np.testing.assert_allclose(logits, z["train_logits"], atol=2e-5, rtol=1e-5)
+    ref_keys = {k[len("train_grad_"):] for k in z.files if k.startswith("train_grad_")}
+    assert {k for k, v in ex.named_parameters() if v.grad is not None} == ref_keys
+    for k, v in ex.named_parameters():
+        if k not in ref_keys:
+            continue
+        gr = z[f"train_grad_{k}"].astype(np.float64)
+        ga = v.grad.detach().cpu().numpy().astype(np.float64)
+        scale = np.abs(gr).max()
+        assert np.linalg.norm(ga - gr) <= 2e-4 * np.linalg.norm(gr) + 1e-9, k
+        assert np.abs(ga - gr).max() <= 1e-8 + 2e-4 * scale, k
+        upd = (v.detach() - p0[k]).cpu().numpy()
+        sure = np.abs(gr) > max(1e-3 * scale, 1e-7)
+        np.testing.assert_allclose(upd[sure], z[f"train_upd_{k}"][sure], atol=2e-6, rtol=1e-3, err_msg=k)
+
+
+def _oracle_check(tm, dev, g, rows, ev, pool, N, E, B, seed, n_batches_enc, ex):
+    """Pipeline on E events vs the C oracle (every sampled field and count) and the torch-fp32 encoder
+    oracle on ``n_batches_enc`` reference batches per side."""
+    from tempme_amd.pipeline import ExplainPipeline
+    src, dst, ts, eidx = ev
+    f = tm.NeighborFinder.from_edges(g["src"][rows], g["dst"][rows], g["eidx"][rows], g["ts"][rows], g["n_nodes"],
+                                     device=dev, seed=seed, split=px.SPLIT_TEST)
+    pipe = ExplainPipeline(ex, f.graph, torch.from_numpy(pool), N, 3, B, seed=seed, split=px.SPLIT_TEST)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a[:E], dtype=dt)).to(dev)  # noqa: E731
+    imp, h1, h2 = pipe.run(t(src, np.int32), t(dst, np.int32), t(ts, np.float64), t(eidx, np.int32),
+                           torch.arange(E, dtype=torch.int32, device=dev))
+    torch.cuda.synchronize()
+    pipe.check_errors()
+    og = orc.OracleGraph(g["src"][rows], g["dst"][rows], g["eidx"][rows], g["ts"][rows], g["n_nodes"])
+    o = orc.event_pipeline(og, seed, px.SPLIT_TEST, N, 3, src[:E], dst[:E], ts[:E], eidx[:E], np.arange(E), pool, 16)
+    b = pipe.buf
+    h = lambda x: x.cpu().numpy()  # noqa: E731
+    assert np.array_equal(h(b.dst_fake[:E]), o["dst_fake"])
+    for name in ("node6", "eid3", "ts3", "cat", "sub1_node", "sub1_eid", "sub1_ts", "sub2_node", "sub2_eid",
+                 "sub2_ts"):
+        assert np.array_equal(h(getattr(b, name)).swapaxes(0, 1), o[name]), name
+    assert np.array_equal(h(b.cnt).swapaxes(0, 1).astype(np.int32), o["cnt"])
+    assert np.array_equal(h(b.hist).astype(np.uint64), o["hist"])
+    sd = {k: v.detach().cpu() for k, v in ex.state_dict().items()}
+    nf, ef = torch.from_numpy(g["n_feat"]), torch.from_numpy(g["e_feat"])
+    for bi in range(n_batches_enc):
+        sl = slice(bi * B, (bi + 1) * B)
+        for s in range(3):
+            ref = er.forward(sd, nf, ef, o["node6"][sl, s], o["eid3"][sl, s], o["ts3"][sl, s], o["cat"][sl, s],
+                             ts[sl], o["cnt"][sl, s].astype(np.float64))
+            np.testing.assert_allclose(h(imp[s, sl]), ref.numpy()[..., 0], rtol=RTOL, atol=ATOL)
+            e0, e1 = er.edge_importance(sd, ef, ref, o["eid3"][sl, s], o["ts3"][sl, s],
+                                        [o["sub1_node"][sl, s], o["sub2_node"][sl, s]],
+                                        [o["sub1_eid"][sl, s], o["sub2_eid"][sl, s]])
+            np.testing.assert_allclose(h(h1[s, sl]), e0.numpy(), rtol=RTOL, atol=ATOL)
+            np.testing.assert_allclose(h(h2[s, sl]), e1.numpy(), rtol=RTOL, atol=ATOL)
+
+
+def test_full_enron_400_events_vs_oracle(dev, g):
+    """configs[2]/[3] bench shape: 400 events (4 reference batches) of the full-Enron graph at N=20, zero
+    node features as the bench runs it, encoder + explanation on two batches per side."""
+    import tempme_amd as tm
+    from tempme_amd.workload import enron_like, split
+    gz = enron_like(n_nodes=184, n_edges=125235, alpha=1.2, seed=0)            # bench.py's graph
+    ev, rows, pool = split(gz)
+    torch.manual_seed(0)
+    ex = tm.TempME(_Base(gz["n_feat"], gz["e_feat"], dev), "tgn", "enron", 40, 64, device=dev,
+                   null_model={k: 1 / 12 for k in range(1, 13)}).to(dev).eval()
+    _oracle_check(tm, dev, gz, rows, ev, pool, 20, 400, 100, 0, 2, ex)
+
+
+def test_1m_edge_200_events_vs_oracle(dev):
+    """configs[4] bench shape: the synthetic 1M-edge graph (V=100,000, Pareto 1.5, de=dn=172 U(0,1)
+    features) at N=30, 200 events; encoder + explanation on one reference batch per side."""
+    import tempme_amd as tm
+    from tempme_amd.workload import enron_like, split
+    gz = enron_like(n_nodes=100000, n_edges=1000000, alpha=1.5, de=172, dn=172, seed=0, node_feat="uniform")
+    ev, rows, pool = split(gz)
+    torch.manual_seed(0)
+    ex = tm.TempME(_Base(gz["n_feat"], gz["e_feat"], dev), "tgn", "synth", 40, 64, device=dev,
+                   null_model={k: 1 / 12 for k in range(1, 13)}).to(dev).eval()
+    _oracle_check(tm, dev, gz, rows, ev, pool, 30, 200, 100, 0, 1, ex)
