@@ -1,26 +1,36 @@
 """bench.py -- explained target-edges/s of the TempME explanation hot path on MI355X.
 
-Metric (BASELINE.json): explained target-edges/sec (TGN+Enron, n_degree=20).  One unit = one
-target event with its fake destination, 2-hop subgraphs x3 sides, temporal walks x3 with
-motif categories and edge counts, encoder forward x3 and retrieve_explanation (eval)
-(SURVEY.md §8(d)); the base TGN's contrast is excluded.
+Metric (BASELINE.json): explained target-edges/sec (TGN+Enron, n_degree=20) at 1/2/4/8 MI355X.  One
+unit = one target event with its fake destination, 2-hop subgraphs x3 sides, temporal walks x3 with
+motif categories and edge counts, encoder forward x3 and retrieve_explanation (eval);
+the base TGN's contrast is excluded.
 
-Workload: BASELINE configs[1] = enron_sampled + TGN explainer scoring on 1 MI355X, n_degree=20.
-Enron is not available offline, so the graph is a seeded synthetic replica of its shape
-(tempme_amd/workload.py: V=183, E=18,780, Pareto(1.2) endpoints, ts in [0, 1e8), de=32,
-dn=172); explainer weights are a seeded random init of the TempME architecture.
+Workload (default --config 2): the metric's own graph, full Enron (V=184 nodes, E=125,235 edges; the
+graph of BASELINE configs[2]/[3]) + TGN explainer scoring at n_degree=20.  Enron is not available
+offline, so the graph is a seeded synthetic replica of its shape (tempme_amd/workload.py: Pareto(1.2)
+endpoints, ts in [0, 1e8), de=32, dn=172); explainer weights are a seeded random init of the TempME
+architecture.  --config 1 = configs[1] (enron_sampled shape, E=18,780), --config 4 = configs[4]
+(synthetic 1M-edge graph, de=dn=172, N=30, the HBM stress case).
 
-A step = one pass of the hot path over one batch of synthetic input: --batches reference
-batches of --batch-size (default 64 x 100 = 6,400) target events per GPU, all on-device
-(tm_sample_events -> tm_encoder_fwd -> tm_edge_importance).  Multi-GPU: one process per GPU
-(torch.distributed.run), whole batches sharded across ranks, no data-path collective
-(weak scaling); barrier + max-over-ranks timing.
+A step = one pass of the hot path over one global batch of synthetic target events already resident
+in HBM: --batches reference batches of --batch-size events (default 64 x 100 = 6,400), all on-device
+(tm_sample_events -> tm_edge_tables -> tm_encoder_fwd_tab -> tm_edge_importance_tab).
 
-Run:  python bench.py [--gpus N --steps K --warmup W]
+Multi-GPU: `python bench.py --gpus N` starts its own N ranks (torch.distributed.run, one process per
+GPU) when it is not already running under a launcher; the driver's `torch.distributed.run ... bench.py
+--gpus N` works the same way.  Whole reference batches are sharded across ranks with no data-path
+collective (the graph, tables and weights are replicated per GPU).  The primary line is STRONG scaling:
+the global batch of one step is fixed and dealt over the ranks (64 / N batches each); the weak-scaling
+figure (64 batches per rank) is reported beside it as "weak".  Barrier + synchronize bracket the timed
+region and the time is the max over ranks.
+
+Run:  python bench.py [--gpus N --steps K --warmup W --config {1,2,4}]
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -34,38 +44,89 @@ METRIC = "explained target-edges/sec (TGN+Enron, n_degree=20) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
 FP32_MFMA_PEAK_TF = 157.3      # MI355X_MICROARCH.md: FP32 matrix (spec)
 
+CONFIGS = {
+    1: dict(name="enron_sampled", graph=dict(n_nodes=183, n_edges=18780), N=20,
+            workload="configs[1]: enron_sampled-shaped synthetic graph (V=183, E=18,780, Pareto {alpha}) + TGN "
+                     "explainer scoring, n_degree={N}"),
+    2: dict(name="enron", graph=dict(n_nodes=184, n_edges=125235), N=20,
+            workload="metric config: full Enron shape (V=184, E=125,235, Pareto {alpha}; the graph of configs[2]/[3]) "
+                     "+ TGN explainer scoring, n_degree={N}"),
+    4: dict(name="synth1m", graph=dict(n_nodes=100000, n_edges=1000000, alpha=1.5, de=172, dn=172,
+                                       node_feat="uniform"), N=30,
+            workload="configs[4]: synthetic 1M-edge temporal graph (V=100,000, Pareto 1.5, de=dn=172 U(0,1) "
+                     "features), TempME explanation scoring, n_degree={N}"),
+}
 
+
+# ----------------------------------------------------------------------------------------------- launcher
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(n):
+    """Start n ranks of this script under torch.distributed.run as a CHILD process (nothing has touched the
+    GPU yet in this process) and return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+# ----------------------------------------------------------------------------------------------- models
 def flops_model(de, dn, h, N, M, etab=False):
-    """Algorithmic MACs per unit for each encoder kernel.  ``etab``: the
-    pipeline's edge table (lin_event's de x dn edge part once per edge id in the gate-table launch,
-    not per executed walk position)."""
+    """MACs x2 per unit for each encoder kernel.  ``walk_kernel``: the SURVEY.md §8(a) a12 model (3 walk
+    positions + head), minus the 3 de x dn edge-feature MACs per walk that the edge table (``etab``) does once
+    per edge id.  ``walk_kernel_executed``: what the kernel actually issues -- position 2 once per hop-1 slot
+    (shared by its M walks), the all-time-feature K steps of lin_event there folded into a bias (dt = 0),
+    the attention's duplicated 2h x 2h W1 product once per slot."""
     kev = de + 3 + dn
     per_pos_gcn = kev * dn + 2 * (dn * h + h * h)                       # lin_event + event_gcn MLP x2
     per_walk_head = 3 * (2 * h) ** 2 + (2 * h) * h + h * h + (h + 12) ** 2 + (h + 12) * h + h + 2 * 2 * h
     per_pos_gate = (de + dn) * h + h * (h // 2) + h // 2
     W = N * M
-    # walk_kernel executes position 2 once per hop-1 slot (shared by the M walks of the slot), and
-    # there the all-time-feature K steps of lin_event (dt = 0: constant) are folded into a bias
     qt = (de + 3 + 15) // 16
     exec_walk = 2 * ((2 + 1.0 / M) * per_pos_gcn + per_walk_head - (1 - 1.0 / M) * (2 * h) ** 2
                      - max(kev - 16 * qt, 0) * dn / M)
     walk = 2 * (3 * per_pos_gcn + per_walk_head)
     if etab:
-        # the per-position edge-feature product (de x dn MACs) is done per edge id by the table
-        # launch: the walk kernel is credited with the rest of the SURVEY model only
         exec_walk -= 2 * (2 + 1.0 / M) * de * dn
         walk -= 2 * 3 * de * dn
-    return dict(gcn_kernel=2 * per_pos_gcn * 3, head_kernel=2 * per_walk_head, explain_kernel=2 * per_pos_gate * 3,
-                walk_kernel=walk, walk_kernel_executed=exec_walk,
-                gate_per_edge=2 * per_pos_gate + (2 * de * dn if etab else 0),
-                per_walk=2 * (3 * per_pos_gcn + per_walk_head + 3 * per_pos_gate), W=W)
+    return dict(walk_kernel=walk, walk_kernel_executed=exec_walk,
+                gate_per_edge=2 * per_pos_gate + (2 * de * dn if etab else 0), W=W,
+                per_walk=2 * (3 * per_pos_gcn + per_walk_head + 3 * per_pos_gate))
 
 
+def sampling_bytes_per_event(N, M):
+    """SURVEY.md §8(d) compulsory-traffic model for (a)+(b), per target event (3 sides)."""
+    W = N * M
+    khop = (N + N * N) * 16 + (N + N * N) * 12 + (1 + N) * 32
+    walks = N * 128 + W * 188
+    return 3 * (khop + walks)
+
+
+def khop_bytes_per_event(N):
+    """SURVEY.md §8(d) compulsory traffic of the k-hop kernel (a1-a4) alone, per target event (3 sides)."""
+    return 3 * ((N + N * N) * 16 + (N + N * N) * 12 + (1 + N) * 32)
+
+
+def load_traffic(cfg_name):
+    """profiles/pmc_traffic_<config>.json (tools/pmc_summary.py --traffic): per-launch HBM bytes (FETCH_SIZE x 2
+    + WRITE_SIZE, MI355X_MICROARCH.md §HBM) of every kernel instance of a PMC run of this config, and the
+    instance the bench's timing name maps to (the one launched most often)."""
+    p = os.path.join(HERE, "profiles", f"pmc_traffic_{cfg_name}.json")
+    if not os.path.exists(p):
+        return {}, None
+    with open(p) as fh:
+        d = json.load(fh)
+    return d.get("by_bench_name", {}), os.path.relpath(p, HERE)
+
+
+# ----------------------------------------------------------------------------------------------- legs
 def aux_rows(finder, src, dst, ts, eidx, pool, graph_build_ms):
     """SURVEY §8 rows outside the per-step unit, timed once (not part of ``value``): a1 the CSR build
-    (NeighborFinder.__init__: host sort + per-edge tables + upload) and a11 the null model's sampling
-    and counting (utils/null_model.py pre_processing + statistic: 500 events, num_neighbors 30, one
-    walk per slot), which the reference spends 2.7-3.2 s on per TempME construction."""
+    (NeighborFinder.__init__) and a11 the null model's sampling and counting (utils/null_model.py
+    pre_processing + statistic: 500 events, num_neighbors 30, one walk per slot)."""
     from tempme_amd.batch_loader import RandEdgeSampler
     from tempme_amd.null_model import null_counts
     from tempme_amd import _lib as L
@@ -79,18 +140,11 @@ def aux_rows(finder, src, dst, ts, eidx, pool, graph_build_ms):
             "null_model_ms": round(null_ms, 3), "null_model_walks": int(cnt.sum())}
 
 
-def khop_bytes_per_event(N):
-    """SURVEY.md §8(d) compulsory traffic of the k-hop kernel (a1-a4) alone, per target event (3 sides)."""
-    return 3 * ((N + N * N) * 16 + (N + N * N) * 12 + (1 + N) * 32)
-
-
 def khop_alone(pipe, inputs, steps, N, group=8):
     """The (a) kernel measured alone (the >= 50 % HBM target applies to it): 2-hop
-    sampling of the three sides of the events of ``group`` steps per call -- src and dst on the e_idx
-    path, the pipeline's fake dst on the time path -- as three independent tm_sample_khop calls on
-    three streams, timed from the first launch to the last completion (HIP events).  One step's 6,400
-    roots per call leave a ~10 us launch/ramp/drain overhead exposed; ``group`` steps per call measure
-    the kernel's throughput."""
+    sampling of the three sides of ``group`` steps' events per call -- src and dst on the e_idx path, the
+    pipeline's fake dst on the time path -- as three tm_sample_khop calls on three streams, timed from the
+    first launch to the last completion (HIP events on the launch streams)."""
     from tempme_amd import _lib as L
     g = pipe.graph
     dev = inputs[0][0].device
@@ -100,9 +154,8 @@ def khop_alone(pipe, inputs, steps, N, group=8):
         fakes = []
         for src, dst, ts, eidx, ev in chunk:
             pipe.sample(src, dst, ts, eidx, ev)      # fake dst of these events (not timed)
-            fakes.append(pipe.buf.dst_fake.clone())
-        cat = [torch.cat([c[j] for c in chunk]) for j in range(5)]
-        src, dst, ts, eidx, ev = cat
+            fakes.append(pipe.buf.dst_fake[:src.numel()].clone())
+        src, dst, ts, eidx, ev = [torch.cat([c[j] for c in chunk]) for j in range(5)]
         plans.append((ts, ev, ((L.SIDE_SRC, src, eidx), (L.SIDE_TGT, dst, eidx), (L.SIDE_BGD, torch.cat(fakes), None))))
     E = int(plans[0][0].numel())
     tot = E * (N + N * N)
@@ -127,26 +180,75 @@ def khop_alone(pipe, inputs, steps, N, group=8):
         ms.append(a.elapsed_time(b))
     ms = ms[len(plans):]
     L.raise_device_error(int(err.item()), "khop_alone")
-    per_step_ms = sum(ms) / len(ms)
-    ach = khop_bytes_per_event(N) * E / (per_step_ms * 1e-3) / 1e9
+    per_call_ms = sum(ms) / len(ms)
+    ach = khop_bytes_per_event(N) * E / (per_call_ms * 1e-3) / 1e9
     return {"kernel": "khop2_kernel (tm_sample_khop k=2), 3 sides on 3 streams", "roots_per_call": E,
-            "avg_ms": round(per_step_ms, 4), "launches": 3 * len(ms), "bound": "hbm", "achieved": round(ach, 1),
+            "avg_ms": round(per_call_ms, 4), "launches": 3 * len(ms), "bound": "hbm", "achieved": round(ach, 1),
             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_event": khop_bytes_per_event(N)}
 
 
-def sampling_bytes_per_event(N, M):
-    """SURVEY.md §8(d) compulsory-traffic model for (a)+(b), per target event (3 sides)."""
-    W = N * M
-    khop = (N + N * N) * 16 + (N + N * N) * 12 + (1 + N) * 32
-    walks = N * 128 + W * 188
-    return 3 * (khop + walks)
+def dropin_leg(ex, pipe, inputs, B, N, budget_s=3.0):
+    """The reference's eval_one_epoch call pattern through the drop-in surface (temp_exp_main.py:446-452):
+    per batch, ``get_item`` / ``get_item_edge`` of a host pack (numpy, float64 as after the H5 round trip),
+    TempME.forward x3 from numpy, then retrieve_explanation(training=False); timed from host arrays to
+    device outputs.  The pack is the pipeline's own sample of one step's events (tempme_amd/pack.py)."""
+    from tempme_amd import pack as P
+    src, dst, ts, eidx, ev = inputs[0]
+    pipe.sample(src, dst, ts, eidx, ev)
+    _, cat_d, edge = P.buffers_to_arrays(pipe.buf, int(src.numel()))
+
+    class A:
+        n_degree = N
+    pk = P.load_subgraph_margin(A(), cat_d)
+    cut = ts.cpu().numpy()
+    n_b = int(src.numel()) // B
+
+    def one(b):
+        idx = np.arange(b * B, (b + 1) * B)
+        sg_s, sg_t, sg_b, w_s, w_t, w_b, _ = P.get_item(pk, idx)
+        e_s, e_t, e_b = P.get_item_edge(edge, idx)
+        with torch.no_grad():
+            i_s, i_t, i_b = ex(w_s, cut[idx], e_s), ex(w_t, cut[idx], e_t), ex(w_b, cut[idx], e_b)
+            return ex.retrieve_explanation(sg_s, i_s, w_s, sg_t, i_t, w_t, sg_b, i_b, w_b, training=False)
+
+    for b in range(min(n_b, 4)):
+        one(b)
+    torch.cuda.synchronize()
+    done, t0 = 0, time.perf_counter()
+    while True:
+        one(done % n_b)
+        done += 1
+        if done % n_b == 0 or done >= 4 * n_b:
+            torch.cuda.synchronize()
+            if time.perf_counter() - t0 > budget_s or done >= 4 * n_b:
+                break
+    el = time.perf_counter() - t0
+    return {"value": round(done * B / el, 2), "unit": "edges/s", "batches": done, "batch_size": B,
+            "ms_per_batch": round(el / done * 1e3, 3),
+            "what": "eval_one_epoch pattern: get_item from a host float64 pack, TempME.forward x3 from numpy, "
+                    "retrieve_explanation(training=False), per reference batch, host arrays -> device outputs"}
+
+
+def _cpu_cores():
+    """Cores this process may run on (= nproc), limited by a cgroup CPU quota when one is set."""
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    use = cores if quota is None else max(1, min(cores, int(quota)))
+    return use, cores, quota
 
 
 def cpu_baseline(g, rows, events, pool, N, M, B, seed, sd, budget_s=12.0, max_batches=400):
     """The oracle port (C sampler + torch-fp32 encoder) on the host cores, bounded sample."""
     from oracle import encoder_ref as er
     from oracle import oracle as orc
-    threads = int(os.environ.get("TEMPME_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    use, nproc, quota = _cpu_cores()
+    threads = int(os.environ.get("TEMPME_CPU_THREADS", use))
     torch.set_num_threads(threads)
     src, dst, ts, eidx = events
     og = orc.OracleGraph(g["src"][rows], g["dst"][rows], g["eidx"][rows], g["ts"][rows], g["n_nodes"])
@@ -167,10 +269,72 @@ def cpu_baseline(g, rows, events, pool, N, M, B, seed, sd, budget_s=12.0, max_ba
                                    [o["sub1_eid"][:, s], o["sub2_eid"][:, s]])
         done += B
     el = time.perf_counter() - t0
-    return {"value": round(done / el, 2), "unit": "edges/s", "cores": threads, "kind": "port",
+    return {"value": round(done / el, 2), "unit": "edges/s", "cores": threads, "kind": "port", "nproc": nproc,
+            "cgroup_cpu_quota": quota,
             "sample": f"{done} target events ({done // B} reference batches of {B}) of the same workload: "
                       f"oracle/tempme_oracle.c sampling+motif ({threads} OpenMP threads) + oracle/encoder_ref.py "
                       f"torch-fp32 encoder+explanation ({threads} threads), {el:.1f} s"}
+
+
+# ----------------------------------------------------------------------------------------------- timing
+def timed(run_step, pipes, inputs, warmup, steps, dist, backend, dev, L):
+    """W untimed warm-up steps, then EXACTLY K steps bracketed by barrier + synchronize; max over ranks."""
+    from tempme_amd.sharding import max_over_ranks
+    for k in range(warmup):
+        run_step(inputs[k % len(inputs)])
+    torch.cuda.synchronize()
+    for p in pipes:
+        p.check_errors()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    L.profile_enable(True)
+    t0 = time.perf_counter()
+    for k in range(warmup, warmup + steps):
+        run_step(inputs[k % len(inputs)])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    prof = L.profile_read()
+    L.profile_enable(False)
+    for p in pipes:
+        p.check_errors()
+    return max_over_ranks(el, dist, dev if backend == "nccl" else "cpu"), prof
+
+
+def make_inputs(n_steps, rank, world, per_rank, events, dev):
+    from tempme_amd.sharding import shard_events
+    src, dst, ts, eidx = events
+    to = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)  # noqa: E731
+    out = []
+    for k in range(n_steps):
+        i, ev = shard_events(k, rank, world, per_rank, len(src))
+        out.append((to(src[i], np.int32), to(dst[i], np.int32), to(ts[i], np.float64), to(eidx[i], np.int32),
+                    to(ev.view(np.int32), np.int32)))
+    return out
+
+
+def kernel_table(prof, units, executed):
+    kernels = {}
+    for name, (ms, cnt) in prof.items():
+        avg_ms = ms / max(cnt, 1)
+        ent = {"avg_ms": round(avg_ms, 4), "launches": cnt}
+        if name in units:
+            bound, work = units[name]
+            if bound == "hbm":
+                ach = work / (avg_ms * 1e-3) / 1e9
+                ent.update(bound="hbm", achieved=round(ach, 1), unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4))
+            else:
+                ach = work / (avg_ms * 1e-3) / 1e12
+                ent.update(bound="mfma", credited_tflops=round(ach, 2), credited_frac=round(ach / FP32_MFMA_PEAK_TF, 4))
+                if name in executed:
+                    ex_tf = executed[name] / (avg_ms * 1e-3) / 1e12
+                    ent.update(achieved=round(ex_tf, 2), unit="TFLOP/s", frac=round(ex_tf / FP32_MFMA_PEAK_TF, 4))
+                else:
+                    ent.update(achieved=round(ach, 2), unit="TFLOP/s", frac=round(ach / FP32_MFMA_PEAK_TF, 4))
+        kernels[name] = ent
+    return kernels
 
 
 def main():
@@ -178,72 +342,71 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batches", type=int, default=64, help="reference batches per step per GPU")
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS),
+                    help="BASELINE.json configs[i] graph: 2 = full Enron (the metric's config, default), "
+                         "1 = enron_sampled, 4 = synthetic 1M-edge de=dn=172 N=30")
+    ap.add_argument("--batches", type=int, default=64, help="reference batches per step (global, strong scaling)")
     ap.add_argument("--batch-size", type=int, default=100, help="temp_exp_main --test_bs")
-    ap.add_argument("--n-degree", type=int, default=20)
+    ap.add_argument("--n-degree", type=int, default=None)
     ap.add_argument("--alpha", type=float, default=1.2)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--strong", action="store_true",
-                    help="strong scaling: --batches is the whole step, split over the ranks (default: per rank)")
+    ap.add_argument("--no-extras", action="store_true", help="skip the k-hop-alone, drop-in and aux legs")
+    ap.add_argument("--weak", action="store_true", help="primary line weak scaling (--batches per rank)")
     ap.add_argument("--no-edge-table", action="store_true",
                     help="lin_event's edge-feature product per walk position instead of per edge id")
-    ap.add_argument("--streams", type=int, default=1,
-                    help="steps in flight (PipelinedExplainer): step k runs on stream k %% S with its own "
-                         "buffers, so its sampling and explanation kernels overlap the neighbouring steps' "
-                         "encoder kernel (encoders chained: +5 %% at 8 batches per step, none at 64)")
-    ap.add_argument("--config", type=int, default=1, choices=(1, 2, 4),
-                    help="BASELINE.json configs[i] workload: 1 = enron_sampled + TGN, N=20 (the headline); "
-                         "2 = full Enron shape (E=125,235), N=20; 4 = synthetic 1M-edge graph, de=dn=172, "
-                         "Pareto 1.5, N=30 (the HBM stress case)")
+    ap.add_argument("--streams", type=int, default=1, help="steps in flight (PipelinedExplainer)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks, form the process group and report it (no GPU work)")
     args = ap.parse_args()
-    if args.config == 4 and args.n_degree == 20:
-        args.n_degree = 30
+    cfg = CONFIGS[args.config]
+    N = args.n_degree or cfg["N"]
 
+    # ---- one process per GPU: start our own ranks unless a launcher already did (before any GPU call)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    # one process per GPU; TEMPME_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks
-    # sharing the GPUs there are (ranks map to local_rank % device_count)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks")
+    # TEMPME_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks sharing the GPUs there are
     backend = os.environ.get("TEMPME_DIST_BACKEND", "nccl")
-    dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
+    dist = None
+    if args.launch_check:
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            t = torch.ones(1)
+            dist.all_reduce(t)
+            if rank == 0:
+                print(json.dumps({"n_gpus": world, "ranks_in_group": int(t.item()), "backend": "gloo"}), flush=True)
+            dist.destroy_process_group()
+        else:
+            print(json.dumps({"n_gpus": 1, "ranks_in_group": 1}), flush=True)
+        return
+    n_dev = torch.cuda.device_count()
+    if backend == "nccl" and world > n_dev:
+        raise SystemExit(f"bench.py: {world} ranks but {n_dev} GPUs visible")
+    dev = torch.device("cuda", local % max(n_dev, 1))
+    torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(dev)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-    torch.cuda.set_device(dev)
 
     import tempme_amd as tm
     from tempme_amd import _lib as L
     from tempme_amd.pipeline import ExplainPipeline, PipelinedExplainer
-    from tempme_amd.sharding import max_over_ranks, shard_events
     from tempme_amd.workload import enron_like, split
 
-    N, M, B = args.n_degree, 3, args.batch_size
-    if args.strong:
-        # strong scaling: the step's args.batches reference batches are dealt over the ranks
-        if args.batches % world:
-            raise SystemExit(f"--strong needs --batches divisible by the {world} ranks")
-        E = args.batches // world * B
-    else:
-        E = args.batches * B
-    if args.config == 1:
-        g = enron_like(alpha=args.alpha, seed=args.seed)
-        workload = ("configs[1]: enron_sampled-shaped synthetic graph (V=183, E=18,780, "
-                    f"Pareto {args.alpha}) + TGN explainer scoring, n_degree={args.n_degree}")
-    elif args.config == 2:
-        g = enron_like(n_nodes=184, n_edges=125235, alpha=args.alpha, seed=args.seed)
-        workload = (f"configs[2]: full-Enron-shaped synthetic graph (V=184, E=125,235, Pareto {args.alpha}), "
-                    f"TempME encoder + explanation, n_degree={args.n_degree}")
-    else:
-        g = enron_like(n_nodes=100000, n_edges=1000000, alpha=1.5, de=172, dn=172, seed=args.seed,
-                       node_feat="uniform")
-        workload = ("configs[4]: synthetic 1M-edge temporal graph (V=100,000, Pareto 1.5, de=dn=172 U(0,1) "
-                    f"features), TempME explanation scoring, n_degree={args.n_degree}")
+    M, B = 3, args.batch_size
+    gkw = dict(cfg["graph"])
+    gkw.setdefault("alpha", args.alpha)
+    g = enron_like(seed=args.seed, **gkw)
+    workload = cfg["workload"].format(alpha=gkw["alpha"], N=N)
     (src, dst, ts, eidx), rows, pool = split(g)
     torch.zeros(1, device=dev)                     # device context and allocator up before timing the build
     torch.cuda.synchronize()
@@ -260,7 +423,7 @@ def main():
         edge_raw_features = torch.nn.Embedding.from_pretrained(e_feat_th, padding_idx=0, freeze=True)
 
     torch.manual_seed(args.seed)
-    ex = tm.TempME(Base(), "tgn", "enron_sampled", out_dim=40, hid_dim=64, device=dev,
+    ex = tm.TempME(Base(), "tgn", cfg["name"], out_dim=40, hid_dim=64, device=dev,
                    null_model={k: 1.0 / 12 for k in range(1, 13)}).to(dev).eval()
     S = max(1, args.streams)
     if S == 1:
@@ -268,118 +431,79 @@ def main():
                                edge_table=not args.no_edge_table)
         pipes = [pipe]
 
-        def run_step(k):
-            pipe.run(*inputs[k])
+        def run_step(x):
+            pipe.run(*x)
     else:
         flight = PipelinedExplainer(ex, finder.graph, torch.from_numpy(pool), N, M, B, seed=args.seed, depth=S,
                                     edge_table=not args.no_edge_table)
         pipes = flight.pipes
         pipe = pipes[0]
 
-        def run_step(k):
-            flight.submit(*inputs[k])
+        def run_step(x):
+            flight.submit(*x)
 
-    # inputs for every step resident in HBM before timing: events cycle through the test split
     n_steps = args.warmup + args.steps
-    to = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)  # noqa: E731
-    inputs = []
-    for k in range(n_steps):
-        i, ev = shard_events(k, rank, world, E, len(src))
-        inputs.append((to(src[i], np.int32), to(dst[i], np.int32), to(ts[i], np.float64), to(eidx[i], np.int32),
-                       to(ev.view(np.int32), np.int32)))
-
-    for k in range(max(args.warmup, S)):        # every stream's buffers allocated before timing
-        run_step(k % n_steps)
-    torch.cuda.synchronize()
-    for p in pipes:
-        p.check_errors()
-
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    L.profile_enable(True)
-    t0 = time.perf_counter()
-    for k in range(args.warmup, n_steps):
-        run_step(k)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    prof = L.profile_read()
-    L.profile_enable(False)
-    for p in pipes:
-        p.check_errors()
-    el = max_over_ranks(el, dist, dev if backend == "nccl" else "cpu")
+    strong = not args.weak
+    if strong and args.batches % world:
+        raise SystemExit(f"bench.py: --batches {args.batches} is not divisible by the {world} ranks")
+    per_rank = (args.batches // world if strong else args.batches) * B
+    inputs = make_inputs(n_steps, rank, world, per_rank, (src, dst, ts, eidx), dev)
+    for k in range(S):                             # every stream's buffers allocated before timing
+        run_step(inputs[k % n_steps])
+    el, prof = timed(run_step, pipes, inputs, args.warmup, args.steps, dist, backend, dev, L)
+    weak = None
+    if world > 1:
+        # the secondary figure: the other scaling mode on the same ranks
+        per_rank2 = (args.batches if strong else args.batches // world) * B
+        inputs2 = make_inputs(n_steps, rank, world, per_rank2, (src, dst, ts, eidx), dev)
+        run_step(inputs2[0])
+        el2, _ = timed(run_step, pipes, inputs2, args.warmup, args.steps, dist, backend, dev, L)
+        weak = {"scaling": "weak" if strong else "strong", "value": round(world * args.steps * per_rank2 / el2, 2),
+                "ms_per_step": round(el2 / args.steps * 1e3, 3), "events_per_step_per_gpu": per_rank2}
 
     if rank == 0:
+        E = per_rank
         fm = flops_model(g["e_feat"].shape[1], g["n_feat"].shape[1], 64, N, M, etab=pipe.etab is not None)
         W = fm["W"]
         units = {"events_kernel": ("hbm", sampling_bytes_per_event(N, M) * E),
-                 "gcn_kernel": ("mfma", fm["gcn_kernel"] * 3 * E * W),
-                 "head_kernel": ("mfma", fm["head_kernel"] * 3 * E * W),
-                 "explain_kernel": ("mfma", fm["explain_kernel"] * 3 * E * W),
-                 "gate_table_kernel": ("mfma", fm["gate_per_edge"] * (g["eidx"].max() + 1)),
+                 "gate_table_kernel": ("mfma", fm["gate_per_edge"] * (int(g["eidx"].max()) + 1)),
                  "walk_kernel": ("mfma", fm["walk_kernel"] * 3 * E * W)}
         executed = {"walk_kernel": fm["walk_kernel_executed"] * 3 * E * W}
-        kernels = {}
-        for name, (ms, cnt) in prof.items():
-            avg_ms = ms / max(cnt, 1)
-            ent = {"avg_ms": round(avg_ms, 4), "launches": cnt}
-            if name in units:
-                bound, work = units[name]
-                if bound == "hbm":
-                    ach = work / (avg_ms * 1e-3) / 1e9
-                    ent.update(bound="hbm", achieved=round(ach, 1), unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4))
-                else:
-                    ach = work / (avg_ms * 1e-3) / 1e12
-                    ent.update(bound="mfma", achieved=round(ach, 2), unit="TFLOP/s",
-                               frac=round(ach / FP32_MFMA_PEAK_TF, 4))
-                    if name in executed:
-                        ex_tf = executed[name] / (avg_ms * 1e-3) / 1e12
-                        ent.update(executed_tflops=round(ex_tf, 2), executed_frac=round(ex_tf / FP32_MFMA_PEAK_TF, 4))
-            kernels[name] = ent
+        kernels = kernel_table(prof, units, executed)
+        traffic, tsrc = load_traffic(cfg["name"])
         dom = max((k for k in kernels if "bound" in kernels[k]), key=lambda k: kernels[k]["avg_ms"])
         d = kernels[dom]
         roof = {"bound": d["bound"], "achieved": d["achieved"],
                 "peak": HBM_PEAK_GBS if d["bound"] == "hbm" else FP32_MFMA_PEAK_TF, "unit": d["unit"],
-                "frac": d["frac"], "traffic": None, "kernel": dom}
-        pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
-            with open(pmc) as fh:
-                tr = json.load(fh).get(dom)
-            if tr is not None:
-                roof["traffic"] = tr
-        total = world * args.steps * E
+                "frac": d["frac"], "traffic": traffic.get(dom), "kernel": dom}
+        if dom in executed:
+            roof["credited_frac"] = d["credited_frac"]
+            roof["note"] = ("achieved/frac = FLOPs the kernel executes (position 2 once per hop-1 slot, time-only "
+                            "K steps folded, edge-feature product in the edge table); credited_frac = the SURVEY "
+                            "§8(d) per-walk model minus the edge-table MACs, for the same launch time")
+        if tsrc:
+            roof["traffic_source"] = tsrc
+        samp = dict(kernels.get("events_kernel", {}))
+        if samp and traffic.get("events_kernel") is not None:
+            samp["traffic"] = traffic["events_kernel"]
+        total = world * args.steps * per_rank
         out = {"metric": METRIC, "value": round(total / el, 2), "unit": "edges/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
-               "higher_is_better": True, "scaling": "strong" if args.strong else "weak", "vs_baseline": None,
+               "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
                "dtype": "fp32",
                "data": "synthetic (seeded graph of the config's shape, random-init TempME weights)",
-               "config": {"workload": workload,
-                          "n_degree": N, "walks_per_slot": M, "batch_size": B, "batches_per_step_per_gpu": E // B,
-                          "events_per_step_per_gpu": E, "parallelism": f"dp{world} (whole batches per rank)",
+               "config": {"workload": workload, "config": f"configs[{args.config}]" if args.config != 2 else
+                          "metric (full Enron + TGN, n_degree=20)", "n_degree": N, "walks_per_slot": M,
+                          "batch_size": B, "global_batches_per_step": per_rank * world // B,
+                          "events_per_step_per_gpu": per_rank, "parallelism": f"dp{world} (whole batches per rank)",
                           "steps_in_flight": S},
-               "roofline": roof, "kernels": kernels,
-               "sampling_roofline": kernels.get("events_kernel")}
-        if S > 1:
-            # with steps in flight the sampling kernel runs in the encoder's shadow (its launch duration
-            # then measures co-residency, not the kernel): its roofline comes from a pass with one step
-            # in flight, right after the timed region
-            L.profile_enable(True)
-            for k in range(min(args.steps, 5)):
-                pipe.run(*inputs[k])
-            torch.cuda.synchronize()
-            iso = L.profile_read()
-            L.profile_enable(False)
-            ms, cnt = iso["events_kernel"]
-            avg_ms = ms / max(cnt, 1)
-            ach = units["events_kernel"][1] / (avg_ms * 1e-3) / 1e9
-            kernels["events_kernel"]["note"] = "launch duration while overlapping the previous step's walk_kernel"
-            out["sampling_roofline"] = {"avg_ms": round(avg_ms, 4), "launches": cnt, "bound": "hbm",
-                                        "achieved": round(ach, 1), "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                                        "measured": "one step in flight (not overlapped), after the timed region"}
-        out["khop_roofline"] = khop_alone(pipe, inputs, min(args.steps, 5), N, group=8)
-        out["aux"] = aux_rows(finder, src, dst, ts, eidx, pool, graph_build_ms)
+               "roofline": roof, "kernels": kernels, "sampling_roofline": samp or None}
+        if weak is not None:
+            out["weak" if strong else "strong"] = weak
+        if not args.no_extras:
+            out["khop_roofline"] = khop_alone(pipe, inputs, min(args.steps, 5), N, group=8)
+            out["dropin"] = dropin_leg(ex, pipe, inputs, B, N)
+            out["aux"] = aux_rows(finder, src, dst, ts, eidx, pool, graph_build_ms)
         if world == 1 and not args.no_cpu_baseline:
             sd = {k: v.detach().cpu() for k, v in ex.state_dict().items()}
             out["cpu_baseline"] = cpu_baseline(g, rows, (src, dst, ts, eidx), pool, N, M, B, args.seed, sd)

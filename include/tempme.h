@@ -305,6 +305,11 @@ int tm_edge_table_cols(const tm_weights *w);
 int tm_edge_tables(const tm_weights *w, const tm_graph *g, const float *e_feat, float *out_gf, float *out_etab,
                    void *stream);
 
+/* The edge table alone, without a graph (the drop-in TempME.forward's table mode): out_etab [n_ids][cols]
+ * for the edge ids [0, n_ids) of the edge-feature table e_feat [n_ids][de]; same values as tm_edge_tables'.
+ * Replaces the per-position E(e) product of explainer_new.py:79-96 (event_conv.lin_event). */
+int tm_edge_feature_table(const tm_weights *w, const float *e_feat, int32_t n_ids, float *out_etab, void *stream);
+
 /* tm_edge_importance driven by a gate table (n_ids entries): bit-identical outputs, no per-walk
  * gate MLP.  *err_flag (nullable) is set if a walk edge id is outside the table. */
 int tm_edge_importance_tab(const float *gf, int32_t n_ids, int32_t n_groups, int32_t B, int32_t W, int32_t N,

@@ -37,7 +37,7 @@ EXPORTS = (
     "tm_encoder_workspace_bytes",
     "tm_encoder_fwd", "tm_encoder_fwd_tab", "tm_encoder_train_fwd", "tm_encoder_bwd", "tm_encoder_wgrad", "tm_wgrad",
     "tm_explain_train_fwd", "tm_explain_train_bwd", "tm_kl_loss", "tm_edge_importance", "tm_edge_gate_table",
-    "tm_edge_table_cols", "tm_edge_tables", "tm_edge_importance_tab", "tm_tgn_attn_fwd", "tm_tgn_attn_bwd",
+    "tm_edge_table_cols", "tm_edge_tables", "tm_edge_feature_table", "tm_edge_importance_tab", "tm_tgn_attn_fwd", "tm_tgn_attn_bwd",
     "tm_mask_least_important", "tm_profile_enable", "tm_profile_sync", "tm_profile_entry",
 )
 
@@ -133,6 +133,7 @@ def _sig(L):
     L.tm_kl_loss.argtypes = [vp, vp, vp, C.c_float, i32, i32, i32, vp, vp, vp]
     L.tm_edge_table_cols.argtypes = [vp]
     L.tm_edge_tables.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.tm_edge_feature_table.argtypes = [vp, vp, i32, vp, vp]
     L.tm_encoder_fwd_tab.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.tm_edge_importance_tab.argtypes = [vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.tm_tgn_attn_fwd.argtypes = [C.POINTER(TgnAttn), vp, vp, vp]

@@ -1006,7 +1006,7 @@ __global__ void __launch_bounds__(256) gate_reg_kernel(EncW P, int32_t n_ids, co
     const bool valid = e < n_ids;
     const int64_t ec = valid ? e : 0;
     const int de = P.de, kdep = P.kdep;
-    const float t = (float)ets[ec];
+    const float t = ets ? (float)ets[ec] : 0.f;        // no timestamps: edge table only (gf is null too)
     const float *erow = e_feat + ec * de;
     floatx4 X[NQ];
 #pragma unroll
@@ -1059,7 +1059,7 @@ __global__ void __launch_bounds__(256) gate_reg_kernel(EncW P, int32_t n_ids, co
     z += __shfl_xor(z, 16);
     z += __shfl_xor(z, 32);
     z += P.d3b[0];
-    if (valid && g == 0) gf[e] = 0.5f + 0.5f * (1.f / (1.f + expf(-z)));
+    if (gf && valid && g == 0) gf[e] = 0.5f + 0.5f * (1.f / (1.f + expf(-z)));
 }
 
 // retrieve_edge_imp_node with the gate table: per (group, event) the LDS hash keeps, per edge id,
@@ -1253,39 +1253,50 @@ extern "C" int tm_edge_gate_table(const tm_weights *w, const tm_graph *g, const 
     return tm_edge_tables(w, g, e_feat, out_gf, nullptr, stream);
 }
 
-extern "C" int tm_edge_tables(const tm_weights *w, const tm_graph *g, const float *e_feat, float *out_gf,
+// gate table (gf, needs the edge timestamps ets) and/or edge table (etab) over edge ids [0, n)
+static int launch_edge_tables(const tm_weights *w, int32_t n, const double *ets, const float *e_feat, float *out_gf,
                               float *out_etab, void *stream) {
-    if (!w || !g || !e_feat || !out_gf) return fail(TM_E_ARG, "tm_edge_tables: bad arguments");
     const int q0 = etab_q0(w->P);
     if (out_etab && q0 == 0) return fail(TM_E_UNSUPPORTED, "tm_edge_tables: no edge table for these encoder dims");
-    if (!g->d.ts_unique)
-        return fail(TM_E_UNSUPPORTED, "tm_edge_gate_table: an edge id carries several timestamps; use tm_edge_importance");
-    const int32_t n = g->d.max_eid + 1;
     hipEvent_t pe = prof_begin(S_(stream));
     const int nq = w->P.d1.nq;
     const unsigned rblocks = (unsigned)((n + 63) / 64);
     if (out_etab) {   // one launch: gate table and edge table from the same edge-feature fragments
         const int nqe = w->P.ev.nq;
-        if (q0 == 2 && nqe == 11) gate_reg_kernel<13, 3, 11><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf, out_etab);
-        else if (q0 == 2 && nqe == 12) gate_reg_kernel<13, 3, 12><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf, out_etab);
-        else if (q0 == 2 && nqe == 13) gate_reg_kernel<13, 3, 13><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf, out_etab);
-        else if (q0 == 2) gate_reg_kernel<13, 3, 14><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf, out_etab);
-        else if (nqe == 21) gate_reg_kernel<22, 11, 21><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf, out_etab);
-        else gate_reg_kernel<22, 11, 22><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf, out_etab);
+        if (q0 == 2 && nqe == 11) gate_reg_kernel<13, 3, 11><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, ets, e_feat, out_gf, out_etab);
+        else if (q0 == 2 && nqe == 12) gate_reg_kernel<13, 3, 12><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, ets, e_feat, out_gf, out_etab);
+        else if (q0 == 2 && nqe == 13) gate_reg_kernel<13, 3, 13><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, ets, e_feat, out_gf, out_etab);
+        else if (q0 == 2) gate_reg_kernel<13, 3, 14><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, ets, e_feat, out_gf, out_etab);
+        else if (nqe == 21) gate_reg_kernel<22, 11, 21><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, ets, e_feat, out_gf, out_etab);
+        else gate_reg_kernel<22, 11, 22><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, ets, e_feat, out_gf, out_etab);
     } else if (w->P.d2.nq == 4 && w->P.d1.nt == 4 && w->P.d2.nt == 2) {   // hid_dim 64: register-resident path
-        if (nq == 11) gate_reg_kernel<11><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf);
-        else if (nq == 12) gate_reg_kernel<12><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf);
-        else if (nq == 13) gate_reg_kernel<13><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf);
-        else if (nq == 22) gate_reg_kernel<22><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, g->d.ets, e_feat, out_gf);
+        if (nq == 11) gate_reg_kernel<11><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, ets, e_feat, out_gf);
+        else if (nq == 12) gate_reg_kernel<12><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, ets, e_feat, out_gf);
+        else if (nq == 13) gate_reg_kernel<13><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, ets, e_feat, out_gf);
+        else if (nq == 22) gate_reg_kernel<22><<<dim3(rblocks), 256, 0, S_(stream)>>>(w->P, n, ets, e_feat, out_gf);
         else gate_table_kernel<<<dim3((n + TILE_ROWS - 1) / TILE_ROWS), 256, gate_lds(w->P), S_(stream)>>>(
-            w->P, n, g->d.ets, e_feat, out_gf);
+            w->P, n, ets, e_feat, out_gf);
     } else {
-        gate_table_kernel<<<dim3((n + TILE_ROWS - 1) / TILE_ROWS), 256, gate_lds(w->P), S_(stream)>>>(w->P, n, g->d.ets,
+        gate_table_kernel<<<dim3((n + TILE_ROWS - 1) / TILE_ROWS), 256, gate_lds(w->P), S_(stream)>>>(w->P, n, ets,
                                                                                                     e_feat, out_gf);
     }
     TM_CHECK_LAUNCH();
     prof_end("gate_table_kernel", S_(stream), pe);
     return TM_OK;
+}
+
+extern "C" int tm_edge_tables(const tm_weights *w, const tm_graph *g, const float *e_feat, float *out_gf,
+                              float *out_etab, void *stream) {
+    if (!w || !g || !e_feat || !out_gf) return fail(TM_E_ARG, "tm_edge_tables: bad arguments");
+    if (!g->d.ts_unique)
+        return fail(TM_E_UNSUPPORTED, "tm_edge_gate_table: an edge id carries several timestamps; use tm_edge_importance");
+    return launch_edge_tables(w, g->d.max_eid + 1, g->d.ets, e_feat, out_gf, out_etab, stream);
+}
+
+extern "C" int tm_edge_feature_table(const tm_weights *w, const float *e_feat, int32_t n_ids, float *out_etab,
+                                     void *stream) {
+    if (!w || !e_feat || !out_etab || n_ids <= 0) return fail(TM_E_ARG, "tm_edge_feature_table: bad arguments");
+    return launch_edge_tables(w, n_ids, nullptr, e_feat, nullptr, out_etab, stream);
 }
 
 extern "C" int tm_edge_importance_tab(const float *gf, int32_t n_ids, int32_t n_groups, int32_t B, int32_t W,

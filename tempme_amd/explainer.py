@@ -7,11 +7,13 @@ weights as the reference), same ``forward`` / ``retrieve_edge_imp_node`` /
 
 Eval-mode scoring (``forward`` under ``model.eval()`` and
 ``retrieve_explanation(..., training=False)``) runs entirely in libtempme_hip.so:
-tm_encoder_fwd (event features, event_gcn x2, temporal-aware attention, MLP) and
-tm_edge_importance (dependency gate, walk->edge scatter-max, gather, Beta mean,
-mask).  Training-mode calls (dropout active, Beta ``rsample``, gradients) use an
-autograd formulation in torch ops on the same device; HIP backward kernels are the
-next step.
+tm_encoder_fwd_tab (event features with lin_event's edge-feature product read from a
+per-edge-id table built once per weight version by tm_edge_feature_table, event_gcn x2,
+temporal-aware attention, MLP) and tm_edge_importance (dependency gate, walk->edge
+scatter-max, gather, Beta mean, mask).  Training-mode calls (dropout, Beta ``rsample``,
+gradients) run the HIP forward/backward kernels through autograd Functions
+(tm_encoder_train_fwd / tm_encoder_bwd / tm_encoder_wgrad, tm_explain_train_fwd / _bwd,
+tm_kl_loss); only Beta ``rsample`` and the padding mask are torch ops.
 """
 import numpy as np
 import torch
@@ -195,6 +197,27 @@ class TempME(nn.Module):
             self._e_tab = self.edge_raw_embed.weight.detach().to(device=dev, dtype=torch.float32).contiguous()
             self._tables_key = key
         return self._n_tab, self._e_tab
+
+    def dropin_edge_table(self):
+        """The drop-in forward's table mode: lin_event's edge-feature product W[:, :de] E(e) for every row of
+        the edge-feature table (tm_edge_feature_table), rebuilt only when the weights or the table change;
+        None when the encoder dims have no table mode or TEMPME_DROPIN_TABLE=0."""
+        import os
+        if os.environ.get("TEMPME_DROPIN_TABLE", "1") == "0":
+            return None
+        w = self.packed_weights()
+        cols = L.lib().tm_edge_table_cols(w)
+        if not cols:
+            return None
+        _, et = self.feature_tables()
+        key = (self._packed_key, et.data_ptr(), tuple(et.shape))
+        if getattr(self, "_dropin_etab_key", None) != key:
+            dev = self._dev()
+            self._dropin_etab = torch.empty((et.shape[0], cols), dtype=torch.float32, device=dev)
+            L.check(L.lib().tm_edge_feature_table(w, L.ptr(et), int(et.shape[0]), L.ptr(self._dropin_etab),
+                                                  L.stream_ptr(dev)), "tm_edge_feature_table")
+            self._dropin_etab_key = key
+        return self._dropin_etab
 
     def encoder_fwd(self, node6, eid3, ts3, cat, cut, cnt, n_groups, B, W, out=None, workspace=None, M=1,
                     etab=None):
@@ -385,11 +408,15 @@ class TempME(nn.Module):
                                       _to(time_idx, dev, torch.float32), _to(cat_feat, dev, torch.int32).reshape(B, W),
                                       _to(cut_time_l, dev, torch.float64), _to(edge_identify, dev, torch.float32), 1, B, W)
             return out.view(B, W, 1)
+        etab = self.dropin_edge_table()
+        if etab is not None and isinstance(edge_idx, np.ndarray) and edge_idx.size and \
+                (edge_idx.max() >= etab.shape[0] or edge_idx.min() < 0):
+            raise IndexError("index out of range in self")     # what the reference's embedding lookup raises
         out = self.encoder_fwd(_to(node_idx, dev, torch.int32).contiguous(), _to(edge_idx, dev, torch.int32).contiguous(),
                                _to(time_idx, dev, torch.float32).contiguous(),
                                _to(cat_feat, dev, torch.int32).reshape(B, W).contiguous(),
                                _to(cut_time_l, dev, torch.float64).contiguous(),
-                               _to(edge_identify, dev, torch.float32).contiguous(), 1, B, W)
+                               _to(edge_identify, dev, torch.float32).contiguous(), 1, B, W, etab=etab)
         return out[:B * W].view(B, W, 1)
 
     def retrieve_edge_imp_node(self, subgraph, graphlet_imp, walks, training=True):

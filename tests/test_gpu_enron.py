@@ -221,3 +221,34 @@ def test_1m_edge_200_events_vs_oracle(dev):
     ex = tm.TempME(_Base(gz["n_feat"], gz["e_feat"], dev), "tgn", "synth", 40, 64, device=dev,
                    null_model={k: 1 / 12 for k in range(1, 13)}).to(dev).eval()
     _oracle_check(tm, dev, gz, rows, ev, pool, 30, 200, 100, 0, 1, ex)
+
+
+def test_dropin_equals_pipeline(dev, finder, g, z):
+    """The drop-in surface (eval_one_epoch's calls from the host pack the pipeline sampled: TempME.forward x3
+    in table mode, retrieve_explanation per-walk gate) returns exactly what the fused pipeline returns for the
+    same events (bench.py reports both throughputs)."""
+    from tempme_amd import pack as P
+    from tempme_amd.pipeline import ExplainPipeline
+    N, E = 20, EI.SETS[20]
+    ex = _explainer(dev, g, z, "N20_base")
+    pipe = ExplainPipeline(ex, finder.graph, torch.from_numpy(z["test_sampler_dst"]), N, 3, E, seed=0,
+                           split=px.SPLIT_TEST)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a[:E], dtype=dt)).to(dev)  # noqa: E731
+    imp, h1, h2 = [x.clone() for x in pipe.run(t(z["test_src"], np.int32), t(z["test_dst"], np.int32),
+                                                t(z["test_ts"], np.float64), t(z["test_eidx"], np.int32),
+                                                torch.arange(E, dtype=torch.int32, device=dev))]
+    _, cat_d, edge = P.buffers_to_arrays(pipe.buf, E)
+
+    class A:
+        n_degree = N
+    sg_s, sg_t, sg_b, w_s, w_t, w_b, _ = P.get_item(P.load_subgraph_margin(A(), cat_d), np.arange(E))
+    e_s, e_t, e_b = P.get_item_edge(edge, np.arange(E))
+    cut = z["test_ts"][:E].astype(np.float64)
+    assert ex.dropin_edge_table() is not None
+    with torch.no_grad():
+        i_s, i_t, i_b = ex(w_s, cut, e_s), ex(w_t, cut, e_t), ex(w_b, cut, e_b)
+        expl = ex.retrieve_explanation(sg_s, i_s, w_s, sg_t, i_t, w_t, sg_b, i_b, w_b, training=False)
+    for k, x in enumerate((i_s, i_t, i_b)):
+        assert torch.equal(x[..., 0], imp[k]), k
+    assert torch.equal(expl[0], h1.reshape(3 * E, N))
+    assert torch.equal(expl[1], h2.reshape(3 * E, N * N))

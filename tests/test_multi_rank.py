@@ -177,3 +177,37 @@ def test_grad_all_reduce_two_ranks():
         p.join(timeout=60)
     assert res == "ok", res
     assert all(p.exitcode == 0 for p in procs)
+
+
+def _bench_env():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    env["MASTER_ADDR"] = "127.0.0.1"
+    return env
+
+
+def test_bench_self_launches_ranks():
+    """`python bench.py --gpus 2` with no launcher starts its own 2 ranks (torch.distributed.run child) and
+    forms a world-2 process group (gloo here: --launch-check does no GPU work)."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--launch-check"],
+                       capture_output=True, text=True, timeout=240, env=_bench_env(), cwd=repo)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["n_gpus"] == 2 and out["ranks_in_group"] == 2
+
+
+def test_bench_rejects_world_mismatch():
+    """Under a launcher that started a different number of ranks than --gpus, bench.py refuses to run."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = _bench_env()
+    env.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--launch-check"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=repo)
+    assert r.returncode != 0 and "--gpus 2" in r.stderr

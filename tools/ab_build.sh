@@ -1,9 +1,9 @@
 #!/bin/bash
-# tools_ab_build.sh <name> <encoder.hip>: build tempme_amd/lib/ab/<name>.so from the current sources
+# tools/ab_build.sh <name> <encoder.hip>: build tempme_amd/lib/ab/<name>.so from the current sources
 # with encoder.hip replaced by the given file (A/B timing of walk_kernel variants on one box);
 # SAMPLER=<file> / TRAIN=<file> replace sampler.hip / encoder_train.hip the same way.
 set -e
-cd "$(dirname "$0")"
+cd "$(dirname "$0")/.."
 name=$1; enc=$2
 out=ab_src/$name; mkdir -p "$out" tempme_amd/lib/ab
 cp tempme_amd/csrc/*.h tempme_amd/csrc/*.cpp tempme_amd/csrc/*.hip "$out/"

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of walk-kernel edge-table variants (tempme_amd/lib/ab/*.so) against the plain mode, configs 1 and 4
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}" || exit 2
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out && export TMPDIR=/tmp
 for r in 1 2; do for c in 1 4; do
   for so in tempme_amd/lib/ab/*.so; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of events_kernel variants (tempme_amd/lib/ab/*.so): the bench's sampling_roofline, three rounds
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}" || exit 2
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out && export TMPDIR=/tmp
 for r in 1 2 3; do for so in tempme_amd/lib/ab/*.so; do
   TEMPME_LIB="$PWD/$so" timeout -k 10 300 python bench.py --steps 20 --warmup 2 --no-cpu-baseline > gpurun_out/eab.log 2>&1 || exit $?

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box driver for one gpurun call: each GPU step under its own timeout; stop at the first
 # crash/abort/timeout (exit codes other than 0 = pass, 1 = test/assert failure).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}" || exit 2
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 step() {  # step <name> <timeout_s> <cmd...>
@@ -16,22 +16,27 @@ step() {  # step <name> <timeout_s> <cmd...>
 }
 for s in "$@"; do
     case $s in
-        tests) step pytest_gpu 900 python -m pytest tests -x -q -m gpu ;;
+        tests) step pytest_gpu 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread ;;
         f3) step pytest_f3 600 python -u -m pytest tests/test_gpu_encoder_train.py tests/test_gpu_explain_train.py tests/test_gpu_train.py tests/test_gpu_pack.py -x -v --timeout 300 -m gpu ;;
         tgn) step pytest_tgn 600 python -m pytest tests/test_gpu_tgn.py tests/test_gpu_train.py tests/test_gpu_graphmixer.py -x -q -m gpu ;;
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-        bench) step bench 600 python bench.py --steps 10 --warmup 2 ;;
+        info) step info 60 bash -c 'nproc; cat /sys/fs/cgroup/cpu.max; python -c "import os; print(os.cpu_count(), len(os.sched_getaffinity(0)))"' ;;
+        bench) step bench 600 python bench.py ;;
+        bench1) step bench_c1 600 python bench.py --config 1 --no-cpu-baseline ;;
         benchq) step bench 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
-        prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --no-cpu-baseline ;;
-        pmc)
-            B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline"
+        prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --no-extras ;;
+        prof4) step rocprof_c4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof4 -o run --output-format csv -- python bench.py --config 4 --no-cpu-baseline --no-extras ;;
+        enron) step pytest_enron 900 python -u -m pytest tests/test_gpu_enron.py -v --timeout 300 --timeout-method thread ;;
+        pmc1|pmc2|pmc4)  # PMC passes (one counter group per run) over a short bench of configs[1|2|4]
+            c=${s#pmc}
+            B="python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-extras"
             i=0
             for ctr in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
                        "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU" \
                        "TCC_HIT_sum TCC_MISS_sum" "FETCH_SIZE" "WRITE_SIZE" \
                        "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_SALU"; do
                 i=$((i+1))
-                step pmc$i 400 rocprofv3 --kernel-trace --pmc $ctr -d gpurun_out/pmc$i -o run --output-format csv -- $B
+                step pmc_c${c}_$i 400 rocprofv3 --kernel-trace --pmc $ctr -d gpurun_out/pmc_c${c}_$i -o run --output-format csv -- $B
             done ;;
         ablate)
             for ab in 0 1 2 4 7 0; do
@@ -49,19 +54,18 @@ for s in "$@"; do
         stamps)  # phase stamps of every -DTM_STAMPS build in tempme_amd/lib/ab/
             for so in tempme_amd/lib/ab/*.so; do
                 n=$(basename "$so" .so)
-                TEMPME_LIB="$PWD/$so" step stamps_$n 300 python tools_stamps.py
+                TEMPME_LIB="$PWD/$so" step stamps_$n 300 python tools/stamps.py
                 { echo "== $n: $(grep -o '"walk_kernel": {"avg_ms": [0-9.]*' gpurun_out/stamps_$n.log)"; grep -E "^(slot|walk) " gpurun_out/stamps_$n.log; } | tee -a gpurun_out/stamps.txt
             done ;;
-        dist2)  # multi-rank rehearsal on one GPU: 2 ranks, gloo barrier/all-reduce, both on cuda:0
-            TEMPME_DIST_BACKEND=gloo step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-                --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu-baseline ;;
+        dist2)  # multi-rank rehearsal on one GPU: bench.py starts its own 2 ranks (gloo barrier/max), both on cuda:0
+            TEMPME_DIST_BACKEND=gloo step dist2 300 python bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu-baseline ;;
         proftrain) step rocprof_train 600 rocprofv3 --kernel-trace --stats -d gpurun_out/proftrain -o run --output-format csv -- python bench_train.py --steps 10 --warmup 2 ;;
         train) step bench_train 600 python bench_train.py --steps 10 --warmup 2 ;;
         train2)  # 2-rank rehearsal of the gradient all-reduce on one GPU (gloo)
             TEMPME_DIST_BACKEND=gloo step bench_train2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                 --master-addr 127.0.0.1 --master-port 29512 bench_train.py --gpus 2 --steps 5 --warmup 1 ;;
         n30) step bench_n30 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --n-degree 30 ;;
-        phases) step phases 300 python tools_train_phases.py ;;
+        phases) step phases 300 python tools/train_phases.py ;;
         c2) step bench_c2 600 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config 2 ;;
         c4) step bench_c4 900 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config 4 ;;
         a3) step bench_a3 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --alpha 3.0 ;;

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes for events_kernel only (short bench), plus the list of available counters
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}" || exit 2
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out && export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 -L > gpurun_out/counters.txt 2>&1
 B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline"

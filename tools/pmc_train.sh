@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes over the training bench (one counter group per run)
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}" || exit 2
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out && export TMPDIR=/tmp
 B="python bench_train.py --steps 5 --warmup 1"
 i=0
