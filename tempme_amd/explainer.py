@@ -15,6 +15,8 @@ gradients) run the HIP forward/backward kernels through autograd Functions
 (tm_encoder_train_fwd / tm_encoder_bwd / tm_encoder_wgrad, tm_explain_train_fwd / _bwd,
 tm_kl_loss); only Beta ``rsample`` and the padding mask are torch ops.
 """
+import warnings
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -159,8 +161,16 @@ class TempME(nn.Module):
         return self.training or (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()))
 
     def _hip_ok(self):
-        return (self.use_temporal_guidance and self.use_dependency_aware_sampling and self.if_cat
-                and self.hid_dim == 64)
+        ok = (self.use_temporal_guidance and self.use_dependency_aware_sampling and self.if_cat
+              and self.hid_dim == 64)
+        if not ok and not getattr(self, "_warned_torch", False):
+            warnings.warn("TempME(use_temporal_guidance=%s, use_dependency_aware_sampling=%s, if_cat_feature=%s, "
+                          "hid_dim=%d): no HIP kernel instance for this constructor variant; forward / "
+                          "retrieve_edge_imp_node run the torch-op formulation on the device"
+                          % (self.use_temporal_guidance, self.use_dependency_aware_sampling, self.if_cat,
+                             self.hid_dim), RuntimeWarning, stacklevel=3)
+            self._warned_torch = True
+        return ok
 
     def _weight_list(self):
         at, ec, m, d = self.attention, self.event_conv, self.MLP, self.edge_dependency_gcn
