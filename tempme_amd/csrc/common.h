@@ -33,11 +33,15 @@ void prof_end(const char *name, hipStream_t s, hipEvent_t a);
     } while (0)
 
 // ------------------------------------------------------------------ device graph layout
-// One 16-byte record per adjacency entry, so a sampled slot is one dwordx4 load.
+// One 16-byte record per adjacency entry, so a sampled slot is one dwordx4 load: the neighbour, the
+// edge id, the timestamp as the fp32 every sampled output carries, and the entry's rank inside its
+// (node, neighbour) block (the number of earlier entries of the node with the same neighbour).  The
+// fp64 timestamps the bisects compare live in their own array (8 B per entry: twice the density).
 struct __attribute__((aligned(16))) Rec {
     int32_t ngh;
     int32_t eid;
-    double ts;
+    float ts;
+    int32_t brank;
 };
 
 // e_idx -> (owner, slice length) for the (at most two) owners of an edge id.
@@ -47,16 +51,11 @@ struct __attribute__((aligned(16))) EdgeEnds {
     int32_t node_a, len_a, node_b, len_b;
 };
 
-// Pair index: each node's entries re-sorted by (neighbor, position); 8 bytes.
-struct __attribute__((aligned(8))) Pair {
-    int32_t ngh;
-    int32_t pos;
-};
-
-// (node, neighbour) -> the block [start, end) of that neighbour's entries in the node's pair-index
-// range: open addressing, linear probing, u = -1 marks an empty slot, capacity a power of two.
+// (node, neighbour) -> that neighbour's block of the node: its n positions (ascending) stored as a
+// 16-ary search tree at ppos[base..]: open addressing, linear probing, u = -1 marks an empty slot,
+// capacity a power of two.
 struct __attribute__((aligned(16))) PairBlk {
-    int32_t u, x, start, end;
+    int32_t u, x, base, n;
 };
 
 __host__ __device__ inline uint32_t pblk_hash(int32_t u, int32_t x) {
@@ -67,14 +66,52 @@ __host__ __device__ inline uint32_t pblk_hash(int32_t u, int32_t x) {
     return h;
 }
 
+// Block search tree (ppos), fan-out F = 2^kBlkLog.  A block of n <= F positions is its keys, padded
+// with INT32_MAX to a multiple of 4 (16-B aligned).  A larger block stores levels L_h .. L_1, L_0 (in
+// that order, 4F-B aligned, each padded with INT32_MAX to a multiple of F): L_0 = the positions,
+// L_l[t] = L_(l-1)[F t], h = the first level with <= F entries.  A lower bound reads one F-key node per
+// level (h + 1 lines instead of log2(n) dependent loads of a binary search).
+#ifndef TM_BLK_LOG
+#define TM_BLK_LOG 3
+#endif
+constexpr int32_t kBlkLog = TM_BLK_LOG, kBlkFan = 1 << kBlkLog;
+__host__ __device__ inline int32_t blk_levels(int32_t n) {
+    int32_t h = 0;
+    while (n > kBlkFan) {
+        n = (n + kBlkFan - 1) >> kBlkLog;
+        ++h;
+    }
+    return h;
+}
+// padded length of level l of a block of n > F keys with h levels
+__host__ __device__ inline int32_t blk_level_len(int32_t n, int32_t l, int32_t h) {
+    if (l == h) return kBlkFan;
+    const int32_t s = (int32_t)(((int64_t)n + ((int64_t)1 << (kBlkLog * l)) - 1) >> (kBlkLog * l));
+    return (s + kBlkFan - 1) & ~(kBlkFan - 1);
+}
+// offset of the keys (L_0) from the block's base
+__host__ __device__ inline int32_t blk_keys_off(int32_t n) {
+    if (n <= kBlkFan) return 0;
+    const int32_t h = blk_levels(n);
+    int32_t o = 0;
+    for (int32_t l = 1; l <= h; ++l) o += blk_level_len(n, l, h);
+    return o;
+}
+// ints the block occupies
+__host__ __device__ inline int32_t blk_region_len(int32_t n) {
+    if (n <= kBlkFan) return (n + 3) & ~3;
+    return blk_keys_off(n) + blk_level_len(n, 0, blk_levels(n));
+}
+
 struct DevGraph {
     int32_t n_nodes;
     int32_t max_eid;
     int64_t n_entries;
     const int32_t *off;     // [V+1]
     const Rec *rec;         // [n_entries]
+    const double *tsd;      // [n_entries] fp64 timestamps (bisect keys)
     const EdgeEnds *ends;   // [max_eid+1]
-    const Pair *pair;       // [n_entries]
+    const int32_t *ppos;    // block search trees
     const double *ets;      // [max_eid+1] timestamp of each edge id (0 for absent ids)
     int32_t ts_unique;      // every record of an edge id carries the same timestamp
     const PairBlk *pblk;    // [pblk_mask+1] (node, neighbour) block table
@@ -186,19 +223,7 @@ __device__ __forceinline__ int32_t bisect_ts(const DevGraph &g, int32_t u, doubl
     int32_t s = g.off[u], lo = 0, hi = g.off[u + 1] - s;
     while (lo < hi) {
         int32_t mid = (lo + hi) >> 1;
-        if (g.rec[s + mid].ts < x) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo;
-}
-
-// first index in node u's pair list with (ngh, pos) >= (x, p)
-__device__ __forceinline__ int32_t pair_lb(const DevGraph &g, int32_t u, int32_t x, int32_t p) {
-    int32_t lo = g.off[u], hi = g.off[u + 1];
-    while (lo < hi) {
-        int32_t mid = (lo + hi) >> 1;
-        Pair q = g.pair[mid];
-        if (q.ngh < x || (q.ngh == x && q.pos < p)) lo = mid + 1;
+        if (g.tsd[s + mid] < x) lo = mid + 1;
         else hi = mid;
     }
     return lo;
@@ -212,8 +237,9 @@ struct tm_graph {
     // device allocations
     int32_t *d_off;
     tmk::Rec *d_rec;
+    double *d_tsd;
     tmk::EdgeEnds *d_ends;
-    tmk::Pair *d_pair;
+    int32_t *d_ppos;
     double *d_ets;
     tmk::PairBlk *d_pblk;
     // host copies (export)

@@ -1,9 +1,19 @@
-// Temporal CSR build (host) + upload.  Replaces NeighborFinder.__init__ / init_off_set /
-// get_ts2idx (utils/graph.py:13-101).  Runs once per split; the hot path only reads the
-// device arrays built here.
+// Temporal CSR build (host, multi-threaded) + upload.  Replaces NeighborFinder.__init__ /
+// init_off_set / get_ts2idx (utils/graph.py:13-101) and temp_exp_main.py:135-144's adjacency
+// build.  Runs once per split; the hot path only reads the device arrays built here.
+//
+// Work split: every node's list is independent (sort by ts, get_ts2idx, (neighbour, position)
+// blocks, their search trees), so nodes are dealt to threads in chunks; the e_idx table keeps the
+// reference's node order (owner a = the first node holding the edge) in one sequential pass, and
+// the block hash table is filled with 64-bit compare-and-swap inserts.
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <memory>
 #include <numeric>
-#include <unordered_map>
+#include <thread>
 #include <vector>
 
 #include "common.h"
@@ -20,14 +30,60 @@ int fail(int code, const std::string &msg) {
 using namespace tmk;
 
 extern "C" const char *tm_last_error(void) { return tmk::g_last_error.c_str(); }
-extern "C" int tm_version(void) { return 1; }
+extern "C" int tm_version(void) { return 2; }
+
+namespace {
+
+// threads for the host build: TEMPME_THREADS, else OMP_NUM_THREADS (the GPU box sets it to its CPU
+// share), else the hardware threads, at most 64
+int build_threads() {
+    for (const char *v : {"TEMPME_THREADS", "OMP_NUM_THREADS"}) {
+        const char *s = std::getenv(v);
+        if (s && std::atoi(s) > 0) return std::min(64, std::atoi(s));
+    }
+    return (int)std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
+}
+
+// f(thread, begin, end) over [0, n) in chunks of `grain`, dealt dynamically; returns the thread count
+template <class F>
+int parallel_for(int64_t n, int64_t grain, F f) {
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(build_threads(), (n + grain - 1) / std::max<int64_t>(grain, 1)));
+    std::atomic<int64_t> next{0};
+    auto work = [&](int t) {
+        for (;;) {
+            const int64_t b = next.fetch_add(grain);
+            if (b >= n) return;
+            f(t, b, std::min(n, b + grain));
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto &t : th) t.join();
+    return nt;
+}
+
+struct Timer {
+    bool on = std::getenv("TEMPME_GRAPH_TIMING") != nullptr;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    void lap(const char *what) {
+        if (!on) return;
+        const auto t1 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "tm_graph_build %-14s %8.2f ms\n", what,
+                     std::chrono::duration<double, std::milli>(t1 - t0).count());
+        t0 = t1;
+    }
+};
+
+}  // namespace
 
 static void free_graph(tm_graph *g) {
     if (!g) return;
     if (g->d_off) (void)hipFree(g->d_off);
     if (g->d_rec) (void)hipFree(g->d_rec);
+    if (g->d_tsd) (void)hipFree(g->d_tsd);
     if (g->d_ends) (void)hipFree(g->d_ends);
-    if (g->d_pair) (void)hipFree(g->d_pair);
+    if (g->d_ppos) (void)hipFree(g->d_ppos);
     if (g->d_ets) (void)hipFree(g->d_ets);
     if (g->d_pblk) (void)hipFree(g->d_pblk);
     delete[] g->h_off;
@@ -42,13 +98,14 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
                               const double *ts, int device, tm_graph **out) {
     if (!out || !in_off || n_nodes <= 0) return fail(TM_E_ARG, "tm_graph_build: bad arguments");
     *out = nullptr;
+    Timer tm;
     const int64_t n = in_off[n_nodes];
     if (in_off[0] != 0 || n < 0) return fail(TM_E_ARG, "tm_graph_build: in_off must start at 0");
     if (n > 0 && (!ngh || !eid || !ts)) return fail(TM_E_ARG, "tm_graph_build: NULL entry arrays");
-    if (n >= INT32_MAX) return fail(TM_E_UNSUPPORTED, "tm_graph_build: more than 2^31-1 adjacency entries");
-    int32_t max_eid = 0;
+    if (n >= INT32_MAX / 2) return fail(TM_E_UNSUPPORTED, "tm_graph_build: more than 2^30-1 adjacency entries");
     for (int32_t u = 0; u < n_nodes; ++u)
         if (in_off[u + 1] < in_off[u]) return fail(TM_E_ARG, "tm_graph_build: in_off not monotone");
+    int32_t max_eid = 0;
     for (int64_t i = 0; i < n; ++i) {
         if (ngh[i] < 0 || ngh[i] >= n_nodes) return fail(TM_E_ARG, "tm_graph_build: neighbor id out of range");
         if (eid[i] < 0) return fail(TM_E_ARG, "tm_graph_build: negative edge id");
@@ -63,10 +120,13 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
     g->h_eid = new int32_t[nn];
     g->h_dict = new int32_t[nn];
     g->h_ts = new double[nn];
-    std::vector<Rec> rec(nn);
-    std::vector<Pair> pair(nn);
-    std::vector<EdgeEnds> ends((size_t)max_eid + 1, EdgeEnds{-1, 0, -1, 0});
+    std::vector<Rec> rec(nn, Rec{0, 0, 0.f, 0});
     std::vector<int32_t> off32(n_nodes + 1);
+    for (int32_t u = 0; u <= n_nodes; ++u) {
+        g->h_off[u] = in_off[u];
+        off32[u] = (int32_t)in_off[u];
+    }
+    // timestamp of each edge id (the first record's) and whether all its records agree
     std::vector<double> ets((size_t)max_eid + 1, 0.0);
     std::vector<char> seen((size_t)max_eid + 1, 0);
     int32_t ts_unique = 1;
@@ -78,59 +138,168 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
             ts_unique = 0;
         }
     }
+    tm.lap("validate");
 
-    std::vector<int64_t> idx;
-    std::unordered_map<int32_t, int32_t> dict;
-    std::vector<int32_t> tie;
-    for (int32_t u = 0; u < n_nodes; ++u) {
-        const int64_t s = in_off[u], d = in_off[u + 1] - s;
-        g->h_off[u] = s;
-        off32[u] = (int32_t)s;
-        // neighbors sorted by time, ties kept in insertion order (graph.py:48: sorted() is stable)
-        idx.resize(d);
-        std::iota(idx.begin(), idx.end(), s);
-        std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return ts[a] < ts[b]; });
-        for (int64_t i = 0; i < d; ++i) {
-            g->h_ngh[s + i] = ngh[idx[i]];
-            g->h_eid[s + i] = eid[idx[i]];
-            g->h_ts[s + i] = ts[idx[i]];
-        }
-        // get_ts2idx (graph.py:77-101), literally: overwrite, then subtract j inside each
-        // finished tie group; the trailing group is never adjusted.
-        dict.clear();
-        tie.clear();
-        double last_ts = -1.0;
-        int32_t last_e = -1;
-        for (int64_t i = 0; i < d; ++i) {
-            const int32_t e = g->h_eid[s + i];
-            const double t = g->h_ts[s + i];
-            dict[e] = (int32_t)i;
-            if (t == last_ts) {
-                if (tie.empty()) {
-                    tie.push_back(last_e);
-                    tie.push_back(e);
-                } else {
-                    tie.push_back(e);
+    // ---- per node: stable sort by ts, get_ts2idx, (neighbour, position) blocks and ranks
+    std::vector<int64_t> pair_key(nn);     // per entry after the sort: ngh << 32 | position
+    std::vector<int32_t> nblk(n_nodes + 1, 0), plen(n_nodes + 1, 0);
+    // per-thread scratch: the dense dict (every slot read is written first in the same list) and the
+    // sort / tie buffers
+    struct Scratch {
+        std::unique_ptr<int32_t[]> dval;
+        std::vector<int64_t> idx;
+        std::vector<int32_t> tie;
+    };
+    std::vector<Scratch> scr(build_threads());
+    parallel_for(n_nodes, 16, [&](int t_, int64_t b, int64_t e) {
+        Scratch &sc = scr[t_];
+        if (!sc.dval) sc.dval.reset(new int32_t[(size_t)max_eid + 1]);
+        int32_t *dval = sc.dval.get();
+        std::vector<int64_t> &idx = sc.idx;
+        std::vector<int32_t> &tie = sc.tie;
+        for (int64_t u = b; u < e; ++u) {
+            const int64_t s = in_off[u], d = in_off[u + 1] - s;
+            // neighbors sorted by time, ties kept in insertion order (graph.py:48: sorted() is stable)
+            bool sorted = true;
+            for (int64_t i = 1; i < d && sorted; ++i) sorted = !(ts[s + i] < ts[s + i - 1]);
+            if (sorted) {
+                std::copy(ngh + s, ngh + s + d, g->h_ngh + s);
+                std::copy(eid + s, eid + s + d, g->h_eid + s);
+                std::copy(ts + s, ts + s + d, g->h_ts + s);
+            } else {
+                idx.resize(d);
+                std::iota(idx.begin(), idx.end(), s);
+                std::stable_sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) { return ts[x] < ts[y]; });
+                for (int64_t i = 0; i < d; ++i) {
+                    g->h_ngh[s + i] = ngh[idx[i]];
+                    g->h_eid[s + i] = eid[idx[i]];
+                    g->h_ts[s + i] = ts[idx[i]];
                 }
             }
-            if (!(t == last_ts) && !tie.empty()) {
-                for (size_t j = 0; j < tie.size(); ++j) dict[tie[j]] -= (int32_t)j;
-                tie.clear();
+            // get_ts2idx (graph.py:77-101), literally: overwrite, then subtract j inside each
+            // finished tie group; the trailing group is never adjusted.
+            tie.clear();
+            double last_ts = -1.0;
+            int32_t last_e = -1;
+            for (int64_t i = 0; i < d; ++i) {
+                const int32_t ei = g->h_eid[s + i];
+                const double t = g->h_ts[s + i];
+                dval[ei] = (int32_t)i;
+                if (t == last_ts) {
+                    if (tie.empty()) tie.push_back(last_e);
+                    tie.push_back(ei);
+                }
+                if (!(t == last_ts) && !tie.empty()) {
+                    for (size_t j = 0; j < tie.size(); ++j) dval[tie[j]] -= (int32_t)j;
+                    tie.clear();
+                }
+                last_ts = t;
+                last_e = ei;
             }
-            last_ts = t;
-            last_e = e;
+            for (int64_t i = 0; i < d; ++i) {
+                g->h_dict[s + i] = dval[g->h_eid[s + i]];
+                pair_key[s + i] = (int64_t)g->h_ngh[s + i] << 32 | (int64_t)i;
+            }
+            std::sort(pair_key.begin() + s, pair_key.begin() + s + d);
+            int32_t blocks = 0, len = 0;
+            for (int64_t i = 0; i < d;) {
+                int64_t j = i + 1;
+                while (j < d && (pair_key[s + j] >> 32) == (pair_key[s + i] >> 32)) ++j;
+                const int32_t bn = (int32_t)(j - i);
+                for (int64_t k = i; k < j; ++k) {
+                    const int32_t p = (int32_t)(pair_key[s + k] & 0xFFFFFFFF);
+                    rec[s + p] = Rec{g->h_ngh[s + p], g->h_eid[s + p], (float)g->h_ts[s + p], (int32_t)(k - i)};
+                }
+                if (bn > kBlkFan) len = (len + kBlkFan - 1) & ~(kBlkFan - 1);     // node-aligned tree
+                len += blk_region_len(bn);
+                ++blocks;
+                i = j;
+            }
+            nblk[u] = blocks;
+            plen[u] = (len + 15) & ~15;                   // node regions 64-B aligned
         }
+    });
+    tm.lap("nodes");
+
+    // ---- block trees
+    std::vector<int64_t> boff(n_nodes + 1, 0), poff(n_nodes + 1, 0);
+    for (int32_t u = 0; u < n_nodes; ++u) {
+        boff[u + 1] = boff[u] + nblk[u];
+        poff[u + 1] = poff[u] + plen[u];
+    }
+    const int64_t n_blocks = boff[n_nodes], n_ppos = std::max<int64_t>(poff[n_nodes], 16);
+    if (n_ppos >= INT32_MAX) {
+        free_graph(g);
+        return fail(TM_E_UNSUPPORTED, "tm_graph_build: block trees exceed 2^31 entries");
+    }
+    std::vector<int32_t> ppos(n_ppos, INT32_MAX);
+    std::vector<PairBlk> blist(std::max<int64_t>(n_blocks, 1));
+    parallel_for(n_nodes, 16, [&](int, int64_t b, int64_t e) {
+        for (int64_t u = b; u < e; ++u) {
+            const int64_t s = in_off[u], d = in_off[u + 1] - s;
+            int64_t bi = boff[u];
+            int32_t len = 0;
+            for (int64_t i = 0; i < d;) {
+                int64_t j = i + 1;
+                while (j < d && (pair_key[s + j] >> 32) == (pair_key[s + i] >> 32)) ++j;
+                const int32_t bn = (int32_t)(j - i);
+                if (bn > kBlkFan) len = (len + kBlkFan - 1) & ~(kBlkFan - 1);
+                const int64_t base = poff[u] + len;
+                int32_t *keys = ppos.data() + base + blk_keys_off(bn);
+                for (int64_t k = i; k < j; ++k) keys[k - i] = (int32_t)(pair_key[s + k] & 0xFFFFFFFF);
+                if (bn > kBlkFan) {   // fence levels, bottom-up: L_l[t] = L_(l-1)[F t]
+                    const int32_t h = blk_levels(bn);
+                    int32_t *lower = keys;
+                    int64_t lo_off = blk_keys_off(bn);
+                    for (int32_t l = 1; l <= h; ++l) {
+                        lo_off -= blk_level_len(bn, l, h);
+                        int32_t *lev = ppos.data() + base + lo_off;
+                        const int32_t cnt =
+                            (int32_t)(((int64_t)bn + ((int64_t)1 << (kBlkLog * l)) - 1) >> (kBlkLog * l));
+                        for (int32_t t = 0; t < cnt; ++t) lev[t] = lower[kBlkFan * t];
+                        lower = lev;
+                    }
+                }
+                blist[bi++] = PairBlk{(int32_t)u, (int32_t)(pair_key[s + i] >> 32), (int32_t)base, bn};
+                len += blk_region_len(bn);
+                i = j;
+            }
+        }
+    });
+    tm.lap("trees");
+
+    // ---- (node, neighbour) -> block hash table, load factor <= 1/2
+    uint32_t cap = 16;
+    while ((int64_t)cap < 2 * n_blocks) cap <<= 1;
+    std::vector<PairBlk> pblk(cap, PairBlk{-1, 0, 0, 0});
+    parallel_for(n_blocks, 4096, [&](int, int64_t b, int64_t e) {
+        for (int64_t i = b; i < e; ++i) {
+            const PairBlk &x = blist[i];
+            const uint64_t key = (uint64_t)(uint32_t)x.u | (uint64_t)(uint32_t)x.x << 32;
+            const uint64_t empty = (uint64_t)0xFFFFFFFFu;
+            uint32_t h = pblk_hash(x.u, x.x) & (cap - 1);
+            for (;;) {
+                uint64_t *slot = reinterpret_cast<uint64_t *>(&pblk[h]);
+                uint64_t expect = empty;
+                if (__atomic_compare_exchange_n(slot, &expect, key, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+                    pblk[h].base = x.base;
+                    pblk[h].n = x.n;
+                    break;
+                }
+                h = (h + 1) & (cap - 1);
+            }
+        }
+    });
+    tm.lap("block table");
+
+    // ---- e_idx -> (owner, slice length), owners in node order
+    std::vector<EdgeEnds> ends((size_t)max_eid + 1, EdgeEnds{-1, 0, -1, 0});
+    for (int32_t u = 0; u < n_nodes; ++u) {
+        const int64_t s = in_off[u], d = in_off[u + 1] - s;
         for (int64_t i = 0; i < d; ++i) {
-            g->h_dict[s + i] = dict[g->h_eid[s + i]];
-            rec[s + i] = Rec{g->h_ngh[s + i], g->h_eid[s + i], g->h_ts[s + i]};
-            pair[s + i] = Pair{g->h_ngh[s + i], (int32_t)i};
-        }
-        std::sort(pair.begin() + s, pair.begin() + s + d,
-                  [](const Pair &a, const Pair &b) { return a.ngh < b.ngh || (a.ngh == b.ngh && a.pos < b.pos); });
-        for (auto &kv : dict) {
-            int32_t v = kv.second;
+            int32_t v = g->h_dict[s + i];
             if (v < 0) v = (int32_t)std::max<int64_t>(0, d + v);  // Python slice with a negative stop
-            EdgeEnds &x = ends[kv.first];
+            EdgeEnds &x = ends[g->h_eid[s + i]];
             if (x.node_a == -1 || x.node_a == u) {
                 x.node_a = u;
                 x.len_a = v;
@@ -139,30 +308,12 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
                 x.len_b = v;
             } else {
                 free_graph(g);
-                return fail(TM_E_UNSUPPORTED, "tm_graph_build: edge id " + std::to_string(kv.first) +
+                return fail(TM_E_UNSUPPORTED, "tm_graph_build: edge id " + std::to_string(g->h_eid[s + i]) +
                                                   " appears in the lists of more than two nodes");
             }
         }
     }
-    g->h_off[n_nodes] = n;
-    off32[n_nodes] = (int32_t)n;
-
-    // (node, neighbour) block table over the pair index, load factor <= 1/2
-    int64_t n_blocks = 0;
-    for (int32_t u = 0; u < n_nodes; ++u)
-        for (int64_t i = off32[u]; i < off32[u + 1]; ++i) n_blocks += (i == off32[u] || pair[i].ngh != pair[i - 1].ngh);
-    uint32_t cap = 16;
-    while ((int64_t)cap < 2 * n_blocks) cap <<= 1;
-    std::vector<PairBlk> pblk(cap, PairBlk{-1, 0, 0, 0});
-    for (int32_t u = 0; u < n_nodes; ++u)
-        for (int64_t i = off32[u]; i < off32[u + 1];) {
-            int64_t j = i + 1;
-            while (j < off32[u + 1] && pair[j].ngh == pair[i].ngh) ++j;
-            uint32_t h = pblk_hash(u, pair[i].ngh) & (cap - 1);
-            while (pblk[h].u != -1) h = (h + 1) & (cap - 1);
-            pblk[h] = PairBlk{u, pair[i].ngh, (int32_t)i, (int32_t)j};
-            i = j;
-        }
+    tm.lap("edge ends");
 
     int prev = 0;
     if (hipGetDevice(&prev) != hipSuccess) prev = 0;
@@ -173,25 +324,62 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
     hipError_t e = hipSuccess;
     e = e ? e : hipMalloc(&g->d_off, sizeof(int32_t) * (n_nodes + 1));
     e = e ? e : hipMalloc(&g->d_rec, sizeof(Rec) * nn);
+    e = e ? e : hipMalloc(&g->d_tsd, sizeof(double) * nn);
     e = e ? e : hipMalloc(&g->d_ends, sizeof(EdgeEnds) * ends.size());
-    e = e ? e : hipMalloc(&g->d_pair, sizeof(Pair) * nn);
+    e = e ? e : hipMalloc(&g->d_ppos, sizeof(int32_t) * ppos.size());
     e = e ? e : hipMalloc(&g->d_ets, sizeof(double) * ets.size());
     e = e ? e : hipMalloc(&g->d_pblk, sizeof(PairBlk) * cap);
     e = e ? e : hipMemcpy(g->d_pblk, pblk.data(), sizeof(PairBlk) * cap, hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(g->d_ets, ets.data(), sizeof(double) * ets.size(), hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(g->d_off, off32.data(), sizeof(int32_t) * (n_nodes + 1), hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(g->d_rec, rec.data(), sizeof(Rec) * nn, hipMemcpyHostToDevice);
+    e = e ? e : hipMemcpy(g->d_tsd, g->h_ts, sizeof(double) * nn, hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(g->d_ends, ends.data(), sizeof(EdgeEnds) * ends.size(), hipMemcpyHostToDevice);
-    e = e ? e : hipMemcpy(g->d_pair, pair.data(), sizeof(Pair) * nn, hipMemcpyHostToDevice);
+    e = e ? e : hipMemcpy(g->d_ppos, ppos.data(), sizeof(int32_t) * ppos.size(), hipMemcpyHostToDevice);
     (void)hipSetDevice(prev);
     if (e != hipSuccess) {
         free_graph(g);
         return fail(TM_E_HIP, std::string("tm_graph_build: ") + hipGetErrorString(e));
     }
-    g->d = DevGraph{n_nodes, max_eid, n, g->d_off, g->d_rec, g->d_ends, g->d_pair, g->d_ets, ts_unique, g->d_pblk,
-                    cap - 1};
+    tm.lap("upload");
+    g->d = DevGraph{n_nodes, max_eid, n,         g->d_off,  g->d_rec, g->d_tsd,
+                    g->d_ends, g->d_ppos, g->d_ets, ts_unique, g->d_pblk, cap - 1};
     *out = g;
     return TM_OK;
+}
+
+// temp_exp_main.py:135-144 on raw edge rows: for every row (dst, e, t) is appended to src's list,
+// then (src, e, t) to dst's; owner-major by a counting sort (stable, so each list keeps the rows'
+// order), then tm_graph_build.
+extern "C" int tm_graph_build_edges(int32_t n_nodes, int64_t n_edges, const int64_t *src, const int64_t *dst,
+                                    const int64_t *eidx, const double *ts, int device, tm_graph **out) {
+    if (!out || n_nodes <= 0 || n_edges < 0) return fail(TM_E_ARG, "tm_graph_build_edges: bad arguments");
+    if (n_edges > 0 && (!src || !dst || !eidx || !ts)) return fail(TM_E_ARG, "tm_graph_build_edges: NULL arrays");
+    if (2 * n_edges >= INT32_MAX / 2) return fail(TM_E_UNSUPPORTED, "tm_graph_build_edges: too many edges");
+    std::vector<int64_t> off((size_t)n_nodes + 1, 0);
+    for (int64_t i = 0; i < n_edges; ++i) {
+        if (src[i] < 0 || src[i] >= n_nodes || dst[i] < 0 || dst[i] >= n_nodes)
+            return fail(TM_E_ARG, "tm_graph_build_edges: node id out of range");
+        if (eidx[i] < 0 || eidx[i] > INT32_MAX) return fail(TM_E_ARG, "tm_graph_build_edges: edge id out of range");
+        ++off[src[i] + 1];
+        ++off[dst[i] + 1];
+    }
+    for (int32_t u = 0; u < n_nodes; ++u) off[u + 1] += off[u];
+    const int64_t n = 2 * n_edges, nn = std::max<int64_t>(n, 1);
+    std::vector<int32_t> ngh(nn), eid(nn);
+    std::vector<double> t(nn);
+    std::vector<int64_t> pos(off.begin(), off.end() - 1);
+    for (int64_t i = 0; i < n_edges; ++i) {
+        int64_t p = pos[src[i]]++;
+        ngh[p] = (int32_t)dst[i];
+        eid[p] = (int32_t)eidx[i];
+        t[p] = ts[i];
+        p = pos[dst[i]]++;
+        ngh[p] = (int32_t)src[i];
+        eid[p] = (int32_t)eidx[i];
+        t[p] = ts[i];
+    }
+    return tm_graph_build(n_nodes, off.data(), ngh.data(), eid.data(), t.data(), device, out);
 }
 
 extern "C" int tm_graph_free(tm_graph *g) {

@@ -15,7 +15,22 @@
 
 #include "common.h"
 
+#ifndef TM_LOCKSTEP
+#define TM_LOCKSTEP 0
+#endif
+
 namespace tmk {
+
+#ifndef TM_NT_STORES
+#define TM_NT_STORES 1
+#endif
+// sampled outputs are written once and read by the next kernel: streamed (non-temporal) so they do not
+// evict the graph's records from L2
+#if TM_NT_STORES
+#define TM_ST(dst, v) __builtin_nontemporal_store((v), &(dst))
+#else
+#define TM_ST(dst, v) ((dst) = (v))
+#endif
 
 constexpr int kMaxN = 64;   // n_degree supported by the sampling kernels (reference: 20..60)
 constexpr int kMaxM = 8;    // walks per hop-1 slot (reference: 3, null model 1)
@@ -49,41 +64,41 @@ __device__ int32_t bisect_ts_wave(const DevGraph &g, int32_t u, double x) {
     int32_t lo = 0, hi = g.off[u + 1] - s;
     while (hi - lo > 64) {
         const int32_t stride = (hi - lo + 63) / 64, q = lo + lane * stride;
-        const bool lt = q < hi && g.rec[s + q].ts < x;
+        const bool lt = q < hi && g.tsd[s + q] < x;
         const int32_t c = __popcll(__ballot(lt));        // sorted: the samples below x are a prefix
         const int32_t nlo = c > 0 ? lo + (c - 1) * stride + 1 : lo;
         hi = min(hi, lo + c * stride);
         lo = nlo;
     }
     const int32_t q = lo + lane;
-    const bool lt = q < hi && g.rec[s + q].ts < x;
+    const bool lt = q < hi && g.tsd[s + q] < x;
     return lo + __popcll(__ballot(lt));
 }
 
 // rank-th smallest position of the union of two sorted, disjoint position lists
-__device__ __forceinline__ int32_t kth_of_two(const Pair *p1, int32_t n1, const Pair *p2, int32_t n2, int32_t r) {
+__device__ __forceinline__ int32_t kth_of_two(const int32_t *p1, int32_t n1, const int32_t *p2, int32_t n2, int32_t r) {
     int32_t lo = max(0, r + 1 - n2), hi = min(n1, r + 1);
     while (lo < hi) {
         int32_t mid = (lo + hi) >> 1, j = r + 1 - mid;
-        if (j == 0 || p1[mid].pos > p2[j - 1].pos) hi = mid;
+        if (j == 0 || p1[mid] > p2[j - 1]) hi = mid;
         else lo = mid + 1;
     }
     int32_t i = lo, j = r + 1 - lo;
-    int32_t a = i > 0 ? p1[i - 1].pos : -1, b = j > 0 ? p2[j - 1].pos : -1;
+    int32_t a = i > 0 ? p1[i - 1] : -1, b = j > 0 ? p2[j - 1] : -1;
     return a > b ? a : b;
 }
 
-// K (node, neighbour) block lookups in lockstep (u < 0: empty block)
+// K (node, neighbour) block lookups in lockstep (u < 0: empty block): base and size of each block
 template <int K>
 __device__ __forceinline__ void pair_blocks(const DevGraph &g, const int32_t (&u)[K], const int32_t (&x)[K],
-                                            int32_t (&st)[K], int32_t (&en)[K]) {
+                                            int32_t (&base)[K], int32_t (&n)[K]) {
     uint32_t h[K];
     bool live[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         live[k] = u[k] >= 0;
         h[k] = pblk_hash(u[k], x[k]) & g.pblk_mask;
-        st[k] = en[k] = 0;
+        base[k] = n[k] = 0;
     }
     while (true) {
         bool any = false;
@@ -97,8 +112,8 @@ __device__ __forceinline__ void pair_blocks(const DevGraph &g, const int32_t (&u
         for (int k = 0; k < K; ++k) {
             if (!live[k]) continue;
             if (b[k].u == u[k] && b[k].x == x[k]) {
-                st[k] = b[k].start;
-                en[k] = b[k].end;
+                base[k] = b[k].base;
+                n[k] = b[k].n;
                 live[k] = false;
             } else if (b[k].u == -1) {
                 live[k] = false;
@@ -109,27 +124,65 @@ __device__ __forceinline__ void pair_blocks(const DevGraph &g, const int32_t (&u
     }
 }
 
-// K lower bounds "first entry of [lo, hi) with pos >= p" in lockstep (entries sorted by pos)
+// K lower bounds "number of the block's positions < p" in lockstep, each down the block's search
+// tree (common.h): one F-key node per level; live[k] false: 0
 template <int K>
-__device__ __forceinline__ void pos_lb_multi(const DevGraph &g, int32_t (&lo)[K], int32_t (&hi)[K],
-                                             const int32_t (&p)[K]) {
+__device__ __forceinline__ void blk_lb_multi(const DevGraph &g, const int32_t (&base)[K], const int32_t (&n)[K],
+                                             const int32_t (&p)[K], const bool (&live)[K], int32_t (&res)[K]) {
+    constexpr int NQ = kBlkFan / 4;      // quads per node
+    int32_t h[K], l[K], off[K], j[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        h[k] = blk_levels(n[k]);
+        l[k] = live[k] && n[k] > 0 ? h[k] : -1;
+        off[k] = base[k];
+        j[k] = 0;
+        res[k] = 0;
+    }
     while (true) {
         bool any = false;
 #pragma unroll
-        for (int k = 0; k < K; ++k) any |= lo[k] < hi[k];
+        for (int k = 0; k < K; ++k) any |= l[k] >= 0;
         if (!any) break;
-        int32_t q[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) q[k] = g.pair[lo[k] < hi[k] ? (lo[k] + hi[k]) >> 1 : 0].pos;
+        int4 v[K][NQ];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            if (lo[k] < hi[k]) {
-                const int32_t mid = (lo[k] + hi[k]) >> 1;
-                if (q[k] < p[k]) lo[k] = mid + 1;
-                else hi[k] = mid;
+            // a block of <= F keys holds ceil(n/4) quads; every tree node F/4
+            const int32_t nq = h[k] == 0 ? (n[k] + 3) >> 2 : NQ;
+            const int4 *q = reinterpret_cast<const int4 *>(g.ppos + off[k] + kBlkFan * j[k]);
+#pragma unroll
+            for (int t = 0; t < NQ; ++t)
+                v[k][t] = (l[k] >= 0 && t < nq) ? q[t] : make_int4(INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (l[k] < 0) continue;
+            int32_t c = 0;
+#pragma unroll
+            for (int t = 0; t < NQ; ++t)
+                c += (v[k][t].x < p[k]) + (v[k][t].y < p[k]) + (v[k][t].z < p[k]) + (v[k][t].w < p[k]);
+            if (l[k] == 0) {
+                res[k] = kBlkFan * j[k] + c;
+                l[k] = -1;
+            } else if (l[k] == h[k] && c == 0) {
+                res[k] = 0;
+                l[k] = -1;
+            } else {
+                off[k] += blk_level_len(n[k], l[k], h[k]);
+                j[k] = kBlkFan * j[k] + c - 1;
+                --l[k];
             }
         }
     }
+}
+
+// one lower bound down a block's search tree
+__device__ __forceinline__ int32_t blk_lb(const DevGraph &g, int32_t base, int32_t n, int32_t p) {
+    const int32_t b[1] = {base}, nn[1] = {n}, pp[1] = {p};
+    const bool live[1] = {true};
+    int32_t r[1];
+    blk_lb_multi<1>(g, b, nn, pp, live, r);
+    return r[0];
 }
 
 struct Step3 {
@@ -142,8 +195,11 @@ struct Step3 {
 //  * case order A (src1==src2 && tgt1!=tgt2) / B (tgt1==src2 && src1!=tgt2) / C (else)
 //  * nodeedge2idx[..].get(e2) of None slices the WHOLE list (future leak)
 //  * node 0 is padding (cut 0) even when it is a real node
+// pos2 / rank2: the step-2 record's position in src2's list and its rank in its (src2, tgt2) block (-1:
+// none).  In the filtered cases the a-side node is src2 and a2 = tgt2, so when the cut of e2 is the
+// record's own position (no tie group moved it) the count of a2-entries before the cut is rank2.
 __device__ Step3 final_step(const DevGraph &g, Key key, uint32_t ev, uint32_t w, int32_t src1, int32_t tgt1,
-                            int32_t src2, int32_t tgt2, int32_t e2) {
+                            int32_t src2, int32_t tgt2, int32_t e2, int32_t pos2, int32_t rank2) {
     int32_t code, a_node, a1 = 0, a2 = 0, b_node, bf = 0;
     bool filt;
     if (src1 == src2 && tgt1 != tgt2) {
@@ -161,24 +217,36 @@ __device__ Step3 final_step(const DevGraph &g, Key key, uint32_t ev, uint32_t w,
     const int32_t ob0 = vb ? g.off[b_node] : 0, ob1 = vb ? g.off[b_node + 1] : 0;
     const int32_t ca = !va ? 0 : x2.node_a == a_node ? x2.len_a : x2.node_b == a_node ? x2.len_b : oa1 - oa0;
     const int32_t cb = !vb ? 0 : x2.node_a == b_node ? x2.len_a : x2.node_b == b_node ? x2.len_b : ob1 - ob0;
-    int32_t na, nb, lb1 = 0, n1 = 0, lb2 = 0, n2 = 0, lbb = 0;
+    int32_t na, nb, k1 = 0, n1 = 0, k2 = 0, n2 = 0, kb = 0;
     if (filt) {
         // filtered counts: the (node, neighbour) block of each of the three neighbours from the block
-        // table (its start is the (x, 0) lower bound), then the entries before the cut inside each
-        // block; the three lookups and the three in-block searches each run in lockstep
+        // table, then the entries before the cut inside each block down its search tree; the lookups
+        // and the searches each run in lockstep
         const bool sa = ca > 0, sb = cb > 0;
         const int32_t us[3] = {sa ? a_node : -1, sa ? a_node : -1, sb ? b_node : -1}, xs[3] = {a1, a2, bf};
-        int32_t st[3], en[3];
-        pair_blocks<3>(g, us, xs, st, en);
-        int32_t lo[3] = {st[0], st[1], st[2]}, hi[3] = {en[0], en[1], en[2]};
-        const int32_t ps[3] = {ca, ca, cb};
-        pos_lb_multi<3>(g, lo, hi, ps);
-        n1 = lo[0] - st[0];
-        n2 = lo[1] - st[1];
-        nb = lo[2] - st[2];
-        lb1 = st[0];
-        lb2 = st[1];
-        lbb = st[2];
+        int32_t bs[3], bn[3], cnt[3];
+        pair_blocks<3>(g, us, xs, bs, bn);
+        const bool r2 = pos2 >= 0 && ca == pos2;
+#if TM_LOCKSTEP
+        {   // a1 and b in lockstep; a2 only when a tie group moved e2's cut off its own record
+            const int32_t b2[2] = {bs[0], bs[2]}, n2_[2] = {bn[0], bn[2]}, p2_[2] = {ca, cb};
+            const bool l2[2] = {true, true};
+            int32_t r2_[2];
+            blk_lb_multi<2>(g, b2, n2_, p2_, l2, r2_);
+            cnt[0] = r2_[0];
+            cnt[2] = r2_[1];
+        }
+#else
+        cnt[0] = blk_lb(g, bs[0], bn[0], ca);
+        cnt[2] = blk_lb(g, bs[2], bn[2], cb);
+#endif
+        cnt[1] = r2 ? 0 : blk_lb(g, bs[1], bn[1], ca);   // a tie group moved e2's cut off its own record
+        n1 = cnt[0];
+        n2 = r2 ? (sa ? rank2 : 0) : cnt[1];
+        nb = cnt[2];
+        k1 = bs[0] + blk_keys_off(bn[0]);
+        k2 = bs[1] + blk_keys_off(bn[1]);
+        kb = bs[2] + blk_keys_off(bn[2]);
         na = n1 + n2;
     } else {
         na = ca;
@@ -190,18 +258,18 @@ __device__ Step3 final_step(const DevGraph &g, Key key, uint32_t ev, uint32_t w,
     int32_t ent;
     if (r < na) {
         o.src = a_node;
-        int32_t pos = filt ? kth_of_two(g.pair + lb1, n1, g.pair + lb2, n2, r) : r;
+        int32_t pos = filt ? kth_of_two(g.ppos + k1, n1, g.ppos + k2, n2, r) : r;
         ent = oa0 + pos;
     } else {
         o.src = b_node;
         int32_t rr = r - na;
-        int32_t pos = filt ? g.pair[lbb + rr].pos : rr;
+        int32_t pos = filt ? g.ppos[kb + rr] : rr;
         ent = ob0 + pos;
     }
     const Rec rc = g.rec[ent];
     o.ngh = rc.ngh;
     o.eid = rc.eid;
-    o.ts = (float)rc.ts;
+    o.ts = rc.ts;
     int32_t t;
     const int32_t s = o.src, n = o.ngh;
     if (code == 2) {
@@ -233,6 +301,7 @@ __device__ __forceinline__ int32_t cat_of(int32_t code, int32_t t, int null_orde
 struct Step2 {
     int32_t src, ngh, eid;
     float ts;
+    int32_t pos, rank;    // the record's position in src's list and its (src, ngh) block rank; -1: none
 };
 
 // candidate cut lengths and record offsets of step 2 for one hop-1 slot (shared by its M walks):
@@ -256,7 +325,7 @@ __device__ __forceinline__ Step2 next_step(const DevGraph &g, Key key, uint32_t 
                                            int32_t m, int32_t u, int32_t v1, const Step2Cuts &sc) {
     constexpr int MX = MC > 0 ? MC : kMaxM;
     if (MC > 0) M = MC;
-    Step2 o{0, 0, 0, 0.f};
+    Step2 o{0, 0, 0, 0.f, -1, -1};
     const int32_t cu = sc.cu, cv = sc.cv, ou = sc.ou, ov = sc.ov, tot = cu + cv;
     if (tot == 0) return o;
     uint32_t dv[MX];
@@ -277,15 +346,18 @@ __device__ __forceinline__ Step2 next_step(const DevGraph &g, Key key, uint32_t 
     int32_t ent;
     if (x < cu) {
         o.src = u;
+        o.pos = x;
         ent = ou + x;
     } else {
         o.src = v1;
+        o.pos = x - cu;
         ent = ov + (x - cu);
     }
     const Rec rc = g.rec[ent];
     o.ngh = rc.ngh;
     o.eid = rc.eid;
-    o.ts = (float)rc.ts;
+    o.ts = rc.ts;
+    o.rank = rc.brank;
     return o;
 }
 
@@ -349,7 +421,7 @@ __global__ void __launch_bounds__(256) khop_kernel(DevGraph g, Key key, uint32_t
     Rec rec[4];
 #pragma unroll
     for (int w = 0; w < 4; ++w)
-        rec[w] = (c > 0 && 4 * kb + w < N) ? g.rec[ro[lr] + (int32_t)d[w]] : Rec{0, 0, 0.0};
+        rec[w] = (c > 0 && 4 * kb + w < N) ? g.rec[ro[lr] + (int32_t)d[w]] : Rec{0, 0, 0.f, 0};
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
         const int32_t k = 4 * kb + w;
@@ -357,7 +429,7 @@ __global__ void __launch_bounds__(256) khop_kernel(DevGraph g, Key key, uint32_t
         const int64_t o = r * N + (c > 0 ? rank[w] : k);
         on[o] = rec[w].ngh;
         oe[o] = rec[w].eid;
-        ot[o] = (float)rec[w].ts;
+        ot[o] = rec[w].ts;
     }
 }
 
@@ -389,7 +461,7 @@ __device__ __forceinline__ void khop_emit(const DevGraph &g, int32_t N, const ui
     // record gathers first (independent of the ranks), then the rank loop under their latency
     Rec rec[4];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) rec[w] = (c > 0 && 4 * kb + w < N) ? g.rec[o + (int32_t)d[w]] : Rec{0, 0, 0.0};
+    for (int w = 0; w < 4; ++w) rec[w] = (c > 0 && 4 * kb + w < N) ? g.rec[o + (int32_t)d[w]] : Rec{0, 0, 0.f, 0};
     int32_t rank[4] = {0, 0, 0, 0};
     if (keyed && c > 0) {
         // dd holds (draw << 6 | index): unique keys, so the np.sort rank (ties by index) is one compare
@@ -440,7 +512,7 @@ __device__ __forceinline__ void khop_emit(const DevGraph &g, int32_t N, const ui
         const int32_t slot = (kStage ? lr * N : 0) + (c > 0 ? rank[w] : k);
         sn[slot] = rec[w].ngh;
         se[slot] = rec[w].eid;
-        st[slot] = (float)rec[w].ts;
+        st[slot] = rec[w].ts;
     }
 }
 
@@ -556,7 +628,7 @@ __global__ void __launch_bounds__(256) walks_kernel(DevGraph g, Key key, int32_t
     const int32_t u = root[b], v1 = h1n[b * N + j], e1 = h1e[b * N + j];
     const float t1 = h1t[b * N + j];
     const Step2 s2 = next_step(g, key, ev, j, M, m, u, v1, step2_cuts(g, u, v1, e1));
-    const Step3 s3 = final_step(g, key, ev, w, u, v1, s2.src, s2.ngh, s2.eid);
+    const Step3 s3 = final_step(g, key, ev, w, u, v1, s2.src, s2.ngh, s2.eid, s2.pos, s2.rank);
     int32_t *nd = node6 + i * 6;
     nd[0] = s3.src; nd[1] = s3.ngh; nd[2] = s2.src; nd[3] = s2.ngh; nd[4] = u; nd[5] = v1;
     eid3[i * 3 + 0] = s3.eid; eid3[i * 3 + 1] = s2.eid; eid3[i * 3 + 2] = e1;
@@ -791,12 +863,12 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
             int32_t slot = tid;
             if (c > 0) {
                 const Rec rc = g.rec[g.off[u] + (int32_t)d];
-                n_ = rc.ngh; e_ = rc.eid; t_ = (float)rc.ts; slot = rank;
+                n_ = rc.ngh; e_ = rc.eid; t_ = rc.ts; slot = rank;
             }
             h1n[slot] = n_; h1e[slot] = e_; h1t[slot] = t_;
-            o_sub1_node[se * N + slot] = n_;
-            o_sub1_eid[se * N + slot] = e_;
-            o_sub1_ts[se * N + slot] = t_;
+            TM_ST(o_sub1_node[se * N + slot], n_);
+            TM_ST(o_sub1_eid[se * N + slot], e_);
+            TM_ST(o_sub1_ts[se * N + slot], t_);
         }
     }
     __syncthreads();
@@ -861,14 +933,14 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
         }
         Rec rc[HB];
 #pragma unroll
-        for (int u = 0; u < HB; ++u) rc[u] = g.n_entries > 0 ? g.rec[idx[u]] : Rec{0, 0, 0.0};
+        for (int u = 0; u < HB; ++u) rc[u] = g.n_entries > 0 ? g.rec[idx[u]] : Rec{0, 0, 0.f, 0};
 #pragma unroll
         for (int u = 0; u < HB; ++u) {
             if (x0 + u * 64 + tid >= N * N) continue;
             const int64_t o = se * N * N + slot[u];
-            o_sub2_node[o] = ok[u] ? rc[u].ngh : 0;
-            o_sub2_eid[o] = ok[u] ? rc[u].eid : 0;
-            o_sub2_ts[o] = ok[u] ? (float)rc[u].ts : 0.f;
+            TM_ST(o_sub2_node[o], ok[u] ? rc[u].ngh : 0);
+            TM_ST(o_sub2_eid[o], ok[u] ? rc[u].eid : 0);
+            TM_ST(o_sub2_ts[o], ok[u] ? rc[u].ts : 0.f);
         }
     }
     TM_EST(3);
@@ -887,14 +959,14 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
         const int32_t j = w / M, m = w % M;
         const int32_t v1 = h1n[j], e1 = h1e[j];
         const Step2 s2 = next_step<MC>(g, key, ev, j, M, m, u, v1, s2c[j]);
-        const Step3 s3 = final_step(g, key, ev, w, u, v1, s2.src, s2.ngh, s2.eid);
+        const Step3 s3 = final_step(g, key, ev, w, u, v1, s2.src, s2.ngh, s2.eid, s2.pos, s2.rank);
         const int64_t o = se * W + w;
         int32_t *nd = o_node6 + o * 6;
-        nd[0] = s3.src; nd[1] = s3.ngh; nd[2] = s2.src; nd[3] = s2.ngh; nd[4] = u; nd[5] = v1;
-        o_eid3[o * 3 + 0] = s3.eid; o_eid3[o * 3 + 1] = s2.eid; o_eid3[o * 3 + 2] = e1;
-        o_ts3[o * 3 + 0] = s3.ts; o_ts3[o * 3 + 1] = s2.ts; o_ts3[o * 3 + 2] = h1t[j];
+        TM_ST(nd[0], s3.src); TM_ST(nd[1], s3.ngh); TM_ST(nd[2], s2.src); TM_ST(nd[3], s2.ngh); TM_ST(nd[4], u); TM_ST(nd[5], v1);
+        TM_ST(o_eid3[o * 3 + 0], s3.eid); TM_ST(o_eid3[o * 3 + 1], s2.eid); TM_ST(o_eid3[o * 3 + 2], e1);
+        TM_ST(o_ts3[o * 3 + 0], s3.ts); TM_ST(o_ts3[o * 3 + 1], s2.ts); TM_ST(o_ts3[o * 3 + 2], h1t[j]);
         const int32_t c = cat_of(s3.code, s3.t, 0);
-        o_cat[o] = c;
+        TM_ST(o_cat[o], c);
         if (c >= 0) atomicAdd(&bins[c], 1u);
         weid[w * 3 + 0] = s3.eid; weid[w * 3 + 1] = s2.eid; weid[w * 3 + 2] = e1;
         ecnt_insert(tkeys, tcnt, tmask, s3.eid, 0);
@@ -910,7 +982,7 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
         for (int p = 0; p < 3; ++p) {
             const uint32_t c = ecnt_lookup(tkeys, tcnt, tmask, weid[w * 3 + p]);
 #pragma unroll
-            for (int q = 0; q < 3; ++q) oc[(w * 3 + p) * 3 + q] = (float)((c >> (10 * q)) & 1023u);
+            for (int q = 0; q < 3; ++q) TM_ST(oc[(w * 3 + p) * 3 + q], (float)((c >> (10 * q)) & 1023u));
         }
     }
     TM_EST(5);

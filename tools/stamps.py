@@ -5,7 +5,7 @@ import ctypes as C
 import runpy
 import sys
 
-sys.argv = ["bench.py", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+sys.argv = ["bench.py", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-extras"] + sys.argv[1:]
 runpy.run_path("bench.py", run_name="__main__")
 from tempme_amd import _lib  # noqa: E402
 
