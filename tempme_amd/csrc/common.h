@@ -72,7 +72,7 @@ __host__ __device__ inline uint32_t pblk_hash(int32_t u, int32_t x) {
 // L_l[t] = L_(l-1)[F t], h = the first level with <= F entries.  A lower bound reads one F-key node per
 // level (h + 1 lines instead of log2(n) dependent loads of a binary search).
 #ifndef TM_BLK_LOG
-#define TM_BLK_LOG 3
+#define TM_BLK_LOG 2
 #endif
 constexpr int32_t kBlkLog = TM_BLK_LOG, kBlkFan = 1 << kBlkLog;
 __host__ __device__ inline int32_t blk_levels(int32_t n) {
@@ -108,6 +108,7 @@ struct DevGraph {
     int32_t max_eid;
     int64_t n_entries;
     const int32_t *off;     // [V+1]
+    const int2 *span;       // [V] {off[u], off[u+1]}: a node's range in one 8-B load
     const Rec *rec;         // [n_entries]
     const double *tsd;      // [n_entries] fp64 timestamps (bisect keys)
     const EdgeEnds *ends;   // [max_eid+1]
@@ -236,6 +237,7 @@ struct tm_graph {
     tmk::DevGraph d;
     // device allocations
     int32_t *d_off;
+    int2 *d_span;
     tmk::Rec *d_rec;
     double *d_tsd;
     tmk::EdgeEnds *d_ends;

@@ -80,6 +80,7 @@ struct Timer {
 static void free_graph(tm_graph *g) {
     if (!g) return;
     if (g->d_off) (void)hipFree(g->d_off);
+    if (g->d_span) (void)hipFree(g->d_span);
     if (g->d_rec) (void)hipFree(g->d_rec);
     if (g->d_tsd) (void)hipFree(g->d_tsd);
     if (g->d_ends) (void)hipFree(g->d_ends);
@@ -323,6 +324,7 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
     }
     hipError_t e = hipSuccess;
     e = e ? e : hipMalloc(&g->d_off, sizeof(int32_t) * (n_nodes + 1));
+    e = e ? e : hipMalloc(&g->d_span, sizeof(int2) * n_nodes);
     e = e ? e : hipMalloc(&g->d_rec, sizeof(Rec) * nn);
     e = e ? e : hipMalloc(&g->d_tsd, sizeof(double) * nn);
     e = e ? e : hipMalloc(&g->d_ends, sizeof(EdgeEnds) * ends.size());
@@ -332,6 +334,11 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
     e = e ? e : hipMemcpy(g->d_pblk, pblk.data(), sizeof(PairBlk) * cap, hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(g->d_ets, ets.data(), sizeof(double) * ets.size(), hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(g->d_off, off32.data(), sizeof(int32_t) * (n_nodes + 1), hipMemcpyHostToDevice);
+    {
+        std::vector<int2> span(n_nodes);
+        for (int32_t u = 0; u < n_nodes; ++u) span[u] = make_int2(off32[u], off32[u + 1]);
+        e = e ? e : hipMemcpy(g->d_span, span.data(), sizeof(int2) * n_nodes, hipMemcpyHostToDevice);
+    }
     e = e ? e : hipMemcpy(g->d_rec, rec.data(), sizeof(Rec) * nn, hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(g->d_tsd, g->h_ts, sizeof(double) * nn, hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(g->d_ends, ends.data(), sizeof(EdgeEnds) * ends.size(), hipMemcpyHostToDevice);
@@ -342,8 +349,8 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
         return fail(TM_E_HIP, std::string("tm_graph_build: ") + hipGetErrorString(e));
     }
     tm.lap("upload");
-    g->d = DevGraph{n_nodes, max_eid, n,         g->d_off,  g->d_rec, g->d_tsd,
-                    g->d_ends, g->d_ppos, g->d_ets, ts_unique, g->d_pblk, cap - 1};
+    g->d = DevGraph{n_nodes,   max_eid,   n,        g->d_off,  g->d_span, g->d_rec,
+                    g->d_tsd,  g->d_ends, g->d_ppos, g->d_ets, ts_unique, g->d_pblk, cap - 1};
     *out = g;
     return TM_OK;
 }

@@ -107,7 +107,7 @@ __device__ __forceinline__ void pair_blocks(const DevGraph &g, const int32_t (&u
         if (!any) break;
         PairBlk b[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) b[k] = g.pblk[h[k]];
+        for (int k = 0; k < K; ++k) b[k] = live[k] ? g.pblk[h[k]] : PairBlk{-1, 0, 0, 0};   // no access when done
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             if (!live[k]) continue;
@@ -213,8 +213,8 @@ __device__ Step3 final_step(const DevGraph &g, Key key, uint32_t ev, uint32_t w,
     // final_len (graph.py:357, :366): node 0 / out of range -> 0; e2 not in the node's dict -> whole list
     const bool va = a_node > 0 && a_node < g.n_nodes, vb = b_node > 0 && b_node < g.n_nodes;
     const EdgeEnds x2 = (e2 >= 0 && e2 <= g.max_eid) ? g.ends[e2] : EdgeEnds{-1, 0, -1, 0};
-    const int32_t oa0 = va ? g.off[a_node] : 0, oa1 = va ? g.off[a_node + 1] : 0;
-    const int32_t ob0 = vb ? g.off[b_node] : 0, ob1 = vb ? g.off[b_node + 1] : 0;
+    const int2 oa = va ? g.span[a_node] : make_int2(0, 0), ob = vb ? g.span[b_node] : make_int2(0, 0);
+    const int32_t oa0 = oa.x, oa1 = oa.y, ob0 = ob.x, ob1 = ob.y;
     const int32_t ca = !va ? 0 : x2.node_a == a_node ? x2.len_a : x2.node_b == a_node ? x2.len_b : oa1 - oa0;
     const int32_t cb = !vb ? 0 : x2.node_a == b_node ? x2.len_a : x2.node_b == b_node ? x2.len_b : ob1 - ob0;
     int32_t na, nb, k1 = 0, n1 = 0, k2 = 0, n2 = 0, kb = 0;
