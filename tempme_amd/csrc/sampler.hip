@@ -15,6 +15,20 @@
 
 #include "common.h"
 
+#ifndef TM_KWAVE
+#define TM_KWAVE 1
+#endif
+#ifndef TM_KNT
+#define TM_KNT 0
+#endif
+#ifndef TM_ABL
+#define TM_ABL 0
+#endif
+
+#ifndef TM_REC3
+#define TM_REC3 0
+#endif
+
 #ifndef TM_LOCKSTEP
 #define TM_LOCKSTEP 0
 #endif
@@ -73,6 +87,16 @@ __device__ int32_t bisect_ts_wave(const DevGraph &g, int32_t u, double x) {
     const int32_t q = lo + lane;
     const bool lt = q < hi && g.tsd[s + q] < x;
     return lo + __popcll(__ballot(lt));
+}
+
+// a record without its block rank: one 12-B load (dwordx3)
+__device__ __forceinline__ Rec rec3(const DevGraph &g, int64_t i) {
+#if TM_REC3
+    const int3 v = *reinterpret_cast<const int3 *>(g.rec + i);
+    return Rec{v.x, v.y, __int_as_float(v.z), 0};
+#else
+    return g.rec[i];
+#endif
 }
 
 // rank-th smallest position of the union of two sorted, disjoint position lists
@@ -454,6 +478,7 @@ __host__ __device__ inline size_t khop2_lds_bytes(int32_t N) {
 
 // one level: record gathers of thread (row lr, block kb)'s 4 draws and their ranks among the row's N
 // draws in dd; results staged in LDS at (row, rank) so the workgroup writes its output range coalesced
+
 template <bool kStage, bool keyed>
 __device__ __forceinline__ void khop_emit(const DevGraph &g, int32_t N, const uint32_t *dd, int32_t lr, int32_t kb,
                                           const uint32_t (&d)[4], int32_t c, int32_t o, int32_t *sn, int32_t *se,
@@ -516,6 +541,56 @@ __device__ __forceinline__ void khop_emit(const DevGraph &g, int32_t N, const ui
     }
 }
 
+// ranks of thread (row lr, block kb)'s 4 draws d among the row's N draws in dd (np.sort order, ties by
+// index); rank stays k for an empty row
+template <bool keyed>
+__device__ __forceinline__ void khop_ranks(int32_t N, const uint32_t *dd, int32_t lr, int32_t kb,
+                                           const uint32_t (&d)[4], int32_t c, int32_t (&rank)[4]) {
+#pragma unroll
+    for (int w = 0; w < 4; ++w) rank[w] = c > 0 ? 0 : 4 * kb + w;
+    if (keyed && c > 0) {
+        // dd holds (draw << 6 | index): unique keys, so the np.sort rank (ties by index) is one compare
+        uint32_t my[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) my[w] = (d[w] << 6) | (uint32_t)(4 * kb + w);
+        const uint4 *row = reinterpret_cast<const uint4 *>(dd + lr * N);
+        if ((N & 3) == 0) {
+            for (int32_t i4 = 0; i4 < (N >> 2); ++i4) {
+                const uint4 q = row[i4];
+#pragma unroll
+                for (int w = 0; w < 4; ++w)
+                    rank[w] += (q.x < my[w]) + (q.y < my[w]) + (q.z < my[w]) + (q.w < my[w]);
+            }
+        } else {
+            for (int32_t i = 0; i < N; ++i) {
+                const uint32_t q = dd[lr * N + i];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) rank[w] += q < my[w];
+            }
+        }
+    } else if (!keyed && c > 0) {
+        if ((N & 3) == 0) {                              // row start 16-B aligned: 4 draws per LDS read
+            const uint4 *row = reinterpret_cast<const uint4 *>(dd + lr * N);
+            for (int32_t i4 = 0; i4 < (N >> 2); ++i4) {
+                const uint4 q = row[i4];
+                const uint32_t qv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int32_t i = 4 * i4 + v;
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) rank[w] += (qv[v] < d[w]) || (i < 4 * kb + w && qv[v] == d[w]);
+                }
+            }
+        } else {
+            for (int32_t i = 0; i < N; ++i) {
+                const uint32_t di = dd[lr * N + i];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) rank[w] += (di < d[w]) || (i < 4 * kb + w && di == d[w]);
+            }
+        }
+    }
+}
+
 template <bool keyed>
 __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t N, int32_t B,
                                                     const int32_t *__restrict__ root, const double *__restrict__ cut,
@@ -536,7 +611,21 @@ __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t
     oe = vptr(oe);
     ot = vptr(ot);
     // hop-1 rows
-    if (tid < ne) {
+    if (time_path && TM_KWAVE) {
+        // bisect_left on the time path by whole waves (64-ary rounds: 3 dependent loads for a
+        // 67k-entry hub list instead of 17), one root per wave at a time
+        for (int32_t r = tid >> 6; r < ne; r += (int32_t)(blockDim.x >> 6)) {
+            const int32_t u = root[e0 + r];
+            const bool vu = u >= 0 && u < g.n_nodes;
+            const int32_t c = vu ? bisect_ts_wave(g, u, cut[e0 + r]) : 0;
+            if ((tid & 63) == 0) {
+                if (!vu) set_err(err, TM_E_ARG);
+                c1[r] = c;
+                o1[r] = vu ? g.off[u] : 0;
+                ev1[r] = event_ids[e0 + r];
+            }
+        }
+    } else if (tid < ne) {
         const int32_t u = root[e0 + tid];
         const int32_t c = find_before_len(g, u, time_path, time_path ? cut[e0 + tid] : 0.0,
                                           time_path ? 0 : eidx[e0 + tid], err);
@@ -600,16 +689,52 @@ __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t
     }
     __syncthreads();
     const int64_t base2 = (int64_t)B * N + (int64_t)e0 * N * N;
-    for (int32_t x = tid; x < ne * N * NB; x += blockDim.x) {
-        const int32_t lr = x / NB, kb = x % NB;
-        uint32_t d[4];
+    // ranks (np.sort order) of each row's draws, whole rows per pass so a pass can rewrite its rows in
+    // slot order as record indices (-1: empty row -> zeros) once every thread of the pass has ranked
+    const int32_t RP = (int32_t)blockDim.x / NB, rows2 = ne * N;
+    for (int32_t r0 = 0; r0 < rows2; r0 += RP) {
+        const int32_t lr = r0 + tid / NB, kb = tid % NB;
+        const bool act = tid < RP * NB && lr < rows2;
+        int32_t rank[4] = {0, 1, 2, 3}, c = 0;
+        uint32_t d[4] = {0, 0, 0, 0};
+        if (act) {
+            c = c2[lr];
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const uint32_t v = 4 * kb + w < N ? d2[lr * N + 4 * kb + w] : 0xFFFFFFFFu;
-            d[w] = keyed ? v >> 6 : v;
+            for (int w = 0; w < 4; ++w) {
+                const uint32_t v = 4 * kb + w < N ? d2[lr * N + 4 * kb + w] : 0xFFFFFFFFu;
+                d[w] = keyed ? v >> 6 : v;
+            }
+            khop_ranks<keyed>(N, d2, lr, kb, d, c, rank);
         }
-        const int64_t ob = base2 + (int64_t)lr * N;
-        khop_emit<false, keyed>(g, N, d2, lr, kb, d, c2[lr], o2[lr], on + ob, oe + ob, ot + ob);
+        __syncthreads();
+        if (act) {
+            const int32_t o = o2[lr];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const int32_t k = 4 * kb + w;
+                if (k < N) d2[lr * N + (c > 0 ? rank[w] : k)] = c > 0 ? (uint32_t)(o + (int32_t)d[w]) : 0xFFFFFFFFu;
+            }
+        }
+    }
+    __syncthreads();
+    // gathers in output order: every store instruction writes one contiguous run per array
+    const int32_t tot = rows2 * N;
+    for (int32_t q0 = tid; q0 < tot; q0 += 4 * (int32_t)blockDim.x) {
+        Rec rc[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int32_t q = q0 + k * (int32_t)blockDim.x;
+            const int32_t ix = q < tot ? (int32_t)d2[q] : -1;
+            rc[k] = ix >= 0 ? g.rec[ix] : Rec{0, 0, 0.f, 0};
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int32_t q = q0 + k * (int32_t)blockDim.x;
+            if (q >= tot) break;
+            on[base2 + q] = rc[k].ngh;
+            oe[base2 + q] = rc[k].eid;
+            ot[base2 + q] = rc[k].ts;
+        }
     }
 }
 
@@ -899,7 +1024,10 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
     __syncthreads();
     // 4 rows of draws per lane per round: ranks from LDS, then the 4 record gathers issued together
     // (unconditional, index 0 when the row is empty) before any output is stored
-    constexpr int HB = 4;
+#ifndef TM_HB
+#define TM_HB 4
+#endif
+    constexpr int HB = TM_HB;
     for (int32_t x0 = 0; x0 < N * N; x0 += HB * 64) {
         int32_t slot[HB], idx[HB], jr[HB], kr[HB], rank[HB];
         uint32_t dr[HB];
@@ -933,7 +1061,7 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
         }
         Rec rc[HB];
 #pragma unroll
-        for (int u = 0; u < HB; ++u) rc[u] = g.n_entries > 0 ? g.rec[idx[u]] : Rec{0, 0, 0.f, 0};
+        for (int u = 0; u < HB; ++u) rc[u] = g.n_entries > 0 ? rec3(g, (TM_ABL & 8) ? (idx[u] & 4095) : (TM_ABL & 16) ? (idx[u] & ~4095) + ((idx[u] * 7) & 4095) % 64 : idx[u]) : Rec{0, 0, 0.f, 0};
 #pragma unroll
         for (int u = 0; u < HB; ++u) {
             if (x0 + u * 64 + tid >= N * N) continue;

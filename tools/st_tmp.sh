@@ -1,4 +1,6 @@
 #!/bin/bash
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
-TEMPME_LIB=$PWD/tempme_amd/lib/ab/stamps.so timeout -k 10 200 python tools/stamps.py > gpurun_out/st2.log 2>&1 || exit $?
-PASSES="1 2 4 6" ./tools/pmc_mem.sh
+timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+./tools/${AB:-khop_ab.sh}
