@@ -62,6 +62,11 @@ int tm_version(void);
  * get_ts2idx (trailing-tie quirk included) and uploads the CSR to `device`. */
 int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int32_t *ngh, const int32_t *eid,
                    const double *ts, int device, tm_graph **out);
+/* The same from raw edge rows (src, dst, e_idx, ts as int64/int64/int64/f64 arrays of n_edges):
+ * (dst, e, t) is appended to src's list, then (src, e, t) to dst's, row by row -- the adj_list
+ * construction of temp_exp_main.py:135-144 -- by a stable counting sort, then tm_graph_build. */
+int tm_graph_build_edges(int32_t n_nodes, int64_t n_edges, const int64_t *src, const int64_t *dst,
+                         const int64_t *eidx, const double *ts, int device, tm_graph **out);
 int tm_graph_free(tm_graph *g);
 int tm_graph_info(const tm_graph *g, int32_t *n_nodes, int64_t *n_entries, int32_t *max_eid);
 /* host copy of node_idx_l / edge_idx_l / node_ts_l / off_set_l (utils/graph.py:23-27) and

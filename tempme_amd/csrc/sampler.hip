@@ -36,10 +36,10 @@
 namespace tmk {
 
 #ifndef TM_NT_STORES
-#define TM_NT_STORES 1
+#define TM_NT_STORES 0
 #endif
-// sampled outputs are written once and read by the next kernel: streamed (non-temporal) so they do not
-// evict the graph's records from L2
+// TM_NT_STORES=1 streams the sampled outputs (non-temporal); measured slower (events_kernel 0.170 ->
+// 0.175 ms, and the k-hop kernel's in-row scattered outputs 2.4x slower), so plain stores by default
 #if TM_NT_STORES
 #define TM_ST(dst, v) __builtin_nontemporal_store((v), &(dst))
 #else
@@ -910,14 +910,14 @@ __device__ __forceinline__ uint32_t ecnt_lookup(const int32_t *keys, const uint3
 }
 
 // LDS of one (event, side): hop-1 row, hop-2 draws (reused as the edge-count table once hop 2 is
-// done), hop-2 cut lengths, walk edge ids, histogram
+// done), hop-2 cut lengths, walk edge ids, histogram, step-2 cuts, hop-2 record indices in slot order
 __host__ __device__ inline size_t events_d2_bytes(int32_t N, int32_t M) {
     const size_t d2 = sizeof(uint32_t) * (size_t)N * N, tab = sizeof(int32_t) * 2 * (size_t)ecnt_slots(N, N * M);
     return d2 > tab ? d2 : tab;
 }
 __host__ __device__ inline size_t events_lds_bytes(int32_t N, int32_t M) {
     return sizeof(int32_t) * ((size_t)3 * N + 2 * N + (size_t)N * M * 3 + 12) + events_d2_bytes(N, M) +
-           sizeof(Step2Cuts) * (size_t)N;
+           sizeof(Step2Cuts) * (size_t)N + sizeof(int32_t) * (size_t)N * N;
 }
 
 // Phase timing (debug builds only, -DTM_STAMPS): s_memtime deltas of lane 0 for events 2000..3999
@@ -946,6 +946,7 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
             *weid = o2 + N;
     unsigned int *bins = reinterpret_cast<unsigned int *>(weid + W * 3);
     Step2Cuts *s2c = reinterpret_cast<Step2Cuts *>(bins + 12);
+    int32_t *sidx = reinterpret_cast<int32_t *>(s2c + N);
     const DevGraph &g = a.g;
     // output pointers live in VGPRs (vptr): kept as uniform SGPR pairs next to the graph and input
     // pointers they overflow the scalar file and spill through v_readlane in every phase
@@ -1022,16 +1023,12 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
         }
     }
     __syncthreads();
-    // 4 rows of draws per lane per round: ranks from LDS, then the 4 record gathers issued together
-    // (unconditional, index 0 when the row is empty) before any output is stored
-#ifndef TM_HB
-#define TM_HB 4
-#endif
-    constexpr int HB = TM_HB;
+    // ranks (np.sort order) of 4 rows' draws per lane per round into slot order: sidx[row * N + rank] =
+    // record index (-1: empty row -> zeros)
+    constexpr int HB = 4;
     for (int32_t x0 = 0; x0 < N * N; x0 += HB * 64) {
-        int32_t slot[HB], idx[HB], jr[HB], kr[HB], rank[HB];
+        int32_t jr[HB], kr[HB], rank[HB];
         uint32_t dr[HB];
-        bool ok[HB];
 #pragma unroll
         for (int u = 0; u < HB; ++u) {
             const int32_t x = x0 + u * 64 + tid;
@@ -1049,26 +1046,34 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
                 if (keyed) rank[u] += di < dr[u];
                 else rank[u] += (di < dr[u]) || (i < kr[u] && di == dr[u]);
             }
-        if (keyed)
-#pragma unroll
-            for (int u = 0; u < HB; ++u) dr[u] >>= 6;                  // back to the draw
 #pragma unroll
         for (int u = 0; u < HB; ++u) {
-            const int32_t x = x0 + u * 64 + tid, c = x < N * N ? c2[jr[u]] : 0;
-            ok[u] = c > 0 && g.n_entries > 0;
-            slot[u] = c > 0 ? jr[u] * N + rank[u] : x;
-            idx[u] = ok[u] ? o2[jr[u]] + (int32_t)dr[u] : 0;
+            const int32_t x = x0 + u * 64 + tid;
+            if (x >= N * N) continue;
+            const int32_t c = c2[jr[u]];
+            const bool ok = c > 0 && g.n_entries > 0;
+            sidx[c > 0 ? jr[u] * N + rank[u] : x] = ok ? o2[jr[u]] + (int32_t)(keyed ? dr[u] >> 6 : dr[u]) : -1;
         }
-        Rec rc[HB];
+    }
+    __syncthreads();
+    // gathers in output order, 4 in flight per lane: each store instruction writes one contiguous run per
+    // array (stores scattered inside the rows cost the k-hop kernel a third of its time)
+    for (int32_t q0 = tid; q0 < N * N; q0 += 4 * 64) {
+        Rec rc[4];
 #pragma unroll
-        for (int u = 0; u < HB; ++u) rc[u] = g.n_entries > 0 ? rec3(g, (TM_ABL & 8) ? (idx[u] & 4095) : (TM_ABL & 16) ? (idx[u] & ~4095) + ((idx[u] * 7) & 4095) % 64 : idx[u]) : Rec{0, 0, 0.f, 0};
+        for (int k = 0; k < 4; ++k) {
+            const int32_t q = q0 + 64 * k;
+            const int32_t ix = q < N * N ? sidx[q] : -1;
+            rc[k] = ix >= 0 ? g.rec[ix] : Rec{0, 0, 0.f, 0};
+        }
 #pragma unroll
-        for (int u = 0; u < HB; ++u) {
-            if (x0 + u * 64 + tid >= N * N) continue;
-            const int64_t o = se * N * N + slot[u];
-            TM_ST(o_sub2_node[o], ok[u] ? rc[u].ngh : 0);
-            TM_ST(o_sub2_eid[o], ok[u] ? rc[u].eid : 0);
-            TM_ST(o_sub2_ts[o], ok[u] ? rc[u].ts : 0.f);
+        for (int k = 0; k < 4; ++k) {
+            const int32_t q = q0 + 64 * k;
+            if (q >= N * N) break;
+            const int64_t o = se * N * N + q;
+            o_sub2_node[o] = rc[k].ngh;
+            o_sub2_eid[o] = rc[k].eid;
+            o_sub2_ts[o] = rc[k].ts;
         }
     }
     TM_EST(3);

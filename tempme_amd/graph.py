@@ -59,18 +59,30 @@ def _flatten_adj(adj_list):
 
 
 class DeviceGraph:
-    """Owns one ``tm_graph`` handle (CSR + e_idx table + pair index on one device)."""
+    """Owns one ``tm_graph`` handle (CSR + e_idx table + block search trees on one device)."""
 
-    def __init__(self, in_off, ngh, eid, ts, device=None):
+    def __init__(self, in_off, ngh, eid, ts, device=None, *, _edges=None):
         self.device = L.require_device(device)
-        in_off = np.ascontiguousarray(in_off, np.int64)
-        ngh = np.ascontiguousarray(ngh, np.int32)
-        eid = np.ascontiguousarray(eid, np.int32)
-        ts = np.ascontiguousarray(ts, np.float64)
-        self.n_nodes = len(in_off) - 1
         h = C.c_void_p()
-        L.check(L.lib().tm_graph_build(self.n_nodes, in_off.ctypes.data, ngh.ctypes.data, eid.ctypes.data,
-                                       ts.ctypes.data, self.device.index, C.byref(h)), "tm_graph_build")
+        if _edges is not None:
+            # edge rows: the owner-major adjacency is built by the library (counting sort, C++)
+            src, dst, e, t, n_nodes = _edges
+            src = np.ascontiguousarray(src, np.int64)
+            dst = np.ascontiguousarray(dst, np.int64)
+            e = np.ascontiguousarray(e, np.int64)
+            t = np.ascontiguousarray(t, np.float64)
+            self.n_nodes = int(n_nodes)
+            L.check(L.lib().tm_graph_build_edges(self.n_nodes, len(src), src.ctypes.data, dst.ctypes.data,
+                                                 e.ctypes.data, t.ctypes.data, self.device.index, C.byref(h)),
+                    "tm_graph_build_edges")
+        else:
+            in_off = np.ascontiguousarray(in_off, np.int64)
+            ngh = np.ascontiguousarray(ngh, np.int32)
+            eid = np.ascontiguousarray(eid, np.int32)
+            ts = np.ascontiguousarray(ts, np.float64)
+            self.n_nodes = len(in_off) - 1
+            L.check(L.lib().tm_graph_build(self.n_nodes, in_off.ctypes.data, ngh.ctypes.data, eid.ctypes.data,
+                                           ts.ctypes.data, self.device.index, C.byref(h)), "tm_graph_build")
         self.handle = h
         n_nodes, n_ent, max_eid = C.c_int32(), C.c_int64(), C.c_int32()
         L.check(L.lib().tm_graph_info(h, C.byref(n_nodes), C.byref(n_ent), C.byref(max_eid)), "tm_graph_info")
@@ -96,7 +108,7 @@ class DeviceGraph:
 
 class NeighborFinder:
     def __init__(self, adj_list, bias=0, ts_precision=PRECISION, use_cache=False, sample_method="multinomial",
-                 device=None, *, seed=0, split=L.SPLIT_TEST, _flat=None):
+                 device=None, *, seed=0, split=L.SPLIT_TEST, _flat=None, _edges=None):
         if not math.isclose(bias, 0) or sample_method != "multinomial":
             # graph.py:219-227 (bias != 0, 'binary') are unreachable from every reference caller
             raise NotImplementedError("only bias=0, sample_method='multinomial' (the reference's only live path)")
@@ -107,16 +119,27 @@ class NeighborFinder:
         self.seed = int(seed)
         self.split = int(split)
         self._next_event = 0
-        off, ngh, eid, ts = _flat if _flat is not None else _flatten_adj(adj_list)
-        self.graph = DeviceGraph(off, ngh, eid, ts, device)
+        if _edges is not None:
+            self.graph = DeviceGraph(None, None, None, None, device, _edges=_edges)
+        else:
+            off, ngh, eid, ts = _flat if _flat is not None else _flatten_adj(adj_list)
+            self.graph = DeviceGraph(off, ngh, eid, ts, device)
         self.device = self.graph.device
-        o, n, e, t, dv = self.graph.export()
-        self.off_set_l = o
-        self.node_idx_l = n.astype(np.int64)
-        self.edge_idx_l = e.astype(np.int64)
-        self.node_ts_l = t
-        self._dict_val = dv
+        self._host = None
         self._ne2i = None
+
+    # host copies of the CSR (graph.py:23-27), exported on first use: the sampling kernels never need them
+    def _export(self):
+        if self._host is None:
+            o, n, e, t, dv = self.graph.export()
+            self._host = (o, n.astype(np.int64), e.astype(np.int64), t, dv)
+        return self._host
+
+    off_set_l = property(lambda self: self._export()[0])
+    node_idx_l = property(lambda self: self._export()[1])
+    edge_idx_l = property(lambda self: self._export()[2])
+    node_ts_l = property(lambda self: self._export()[3])
+    _dict_val = property(lambda self: self._export()[4])
 
     @classmethod
     def from_edges(cls, src, dst, eidx, ts, n_nodes=None, **kw):
@@ -124,7 +147,7 @@ class NeighborFinder:
         the adj_list construction of temp_exp_main.py:135-144)."""
         if n_nodes is None:
             n_nodes = int(max(np.max(src), np.max(dst))) + 1
-        return cls(None, _flat=adjacency_from_edges(src, dst, eidx, ts, n_nodes), **kw)
+        return cls(None, _edges=(src, dst, eidx, ts, n_nodes), **kw)
 
     # ------------------------------------------------------------ host-side views
     @property
