@@ -15,23 +15,8 @@
 
 #include "common.h"
 
-#ifndef TM_KWAVE
-#define TM_KWAVE 1
-#endif
-#ifndef TM_KNT
-#define TM_KNT 0
-#endif
-#ifndef TM_ABL
-#define TM_ABL 0
-#endif
 
-#ifndef TM_REC3
-#define TM_REC3 0
-#endif
 
-#ifndef TM_LOCKSTEP
-#define TM_LOCKSTEP 0
-#endif
 
 namespace tmk {
 
@@ -87,16 +72,6 @@ __device__ int32_t bisect_ts_wave(const DevGraph &g, int32_t u, double x) {
     const int32_t q = lo + lane;
     const bool lt = q < hi && g.tsd[s + q] < x;
     return lo + __popcll(__ballot(lt));
-}
-
-// a record without its block rank: one 12-B load (dwordx3)
-__device__ __forceinline__ Rec rec3(const DevGraph &g, int64_t i) {
-#if TM_REC3
-    const int3 v = *reinterpret_cast<const int3 *>(g.rec + i);
-    return Rec{v.x, v.y, __int_as_float(v.z), 0};
-#else
-    return g.rec[i];
-#endif
 }
 
 // rank-th smallest position of the union of two sorted, disjoint position lists
@@ -251,19 +226,8 @@ __device__ Step3 final_step(const DevGraph &g, Key key, uint32_t ev, uint32_t w,
         int32_t bs[3], bn[3], cnt[3];
         pair_blocks<3>(g, us, xs, bs, bn);
         const bool r2 = pos2 >= 0 && ca == pos2;
-#if TM_LOCKSTEP
-        {   // a1 and b in lockstep; a2 only when a tie group moved e2's cut off its own record
-            const int32_t b2[2] = {bs[0], bs[2]}, n2_[2] = {bn[0], bn[2]}, p2_[2] = {ca, cb};
-            const bool l2[2] = {true, true};
-            int32_t r2_[2];
-            blk_lb_multi<2>(g, b2, n2_, p2_, l2, r2_);
-            cnt[0] = r2_[0];
-            cnt[2] = r2_[1];
-        }
-#else
         cnt[0] = blk_lb(g, bs[0], bn[0], ca);
         cnt[2] = blk_lb(g, bs[2], bn[2], cb);
-#endif
         cnt[1] = r2 ? 0 : blk_lb(g, bs[1], bn[1], ca);   // a tie group moved e2's cut off its own record
         n1 = cnt[0];
         n2 = r2 ? (sa ? rank2 : 0) : cnt[1];
@@ -611,21 +575,7 @@ __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t
     oe = vptr(oe);
     ot = vptr(ot);
     // hop-1 rows
-    if (time_path && TM_KWAVE) {
-        // bisect_left on the time path by whole waves (64-ary rounds: 3 dependent loads for a
-        // 67k-entry hub list instead of 17), one root per wave at a time
-        for (int32_t r = tid >> 6; r < ne; r += (int32_t)(blockDim.x >> 6)) {
-            const int32_t u = root[e0 + r];
-            const bool vu = u >= 0 && u < g.n_nodes;
-            const int32_t c = vu ? bisect_ts_wave(g, u, cut[e0 + r]) : 0;
-            if ((tid & 63) == 0) {
-                if (!vu) set_err(err, TM_E_ARG);
-                c1[r] = c;
-                o1[r] = vu ? g.off[u] : 0;
-                ev1[r] = event_ids[e0 + r];
-            }
-        }
-    } else if (tid < ne) {
+    if (tid < ne) {
         const int32_t u = root[e0 + tid];
         const int32_t c = find_before_len(g, u, time_path, time_path ? cut[e0 + tid] : 0.0,
                                           time_path ? 0 : eidx[e0 + tid], err);
@@ -1095,6 +1045,8 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
         const Step3 s3 = final_step(g, key, ev, w, u, v1, s2.src, s2.ngh, s2.eid, s2.pos, s2.rank);
         const int64_t o = se * W + w;
         int32_t *nd = o_node6 + o * 6;
+        // per-lane row stores (24 / 12 B per walk); staging them in LDS for contiguous runs measured
+        // slower (0.170 -> 0.178 ms: the extra LDS costs resident workgroups)
         TM_ST(nd[0], s3.src); TM_ST(nd[1], s3.ngh); TM_ST(nd[2], s2.src); TM_ST(nd[3], s2.ngh); TM_ST(nd[4], u); TM_ST(nd[5], v1);
         TM_ST(o_eid3[o * 3 + 0], s3.eid); TM_ST(o_eid3[o * 3 + 1], s2.eid); TM_ST(o_eid3[o * 3 + 2], e1);
         TM_ST(o_ts3[o * 3 + 0], s3.ts); TM_ST(o_ts3[o * 3 + 1], s2.ts); TM_ST(o_ts3[o * 3 + 2], h1t[j]);
