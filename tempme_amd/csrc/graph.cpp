@@ -106,12 +106,23 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
     if (n >= INT32_MAX / 2) return fail(TM_E_UNSUPPORTED, "tm_graph_build: more than 2^30-1 adjacency entries");
     for (int32_t u = 0; u < n_nodes; ++u)
         if (in_off[u + 1] < in_off[u]) return fail(TM_E_ARG, "tm_graph_build: in_off not monotone");
-    int32_t max_eid = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        if (ngh[i] < 0 || ngh[i] >= n_nodes) return fail(TM_E_ARG, "tm_graph_build: neighbor id out of range");
-        if (eid[i] < 0) return fail(TM_E_ARG, "tm_graph_build: negative edge id");
-        max_eid = std::max(max_eid, eid[i]);
-    }
+    // range checks and the largest edge id, in parallel chunks
+    std::atomic<int32_t> max_eid_a{0}, bad{0};
+    parallel_for(n, 1 << 16, [&](int, int64_t b, int64_t e) {
+        int32_t m = 0, bd = 0;
+        for (int64_t i = b; i < e; ++i) {
+            if (ngh[i] < 0 || ngh[i] >= n_nodes) bd |= 1;
+            if (eid[i] < 0) bd |= 2;
+            m = std::max(m, eid[i]);
+        }
+        int32_t cur = max_eid_a.load();
+        while (m > cur && !max_eid_a.compare_exchange_weak(cur, m)) {
+        }
+        if (bd) bad.fetch_or(bd);
+    });
+    if (bad.load() & 1) return fail(TM_E_ARG, "tm_graph_build: neighbor id out of range");
+    if (bad.load() & 2) return fail(TM_E_ARG, "tm_graph_build: negative edge id");
+    const int32_t max_eid = max_eid_a.load();
 
     tm_graph *g = new tm_graph();
     g->device = device;
@@ -121,28 +132,46 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
     g->h_eid = new int32_t[nn];
     g->h_dict = new int32_t[nn];
     g->h_ts = new double[nn];
-    std::vector<Rec> rec(nn, Rec{0, 0, 0.f, 0});
+    std::unique_ptr<Rec[]> rec(new Rec[nn]);          // every entry written by the node pass
     std::vector<int32_t> off32(n_nodes + 1);
     for (int32_t u = 0; u <= n_nodes; ++u) {
         g->h_off[u] = in_off[u];
         off32[u] = (int32_t)in_off[u];
     }
-    // timestamp of each edge id (the first record's) and whether all its records agree
-    std::vector<double> ets((size_t)max_eid + 1, 0.0);
-    std::vector<char> seen((size_t)max_eid + 1, 0);
-    int32_t ts_unique = 1;
-    for (int64_t i = 0; i < n; ++i) {
-        if (!seen[eid[i]]) {
-            seen[eid[i]] = 1;
-            ets[eid[i]] = ts[i];
-        } else if (!(ets[eid[i]] == ts[i])) {
-            ts_unique = 0;
+    // timestamp of each edge id (its first record's) and whether all its records agree: the first
+    // record by an atomic min over entry indices, then a parallel compare
+    std::unique_ptr<std::atomic<int64_t>[]> first(new std::atomic<int64_t>[(size_t)max_eid + 1]);
+    parallel_for((int64_t)max_eid + 1, 1 << 16, [&](int, int64_t b, int64_t e) {
+        for (int64_t i = b; i < e; ++i) first[i].store(INT64_MAX, std::memory_order_relaxed);
+    });
+    parallel_for(n, 1 << 16, [&](int, int64_t b, int64_t e) {
+        for (int64_t i = b; i < e; ++i) {
+            std::atomic<int64_t> &f = first[eid[i]];
+            int64_t cur = f.load(std::memory_order_relaxed);
+            while (i < cur && !f.compare_exchange_weak(cur, i, std::memory_order_relaxed)) {
+            }
         }
-    }
+    });
+    std::vector<double> ets((size_t)max_eid + 1);
+    parallel_for((int64_t)max_eid + 1, 1 << 16, [&](int, int64_t b, int64_t e) {
+        for (int64_t i = b; i < e; ++i) {
+            const int64_t f = first[i].load(std::memory_order_relaxed);
+            ets[i] = f == INT64_MAX ? 0.0 : ts[f];
+        }
+    });
+    std::atomic<int32_t> ts_diff{0};
+    parallel_for(n, 1 << 16, [&](int, int64_t b, int64_t e) {
+        for (int64_t i = b; i < e; ++i)
+            if (!(ets[eid[i]] == ts[i])) {
+                ts_diff.store(1);
+                return;
+            }
+    });
+    const int32_t ts_unique = ts_diff.load() ? 0 : 1;
     tm.lap("validate");
 
     // ---- per node: stable sort by ts, get_ts2idx, (neighbour, position) blocks and ranks
-    std::vector<int64_t> pair_key(nn);     // per entry after the sort: ngh << 32 | position
+    std::unique_ptr<int64_t[]> pair_key(new int64_t[nn]);     // per entry after the sort: ngh << 32 | position
     std::vector<int32_t> nblk(n_nodes + 1, 0), plen(n_nodes + 1, 0);
     // per-thread scratch: the dense dict (every slot read is written first in the same list) and the
     // sort / tie buffers
@@ -201,7 +230,7 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
                 g->h_dict[s + i] = dval[g->h_eid[s + i]];
                 pair_key[s + i] = (int64_t)g->h_ngh[s + i] << 32 | (int64_t)i;
             }
-            std::sort(pair_key.begin() + s, pair_key.begin() + s + d);
+            std::sort(pair_key.get() + s, pair_key.get() + s + d);
             int32_t blocks = 0, len = 0;
             for (int64_t i = 0; i < d;) {
                 int64_t j = i + 1;
@@ -233,8 +262,9 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
         free_graph(g);
         return fail(TM_E_UNSUPPORTED, "tm_graph_build: block trees exceed 2^31 entries");
     }
-    std::vector<int32_t> ppos(n_ppos, INT32_MAX);
-    std::vector<PairBlk> blist(std::max<int64_t>(n_blocks, 1));
+    std::unique_ptr<int32_t[]> ppos(new int32_t[n_ppos]);
+    parallel_for(n_ppos, 1 << 18, [&](int, int64_t b, int64_t e) { std::fill(ppos.get() + b, ppos.get() + e, INT32_MAX); });
+    std::unique_ptr<PairBlk[]> blist(new PairBlk[std::max<int64_t>(n_blocks, 1)]);
     parallel_for(n_nodes, 16, [&](int, int64_t b, int64_t e) {
         for (int64_t u = b; u < e; ++u) {
             const int64_t s = in_off[u], d = in_off[u + 1] - s;
@@ -246,7 +276,7 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
                 const int32_t bn = (int32_t)(j - i);
                 if (bn > kBlkFan) len = (len + kBlkFan - 1) & ~(kBlkFan - 1);
                 const int64_t base = poff[u] + len;
-                int32_t *keys = ppos.data() + base + blk_keys_off(bn);
+                int32_t *keys = ppos.get() + base + blk_keys_off(bn);
                 for (int64_t k = i; k < j; ++k) keys[k - i] = (int32_t)(pair_key[s + k] & 0xFFFFFFFF);
                 if (bn > kBlkFan) {   // fence levels, bottom-up: L_l[t] = L_(l-1)[F t]
                     const int32_t h = blk_levels(bn);
@@ -254,7 +284,7 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
                     int64_t lo_off = blk_keys_off(bn);
                     for (int32_t l = 1; l <= h; ++l) {
                         lo_off -= blk_level_len(bn, l, h);
-                        int32_t *lev = ppos.data() + base + lo_off;
+                        int32_t *lev = ppos.get() + base + lo_off;
                         const int32_t cnt =
                             (int32_t)(((int64_t)bn + ((int64_t)1 << (kBlkLog * l)) - 1) >> (kBlkLog * l));
                         for (int32_t t = 0; t < cnt; ++t) lev[t] = lower[kBlkFan * t];
@@ -272,7 +302,10 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
     // ---- (node, neighbour) -> block hash table, load factor <= 1/2
     uint32_t cap = 16;
     while ((int64_t)cap < 2 * n_blocks) cap <<= 1;
-    std::vector<PairBlk> pblk(cap, PairBlk{-1, 0, 0, 0});
+    std::unique_ptr<PairBlk[]> pblk(new PairBlk[cap]);
+    parallel_for(cap, 1 << 18, [&](int, int64_t b, int64_t e) {
+        std::fill(pblk.get() + b, pblk.get() + e, PairBlk{-1, 0, 0, 0});
+    });
     parallel_for(n_blocks, 4096, [&](int, int64_t b, int64_t e) {
         for (int64_t i = b; i < e; ++i) {
             const PairBlk &x = blist[i];
@@ -293,27 +326,63 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
     });
     tm.lap("block table");
 
-    // ---- e_idx -> (owner, slice length), owners in node order
-    std::vector<EdgeEnds> ends((size_t)max_eid + 1, EdgeEnds{-1, 0, -1, 0});
-    for (int32_t u = 0; u < n_nodes; ++u) {
-        const int64_t s = in_off[u], d = in_off[u + 1] - s;
-        for (int64_t i = 0; i < d; ++i) {
-            int32_t v = g->h_dict[s + i];
-            if (v < 0) v = (int32_t)std::max<int64_t>(0, d + v);  // Python slice with a negative stop
-            EdgeEnds &x = ends[g->h_eid[s + i]];
-            if (x.node_a == -1 || x.node_a == u) {
-                x.node_a = u;
-                x.len_a = v;
-            } else if (x.node_b == -1 || x.node_b == u) {
-                x.node_b = u;
-                x.len_b = v;
-            } else {
-                free_graph(g);
-                return fail(TM_E_UNSUPPORTED, "tm_graph_build: edge id " + std::to_string(g->h_eid[s + i]) +
-                                                  " appears in the lists of more than two nodes");
+    // ---- e_idx -> (owner, slice length): owner a = the first node (in node order) holding the edge, b the
+    // second (graph.py's dict per node); more than two owners is unsupported.  Owners by atomic min/max,
+    // then every entry writes its owner's slice length (the same value for every entry of one list).
+    std::vector<EdgeEnds> ends((size_t)max_eid + 1);
+    std::unique_ptr<std::atomic<int32_t>[]> amin(new std::atomic<int32_t>[(size_t)max_eid + 1]),
+        amax(new std::atomic<int32_t>[(size_t)max_eid + 1]);
+    parallel_for((int64_t)max_eid + 1, 1 << 16, [&](int, int64_t b, int64_t e) {
+        for (int64_t i = b; i < e; ++i) {
+            amin[i].store(INT32_MAX, std::memory_order_relaxed);
+            amax[i].store(-1, std::memory_order_relaxed);
+        }
+    });
+    parallel_for(n_nodes, 64, [&](int, int64_t b, int64_t e) {
+        for (int64_t u = b; u < e; ++u)
+            for (int64_t i = in_off[u]; i < in_off[u + 1]; ++i) {
+                const int32_t x = g->h_eid[i];
+                int32_t c = amin[x].load(std::memory_order_relaxed);
+                while ((int32_t)u < c && !amin[x].compare_exchange_weak(c, (int32_t)u, std::memory_order_relaxed)) {
+                }
+                c = amax[x].load(std::memory_order_relaxed);
+                while ((int32_t)u > c && !amax[x].compare_exchange_weak(c, (int32_t)u, std::memory_order_relaxed)) {
+                }
+            }
+    });
+    std::atomic<int64_t> third{-1};
+    parallel_for(n_nodes, 64, [&](int, int64_t b, int64_t e) {
+        for (int64_t u = b; u < e; ++u) {
+            const int64_t s0 = in_off[u], d = in_off[u + 1] - s0;
+            for (int64_t i = s0; i < s0 + d; ++i) {
+                const int32_t x = g->h_eid[i];
+                const int32_t a = amin[x].load(std::memory_order_relaxed), bb = amax[x].load(std::memory_order_relaxed);
+                int32_t v = g->h_dict[i];
+                if (v < 0) v = (int32_t)std::max<int64_t>(0, d + v);  // Python slice with a negative stop
+                if (u == a) {
+                    ends[x].node_a = a;
+                    ends[x].len_a = v;
+                } else if (u == bb) {
+                    ends[x].node_b = bb;
+                    ends[x].len_b = v;
+                } else {
+                    third.store(x);
+                }
             }
         }
+    });
+    if (third.load() >= 0) {
+        free_graph(g);
+        return fail(TM_E_UNSUPPORTED, "tm_graph_build: edge id " + std::to_string(third.load()) +
+                                          " appears in the lists of more than two nodes");
     }
+    parallel_for((int64_t)max_eid + 1, 1 << 16, [&](int, int64_t b, int64_t e) {
+        for (int64_t i = b; i < e; ++i) {
+            const int32_t a = amin[i].load(std::memory_order_relaxed), bb = amax[i].load(std::memory_order_relaxed);
+            if (a == INT32_MAX) ends[i] = EdgeEnds{-1, 0, -1, 0};
+            else if (a == bb) ends[i].node_b = -1, ends[i].len_b = 0;
+        }
+    });
     tm.lap("edge ends");
 
     int prev = 0;
@@ -328,10 +397,10 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
     e = e ? e : hipMalloc(&g->d_rec, sizeof(Rec) * nn);
     e = e ? e : hipMalloc(&g->d_tsd, sizeof(double) * nn);
     e = e ? e : hipMalloc(&g->d_ends, sizeof(EdgeEnds) * ends.size());
-    e = e ? e : hipMalloc(&g->d_ppos, sizeof(int32_t) * ppos.size());
+    e = e ? e : hipMalloc(&g->d_ppos, sizeof(int32_t) * n_ppos);
     e = e ? e : hipMalloc(&g->d_ets, sizeof(double) * ets.size());
     e = e ? e : hipMalloc(&g->d_pblk, sizeof(PairBlk) * cap);
-    e = e ? e : hipMemcpy(g->d_pblk, pblk.data(), sizeof(PairBlk) * cap, hipMemcpyHostToDevice);
+    e = e ? e : hipMemcpy(g->d_pblk, pblk.get(), sizeof(PairBlk) * cap, hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(g->d_ets, ets.data(), sizeof(double) * ets.size(), hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(g->d_off, off32.data(), sizeof(int32_t) * (n_nodes + 1), hipMemcpyHostToDevice);
     {
@@ -339,10 +408,10 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
         for (int32_t u = 0; u < n_nodes; ++u) span[u] = make_int2(off32[u], off32[u + 1]);
         e = e ? e : hipMemcpy(g->d_span, span.data(), sizeof(int2) * n_nodes, hipMemcpyHostToDevice);
     }
-    e = e ? e : hipMemcpy(g->d_rec, rec.data(), sizeof(Rec) * nn, hipMemcpyHostToDevice);
+    e = e ? e : hipMemcpy(g->d_rec, rec.get(), sizeof(Rec) * nn, hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(g->d_tsd, g->h_ts, sizeof(double) * nn, hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(g->d_ends, ends.data(), sizeof(EdgeEnds) * ends.size(), hipMemcpyHostToDevice);
-    e = e ? e : hipMemcpy(g->d_ppos, ppos.data(), sizeof(int32_t) * ppos.size(), hipMemcpyHostToDevice);
+    e = e ? e : hipMemcpy(g->d_ppos, ppos.get(), sizeof(int32_t) * n_ppos, hipMemcpyHostToDevice);
     (void)hipSetDevice(prev);
     if (e != hipSuccess) {
         free_graph(g);
@@ -363,30 +432,62 @@ extern "C" int tm_graph_build_edges(int32_t n_nodes, int64_t n_edges, const int6
     if (!out || n_nodes <= 0 || n_edges < 0) return fail(TM_E_ARG, "tm_graph_build_edges: bad arguments");
     if (n_edges > 0 && (!src || !dst || !eidx || !ts)) return fail(TM_E_ARG, "tm_graph_build_edges: NULL arrays");
     if (2 * n_edges >= INT32_MAX / 2) return fail(TM_E_UNSUPPORTED, "tm_graph_build_edges: too many edges");
+    Timer tm;
+    // per-chunk node counts, then each chunk scatters its rows in order (stable)
+    const int T = std::max(1, (int)std::min<int64_t>(build_threads(), (n_edges + 65535) / 65536));
+    const int64_t chunk = (n_edges + T - 1) / T;
+    std::vector<std::vector<int32_t>> cnt(T);
+    std::atomic<int> bad{0};
+    parallel_for(T, 1, [&](int, int64_t tb, int64_t te) {
+        for (int64_t t = tb; t < te; ++t) {
+            std::vector<int32_t> &c = cnt[t];
+            c.assign((size_t)n_nodes, 0);
+            for (int64_t i = t * chunk; i < std::min(n_edges, (t + 1) * chunk); ++i) {
+                if (src[i] < 0 || src[i] >= n_nodes || dst[i] < 0 || dst[i] >= n_nodes) {
+                    bad.store(1);
+                    return;
+                }
+                if (eidx[i] < 0 || eidx[i] > INT32_MAX) {
+                    bad.store(2);
+                    return;
+                }
+                ++c[src[i]];
+                ++c[dst[i]];
+            }
+        }
+    });
+    if (bad.load() == 1) return fail(TM_E_ARG, "tm_graph_build_edges: node id out of range");
+    if (bad.load() == 2) return fail(TM_E_ARG, "tm_graph_build_edges: edge id out of range");
     std::vector<int64_t> off((size_t)n_nodes + 1, 0);
-    for (int64_t i = 0; i < n_edges; ++i) {
-        if (src[i] < 0 || src[i] >= n_nodes || dst[i] < 0 || dst[i] >= n_nodes)
-            return fail(TM_E_ARG, "tm_graph_build_edges: node id out of range");
-        if (eidx[i] < 0 || eidx[i] > INT32_MAX) return fail(TM_E_ARG, "tm_graph_build_edges: edge id out of range");
-        ++off[src[i] + 1];
-        ++off[dst[i] + 1];
+    for (int32_t u = 0; u < n_nodes; ++u) {
+        int64_t acc = off[u];
+        for (int t = 0; t < T; ++t) {       // chunk t's first slot of node u
+            const int32_t c = cnt[t][u];
+            cnt[t][u] = (int32_t)(acc - off[u]);
+            acc += c;
+        }
+        off[u + 1] = acc;
     }
-    for (int32_t u = 0; u < n_nodes; ++u) off[u + 1] += off[u];
     const int64_t n = 2 * n_edges, nn = std::max<int64_t>(n, 1);
-    std::vector<int32_t> ngh(nn), eid(nn);
-    std::vector<double> t(nn);
-    std::vector<int64_t> pos(off.begin(), off.end() - 1);
-    for (int64_t i = 0; i < n_edges; ++i) {
-        int64_t p = pos[src[i]]++;
-        ngh[p] = (int32_t)dst[i];
-        eid[p] = (int32_t)eidx[i];
-        t[p] = ts[i];
-        p = pos[dst[i]]++;
-        ngh[p] = (int32_t)src[i];
-        eid[p] = (int32_t)eidx[i];
-        t[p] = ts[i];
-    }
-    return tm_graph_build(n_nodes, off.data(), ngh.data(), eid.data(), t.data(), device, out);
+    std::unique_ptr<int32_t[]> ngh(new int32_t[nn]), eid(new int32_t[nn]);
+    std::unique_ptr<double[]> t(new double[nn]);
+    parallel_for(T, 1, [&](int, int64_t tb, int64_t te) {
+        for (int64_t c = tb; c < te; ++c) {
+            std::vector<int32_t> &pos = cnt[c];
+            for (int64_t i = c * chunk; i < std::min(n_edges, (c + 1) * chunk); ++i) {
+                int64_t p = off[src[i]] + pos[src[i]]++;
+                ngh[p] = (int32_t)dst[i];
+                eid[p] = (int32_t)eidx[i];
+                t[p] = ts[i];
+                p = off[dst[i]] + pos[dst[i]]++;
+                ngh[p] = (int32_t)src[i];
+                eid[p] = (int32_t)eidx[i];
+                t[p] = ts[i];
+            }
+        }
+    });
+    tm.lap("edge rows");
+    return tm_graph_build(n_nodes, off.data(), ngh.get(), eid.get(), t.get(), device, out);
 }
 
 extern "C" int tm_graph_free(tm_graph *g) {
