@@ -381,6 +381,38 @@ int tm_profile_enable(int on);
 int tm_profile_sync(void);
 int tm_profile_entry(int i, const char **name, double *total_ms, int64_t *count);
 
+/* ---------------------------------------------------------------- base GraphMixer (f4)
+ * GraphMixer.compute_node_temporal_embeddings (GM/graphmixer.py:142-193) for R rows (roots) up to the
+ * output layer: x_mean [R, C] = the masked token mean of the mixed features (:176-178) and node_out
+ * [R, D] = the softmax-weighted neighbour-feature mean plus the root's features (:181-189).  The
+ * output layer (Linear(C + D, D)) and MergeLayer score are plain GEMMs on [x_mean | node_out].
+ * Explanation weights ew [R, N] (hop-1, NULL: none) are applied as the reference does (input and
+ * both branch outputs of every mixer, the token mean, the neighbour mean).  Eval semantics (dropout =
+ * identity).  Limits: N <= 32, HT <= 16, L <= 4, C <= 256. */
+typedef struct {
+    int32_t R, N, C, T, D, L, HT, HC; /* rows, tokens (= n_neighbors), channels (edge dim), time dim, node
+                                         dim, mixer layers, token-FFN hidden, channel-FFN hidden */
+    const int32_t *node;      /* [R] root node ids */
+    const int32_t *nid, *eid; /* [R, N] hop-1 neighbour ids / edge ids (eid unused with edge_attr) */
+    const double *cut, *ts;   /* [R] cut times, [R, N] neighbour times */
+    const float *ew;          /* [R, N] explanation weights or NULL */
+    const float *edge_attr;   /* [R, N, C] or NULL (then e_feat[eid], zeroed on padding neighbours) */
+    const float *n_feat;      /* [V, D] */
+    const float *e_feat;      /* [E, C] */
+    const float *time_w, *time_b; /* [T] TimeEncoder Linear(1, T) weight and bias */
+    const float *proj_w;      /* projection_layer.weight [C, C+T] packed by tm_gm_pack */
+    const float *proj_b;      /* [C] */
+    /* per mixer: token_norm w/b [N], token ffn.0 w [HT,N] / b, ffn.3 w [N,HT] / b, channel_norm w/b [C],
+       channel ffn.0 w [HC,C] packed / b [HC], ffn.3 w [C,HC] packed / b [C] */
+    const float *layer[4][12];
+    float *x_mean, *node_out; /* outputs */
+} tm_gm_embed_args;
+/* floats of tm_gm_pack's output for a [n_out, k] weight */
+int64_t tm_gm_packed_floats(int32_t n_out, int32_t k);
+/* W [n_out, k] row-major (nn.Linear.weight) -> MFMA B-operand fragments */
+int tm_gm_pack(const float *w, int32_t n_out, int32_t k, float *packed, void *stream);
+int tm_gm_embed(const tm_gm_embed_args *a, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -13,9 +13,46 @@ __device__ __forceinline__ int lane_id() {
     return l;
 }
 
-// MODE 0: t-major (dependent chain per tile), MODE 1: pair-interleaved tiles
+// MODE 0: t-major (dependent chain per tile), MODE 1: pair-interleaved tiles, MODE 2/4: groups of 2/4
+// tiles whose MFMAs alternate accumulators (consecutive MFMAs independent)
+template <int NTO, int NQ, int D, int GS>
+__device__ __forceinline__ void rgemm_alt(const float4 *w, const floatx4 (&x)[NQ], floatx4 (&o)[NTO]) {
+    const float4 *wp = w + lane_id();
+    constexpr int N = NTO * NQ;
+#pragma unroll
+    for (int t = 0; t < NTO; ++t) o[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float4 buf[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) buf[i] = wp[i * 64];
+    // fragment order: (group pr, step q, k): tile GS*pr + k
+#pragma unroll
+    for (int i0 = 0; i0 < N; i0 += GS) {
+        float4 wv[GS];
+#pragma unroll
+        for (int k = 0; k < GS; ++k) {
+            const int i = i0 + k;
+            wv[k] = buf[i % D];
+            if (i + D < N) buf[i % D] = wp[(i + D) * 64];
+        }
+        const int pr = i0 / (GS * NQ), q = (i0 % (GS * NQ)) / GS;
+#pragma unroll
+        for (int k = 0; k < GS; ++k) o[GS * pr + k] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[k].x, x[q].x, o[GS * pr + k], 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < GS; ++k) o[GS * pr + k] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[k].y, x[q].y, o[GS * pr + k], 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < GS; ++k) o[GS * pr + k] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[k].z, x[q].z, o[GS * pr + k], 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < GS; ++k) o[GS * pr + k] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[k].w, x[q].w, o[GS * pr + k], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 template <int NTO, int NQ, int D, int MODE>
 __device__ __forceinline__ void rgemm(const float4 *w, const floatx4 (&x)[NQ], floatx4 (&o)[NTO]) {
+    if constexpr (MODE >= 2) {
+        rgemm_alt<NTO, NQ, D, MODE>(w, x, o);
+        return;
+    }
     const float4 *wp = w + lane_id();
     constexpr int N = NTO * NQ;
 #pragma unroll
@@ -121,6 +158,13 @@ int main() {
     run<3, 0, 2>("D3 tmajor valu256 1w", w, out, blocks, iters, 100 * 1024);
     run<3, 0, 2>("D3 tmajor valu256 4w", w, out, blocks, iters, 32 * 1024);
     run<3, 1, 2>("D3 pairs valu256 2w", w, out, blocks, iters);
+    run<4, 2, 1>("D4 alt2 epi", w, out, blocks, iters);
+    run<6, 2, 1>("D6 alt2 epi", w, out, blocks, iters);
+    run<4, 4, 1>("D4 alt4 epi", w, out, blocks, iters);
+    run<8, 4, 1>("D8 alt4 epi", w, out, blocks, iters);
+    run<4, 2, 1>("D4 alt2 epi 1 wave/SIMD", w, out, blocks, iters, 100 * 1024);
+    run<4, 2, 2>("D4 alt2 valu256 2w", w, out, blocks, iters);
+    run<4, 2, 2>("D4 alt2 valu256 1w", w, out, blocks, iters, 100 * 1024);
     run<3, 0, 1>("D3 tmajor epi 1 wave/SIMD", w, out, blocks, iters, 100 * 1024);
     run<3, 0, 1>("D3 tmajor epi 4 waves/SIMD", w, out, blocks, iters, 32 * 1024);
     run<3, 1, 1>("D3 pairs epi 4 waves/SIMD", w, out, blocks, iters, 32 * 1024);

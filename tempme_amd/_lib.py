@@ -37,7 +37,7 @@ EXPORTS = (
     "tm_encoder_workspace_bytes",
     "tm_encoder_fwd", "tm_encoder_fwd_tab", "tm_encoder_train_fwd", "tm_encoder_bwd", "tm_encoder_wgrad", "tm_wgrad",
     "tm_explain_train_fwd", "tm_explain_train_bwd", "tm_kl_loss", "tm_edge_importance", "tm_edge_gate_table",
-    "tm_edge_table_cols", "tm_edge_tables", "tm_edge_feature_table", "tm_edge_importance_tab", "tm_tgn_attn_fwd", "tm_tgn_attn_bwd",
+    "tm_edge_table_cols", "tm_edge_tables", "tm_edge_feature_table", "tm_edge_importance_tab", "tm_tgn_attn_fwd", "tm_tgn_attn_bwd", "tm_gm_packed_floats", "tm_gm_pack", "tm_gm_embed",
     "tm_mask_least_important", "tm_profile_enable", "tm_profile_sync", "tm_profile_entry",
 )
 
@@ -56,6 +56,14 @@ class TgnAttn(C.Structure):
                 ("node_tab", C.c_void_p), ("node_idx", C.c_void_p), ("edge_tab", C.c_void_p),
                 ("edge_idx", C.c_void_p), ("dt", C.c_void_p), ("time_w", C.c_void_p), ("time_b", C.c_void_p),
                 ("mask_node", C.c_void_p), ("ew", C.c_void_p), ("qf", C.c_void_p), ("err_flag", C.c_void_p)]
+
+
+class GmEmbedArgs(C.Structure):
+    """tm_gm_embed_args (include/tempme.h)."""
+    _fields_ = [(n, C.c_int32) for n in ("R", "N", "C", "T", "D", "L", "HT", "HC")] + \
+               [(n, C.c_void_p) for n in ("node", "nid", "eid", "cut", "ts", "ew", "edge_attr", "n_feat", "e_feat",
+                                          "time_w", "time_b", "proj_w", "proj_b")] + \
+               [("layer", (C.c_void_p * 12) * 4), ("x_mean", C.c_void_p), ("node_out", C.c_void_p)]
 
 
 GRAD_IO_FIELDS = ("imp", "dlogit", "M2", "dM2", "M1d", "dM1", "X", "dY2", "H1d", "dH1", "O", "dP", "dQ", "dF",
@@ -137,6 +145,10 @@ def _sig(L):
     L.tm_edge_feature_table.argtypes = [vp, vp, i32, vp, vp]
     L.tm_encoder_fwd_tab.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.tm_edge_importance_tab.argtypes = [vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.tm_gm_packed_floats.restype = i64
+    L.tm_gm_packed_floats.argtypes = [i32, i32]
+    L.tm_gm_pack.argtypes = [vp, i32, i32, vp, vp]
+    L.tm_gm_embed.argtypes = [C.POINTER(GmEmbedArgs), vp]
     L.tm_tgn_attn_fwd.argtypes = [C.POINTER(TgnAttn), vp, vp, vp]
     L.tm_tgn_attn_bwd.argtypes = [C.POINTER(TgnAttn), vp, vp, vp, vp, vp]
     L.tm_mask_least_important.argtypes = [vp, i32, i32, vp, i32, vp, vp, vp]

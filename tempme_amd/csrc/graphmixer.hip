@@ -1,0 +1,350 @@
+// Base-GraphMixer node embeddings with hop-1 explanation weights on gfx950 (the consumer of the
+// explanation path for base_type == 'graphmixer': temp_exp_main.py feeds retrieve_explanation's
+// hop-1 weights into GraphMixer.contrast).
+//
+// Reference (dharunm236/TempME, GraphM/graphmixer.py):
+//   compute_node_temporal_embeddings :142-193  edge features (zeroed on padding neighbours unless
+//                                              edge_attr is given), TimeEncoder of cut - t (zeroed on
+//                                              padding), projection, MLPMixer x L, masked mean over the
+//                                              tokens, softmax(valid ? 1 : -1e10) * ew neighbour mean
+//   TimeEncoder                      :21-50    cos(Linear(1, d)(t))
+//   MLPMixer / FeedForwardNet        :244-315  token mix (LayerNorm over tokens, N -> N/2 -> N, GELU),
+//                                              channel mix (LayerNorm over channels, C -> 4C -> C), the
+//                                              explanation weight on the input and both branch outputs
+//
+// One workgroup (4 waves) per row (root node): the row's N <= 32 neighbour tokens stay in LDS for the
+// whole embedding.  GEMMs (projection, channel FFN) on fp32 MFMA 16x16x4 with the activations as the
+// A operand read from LDS (ds_read_b128: LDS layout swaps the (4 k-steps x 4 lane groups) inside every
+// 16-wide K block so a lane's four K values are contiguous) and the weights as the B operand from
+// fragments packed once per weight version (tm_gm_pack, one dwordx4 per lane per 16-K block); the
+// waves split the output tiles and each does both 16-token tiles with one weight fragment.  The
+// channel FFN's 4C hidden features go through LDS in chunks of 256 (GELU in the first GEMM's
+// epilogue, the second GEMM accumulating across chunks in registers).  Token mixing, LayerNorms and
+// the masked means are VALU / wave reductions.  The output layer and the MergeLayer score are plain
+// [rows x 2C] GEMMs left to the library (tempme_amd/graphmixer.py).
+#include <algorithm>
+
+#include "common.h"
+
+namespace tmk {
+
+typedef float gmx4 __attribute__((ext_vector_type(4)));
+
+constexpr int GM_MT = 32;      // tokens per row (two 16-row MFMA tiles)
+constexpr int GM_HCH = 256;    // channel-FFN hidden features per LDS chunk
+constexpr int GM_MAXL = 4;
+
+struct GmArgs {
+    int32_t R, N, C, T, D, L, HT, HC;
+    const int32_t *node, *nid, *eid;
+    const double *cut, *ts;
+    const float *ew, *edge_attr, *n_feat, *e_feat, *time_w, *time_b;
+    const float4 *proj_w;
+    const float *proj_b;
+    const float *lw[GM_MAXL][12];
+    float *x_mean, *node_out;
+};
+
+__host__ __device__ inline int32_t gm_r16(int32_t x) { return (x + 15) & ~15; }
+
+// LDS index of (token m, feature k) in a [32][P] image: inside each 16-wide K block the position of
+// k = 16G + 4s + j is 16G + 4j + s, so lane group j's four K values of one MFMA block are one float4
+__device__ __forceinline__ int gm_idx(int m, int k, int P) { return m * P + (k & ~15) + 4 * (k & 3) + ((k >> 2) & 3); }
+
+__device__ __forceinline__ float gm_gelu(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+
+// acc[mt] (16x16 output tile nt, token tiles mt < NMT) += X[.., 16 G0 .. 16 (G0 + nG)) * W^T over K
+// blocks G0..G0+nG of the packed weights (NT output tiles); X in LDS ([32][P] image, K block g of the
+// image = packed K block G0 + g - GX)
+template <int NMT>
+__device__ __forceinline__ void gm_gemm(const float *X, int P, int GX, const float4 *Wp, int NT, int nt, int G0, int nG,
+                                        gmx4 (&acc)[2]) {
+    const int lane = threadIdx.x & 63, m = lane & 15, j = lane >> 4;
+    for (int g = 0; g < nG; ++g) {
+        const int G = G0 + g;
+        const float4 b = Wp[(size_t)(G * NT + nt) * 64 + lane];
+#pragma unroll
+        for (int mt = 0; mt < NMT; ++mt) {
+            const float4 av = *reinterpret_cast<const float4 *>(X + (16 * mt + m) * P + 16 * (G - GX) + 4 * j);
+            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, b.x, acc[mt], 0, 0, 0);
+            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, b.y, acc[mt], 0, 0, 0);
+            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, b.z, acc[mt], 0, 0, 0);
+            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, b.w, acc[mt], 0, 0, 0);
+        }
+    }
+}
+
+// sum over the 64 lanes of a wave
+__device__ __forceinline__ float gm_wsum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+template <int NMT>
+__global__ void __launch_bounds__(256) gm_embed_kernel(GmArgs a) {
+    extern __shared__ float gm_lds[];
+    const int r = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int N = a.N, C = a.C, T = a.T, D = a.D;
+    const int C16 = gm_r16(C), K016 = gm_r16(C + T);
+    const int XP = C16 + 4, K0P = K016 + 4, HP = GM_HCH + 4;
+    // LDS: X [32][XP] | U = max(X0 [32][K0P], XN [32][XP] + H [32][HP]) | ew_eff, valid [32]
+    float *X = gm_lds, *U = X + GM_MT * XP;
+    float *X0 = U, *XN = U, *H = U + GM_MT * XP;
+    const int ulen = max(GM_MT * K0P, GM_MT * (XP + HP));
+    float *sew = U + ulen, *sval = sew + GM_MT;
+    const bool has_ew = a.ew != nullptr;
+    if (tid < GM_MT) {
+        const bool v = tid < N && a.nid[(size_t)r * N + tid] != 0;
+        sval[tid] = v ? 1.f : 0.f;
+        // exp_src * mask (:154-155); without explanation weights the mixer multiplies by nothing (1.0)
+        sew[tid] = tid < N ? (has_ew ? a.ew[(size_t)r * N + tid] * (v ? 1.f : 0.f) : 1.f) : 0.f;
+    }
+    __syncthreads();
+    // ---- projection input [E(e) | cos(dt w + b)] (padding neighbours: time part zeroed, edge part too
+    // unless edge_attr is given) (:156-167)
+    const double cut = a.cut[r];
+    for (int i = tid; i < GM_MT * K016; i += blockDim.x) {
+        const int t = i / K016, k = i - t * K016;
+        float v = 0.f;
+        if (t < N) {
+            const bool valid = sval[t] != 0.f;
+            if (k < C) {
+                if (a.edge_attr) v = a.edge_attr[((size_t)r * N + t) * C + k];
+                else if (valid) v = a.e_feat[(size_t)a.eid[(size_t)r * N + t] * C + k];
+            } else if (k < C + T && valid) {
+                // Linear(1, d) on fp32 dt: one rounding of dt * w + b (what the reference's CPU addmm gives)
+                const float dt = (float)(cut - a.ts[(size_t)r * N + t]);
+                const float arg = (float)((double)dt * (double)a.time_w[k - C] + (double)a.time_b[k - C]);
+                v = (float)cos((double)arg);
+            }
+        }
+        X0[gm_idx(t, k, K0P)] = v;
+    }
+    __syncthreads();
+    const int NT = C16 / 16;
+    {   // projection (:167): X = X0 Wp^T + bp
+        for (int nt = wave; nt < NT; nt += 4) {
+            gmx4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+            gm_gemm<NMT>(X0, K0P, 0, a.proj_w, NT, nt, 0, K016 / 16, acc);
+            const int n = 16 * nt + (lane & 15);
+            const float bv = n < C ? a.proj_b[n] : 0.f;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int t = 16 * mt + 4 * (lane >> 4) + i;
+                    X[gm_idx(t, n, XP)] = (mt < NMT && n < C && t < N) ? acc[mt][i] + bv : 0.f;
+                }
+        }
+    }
+    __syncthreads();
+    for (int l = 0; l < a.L; ++l) {
+        const float *const *w = a.lw[l];
+        // ---- token mixing (:289-297), one thread per channel
+        for (int c = tid; c < C; c += blockDim.x) {
+            float x[GM_MT], xn[GM_MT];
+            float s = 0.f;
+#pragma unroll
+            for (int t = 0; t < GM_MT; ++t) {
+                x[t] = t < N ? X[gm_idx(t, c, XP)] * sew[t] : 0.f;
+                s += x[t];
+            }
+            const float mean = s / (float)N;
+            float q = 0.f;
+#pragma unroll
+            for (int t = 0; t < GM_MT; ++t) {
+                const float d = t < N ? x[t] - mean : 0.f;
+                q += d * d;
+            }
+            const float rstd = 1.f / sqrtf(q / (float)N + 1e-5f);
+#pragma unroll
+            for (int t = 0; t < GM_MT; ++t) xn[t] = t < N ? (x[t] - mean) * rstd * w[0][t] + w[1][t] : 0.f;
+            float h[GM_MT / 2];
+#pragma unroll
+            for (int jh = 0; jh < GM_MT / 2; ++jh) {
+                float v = 0.f;
+                if (jh < a.HT) {
+                    v = w[3][jh];
+#pragma unroll
+                    for (int t = 0; t < GM_MT; ++t)
+                        if (t < N) v += w[2][jh * N + t] * xn[t];
+                    v = gm_gelu(v);
+                }
+                h[jh] = v;
+            }
+#pragma unroll
+            for (int t = 0; t < GM_MT; ++t) {
+                if (t >= N) break;
+                float y = w[5][t];
+#pragma unroll
+                for (int jh = 0; jh < GM_MT / 2; ++jh)
+                    if (jh < a.HT) y += w[4][t * a.HT + jh] * h[jh];
+                X[gm_idx(t, c, XP)] = y * sew[t] + x[t];
+            }
+        }
+        __syncthreads();
+        // ---- channel LayerNorm (:300), one wave per token
+        for (int t = wave; t < GM_MT; t += 4) {
+            float s = 0.f, q = 0.f;
+            if (t < N) {
+                for (int c = lane; c < C; c += 64) s += X[gm_idx(t, c, XP)];
+                const float mean = gm_wsum(s) / (float)C;
+                for (int c = lane; c < C; c += 64) {
+                    const float d = X[gm_idx(t, c, XP)] - mean;
+                    q += d * d;
+                }
+                const float rstd = 1.f / sqrtf(gm_wsum(q) / (float)C + 1e-5f);
+                for (int c = lane; c < C16; c += 64)
+                    XN[gm_idx(t, c, XP)] = c < C ? (X[gm_idx(t, c, XP)] - mean) * rstd * w[6][c] + w[7][c] : 0.f;
+            } else {
+                for (int c = lane; c < C16; c += 64) XN[gm_idx(t, c, XP)] = 0.f;
+            }
+        }
+        __syncthreads();
+        // ---- channel FFN (:302-305): hidden chunks of 256 through LDS, output tiles in registers
+        const int NH = gm_r16(a.HC) / 16;
+        const float4 *W1 = reinterpret_cast<const float4 *>(w[8]), *W2 = reinterpret_cast<const float4 *>(w[10]);
+        gmx4 out[4][2];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) out[k][0] = out[k][1] = gmx4{0.f, 0.f, 0.f, 0.f};
+        for (int h0 = 0; h0 < NH; h0 += GM_HCH / 16) {
+            const int nh = min(GM_HCH / 16, NH - h0);
+            for (int ht = wave; ht < nh; ht += 4) {
+                gmx4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+                gm_gemm<NMT>(XN, XP, 0, W1, NH, h0 + ht, 0, C16 / 16, acc);
+                const int n = 16 * (h0 + ht) + (lane & 15);
+                const float bv = n < a.HC ? w[9][n] : 0.f;
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int t = 16 * mt + 4 * (lane >> 4) + i;
+                        H[gm_idx(t, 16 * ht + (lane & 15), HP)] = (mt < NMT && n < a.HC) ? gm_gelu(acc[mt][i] + bv) : 0.f;
+                    }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int nt = wave + 4 * k;
+                if (nt < NT) gm_gemm<NMT>(H, HP, h0, W2, NT, nt, h0, nh, out[k]);
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int nt = wave + 4 * k;
+            if (nt >= NT) continue;
+            const int n = 16 * nt + (lane & 15);
+            const float bv = n < C ? w[11][n] : 0.f;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int t = 16 * mt + 4 * (lane >> 4) + i;
+                    if (mt < NMT && t < N && n < C) {
+                        const int ix = gm_idx(t, n, XP);
+                        X[ix] = (out[k][mt][i] + bv) * sew[t] + X[ix];
+                    }
+                }
+        }
+        __syncthreads();
+    }
+    // ---- masked mean over the tokens (:176-178) and the neighbour-feature mean (:181-189)
+    for (int c = tid; c < C; c += blockDim.x) {
+        float s = 0.f;
+        for (int t = 0; t < N; ++t) s += X[gm_idx(t, c, XP)] * sval[t] * (has_ew ? sew[t] : 1.f);
+        a.x_mean[(size_t)r * C + c] = s / (float)N;
+    }
+    float nvalid = 0.f;
+    for (int t = 0; t < N; ++t) nvalid += sval[t];
+    for (int d = tid; d < D; d += blockDim.x) {
+        float s = 0.f;
+        for (int t = 0; t < N; ++t) {
+            // softmax(valid ? 1 : -1e10) over the row: 1 / n_valid on valid neighbours (exp(-1e10 - 1) == 0),
+            // 1 / N everywhere when none is valid
+            float sc = nvalid > 0.f ? sval[t] / nvalid : 1.f / (float)N;
+            if (has_ew) sc *= sew[t];
+            s += a.n_feat[(size_t)a.nid[(size_t)r * N + t] * D + d] * sc;
+        }
+        a.node_out[(size_t)r * D + d] = s / (float)N + a.n_feat[(size_t)a.node[r] * D + d];
+    }
+}
+
+// W [n_out][k] row-major -> B-operand fragments: packed[(G * NT + nt) * 64 + lane][s] =
+// W[16 nt + (lane & 15)][16 G + 4 s + (lane >> 4)] (zero outside W)
+__global__ void gm_pack_kernel(const float *__restrict__ w, int32_t n_out, int32_t k, float *__restrict__ out) {
+    const int32_t NT = gm_r16(n_out) / 16, KG = gm_r16(k) / 16;
+    const int64_t total = (int64_t)KG * NT * 64 * 4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int s = (int)(i & 3), lane = (int)((i >> 2) & 63);
+        const int64_t f = i >> 8;
+        const int nt = (int)(f % NT), G = (int)(f / NT);
+        const int n = 16 * nt + (lane & 15), kk = 16 * G + 4 * s + (lane >> 4);
+        out[i] = (n < n_out && kk < k) ? w[(int64_t)n * k + kk] : 0.f;
+    }
+}
+
+}  // namespace tmk
+
+using namespace tmk;
+
+static inline size_t gm_lds_bytes(int32_t C, int32_t T) {
+    const size_t XP = gm_r16(C) + 4, K0P = gm_r16(C + T) + 4, HP = GM_HCH + 4;
+    const size_t ulen = std::max(GM_MT * K0P, GM_MT * (XP + HP));
+    return sizeof(float) * (GM_MT * XP + ulen + 2 * GM_MT);
+}
+
+extern "C" int64_t tm_gm_packed_floats(int32_t n_out, int32_t k) {
+    if (n_out <= 0 || k <= 0) return 0;
+    return (int64_t)(gm_r16(n_out) / 16) * (gm_r16(k) / 16) * 256;
+}
+
+extern "C" int tm_gm_pack(const float *w, int32_t n_out, int32_t k, float *packed, void *stream) {
+    if (!w || !packed || n_out <= 0 || k <= 0) return fail(TM_E_ARG, "tm_gm_pack: bad arguments");
+    const int64_t total = tm_gm_packed_floats(n_out, k);
+    const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, 4096);
+    gm_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(w, n_out, k, packed);
+    TM_CHECK_LAUNCH();
+    return TM_OK;
+}
+
+extern "C" int tm_gm_embed(const tm_gm_embed_args *p, void *stream) {
+    if (!p) return fail(TM_E_ARG, "tm_gm_embed: NULL arguments");
+    const tm_gm_embed_args &q = *p;
+    if (q.R < 0 || q.N <= 0 || q.C <= 0 || q.T < 0 || q.D <= 0 || q.L < 0 || q.HT < 0 || q.HC <= 0)
+        return fail(TM_E_ARG, "tm_gm_embed: bad dimensions");
+    if (q.N > GM_MT || q.HT > GM_MT / 2 || q.L > GM_MAXL || q.C > 256)
+        return fail(TM_E_UNSUPPORTED, "tm_gm_embed: needs num_tokens <= 32, token hidden <= 16, <= 4 layers, "
+                                      "channels <= 256");
+    if (q.R == 0) return TM_OK;
+    if (!q.node || !q.nid || !q.cut || !q.ts || !q.n_feat || (!q.e_feat && !q.edge_attr) || (q.T && (!q.time_w || !q.time_b)) ||
+        !q.proj_w || !q.proj_b || !q.x_mean || !q.node_out || (!q.eid && !q.edge_attr))
+        return fail(TM_E_ARG, "tm_gm_embed: NULL pointer");
+    GmArgs a{};
+    a.R = q.R; a.N = q.N; a.C = q.C; a.T = q.T; a.D = q.D; a.L = q.L; a.HT = q.HT; a.HC = q.HC;
+    a.node = q.node; a.nid = q.nid; a.eid = q.eid; a.cut = q.cut; a.ts = q.ts; a.ew = q.ew; a.edge_attr = q.edge_attr;
+    a.n_feat = q.n_feat; a.e_feat = q.e_feat; a.time_w = q.time_w; a.time_b = q.time_b;
+    a.proj_w = reinterpret_cast<const float4 *>(q.proj_w);
+    a.proj_b = q.proj_b;
+    for (int l = 0; l < q.L; ++l)
+        for (int k = 0; k < 12; ++k) {
+            if (!q.layer[l][k]) return fail(TM_E_ARG, "tm_gm_embed: NULL layer weight");
+            a.lw[l][k] = q.layer[l][k];
+        }
+    a.x_mean = q.x_mean;
+    a.node_out = q.node_out;
+    const size_t lds = gm_lds_bytes(q.C, q.T);
+    if (lds > 160 * 1024) return fail(TM_E_UNSUPPORTED, "tm_gm_embed: edge + time dims too large for LDS");
+    hipEvent_t pe = prof_begin((hipStream_t)stream);
+    if (q.N > 16) {
+        TM_HIP(hipFuncSetAttribute((const void *)gm_embed_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        gm_embed_kernel<2><<<q.R, 256, lds, (hipStream_t)stream>>>(a);
+    } else {
+        TM_HIP(hipFuncSetAttribute((const void *)gm_embed_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        gm_embed_kernel<1><<<q.R, 256, lds, (hipStream_t)stream>>>(a);
+    }
+    TM_CHECK_LAUNCH();
+    prof_end("gm_embed_kernel", (hipStream_t)stream, pe);
+    return TM_OK;
+}

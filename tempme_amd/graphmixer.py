@@ -16,6 +16,8 @@ restated over all three sides at once (3B rows) on the device:
 The time-encoder argument is formed as the reference's CPU addmm forms it (one rounding of
 t*w+b: computed in fp64, rounded to fp32), since cos of a large argument depends on that rounding.
 """
+import ctypes
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -135,10 +137,97 @@ class GraphMixer(nn.Module):
             self._tab_key = key
         return self._ntab, self._etab
 
+    # ------------------------------------------------------------------ HIP path (tm_gm_embed)
+    def _hip_ok(self, explain_weight, N):
+        """Eval forward without gradients (threshold_test, scoring): the fused HIP embedding.  With
+        gradients (explainer training through the base model) or dropout active, the torch formulation
+        below runs under autograd."""
+        import os
+        if os.environ.get("TEMPME_GM_TORCH") == "1" or self.training:
+            return False
+        if torch.is_grad_enabled() and ((explain_weight is not None and explain_weight.requires_grad)
+                                        or any(p.requires_grad for p in self.parameters())):
+            return False
+        ht = int(self.mlp_mixers[0].token_feedforward.dim_expansion_factor * N) if self.num_layers else 0
+        return (N <= 32 and ht <= 16 and self.num_layers <= 4 and self.num_channels <= 256 and N == self.num_tokens)
+
+    def _gm_packed(self, dev):
+        """Packed MFMA fragments of projection_layer and every channel FFN (tm_gm_pack), rebuilt when a
+        parameter changes (version counters)."""
+        ps = list(self.parameters())
+        key = (dev, tuple((p.data_ptr(), p._version) for p in ps))
+        if getattr(self, "_gm_key", None) != key:
+            st = L.stream_ptr(dev)
+            keep = []
+
+            def pack(w):
+                w = w.detach().to(dev, torch.float32).contiguous()
+                n_out, k = w.shape
+                out = torch.empty(int(L.lib().tm_gm_packed_floats(n_out, k)), dtype=torch.float32, device=dev)
+                L.check(L.lib().tm_gm_pack(L.ptr(w), n_out, k, L.ptr(out), st), "tm_gm_pack")
+                keep.append(w)
+                return out
+
+            def flat(t):
+                t = t.detach().to(dev, torch.float32).contiguous()
+                keep.append(t)
+                return t
+
+            layers = []
+            for m in self.mlp_mixers:
+                tf, cf = m.token_feedforward.ffn, m.channel_feedforward.ffn
+                layers.append([flat(m.token_norm.weight), flat(m.token_norm.bias), flat(tf[0].weight), flat(tf[0].bias),
+                               flat(tf[3].weight), flat(tf[3].bias), flat(m.channel_norm.weight),
+                               flat(m.channel_norm.bias), pack(cf[0].weight), flat(cf[0].bias), pack(cf[3].weight),
+                               flat(cf[3].bias)])
+            self._gm_pack = dict(proj_w=pack(self.projection_layer.weight), proj_b=flat(self.projection_layer.bias),
+                                 tw=flat(self.time_encoder.w.weight.reshape(-1)), tb=flat(self.time_encoder.w.bias),
+                                 layers=layers, keep=keep)
+            self._gm_key = key
+        return self._gm_pack
+
+    def _embed_hip(self, dev, node_ids, cut, nid, eid, t, explain_weight, edge_attr):
+        ntab, etab = self._tables(dev)
+        R, N = nid.shape
+        pk = self._gm_packed(dev)
+        i32 = lambda x: x.to(dev, torch.int32).contiguous()  # noqa: E731
+        node, nid32 = i32(node_ids), i32(nid)
+        eid32 = i32(eid)
+        cut64 = cut.to(dev, torch.float64).reshape(-1).contiguous()
+        t64 = t.to(dev, torch.float64).contiguous()
+        ew = None if explain_weight is None else explain_weight.detach().to(dev, torch.float32).contiguous()
+        ea = None if edge_attr is None else edge_attr.detach().to(dev, torch.float32).contiguous()
+        C, D = self.num_channels, self.node_feat_dim
+        x_mean = torch.empty(max(R, 1), C, dtype=torch.float32, device=dev)
+        node_out = torch.empty(max(R, 1), D, dtype=torch.float32, device=dev)
+        a = L.GmEmbedArgs()
+        a.R, a.N, a.C, a.T, a.D, a.L = R, N, C, self.time_feat_dim, D, self.num_layers
+        a.HT = int(self.mlp_mixers[0].token_feedforward.dim_expansion_factor * N) if self.num_layers else 0
+        a.HC = int(self.channel_dim_expansion_factor * C)
+        a.node, a.nid, a.eid, a.cut, a.ts = L.ptr(node), L.ptr(nid32), L.ptr(eid32), L.ptr(cut64), L.ptr(t64)
+        a.ew = None if ew is None else L.ptr(ew)
+        a.edge_attr = None if ea is None else L.ptr(ea)
+        a.n_feat, a.e_feat = L.ptr(ntab), L.ptr(etab)
+        a.time_w, a.time_b = L.ptr(pk["tw"]), L.ptr(pk["tb"])
+        a.proj_w, a.proj_b = L.ptr(pk["proj_w"]), L.ptr(pk["proj_b"])
+        for li, lw in enumerate(pk["layers"]):
+            for k, tsr in enumerate(lw):
+                a.layer[li][k] = L.ptr(tsr)
+        a.x_mean, a.node_out = L.ptr(x_mean), L.ptr(node_out)
+        L.check(L.lib().tm_gm_embed(ctypes.byref(a), L.stream_ptr(dev)), "GraphMixer.compute_node_temporal_embeddings")
+        return F.linear(torch.cat([x_mean[:R], node_out[:R]], dim=1), self.output_layer.weight.to(dev),
+                        self.output_layer.bias.to(dev))
+
     def node_embeddings(self, node_ids, cut_time, nid, eid, times, explain_weight=None, edge_attr=None):
         """compute_node_temporal_embeddings (graphmixer.py:142-193) for R rows at once:
         node_ids [R], cut_time [R] (f64), nid/eid/times [R, N] (hop-1 records), explain_weight [R, N]."""
         dev = self._dev()
+        N0 = np.shape(nid)[-1]
+        if self._hip_ok(explain_weight, N0):
+            return self._embed_hip(dev, _as_dev(node_ids, dev, torch.long).reshape(-1),
+                                   _as_dev(cut_time, dev, torch.float64).reshape(-1), _as_dev(nid, dev, torch.long),
+                                   _as_dev(eid, dev, torch.long), _as_dev(times, dev, torch.float64), explain_weight,
+                                   None if edge_attr is None else _as_dev(edge_attr, dev, torch.float32))
         ntab, etab = self._tables(dev)
         node_ids = _as_dev(node_ids, dev, torch.long).reshape(-1)
         nid = _as_dev(nid, dev, torch.long)

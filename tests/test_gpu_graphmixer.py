@@ -97,3 +97,57 @@ def test_config5_dims_and_gradient_vs_oracle(dev):
                                atol=ATOL, rtol=RTOL)
     ga, gb = ew.grad.double().cpu(), ew64.grad
     assert torch.linalg.norm(ga - gb) <= 1e-4 * torch.linalg.norm(gb)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_hip_embedding_matches_reference(dev, case):
+    """The fused HIP embedding (tm_gm_embed: eval, no gradients) against the reference's outputs, for
+    every explanation-weight / edge_attr variant of the golden batch."""
+    g, d = golden(), TI.load_batch()
+    m = build(case).to(dev).eval()
+    expl = [TI.explanation(case)[0].to(dev)]
+    with torch.no_grad():
+        for tag, ew, ea in (("ori", None, None), ("expl", expl, None),
+                            ("rand", [torch.from_numpy(g[f"{case}_ew_rand"]).to(dev)], None),
+                            ("attr", expl, torch.from_numpy(g[f"{case}_edge_attr"]).to(dev))):
+            p, n = m.contrast(d["src"], d["dst"], d["fake"], d["ts_cut"], d["e_idx"], d["sg_src"], d["sg_tgt"],
+                              d["sg_bgd"], explain_weights=ew, edge_attr=ea)
+            np.testing.assert_allclose(torch.cat([p, n]).cpu().numpy(), g[f"{case}_{tag}"], atol=ATOL, rtol=RTOL,
+                                       err_msg=tag)
+    assert getattr(m, "_gm_key", None) is not None, "the HIP embedding did not run"
+
+
+@pytest.mark.parametrize("N", [30, 12])
+def test_hip_embedding_config5_dims_vs_oracle(dev, N):
+    """de = dn = 172 (BASELINE configs[4] shapes), N = 30 (two token tiles) and 12 (one): HIP logits vs the
+    fp64 oracle, with and without explanation weights, padding neighbours included."""
+    from tempme_amd.graphmixer import GraphMixer
+    rng = np.random.default_rng(7 + N)
+    V, E, B, d = 400, 3000, 40, 172
+    nf = rng.uniform(0, 1, (V, d)).astype(np.float32)
+    ef = rng.uniform(0, 1, (E + 1, d)).astype(np.float32)
+    nf[0] = ef[0] = 0
+    torch.manual_seed(11)
+    m = GraphMixer(nf, ef, n_neighbors=N, device=dev, num_tokens=N, num_layers=2, dropout=0.1).to(dev).eval()
+    cut = np.floor(rng.uniform(5e7, 1e8, B))
+    sgs = []
+    for _ in range(3):
+        node = rng.integers(1, V, (B, N))
+        node[rng.uniform(size=node.shape) < 0.25] = 0
+        node[0] = 0                                   # a row without any valid neighbour
+        eid = np.where(node > 0, rng.integers(1, E + 1, node.shape), 0)
+        ts = np.where(node > 0, np.floor(cut[:, None] - rng.uniform(0, 5e7, node.shape)), 0.0)
+        sgs.append(([node.astype(np.float64), None], [eid.astype(np.float64), None], [ts, None]))
+    src, dst, fake = (rng.integers(1, V, B) for _ in range(3))
+    ew0 = rng.uniform(0, 1, (3 * B, N)).astype(np.float32)
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    for ew in (None, ew0):
+        with torch.no_grad():
+            p, n = m.contrast(src, dst, fake, cut, None, *sgs,
+                              explain_weights=None if ew is None else [torch.from_numpy(ew).to(dev)])
+        p64, n64 = O.contrast(sd, 2, src, dst, fake, cut, *sgs,
+                              explain_weights=None if ew is None else [torch.from_numpy(ew).double()],
+                              dtype=torch.float64)
+        np.testing.assert_allclose(torch.cat([p, n]).cpu().double().numpy(), torch.cat([p64, n64]).numpy(),
+                                   atol=ATOL, rtol=RTOL)
+    assert getattr(m, "_gm_key", None) is not None, "the HIP embedding did not run"

@@ -1,5 +1,4 @@
 #!/bin/bash
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
-step() { local n=$1 t=$2; shift 2; timeout -k 10 $t "$@" > gpurun_out/$n.log 2>&1; local rc=$?; echo "$n rc=$rc"; if [ $rc -ne 0 ]; then tail -20 gpurun_out/$n.log; exit $rc; fi; }
-step pytest_gpu 600 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread
-TEMPME_GRAPH_TIMING=1 step graph_build 300 python tools/graph_build.py
+timeout -k 10 600 python -u -m pytest tests/test_gpu_graphmixer.py -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gm.log 2>&1; rc=$?
+echo "pytest rc=$rc"; grep -E "PASS|FAIL|Error|error|Mismatch|Max abs" gpurun_out/pytest_gm.log | head -30
