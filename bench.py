@@ -303,6 +303,22 @@ def timed(run_step, pipes, inputs, warmup, steps, dist, backend, dev, L):
     return max_over_ranks(el, dist, dev if backend == "nccl" else "cpu"), prof
 
 
+@torch.no_grad()
+def gm_contrast(gm, buf, x, h1):
+    """GraphMixer.contrast (GM/graphmixer.py:206-218) of every event of the step with its hop-1
+    explanation: the three sides' roots at once (rows are independent, so one call equals the reference's
+    per-batch calls), then the MergeLayer scores of (src, dst) and (src, fake)."""
+    src, dst, ts, eidx, _ = x
+    E = src.numel()
+    N = buf.N
+    roots = torch.cat([src, dst, buf.dst_fake[:E]])
+    cut = ts.repeat(3)
+    emb = gm.node_embeddings(roots, cut, buf.sub1_node[:, :E].reshape(3 * E, N), buf.sub1_eid[:, :E].reshape(3 * E, N),
+                             buf.sub1_ts[:, :E].reshape(3 * E, N).double(), h1.reshape(3 * E, N))
+    s, d, n = emb[:E], emb[E:2 * E], emb[2 * E:]
+    return gm.affinity(torch.cat([s, s]), torch.cat([d, n]))
+
+
 def make_inputs(n_steps, rank, world, per_rank, events, dev):
     from tempme_amd.sharding import shard_events
     src, dst, ts, eidx = events
@@ -356,6 +372,9 @@ def main():
     ap.add_argument("--no-edge-table", action="store_true",
                     help="lin_event's edge-feature product per walk position instead of per edge id")
     ap.add_argument("--streams", type=int, default=1, help="steps in flight (PipelinedExplainer)")
+    ap.add_argument("--contrast", choices=("auto", "graphmixer", "none"), default="auto",
+                    help="base-model contrast with the explanation (auto: GraphMixer for --config 4, as configs[4] "
+                         "names it; none elsewhere: SURVEY §8(d) excludes the base contrast from the scoring unit)")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks, form the process group and report it (no GPU work)")
     args = ap.parse_args()
@@ -426,13 +445,24 @@ def main():
     ex = tm.TempME(Base(), "tgn", cfg["name"], out_dim=40, hid_dim=64, device=dev,
                    null_model={k: 1.0 / 12 for k in range(1, 13)}).to(dev).eval()
     S = max(1, args.streams)
+    contrast = args.contrast if args.contrast != "auto" else ("graphmixer" if args.config == 4 else "none")
+    gm = None
+    if contrast == "graphmixer":
+        # configs[4]'s base model, random-init (no checkpoint travels), scoring the explanation
+        from tempme_amd.graphmixer import GraphMixer
+        torch.manual_seed(args.seed + 1)
+        gm = GraphMixer(g["n_feat"], g["e_feat"], n_neighbors=N, device=dev, num_tokens=N, num_layers=2,
+                        dropout=0.1).to(dev).eval()
+        workload += " + GraphMixer contrast with the hop-1 explanation (fused HIP embedding)"
     if S == 1:
         pipe = ExplainPipeline(ex, finder.graph, torch.from_numpy(pool), N, M, B, seed=args.seed,
                                edge_table=not args.no_edge_table)
         pipes = [pipe]
 
         def run_step(x):
-            pipe.run(*x)
+            _, h1, _ = pipe.run(*x)
+            if gm is not None:
+                gm_contrast(gm, pipe.buf, x, h1)
     else:
         flight = PipelinedExplainer(ex, finder.graph, torch.from_numpy(pool), N, M, B, seed=args.seed, depth=S,
                                     edge_table=not args.no_edge_table)
@@ -496,7 +526,7 @@ def main():
                           "metric (full Enron + TGN, n_degree=20)", "n_degree": N, "walks_per_slot": M,
                           "batch_size": B, "global_batches_per_step": per_rank * world // B,
                           "events_per_step_per_gpu": per_rank, "parallelism": f"dp{world} (whole batches per rank)",
-                          "steps_in_flight": S},
+                          "steps_in_flight": S, "base_contrast": contrast},
                "roofline": roof, "kernels": kernels, "sampling_roofline": samp or None}
         if weak is not None:
             out["weak" if strong else "strong"] = weak

@@ -402,9 +402,9 @@ typedef struct {
     const float *time_w, *time_b; /* [T] TimeEncoder Linear(1, T) weight and bias */
     const float *proj_w;      /* projection_layer.weight [C, C+T] packed by tm_gm_pack */
     const float *proj_b;      /* [C] */
-    /* per mixer: token_norm w/b [N], token ffn.0 w [HT,N] / b, ffn.3 w [N,HT] / b, channel_norm w/b [C],
-       channel ffn.0 w [HC,C] packed / b [HC], ffn.3 w [C,HC] packed / b [C] */
-    const float *layer[4][12];
+    /* DEVICE array of L x 12 pointers, per mixer: token_norm w/b [N], token ffn.0 w [HT,N] / b, ffn.3 w
+       [N,HT] / b, channel_norm w/b [C], channel ffn.0 w [HC,C] packed / b [HC], ffn.3 w [C,HC] packed / b */
+    const float *const *layer_table;
     float *x_mean, *node_out; /* outputs */
 } tm_gm_embed_args;
 /* floats of tm_gm_pack's output for a [n_out, k] weight */

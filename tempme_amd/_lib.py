@@ -63,7 +63,7 @@ class GmEmbedArgs(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("R", "N", "C", "T", "D", "L", "HT", "HC")] + \
                [(n, C.c_void_p) for n in ("node", "nid", "eid", "cut", "ts", "ew", "edge_attr", "n_feat", "e_feat",
                                           "time_w", "time_b", "proj_w", "proj_b")] + \
-               [("layer", (C.c_void_p * 12) * 4), ("x_mean", C.c_void_p), ("node_out", C.c_void_p)]
+               [("layer_table", C.c_void_p), ("x_mean", C.c_void_p), ("node_out", C.c_void_p)]
 
 
 GRAD_IO_FIELDS = ("imp", "dlogit", "M2", "dM2", "M1d", "dM1", "X", "dY2", "H1d", "dH1", "O", "dP", "dQ", "dF",

@@ -41,7 +41,7 @@ struct GmArgs {
     const float *ew, *edge_attr, *n_feat, *e_feat, *time_w, *time_b;
     const float4 *proj_w;
     const float *proj_b;
-    const float *lw[GM_MAXL][12];
+    const float *const *lw;   // [L][12] device table (kept out of the scalar register file)
     float *x_mean, *node_out;
 };
 
@@ -59,17 +59,29 @@ __device__ __forceinline__ float gm_gelu(float x) { return 0.5f * x * (1.f + erf
 template <int NMT>
 __device__ __forceinline__ void gm_gemm(const float *X, int P, int GX, const float4 *Wp, int NT, int nt, int G0, int nG,
                                         gmx4 (&acc)[2]) {
+    constexpr int PF = 4;   // weight fragments in flight (L2 latency behind the MFMAs of the blocks before)
     const int lane = threadIdx.x & 63, m = lane & 15, j = lane >> 4;
-    for (int g = 0; g < nG; ++g) {
-        const int G = G0 + g;
-        const float4 b = Wp[(size_t)(G * NT + nt) * 64 + lane];
+    const float4 *wp = Wp + (size_t)nt * 64 + lane;
+    const size_t gs = (size_t)NT * 64;
+    float4 bq[PF];
 #pragma unroll
-        for (int mt = 0; mt < NMT; ++mt) {
-            const float4 av = *reinterpret_cast<const float4 *>(X + (16 * mt + m) * P + 16 * (G - GX) + 4 * j);
-            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, b.x, acc[mt], 0, 0, 0);
-            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, b.y, acc[mt], 0, 0, 0);
-            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, b.z, acc[mt], 0, 0, 0);
-            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, b.w, acc[mt], 0, 0, 0);
+    for (int u = 0; u < PF; ++u) bq[u] = u < nG ? wp[(size_t)(G0 + u) * gs] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float *xr = X + m * P + 4 * j + 16 * (G0 - GX);
+    for (int g0 = 0; g0 < nG; g0 += PF) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            const int g = g0 + u;
+            if (g >= nG) break;
+            const float4 b = bq[u];
+            if (g + PF < nG) bq[u] = wp[(size_t)(G0 + g + PF) * gs];
+#pragma unroll
+            for (int mt = 0; mt < NMT; ++mt) {
+                const float4 av = *reinterpret_cast<const float4 *>(xr + 16 * mt * P + 16 * g);
+                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, b.x, acc[mt], 0, 0, 0);
+                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, b.y, acc[mt], 0, 0, 0);
+                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, b.z, acc[mt], 0, 0, 0);
+                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, b.w, acc[mt], 0, 0, 0);
+            }
         }
     }
 }
@@ -116,7 +128,7 @@ __global__ void __launch_bounds__(256) gm_embed_kernel(GmArgs a) {
                 // Linear(1, d) on fp32 dt: one rounding of dt * w + b (what the reference's CPU addmm gives)
                 const float dt = (float)(cut - a.ts[(size_t)r * N + t]);
                 const float arg = (float)((double)dt * (double)a.time_w[k - C] + (double)a.time_b[k - C]);
-                v = (float)cos((double)arg);
+                v = cos_rd(arg);   // branch-free fp64-reduced cos (common.h), |err| <= 1.7e-7
             }
         }
         X0[gm_idx(t, k, K0P)] = v;
@@ -140,47 +152,74 @@ __global__ void __launch_bounds__(256) gm_embed_kernel(GmArgs a) {
     }
     __syncthreads();
     for (int l = 0; l < a.L; ++l) {
-        const float *const *w = a.lw[l];
-        // ---- token mixing (:289-297), one thread per channel
+        const float *const *w = a.lw + 12 * l;
+        // ---- token mixing (:289-297).  Per channel c: H = gelu(W1 LN_t(X[:, c] * ew) + b1), Y = W2 H + b2,
+        // X[:, c] = (Y + ... ) * ew + X[:, c] * ew -- two tiny GEMMs per 16-channel tile on MFMA: W1 (HT x N) as
+        // the A operand against the normalised column (B, K = tokens), then W2 (N x HT) against H, whose
+        // K order is permuted (step s, lane group g <-> hidden unit 4g + s) so H stays in the registers the
+        // first MFMA left it in.  Column statistics first, one thread per channel.
+        float *cm = XN, *cr = XN + C16;
         for (int c = tid; c < C; c += blockDim.x) {
-            float x[GM_MT], xn[GM_MT];
-            float s = 0.f;
-#pragma unroll
-            for (int t = 0; t < GM_MT; ++t) {
-                x[t] = t < N ? X[gm_idx(t, c, XP)] * sew[t] : 0.f;
-                s += x[t];
-            }
-            const float mean = s / (float)N;
+            float sm = 0.f;
+            for (int t = 0; t < N; ++t) sm += X[gm_idx(t, c, XP)] * sew[t];
+            const float mean = sm / (float)N;
             float q = 0.f;
-#pragma unroll
-            for (int t = 0; t < GM_MT; ++t) {
-                const float d = t < N ? x[t] - mean : 0.f;
+            for (int t = 0; t < N; ++t) {
+                const float d = X[gm_idx(t, c, XP)] * sew[t] - mean;
                 q += d * d;
             }
-            const float rstd = 1.f / sqrtf(q / (float)N + 1e-5f);
+            cm[c] = mean;
+            cr[c] = 1.f / sqrtf(q / (float)N + 1e-5f);
+        }
+        __syncthreads();
+        {
+            const int g = lane >> 4, li = lane & 15, HT = a.HT;
+            float a1[2][4], a2[2][4], lg[2][4], lb[2][4], b2v[2][4], b1v[4];
 #pragma unroll
-            for (int t = 0; t < GM_MT; ++t) xn[t] = t < N ? (x[t] - mean) * rstd * w[0][t] + w[1][t] : 0.f;
-            float h[GM_MT / 2];
+            for (int G = 0; G < 2; ++G)
 #pragma unroll
-            for (int jh = 0; jh < GM_MT / 2; ++jh) {
-                float v = 0.f;
-                if (jh < a.HT) {
-                    v = w[3][jh];
-#pragma unroll
-                    for (int t = 0; t < GM_MT; ++t)
-                        if (t < N) v += w[2][jh * N + t] * xn[t];
-                    v = gm_gelu(v);
+                for (int s2 = 0; s2 < 4; ++s2) {
+                    const int t = 16 * G + 4 * s2 + g;          // step-2 K index of this lane
+                    a1[G][s2] = (li < HT && t < N) ? w[2][li * N + t] : 0.f;
+                    lg[G][s2] = t < N ? w[0][t] : 0.f;
+                    lb[G][s2] = t < N ? w[1][t] : 0.f;
+                    const int tt = 16 * G + li, j = 4 * g + s2;   // step-3 A: W2[t][j], K permuted
+                    a2[G][s2] = (tt < N && j < HT) ? w[4][tt * HT + j] : 0.f;
+                    const int tr = 16 * G + 4 * g + s2;         // step-3 D row of this lane's element s2
+                    b2v[G][s2] = tr < N ? w[5][tr] : 0.f;
                 }
-                h[jh] = v;
-            }
 #pragma unroll
-            for (int t = 0; t < GM_MT; ++t) {
-                if (t >= N) break;
-                float y = w[5][t];
+            for (int i = 0; i < 4; ++i) b1v[i] = 4 * g + i < HT ? w[3][4 * g + i] : 0.f;
+            for (int nt = wave; nt < NT; nt += 4) {
+                const int c = 16 * nt + li;
+                const bool cv = c < C;
+                const float mean = cv ? cm[c] : 0.f, rstd = cv ? cr[c] : 0.f;
+                gmx4 hacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int jh = 0; jh < GM_MT / 2; ++jh)
-                    if (jh < a.HT) y += w[4][t * a.HT + jh] * h[jh];
-                X[gm_idx(t, c, XP)] = y * sew[t] + x[t];
+                for (int G = 0; G < 2; ++G)
+#pragma unroll
+                    for (int s2 = 0; s2 < 4; ++s2) {
+                        const int t = 16 * G + 4 * s2 + g;
+                        const float xn = (cv && t < N) ? (X[gm_idx(t, c, XP)] * sew[t] - mean) * rstd * lg[G][s2] + lb[G][s2] : 0.f;
+                        hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[G][s2], xn, hacc, 0, 0, 0);
+                    }
+                float h[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) h[i] = 4 * g + i < HT ? gm_gelu(hacc[i] + b1v[i]) : 0.f;
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    gmx4 y = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int s2 = 0; s2 < 4; ++s2) y = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[mt][s2], h[s2], y, 0, 0, 0);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int t = 16 * mt + 4 * g + i;
+                        if (cv && t < N) {
+                            const int ix = gm_idx(t, c, XP);
+                            X[ix] = (y[i] + b2v[mt][i]) * sew[t] + X[ix] * sew[t];
+                        }
+                    }
+                }
             }
         }
         __syncthreads();
@@ -327,11 +366,8 @@ extern "C" int tm_gm_embed(const tm_gm_embed_args *p, void *stream) {
     a.n_feat = q.n_feat; a.e_feat = q.e_feat; a.time_w = q.time_w; a.time_b = q.time_b;
     a.proj_w = reinterpret_cast<const float4 *>(q.proj_w);
     a.proj_b = q.proj_b;
-    for (int l = 0; l < q.L; ++l)
-        for (int k = 0; k < 12; ++k) {
-            if (!q.layer[l][k]) return fail(TM_E_ARG, "tm_gm_embed: NULL layer weight");
-            a.lw[l][k] = q.layer[l][k];
-        }
+    if (q.L > 0 && !q.layer_table) return fail(TM_E_ARG, "tm_gm_embed: NULL layer table");
+    a.lw = q.layer_table;
     a.x_mean = q.x_mean;
     a.node_out = q.node_out;
     const size_t lds = gm_lds_bytes(q.C, q.T);

@@ -180,9 +180,10 @@ class GraphMixer(nn.Module):
                                flat(tf[3].weight), flat(tf[3].bias), flat(m.channel_norm.weight),
                                flat(m.channel_norm.bias), pack(cf[0].weight), flat(cf[0].bias), pack(cf[3].weight),
                                flat(cf[3].bias)])
+            table = torch.tensor([[t.data_ptr() for t in lw] for lw in layers] or [[0] * 12], dtype=torch.int64)
             self._gm_pack = dict(proj_w=pack(self.projection_layer.weight), proj_b=flat(self.projection_layer.bias),
                                  tw=flat(self.time_encoder.w.weight.reshape(-1)), tb=flat(self.time_encoder.w.bias),
-                                 layers=layers, keep=keep)
+                                 layers=layers, table=table.to(dev), keep=keep)
             self._gm_key = key
         return self._gm_pack
 
@@ -210,9 +211,7 @@ class GraphMixer(nn.Module):
         a.n_feat, a.e_feat = L.ptr(ntab), L.ptr(etab)
         a.time_w, a.time_b = L.ptr(pk["tw"]), L.ptr(pk["tb"])
         a.proj_w, a.proj_b = L.ptr(pk["proj_w"]), L.ptr(pk["proj_b"])
-        for li, lw in enumerate(pk["layers"]):
-            for k, tsr in enumerate(lw):
-                a.layer[li][k] = L.ptr(tsr)
+        a.layer_table = L.ptr(pk["table"])
         a.x_mean, a.node_out = L.ptr(x_mean), L.ptr(node_out)
         L.check(L.lib().tm_gm_embed(ctypes.byref(a), L.stream_ptr(dev)), "GraphMixer.compute_node_temporal_embeddings")
         return F.linear(torch.cat([x_mean[:R], node_out[:R]], dim=1), self.output_layer.weight.to(dev),
