@@ -499,6 +499,11 @@ def main():
                  "gate_table_kernel": ("mfma", fm["gate_per_edge"] * (int(g["eidx"].max()) + 1)),
                  "walk_kernel": ("mfma", fm["walk_kernel"] * 3 * E * W)}
         executed = {"walk_kernel": fm["walk_kernel_executed"] * 3 * E * W}
+        if gm is not None:
+            # per row: projection N (C+T) C + per mixer channel FFN 2 N C HC + token FFN 2 N HT C MACs
+            C_, T_, HT_, HC_ = gm.num_channels, gm.time_feat_dim, int(0.5 * N), int(4 * gm.num_channels)
+            per_row = 2 * (N * (C_ + T_) * C_ + gm.num_layers * (2 * N * C_ * HC_ + 2 * N * HT_ * C_))
+            units["gm_embed_kernel"] = ("mfma", per_row * 3 * E)
         kernels = kernel_table(prof, units, executed)
         traffic, tsrc = load_traffic(cfg["name"])
         dom = max((k for k in kernels if "bound" in kernels[k]), key=lambda k: kernels[k]["avg_ms"])
