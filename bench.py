@@ -13,15 +13,16 @@ architecture.  --config 1 = configs[1] (enron_sampled shape, E=18,780), --config
 (synthetic 1M-edge graph, de=dn=172, N=30, the HBM stress case).
 
 A step = one pass of the hot path over one global batch of synthetic target events already resident
-in HBM: --batches reference batches of --batch-size events (default 64 x 100 = 6,400), all on-device
+in HBM: --batches reference batches of --batch-size events (default 192 x 100 = 19,200 = one eval epoch
+over the full-Enron test split), all on-device
 (tm_sample_events -> tm_edge_tables -> tm_encoder_fwd_tab -> tm_edge_importance_tab).
 
 Multi-GPU: `python bench.py --gpus N` starts its own N ranks (torch.distributed.run, one process per
 GPU) when it is not already running under a launcher; the driver's `torch.distributed.run ... bench.py
 --gpus N` works the same way.  Whole reference batches are sharded across ranks with no data-path
 collective (the graph, tables and weights are replicated per GPU).  The primary line is STRONG scaling:
-the global batch of one step is fixed and dealt over the ranks (64 / N batches each); the weak-scaling
-figure (64 batches per rank) is reported beside it as "weak".  Barrier + synchronize bracket the timed
+the global batch of one step is fixed and dealt over the ranks (192 / N batches each); the weak-scaling
+figure (192 batches per rank) is reported beside it as "weak".  Barrier + synchronize bracket the timed
 region and the time is the max over ranks.
 
 Run:  python bench.py [--gpus N --steps K --warmup W --config {1,2,4}]
@@ -361,7 +362,10 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS),
                     help="BASELINE.json configs[i] graph: 2 = full Enron (the metric's config, default), "
                          "1 = enron_sampled, 4 = synthetic 1M-edge de=dn=172 N=30")
-    ap.add_argument("--batches", type=int, default=64, help="reference batches per step (global, strong scaling)")
+    ap.add_argument("--batches", type=int, default=192,
+                    help="reference batches of --batch-size events per step (global; strong scaling splits them over "
+                         "the ranks).  192 x 100 = 19,200 events = one eval epoch over the full-Enron test split "
+                         "(15 %% of 125,235 edges), a multiple of 8 ranks")
     ap.add_argument("--batch-size", type=int, default=100, help="temp_exp_main --test_bs")
     ap.add_argument("--n-degree", type=int, default=None)
     ap.add_argument("--alpha", type=float, default=1.2)

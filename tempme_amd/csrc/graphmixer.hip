@@ -244,9 +244,8 @@ __global__ void __launch_bounds__(256) gm_embed_kernel(GmArgs a) {
         // ---- channel FFN (:302-305): hidden chunks of 256 through LDS, output tiles in registers
         const int NH = gm_r16(a.HC) / 16;
         const float4 *W1 = reinterpret_cast<const float4 *>(w[8]), *W2 = reinterpret_cast<const float4 *>(w[10]);
-        gmx4 out[4][2];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) out[k][0] = out[k][1] = gmx4{0.f, 0.f, 0.f, 0.f};
+        // the second GEMM's chunk partials are added into X scaled by ew as they come ((y + b) * ew + x
+        // distributed over the chunks): no accumulators live across the chunk loop
         for (int h0 = 0; h0 < NH; h0 += GM_HCH / 16) {
             const int nh = min(GM_HCH / 16, NH - h0);
             for (int ht = wave; ht < nh; ht += 4) {
@@ -263,31 +262,24 @@ __global__ void __launch_bounds__(256) gm_embed_kernel(GmArgs a) {
                     }
             }
             __syncthreads();
+            for (int nt = wave; nt < NT; nt += 4) {
+                gmx4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+                gm_gemm<NMT>(H, HP, h0, W2, NT, nt, h0, nh, acc);
+                const int n = 16 * nt + (lane & 15);
+                const float bv = (h0 == 0 && n < C) ? w[11][n] : 0.f;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int nt = wave + 4 * k;
-                if (nt < NT) gm_gemm<NMT>(H, HP, h0, W2, NT, nt, h0, nh, out[k]);
+                for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int t = 16 * mt + 4 * (lane >> 4) + i;
+                        if (mt < NMT && t < N && n < C) {
+                            const int ix = gm_idx(t, n, XP);
+                            X[ix] = (acc[mt][i] + bv) * sew[t] + X[ix];
+                        }
+                    }
             }
             __syncthreads();
         }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int nt = wave + 4 * k;
-            if (nt >= NT) continue;
-            const int n = 16 * nt + (lane & 15);
-            const float bv = n < C ? w[11][n] : 0.f;
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int t = 16 * mt + 4 * (lane >> 4) + i;
-                    if (mt < NMT && t < N && n < C) {
-                        const int ix = gm_idx(t, n, XP);
-                        X[ix] = (out[k][mt][i] + bv) * sew[t] + X[ix];
-                    }
-                }
-        }
-        __syncthreads();
     }
     // ---- masked mean over the tokens (:176-178) and the neighbour-feature mean (:181-189)
     for (int c = tid; c < C; c += blockDim.x) {
