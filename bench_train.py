@@ -14,6 +14,7 @@ Prints one JSON line (rank 0); value = trained target edges per second over all 
 import argparse
 import json
 import os
+import sys
 import time
 
 import numpy as np
@@ -36,7 +37,19 @@ def main():
     ap.add_argument("--no-fused-adam", action="store_true", help="torch's default (foreach) Adam")
     args = ap.parse_args()
 
+    # one process per GPU: start our own ranks unless a launcher already did (before any GPU call)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        import subprocess
+        import socket
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s_:
+            s_.bind(("127.0.0.1", 0))
+            port = s_.getsockname()[1]
+        sys.exit(subprocess.call([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                                  f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+                                  os.path.abspath(__file__)] + sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench_train.py: --gpus {args.gpus} but the launcher started {world} ranks")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = os.environ.get("TEMPME_DIST_BACKEND", "nccl")
