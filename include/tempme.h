@@ -148,6 +148,11 @@ int tm_gather_rows(const tm_gather_job *jobs, int32_t n_jobs, const int64_t *row
 #define TM_N_WEIGHTS 28
 int tm_weights_create(int32_t de, int32_t dn, int32_t h, int device, tm_weights **out);
 int tm_weights_pack(tm_weights *w, const float *const *tensors, void *stream);
+/* TempME constructor variants for the eval kernels (explainer_new.py:103-105, :121, :141-145, :367):
+ * temporal_guidance = 0 -> the plain Attention (scores not time-weighted; the batch std is not needed),
+ * dependency_gate = 0 -> no dependency gate in retrieve_edge_imp_node (walk importance used as is).
+ * Defaults 1, 1.  The training kernels support the defaults only. */
+int tm_weights_variant(tm_weights *w, int32_t temporal_guidance, int32_t dependency_gate);
 int tm_weights_free(tm_weights *w);
 
 /* Workspace bytes tm_encoder_fwd needs for n_walks walks. */

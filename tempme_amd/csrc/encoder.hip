@@ -173,7 +173,7 @@ __global__ void __launch_bounds__(256) head_kernel(EncW P, int64_t n_walks, int6
             const int64_t g = gw / walks_per_group, b = (gw % walks_per_group) / W;
             const float c = (float)cut[g * (walks_per_group / W) + b];
             const float diff = fabsf(c - ts3[gw * 3 + p]);
-            tw = expf(-diff / (stdv[g] + 1e-6f));
+            tw = P.tg ? expf(-diff / (stdv[g] + 1e-6f)) : 1.f;   // plain Attention: 0.7 + 0.3 * 1 == 1 exactly
         }
         s_tw[tid] = tw;
     }
@@ -347,7 +347,7 @@ __global__ void __launch_bounds__(256) explain_kernel(EncW P, int32_t W, int32_t
                 const float z = s + P.d3b[0];
                 const float gate = 1.f / (1.f + expf(-z));
                 // walk_imp = graphlet_imp (repeated over 3 positions) * (0.5 + 0.5 * gate)   (:364, :386)
-                const float v = imp[ge * W + gr / 3] * (0.5f + 0.5f * gate);
+                const float v = P.dep ? imp[ge * W + gr / 3] * (0.5f + 0.5f * gate) : imp[ge * W + gr / 3];
                 const int32_t key = s_eid[r];
                 uint32_t h = hash_eid(key) >> (32 - hbits);
                 while (true) {
@@ -819,8 +819,8 @@ __device__ __forceinline__ void walk_head(const WalkArgs &a, const float *cs, in
     }
     s0 = col_sum(s0);
     s1 = col_sum(s1);
-    float tw0 = 0.f, tw1 = 0.f;
-    if (valid) {
+    float tw0 = 1.f, tw1 = 1.f;                          // plain Attention (tg = 0): 0.7f + 0.3f == 1.0f exactly
+    if (valid && P.tg) {
         tw0 = expf(-fabsf(hi.cu - hi.t0) / hi.sd);
         tw1 = expf(-fabsf(hi.cu - hi.t1) / hi.sd);
     }
@@ -986,7 +986,7 @@ __global__ void __launch_bounds__(256) gate_table_kernel(EncW P, int32_t n_ids, 
     const float s = gate_logit_lds(G2 + r * ldg2, P.d3w, sub);
     if (sub == 0 && e0 + r < n_ids) {
         const float z = s + P.d3b[0];
-        gf[e0 + r] = 0.5f + 0.5f * (1.f / (1.f + expf(-z)));
+        gf[e0 + r] = P.dep ? 0.5f + 0.5f * (1.f / (1.f + expf(-z))) : 1.f;
     }
 }
 
@@ -1059,7 +1059,7 @@ __global__ void __launch_bounds__(256) gate_reg_kernel(EncW P, int32_t n_ids, co
     z += __shfl_xor(z, 16);
     z += __shfl_xor(z, 32);
     z += P.d3b[0];
-    if (gf && valid && g == 0) gf[e] = 0.5f + 0.5f * (1.f / (1.f + expf(-z)));
+    if (gf && valid && g == 0) gf[e] = P.dep ? 0.5f + 0.5f * (1.f / (1.f + expf(-z))) : 1.f;
 }
 
 // retrieve_edge_imp_node with the gate table: per (group, event) the LDS hash keeps, per edge id,
@@ -1204,6 +1204,13 @@ extern "C" int tm_weights_create(int32_t de, int32_t dn, int32_t h, int device, 
         return rc;
     }
     *out = w;
+    return TM_OK;
+}
+
+extern "C" int tm_weights_variant(tm_weights *w, int32_t temporal_guidance, int32_t dependency_gate) {
+    if (!w) return fail(TM_E_ARG, "tm_weights_variant: NULL weights");
+    w->P.tg = temporal_guidance ? 1 : 0;
+    w->P.dep = dependency_gate ? 1 : 0;
     return TM_OK;
 }
 
@@ -1356,7 +1363,7 @@ extern "C" int tm_encoder_fwd_tab(const tm_weights *w, const float *n_feat, cons
     float *F = reinterpret_cast<float *>(workspace);
     float *stdv = F + n_walks * 3 * 2 * HID;
     hipEvent_t pe = prof_begin(s);
-    std_kernel<<<dim3(n_groups), 1024, 0, s>>>(B, W, cut, ts3, stdv);
+    if (P.tg) std_kernel<<<dim3(n_groups), 1024, 0, s>>>(B, W, cut, ts3, stdv);
     TM_CHECK_LAUNCH();
     prof_end("std_kernel", s, pe);
     if (etab && etab_q0(P) == 0) return fail(TM_E_UNSUPPORTED, "tm_encoder_fwd_tab: no edge table for these dims");
@@ -1423,7 +1430,7 @@ extern "C" int tm_encoder_train_fwd(const tm_weights *w, const float *n_feat, co
     float *F = reinterpret_cast<float *>(workspace);
     float *stdv = F + n_walks * 3 * 2 * HID;
     hipEvent_t pe = prof_begin(s);
-    std_kernel<<<dim3(n_groups), 1024, 0, s>>>(B, W, cut, ts3, stdv);
+    if (P.tg) std_kernel<<<dim3(n_groups), 1024, 0, s>>>(B, W, cut, ts3, stdv);
     TM_CHECK_LAUNCH();
     prof_end("std_kernel", s, pe);
     const int64_t n_rows = n_walks * 3;

@@ -27,6 +27,9 @@ struct EncW {
     // relative to itself, so those steps are the constant cos(phase) (walk_kernel's slot pass)
     const float *evc;
     int qt;
+    // constructor variants (explainer_new.py:103-105, :121, :141): tg = use_temporal_guidance (0: the plain
+    // Attention, no time weighting of the scores), dep = use_dependency_aware_sampling (0: no gate)
+    int tg = 1, dep = 1;
 };
 
 // ------------------------------------------------------------------ MFMA tile GEMM

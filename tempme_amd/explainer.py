@@ -160,25 +160,49 @@ class TempME(nn.Module):
         parameters (temp_exp_main.py:605-631): the autograd formulation runs then."""
         return self.training or (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()))
 
-    def _hip_ok(self):
-        ok = (self.use_temporal_guidance and self.use_dependency_aware_sampling and self.if_cat
-              and self.hid_dim == 64)
+    def _hip_eval_ok(self):
+        """The eval kernels cover every constructor variant with hid_dim == 64 and the category feature
+        (use_temporal_guidance / use_dependency_aware_sampling through tm_weights_variant)."""
+        ok = self.if_cat and self.hid_dim == 64
         if not ok and not getattr(self, "_warned_torch", False):
-            warnings.warn("TempME(use_temporal_guidance=%s, use_dependency_aware_sampling=%s, if_cat_feature=%s, "
-                          "hid_dim=%d): no HIP kernel instance for this constructor variant; forward / "
-                          "retrieve_edge_imp_node run the torch-op formulation on the device"
-                          % (self.use_temporal_guidance, self.use_dependency_aware_sampling, self.if_cat,
-                             self.hid_dim), RuntimeWarning, stacklevel=3)
+            warnings.warn("TempME(if_cat_feature=%s, hid_dim=%d): no HIP kernel instance for this constructor "
+                          "variant; forward / retrieve_edge_imp_node run the torch-op formulation on the device"
+                          % (self.if_cat, self.hid_dim), RuntimeWarning, stacklevel=3)
             self._warned_torch = True
         return ok
 
+    def _hip_ok(self):
+        """The training kernels (f3): the default constructor only."""
+        ok = (self.use_temporal_guidance and self.use_dependency_aware_sampling and self.if_cat
+              and self.hid_dim == 64)
+        if not ok and not getattr(self, "_warned_torch_train", False):
+            warnings.warn("TempME(use_temporal_guidance=%s, use_dependency_aware_sampling=%s, if_cat_feature=%s, "
+                          "hid_dim=%d): the HIP training kernels cover the default constructor; gradients run "
+                          "through the torch-op formulation on the device"
+                          % (self.use_temporal_guidance, self.use_dependency_aware_sampling, self.if_cat,
+                             self.hid_dim), RuntimeWarning, stacklevel=3)
+            self._warned_torch_train = True
+        return ok
+
     def _weight_list(self):
-        at, ec, m, d = self.attention, self.event_conv, self.MLP, self.edge_dependency_gcn
-        mods = [ec.lin_event, ec.MLP[0], ec.MLP[2], at.W1, at.W2, at.MLP[0], at.MLP[3], m[0], m[3], m[5],
-                d[0], d[3], d[6]]
+        at, ec, m = self.attention, self.event_conv, self.MLP
+        # TemporalAwareAttention.MLP = (Linear, ReLU, Dropout, Linear), Attention.MLP = (Linear, ReLU, Linear)
+        am = (at.MLP[0], at.MLP[3]) if isinstance(at, TemporalAwareAttention) else (at.MLP[0], at.MLP[2])
+        mods = [ec.lin_event, ec.MLP[0], ec.MLP[2], at.W1, at.W2, am[0], am[1], m[0], m[3], m[5]]
         ts = []
         for mod in mods:
             ts += [mod.weight, mod.bias]
+        if self.use_dependency_aware_sampling:
+            d = self.edge_dependency_gcn
+            for mod in (d[0], d[3], d[6]):
+                ts += [mod.weight, mod.bias]
+        else:
+            # no gate (tm_weights_variant(dep = 0)): shape-correct zeros keep the pack layout
+            h = self.hid_dim
+            if getattr(self, "_zero_gate", None) is None:
+                z = lambda *sh: torch.zeros(*sh, device=self.node_raw_embed.weight.device)  # noqa: E731
+                self._zero_gate = [z(h, self.edge_dim + self.time_dim), z(h), z(h // 2, h), z(h // 2), z(1, h // 2), z(1)]
+            ts += self._zero_gate
         return ts + [self.time_encoder.basis_freq, self.time_encoder.phase]
 
     def packed_weights(self, force=False):
@@ -193,6 +217,8 @@ class TempME(nn.Module):
                 L.check(L.lib().tm_weights_create(self.edge_dim, self.node_dim, self.hid_dim, dev.index,
                                                   L.C.byref(h)), "tm_weights_create")
                 self._packed = _Packed(h)
+                L.check(L.lib().tm_weights_variant(h, int(bool(self.use_temporal_guidance)),
+                                                   int(bool(self.use_dependency_aware_sampling))), "tm_weights_variant")
             self._raw = [w.detach().to(device=dev, dtype=torch.float32).contiguous() for w in ws]
             arr = (L.C.c_void_p * L.N_WEIGHTS)(*[w.data_ptr() for w in self._raw])
             L.check(L.lib().tm_weights_pack(self._packed.h, arr, L.stream_ptr(dev)), "tm_weights_pack")
@@ -411,7 +437,7 @@ class TempME(nn.Module):
         dev = self._dev()
         B, W = np.shape(edge_idx)[0], np.shape(edge_idx)[1]
         assert np.shape(edge_identify)[-1] == 3 and np.shape(edge_idx)[-1] == 3, "event_dim mismatch (:180)"
-        if not self._hip_ok():
+        if not self._hip_eval_ok() or (self._needs_autograd() and not self._hip_ok()):
             return self._forward_torch(walks, cut_time_l, edge_identify)
         if self._needs_autograd():
             out = self.forward_groups(_to(node_idx, dev, torch.int32), _to(edge_idx, dev, torch.int32),
@@ -433,7 +459,8 @@ class TempME(nn.Module):
         """explainer_new.py:354-406 -> (hop-1 [B,N], hop-2 [B,N^2])."""
         node_record, eidx_record, _ = subgraph
         dev = self._dev()
-        if not self._hip_ok():
+        needs_grad = training or (graphlet_imp.requires_grad and torch.is_grad_enabled())
+        if not self._hip_eval_ok() or (needs_grad and not self._hip_ok()):
             return self._edge_imp_torch(subgraph, graphlet_imp, walks, training)
         if training or (graphlet_imp.requires_grad and torch.is_grad_enabled()):
             B, N = np.shape(node_record[0])[0], np.shape(node_record[0])[1]

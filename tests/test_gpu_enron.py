@@ -90,6 +90,8 @@ def test_dropin_tempme_matches_reference_enron(dev, g, z, tag):
     for k in range(3):
         kl = ex.kl_loss(imps[k], walks[k], target=0.3)
         np.testing.assert_allclose(float(kl), z[f"{tag}_kl"][k], rtol=RTOL, atol=ATOL)
+    if var != "h32":      # every variant but hid_dim != 64 runs the HIP eval kernels (tm_weights_variant)
+        assert ex._packed is not None, "the HIP encoder did not run"
 
 
 @pytest.mark.parametrize("edge_table", [True, False])
