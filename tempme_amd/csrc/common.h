@@ -244,6 +244,10 @@ struct tm_graph {
     int32_t *d_ppos;
     double *d_ets;
     tmk::PairBlk *d_pblk;
+    // device-built graphs (graph_dev.hip): the sorted CSR columns and get_ts2idx values stay on the device
+    // until tm_graph_export asks for them
+    int32_t *d_hngh, *d_heid, *d_dict;
+    int dev_built;
     // host copies (export)
     int64_t *h_off;
     int32_t *h_ngh, *h_eid, *h_dict;

@@ -87,6 +87,9 @@ static void free_graph(tm_graph *g) {
     if (g->d_ppos) (void)hipFree(g->d_ppos);
     if (g->d_ets) (void)hipFree(g->d_ets);
     if (g->d_pblk) (void)hipFree(g->d_pblk);
+    if (g->d_hngh) (void)hipFree(g->d_hngh);
+    if (g->d_heid) (void)hipFree(g->d_heid);
+    if (g->d_dict) (void)hipFree(g->d_dict);
     delete[] g->h_off;
     delete[] g->h_ngh;
     delete[] g->h_eid;
@@ -427,11 +430,23 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
 // temp_exp_main.py:135-144 on raw edge rows: for every row (dst, e, t) is appended to src's list,
 // then (src, e, t) to dst's; owner-major by a counting sort (stable, so each list keeps the rows'
 // order), then tm_graph_build.
+int tm_graph_build_edges_device(int32_t V, int64_t n_edges, const int64_t *src, const int64_t *dst, const int64_t *eidx,
+                                const double *ts, int device, tm_graph **out);
+
 extern "C" int tm_graph_build_edges(int32_t n_nodes, int64_t n_edges, const int64_t *src, const int64_t *dst,
                                     const int64_t *eidx, const double *ts, int device, tm_graph **out) {
     if (!out || n_nodes <= 0 || n_edges < 0) return fail(TM_E_ARG, "tm_graph_build_edges: bad arguments");
     if (n_edges > 0 && (!src || !dst || !eidx || !ts)) return fail(TM_E_ARG, "tm_graph_build_edges: NULL arrays");
     if (2 * n_edges >= INT32_MAX / 2) return fail(TM_E_UNSUPPORTED, "tm_graph_build_edges: too many edges");
+    *out = nullptr;
+    // the device builder (graph_dev.hip); the host builder below for rows that repeat an edge id, or on
+    // request (TEMPME_HOST_BUILD=1)
+    if (!std::getenv("TEMPME_HOST_BUILD")) {
+        Timer tmd;
+        const int rc = tm_graph_build_edges_device(n_nodes, n_edges, src, dst, eidx, ts, device, out);
+        tmd.lap("device build");
+        if (rc != 1) return rc;
+    }
     Timer tm;
     // per-chunk node counts, then each chunk scatters its rows in order (stable)
     const int T = std::max(1, (int)std::min<int64_t>(build_threads(), (n_edges + 65535) / 65536));
@@ -503,10 +518,29 @@ extern "C" int tm_graph_info(const tm_graph *g, int32_t *n_nodes, int64_t *n_ent
     return TM_OK;
 }
 
-extern "C" int tm_graph_export(const tm_graph *g, int64_t *off, int32_t *ngh, int32_t *eid, double *ts,
+extern "C" int tm_graph_export(const tm_graph *gc, int64_t *off, int32_t *ngh, int32_t *eid, double *ts,
                                int32_t *dict_val) {
-    if (!g) return fail(TM_E_ARG, "tm_graph_export: NULL graph");
+    if (!gc) return fail(TM_E_ARG, "tm_graph_export: NULL graph");
+    tm_graph *g = const_cast<tm_graph *>(gc);
     const int64_t n = g->d.n_entries;
+    if (g->dev_built && !g->h_off) {   // host copies of a device-built graph, made once
+        const int32_t V = g->d.n_nodes;
+        const int64_t nn = std::max<int64_t>(n, 1);
+        std::vector<int32_t> off32(V + 1);
+        g->h_off = new int64_t[V + 1];
+        g->h_ngh = new int32_t[nn];
+        g->h_eid = new int32_t[nn];
+        g->h_dict = new int32_t[nn];
+        g->h_ts = new double[nn];
+        hipError_t e = hipSuccess;
+        e = e ? e : hipMemcpy(off32.data(), g->d_off, sizeof(int32_t) * (V + 1), hipMemcpyDeviceToHost);
+        e = e ? e : hipMemcpy(g->h_ngh, g->d_hngh, sizeof(int32_t) * nn, hipMemcpyDeviceToHost);
+        e = e ? e : hipMemcpy(g->h_eid, g->d_heid, sizeof(int32_t) * nn, hipMemcpyDeviceToHost);
+        e = e ? e : hipMemcpy(g->h_dict, g->d_dict, sizeof(int32_t) * nn, hipMemcpyDeviceToHost);
+        e = e ? e : hipMemcpy(g->h_ts, g->d_tsd, sizeof(double) * nn, hipMemcpyDeviceToHost);
+        for (int32_t u = 0; u <= V; ++u) g->h_off[u] = off32[u];
+        if (e != hipSuccess) return fail(TM_E_HIP, std::string("tm_graph_export: ") + hipGetErrorString(e));
+    }
     if (off) std::copy(g->h_off, g->h_off + g->d.n_nodes + 1, off);
     if (ngh) std::copy(g->h_ngh, g->h_ngh + n, ngh);
     if (eid) std::copy(g->h_eid, g->h_eid + n, eid);
