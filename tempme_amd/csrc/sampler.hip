@@ -964,12 +964,20 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
         const int32_t j = x / NB, kb = x % NB, c = c2[j];
         const uint4 b = draw_block(key, 2, ev, j, kb);
         const uint32_t wv[4] = {b.x, b.y, b.z, b.w};
+        uint32_t o4[4];
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
             const int32_t k = 4 * kb + w;
             // keyed: (draw << 6 | index), unique, so the np.sort rank is one compare (see khop2_kernel)
             const uint32_t dv = (uint32_t)scale_draw(wv[w], c);
-            if (k < N) d2[j * N + k] = c > 0 ? (keyed ? (dv << 6) | (uint32_t)k : dv) : 0xFFFFFFFFu;
+            o4[w] = c > 0 ? (keyed ? (dv << 6) | (uint32_t)k : dv) : 0xFFFFFFFFu;
+        }
+        if ((N & 3) == 0) {          // one 16-B store per lane (4-B stores at a 16-B lane stride: 4-way bank conflicts)
+            *reinterpret_cast<uint4 *>(d2 + j * N + 4 * kb) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+        } else {
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+                if (4 * kb + w < N) d2[j * N + 4 * kb + w] = o4[w];
         }
     }
     __syncthreads();
@@ -1052,8 +1060,17 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
         TM_ST(o_ts3[o * 3 + 0], s3.ts); TM_ST(o_ts3[o * 3 + 1], s2.ts); TM_ST(o_ts3[o * 3 + 2], h1t[j]);
         const int32_t c = cat_of(s3.code, s3.t, 0);
         TM_ST(o_cat[o], c);
-        if (c >= 0) atomicAdd(&bins[c], 1u);
-        weid[w * 3 + 0] = s3.eid; weid[w * 3 + 1] = s2.eid; weid[w * 3 + 2] = e1;
+        {   // histogram by wave ballots: one lane adds each category's count (LDS atomics from 60 lanes into
+            // 12 words serialised on bank conflicts)
+            const int lead = __ffsll((unsigned long long)__ballot(1)) - 1;
+#pragma unroll
+            for (int k = 0; k < 12; ++k) {
+                const int nk = __popcll(__ballot(c == k));
+                if (tid == lead && nk) bins[k] += (unsigned)nk;
+            }
+        }
+        // walk ids column-major (p * W + w): 4-B lane stride, conflict-free
+        weid[w] = s3.eid; weid[W + w] = s2.eid; weid[2 * W + w] = e1;
         ecnt_insert(tkeys, tcnt, tmask, s3.eid, 0);
         ecnt_insert(tkeys, tcnt, tmask, s2.eid, 1);
         ecnt_insert(tkeys, tcnt, tmask, e1, 2);
@@ -1065,7 +1082,7 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
     for (int32_t w = tid; w < W; w += blockDim.x) {
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
-            const uint32_t c = ecnt_lookup(tkeys, tcnt, tmask, weid[w * 3 + p]);
+            const uint32_t c = ecnt_lookup(tkeys, tcnt, tmask, weid[p * W + w]);
 #pragma unroll
             for (int q = 0; q < 3; ++q) TM_ST(oc[(w * 3 + p) * 3 + q], (float)((c >> (10 * q)) & 1023u));
         }
