@@ -67,6 +67,11 @@ __device__ __forceinline__ void gm_gemm(const float *X, int P, int GX, const flo
 #pragma unroll
     for (int u = 0; u < PF; ++u) bq[u] = u < nG ? wp[(size_t)(G0 + u) * gs] : make_float4(0.f, 0.f, 0.f, 0.f);
     const float *xr = X + m * P + 4 * j + 16 * (G0 - GX);
+    // the A fragments of block g + 1 are read from LDS while block g's MFMAs run
+    float4 an[NMT];
+#pragma unroll
+    for (int mt = 0; mt < NMT; ++mt)
+        an[mt] = nG > 0 ? *reinterpret_cast<const float4 *>(xr + 16 * mt * P) : make_float4(0.f, 0.f, 0.f, 0.f);
     for (int g0 = 0; g0 < nG; g0 += PF) {
 #pragma unroll
         for (int u = 0; u < PF; ++u) {
@@ -74,13 +79,18 @@ __device__ __forceinline__ void gm_gemm(const float *X, int P, int GX, const flo
             if (g >= nG) break;
             const float4 b = bq[u];
             if (g + PF < nG) bq[u] = wp[(size_t)(G0 + g + PF) * gs];
+            float4 av[NMT];
 #pragma unroll
             for (int mt = 0; mt < NMT; ++mt) {
-                const float4 av = *reinterpret_cast<const float4 *>(xr + 16 * mt * P + 16 * g);
-                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, b.x, acc[mt], 0, 0, 0);
-                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, b.y, acc[mt], 0, 0, 0);
-                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, b.z, acc[mt], 0, 0, 0);
-                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, b.w, acc[mt], 0, 0, 0);
+                av[mt] = an[mt];
+                if (g + 1 < nG) an[mt] = *reinterpret_cast<const float4 *>(xr + 16 * mt * P + 16 * (g + 1));
+            }
+#pragma unroll
+            for (int mt = 0; mt < NMT; ++mt) {
+                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt].x, b.x, acc[mt], 0, 0, 0);
+                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt].y, b.y, acc[mt], 0, 0, 0);
+                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt].z, b.z, acc[mt], 0, 0, 0);
+                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt].w, b.w, acc[mt], 0, 0, 0);
             }
         }
     }
