@@ -13,15 +13,18 @@
 //                                              explanation weight on the input and both branch outputs
 //
 // One workgroup (4 waves) per row (root node): the row's N <= 32 neighbour tokens stay in LDS for the
-// whole embedding.  GEMMs (projection, channel FFN) on fp32 MFMA 16x16x4 with the activations as the
-// A operand read from LDS (ds_read_b128: LDS layout swaps the (4 k-steps x 4 lane groups) inside every
-// 16-wide K block so a lane's four K values are contiguous) and the weights as the B operand from
-// fragments packed once per weight version (tm_gm_pack, one dwordx4 per lane per 16-K block); the
-// waves split the output tiles and each does both 16-token tiles with one weight fragment.  The
-// channel FFN's 4C hidden features go through LDS in chunks of 256 (GELU in the first GEMM's
-// epilogue, the second GEMM accumulating across chunks in registers).  Token mixing, LayerNorms and
-// the masked means are VALU / wave reductions.  The output layer and the MergeLayer score are plain
-// [rows x 2C] GEMMs left to the library (tempme_amd/graphmixer.py).
+// whole embedding, in ~50 KB at C = T = 172 so three workgroups share a CU (12 waves, the register
+// budget set to match).  GEMMs (projection, channel FFN) on fp32 MFMA 16x16x4 with the activations as
+// the A operand read from LDS (ds_read_b128: LDS layout swaps the (4 k-steps x 4 lane groups) inside
+// every 16-wide K block so a lane's four K values are contiguous) and the weights as the B operand from
+// fragments packed once per weight version (tm_gm_pack, one dwordx4 per lane per 16-K block); a wave
+// takes the output tiles wave + 4i and runs them in one K loop (each A fragment read once for all of
+// them, the next block's fragments in flight, ping-pong registers).  The projection input goes through
+// LDS one K half at a time; the channel LayerNorm is applied to the first FFN GEMM's A fragments as they
+// are read (no normalised copy of X); the 4C hidden features go through LDS in chunks of 192 (GELU in
+// the first GEMM's epilogue) and the second GEMM accumulates across the chunks in registers.  Token
+// mixing, LayerNorm statistics and the masked means are VALU / wave reductions.  The output layer and
+// the MergeLayer score are plain [rows x 2C] GEMMs left to the library (tempme_amd/graphmixer.py).
 #include <algorithm>
 
 #include "common.h"
@@ -31,7 +34,7 @@ namespace tmk {
 typedef float gmx4 __attribute__((ext_vector_type(4)));
 
 constexpr int GM_MT = 32;      // tokens per row (two 16-row MFMA tiles)
-constexpr int GM_HCH = 256;    // channel-FFN hidden features per LDS chunk
+constexpr int GM_HCH = 192;    // channel-FFN hidden features per LDS chunk (12 tiles: 3 per wave; 128: 2 % slower)
 constexpr int GM_MAXL = 4;
 
 struct GmArgs {
@@ -51,50 +54,15 @@ __host__ __device__ inline int32_t gm_r16(int32_t x) { return (x + 15) & ~15; }
 // k = 16G + 4s + j is 16G + 4j + s, so lane group j's four K values of one MFMA block are one float4
 __device__ __forceinline__ int gm_idx(int m, int k, int P) { return m * P + (k & ~15) + 4 * (k & 3) + ((k >> 2) & 3); }
 
-__device__ __forceinline__ float gm_gelu(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
-
-// acc[mt] (16x16 output tile nt, token tiles mt < NMT) += X[.., 16 G0 .. 16 (G0 + nG)) * W^T over K
-// blocks G0..G0+nG of the packed weights (NT output tiles); X in LDS ([32][P] image, K block g of the
-// image = packed K block G0 + g - GX)
-template <int NMT>
-__device__ __forceinline__ void gm_gemm(const float *X, int P, int GX, const float4 *Wp, int NT, int nt, int G0, int nG,
-                                        gmx4 (&acc)[2]) {
-    constexpr int PF = 4;   // weight fragments in flight (L2 latency behind the MFMAs of the blocks before)
-    const int lane = threadIdx.x & 63, m = lane & 15, j = lane >> 4;
-    const float4 *wp = Wp + (size_t)nt * 64 + lane;
-    const size_t gs = (size_t)NT * 64;
-    float4 bq[PF];
-#pragma unroll
-    for (int u = 0; u < PF; ++u) bq[u] = u < nG ? wp[(size_t)(G0 + u) * gs] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float *xr = X + m * P + 4 * j + 16 * (G0 - GX);
-    // the A fragments of block g + 1 are read from LDS while block g's MFMAs run
-    float4 an[NMT];
-#pragma unroll
-    for (int mt = 0; mt < NMT; ++mt)
-        an[mt] = nG > 0 ? *reinterpret_cast<const float4 *>(xr + 16 * mt * P) : make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int g0 = 0; g0 < nG; g0 += PF) {
-#pragma unroll
-        for (int u = 0; u < PF; ++u) {
-            const int g = g0 + u;
-            if (g >= nG) break;
-            const float4 b = bq[u];
-            if (g + PF < nG) bq[u] = wp[(size_t)(G0 + g + PF) * gs];
-            float4 av[NMT];
-#pragma unroll
-            for (int mt = 0; mt < NMT; ++mt) {
-                av[mt] = an[mt];
-                if (g + 1 < nG) an[mt] = *reinterpret_cast<const float4 *>(xr + 16 * mt * P + 16 * (g + 1));
-            }
-#pragma unroll
-            for (int mt = 0; mt < NMT; ++mt) {
-                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt].x, b.x, acc[mt], 0, 0, 0);
-                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt].y, b.y, acc[mt], 0, 0, 0);
-                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt].z, b.z, acc[mt], 0, 0, 0);
-                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt].w, b.w, acc[mt], 0, 0, 0);
-            }
-        }
-    }
+// threadIdx.x laundered through an opaque asm: lane-dependent addresses computed from it cannot be hoisted
+// out of the layer loop by LICM (hoisted, they stay live across every phase and cost the third wave)
+__device__ __forceinline__ int gm_tid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
 }
+
+__device__ __forceinline__ float gm_gelu(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
 // sum over the 64 lanes of a wave
 __device__ __forceinline__ float gm_wsum(float v) {
@@ -103,18 +71,84 @@ __device__ __forceinline__ float gm_wsum(float v) {
     return v;
 }
 
-template <int NMT>
-__global__ void __launch_bounds__(256) gm_embed_kernel(GmArgs a) {
+// The wave's output tiles nt0 + 4 i (i < ntw <= NTW) in one K loop: per K block the A fragments are read
+// from LDS once for all of them (and, LN, normalised once: the channel LayerNorm (:300) applied as they
+// are read, (x - mean_m) * rstd_m * w_k + b_k with the LN parameters in the image's permuted K order, so
+// no normalised copy of X takes LDS), and the next block's weight fragments and A fragments are in
+// flight during this block's NTW * NMT * 4 MFMAs.  acc accumulates (callers zero it).  Padding tokens
+// (m >= N) only produce rows the caller discards; channels >= C have w = b = 0.
+template <int NMT, int NTW, bool LN>
+__device__ __forceinline__ void gm_gemm_mt(const float *X, int P, int GX, const float4 *Wp, int NT, int nt0, int ntw,
+                                           int G0, int nG, gmx4 (&acc)[NTW][2], const float *lnw, const float *lnb,
+                                           const float (&mr)[2], const float (&rr)[2]) {
+    const int lane = gm_tid() & 63, m = lane & 15, j = lane >> 4;
+    const size_t gs = (size_t)NT * 64;
+    const float4 *wp = Wp + (size_t)nt0 * 64 + lane + (size_t)G0 * gs;
+    const float *xr = X + m * P + 4 * j + 16 * (G0 - GX);
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    // block g's fragments: B of the wave's tiles, A of its token tiles, LN weight / bias of its K values
+    auto load = [&](int g, float4 (&b)[NTW], float4 (&x)[NMT], float4 &lw, float4 &lb) {
+#pragma unroll
+        for (int i = 0; i < NTW; ++i) b[i] = i < ntw ? wp[i * 256 + (size_t)g * gs] : z4;
+#pragma unroll
+        for (int q = 0; q < NMT; ++q) x[q] = *reinterpret_cast<const float4 *>(xr + 16 * q * P + 16 * g);
+        if (LN) {
+            lw = *reinterpret_cast<const float4 *>(lnw + 16 * (G0 + g) + 4 * j);
+            lb = *reinterpret_cast<const float4 *>(lnb + 16 * (G0 + g) + 4 * j);
+        }
+    };
+    auto mma = [&](const float4 (&b)[NTW], const float4 (&x)[NMT], const float4 &lw, const float4 &lb) {
+        float4 av[NMT];
+#pragma unroll
+        for (int q = 0; q < NMT; ++q) {
+            av[q] = x[q];
+            if (LN) {
+                av[q].x = (x[q].x - mr[q]) * rr[q] * lw.x + lb.x;
+                av[q].y = (x[q].y - mr[q]) * rr[q] * lw.y + lb.y;
+                av[q].z = (x[q].z - mr[q]) * rr[q] * lw.z + lb.z;
+                av[q].w = (x[q].w - mr[q]) * rr[q] * lw.w + lb.w;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NTW; ++i) {
+            if (i >= ntw) break;
+#pragma unroll
+            for (int q = 0; q < NMT; ++q) {
+                acc[i][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q].x, b[i].x, acc[i][q], 0, 0, 0);
+                acc[i][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q].y, b[i].y, acc[i][q], 0, 0, 0);
+                acc[i][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q].z, b[i].z, acc[i][q], 0, 0, 0);
+                acc[i][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q].w, b[i].w, acc[i][q], 0, 0, 0);
+            }
+        }
+    };
+    // ping-pong buffers (no register copies: a copy of a pending load would wait for it)
+    float4 b0[NTW], b1[NTW], x0[NMT], x1[NMT], w0 = z4, w1 = z4, l0 = z4, l1 = z4;
+    if (nG > 0) load(0, b0, x0, w0, l0);
+    for (int g = 0; g < nG; g += 2) {
+        if (g + 1 < nG) load(g + 1, b1, x1, w1, l1);
+        mma(b0, x0, w0, l0);
+        if (g + 1 >= nG) break;
+        if (g + 2 < nG) load(g + 2, b0, x0, w0, l0);
+        mma(b1, x1, w1, l1);
+    }
+}
+
+// LDS plan (floats): X [32][XP] | U [ulen] | token mean, rstd [2][32] | LN weight, bias [2][C16] | ew_eff,
+// valid [2][32].  U holds, in turn, the projection input one K half at a time ([32][16 KH + 4]), the token
+// mixing's column statistics and the channel FFN's hidden chunk ([32][GM_HCH + 4]).  ~50 KB at C = T =
+// 172: three workgroups (12 waves) per CU, the register budget set to match (amdgpu_waves_per_eu).
+template <int NMT, int NTW>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) gm_embed_kernel(GmArgs a) {
     extern __shared__ float gm_lds[];
     const int r = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int N = a.N, C = a.C, T = a.T, D = a.D;
-    const int C16 = gm_r16(C), K016 = gm_r16(C + T);
-    const int XP = C16 + 4, K0P = K016 + 4, HP = GM_HCH + 4;
-    // LDS: X [32][XP] | U = max(X0 [32][K0P], XN [32][XP] + H [32][HP]) | ew_eff, valid [32]
+    const int C16 = gm_r16(C), KG = gm_r16(C + T) / 16, KH = (KG + 1) / 2;
+    const int XP = C16 + 4, HP = GM_HCH + 4, K0P = 16 * KH + 4;
+    const int ulen = max(max(GM_MT * K0P, GM_MT * HP), 2 * C16);
     float *X = gm_lds, *U = X + GM_MT * XP;
-    float *X0 = U, *XN = U, *H = U + GM_MT * XP;
-    const int ulen = max(GM_MT * K0P, GM_MT * (XP + HP));
-    float *sew = U + ulen, *sval = sew + GM_MT;
+    float *X0 = U, *H = U;
+    float *tmean = U + ulen, *trstd = tmean + GM_MT, *lnw = trstd + GM_MT, *lnb = lnw + C16;
+    float *sew = lnb + C16, *sval = sew + GM_MT;
     const bool has_ew = a.ew != nullptr;
     if (tid < GM_MT) {
         const bool v = tid < N && a.nid[(size_t)r * N + tid] != 0;
@@ -123,44 +157,64 @@ __global__ void __launch_bounds__(256) gm_embed_kernel(GmArgs a) {
         sew[tid] = tid < N ? (has_ew ? a.ew[(size_t)r * N + tid] * (v ? 1.f : 0.f) : 1.f) : 0.f;
     }
     __syncthreads();
-    // ---- projection input [E(e) | cos(dt w + b)] (padding neighbours: time part zeroed, edge part too
-    // unless edge_attr is given) (:156-167)
+    const int NT = C16 / 16, ntw = (NT - wave + 3) / 4;   // this wave's output tiles: wave + 4 i, i < ntw
+    float mr[2] = {0.f, 0.f}, rr[2] = {0.f, 0.f};
+    // ---- projection (:156-167): X = [E(e) | cos(dt w + b)] Wp^T + bp, K in two halves through U
+    // (padding neighbours: time part zeroed, edge part too unless edge_attr is given)
     const double cut = a.cut[r];
-    for (int i = tid; i < GM_MT * K016; i += blockDim.x) {
-        const int t = i / K016, k = i - t * K016;
-        float v = 0.f;
-        if (t < N) {
-            const bool valid = sval[t] != 0.f;
-            if (k < C) {
-                if (a.edge_attr) v = a.edge_attr[((size_t)r * N + t) * C + k];
-                else if (valid) v = a.e_feat[(size_t)a.eid[(size_t)r * N + t] * C + k];
-            } else if (k < C + T && valid) {
-                // Linear(1, d) on fp32 dt: one rounding of dt * w + b (what the reference's CPU addmm gives)
-                const float dt = (float)(cut - a.ts[(size_t)r * N + t]);
-                const float arg = (float)((double)dt * (double)a.time_w[k - C] + (double)a.time_b[k - C]);
-                v = cos_rd(arg);   // branch-free fp64-reduced cos (common.h), |err| <= 1.7e-7
+    for (int h = 0; h < 2; ++h) {
+        const int G0 = h * KH, nG = min(KH, KG - G0), W16 = 16 * nG;
+        if (nG <= 0) break;
+        for (int i = tid; i < GM_MT * W16; i += blockDim.x) {
+            const int t = i / W16, k = 16 * G0 + (i - t * W16);
+            float v = 0.f;
+            if (t < N) {
+                const bool valid = sval[t] != 0.f;
+                if (k < C) {
+                    if (a.edge_attr) v = a.edge_attr[((size_t)r * N + t) * C + k];
+                    else if (valid) v = a.e_feat[(size_t)a.eid[(size_t)r * N + t] * C + k];
+                } else if (k < C + T && valid) {
+                    // Linear(1, d) on fp32 dt: one rounding of dt * w + b (what the reference's CPU addmm gives)
+                    const float dt = (float)(cut - a.ts[(size_t)r * N + t]);
+                    const float arg = (float)((double)dt * (double)a.time_w[k - C] + (double)a.time_b[k - C]);
+                    v = cos_rd(arg);   // branch-free fp64-reduced cos (common.h), |err| <= 1.7e-7
+                }
+            }
+            X0[gm_idx(t, k - 16 * G0, K0P)] = v;
+        }
+        __syncthreads();
+        {
+            gmx4 acc[NTW][2];
+#pragma unroll
+            for (int i = 0; i < NTW; ++i) acc[i][0] = acc[i][1] = gmx4{0.f, 0.f, 0.f, 0.f};
+            gm_gemm_mt<NMT, NTW, false>(X0, K0P, G0, a.proj_w, NT, wave, ntw, G0, nG, acc, nullptr, nullptr, mr, rr);
+#pragma unroll
+            for (int i = 0; i < NTW; ++i) {
+                if (i >= ntw) break;
+                const int n = 16 * (wave + 4 * i) + (lane & 15);
+                const float bv = n < C ? a.proj_b[n] : 0.f;
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int t = 16 * mt + 4 * (lane >> 4) + e;
+                        const int ix = gm_idx(t, n, XP);
+                        const bool in = mt < NMT && n < C && t < N;
+                        // first half stored, second half (+ bias) added: the same two-part sum for every element
+                        if (h == 0) X[ix] = in ? acc[i][mt][e] : 0.f;
+                        else if (in) X[ix] = X[ix] + acc[i][mt][e] + bv;
+                    }
             }
         }
-        X0[gm_idx(t, k, K0P)] = v;
+        __syncthreads();
     }
-    __syncthreads();
-    const int NT = C16 / 16;
-    {   // projection (:167): X = X0 Wp^T + bp
-        for (int nt = wave; nt < NT; nt += 4) {
-            gmx4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-            gm_gemm<NMT>(X0, K0P, 0, a.proj_w, NT, nt, 0, K016 / 16, acc);
-            const int n = 16 * nt + (lane & 15);
-            const float bv = n < C ? a.proj_b[n] : 0.f;
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int t = 16 * mt + 4 * (lane >> 4) + i;
-                    X[gm_idx(t, n, XP)] = (mt < NMT && n < C && t < N) ? acc[mt][i] + bv : 0.f;
-                }
+    if (KG == 1) {   // one K half only: the bias is still owed
+        for (int i = tid; i < GM_MT * C16; i += blockDim.x) {
+            const int t = i / C16, n = i - t * C16;
+            if (t < N && n < C) X[gm_idx(t, n, XP)] += a.proj_b[n];
         }
+        __syncthreads();
     }
-    __syncthreads();
     for (int l = 0; l < a.L; ++l) {
         const float *const *w = a.lw + 12 * l;
         // ---- token mixing (:289-297).  Per channel c: H = gelu(W1 LN_t(X[:, c] * ew) + b1), Y = W2 H + b2,
@@ -168,7 +222,7 @@ __global__ void __launch_bounds__(256) gm_embed_kernel(GmArgs a) {
         // the A operand against the normalised column (B, K = tokens), then W2 (N x HT) against H, whose
         // K order is permuted (step s, lane group g <-> hidden unit 4g + s) so H stays in the registers the
         // first MFMA left it in.  Column statistics first, one thread per channel.
-        float *cm = XN, *cr = XN + C16;
+        float *cm = U, *cr = U + C16;
         for (int c = tid; c < C; c += blockDim.x) {
             float sm = 0.f;
             for (int t = 0; t < N; ++t) sm += X[gm_idx(t, c, XP)] * sew[t];
@@ -181,9 +235,15 @@ __global__ void __launch_bounds__(256) gm_embed_kernel(GmArgs a) {
             cm[c] = mean;
             cr[c] = 1.f / sqrtf(q / (float)N + 1e-5f);
         }
+        // channel LayerNorm parameters in the image's permuted K order (read as float4 by gm_gemm_mt)
+        for (int k = tid; k < C16; k += blockDim.x) {
+            const int p = (k & ~15) + 4 * (k & 3) + ((k >> 2) & 3);
+            lnw[p] = k < C ? w[6][k] : 0.f;
+            lnb[p] = k < C ? w[7][k] : 0.f;
+        }
         __syncthreads();
         {
-            const int g = lane >> 4, li = lane & 15, HT = a.HT;
+            const int ln = gm_tid() & 63, g = ln >> 4, li = ln & 15, HT = a.HT;
             float a1[2][4], a2[2][4], lg[2][4], lb[2][4], b2v[2][4], b1v[4];
 #pragma unroll
             for (int G = 0; G < 2; ++G)
@@ -233,63 +293,82 @@ __global__ void __launch_bounds__(256) gm_embed_kernel(GmArgs a) {
             }
         }
         __syncthreads();
-        // ---- channel LayerNorm (:300), one wave per token
+        // ---- channel LayerNorm statistics (:300), one wave per token; applied inside the first FFN GEMM
         for (int t = wave; t < GM_MT; t += 4) {
-            float s = 0.f, q = 0.f;
+            float mean = 0.f, rstd = 0.f;
             if (t < N) {
+                float s = 0.f, q = 0.f;
                 for (int c = lane; c < C; c += 64) s += X[gm_idx(t, c, XP)];
-                const float mean = gm_wsum(s) / (float)C;
+                mean = gm_wsum(s) / (float)C;
                 for (int c = lane; c < C; c += 64) {
                     const float d = X[gm_idx(t, c, XP)] - mean;
                     q += d * d;
                 }
-                const float rstd = 1.f / sqrtf(gm_wsum(q) / (float)C + 1e-5f);
-                for (int c = lane; c < C16; c += 64)
-                    XN[gm_idx(t, c, XP)] = c < C ? (X[gm_idx(t, c, XP)] - mean) * rstd * w[6][c] + w[7][c] : 0.f;
-            } else {
-                for (int c = lane; c < C16; c += 64) XN[gm_idx(t, c, XP)] = 0.f;
+                rstd = 1.f / sqrtf(gm_wsum(q) / (float)C + 1e-5f);
+            }
+            if (lane == 0) {
+                tmean[t] = mean;
+                trstd[t] = rstd;
             }
         }
         __syncthreads();
-        // ---- channel FFN (:302-305): hidden chunks of 256 through LDS, output tiles in registers
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+            mr[mt] = tmean[16 * mt + (lane & 15)];
+            rr[mt] = trstd[16 * mt + (lane & 15)];
+        }
+        // ---- channel FFN (:302-305): hidden chunks of GM_HCH through LDS (GELU in the first GEMM's epilogue)
         const int NH = gm_r16(a.HC) / 16;
         const float4 *W1 = reinterpret_cast<const float4 *>(w[8]), *W2 = reinterpret_cast<const float4 *>(w[10]);
-        // the second GEMM's chunk partials are added into X scaled by ew as they come ((y + b) * ew + x
-        // distributed over the chunks): no accumulators live across the chunk loop
+        // every chunk's first GEMM normalises the layer's input X, so the second GEMM accumulates its
+        // output tiles in registers across the chunks and X is updated once, after them
+        gmx4 acc2[NTW][2];
+#pragma unroll
+        for (int i = 0; i < NTW; ++i) acc2[i][0] = acc2[i][1] = gmx4{0.f, 0.f, 0.f, 0.f};
         for (int h0 = 0; h0 < NH; h0 += GM_HCH / 16) {
-            const int nh = min(GM_HCH / 16, NH - h0);
-            for (int ht = wave; ht < nh; ht += 4) {
-                gmx4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-                gm_gemm<NMT>(XN, XP, 0, W1, NH, h0 + ht, 0, C16 / 16, acc);
-                const int n = 16 * (h0 + ht) + (lane & 15);
-                const float bv = n < a.HC ? w[9][n] : 0.f;
+            const int nh = min(GM_HCH / 16, NH - h0), nw1 = (nh - wave + 3) / 4;
+            {
+                gmx4 acc[GM_HCH / 64][2];
 #pragma unroll
-                for (int mt = 0; mt < 2; ++mt)
+                for (int i = 0; i < GM_HCH / 64; ++i) acc[i][0] = acc[i][1] = gmx4{0.f, 0.f, 0.f, 0.f};
+                gm_gemm_mt<NMT, GM_HCH / 64, true>(X, XP, 0, W1, NH, h0 + wave, nw1, 0, C16 / 16, acc, lnw, lnb, mr, rr);
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int t = 16 * mt + 4 * (lane >> 4) + i;
-                        H[gm_idx(t, 16 * ht + (lane & 15), HP)] = (mt < NMT && n < a.HC) ? gm_gelu(acc[mt][i] + bv) : 0.f;
-                    }
+                for (int i = 0; i < GM_HCH / 64; ++i) {
+                    if (i >= nw1) break;
+                    const int ht = wave + 4 * i, n = 16 * (h0 + ht) + (lane & 15);
+                    const float bv = n < a.HC ? w[9][n] : 0.f;
+#pragma unroll
+                    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const int t = 16 * mt + 4 * (lane >> 4) + e;
+                            H[gm_idx(t, 16 * ht + (lane & 15), HP)] = (mt < NMT && n < a.HC) ? gm_gelu(acc[i][mt][e] + bv) : 0.f;
+                        }
+                }
             }
             __syncthreads();
-            for (int nt = wave; nt < NT; nt += 4) {
-                gmx4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-                gm_gemm<NMT>(H, HP, h0, W2, NT, nt, h0, nh, acc);
-                const int n = 16 * nt + (lane & 15);
-                const float bv = (h0 == 0 && n < C) ? w[11][n] : 0.f;
-#pragma unroll
-                for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int t = 16 * mt + 4 * (lane >> 4) + i;
-                        if (mt < NMT && t < N && n < C) {
-                            const int ix = gm_idx(t, n, XP);
-                            X[ix] = (acc[mt][i] + bv) * sew[t] + X[ix];
-                        }
-                    }
-            }
+            gm_gemm_mt<NMT, NTW, false>(H, HP, h0, W2, NT, wave, ntw, h0, nh, acc2, nullptr, nullptr, mr, rr);
             __syncthreads();
         }
+        // X = (Y + b2) * ew + X (:305, the explanation weight on the branch output)
+#pragma unroll
+        for (int i = 0; i < NTW; ++i) {
+            const int nt = wave + 4 * i;
+            if (nt >= NT) break;
+            const int n = 16 * nt + (lane & 15);
+            const float bv = n < C ? w[11][n] : 0.f;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int t = 16 * mt + 4 * (lane >> 4) + e;
+                    if (mt < NMT && t < N && n < C) {
+                        const int ix = gm_idx(t, n, XP);
+                        X[ix] = (acc2[i][mt][e] + bv) * sew[t] + X[ix];
+                    }
+                }
+        }
+        __syncthreads();
     }
     // ---- masked mean over the tokens (:176-178) and the neighbour-feature mean (:181-189)
     for (int c = tid; c < C; c += blockDim.x) {
@@ -331,9 +410,9 @@ __global__ void gm_pack_kernel(const float *__restrict__ w, int32_t n_out, int32
 using namespace tmk;
 
 static inline size_t gm_lds_bytes(int32_t C, int32_t T) {
-    const size_t XP = gm_r16(C) + 4, K0P = gm_r16(C + T) + 4, HP = GM_HCH + 4;
-    const size_t ulen = std::max(GM_MT * K0P, GM_MT * (XP + HP));
-    return sizeof(float) * (GM_MT * XP + ulen + 2 * GM_MT);
+    const size_t C16 = gm_r16(C), XP = C16 + 4, KG = gm_r16(C + T) / 16, K0P = 16 * ((KG + 1) / 2) + 4, HP = GM_HCH + 4;
+    const size_t ulen = std::max(std::max(GM_MT * K0P, GM_MT * HP), 2 * C16);
+    return sizeof(float) * (GM_MT * XP + ulen + 2 * GM_MT + 2 * C16 + 2 * GM_MT);
 }
 
 extern "C" int64_t tm_gm_packed_floats(int32_t n_out, int32_t k) {
@@ -375,13 +454,17 @@ extern "C" int tm_gm_embed(const tm_gm_embed_args *p, void *stream) {
     const size_t lds = gm_lds_bytes(q.C, q.T);
     if (lds > 160 * 1024) return fail(TM_E_UNSUPPORTED, "tm_gm_embed: edge + time dims too large for LDS");
     hipEvent_t pe = prof_begin((hipStream_t)stream);
-    if (q.N > 16) {
-        TM_HIP(hipFuncSetAttribute((const void *)gm_embed_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        gm_embed_kernel<2><<<q.R, 256, lds, (hipStream_t)stream>>>(a);
-    } else {
-        TM_HIP(hipFuncSetAttribute((const void *)gm_embed_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        gm_embed_kernel<1><<<q.R, 256, lds, (hipStream_t)stream>>>(a);
-    }
+    // output tiles per wave in the channel FFN's second GEMM (accumulated across the hidden chunks)
+    const bool t3 = gm_r16(q.C) / 16 <= 12;
+    auto launch = [&](auto kern) -> int {
+        TM_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        kern<<<q.R, 256, lds, (hipStream_t)stream>>>(a);
+        return TM_OK;
+    };
+    int rc;
+    if (q.N > 16) rc = t3 ? launch(gm_embed_kernel<2, 3>) : launch(gm_embed_kernel<2, 4>);
+    else rc = t3 ? launch(gm_embed_kernel<1, 3>) : launch(gm_embed_kernel<1, 4>);
+    if (rc != TM_OK) return rc;
     TM_CHECK_LAUNCH();
     prof_end("gm_embed_kernel", (hipStream_t)stream, pe);
     return TM_OK;

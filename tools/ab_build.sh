@@ -1,7 +1,7 @@
 #!/bin/bash
 # tools/ab_build.sh <name> <encoder.hip>: build tempme_amd/lib/ab/<name>.so from the current sources
 # with encoder.hip replaced by the given file (A/B timing of walk_kernel variants on one box);
-# SAMPLER=<file> / TRAIN=<file> replace sampler.hip / encoder_train.hip the same way.
+# SAMPLER=<file> / TRAIN=<file> / GM=<file> replace sampler.hip / encoder_train.hip / graphmixer.hip the same way.
 set -e
 cd "$(dirname "$0")/.."
 name=$1; enc=$2
@@ -10,6 +10,7 @@ cp tempme_amd/csrc/*.h tempme_amd/csrc/*.cpp tempme_amd/csrc/*.hip "$out/"
 cp "$enc" "$out/encoder.hip"
 [ -n "$SAMPLER" ] && cp "$SAMPLER" "$out/sampler.hip"
 [ -n "$TRAIN" ] && cp "$TRAIN" "$out/encoder_train.hip"
+[ -n "$GM" ] && cp "$GM" "$out/graphmixer.hip"
 F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -mcode-object-version=5 -Wno-unused-result -Iinclude $EXTRA"
 for s in $(cd "$out" && ls *.cpp *.hip); do /opt/rocm/bin/hipcc $F -x hip -c "$out/$s" -o "$out/$s.o" & done
 wait
