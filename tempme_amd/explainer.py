@@ -100,6 +100,59 @@ def _to(x, device, dtype):
     return torch.from_numpy(np.ascontiguousarray(x)).to(device=device, dtype=dtype)
 
 
+_NP = {torch.int32: np.int32, torch.float32: np.float32, torch.float64: np.float64}
+
+
+class _Stager:
+    """Host arrays of one drop-in call -> device tensors in ONE host->device copy: each array is cast on
+    the host (numpy's float->int truncation and float64->float32 rounding are torch's) into a pinned
+    buffer, the buffer is copied asynchronously into a fresh caching-allocator block, and the results
+    are views of it.  The reference's loop hands every call float64 numpy arrays; one pageable copy and
+    one cast kernel per array (six per forward, six per retrieve_edge_imp_node) dominated a batch.
+    Pinned buffers rotate over ``slots``; a slot is rewritten only after its previous copy finished."""
+
+    def __init__(self, slots=4):
+        self.slots = [None] * slots
+        self.i = 0
+
+    def __call__(self, device, items):
+        shapes = [np.shape(a) for a, _ in items]
+        nbytes = [int(np.prod(s, dtype=np.int64)) * torch.empty(0, dtype=d).element_size() for s, (_, d) in
+                  zip(shapes, items)]
+        offs, tot = [], 0
+        for n in nbytes:
+            offs.append(tot)
+            tot += (n + 15) & ~15
+        k = self.i
+        self.i = (self.i + 1) % len(self.slots)
+        slot = self.slots[k]
+        if slot is None or slot[0].numel() < tot:
+            slot = [torch.empty(max(tot, 1 << 16) * 2, dtype=torch.uint8, pin_memory=True), None]
+            self.slots[k] = slot
+        elif slot[1] is not None:
+            slot[1].synchronize()
+        host = slot[0].numpy()
+        for (a, d), s, o, n in zip(items, shapes, offs, nbytes):
+            np.copyto(host[o:o + n].view(_NP[d]).reshape(s), a, casting="unsafe")
+        dev = torch.empty(max(tot, 1), dtype=torch.uint8, device=device)
+        dev.copy_(slot[0][:max(tot, 1)], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        slot[1] = ev
+        return [dev[o:o + n].view(d).view(s) for (_, d), s, o, n in zip(items, shapes, offs, nbytes)]
+
+
+_STAGE = _Stager()
+
+
+def _to_many(device, *items):
+    """[_to(a, device, dtype) for (a, dtype) in items], staged through one pinned copy when every
+    array is a host numpy array and the device is a GPU."""
+    if device.type == "cuda" and all(isinstance(a, np.ndarray) and d in _NP for a, d in items):
+        return _STAGE(device, items)
+    return [_to(a, device, d).contiguous() for a, d in items]
+
+
 class TempME(nn.Module):
     def __init__(self, base, base_model_type, data, out_dim, hid_dim, prior="empirical", temp=0.07,
                  if_cat_feature=True, dropout_p=0.1, device=None, use_temporal_guidance=True,
@@ -448,11 +501,10 @@ class TempME(nn.Module):
         if etab is not None and isinstance(edge_idx, np.ndarray) and edge_idx.size and \
                 (edge_idx.max() >= etab.shape[0] or edge_idx.min() < 0):
             raise IndexError("index out of range in self")     # what the reference's embedding lookup raises
-        out = self.encoder_fwd(_to(node_idx, dev, torch.int32).contiguous(), _to(edge_idx, dev, torch.int32).contiguous(),
-                               _to(time_idx, dev, torch.float32).contiguous(),
-                               _to(cat_feat, dev, torch.int32).reshape(B, W).contiguous(),
-                               _to(cut_time_l, dev, torch.float64).contiguous(),
-                               _to(edge_identify, dev, torch.float32).contiguous(), 1, B, W, etab=etab)
+        n6, e3, t3, ct, cu, ei = _to_many(dev, (node_idx, torch.int32), (edge_idx, torch.int32), (time_idx, torch.float32),
+                                          (cat_feat, torch.int32), (cut_time_l, torch.float64),
+                                          (edge_identify, torch.float32))
+        out = self.encoder_fwd(n6, e3, t3, ct.reshape(B, W), cu, ei, 1, B, W, etab=etab)
         return out[:B * W].view(B, W, 1)
 
     def retrieve_edge_imp_node(self, subgraph, graphlet_imp, walks, training=True):
@@ -472,13 +524,11 @@ class TempME(nn.Module):
             return e0.view(B, N), e1.view(B, N * N)
         B, N = np.shape(node_record[0])[0], np.shape(node_record[0])[1]
         W = np.shape(walks[1])[1]
-        o1, o2 = self.edge_importance(_to(walks[1], dev, torch.int32).contiguous(),
-                                      _to(walks[2], dev, torch.float32).contiguous(),
-                                      graphlet_imp.detach().to(dev, torch.float32).contiguous(),
-                                      _to(node_record[0], dev, torch.int32).contiguous(),
-                                      _to(eidx_record[0], dev, torch.int32).contiguous(),
-                                      _to(node_record[1], dev, torch.int32).contiguous(),
-                                      _to(eidx_record[1], dev, torch.int32).contiguous(), 1, B, W, N)
+        e3, t3, n1, x1, n2, x2 = _to_many(dev, (walks[1], torch.int32), (walks[2], torch.float32),
+                                          (node_record[0], torch.int32), (eidx_record[0], torch.int32),
+                                          (node_record[1], torch.int32), (eidx_record[1], torch.int32))
+        o1, o2 = self.edge_importance(e3, t3, graphlet_imp.detach().to(dev, torch.float32).contiguous(), n1, x1, n2, x2,
+                                      1, B, W, N)
         return o1[:B * N].view(B, N), o2[:B * N * N].view(B, N * N)
 
     def retrieve_explanation(self, subgraph_src, graphlet_imp_src, walks_src, subgraph_tgt, graphlet_imp_tgt,
