@@ -117,8 +117,7 @@ class _Stager:
 
     def __call__(self, device, items):
         shapes = [np.shape(a) for a, _ in items]
-        nbytes = [int(np.prod(s, dtype=np.int64)) * torch.empty(0, dtype=d).element_size() for s, (_, d) in
-                  zip(shapes, items)]
+        nbytes = [int(np.prod(s, dtype=np.int64)) * np.dtype(_NP[d]).itemsize for s, (_, d) in zip(shapes, items)]
         offs, tot = [], 0
         for n in nbytes:
             offs.append(tot)
@@ -237,7 +236,25 @@ class TempME(nn.Module):
             self._warned_torch_train = True
         return ok
 
+    def __setattr__(self, name, value):
+        if isinstance(value, (nn.Module, nn.Parameter)):
+            self.__dict__["_wl_cache"] = None          # a replaced submodule / parameter: rebuild the list
+        super().__setattr__(name, value)
+
+    def _apply(self, fn, *args, **kwargs):
+        self.__dict__["_wl_cache"] = None
+        return super()._apply(fn, *args, **kwargs)
+
     def _weight_list(self):
+        """The encoder's parameters in pack order.  Cached: walking the submodules through
+        nn.Module.__getattr__ cost ~35 us per call, several calls per drop-in forward; the cache is
+        dropped when a submodule or parameter of the explainer is reassigned or the module is moved."""
+        wl = self.__dict__.get("_wl_cache")
+        if wl is None:
+            wl = self.__dict__["_wl_cache"] = self._build_weight_list()
+        return wl
+
+    def _build_weight_list(self):
         at, ec, m = self.attention, self.event_conv, self.MLP
         # TemporalAwareAttention.MLP = (Linear, ReLU, Dropout, Linear), Attention.MLP = (Linear, ReLU, Linear)
         am = (at.MLP[0], at.MLP[3]) if isinstance(at, TemporalAwareAttention) else (at.MLP[0], at.MLP[2])

@@ -141,9 +141,21 @@ def load_subgraph_margin(args, file):
     return (*subs, *walks, file["dst_fake"][:])
 
 
+def _as_slice(batch_id, n):
+    """A contiguous ascending index array (the eval loop's np.arange(s, e)) as the equivalent slice: the
+    rows come back as views instead of fancy-indexing copies (same values; the callers only read them).
+    Out-of-range ids keep the array, so fancy indexing raises the reference's IndexError."""
+    if isinstance(batch_id, np.ndarray) and batch_id.ndim == 1 and batch_id.size > 1 and \
+            np.issubdtype(batch_id.dtype, np.integer) and batch_id[0] >= 0 and batch_id[-1] < n and \
+            int(batch_id[-1]) - int(batch_id[0]) + 1 == batch_id.size and bool((np.diff(batch_id) == 1).all()):
+        return slice(int(batch_id[0]), int(batch_id[-1]) + 1)
+    return batch_id
+
+
 def get_item(input_pack, batch_id):
     """utils/batch_loader.py:200-235."""
     *subs, ws, wt, wb, dst_fake = input_pack
+    batch_id = _as_slice(batch_id, len(dst_fake))
     out = []
     for node_records, eidx_records, t_records in subs:
         out.append(([i[batch_id] for i in node_records], [i[batch_id] for i in eidx_records],
@@ -156,7 +168,7 @@ def get_item(input_pack, batch_id):
 
 def get_item_edge(edge_features, batch_id):
     """utils/batch_loader.py:238-242: [3, n, W, 3, 3] -> (src_edge, tgt_edge, bgd_edge)."""
-    e = edge_features[:, batch_id, :, :, :]
+    e = edge_features[:, _as_slice(batch_id, np.shape(edge_features)[1]), :, :, :]
     return e[0], e[1], e[2]
 
 
