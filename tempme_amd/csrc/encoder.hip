@@ -11,7 +11,8 @@
 //   std_kernel      per group: unbiased std of |cut - t| over the [B,W,2] walk times (f64 accumulate)
 //   gcn_kernel      per 32 walk-positions: [E(e)|cnt|cos(dt*w+phi)] -> lin_event -> (A,B) -> MLP -> F rows
 //   head_kernel     per 32 walks: W1/W2 attention with temporal scaling, softmax, MLP, one-hot, MLP, sigmoid
-//   explain_kernel  per (group, event): dependency-gate MLP, LDS hash scatter-max over walk edge ids,
+//   gate_pos_kernel per 32 walk positions of the call: dependency-gate MLP -> walk_imp
+//   explain_hash_kernel  per (group, event): LDS hash scatter-max of walk_imp over the walk edge ids,
 //                   gather at subgraph edge ids, Beta mean, node==0 mask
 // Every dense projection runs on MFMA with the packed weight stream read from L2 and the
 // activations staged in LDS (row stride K16+8 floats: conflict-free ds_read_b128).
@@ -284,80 +285,98 @@ __global__ void __launch_bounds__(256) head_kernel(EncW P, int64_t n_walks, int6
 // ------------------------------------------------------------------ edge importance: one block per (group, event)
 __device__ __forceinline__ uint32_t hash_eid(int32_t e) { return (uint32_t)e * 0x9E3779B1u; }
 
-__global__ void __launch_bounds__(256) explain_kernel(EncW P, int32_t W, int32_t N, int32_t hbits,
-                                                      const float *__restrict__ e_feat, const int32_t *__restrict__ eid3,
-                                                      const float *__restrict__ ts3, const float *__restrict__ imp,
-                                                      const int32_t *__restrict__ sub1_node,
-                                                      const int32_t *__restrict__ sub1_eid,
-                                                      const int32_t *__restrict__ sub2_node,
-                                                      const int32_t *__restrict__ sub2_eid, float *__restrict__ out1,
-                                                      float *__restrict__ out2) {
+// Per walk position, 32 flattened (group, event, position) rows per workgroup: the dependency gate
+// (:367-386) on MFMA from LDS tiles and walk_imp = graphlet_imp * (0.5 + 0.5 * gate) (:364, :386).  A
+// launch covers every position of the call, so a single reference batch (3 W x B positions) still fills
+// the chip; the per-(group, event) scatter-max and gather follow in explain_hash_kernel.
+__global__ void __launch_bounds__(256) gate_pos_kernel(EncW P, int64_t n_rows, int32_t W,
+                                                       const float *__restrict__ e_feat,
+                                                       const int32_t *__restrict__ eid3, const float *__restrict__ ts3,
+                                                       const float *__restrict__ imp, float *__restrict__ wv) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int de = P.de, kdep = P.kdep, kd16 = r16(kdep), ldx = kd16 + 8, ldg = HID + 8,
-              ldg2 = HID / 2 + 8;
-    const int hsize = 1 << hbits;
+    const int de = P.de, kdep = P.kdep, kd16 = r16(kdep), ldx = kd16 + 8, ldg = HID + 8, ldg2 = HID / 2 + 8;
     float *X = smem;                       // [32][ldx]
     float *G1 = X + TILE_ROWS * ldx;       // [32][ldg]
     float *G2 = G1 + TILE_ROWS * ldg;      // [32][ldg2]
-    int32_t *hkey = reinterpret_cast<int32_t *>(G2 + TILE_ROWS * ldg2);   // [hsize]
-    uint32_t *hval = reinterpret_cast<uint32_t *>(hkey + hsize);         // [hsize] float bits
     __shared__ int32_t s_eid[TILE_ROWS];
     __shared__ float s_t[TILE_ROWS];
-    const int64_t ge = blockIdx.x;         // (group, event) row
+    const int tid = threadIdx.x;
+    const int64_t c0 = (int64_t)blockIdx.x * TILE_ROWS;
+    const int64_t W3 = 3 * (int64_t)W;
+    if (!P.dep) {                          // no dependency gate (tm_weights_variant): walk_imp = graphlet_imp
+        if (tid < TILE_ROWS && c0 + tid < n_rows) {
+            const int64_t r = c0 + tid;
+            wv[r] = imp[(r / W3) * W + (r % W3) / 3];
+        }
+        return;
+    }
+    if (tid < TILE_ROWS) {
+        const int64_t r = c0 + tid;
+        s_eid[tid] = r < n_rows ? eid3[r] : 0;
+        s_t[tid] = r < n_rows ? ts3[r] : 0.f;   // raw event time (:371), not dt
+    }
+    __syncthreads();
+    for (int i = tid; i < TILE_ROWS * kd16; i += blockDim.x) {
+        const int r = i / kd16, c = i % kd16;
+        float v = 0.f;
+        if (c0 + r < n_rows) {
+            if (c < de) v = e_feat[(int64_t)s_eid[r] * de + c];
+            else if (c < kdep) v = time_cos(s_t[r], P.freq[c - de], P.phase[c - de]);
+        }
+        X[r * ldx + c] = v;
+    }
+    __syncthreads();
+    gemm<2>(X, ldx, P.d1, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) G1[erow(mt, r) * ldg + c] = relu(acc[r] + P.d1.b[c]);
+    });
+    __syncthreads();
+    gemm<2>(G1, ldg, P.d2, [&](int mt, int nt, floatx4 acc) {
+        const int c = ecol(nt);
+        for (int r = 0; r < 4; ++r) G2[erow(mt, r) * ldg2 + c] = relu(acc[r] + P.d2.b[c]);
+    });
+    __syncthreads();
+    const int r = tid >> 3, sub = tid & 7;
+    const float sc = gate_logit_lds(G2 + r * ldg2, P.d3w, sub);
+    const int64_t gr = c0 + r;
+    if (sub == 0 && gr < n_rows) {
+        const float gate = 1.f / (1.f + expf(-(sc + P.d3b[0])));
+        wv[gr] = imp[(gr / W3) * W + (gr % W3) / 3] * (0.5f + 0.5f * gate);
+    }
+}
+
+// One workgroup per (group, event): scatter-max of the 3 W walk_imp values onto their edge ids (LDS
+// open-addressing table; atomicMax on the float bits, values >= 0), then the gather at the subgraph's
+// hop-1 / hop-2 edge ids, the Beta mean (eval) and the padding mask (:388-406, :420-430).
+__global__ void __launch_bounds__(256) explain_hash_kernel(int32_t W, int32_t N, int32_t hbits,
+                                                           const int32_t *__restrict__ eid3,
+                                                           const float *__restrict__ wv,
+                                                           const int32_t *__restrict__ sub1_node,
+                                                           const int32_t *__restrict__ sub1_eid,
+                                                           const int32_t *__restrict__ sub2_node,
+                                                           const int32_t *__restrict__ sub2_eid,
+                                                           float *__restrict__ out1, float *__restrict__ out2) {
+    extern __shared__ __attribute__((aligned(16))) int32_t hsm[];
+    const int hsize = 1 << hbits;
+    int32_t *hkey = hsm;
+    uint32_t *hval = reinterpret_cast<uint32_t *>(hkey + hsize);
+    const int64_t ge = blockIdx.x;
     const int tid = threadIdx.x, nrow = 3 * W;
-    const int32_t *e3 = eid3 + ge * (int64_t)W * 3;
-    const float *t3 = ts3 + ge * (int64_t)W * 3;
     for (int i = tid; i < hsize; i += blockDim.x) {
         hkey[i] = -1;
         hval[i] = 0u;
     }
-    for (int c0 = 0; c0 < nrow; c0 += TILE_ROWS) {
-        __syncthreads();
-        if (tid < TILE_ROWS) {
-            const int r = c0 + tid;
-            s_eid[tid] = r < nrow ? e3[r] : 0;
-            s_t[tid] = r < nrow ? t3[r] : 0.f;   // raw event time (:371), not dt
+    __syncthreads();
+    for (int i = tid; i < nrow; i += blockDim.x) {
+        const int32_t key = eid3[ge * nrow + i];
+        const float v = wv[ge * nrow + i];
+        uint32_t h = hash_eid(key) >> (32 - hbits);
+        while (true) {
+            const int32_t prev = atomicCAS(&hkey[h], -1, key);
+            if (prev == -1 || prev == key) break;
+            h = (h + 1) & (hsize - 1);
         }
-        __syncthreads();
-        for (int i = tid; i < TILE_ROWS * kd16; i += blockDim.x) {
-            const int r = i / kd16, c = i % kd16;
-            float v = 0.f;
-            if (c0 + r < nrow) {
-                if (c < de) v = e_feat[(int64_t)s_eid[r] * de + c];
-                else if (c < kdep) v = time_cos(s_t[r], P.freq[c - de], P.phase[c - de]);
-            }
-            X[r * ldx + c] = v;
-        }
-        __syncthreads();
-        gemm<2>(X, ldx, P.d1, [&](int mt, int nt, floatx4 acc) {
-            const int c = ecol(nt);
-            for (int r = 0; r < 4; ++r) G1[erow(mt, r) * ldg + c] = relu(acc[r] + P.d1.b[c]);
-        });
-        __syncthreads();
-        gemm<2>(G1, ldg, P.d2, [&](int mt, int nt, floatx4 acc) {
-            const int c = ecol(nt);
-            for (int r = 0; r < 4; ++r) G2[erow(mt, r) * ldg2 + c] = relu(acc[r] + P.d2.b[c]);
-        });
-        __syncthreads();
-        {
-            const int r = tid >> 3, sub = tid & 7;
-            const float s = gate_logit_lds(G2 + r * ldg2, P.d3w, sub);
-            const int gr = c0 + r;
-            if (sub == 0 && gr < nrow) {
-                const float z = s + P.d3b[0];
-                const float gate = 1.f / (1.f + expf(-z));
-                // walk_imp = graphlet_imp (repeated over 3 positions) * (0.5 + 0.5 * gate)   (:364, :386)
-                const float v = P.dep ? imp[ge * W + gr / 3] * (0.5f + 0.5f * gate) : imp[ge * W + gr / 3];
-                const int32_t key = s_eid[r];
-                uint32_t h = hash_eid(key) >> (32 - hbits);
-                while (true) {
-                    const int32_t prev = atomicCAS(&hkey[h], -1, key);
-                    if (prev == -1 || prev == key) break;
-                    h = (h + 1) & (hsize - 1);
-                }
-                atomicMax(&hval[h], __float_as_uint(v));   // v >= 0: uint order == float order
-            }
-        }
+        atomicMax(&hval[h], __float_as_uint(v));   // v >= 0: uint order == float order
     }
     __syncthreads();
     // gather at the subgraph edge ids, Beta mean (eval), padding mask
@@ -1460,12 +1479,18 @@ extern "C" int tm_edge_importance(const tm_weights *w, const float *e_feat, int3
     while ((1 << hbits) < 2 * 3 * W) ++hbits;
     if (hbits > 14) return fail(TM_E_UNSUPPORTED, "tm_edge_importance: too many walks per event");
     const EncW &P = w->P;
-    const size_t lds = sizeof(float) * (TILE_ROWS * (r16(P.kdep) + 8) + TILE_ROWS * (HID + 8) + TILE_ROWS * (HID / 2 + 8)) +
-                       2 * sizeof(int32_t) * (1u << hbits);
+    const size_t lds = sizeof(float) * (TILE_ROWS * (r16(P.kdep) + 8) + TILE_ROWS * (HID + 8) + TILE_ROWS * (HID / 2 + 8));
+    const size_t hlds = 2 * sizeof(int32_t) * (1u << hbits);
     if (lds > 160 * 1024) return fail(TM_E_UNSUPPORTED, "tm_edge_importance: LDS budget exceeded");
+    const int64_t n_pos = rows * 3 * W;
+    float *wv = static_cast<float *>(scratch(sizeof(float) * (size_t)n_pos, S_(stream)));
+    if (!wv) return fail(TM_E_HIP, "tm_edge_importance: scratch allocation failed");
     hipEvent_t pe = prof_begin(S_(stream));
-    explain_kernel<<<dim3((unsigned)rows), 256, lds, S_(stream)>>>(P, W, N, hbits, e_feat, eid3, ts3, imp, sub1_node,
-                                                                  sub1_eid, sub2_node, sub2_eid, out_h1, out_h2);
+    gate_pos_kernel<<<dim3((unsigned)((n_pos + TILE_ROWS - 1) / TILE_ROWS)), 256, lds, S_(stream)>>>(P, n_pos, W, e_feat,
+                                                                                                   eid3, ts3, imp, wv);
+    TM_CHECK_LAUNCH();
+    explain_hash_kernel<<<dim3((unsigned)rows), 256, hlds, S_(stream)>>>(W, N, hbits, eid3, wv, sub1_node, sub1_eid,
+                                                                        sub2_node, sub2_eid, out_h1, out_h2);
     TM_CHECK_LAUNCH();
     prof_end("explain_kernel", S_(stream), pe);
     return TM_OK;
