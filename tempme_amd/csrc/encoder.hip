@@ -712,6 +712,14 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, const float *
     floatx4 L[NTD];
 #pragma unroll
     for (int t = 0; t < NTD; ++t) L[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // the source node's feature rows requested before lin_event, consumed in its epilogue (their wait
+    // overlaps the K loop: -0.8 %; the target's too would need 256 VGPRs and spill).  Ablation: both
+    // rows' gathers cost 17 % of the kernel (all columns reading one row: 12.07 -> 10.01 ms)
+#pragma unroll
+    for (int t = 0; t < NTD; ++t) {
+        const int f4 = (t < NTD - 1) ? 4 * t + g : min(4 * t + g, dn / 4 - 1);
+        xs[t] = nrow_s[f4];
+    }
     TM_STAMP(1);
     {
         const auto wr = wrsrc(P.ev.w);
@@ -773,7 +781,6 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, const float *
         // tiles below the last are inside the row (dispatch: 160 < dn <= 176), so their offsets are
         // immediates on one row address; the last tile's index is clamped and masked below
         const int f4 = (t < NTD - 1) ? 4 * t + g : min(4 * t + g, dn / 4 - 1);
-        xs[t] = nrow_s[f4];
         xt[t] = nrow_t[f4];
         const float sv[4] = {xs[t].x, xs[t].y, xs[t].z, xs[t].w}, tv[4] = {xt[t].x, xt[t].y, xt[t].z, xt[t].w};
 #pragma unroll
