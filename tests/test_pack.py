@@ -104,3 +104,30 @@ def test_pack_errors(tmp_path):
             P.DevicePack(f, edge[:, :3], 20, torch.device("cpu"))
         with pytest.raises(AssertionError):
             P.DevicePack(f, edge, 7, torch.device("cpu"))
+
+
+def test_get_item_slice_path_matches_fancy_indexing(tmp_path):
+    """get_item / get_item_edge index a contiguous np.arange batch by a slice (views, no copies); the
+    values must equal fancy indexing with the same ids, and ids past the pack still raise IndexError
+    as the reference's fancy indexing does (utils/batch_loader.py:200-242)."""
+    _, _, cat, edge = _golden_pack()
+    p_cat = P.write_pack(str(tmp_path / "s_cat.h5"), cat, P.CAT_KEYS)
+    with P.open_pack(p_cat) as f:
+        pk = P.load_subgraph_margin(types.SimpleNamespace(n_degree=20), f)
+    bid = np.arange(7, 19)
+    fast, ref = P.get_item(pk, bid), P.get_item(pk, list(bid))
+    for a, b in zip(fast[:3], ref[:3]):          # subgraphs: (node, eidx, ts) lists per hop
+        for x, y in zip(a, b):
+            for u, v in zip(x, y):
+                assert np.array_equal(u, v)
+    for a, b in zip(fast[3:6], ref[3:6]):        # walks
+        for u, v in zip(a, b):
+            assert u.dtype == v.dtype and np.array_equal(u, v)
+    assert np.array_equal(fast[6], ref[6])
+    for u, v in zip(P.get_item_edge(edge, bid), P.get_item_edge(edge, list(bid))):
+        assert np.array_equal(u, v)
+    n = len(pk[-1])
+    with pytest.raises(IndexError):
+        P.get_item(pk, np.arange(n - 2, n + 2))
+    with pytest.raises(IndexError):
+        P.get_item_edge(edge, np.arange(n - 2, n + 2))
