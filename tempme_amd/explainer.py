@@ -15,6 +15,7 @@ gradients) run the HIP forward/backward kernels through autograd Functions
 (tm_encoder_train_fwd / tm_encoder_bwd / tm_encoder_wgrad, tm_explain_train_fwd / _bwd,
 tm_kl_loss); only Beta ``rsample`` and the padding mask are torch ops.
 """
+import threading
 import warnings
 
 import numpy as np
@@ -114,8 +115,13 @@ class _Stager:
     def __init__(self, slots=4):
         self.slots = [None] * slots
         self.i = 0
+        self.lock = threading.Lock()   # the slots are shared by every TempME instance of the process
 
     def __call__(self, device, items):
+        with self.lock:
+            return self._stage(device, items)
+
+    def _stage(self, device, items):
         shapes = [np.shape(a) for a, _ in items]
         nbytes = [int(np.prod(s, dtype=np.int64)) * np.dtype(_NP[d]).itemsize for s, (_, d) in zip(shapes, items)]
         offs, tot = [], 0
