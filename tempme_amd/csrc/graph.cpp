@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
+#include <mutex>
 #include <numeric>
 #include <thread>
 #include <vector>
@@ -523,23 +524,34 @@ extern "C" int tm_graph_export(const tm_graph *gc, int64_t *off, int32_t *ngh, i
     if (!gc) return fail(TM_E_ARG, "tm_graph_export: NULL graph");
     tm_graph *g = const_cast<tm_graph *>(gc);
     const int64_t n = g->d.n_entries;
-    if (g->dev_built && !g->h_off) {   // host copies of a device-built graph, made once
-        const int32_t V = g->d.n_nodes;
-        const int64_t nn = std::max<int64_t>(n, 1);
-        std::vector<int32_t> off32(V + 1);
-        g->h_off = new int64_t[V + 1];
-        g->h_ngh = new int32_t[nn];
-        g->h_eid = new int32_t[nn];
-        g->h_dict = new int32_t[nn];
-        g->h_ts = new double[nn];
-        hipError_t e = hipSuccess;
-        e = e ? e : hipMemcpy(off32.data(), g->d_off, sizeof(int32_t) * (V + 1), hipMemcpyDeviceToHost);
-        e = e ? e : hipMemcpy(g->h_ngh, g->d_hngh, sizeof(int32_t) * nn, hipMemcpyDeviceToHost);
-        e = e ? e : hipMemcpy(g->h_eid, g->d_heid, sizeof(int32_t) * nn, hipMemcpyDeviceToHost);
-        e = e ? e : hipMemcpy(g->h_dict, g->d_dict, sizeof(int32_t) * nn, hipMemcpyDeviceToHost);
-        e = e ? e : hipMemcpy(g->h_ts, g->d_tsd, sizeof(double) * nn, hipMemcpyDeviceToHost);
-        for (int32_t u = 0; u <= V; ++u) g->h_off[u] = off32[u];
-        if (e != hipSuccess) return fail(TM_E_HIP, std::string("tm_graph_export: ") + hipGetErrorString(e));
+    if (g->dev_built) {   // host copies of a device-built graph, made once (the first export publishes them)
+        static std::mutex export_mu;
+        std::lock_guard<std::mutex> lock(export_mu);
+        if (!g->h_off) {
+            const int32_t V = g->d.n_nodes;
+            const int64_t nn = std::max<int64_t>(n, 1);
+            std::vector<int32_t> off32(V + 1);
+            std::unique_ptr<int64_t[]> h_off(new int64_t[V + 1]);
+            std::unique_ptr<int32_t[]> h_ngh(new int32_t[nn]), h_eid(new int32_t[nn]), h_dict(new int32_t[nn]);
+            std::unique_ptr<double[]> h_ts(new double[nn]);
+            int prev = 0;
+            if (hipGetDevice(&prev) != hipSuccess) prev = 0;
+            hipError_t e = hipSetDevice(g->device);
+            e = e ? e : hipMemcpy(off32.data(), g->d_off, sizeof(int32_t) * (V + 1), hipMemcpyDeviceToHost);
+            e = e ? e : hipMemcpy(h_ngh.get(), g->d_hngh, sizeof(int32_t) * nn, hipMemcpyDeviceToHost);
+            e = e ? e : hipMemcpy(h_eid.get(), g->d_heid, sizeof(int32_t) * nn, hipMemcpyDeviceToHost);
+            e = e ? e : hipMemcpy(h_dict.get(), g->d_dict, sizeof(int32_t) * nn, hipMemcpyDeviceToHost);
+            e = e ? e : hipMemcpy(h_ts.get(), g->d_tsd, sizeof(double) * nn, hipMemcpyDeviceToHost);
+            (void)hipSetDevice(prev);
+            // nothing is published unless every copy succeeded (a failed export leaves no partial state)
+            if (e != hipSuccess) return fail(TM_E_HIP, std::string("tm_graph_export: ") + hipGetErrorString(e));
+            for (int32_t u = 0; u <= V; ++u) h_off[u] = off32[u];
+            g->h_ngh = h_ngh.release();
+            g->h_eid = h_eid.release();
+            g->h_dict = h_dict.release();
+            g->h_ts = h_ts.release();
+            g->h_off = h_off.release();
+        }
     }
     if (off) std::copy(g->h_off, g->h_off + g->d.n_nodes + 1, off);
     if (ngh) std::copy(g->h_ngh, g->h_ngh + n, ngh);

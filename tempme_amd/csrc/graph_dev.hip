@@ -275,6 +275,9 @@ using namespace tmk::gdev;
 // 0: built; 1: rows need the host builder (an edge id on several rows); < 0: error
 int tm_graph_build_edges_device(int32_t V, int64_t n_edges, const int64_t *src, const int64_t *dst, const int64_t *eidx,
                                 const double *ts, int device, tm_graph **out) {
+    // an empty edge set: nothing to sort or scan on the device (zero-size grids, no last block element
+    // to read back); the host builder makes the empty graph
+    if (n_edges <= 0) return 1;
     int32_t max_eid = 0;
     for (int64_t i = 0; i < n_edges; ++i) max_eid = (int32_t)std::max<int64_t>(max_eid, std::min<int64_t>(eidx[i], INT32_MAX));
     const int64_t n = 2 * n_edges, nn = std::max<int64_t>(n, 1);

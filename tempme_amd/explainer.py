@@ -139,10 +139,13 @@ class _Stager:
         host = slot[0].numpy()
         for (a, d), s, o, n in zip(items, shapes, offs, nbytes):
             np.copyto(host[o:o + n].view(_NP[d]).reshape(s), a, casting="unsafe")
-        dev = torch.empty(max(tot, 1), dtype=torch.uint8, device=device)
-        dev.copy_(slot[0][:max(tot, 1)], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
+        # the copy and its event on the current stream of `device` (not of the process's current device),
+        # so the slot's next reuse waits for this very copy
+        with torch.cuda.device(device):
+            dev = torch.empty(max(tot, 1), dtype=torch.uint8, device=device)
+            dev.copy_(slot[0][:max(tot, 1)], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(device))
         slot[1] = ev
         return [dev[o:o + n].view(d).view(s) for (_, d), s, o, n in zip(items, shapes, offs, nbytes)]
 
@@ -242,44 +245,60 @@ class TempME(nn.Module):
             self._warned_torch_train = True
         return ok
 
-    def __setattr__(self, name, value):
-        if isinstance(value, (nn.Module, nn.Parameter)):
-            self.__dict__["_wl_cache"] = None          # a replaced submodule / parameter: rebuild the list
-        super().__setattr__(name, value)
-
-    def _apply(self, fn, *args, **kwargs):
-        self.__dict__["_wl_cache"] = None
-        return super()._apply(fn, *args, **kwargs)
-
     def _weight_list(self):
         """The encoder's parameters in pack order.  Cached: walking the submodules through
-        nn.Module.__getattr__ cost ~35 us per call, several calls per drop-in forward; the cache is
-        dropped when a submodule or parameter of the explainer is reassigned or the module is moved."""
-        wl = self.__dict__.get("_wl_cache")
-        if wl is None:
-            wl = self.__dict__["_wl_cache"] = self._build_weight_list()
+        nn.Module.__getattr__ cost ~35 us per call, several calls per drop-in forward.  The cache holds,
+        beside the list, every (module dict, key, object) link from the explainer down to each listed
+        parameter; it is reused only while every link still holds the same object, so reassigning a
+        submodule at any depth (``ex.MLP[0] = nn.Linear(...)``), a parameter (``lin.weight =
+        nn.Parameter(...)``, ``load_state_dict(..., assign=True)``) or moving the module rebuilds it."""
+        c = self.__dict__.get("_wl_cache")
+        if c is not None:
+            wl, links = c
+            if all(d.get(k) is v for d, k, v in links):
+                return wl
+        wl, links = self._build_weight_list()
+        self.__dict__["_wl_cache"] = (wl, links)
         return wl
 
-    def _build_weight_list(self):
-        at, ec, m = self.attention, self.event_conv, self.MLP
+    def _weight_paths(self):
         # TemporalAwareAttention.MLP = (Linear, ReLU, Dropout, Linear), Attention.MLP = (Linear, ReLU, Linear)
-        am = (at.MLP[0], at.MLP[3]) if isinstance(at, TemporalAwareAttention) else (at.MLP[0], at.MLP[2])
-        mods = [ec.lin_event, ec.MLP[0], ec.MLP[2], at.W1, at.W2, am[0], am[1], m[0], m[3], m[5]]
-        ts = []
-        for mod in mods:
-            ts += [mod.weight, mod.bias]
+        a_last = "3" if isinstance(self.attention, TemporalAwareAttention) else "2"
+        paths = [("event_conv", "lin_event"), ("event_conv", "MLP", "0"), ("event_conv", "MLP", "2"),
+                 ("attention", "W1"), ("attention", "W2"), ("attention", "MLP", "0"), ("attention", "MLP", a_last),
+                 ("MLP", "0"), ("MLP", "3"), ("MLP", "5")]
         if self.use_dependency_aware_sampling:
-            d = self.edge_dependency_gcn
-            for mod in (d[0], d[3], d[6]):
-                ts += [mod.weight, mod.bias]
-        else:
+            paths += [("edge_dependency_gcn", "0"), ("edge_dependency_gcn", "3"), ("edge_dependency_gcn", "6")]
+        return paths
+
+    def _build_weight_list(self):
+        links, ts = [], []
+
+        def param(mod, name):
+            p = mod._parameters[name]
+            links.append((mod._parameters, name, p))
+            return p
+
+        for path in self._weight_paths():
+            mod = self
+            for k in path:
+                child = mod._modules[k]
+                links.append((mod._modules, k, child))
+                mod = child
+            ts += [param(mod, "weight"), param(mod, "bias")]
+        if not self.use_dependency_aware_sampling:
             # no gate (tm_weights_variant(dep = 0)): shape-correct zeros keep the pack layout
             h = self.hid_dim
-            if getattr(self, "_zero_gate", None) is None:
-                z = lambda *sh: torch.zeros(*sh, device=self.node_raw_embed.weight.device)  # noqa: E731
+            dev = self.node_raw_embed.weight.device
+            zg = getattr(self, "_zero_gate", None)
+            if zg is None or zg[0].device != dev:
+                z = lambda *sh: torch.zeros(*sh, device=dev)  # noqa: E731
                 self._zero_gate = [z(h, self.edge_dim + self.time_dim), z(h), z(h // 2, h), z(h // 2), z(1, h // 2), z(1)]
             ts += self._zero_gate
-        return ts + [self.time_encoder.basis_freq, self.time_encoder.phase]
+        te = self._modules["time_encoder"]
+        links.append((self._modules, "time_encoder", te))
+        ts += [param(te, "basis_freq"), param(te, "phase")]
+        return ts, links
 
     def packed_weights(self, force=False):
         """tm_weights handle, re-packed whenever a parameter changed (version counters) or when forced

@@ -34,6 +34,14 @@ def _ties(n_nodes, n_edges, n_ts, seed, loops=0.05):
     return src, dst, np.arange(1, n_edges + 1), ts, n_nodes
 
 
+def _shuffled(n_nodes, n_edges, n_ts, seed):
+    """Rows not in time order (a permutation of a tie-heavy graph): the host builder takes its
+    stable_sort path (not the already-sorted copy), the device its radix sorts; ties keep row order."""
+    src, dst, eidx, ts, V = _ties(n_nodes, n_edges, n_ts, seed)
+    p = np.random.default_rng(seed + 100).permutation(n_edges)
+    return src[p], dst[p], eidx[p], ts[p], V
+
+
 def _enron(n_nodes, n_edges, alpha, seed):
     g = enron_like(n_nodes=n_nodes, n_edges=n_edges, alpha=alpha, de=4, dn=4, seed=seed)
     return g["src"], g["dst"], g["eidx"], g["ts"], g["n_nodes"]
@@ -53,6 +61,8 @@ CASES = {
     "ties_mid": lambda: _ties(300, 20000, 50, 2),
     "enron_hub": lambda: _enron(184, 60000, 1.2, 3),
     "sparse_100k": lambda: _enron(100000, 200000, 1.5, 4),
+    "shuffled_ties": lambda: _shuffled(40, 5000, 12, 6),
+    "shuffled_hub": lambda: _shuffled(8, 20000, 300, 7),
 }
 
 
@@ -79,6 +89,14 @@ def test_device_build_equals_host_build(dev, case):
     for k in ("dst_fake", "sub1_node", "sub1_eid", "sub1_ts", "sub2_node", "sub2_eid", "sub2_ts", "node6", "eid3",
               "ts3", "cat", "cnt", "hist", "err"):
         assert torch.equal(getattr(outs[0], k), getattr(outs[1], k)), k
+
+
+def test_empty_edge_set(dev):
+    """n_edges == 0: the device builder hands over to the host builder (no zero-size device scans)."""
+    z = np.zeros(0, dtype=np.int64)
+    f = tm.NeighborFinder.from_edges(z, z, z, z.astype(np.float64), 5, device=dev, seed=3)
+    off, ngh, eid, ts, dct = f.graph.export()
+    assert off.tolist() == [0] * 6 and len(ngh) == len(eid) == len(ts) == 0
 
 
 def test_repeated_edge_ids_use_the_host_builder(dev):

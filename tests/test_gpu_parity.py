@@ -244,6 +244,37 @@ def test_encoder_matches_reference_goldens(tm, case):
         np.testing.assert_allclose(float(kl), d["kl"][k], rtol=RTOL, atol=ATOL)
 
 
+def test_nested_reassignment_repacks(tm):
+    """The cached weight list follows nested reassignments: a new Linear deep inside a Sequential, a new
+    Parameter on a submodule, and load_state_dict(assign=True) all change the HIP forward's output
+    exactly as they change the torch formulation's."""
+    from tests.encoder_inputs import SIDES, load
+    d = load("uslegis")
+    ex = _explainer(tm, d)
+    x = d[SIDES[0]]
+    w = (x["node"], x["eid"], x["ts"], x["cat"], x["marg"])
+
+    def both():
+        with torch.no_grad():
+            hip = ex(w, d["ts_cut"], x["cnt"]).cpu().numpy()
+            ref = ex._forward_torch(w, d["ts_cut"], x["cnt"]).cpu().numpy()
+        np.testing.assert_allclose(hip, ref, rtol=RTOL, atol=ATOL)
+        return hip
+
+    base = both()
+    torch.manual_seed(11)
+    ex.MLP[0] = torch.nn.Linear(ex.mlp_dim, ex.mlp_dim).to(ex.device)
+    a = both()
+    assert not np.allclose(a, base)
+    ex.event_conv.lin_event.weight = torch.nn.Parameter(ex.event_conv.lin_event.weight.detach() * 0.5)
+    b = both()
+    assert not np.allclose(b, a)
+    sd = {k: v.clone() * 1.1 if k.startswith("attention.W1") else v.clone() for k, v in ex.state_dict().items()}
+    ex.load_state_dict(sd, assign=True)
+    c = both()
+    assert not np.allclose(c, b)
+
+
 def test_pipeline_full_size_vs_oracle(tm):
     """Bench workload shape (enron-like, N=20, B=100): sampled outputs bit-exact vs the C oracle on
     every event of one batch per side, encoder + explanation vs the torch-fp32 oracle."""
