@@ -78,20 +78,24 @@ def self_launch(n):
 def flops_model(de, dn, h, N, M, etab=False):
     """MACs x2 per unit for each encoder kernel.  ``walk_kernel``: the SURVEY.md §8(a) a12 model (3 walk
     positions + head), minus the 3 de x dn edge-feature MACs per walk that the edge table (``etab``) does once
-    per edge id.  ``walk_kernel_executed``: what the kernel actually issues -- position 2 once per hop-1 slot
-    (shared by its M walks), the all-time-feature K steps of lin_event there folded into a bias (dt = 0),
-    the attention's duplicated 2h x 2h W1 product once per slot."""
+    per edge id.  ``walk_kernel_executed``: what the kernel actually issues (folded form) --
+    per walk position 0/1: lin_event, event_gcn's first layer on both branches, the folded attention.MLP.0
+    product A1G (h x 2h) and the score dot (2h); per hop-1 slot (shared by its M walks): position 2's
+    lin_event over the K steps below qt (the all-time-feature steps are a bias at dt = 0), event_gcn's
+    first layer, the folded W1D and G^T (2h x 2h each), A1D (h x 2h) and the beta dot; per walk the head:
+    MLP.0 folded with attention.MLP.3 (h+12 x h), MLP.3 (h x h+12) and the last row (h)."""
     kev = de + 3 + dn
     per_pos_gcn = kev * dn + 2 * (dn * h + h * h)                       # lin_event + event_gcn MLP x2
     per_walk_head = 3 * (2 * h) ** 2 + (2 * h) * h + h * h + (h + 12) ** 2 + (h + 12) * h + h + 2 * 2 * h
     per_pos_gate = (de + dn) * h + h * (h // 2) + h // 2
     W = N * M
     qt = (de + 3 + 15) // 16
-    exec_walk = 2 * ((2 + 1.0 / M) * per_pos_gcn + per_walk_head - (1 - 1.0 / M) * (2 * h) ** 2
-                     - max(kev - 16 * qt, 0) * dn / M)
+    edge = de * dn if etab else 0
+    pos = kev * dn - edge + 2 * dn * h
+    slot = kev * dn - max(kev - 16 * qt, 0) * dn - edge + 2 * dn * h + h * 2 * h + 2 * (2 * h) ** 2 + 2 * h
+    exec_walk = 2 * (2 * (pos + h * 2 * h + 2 * h) + slot / M + (h + 12) * h + h * (h + 12) + h)
     walk = 2 * (3 * per_pos_gcn + per_walk_head)
     if etab:
-        exec_walk -= 2 * (2 + 1.0 / M) * de * dn
         walk -= 2 * 3 * de * dn
     return dict(walk_kernel=walk, walk_kernel_executed=exec_walk,
                 gate_per_edge=2 * per_pos_gate + (2 * de * dn if etab else 0), W=W,

@@ -495,17 +495,80 @@ __device__ __forceinline__ void rgemm2(const Lin &L, const floatx4 (&x)[NQ], con
     }
 }
 
-// Per-workgroup LDS table of the small per-feature vectors the walk kernel reads in its epilogues:
-// every bias (zero padded to its tiles), the last MLP row, and the time encoder's frequency and phase
-// laid out on the event-feature axis k (zero outside the time block), so the per-lane reads in the
-// feature generation and the epilogues are ds_reads (broadcast within a lane group), not L2 loads
-// whose latency a dependent epilogue would wait for in every layer.
+// Weight layout of the fused walk kernel (hid_dim 64, 11 node-feature tiles): float offsets into
+// tm_weights::buf -- the folded region (FoldLay) first, then the reference layers in
+// tm_weights_create's order; compile-time for a kernel instance (NQE = lin_event's K steps), so every
+// weight fragment is one buffer load off a single resource with a constant offset.  The host checks the
+// live pointers against it before the launch (walk_layout_ok).
+template <int NQE>
+struct WalkLay {
+    static constexpr int EV = FoldLay::SIZE, EVB = EV + 11 * NQE * 256, G1 = EVB + 176, G1B = G1 + 4 * 11 * 256,
+                         G2 = G1B + 64, G2B = G2 + 4 * 4 * 256, W1 = G2B + 64, W1B = W1 + 8 * 8 * 256, W2 = W1B + 128,
+                         W2B = W2 + 8 * 8 * 256, A1 = W2B + 128, A1B = A1 + 4 * 8 * 256, A2 = A1B + 64,
+                         A2B = A2 + 4 * 4 * 256, M1 = A2B + 64, M1B = M1 + 5 * 5 * 256, M2 = M1B + 80,
+                         M2B = M2 + 4 * 5 * 256;
+};
+
+// out[t] += W tile t * x over the K steps [0, NQ) of a pack with NQL K steps at float offset BASE (the
+// caller initialises out: bias rows from LDS, a table row, or zero); weights streamed PF fragments ahead
+template <int NTO, int NQ, int NQL, int BASE>
+__device__ __forceinline__ void cgemm(__amdgpu_buffer_rsrc_t wr, const floatx4 (&x)[NQ], floatx4 (&o)[NTO]) {
+    const int vo = lane_id() * 16;
+    constexpr int N = NTO * NQ, D = PF < N ? PF : N;
+    float4 buf[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) buf[i] = wload(wr, vo, BASE / 4 + ((i / NQ) * NQL + i % NQ) * 64);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const int t = i / NQ, q = i % NQ;
+        const float4 w = buf[i % D];
+        if (i + D < N) buf[i % D] = wload(wr, vo, BASE / 4 + (((i + D) / NQ) * NQL + (i + D) % NQ) * 64);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, x[q].x, o[t], 0, 0, 0);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, x[q].y, o[t], 0, 0, 0);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, x[q].z, o[t], 0, 0, 0);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, x[q].w, o[t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// two column sets through the same weight fragments (one load feeds 8 MFMAs)
+template <int NTO, int NQ, int BASE>
+__device__ __forceinline__ void cgemm2(__amdgpu_buffer_rsrc_t wr, const floatx4 (&x)[NQ], const floatx4 (&y)[NQ],
+                                       floatx4 (&o)[NTO], floatx4 (&p)[NTO]) {
+    const int vo = lane_id() * 16;
+    constexpr int N = NTO * NQ, D = PF < N ? PF : N;
+    float4 buf[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) buf[i] = wload(wr, vo, BASE / 4 + i * 64);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const int t = i / NQ, q = i % NQ;
+        const float4 w = buf[i % D];
+        if (i + D < N) buf[i % D] = wload(wr, vo, BASE / 4 + (i + D) * 64);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, x[q].x, o[t], 0, 0, 0);
+        p[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, y[q].x, p[t], 0, 0, 0);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, x[q].y, o[t], 0, 0, 0);
+        p[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, y[q].y, p[t], 0, 0, 0);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, x[q].z, o[t], 0, 0, 0);
+        p[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, y[q].z, p[t], 0, 0, 0);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, x[q].w, o[t], 0, 0, 0);
+        p[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, y[q].w, p[t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// Per-workgroup LDS table of the small per-feature vectors the walk kernel reads: accumulator
+// initialisers (biases, folded constant vectors, the category table), the last MLP row, and the time
+// encoder's frequency and phase laid out on the event-feature axis k (zero outside the time block), so
+// they are ds_reads (broadcast within a lane group; no VALU work), not L2 loads.  G1 and G1C hold the
+// same bias (two copies: the two branches' accumulators are initialised by two reads, not a read and
+// four register moves).
 template <int NQE, int NTD>
 struct WalkConsts {
-    static constexpr int XW = 0, XP = XW + 16 * NQE, EV = XP + 16 * NQE, EVC = EV + 16 * NTD, G1 = EVC + 16 * NTD,
-                         G2 = G1 + HID,
-                         W1 = G2 + HID, W2 = W1 + 2 * HID, A1 = W2 + 2 * HID, A2 = A1 + HID, M1 = A2 + HID,
-                         M2 = M1 + 80, M3 = M2 + HID, SIZE = M3 + HID;
+    static constexpr int XW = 0, XP = XW + 16 * NQE, EV = XP + 16 * NQE, EVC = EV + 16 * NTD, DEVC = EVC + 16 * NTD,
+                         G1 = DEVC + 16 * NTD, G1C = G1 + HID, B1D = G1C + HID, CP = B1D + 2 * HID,
+                         BETA = CP + HID, M2 = BETA + 2 * HID, M3 = M2 + HID, TC = M3 + HID, M3B = TC + 13 * 80,
+                         SIZE = M3B + 4;
 };
 
 template <int NQE, int NTD>
@@ -517,16 +580,17 @@ __device__ __forceinline__ void load_consts(const EncW &P, float *cs) {
             const int k = i < C::XP ? i : i - C::XP, ti = k - P.de - 3;
             v = (ti >= 0 && ti < P.dn) ? (i < C::XP ? P.freq[ti] : P.phase[ti]) : 0.f;
         } else if (i < C::EVC) v = P.ev.b[i - C::EV];
-        else if (i < C::G1) v = P.evc[i - C::EVC];
-        else if (i < C::G2) v = P.g1.b[i - C::G1];
-        else if (i < C::W1) v = P.g2.b[i - C::G2];
-        else if (i < C::W2) v = P.w1.b[i - C::W1];
-        else if (i < C::A1) v = P.w2.b[i - C::W2];
-        else if (i < C::A2) v = P.a1.b[i - C::A1];
-        else if (i < C::M1) v = P.a2.b[i - C::A2];
-        else if (i < C::M2) v = P.m1.b[i - C::M1];
+        else if (i < C::DEVC) v = P.evc[i - C::EVC];
+        else if (i < C::G1) v = P.devc[i - C::DEVC];
+        else if (i < C::G1C) v = P.g1.b[i - C::G1];
+        else if (i < C::B1D) v = P.g1.b[i - C::G1C];
+        else if (i < C::CP) v = P.b1d[i - C::B1D];
+        else if (i < C::BETA) v = P.cp[i - C::CP];
+        else if (i < C::M2) v = P.beta[i - C::BETA];
         else if (i < C::M3) v = P.m2.b[i - C::M2];
-        else v = P.m3w[i - C::M3];
+        else if (i < C::TC) v = P.m3w[i - C::M3];
+        else if (i < C::M3B) v = P.tc[i - C::TC];
+        else v = P.m3b[0];
         cs[i] = v;
     }
 }
@@ -535,6 +599,10 @@ __device__ __forceinline__ void load_consts(const EncW &P, float *cs) {
 __device__ __forceinline__ float4 lds4(const float *v, int t) {
     return *reinterpret_cast<const float4 *>(v + 16 * t + 4 * ((threadIdx.x & 63) >> 4));
 }
+__device__ __forceinline__ floatx4 ldsx4(const float *v, int t) {
+    const float4 b = lds4(v, t);
+    return floatx4{b.x, b.y, b.z, b.w};
+}
 
 __device__ __forceinline__ floatx4 add4(const floatx4 &a, const float4 &b) {
     return floatx4{a[0] + b.x, a[1] + b.y, a[2] + b.z, a[3] + b.w};
@@ -542,6 +610,10 @@ __device__ __forceinline__ floatx4 add4(const floatx4 &a, const float4 &b) {
 
 __device__ __forceinline__ floatx4 relu_add4(const floatx4 &a, const float4 &b) {
     return floatx4{relu(a[0] + b.x), relu(a[1] + b.y), relu(a[2] + b.z), relu(a[3] + b.w)};
+}
+
+__device__ __forceinline__ floatx4 relu4(const floatx4 &a) {
+    return floatx4{relu(a[0]), relu(a[1]), relu(a[2]), relu(a[3])};
 }
 
 struct WalkArgs {
@@ -553,10 +625,10 @@ struct WalkArgs {
     const float *ts3, *cnt, *stdv;
     const double *cut;
     float *out;
-    const float *etab;    // [n_ids][16*NTD] lin_event's edge-feature part per edge id (walk_kernel Q0 > 0)
+    const float *etab;    // [n_ids][16*NTD] lin_event's edge-feature part + bias per edge id (Q0 > 0)
 };
 
-// Phase timing (debug builds only, -DTM_STAMPS; tools_stamps.py): s_memtime deltas of lane 0 per
+// Phase timing (debug builds only, -DTM_STAMPS; tools/stamps.py): s_memtime deltas of lane 0 per
 // pass type accumulated for workgroups 512..1023 (past the first dispatch round).
 #ifdef TM_STAMPS
 __device__ unsigned long long g_st[3][10];
@@ -616,31 +688,29 @@ __device__ __forceinline__ void load_ef(const WalkArgs &a, int32_t e, float (&ef
     }
 }
 
-// K step q of the event features x[k] = [E(e) | cnt | cos(dt * w + phi)] (:176-179, TimeEncode :45-59)
-template <int NQE, int NTD, bool ETAB = false>
-__device__ __forceinline__ floatx4 gen_x(int q, const float *cs, const float (&ef)[EQ_MAX][4], int g, int de, int kev,
-                                         float dt, float c0, float c1, float c2) {
-    using C = WalkConsts<NQE, NTD>;
-    floatx4 xq;
-    const float4 w4 = lds4(cs + C::XW, q), p4 = lds4(cs + C::XP, q);
-    const float wv[4] = {w4.x, w4.y, w4.z, w4.w}, pv[4] = {p4.x, p4.y, p4.z, p4.w};
+// Element s of K step q of the event features x[k] = [E(e) | cnt | cos(dt * w + phi)] (:176-179,
+// TimeEncode :45-59) for this lane's feature k = 16q + 4g + s, with the step's time-encoder frequency w
+// and phase ph in registers.  PURE (a step holding only time features, known at compile time): the cos
+// alone.  Otherwise the cos is evaluated unconditionally (the opaque asm keeps the compiler from wrapping
+// the polynomial in an exec-mask branch, which serialised it against the MFMAs) and the count / edge
+// lanes select their values.  Padding lanes (k >= kev) keep cos(0) = 1: lin_event's packed weights are
+// zero there.  In table mode the edge lanes are 0 (their product comes from the table row).
+template <bool ETAB, bool PURE>
+__device__ __forceinline__ float gen_one(int q, int s, float w, float ph, const float (&ef)[EQ_MAX][4], int g,
+                                         int de, float dt, float c0, float c1, float c2) {
+    float c = time_cos(dt, w, ph);
+    if constexpr (PURE) return c;
+    const int k = 16 * q + 4 * g + s;
     const int qe = q < EQ_MAX ? q : 0;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        const int k = 16 * q + 4 * g + s;
-        float v;
-        if (!ETAB && 16 * q + 16 <= de) v = ef[qe][s];
-        else {
-            v = (k < kev) ? time_cos(dt, wv[s], pv[s]) : 0.f;
-            if (k < de + 3) v = (k == de) ? c0 : (k == de + 1) ? c1 : c2;
-            if (k < de) v = ETAB ? 0.f : ef[qe][s];      // table mode: the edge part comes from etab
-        }
-        xq[s] = v;
-    }
-    return xq;
+    if (!ETAB && 16 * q + 16 <= de) return ef[qe][s];
+    asm volatile("" : "+v"(c));
+    float v = c;
+    if (k < de + 3) v = (k == de) ? c0 : (k == de + 1) ? c1 : c2;
+    if (k < de) v = ETAB ? 0.f : ef[qe][s];
+    return v;
 }
 
-// gen_x for the streamed-edge-feature variant: e4 = this lane's 4 edge features of K step q
+// streamed-edge-feature variant (EQ_MAX*16 < de): e4 = this lane's 4 edge features of K step q
 template <int NQE, int NTD>
 __device__ __forceinline__ floatx4 gen_x_s(int q, const float *cs, const float4 &e4, int g, int de, int kev, float dt,
                                            float c0, float c1, float c2) {
@@ -672,7 +742,7 @@ __device__ __forceinline__ float4 ef_step(const float4 *erow4, int q, int g, int
 }
 
 // table mode: this lane's 4 features of each of the 11 output tiles of edge e's table row (loaded a
-// pass ahead, as load_ef does for the plain mode's edge features)
+// pass ahead; they initialise the next pass's lin_event accumulators)
 #define ETAB_N(q0) ((q0) > 0 ? 11 : 1)
 template <int Q0>
 __device__ __forceinline__ void load_et(const WalkArgs &a, int32_t e, float4 (&et)[ETAB_N(Q0)]) {
@@ -684,84 +754,135 @@ __device__ __forceinline__ void load_et(const WalkArgs &a, int32_t e, float4 (&e
     }
 }
 
-// one walk position for the 16 columns of this wave -> F = [U_s | U_t] (8 tiles, B layout).
-// lin_event runs K-outer ((q, t) fragment order): the event features of K step q+1 are generated
-// while step q's MFMAs run and only L and two x fragments are live.  Node-feature rows are float4
-// gathers (dn % 4 == 0) in the epilogue, unconditional with a clamped index (issuing them during the
-// GEMM keeps 88 more registers live and costs the second wave per SIMD).
+// One walk position for the 16 columns of this wave -> H = [relu(g1 A + b) | relu(g1 B + b)] (8 tiles,
+// B layout), event_gcn's hidden layer of both branches; the second MLP layer (g2) is folded into the
+// layers that read F = [U_s | U_t] (FoldLay).
+// lin_event runs K-outer ((q, t) fragment order): the next K step's 4 event features are generated one
+// element per tile between this step's MFMAs.  Its accumulators start from the bias (LDS) or, in table
+// mode, from the edge's table row (edge-feature product + bias; the slot pass adds the folded time steps).
+// Both nodes' feature rows are requested before the K loop (their latency overlaps it) and consumed
+// in its epilogue.  Tiles past dn in the last node tile hold a clamped duplicate; g1's packed weights are
+// zero for those inputs, so they contribute nothing.
 // SEF (streamed edge features, EQ_MAX*16 < de <= 176): ef holds K steps 0 and 1 (loaded during the
 // previous pass); step q + 2's float4 is loaded while step q's MFMAs run.
-// Q0 > 0 (edge table): K steps < Q0 hold only edge features, whose product with lin_event's weights
-// is the per-edge-id row etab[e] (computed once per call with the gate table); the loop starts at
-// step Q0 with the edge lanes of step Q0 zeroed, and the epilogue adds the row.
 template <int NQE, int NTD, bool SEF, int Q0 = 0>
-__device__ __forceinline__ void encode_position(const WalkArgs &a, const float *cs, const PosIn &pi,
-                                                const float (&ef)[EQ_MAX][4], const float4 (&et)[ETAB_N(Q0)], int p,
-                                                floatx4 (&F)[8], unsigned long long (&T)[10]) {
+__device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buffer_rsrc_t wr, const float *cs,
+                                                const PosIn &pi, const float (&ef)[EQ_MAX][4],
+                                                const float4 (&et)[ETAB_N(Q0)], int p, floatx4 (&H)[8],
+                                                unsigned long long (&T)[10]) {
     constexpr bool ETAB = Q0 > 0;
     static_assert(!(ETAB && SEF), "table mode replaces the streamed edge features");
     using C = WalkConsts<NQE, NTD>;
+    using LY = WalkLay<NQE>;
     const EncW &P = a.P;
     const int g = lane_id() >> 4;
     const int de = P.de, dn = P.dn, kev = P.kev;
-    const int32_t ns = pi.ns, nt = pi.nt;
     const float dt = pi.dt, c0 = pi.c0, c1 = pi.c1, c2 = pi.c2;
-    const float4 *nrow_s = reinterpret_cast<const float4 *>(a.n_feat + (int64_t)ns * dn);
-    const float4 *nrow_t = reinterpret_cast<const float4 *>(a.n_feat + (int64_t)nt * dn);
+    const float4 *nrow_s = reinterpret_cast<const float4 *>(a.n_feat + (int64_t)pi.ns * dn);
+    const float4 *nrow_t = reinterpret_cast<const float4 *>(a.n_feat + (int64_t)pi.nt * dn);
     float4 xs[NTD], xt[NTD];
     floatx4 L[NTD];
+    if constexpr (ETAB) {
 #pragma unroll
-    for (int t = 0; t < NTD; ++t) L[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    // the source node's feature rows requested before lin_event, consumed in its epilogue (their wait
-    // overlaps the K loop: -0.8 %; the target's too would need 256 VGPRs and spill).  Ablation: both
-    // rows' gathers cost 17 % of the kernel (all columns reading one row: 12.07 -> 10.01 ms)
+        for (int t = 0; t < NTD; ++t) L[t] = floatx4{et[t].x, et[t].y, et[t].z, et[t].w};
+        if (p == 2) {                                    // slot pass: + the folded time steps (wave-uniform)
+#pragma unroll
+            for (int t = 0; t < NTD; ++t) L[t] = add4(L[t], lds4(cs + C::DEVC, t));
+        }
+    } else {
+        const float *bias = cs + (p == 2 ? C::EVC : C::EV);
+#pragma unroll
+        for (int t = 0; t < NTD; ++t) L[t] = ldsx4(bias, t);
+    }
 #pragma unroll
     for (int t = 0; t < NTD; ++t) {
         const int f4 = (t < NTD - 1) ? 4 * t + g : min(4 * t + g, dn / 4 - 1);
         xs[t] = nrow_s[f4];
     }
+#pragma unroll
+    for (int t = 0; t < NTD; ++t) {
+        const int f4 = (t < NTD - 1) ? 4 * t + g : min(4 * t + g, dn / 4 - 1);
+        xt[t] = nrow_t[f4];
+    }
     TM_STAMP(1);
     {
-        const auto wr = wrsrc(P.ev.w);
         const int vo = lane_id() * 16;
         constexpr int nq = NQE;
         constexpr int N = NTD * (NQE - Q0), D = PF;
+        constexpr int EVF4 = LY::EV / 4;
         float4 buf[D];
 #pragma unroll
-        for (int i = 0; i < D; ++i) buf[i] = wload(wr, vo, ((i % NTD) * nq + Q0 + i / NTD) * 64);
-        const float4 *erow4 = reinterpret_cast<const float4 *>(a.e_feat + (int64_t)pi.e * de);
-        float4 ring[2];
+        for (int i = 0; i < D; ++i) buf[i] = wload(wr, vo, EVF4 + ((i % NTD) * nq + Q0 + i / NTD) * 64);
+        const int qend = p == 2 ? P.qt : NQE;            // slot pass: steps >= qt folded into evc / devc
         if constexpr (SEF) {
+            const float4 *erow4 = reinterpret_cast<const float4 *>(a.e_feat + (int64_t)pi.e * de);
+            float4 ring[2];
             ring[0] = make_float4(ef[0][0], ef[0][1], ef[0][2], ef[0][3]);
             ring[1] = make_float4(ef[1][0], ef[1][1], ef[1][2], ef[1][3]);
-        }
-        floatx4 xq = SEF ? gen_x_s<NQE, NTD>(0, cs, ring[0], g, de, kev, dt, c0, c1, c2)
-                         : gen_x<NQE, NTD, ETAB>(Q0, cs, ef, g, de, kev, dt, c0, c1, c2);
-        const int qend = p == 2 ? P.qt : NQE;            // slot pass: steps >= qt folded into evc
+            floatx4 xq = gen_x_s<NQE, NTD>(0, cs, ring[0], g, de, kev, dt, c0, c1, c2);
 #pragma unroll
-        for (int q = Q0; q < NQE; ++q) {
-            if (q < qend) {                               // wave-uniform (a break would stop the unrolling)
-                floatx4 xn = xq;
-                float4 e2 = make_float4(0.f, 0.f, 0.f, 0.f);
-                if constexpr (SEF) {
+            for (int q = 0; q < NQE; ++q) {
+                if (q < qend) {                           // wave-uniform (a break would stop the unrolling)
+                    floatx4 xn = xq;
+                    float4 e2 = make_float4(0.f, 0.f, 0.f, 0.f);
                     if (q + 2 < NQE && 16 * (q + 2) < de) e2 = ef_step(erow4, q + 2, g, de);
                     if (q + 1 < NQE) xn = gen_x_s<NQE, NTD>(q + 1, cs, ring[(q + 1) & 1], g, de, kev, dt, c0, c1, c2);
-                } else {
-                    if (q + 1 < NQE) xn = gen_x<NQE, NTD, ETAB>(q + 1, cs, ef, g, de, kev, dt, c0, c1, c2);
-                }
 #pragma unroll
-                for (int t = 0; t < NTD; ++t) {
-                    const int i = (q - Q0) * NTD + t;
-                    const float4 w = buf[i % D];
-                    if (i + D < N) buf[i % D] = wload(wr, vo, (((i + D) % NTD) * nq + Q0 + (i + D) / NTD) * 64);
-                    L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, xq.x, L[t], 0, 0, 0);
-                    L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, xq.y, L[t], 0, 0, 0);
-                    L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, xq.z, L[t], 0, 0, 0);
-                    L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, xq.w, L[t], 0, 0, 0);
-                    __builtin_amdgcn_sched_barrier(0);
+                    for (int t = 0; t < NTD; ++t) {
+                        const int i = q * NTD + t;
+                        const float4 w = buf[i % D];
+                        if (i + D < N) buf[i % D] = wload(wr, vo, EVF4 + (((i + D) % NTD) * nq + (i + D) / NTD) * 64);
+                        L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, xq.x, L[t], 0, 0, 0);
+                        L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, xq.y, L[t], 0, 0, 0);
+                        L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, xq.z, L[t], 0, 0, 0);
+                        L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, xq.w, L[t], 0, 0, 0);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                    ring[q & 1] = e2;
+                    xq = xn;
                 }
-                if constexpr (SEF) ring[q & 1] = e2;
-                xq = xn;
+            }
+        } else {
+            const float *cw = cs + C::XW, *cp = cs + C::XP;
+            floatx4 xq;
+            {
+                const float4 w4 = lds4(cw, Q0), p4 = lds4(cp, Q0);
+                xq[0] = gen_one<ETAB, false>(Q0, 0, w4.x, p4.x, ef, g, de, dt, c0, c1, c2);
+                xq[1] = gen_one<ETAB, false>(Q0, 1, w4.y, p4.y, ef, g, de, dt, c0, c1, c2);
+                xq[2] = gen_one<ETAB, false>(Q0, 2, w4.z, p4.z, ef, g, de, dt, c0, c1, c2);
+                xq[3] = gen_one<ETAB, false>(Q0, 3, w4.w, p4.w, ef, g, de, dt, c0, c1, c2);
+            }
+#pragma unroll
+            for (int q = Q0; q < NQE; ++q) {
+                if (q < qend) {                           // wave-uniform (a break would stop the unrolling)
+                    // step q + 1's constants from LDS now (first use after tile 0's MFMAs)
+                    float4 w4 = make_float4(0.f, 0.f, 0.f, 0.f), p4 = w4;
+                    if (q + 1 < NQE) {
+                        w4 = lds4(cw, q + 1);
+                        p4 = lds4(cp, q + 1);
+                    }
+                    const float wq[4] = {w4.x, w4.y, w4.z, w4.w}, pq[4] = {p4.x, p4.y, p4.z, p4.w};
+                    constexpr bool pure_next_ok = ETAB;   // table mode: steps >= Q0 + 2 hold only time features
+                    floatx4 xn = xq;
+#pragma unroll
+                    for (int t = 0; t < NTD; ++t) {
+                        const int i = (q - Q0) * NTD + t;
+                        const float4 w = buf[i % D];
+                        if (i + D < N) buf[i % D] = wload(wr, vo, EVF4 + (((i + D) % NTD) * nq + Q0 + (i + D) / NTD) * 64);
+                        L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, xq.x, L[t], 0, 0, 0);
+                        L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, xq.y, L[t], 0, 0, 0);
+                        L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, xq.z, L[t], 0, 0, 0);
+                        L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, xq.w, L[t], 0, 0, 0);
+                        if (q + 1 < NQE && t < 4) {
+                            if (pure_next_ok && q + 1 >= Q0 + 2)
+                                xn[t] = gen_one<ETAB, true>(q + 1, t, wq[t], pq[t], ef, g, de, dt, c0, c1, c2);
+                            else
+                                xn[t] = gen_one<ETAB, false>(q + 1, t, wq[t], pq[t], ef, g, de, dt, c0, c1, c2);
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                    xq = xn;
+                }
             }
         }
     }
@@ -770,46 +891,29 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, const float *
     floatx4 A[NTD], Bv[NTD];
 #pragma unroll
     for (int t = 0; t < NTD; ++t) {
-        const float4 b = lds4(cs + (p == 2 ? C::EVC : C::EV), t);
-        float bv[4] = {b.x, b.y, b.z, b.w};
-        if constexpr (ETAB) {
-            bv[0] += et[t].x;
-            bv[1] += et[t].y;
-            bv[2] += et[t].z;
-            bv[3] += et[t].w;
-        }
-        // tiles below the last are inside the row (dispatch: 160 < dn <= 176), so their offsets are
-        // immediates on one row address; the last tile's index is clamped and masked below
-        const int f4 = (t < NTD - 1) ? 4 * t + g : min(4 * t + g, dn / 4 - 1);
-        xt[t] = nrow_t[f4];
         const float sv[4] = {xs[t].x, xs[t].y, xs[t].z, xs[t].w}, tv[4] = {xt[t].x, xt[t].y, xt[t].z, xt[t].w};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const bool in = 16 * t + 4 * g + r < dn;
-            const float l = L[t][r] + bv[r];
-            A[t][r] = in ? sv[r] + relu(tv[r] + l) : 0.f;
-            Bv[t][r] = in ? tv[r] + relu(sv[r] + l) : 0.f;
+            const float l = L[t][r];
+            A[t][r] = sv[r] + relu(tv[r] + l);
+            Bv[t][r] = tv[r] + relu(sv[r] + l);
         }
     }
-    floatx4 Hs[4], Ht[4];
     TM_STAMP(3);
-    rgemm2<4, NTD>(P.g1, A, Bv, Hs, Ht);
+    floatx4 Hs[4], Ht[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        Hs[t] = ldsx4(cs + C::G1, t);
+        Ht[t] = ldsx4(cs + C::G1C, t);
+    }
+    cgemm2<4, NTD, LY::G1>(wr, A, Bv, Hs, Ht);
     TM_STAMP(4);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        const float4 b = lds4(cs + C::G1, t);
-        Hs[t] = relu_add4(Hs[t], b);
-        Ht[t] = relu_add4(Ht[t], b);
+        H[t] = relu4(Hs[t]);
+        H[4 + t] = relu4(Ht[t]);
     }
-    floatx4 Us[4], Ut[4];
-    rgemm2<4, 4>(P.g2, Hs, Ht, Us, Ut);
     TM_STAMP(5);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        const float4 b = lds4(cs + C::G2, t);
-        F[t] = add4(Us[t], b);
-        F[4 + t] = add4(Ut[t], b);
-    }
 }
 
 // sum over the 4 lane groups sharing a column (lanes l, l^16, l^32, l^48)
@@ -825,26 +929,25 @@ struct HeadIn {
     int32_t c;
 };
 
-// attention head + final MLP for the 16 walks of this wave (Q1 in registers, F2/Wp/Q0 in the stash)
+// per-wave LDS stash of a slot's position-2 results, read by its walks' position-0/1 passes
+struct Stash {
+    floatx4 V[8][64];     // G^T Wp: the attention score of position i is V . H_i + cw
+    floatx4 P2[4][64];    // A1D H_2 + cp: attention.MLP.0's input part that does not depend on alpha
+    float cw[64];         // Wp . beta
+};
+
+// Attention head + final MLP for the 16 walks of this wave (explainer_new.py:789-846 and :121-125,
+// :195-201) in the folded form: score_i = V . H_i + cw, alpha = softmax(score * time weight),
+// hid = relu(P2 + alpha_0 R_0 + alpha_1 R_1) (R_i = A1G H_i; alpha_0 + alpha_1 = 1 carries a1 beta),
+// M1 = relu(M1A2 hid + tc[cat]), M2 = relu(m2 M1 + b), imp = sigmoid(m3 . M2 + b).
 template <int NQE, int NTD>
-__device__ __forceinline__ void walk_head(const WalkArgs &a, const float *cs, int64_t gw, bool valid, const HeadIn &hi,
-                                          const floatx4 (&sF2)[8][64], const floatx4 (&sWp)[8][64],
-                                          const floatx4 (&Q0)[8], const floatx4 (&Q1)[8]) {
+__device__ __forceinline__ void walk_head(const WalkArgs &a, __amdgpu_buffer_rsrc_t wr, const float *cs, int64_t gw,
+                                          bool valid, const HeadIn &hi, const Stash &st, float s0, float s1,
+                                          const floatx4 (&R0)[4], const floatx4 (&R1)[4]) {
     using C = WalkConsts<NQE, NTD>;
+    using LY = WalkLay<NQE>;
     const EncW &P = a.P;
     const int lane = threadIdx.x & 63, g = lane_id() >> 4;
-    float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-        const floatx4 wp = sWp[t][lane];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            s0 += wp[r] * Q0[t][r];
-            s1 += wp[r] * Q1[t][r];
-        }
-    }
-    s0 = col_sum(s0);
-    s1 = col_sum(s1);
     float tw0 = 1.f, tw1 = 1.f;                          // plain Attention (tg = 0): 0.7f + 0.3f == 1.0f exactly
     if (valid && P.tg) {
         tw0 = expf(-fabsf(hi.cu - hi.t0) / hi.sd);
@@ -855,43 +958,50 @@ __device__ __forceinline__ void walk_head(const WalkArgs &a, const float *cs, in
     s1 *= __fadd_rn(0.7f, __fmul_rn(0.3f, tw1));
     const float mx = fmaxf(s0, s1), e0 = expf(s0 - mx), e1 = expf(s1 - mx), sum = e0 + e1;
     const float al0 = e0 / sum, al1 = e1 / sum;
-    floatx4 O[8];
+    floatx4 X[4];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-        const floatx4 f2 = sF2[t][lane];
+    for (int t = 0; t < 4; ++t) {
+        const floatx4 p2 = st.P2[t][lane];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) O[t][r] = f2[r] + (al0 * Q0[t][r] + al1 * Q1[t][r]);
+        for (int r = 0; r < 4; ++r) X[t][r] = relu(p2[r] + (al0 * R0[t][r] + al1 * R1[t][r]));
     }
-    floatx4 H1[4];
-    rgemm<4, 8>(P.a1, O, H1);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) H1[t] = relu_add4(H1[t], lds4(cs + C::A1, t));
-    floatx4 X5[5];
-    {
-        floatx4 H2[4];
-        rgemm<4, 4>(P.a2, H1, H2);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) X5[t] = add4(H2[t], lds4(cs + C::A2, t));
-        // one-hot category in features 64..75 (compute_catogory_feautres :308-315)
-        const int32_t c = valid ? hi.c : -1;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) X5[4][r] = (c == 4 * g + r) ? 1.f : 0.f;
-    }
+    // MLP.0 over [attention out | one-hot(cat)] (compute_catogory_feautres :308-315): the one-hot column and
+    // the biases come in as the accumulators' initial value, row cat of tc (row 12 for a padding column)
+    const int32_t c = (valid && hi.c >= 0 && hi.c < 12) ? hi.c : 12;
     floatx4 M1[5];
-    rgemm<5, 5>(P.m1, X5, M1);
 #pragma unroll
-    for (int t = 0; t < 5; ++t) M1[t] = relu_add4(M1[t], lds4(cs + C::M1, t));
+    for (int t = 0; t < 5; ++t) {
+        const float4 b = *reinterpret_cast<const float4 *>(cs + C::TC + 80 * c + 16 * t + 4 * g);
+        M1[t] = floatx4{b.x, b.y, b.z, b.w};
+    }
+    cgemm<5, 4, 4, FoldLay::M1A2>(wr, X, M1);
+#pragma unroll
+    for (int t = 0; t < 5; ++t) M1[t] = relu4(M1[t]);
     floatx4 M2[4];
-    rgemm<4, 5>(P.m2, M1, M2);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) M2[t] = ldsx4(cs + C::M2, t);
+    cgemm<4, 5, 5, LY::M2>(wr, M1, M2);
     float z = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        const floatx4 h = relu_add4(M2[t], lds4(cs + C::M2, t));
         const float4 w3 = lds4(cs + C::M3, t);
-        z += h[0] * w3.x + h[1] * w3.y + h[2] * w3.z + h[3] * w3.w;
+        z += relu(M2[t][0]) * w3.x + relu(M2[t][1]) * w3.y + relu(M2[t][2]) * w3.z + relu(M2[t][3]) * w3.w;
     }
-    z = col_sum(z) + P.m3b[0];
+    z = col_sum(z) + cs[C::M3B];
     if (valid && g == 0) a.out[gw] = 1.f / (1.f + expf(-z));
+}
+
+// this column's V . H (the 4 lane groups' parts summed)
+__device__ __forceinline__ float score_dot(const Stash &st, const floatx4 (&H)[8]) {
+    const int lane = threadIdx.x & 63;
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        const floatx4 v = st.V[t][lane];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s = __builtin_fmaf(v[r], H[t][r], s);
+    }
+    return col_sum(s) + st.cw[lane];
 }
 
 template <int NQE, int NTD, bool SEF = false, int QE0 = 0>
@@ -905,17 +1015,18 @@ __global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
     const int32_t NS = a.W / a.M;
     const int64_t eg = valid ? gs / NS : 0;             // (group, event) row
     const int32_t j = valid ? (int32_t)(gs % NS) : 0;
-    // LDS: per-wave stash of the slot's position-2 features and their W1 projection (16 KB per wave),
-    // then the constant table
-    __shared__ floatx4 stash[4][2][8][64];
+    // LDS: per-wave stash of the slot's position-2 results (12.25 KB per wave), then the constant table
+    __shared__ Stash stash[4];
     __shared__ float4 cs4[(C::SIZE + 3) / 4];
     float *cs = reinterpret_cast<float *>(cs4);
     load_consts<NQE, NTD>(P, cs);
     __syncthreads();
     if (unit * 16 >= a.n_slots) return;                 // whole wave idle (wave-uniform)
-    floatx4(&sF2)[8][64] = stash[threadIdx.x >> 6][0];
-    floatx4(&sWp)[8][64] = stash[threadIdx.x >> 6][1];
-    floatx4 Q0[8];                                      // W2(position 0), carried to the position-1 pass
+    Stash &st = stash[threadIdx.x >> 6];
+    // every weight fragment off one buffer resource (WalkLay offsets from the folded region's base)
+    const auto wr = wrsrc(P.w1d.w);
+    floatx4 R0[4];                                      // A1G H_0, carried to the position-1 pass
+    float s0 = 0.f;
     const int n_pass = 1 + 2 * a.M;
     PosIn cur = load_pos(a, eg * a.W + (int64_t)j * a.M, 2, valid);
     float ef[EQ_MAX][4] = {};
@@ -936,35 +1047,62 @@ __global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
             hi.t1 = a.ts3[gw * 3 + 1];
             hi.c = a.cat[gw];
         }
-        // next pass's scalars now; its edge features once this pass's lin_event is done
+        // next pass's scalars now; its edge features / table row once this pass's lin_event is done
         const int pn = pass + 1 < n_pass ? ((pass & 1) == 0 ? 0 : 1) : 0;
         const int64_t gwn = eg * a.W + (int64_t)j * a.M + (pass >> 1);
         const PosIn nxt = load_pos(a, gwn, pn, valid && pass + 1 < n_pass);
-        floatx4 F[8];
+        floatx4 H[8];
         unsigned long long T[10];
         TM_STAMP(0);
-        encode_position<NQE, NTD, SEF, QE0>(a, cs, cur, ef, et, p, F, T);
+        encode_position<NQE, NTD, SEF, QE0>(a, wr, cs, cur, ef, et, p, H, T);
         if constexpr (QE0 == 0) load_ef(a, nxt.e, ef);
         else load_et<QE0>(a, nxt.e, et);
         cur = nxt;
-        floatx4 Y[8];
         TM_STAMP(6);
-        rgemm<8, 8>(p == 2 ? P.w1 : P.w2, F, Y);
-        TM_STAMP(7);
-        const float *bb = cs + (p == 2 ? C::W1 : C::W2);
-#pragma unroll
-        for (int t = 0; t < 8; ++t) Y[t] = add4(Y[t], lds4(bb, t));
         if (p == 2) {
+            // P2 = A1D H_2 + cp; Wp = W1D H_2 + b1d (attention.W1 of F_2); V = G^T Wp; cw = Wp . beta
+            floatx4 P2[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) P2[t] = ldsx4(cs + C::CP, t);
+            cgemm<4, 8, 8, FoldLay::A1D>(wr, H, P2);
+            floatx4 Wp[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) Wp[t] = ldsx4(cs + C::B1D, t);
+            cgemm<8, 8, 8, FoldLay::W1D>(wr, H, Wp);
+            floatx4 V[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) V[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+            cgemm<8, 8, 8, FoldLay::GT>(wr, Wp, V);
+            float cw = 0.f;
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
-                sF2[t][lane] = F[t];
-                sWp[t][lane] = Y[t];
+                const float4 b = lds4(cs + C::BETA, t);
+                cw = __builtin_fmaf(Wp[t][0], b.x, cw);
+                cw = __builtin_fmaf(Wp[t][1], b.y, cw);
+                cw = __builtin_fmaf(Wp[t][2], b.z, cw);
+                cw = __builtin_fmaf(Wp[t][3], b.w, cw);
             }
-        } else if (p == 0) {
+            cw = col_sum(cw);
 #pragma unroll
-            for (int t = 0; t < 8; ++t) Q0[t] = Y[t];
+            for (int t = 0; t < 8; ++t) st.V[t][lane] = V[t];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) st.P2[t][lane] = P2[t];
+            st.cw[lane] = cw;
         } else {
-            walk_head<NQE, NTD>(a, cs, gw, valid, hi, sF2, sWp, Q0, Y);
+            // R = A1G H_p (attention.MLP.0 of W2's output for this position), score = V . H_p + cw
+            floatx4 R[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) R[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+            cgemm<4, 8, 8, FoldLay::A1G>(wr, H, R);
+            const float s = score_dot(st, H);
+            TM_STAMP(7);
+            if (p == 0) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) R0[t] = R[t];
+                s0 = s;
+            } else {
+                walk_head<NQE, NTD>(a, wr, cs, gw, valid, hi, st, s0, s, R0, R);
+            }
         }
         TM_STAMP(8);
 #ifdef TM_STAMPS
@@ -974,6 +1112,18 @@ __global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
         }
 #endif
     }
+}
+
+// host: the live weight pointers are where WalkLay<nqe> puts them
+static bool walk_layout_ok(const EncW &P, int nqe) {
+    const float *base = reinterpret_cast<const float *>(P.w1d.w);
+    auto at = [&](const float4 *w, int off) { return reinterpret_cast<const float *>(w) == base + off; };
+    const int ev = FoldLay::SIZE, g1 = ev + 11 * nqe * 256 + 176, m2 = g1 + 4 * 11 * 256 + 64 + 4 * 4 * 256 + 64 +
+                                                                     2 * (8 * 8 * 256 + 128) + 4 * 8 * 256 + 64 +
+                                                                     4 * 4 * 256 + 64 + 5 * 5 * 256 + 80;
+    return at(P.ev.w, ev) && at(P.g1.w, g1) && at(P.m2.w, m2) && at(P.gt.w, FoldLay::GT) &&
+           at(P.a1d.w, FoldLay::A1D) && at(P.a1g.w, FoldLay::A1G) && at(P.m1a2.w, FoldLay::M1A2) &&
+           P.g1.nt == 4 && P.g1.nq == 11 && P.m2.nt == 4 && P.m2.nq == 5 && P.ev.nt == 11 && P.ev.nq == nqe;
 }
 
 // ------------------------------------------------------------------ per-edge dependency gate table
@@ -1020,8 +1170,9 @@ __global__ void __launch_bounds__(256) gate_table_kernel(EncW P, int32_t n_ids, 
 // A operand (walk_kernel's layout), X = [E[e] | cos(t_e w + phi)] generated straight into the B
 // fragments, G1 -> G2 -> logit chained in registers.  NQ = K steps of X (de + dn rounded up / 16).
 // NQX > 0: the same edge-feature fragments also give the walk kernel's edge table, etab[e] =
-// lin_event.W[:, :de] . E[e] (16 * 11 features, no bias), from lin_event's pack (NQL K steps): the
-// first NQX K steps with the lanes past de zeroed.
+// lin_event.W[:, :de] . E[e] + lin_event.b (16 * 11 features; the walk kernel starts lin_event's
+// accumulators from it), from lin_event's pack (NQL K steps): the first NQX K steps with the lanes past
+// de zeroed.
 template <int NQ, int NQX = 0, int NQL = 1>
 __global__ void __launch_bounds__(256) gate_reg_kernel(EncW P, int32_t n_ids, const double *__restrict__ ets,
                                                        const float *__restrict__ e_feat, float *__restrict__ gf,
@@ -1062,7 +1213,10 @@ __global__ void __launch_bounds__(256) gate_reg_kernel(EncW P, int32_t n_ids, co
         if (valid) {
             float4 *row = reinterpret_cast<float4 *>(etab + e * 176);
 #pragma unroll
-            for (int t = 0; t < 11; ++t) row[4 * t + g] = make_float4(ET[t][0], ET[t][1], ET[t][2], ET[t][3]);
+            for (int t = 0; t < 11; ++t) {
+                const float4 b = *reinterpret_cast<const float4 *>(P.ev.b + 16 * t + 4 * g);
+                row[4 * t + g] = make_float4(ET[t][0] + b.x, ET[t][1] + b.y, ET[t][2] + b.z, ET[t][3] + b.w);
+            }
         }
     }
     floatx4 G1[4];
@@ -1181,7 +1335,9 @@ extern "C" int tm_weights_create(int32_t de, int32_t dn, int32_t h, int device, 
     } ls[] = {{&P.ev, 0, dn, P.kev}, {&P.g1, 2, h, dn},  {&P.g2, 4, h, h},   {&P.w1, 6, h2, h2},
               {&P.w2, 8, h2, h2},    {&P.a1, 10, h, h2}, {&P.a2, 12, h, h},  {&P.m1, 14, hm, hm},
               {&P.m2, 16, h, hm},    {&P.d1, 20, h, P.kdep}, {&P.d2, 22, h / 2, h}};
-    size_t total = 0;
+    // the folded packs of the fused walk kernel first (fixed size: their offsets and those of the layers
+    // after them are compile-time constants of the kernel, WalkLay)
+    size_t total = tmk::FoldLay::SIZE;
     std::vector<size_t> woff, boff;
     for (auto &l : ls) {
         l.lin->nt = r16(l.nout) / 16;
@@ -1201,6 +1357,7 @@ extern "C" int tm_weights_create(int32_t de, int32_t dn, int32_t h, int device, 
     const size_t fq = total; total += r16(dn);
     const size_t ph = total; total += r16(dn);
     const size_t evc = total; total += r16(dn);
+    const size_t devc = total; total += r16(dn);
     int prev = 0;
     (void)hipGetDevice(&prev);
     if (hipSetDevice(device) != hipSuccess || hipMalloc(&w->buf, total * sizeof(float)) != hipSuccess ||
@@ -1223,10 +1380,39 @@ extern "C" int tm_weights_create(int32_t de, int32_t dn, int32_t h, int device, 
     P.freq = w->buf + fq;
     P.phase = w->buf + ph;
     P.evc = w->buf + evc;
+    P.devc = w->buf + devc;
     P.qt = (de + 3 + 15) / 16;
+    {   // folded packs (tmk::FoldLay)
+        using F = tmk::FoldLay;
+        struct FL {
+            Lin *lin;
+            int off, nout, k;
+        } fl[] = {{&P.w1d, F::W1D, h2, h2}, {&P.gt, F::GT, h2, h2}, {&P.a1d, F::A1D, h, h2}, {&P.a1g, F::A1G, h, h2},
+                  {&P.m1a2, F::M1A2, hm, h}};
+        for (auto &f : fl) {
+            f.lin->w = reinterpret_cast<const float4 *>(w->buf + f.off);
+            f.lin->b = nullptr;
+            f.lin->nout = f.nout;
+            f.lin->k = f.k;
+            f.lin->nt = r16(f.nout) / 16;
+            f.lin->nq = r16(f.k) / 16;
+        }
+        P.b1d = w->buf + F::B1D;
+        P.beta = w->buf + F::BETA;
+        P.cp = w->buf + F::CP;
+        P.tc = w->buf + F::TC;
+        (void)hipGetDevice(&prev);
+        const bool ok = hipSetDevice(device) == hipSuccess &&
+                        hipMalloc(&w->fold64, sizeof(double) * F::S64_SIZE) == hipSuccess &&
+                        hipMalloc(&w->fold32, sizeof(float) * F::S_SIZE) == hipSuccess;
+        (void)hipSetDevice(prev);
+        if (!ok) {
+            tm_weights_free(w);
+            return fail(TM_E_HIP, "tm_weights_create: allocation failed");
+        }
+    }
     if (int rc = train_packs_create(w)) {
-        (void)hipFree(w->buf);
-        delete w;
+        tm_weights_free(w);
         return rc;
     }
     *out = w;
@@ -1253,6 +1439,8 @@ extern "C" int tm_weights_pack(tm_weights *w, const float *const *t, void *strea
 extern "C" int tm_weights_free(tm_weights *w) {
     if (!w) return TM_OK;
     if (w->buf) (void)hipFree(w->buf);
+    if (w->fold64) (void)hipFree(w->fold64);
+    if (w->fold32) (void)hipFree(w->fold32);
     train_packs_free(w);
     delete w;
     return TM_OK;
@@ -1399,6 +1587,7 @@ extern "C" int tm_encoder_fwd_tab(const tm_weights *w, const float *n_feat, cons
     const bool wide = (nqe == 21 || nqe == 22) && P.de > 16 * EQ_MAX && P.de % 4 == 0;
     if (ntd == 11 && P.dn % 4 == 0 && (narrow || wide)) {
         // fused register-resident path
+        if (!walk_layout_ok(P, nqe)) return fail(TM_E_UNSUPPORTED, "tm_encoder_fwd: weight layout mismatch");
         const int64_t n_slots = n_walks / M;
         const int64_t units = (n_slots + 15) / 16;
         WalkArgs a{P, n_slots, W, M, B * W, n_feat, e_feat, node6, eid3, cat, ts3, cnt, stdv, cut, out_imp, etab};

@@ -27,6 +27,16 @@ struct EncW {
     // relative to itself, so those steps are the constant cos(phase) (walk_kernel's slot pass)
     const float *evc;
     int qt;
+    // lin_event's folded time steps alone (evc - bias, fp64 sum rounded once): the table-mode slot pass,
+    // whose edge-table row already carries the bias
+    const float *devc;
+    // fused walk kernel (eval, hid_dim 64): layers folded at pack time in fp64 (tm_weights_pack) --
+    // F = blockdiag(g2, g2) H + [bg2; bg2] (H = event_gcn's relu'd hidden layer of both branches),
+    // W1D = W1 blockdiag(g2,g2), G = W2 blockdiag(g2,g2) (packed transposed), A1D = a1 blockdiag(g2,g2),
+    // A1G = a1 G, M1A2 = MLP.0[:, :h] a2; vectors b1d = W1 [bg2;bg2] + b1, beta = W2 [bg2;bg2] + b2,
+    // cp = a1 [bg2;bg2] + a1 beta + ba1, tc[c] = MLP.0[:, h + c] + bm1 + MLP.0[:, :h] ba2 (row 12: no category)
+    Lin w1d, gt, a1d, a1g, m1a2;
+    const float *b1d, *beta, *cp, *tc;
     // constructor variants (explainer_new.py:103-105, :121, :141): tg = use_temporal_guidance (0: the plain
     // Attention, no time weighting of the scores), dep = use_dependency_aware_sampling (0: no gate)
     int tg = 1, dep = 1;
@@ -115,6 +125,18 @@ __device__ __forceinline__ float gate_logit_lds(const float *g2, const float *w3
     return v;
 }
 
+// Folded region at the start of tm_weights::buf (float offsets; hid_dim 64): the fused walk kernel's
+// packs and vectors (EncW::w1d ...), then the reference layers in tm_weights_create's order.
+struct FoldLay {
+    static constexpr int W1D = 0, B1D = W1D + 8 * 8 * 256, GT = B1D + 128, BETA = GT + 8 * 8 * 256,
+                         A1D = BETA + 128, CP = A1D + 4 * 8 * 256, A1G = CP + 64, M1A2 = A1G + 4 * 8 * 256,
+                         TC = M1A2 + 5 * 4 * 256, SIZE = (TC + 13 * 80 + 63) & ~63;
+    // fold32 scratch (row-major fp32 matrices before packing)
+    static constexpr int S_W1D = 0, S_GT = S_W1D + 128 * 128, S_A1D = S_GT + 128 * 128, S_A1G = S_A1D + 64 * 128,
+                         S_M1A2 = S_A1G + 64 * 128, S_SIZE = S_M1A2 + 76 * 64;
+    static constexpr int S64_A1W2 = 0, S64_A1B2 = 64 * 128, S64_SIZE = S64_A1B2 + 64;
+};
+
 // Transposed weight packs for the backward's data-gradient GEMMs (dX = dY W = dY (W^T)^T), same
 // fragment format as the forward packs; no biases.  evT holds only lin_event's time-feature columns.
 struct EncWT {
@@ -150,6 +172,9 @@ struct tm_weights {
     tmk::EncWT T;
     float *tbuf = nullptr;
     size_t t_floats = 0;
+    // fold scratch (tm_weights_pack): fp64 a1 W2 [h][2h] and fp32 row-major folded matrices before packing
+    double *fold64 = nullptr;
+    float *fold32 = nullptr;
 };
 
 // encoder_train.hip: transposed packs (tm_weights_create / _free) and the one-launch packing of every tensor

@@ -33,7 +33,7 @@ struct PackJob {
     int32_t so, sc, nout, k, nt, nq;
     int64_t begin;
 };
-constexpr int MAX_PACK_JOBS = 40;
+constexpr int MAX_PACK_JOBS = 56;
 struct PackJobs {
     PackJob j[MAX_PACK_JOBS];
     int32_t n;
@@ -59,17 +59,127 @@ __global__ void pack_jobs_kernel(PackJobs J) {
 }
 
 // evc[f] = b[f] + sum_{k >= 16 qt} W[f][k] * cos(0 * w + phi): one wave per output feature, fp64
-// partial sums combined in a fixed butterfly order, one rounding to fp32 (walk_kernel's slot pass)
+// partial sums combined in a fixed butterfly order, one rounding to fp32 (walk_kernel's slot pass);
+// devc[f] = the same sum without the bias (the table-mode slot pass: the edge-table row carries the bias)
 __global__ void __launch_bounds__(64) evc_par_kernel(const float *__restrict__ W, const float *__restrict__ b,
                                                      const float *__restrict__ phase, int de, int dn, int kev, int qt,
-                                                     float *__restrict__ out) {
+                                                     float *__restrict__ out, float *__restrict__ dout) {
     const int f = blockIdx.x, lane = threadIdx.x;
     double acc = 0.0;
     if (f < dn)
         for (int k = 16 * qt + lane; k < kev; k += 64) acc += (double)W[(int64_t)f * kev + k] * (double)cos_rd(phase[k - de - 3]);
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-    if (lane == 0) out[f] = f < dn ? (float)(acc + (double)b[f]) : 0.f;
+    if (lane == 0) {
+        out[f] = f < dn ? (float)(acc + (double)b[f]) : 0.f;
+        dout[f] = f < dn ? (float)acc : 0.f;
+    }
 }
+
+// ------------------------------------------------------------------ folded layers of the fused walk kernel
+// (EncW::w1d ..., tmk::FoldLay), fp64 products of the reference's fp32 weights rounded once.  Raw tensors
+// t[] in tm_weights_pack's order: 4/5 event_conv.MLP.2 (g2), 6/7 attention.W1, 8/9 attention.W2,
+// 10/11 attention.MLP.0 (a1), 12/13 attention.MLP.3|2 (a2), 14/15 MLP.0 (m1).  h = 64.
+struct FoldIn {
+    const float *g2w, *g2b, *w1, *b1, *w2, *b2, *a1, *ba1, *a2, *ba2, *m1, *bm1;
+};
+
+// stage 1: a1 W2 [64][128] and a1 b2 [64] in fp64
+__global__ void __launch_bounds__(256) fold1_kernel(FoldIn F, double *__restrict__ s64) {
+    constexpr int H = 64, H2 = 128;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < H * H2) {
+        const int o = i / H2, k = i % H2;
+        double acc = 0.0;
+        for (int j = 0; j < H2; ++j) acc += (double)F.a1[o * H2 + j] * (double)F.w2[j * H2 + k];
+        s64[FoldLay::S64_A1W2 + i] = acc;
+    } else if (i < H * H2 + H) {
+        const int o = i - H * H2;
+        double acc = 0.0;
+        for (int j = 0; j < H2; ++j) acc += (double)F.a1[o * H2 + j] * (double)F.b2[j];
+        s64[FoldLay::S64_A1B2 + o] = acc;
+    }
+}
+
+// stage 2: every folded matrix (fp32 row-major into s32, packed afterwards) and vector (into buf)
+// X blockdiag(g2, g2)[o][k] = sum_{j < 64} X[o][64 (k >= 64) + j] g2[j][k % 64]
+__global__ void __launch_bounds__(256) fold2_kernel(FoldIn F, const double *__restrict__ s64, float *__restrict__ s32,
+                                                    float *__restrict__ buf) {
+    constexpr int H = 64, H2 = 128, HM = 76;
+    using L = FoldLay;
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    auto bd = [&](auto row, int k) {   // row(j) = X[o][j], j < 128
+        double acc = 0.0;
+        const int base = k >= H ? H : 0, kk = k % H;
+        for (int j = 0; j < H; ++j) acc += (double)row(base + j) * (double)F.g2w[j * H + kk];
+        return acc;
+    };
+    auto bvec = [&](auto row) {        // sum_j X[o][j] [bg2; bg2][j]
+        double acc = 0.0;
+        for (int j = 0; j < H2; ++j) acc += (double)row(j) * (double)F.g2b[j % H];
+        return acc;
+    };
+    if (i < H2 * H2) {                                   // W1D [128][128]
+        const int o = i / H2, k = i % H2;
+        s32[L::S_W1D + i] = (float)bd([&](int j) { return F.w1[o * H2 + j]; }, k);
+        return;
+    }
+    i -= H2 * H2;
+    if (i < H2 * H2) {                                   // G^T: row k, column o = G[o][k]
+        const int k = i / H2, o = i % H2;
+        s32[L::S_GT + i] = (float)bd([&](int j) { return F.w2[o * H2 + j]; }, k);
+        return;
+    }
+    i -= H2 * H2;
+    if (i < H * H2) {                                    // A1D [64][128]
+        const int o = i / H2, k = i % H2;
+        s32[L::S_A1D + i] = (float)bd([&](int j) { return F.a1[o * H2 + j]; }, k);
+        return;
+    }
+    i -= H * H2;
+    if (i < H * H2) {                                    // A1G = (a1 W2) blockdiag(g2, g2) [64][128]
+        const int o = i / H2, k = i % H2;
+        s32[L::S_A1G + i] = (float)bd([&](int j) { return s64[L::S64_A1W2 + o * H2 + j]; }, k);
+        return;
+    }
+    i -= H * H2;
+    if (i < HM * H) {                                    // M1A2 = m1[:, :64] a2 [76][64]
+        const int o = i / H, k = i % H;
+        double acc = 0.0;
+        for (int j = 0; j < H; ++j) acc += (double)F.m1[o * HM + j] * (double)F.a2[j * H + k];
+        s32[L::S_M1A2 + i] = (float)acc;
+        return;
+    }
+    i -= HM * H;
+    if (i < H2) {                                        // b1d = W1 [bg2; bg2] + b1
+        buf[L::B1D + i] = (float)(bvec([&](int j) { return F.w1[i * H2 + j]; }) + (double)F.b1[i]);
+        return;
+    }
+    i -= H2;
+    if (i < H2) {                                        // beta = W2 [bg2; bg2] + b2
+        buf[L::BETA + i] = (float)(bvec([&](int j) { return F.w2[i * H2 + j]; }) + (double)F.b2[i]);
+        return;
+    }
+    i -= H2;
+    if (i < H) {                                         // cp = a1 [bg2;bg2] + a1 W2 [bg2;bg2] + a1 b2 + ba1
+        const double a = bvec([&](int j) { return F.a1[i * H2 + j]; });
+        const double g = bvec([&](int j) { return s64[L::S64_A1W2 + i * H2 + j]; });
+        buf[L::CP + i] = (float)(a + g + s64[L::S64_A1B2 + i] + (double)F.ba1[i]);
+        return;
+    }
+    i -= H;
+    if (i < 13 * 80) {                                   // tc[c][o] = m1[o][64 + c] + bm1[o] + m1[o][:64] ba2
+        const int c = i / 80, o = i % 80;
+        float v = 0.f;
+        if (o < HM) {
+            double acc = (double)F.bm1[o];
+            for (int j = 0; j < H; ++j) acc += (double)F.m1[o * HM + j] * (double)F.ba2[j];
+            if (c < 12) acc += (double)F.m1[o * HM + H + c];
+            v = (float)acc;
+        }
+        buf[L::TC + i] = v;
+    }
+}
+constexpr int FOLD2_N = 2 * 128 * 128 + 2 * 64 * 128 + 76 * 64 + 128 + 128 + 64 + 13 * 80;
 
 // ------------------------------------------------------------------ head backward
 struct HeadBwdOut {
@@ -943,9 +1053,23 @@ void pack_all_weights(tm_weights *w, const float *const *t, hipStream_t s) {
     frag(w->T.m2T, t[16], 1, hm);
     frag(w->T.d1T, t[20] + de, 1, de + dn);
     frag(w->T.d2T, t[22], 1, h);
+    // the fused walk kernel's folded layers (hid_dim 64): fp64 products first, then packed with the rest
+    const bool fold = h == HID && w->fold64 && w->fold32;
+    if (fold) {
+        using L = FoldLay;
+        const FoldIn F{t[4], t[5], t[6], t[7], t[8], t[9], t[10], t[11], t[12], t[13], t[14], t[15]};
+        fold1_kernel<<<dim3((64 * 128 + 64 + 255) / 256), 256, 0, s>>>(F, w->fold64);
+        fold2_kernel<<<dim3((FOLD2_N + 255) / 256), 256, 0, s>>>(F, w->fold64, w->fold32, w->buf);
+        frag(w->P.w1d, w->fold32 + L::S_W1D, h2, 1);
+        frag(w->P.gt, w->fold32 + L::S_GT, h2, 1);
+        frag(w->P.a1d, w->fold32 + L::S_A1D, h2, 1);
+        frag(w->P.a1g, w->fold32 + L::S_A1G, h2, 1);
+        frag(w->P.m1a2, w->fold32 + L::S_M1A2, h, 1);
+    }
     P.total = total;
     pack_jobs_kernel<<<dim3((unsigned)std::min<int64_t>((total + 255) / 256, 1024)), 256, 0, s>>>(P);
-    evc_par_kernel<<<dim3(r16(dn)), 64, 0, s>>>(t[0], t[1], t[27], de, dn, kev, w->P.qt, const_cast<float *>(w->P.evc));
+    evc_par_kernel<<<dim3(r16(dn)), 64, 0, s>>>(t[0], t[1], t[27], de, dn, kev, w->P.qt, const_cast<float *>(w->P.evc),
+                                                const_cast<float *>(w->P.devc));
 }
 
 void train_packs_free(tm_weights *w) {

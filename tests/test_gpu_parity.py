@@ -519,7 +519,7 @@ def test_fused_events_sizes_vs_oracle(tm, N, M):
 
 @pytest.mark.parametrize("de", [32, 172])
 def test_edge_table_path(tm, de):
-    """tm_edge_tables' edge table = lin_event.W[:, :de] E[e] (fp64 reference, 1e-5), zero past dn;
+    """tm_edge_tables' edge table = lin_event.W[:, :de] E[e] + lin_event.b (fp64 reference, 1e-5), zero past dn;
     the pipeline's table mode (lin_event's edge part read per edge id) agrees with the per-walk
     product (edge_table=False, the drop-in TempME.forward arithmetic) within the 1e-5 contract, and
     its gate table is unchanged."""
@@ -546,7 +546,7 @@ def test_edge_table_path(tm, de):
     assert pt.etab is not None and pp.etab is None
     w = ex.event_conv.lin_event.weight.detach().double().cpu()
     ef = torch.from_numpy(g["e_feat"]).double()[:pt.etab.shape[0]]
-    want = ef @ w[:, :de].T
+    want = ef @ w[:, :de].T + ex.event_conv.lin_event.bias.detach().double().cpu()
     got = pt.etab.double().cpu()
     np.testing.assert_allclose(got[:, :172].numpy(), want.numpy(), rtol=1e-5, atol=1e-6)
     assert (got[:, 172:] == 0).all()

@@ -51,8 +51,8 @@ for s in "$@"; do
                     echo "$n round $r: $(grep -o '"walk_kernel": {"avg_ms": [0-9.]*' gpurun_out/ab_${n}_$r.log) $(grep -o '"events_kernel": {"avg_ms": [0-9.]*' gpurun_out/ab_${n}_$r.log) $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_${n}_$r.log)" | tee -a gpurun_out/ab.txt
                 done
             done ;;
-        stamps)  # phase stamps of every -DTM_STAMPS build in tempme_amd/lib/ab/
-            for so in tempme_amd/lib/ab/*.so; do
+        stamps)  # phase stamps of every -DTM_STAMPS build in tempme_amd/lib/ab_st/
+            for so in tempme_amd/lib/ab_st/*.so; do
                 n=$(basename "$so" .so)
                 TEMPME_LIB="$PWD/$so" step stamps_$n 300 python tools/stamps.py
                 { echo "== $n: $(grep -o '"walk_kernel": {"avg_ms": [0-9.]*' gpurun_out/stamps_$n.log)"; grep -E "^(slot|walk) " gpurun_out/stamps_$n.log; } | tee -a gpurun_out/stamps.txt
