@@ -82,7 +82,7 @@ def flops_model(de, dn, h, N, M, etab=False):
     per walk position 0/1: lin_event, event_gcn's first layer on both branches, the folded attention.MLP.0
     product A1G (h x 2h) and the score dot (2h); per hop-1 slot (shared by its M walks): position 2's
     lin_event over the K steps below qt (the all-time-feature steps are a bias at dt = 0), event_gcn's
-    first layer, the folded W1D and G^T (2h x 2h each), A1D (h x 2h) and the beta dot; per walk the head:
+    first layer, the folded kv = G^T W1D (2h x 2h), A1D (h x 2h) and the u dot; per walk the head:
     MLP.0 folded with attention.MLP.3 (h+12 x h), MLP.3 (h x h+12) and the last row (h)."""
     kev = de + 3 + dn
     per_pos_gcn = kev * dn + 2 * (dn * h + h * h)                       # lin_event + event_gcn MLP x2
@@ -92,7 +92,7 @@ def flops_model(de, dn, h, N, M, etab=False):
     qt = (de + 3 + 15) // 16
     edge = de * dn if etab else 0
     pos = kev * dn - edge + 2 * dn * h
-    slot = kev * dn - max(kev - 16 * qt, 0) * dn - edge + 2 * dn * h + h * 2 * h + 2 * (2 * h) ** 2 + 2 * h
+    slot = kev * dn - max(kev - 16 * qt, 0) * dn - edge + 2 * dn * h + h * 2 * h + (2 * h) ** 2 + 2 * h
     exec_walk = 2 * (2 * (pos + h * 2 * h + 2 * h) + slot / M + (h + 12) * h + h * (h + 12) + h)
     walk = 2 * (3 * per_pos_gcn + per_walk_head)
     if etab:

@@ -184,27 +184,16 @@ __device__ __forceinline__ int32_t draw(Key k, uint32_t stage, uint32_t event, u
     return (int32_t)(((uint64_t)u * (uint64_t)high) >> 32);
 }
 
-// cos of an fp32 argument, branch-free: exact reduction by pi in fp64 (the 1.5*2^52 shifter gives
-// j = rint(x/pi) and its parity in the low word; pi split in two doubles, valid for |x| < 2^40),
-// then the even Taylor polynomial of cos to r^12 on [-pi/2, pi/2] (truncation 6.4e-9).  Max abs
-// error vs cos of the same fp32 argument ~1.7e-7 at every magnitude (torch's cosf: 3.6e-8); no
-// slow path, so it interleaves with the MFMAs it feeds instead of branching per element.
+// cos of an fp32 argument, branch-free: the argument in revolutions, x / (2 pi), reduced to [-1/2, 1/2]
+// in fp64 (relative error 2^-53: |x| < 2^40 keeps the reduced fraction exact to ~1e-9), then the
+// hardware v_cos_f32 (input in revolutions).  Max abs error vs cos of the same fp32 argument 1.8e-7
+// over the time encoder's whole argument range (micro/cosacc.hip, profiles/r03_cos_accuracy.txt: the
+// round-2 fp64-reduction + r^12 polynomial form measured 1.5e-7 at about twice the VALU cost; torch's
+// cosf 3.6e-8).  No slow path, so it interleaves with the MFMAs it feeds.
 __device__ __forceinline__ float cos_rd(float xf) {
-    const double x = (double)xf;
-    const double t = __builtin_fma(x, 0.31830988618379067154, 6755399441055744.0);
-    const double j = t - 6755399441055744.0;
-    double r = __builtin_fma(-j, 3.141592653589793116, x);
-    r = __builtin_fma(-j, 1.2246467991473532e-16, r);
-    const float rf = (float)r, z = rf * rf;
-    float c = 2.08767569878681e-09f;                       // 1/12!
-    c = __builtin_fmaf(c, z, -2.755731922398589e-07f);     // -1/10!
-    c = __builtin_fmaf(c, z, 2.48015873015873e-05f);       // 1/8!
-    c = __builtin_fmaf(c, z, -1.388888888888889e-03f);     // -1/6!
-    c = __builtin_fmaf(c, z, 4.166666666666666e-02f);      // 1/4!
-    c = __builtin_fmaf(c, z, -0.5f);
-    c = __builtin_fmaf(c, z, 1.0f);
-    const uint32_t odd = (uint32_t)__double2loint(t) << 31;
-    return __uint_as_float(__float_as_uint(c) ^ odd);
+    const double u = (double)xf * 0.15915494309189533577;
+    const double f = u - __builtin_rint(u);
+    return __builtin_amdgcn_cosf((float)f);
 }
 
 // ------------------------------------------------------------------ lookups

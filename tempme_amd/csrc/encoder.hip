@@ -566,9 +566,9 @@ __device__ __forceinline__ void cgemm2(__amdgpu_buffer_rsrc_t wr, const floatx4 
 template <int NQE, int NTD>
 struct WalkConsts {
     static constexpr int XW = 0, XP = XW + 16 * NQE, EV = XP + 16 * NQE, EVC = EV + 16 * NTD, DEVC = EVC + 16 * NTD,
-                         G1 = DEVC + 16 * NTD, G1C = G1 + HID, B1D = G1C + HID, CP = B1D + 2 * HID,
-                         BETA = CP + HID, M2 = BETA + 2 * HID, M3 = M2 + HID, TC = M3 + HID, M3B = TC + 13 * 80,
-                         SIZE = M3B + 4;
+                         G1 = DEVC + 16 * NTD, G1C = G1 + HID, V0 = G1C + HID, CP = V0 + 2 * HID,
+                         U = CP + HID, M2 = U + 2 * HID, M3 = M2 + HID, TC = M3 + HID, M3B = TC + 13 * 80,
+                         C0 = M3B + 1, SIZE = M3B + 4;
 };
 
 template <int NQE, int NTD>
@@ -583,14 +583,16 @@ __device__ __forceinline__ void load_consts(const EncW &P, float *cs) {
         else if (i < C::DEVC) v = P.evc[i - C::EVC];
         else if (i < C::G1) v = P.devc[i - C::DEVC];
         else if (i < C::G1C) v = P.g1.b[i - C::G1];
-        else if (i < C::B1D) v = P.g1.b[i - C::G1C];
-        else if (i < C::CP) v = P.b1d[i - C::B1D];
-        else if (i < C::BETA) v = P.cp[i - C::CP];
-        else if (i < C::M2) v = P.beta[i - C::BETA];
+        else if (i < C::V0) v = P.g1.b[i - C::G1C];
+        else if (i < C::CP) v = P.v0[i - C::V0];
+        else if (i < C::U) v = P.cp[i - C::CP];
+        else if (i < C::M2) v = P.u[i - C::U];
         else if (i < C::M3) v = P.m2.b[i - C::M2];
         else if (i < C::TC) v = P.m3w[i - C::M3];
         else if (i < C::M3B) v = P.tc[i - C::TC];
-        else v = P.m3b[0];
+        else if (i == C::M3B) v = P.m3b[0];
+        else if (i == C::C0) v = P.c0[0];
+        else v = 0.f;
         cs[i] = v;
     }
 }
@@ -931,9 +933,9 @@ struct HeadIn {
 
 // per-wave LDS stash of a slot's position-2 results, read by its walks' position-0/1 passes
 struct Stash {
-    floatx4 V[8][64];     // G^T Wp: the attention score of position i is V . H_i + cw
+    floatx4 V[8][64];     // kv H_2 + v0 (= G^T Wp): the attention score of position i is V . H_i + cw
     floatx4 P2[4][64];    // A1D H_2 + cp: attention.MLP.0's input part that does not depend on alpha
-    float cw[64];         // Wp . beta
+    float cw[64];         // u . H_2 + c0 (= Wp . beta)
 };
 
 // Attention head + final MLP for the 16 walks of this wave (explainer_new.py:789-846 and :121-125,
@@ -1024,7 +1026,7 @@ __global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
     if (unit * 16 >= a.n_slots) return;                 // whole wave idle (wave-uniform)
     Stash &st = stash[threadIdx.x >> 6];
     // every weight fragment off one buffer resource (WalkLay offsets from the folded region's base)
-    const auto wr = wrsrc(P.w1d.w);
+    const auto wr = wrsrc(P.kv.w);
     floatx4 R0[4];                                      // A1G H_0, carried to the position-1 pass
     float s0 = 0.f;
     const int n_pass = 1 + 2 * a.M;
@@ -1033,6 +1035,9 @@ __global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
     float4 et[ETAB_N(QE0)];
     if constexpr (QE0 == 0) load_ef(a, cur.e, ef);
     else load_et<QE0>(a, cur.e, et);
+#ifdef TM_STAMPS
+    const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
     // pass 0: position 2 once per slot (walk j*M carries it); then per walk m: position 0, position 1
 #pragma nounroll
     for (int pass = 0; pass < n_pass; ++pass) {
@@ -1060,29 +1065,26 @@ __global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
         cur = nxt;
         TM_STAMP(6);
         if (p == 2) {
-            // P2 = A1D H_2 + cp; Wp = W1D H_2 + b1d (attention.W1 of F_2); V = G^T Wp; cw = Wp . beta
+            // P2 = A1D H_2 + cp; V = kv H_2 + v0 (= G^T Wp); cw = u . H_2 + c0 (= Wp . beta)
             floatx4 P2[4];
 #pragma unroll
             for (int t = 0; t < 4; ++t) P2[t] = ldsx4(cs + C::CP, t);
             cgemm<4, 8, 8, FoldLay::A1D>(wr, H, P2);
-            floatx4 Wp[8];
-#pragma unroll
-            for (int t = 0; t < 8; ++t) Wp[t] = ldsx4(cs + C::B1D, t);
-            cgemm<8, 8, 8, FoldLay::W1D>(wr, H, Wp);
             floatx4 V[8];
 #pragma unroll
-            for (int t = 0; t < 8; ++t) V[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-            cgemm<8, 8, 8, FoldLay::GT>(wr, Wp, V);
+            for (int t = 0; t < 8; ++t) V[t] = ldsx4(cs + C::V0, t);
+            cgemm<8, 8, 8, FoldLay::KV>(wr, H, V);
+            TM_STAMP(7);
             float cw = 0.f;
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
-                const float4 b = lds4(cs + C::BETA, t);
-                cw = __builtin_fmaf(Wp[t][0], b.x, cw);
-                cw = __builtin_fmaf(Wp[t][1], b.y, cw);
-                cw = __builtin_fmaf(Wp[t][2], b.z, cw);
-                cw = __builtin_fmaf(Wp[t][3], b.w, cw);
+                const float4 b = lds4(cs + C::U, t);
+                cw = __builtin_fmaf(H[t][0], b.x, cw);
+                cw = __builtin_fmaf(H[t][1], b.y, cw);
+                cw = __builtin_fmaf(H[t][2], b.z, cw);
+                cw = __builtin_fmaf(H[t][3], b.w, cw);
             }
-            cw = col_sum(cw);
+            cw = col_sum(cw) + cs[C::C0];
 #pragma unroll
             for (int t = 0; t < 8; ++t) st.V[t][lane] = V[t];
 #pragma unroll
@@ -1112,18 +1114,24 @@ __global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
         }
 #endif
     }
+#ifdef TM_STAMPS
+    // in-kernel clock: shader-clock ticks over 100 MHz real-time ticks of the wave's pass loop
+    if (lane == 0 && blockIdx.x >= 512 && blockIdx.x < 1024) {
+        atomicAdd(&g_st[0][9], __builtin_amdgcn_s_memtime() - clk_t0);
+        atomicAdd(&g_st[1][9], __builtin_amdgcn_s_memrealtime() - clk_r0);
+    }
+#endif
 }
 
 // host: the live weight pointers are where WalkLay<nqe> puts them
 static bool walk_layout_ok(const EncW &P, int nqe) {
-    const float *base = reinterpret_cast<const float *>(P.w1d.w);
+    const float *base = reinterpret_cast<const float *>(P.kv.w);
     auto at = [&](const float4 *w, int off) { return reinterpret_cast<const float *>(w) == base + off; };
     const int ev = FoldLay::SIZE, g1 = ev + 11 * nqe * 256 + 176, m2 = g1 + 4 * 11 * 256 + 64 + 4 * 4 * 256 + 64 +
                                                                      2 * (8 * 8 * 256 + 128) + 4 * 8 * 256 + 64 +
                                                                      4 * 4 * 256 + 64 + 5 * 5 * 256 + 80;
-    return at(P.ev.w, ev) && at(P.g1.w, g1) && at(P.m2.w, m2) && at(P.gt.w, FoldLay::GT) &&
-           at(P.a1d.w, FoldLay::A1D) && at(P.a1g.w, FoldLay::A1G) && at(P.m1a2.w, FoldLay::M1A2) &&
-           P.g1.nt == 4 && P.g1.nq == 11 && P.m2.nt == 4 && P.m2.nq == 5 && P.ev.nt == 11 && P.ev.nq == nqe;
+    return at(P.ev.w, ev) && at(P.g1.w, g1) && at(P.m2.w, m2) && at(P.a1d.w, FoldLay::A1D) &&
+           at(P.a1g.w, FoldLay::A1G) && at(P.m1a2.w, FoldLay::M1A2) && P.g1.nt == 4 && P.g1.nq == 11 && P.m2.nt == 4 && P.m2.nq == 5 && P.ev.nt == 11 && P.ev.nq == nqe;
 }
 
 // ------------------------------------------------------------------ per-edge dependency gate table
@@ -1387,8 +1395,7 @@ extern "C" int tm_weights_create(int32_t de, int32_t dn, int32_t h, int device, 
         struct FL {
             Lin *lin;
             int off, nout, k;
-        } fl[] = {{&P.w1d, F::W1D, h2, h2}, {&P.gt, F::GT, h2, h2}, {&P.a1d, F::A1D, h, h2}, {&P.a1g, F::A1G, h, h2},
-                  {&P.m1a2, F::M1A2, hm, h}};
+        } fl[] = {{&P.kv, F::KV, h2, h2}, {&P.a1d, F::A1D, h, h2}, {&P.a1g, F::A1G, h, h2}, {&P.m1a2, F::M1A2, hm, h}};
         for (auto &f : fl) {
             f.lin->w = reinterpret_cast<const float4 *>(w->buf + f.off);
             f.lin->b = nullptr;
@@ -1397,8 +1404,9 @@ extern "C" int tm_weights_create(int32_t de, int32_t dn, int32_t h, int device, 
             f.lin->nt = r16(f.nout) / 16;
             f.lin->nq = r16(f.k) / 16;
         }
-        P.b1d = w->buf + F::B1D;
-        P.beta = w->buf + F::BETA;
+        P.v0 = w->buf + F::V0;
+        P.u = w->buf + F::U;
+        P.c0 = w->buf + F::C0;
         P.cp = w->buf + F::CP;
         P.tc = w->buf + F::TC;
         (void)hipGetDevice(&prev);

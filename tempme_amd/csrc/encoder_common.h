@@ -30,13 +30,17 @@ struct EncW {
     // lin_event's folded time steps alone (evc - bias, fp64 sum rounded once): the table-mode slot pass,
     // whose edge-table row already carries the bias
     const float *devc;
-    // fused walk kernel (eval, hid_dim 64): layers folded at pack time in fp64 (tm_weights_pack) --
-    // F = blockdiag(g2, g2) H + [bg2; bg2] (H = event_gcn's relu'd hidden layer of both branches),
-    // W1D = W1 blockdiag(g2,g2), G = W2 blockdiag(g2,g2) (packed transposed), A1D = a1 blockdiag(g2,g2),
-    // A1G = a1 G, M1A2 = MLP.0[:, :h] a2; vectors b1d = W1 [bg2;bg2] + b1, beta = W2 [bg2;bg2] + b2,
-    // cp = a1 [bg2;bg2] + a1 beta + ba1, tc[c] = MLP.0[:, h + c] + bm1 + MLP.0[:, :h] ba2 (row 12: no category)
-    Lin w1d, gt, a1d, a1g, m1a2;
-    const float *b1d, *beta, *cp, *tc;
+    // fused walk kernel (eval, hid_dim 64): layers folded at pack time in fp64 (tm_weights_pack).  With
+    // H = event_gcn's relu'd hidden layer of both branches, F = blockdiag(g2, g2) H + [bg2; bg2];
+    // W1D = W1 blockdiag(g2,g2), b1d = W1 [bg2;bg2] + b1 (so Wp = W1 F_2 + b1 = W1D H_2 + b1d),
+    // G = W2 blockdiag(g2,g2), beta = W2 [bg2;bg2] + b2 (Q_i = W2 F_i + b2 = G H_i + beta).  The score
+    // Wp . Q_i = V . H_i + cw with V = G^T Wp = kv H_2 + v0 (kv = G^T W1D, v0 = G^T b1d) and
+    // cw = Wp . beta = u . H_2 + c0 (u = W1D^T beta, c0 = b1d . beta); attention.MLP.0 of the
+    // attention output = P2 + alpha_0 R_0 + alpha_1 R_1 with P2 = A1D H_2 + cp, R_i = A1G H_i
+    // (A1D = a1 blockdiag(g2,g2), A1G = a1 G, cp = a1 [bg2;bg2] + a1 beta + ba1; alpha_0 + alpha_1 = 1);
+    // M1A2 = MLP.0[:, :h] a2, tc[c] = MLP.0[:, h + c] + bm1 + MLP.0[:, :h] ba2 (row 12: no category).
+    Lin kv, a1d, a1g, m1a2;
+    const float *v0, *u, *c0, *cp, *tc;
     // constructor variants (explainer_new.py:103-105, :121, :141): tg = use_temporal_guidance (0: the plain
     // Attention, no time weighting of the scores), dep = use_dependency_aware_sampling (0: no gate)
     int tg = 1, dep = 1;
@@ -128,13 +132,16 @@ __device__ __forceinline__ float gate_logit_lds(const float *g2, const float *w3
 // Folded region at the start of tm_weights::buf (float offsets; hid_dim 64): the fused walk kernel's
 // packs and vectors (EncW::w1d ...), then the reference layers in tm_weights_create's order.
 struct FoldLay {
-    static constexpr int W1D = 0, B1D = W1D + 8 * 8 * 256, GT = B1D + 128, BETA = GT + 8 * 8 * 256,
-                         A1D = BETA + 128, CP = A1D + 4 * 8 * 256, A1G = CP + 64, M1A2 = A1G + 4 * 8 * 256,
-                         TC = M1A2 + 5 * 4 * 256, SIZE = (TC + 13 * 80 + 63) & ~63;
+    static constexpr int KV = 0, V0 = KV + 8 * 8 * 256, U = V0 + 128, C0 = U + 128, A1D = C0 + 4, CP = A1D + 4 * 8 * 256,
+                         A1G = CP + 64, M1A2 = A1G + 4 * 8 * 256, TC = M1A2 + 5 * 4 * 256,
+                         SIZE = (TC + 13 * 80 + 63) & ~63;
     // fold32 scratch (row-major fp32 matrices before packing)
-    static constexpr int S_W1D = 0, S_GT = S_W1D + 128 * 128, S_A1D = S_GT + 128 * 128, S_A1G = S_A1D + 64 * 128,
-                         S_M1A2 = S_A1G + 64 * 128, S_SIZE = S_M1A2 + 76 * 64;
-    static constexpr int S64_A1W2 = 0, S64_A1B2 = 64 * 128, S64_SIZE = S64_A1B2 + 64;
+    static constexpr int S_KV = 0, S_A1D = S_KV + 128 * 128, S_A1G = S_A1D + 64 * 128, S_M1A2 = S_A1G + 64 * 128,
+                         S_SIZE = S_M1A2 + 76 * 64;
+    // fold64 scratch (stage 1): a1 W2, a1 b2, W1D = W1 blockdiag(g2,g2), G = W2 blockdiag(g2,g2), b1d, beta
+    static constexpr int S64_A1W2 = 0, S64_A1B2 = S64_A1W2 + 64 * 128, S64_W1D = S64_A1B2 + 64,
+                         S64_G = S64_W1D + 128 * 128, S64_B1D = S64_G + 128 * 128, S64_BETA = S64_B1D + 128,
+                         S64_SIZE = S64_BETA + 128;
 };
 
 // Transposed weight packs for the backward's data-gradient GEMMs (dX = dY W = dY (W^T)^T), same

@@ -83,103 +83,136 @@ struct FoldIn {
     const float *g2w, *g2b, *w1, *b1, *w2, *b2, *a1, *ba1, *a2, *ba2, *m1, *bm1;
 };
 
-// stage 1: a1 W2 [64][128] and a1 b2 [64] in fp64
-__global__ void __launch_bounds__(256) fold1_kernel(FoldIn F, double *__restrict__ s64) {
-    constexpr int H = 64, H2 = 128;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < H * H2) {
-        const int o = i / H2, k = i % H2;
-        double acc = 0.0;
-        for (int j = 0; j < H2; ++j) acc += (double)F.a1[o * H2 + j] * (double)F.w2[j * H2 + k];
-        s64[FoldLay::S64_A1W2 + i] = acc;
-    } else if (i < H * H2 + H) {
-        const int o = i - H * H2;
-        double acc = 0.0;
-        for (int j = 0; j < H2; ++j) acc += (double)F.a1[o * H2 + j] * (double)F.b2[j];
-        s64[FoldLay::S64_A1B2 + o] = acc;
-    }
+// X blockdiag(g2, g2)[o][k] = sum_{j < 64} X[o][64 (k >= 64) + j] g2[j][k % 64];  X [bg2; bg2][o]
+template <class Row>
+__device__ __forceinline__ double fold_bd(const FoldIn &F, Row row, int k) {
+    double acc = 0.0;
+    const int base = k >= 64 ? 64 : 0, kk = k % 64;
+    for (int j = 0; j < 64; ++j) acc += (double)row(base + j) * (double)F.g2w[j * 64 + kk];
+    return acc;
+}
+template <class Row>
+__device__ __forceinline__ double fold_bv(const FoldIn &F, Row row) {
+    double acc = 0.0;
+    for (int j = 0; j < 128; ++j) acc += (double)row(j) * (double)F.g2b[j % 64];
+    return acc;
 }
 
-// stage 2: every folded matrix (fp32 row-major into s32, packed afterwards) and vector (into buf)
-// X blockdiag(g2, g2)[o][k] = sum_{j < 64} X[o][64 (k >= 64) + j] g2[j][k % 64]
-__global__ void __launch_bounds__(256) fold2_kernel(FoldIn F, const double *__restrict__ s64, float *__restrict__ s32,
-                                                    float *__restrict__ buf) {
-    constexpr int H = 64, H2 = 128, HM = 76;
+// stage 1 (fp64 scratch): a1 W2 [64][128], a1 b2 [64], W1D [128][128], G [128][128], b1d [128], beta [128]
+constexpr int FOLD1_N = 64 * 128 + 64 + 2 * 128 * 128 + 2 * 128;
+__global__ void __launch_bounds__(256) fold1_kernel(FoldIn F, double *__restrict__ s64) {
     using L = FoldLay;
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    auto bd = [&](auto row, int k) {   // row(j) = X[o][j], j < 128
+    if (i < 64 * 128) {
+        const int o = i / 128, k = i % 128;
         double acc = 0.0;
-        const int base = k >= H ? H : 0, kk = k % H;
-        for (int j = 0; j < H; ++j) acc += (double)row(base + j) * (double)F.g2w[j * H + kk];
-        return acc;
-    };
-    auto bvec = [&](auto row) {        // sum_j X[o][j] [bg2; bg2][j]
+        for (int j = 0; j < 128; ++j) acc += (double)F.a1[o * 128 + j] * (double)F.w2[j * 128 + k];
+        s64[L::S64_A1W2 + i] = acc;
+        return;
+    }
+    i -= 64 * 128;
+    if (i < 64) {
         double acc = 0.0;
-        for (int j = 0; j < H2; ++j) acc += (double)row(j) * (double)F.g2b[j % H];
-        return acc;
-    };
-    if (i < H2 * H2) {                                   // W1D [128][128]
-        const int o = i / H2, k = i % H2;
-        s32[L::S_W1D + i] = (float)bd([&](int j) { return F.w1[o * H2 + j]; }, k);
+        for (int j = 0; j < 128; ++j) acc += (double)F.a1[i * 128 + j] * (double)F.b2[j];
+        s64[L::S64_A1B2 + i] = acc;
         return;
     }
-    i -= H2 * H2;
-    if (i < H2 * H2) {                                   // G^T: row k, column o = G[o][k]
-        const int k = i / H2, o = i % H2;
-        s32[L::S_GT + i] = (float)bd([&](int j) { return F.w2[o * H2 + j]; }, k);
+    i -= 64;
+    if (i < 128 * 128) {
+        const int o = i / 128, k = i % 128;
+        s64[L::S64_W1D + i] = fold_bd(F, [&](int j) { return F.w1[o * 128 + j]; }, k);
         return;
     }
-    i -= H2 * H2;
-    if (i < H * H2) {                                    // A1D [64][128]
-        const int o = i / H2, k = i % H2;
-        s32[L::S_A1D + i] = (float)bd([&](int j) { return F.a1[o * H2 + j]; }, k);
+    i -= 128 * 128;
+    if (i < 128 * 128) {
+        const int o = i / 128, k = i % 128;
+        s64[L::S64_G + i] = fold_bd(F, [&](int j) { return F.w2[o * 128 + j]; }, k);
         return;
     }
-    i -= H * H2;
-    if (i < H * H2) {                                    // A1G = (a1 W2) blockdiag(g2, g2) [64][128]
-        const int o = i / H2, k = i % H2;
-        s32[L::S_A1G + i] = (float)bd([&](int j) { return s64[L::S64_A1W2 + o * H2 + j]; }, k);
+    i -= 128 * 128;
+    if (i < 128) {
+        s64[L::S64_B1D + i] = fold_bv(F, [&](int j) { return F.w1[i * 128 + j]; }) + (double)F.b1[i];
         return;
     }
-    i -= H * H2;
-    if (i < HM * H) {                                    // M1A2 = m1[:, :64] a2 [76][64]
-        const int o = i / H, k = i % H;
+    i -= 128;
+    if (i < 128) s64[L::S64_BETA + i] = fold_bv(F, [&](int j) { return F.w2[i * 128 + j]; }) + (double)F.b2[i];
+}
+
+// stage 2: the packed matrices (fp32 row-major into s32, packed afterwards) and the vectors (into buf)
+constexpr int FOLD2_N = 128 * 128 + 2 * 64 * 128 + 76 * 64 + 128 + 128 + 1 + 64 + 13 * 80;
+__global__ void __launch_bounds__(256) fold2_kernel(FoldIn F, const double *__restrict__ s64, float *__restrict__ s32,
+                                                    float *__restrict__ buf) {
+    using L = FoldLay;
+    const double *W1D = s64 + L::S64_W1D, *G = s64 + L::S64_G, *b1d = s64 + L::S64_B1D, *beta = s64 + L::S64_BETA;
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < 128 * 128) {                                 // kv = G^T W1D
+        const int o = i / 128, k = i % 128;
         double acc = 0.0;
-        for (int j = 0; j < H; ++j) acc += (double)F.m1[o * HM + j] * (double)F.a2[j * H + k];
+        for (int j = 0; j < 128; ++j) acc += G[j * 128 + o] * W1D[j * 128 + k];
+        s32[L::S_KV + i] = (float)acc;
+        return;
+    }
+    i -= 128 * 128;
+    if (i < 64 * 128) {                                  // A1D = a1 blockdiag(g2, g2)
+        const int o = i / 128, k = i % 128;
+        s32[L::S_A1D + i] = (float)fold_bd(F, [&](int j) { return F.a1[o * 128 + j]; }, k);
+        return;
+    }
+    i -= 64 * 128;
+    if (i < 64 * 128) {                                  // A1G = (a1 W2) blockdiag(g2, g2)
+        const int o = i / 128, k = i % 128;
+        s32[L::S_A1G + i] = (float)fold_bd(F, [&](int j) { return s64[L::S64_A1W2 + o * 128 + j]; }, k);
+        return;
+    }
+    i -= 64 * 128;
+    if (i < 76 * 64) {                                   // M1A2 = m1[:, :64] a2 [76][64]
+        const int o = i / 64, k = i % 64;
+        double acc = 0.0;
+        for (int j = 0; j < 64; ++j) acc += (double)F.m1[o * 76 + j] * (double)F.a2[j * 64 + k];
         s32[L::S_M1A2 + i] = (float)acc;
         return;
     }
-    i -= HM * H;
-    if (i < H2) {                                        // b1d = W1 [bg2; bg2] + b1
-        buf[L::B1D + i] = (float)(bvec([&](int j) { return F.w1[i * H2 + j]; }) + (double)F.b1[i]);
+    i -= 76 * 64;
+    if (i < 128) {                                       // v0 = G^T b1d
+        double acc = 0.0;
+        for (int j = 0; j < 128; ++j) acc += G[j * 128 + i] * b1d[j];
+        buf[L::V0 + i] = (float)acc;
         return;
     }
-    i -= H2;
-    if (i < H2) {                                        // beta = W2 [bg2; bg2] + b2
-        buf[L::BETA + i] = (float)(bvec([&](int j) { return F.w2[i * H2 + j]; }) + (double)F.b2[i]);
+    i -= 128;
+    if (i < 128) {                                       // u = W1D^T beta
+        double acc = 0.0;
+        for (int j = 0; j < 128; ++j) acc += W1D[j * 128 + i] * beta[j];
+        buf[L::U + i] = (float)acc;
         return;
     }
-    i -= H2;
-    if (i < H) {                                         // cp = a1 [bg2;bg2] + a1 W2 [bg2;bg2] + a1 b2 + ba1
-        const double a = bvec([&](int j) { return F.a1[i * H2 + j]; });
-        const double g = bvec([&](int j) { return s64[L::S64_A1W2 + i * H2 + j]; });
+    i -= 128;
+    if (i < 1) {                                         // c0 = b1d . beta
+        double acc = 0.0;
+        for (int j = 0; j < 128; ++j) acc += b1d[j] * beta[j];
+        buf[L::C0] = (float)acc;
+        return;
+    }
+    i -= 1;
+    if (i < 64) {                                        // cp = a1 [bg2;bg2] + a1 W2 [bg2;bg2] + a1 b2 + ba1
+        const double a = fold_bv(F, [&](int j) { return F.a1[i * 128 + j]; });
+        const double g = fold_bv(F, [&](int j) { return s64[L::S64_A1W2 + i * 128 + j]; });
         buf[L::CP + i] = (float)(a + g + s64[L::S64_A1B2 + i] + (double)F.ba1[i]);
         return;
     }
-    i -= H;
+    i -= 64;
     if (i < 13 * 80) {                                   // tc[c][o] = m1[o][64 + c] + bm1[o] + m1[o][:64] ba2
         const int c = i / 80, o = i % 80;
         float v = 0.f;
-        if (o < HM) {
+        if (o < 76) {
             double acc = (double)F.bm1[o];
-            for (int j = 0; j < H; ++j) acc += (double)F.m1[o * HM + j] * (double)F.ba2[j];
-            if (c < 12) acc += (double)F.m1[o * HM + H + c];
+            for (int j = 0; j < 64; ++j) acc += (double)F.m1[o * 76 + j] * (double)F.ba2[j];
+            if (c < 12) acc += (double)F.m1[o * 76 + 64 + c];
             v = (float)acc;
         }
         buf[L::TC + i] = v;
     }
 }
-constexpr int FOLD2_N = 2 * 128 * 128 + 2 * 64 * 128 + 76 * 64 + 128 + 128 + 64 + 13 * 80;
 
 // ------------------------------------------------------------------ head backward
 struct HeadBwdOut {
@@ -1058,10 +1091,9 @@ void pack_all_weights(tm_weights *w, const float *const *t, hipStream_t s) {
     if (fold) {
         using L = FoldLay;
         const FoldIn F{t[4], t[5], t[6], t[7], t[8], t[9], t[10], t[11], t[12], t[13], t[14], t[15]};
-        fold1_kernel<<<dim3((64 * 128 + 64 + 255) / 256), 256, 0, s>>>(F, w->fold64);
+        fold1_kernel<<<dim3((FOLD1_N + 255) / 256), 256, 0, s>>>(F, w->fold64);
         fold2_kernel<<<dim3((FOLD2_N + 255) / 256), 256, 0, s>>>(F, w->fold64, w->fold32, w->buf);
-        frag(w->P.w1d, w->fold32 + L::S_W1D, h2, 1);
-        frag(w->P.gt, w->fold32 + L::S_GT, h2, 1);
+        frag(w->P.kv, w->fold32 + L::S_KV, h2, 1);
         frag(w->P.a1d, w->fold32 + L::S_A1D, h2, 1);
         frag(w->P.a1g, w->fold32 + L::S_A1G, h2, 1);
         frag(w->P.m1a2, w->fold32 + L::S_M1A2, h, 1);

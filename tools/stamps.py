@@ -16,9 +16,11 @@ print("events_kernel n=%d" % ev[7], " ".join("%s=%.0f" % (nm, ev[k] / n) for k, 
                                              enumerate(["hop1", "hop2_cuts", "hop2", "walks", "edge_counts"])))
 buf = (C.c_ulonglong * 30)()
 assert _lib.lib().tm_debug_stamps(buf) == 0
-names = ["issue", "xgen+ev_gemm", "A/B+gather", "g1", "g2+ep", "F ep", "W gemm", "head/stash"]
+names = ["issue", "lin_event", "A/B", "g1", "relu", "next row", "folded gemms", "head/stash"]
 for pt, pname in ((2, "slot p2"), (0, "walk p0"), (1, "walk p1")):
     row = buf[pt * 10:(pt + 1) * 10]
     n = max(1, row[8])
     print(pname, "n=%d" % row[8], " ".join("%s=%.0f" % (names[k], row[k] / n) for k in range(8)),
           "total=%.0f" % (sum(row[:8]) / n))
+print("walk_kernel in-kernel clock %.3f GHz (s_memtime / s_memrealtime over each wave's pass loop)"
+      % (0.1 * buf[9] / max(1, buf[19])))
