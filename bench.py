@@ -193,45 +193,61 @@ def khop_alone(pipe, inputs, steps, N, group=8):
 
 
 def dropin_leg(ex, pipe, inputs, B, N, budget_s=3.0):
-    """The reference's eval_one_epoch call pattern through the drop-in surface (temp_exp_main.py:446-452):
-    per batch, ``get_item`` / ``get_item_edge`` of a host pack (numpy, float64 as after the H5 round trip),
-    TempME.forward x3 from numpy, then retrieve_explanation(training=False); timed from host arrays to
-    device outputs.  The pack is the pipeline's own sample of one step's events (tempme_amd/pack.py)."""
+    """The reference's eval_one_epoch call pattern through the drop-in surface (temp_exp_main.py:441-452):
+    per batch ``get_item`` / ``get_item_edge``, TempME.forward x3 (outside no_grad, as the reference calls
+    it), then retrieve_explanation(training=False); timed from the pack to device outputs.  The pack is the
+    pipeline's own sample of one step's events (tempme_amd/pack.py), held two ways: the reference's host
+    float64 arrays (``load_subgraph_margin(args, f)``, ``np.load`` edge counts) and the device pack
+    (``load_subgraph_margin(args, f, device=...)``, ``load_edge``) -- ``value`` is the device pack's rate."""
     from tempme_amd import pack as P
     src, dst, ts, eidx, ev = inputs[0]
+    dev = src.device
     pipe.sample(src, dst, ts, eidx, ev)
     _, cat_d, edge = P.buffers_to_arrays(pipe.buf, int(src.numel()))
 
     class A:
         n_degree = N
-    pk = P.load_subgraph_margin(A(), cat_d)
     cut = ts.cpu().numpy()
     n_b = int(src.numel()) // B
 
-    def one(b):
-        idx = np.arange(b * B, (b + 1) * B)
-        sg_s, sg_t, sg_b, w_s, w_t, w_b, _ = P.get_item(pk, idx)
-        e_s, e_t, e_b = P.get_item_edge(edge, idx)
-        with torch.no_grad():
+    def run(pk, ed):
+        def one(b):
+            idx = np.arange(b * B, (b + 1) * B)
+            sg_s, sg_t, sg_b, w_s, w_t, w_b, _ = P.get_item(pk, idx)
+            e_s, e_t, e_b = P.get_item_edge(ed, idx)
             i_s, i_t, i_b = ex(w_s, cut[idx], e_s), ex(w_t, cut[idx], e_t), ex(w_b, cut[idx], e_b)
             return ex.retrieve_explanation(sg_s, i_s, w_s, sg_t, i_t, w_t, sg_b, i_b, w_b, training=False)
 
-    for b in range(min(n_b, 4)):
-        one(b)
-    torch.cuda.synchronize()
-    done, t0 = 0, time.perf_counter()
-    while True:
-        one(done % n_b)
-        done += 1
-        if done % n_b == 0 or done >= 4 * n_b:
-            torch.cuda.synchronize()
-            if time.perf_counter() - t0 > budget_s or done >= 4 * n_b:
-                break
-    el = time.perf_counter() - t0
-    return {"value": round(done * B / el, 2), "unit": "edges/s", "batches": done, "batch_size": B,
-            "ms_per_batch": round(el / done * 1e3, 3),
-            "what": "eval_one_epoch pattern: get_item from a host float64 pack, TempME.forward x3 from numpy, "
-                    "retrieve_explanation(training=False), per reference batch, host arrays -> device outputs"}
+        for b in range(min(n_b, 4)):
+            one(b)
+        torch.cuda.synchronize()
+        done, t0 = 0, time.perf_counter()
+        while True:
+            one(done % n_b)
+            done += 1
+            if done % n_b == 0 or done >= 4 * n_b:
+                torch.cuda.synchronize()
+                if time.perf_counter() - t0 > budget_s or done >= 4 * n_b:
+                    break
+        el = time.perf_counter() - t0
+        return {"value": round(done * B / el, 2), "batches": done, "ms_per_batch": round(el / done * 1e3, 3)}
+
+    host = run(P.load_subgraph_margin(A(), cat_d), edge)
+    dpk, ded = P.load_subgraph_margin(A(), cat_d, device=dev), P.load_edge(edge, dev)
+    if os.environ.get("TEMPME_DROPIN_PROFILE"):        # host-side profile of the device-pack loop (stderr)
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        run(dpk, ded)
+        pr.disable()
+        pstats.Stats(pr, stream=sys.stderr).sort_stats("tottime").print_stats(30)
+    devp = run(dpk, ded)
+    return {"value": devp["value"], "unit": "edges/s", "batch_size": B, "batches": devp["batches"],
+            "ms_per_batch": devp["ms_per_batch"], "host_pack": host,
+            "what": "eval_one_epoch pattern: get_item / get_item_edge, TempME.forward x3 (grad enabled, eval mode), "
+                    "retrieve_explanation(training=False) per reference batch; value = device pack "
+                    "(load_subgraph_margin(..., device=)), host_pack = the reference's host float64 arrays"}
 
 
 def _cpu_cores():

@@ -209,6 +209,9 @@ def ptr(t):
 
 
 def stream_ptr(device=None):
+    """hipStream_t of the current stream of `device` (torch's raw accessor: no Stream object per call)."""
+    if isinstance(device, torch.device) and device.index is not None:
+        return C.c_void_p(torch._C._cuda_getCurrentRawStream(device.index))
     return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 

@@ -97,6 +97,8 @@ class event_gcn(nn.Module):  # noqa: N801  (reference name, kept for state_dict 
 
 def _to(x, device, dtype):
     if isinstance(x, torch.Tensor):
+        if x.dtype == dtype and x.device == device:
+            return x
         return x.to(device=device, dtype=dtype)
     return torch.from_numpy(np.ascontiguousarray(x)).to(device=device, dtype=dtype)
 
@@ -151,6 +153,19 @@ class _Stager:
 
 
 _STAGE = _Stager()
+
+# Generation of the process's module/parameter registrations (torch's global registration hooks fire on
+# every submodule or parameter assignment, load_state_dict(assign=True) included): TempME's cached weight
+# list is re-validated only when it moved, instead of walking its ~100 links on every call.
+_REG_GEN = [0]
+
+
+def _bump_gen(*_args):
+    _REG_GEN[0] += 1
+
+
+torch.nn.modules.module.register_module_parameter_registration_hook(_bump_gen)
+torch.nn.modules.module.register_module_module_registration_hook(_bump_gen)
 
 
 def _to_many(device, *items):
@@ -214,12 +229,22 @@ class TempME(nn.Module):
 
     # ------------------------------------------------------------------ HIP plumbing
     def _dev(self):
-        return L.require_device(self.device)
+        d = self.__dict__.get("_dev_cache")
+        if d is None or d[0] is not self.device:
+            d = self.__dict__["_dev_cache"] = (self.device, L.require_device(self.device))
+        return d[1]
 
     def _needs_autograd(self):
         """Training mode, or a forward whose result must carry gradients to the explainer's
-        parameters (temp_exp_main.py:605-631): the autograd formulation runs then."""
-        return self.training or (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()))
+        parameters (temp_exp_main.py:605-631): the autograd formulation runs then.  Only the parameters
+        the forward / explanation read matter (the cached weight list; no walk over every submodule)."""
+        if self.training:
+            return True
+        if not torch.is_grad_enabled():
+            return False
+        if self.if_cat and self.hid_dim == 64:
+            return any(p.requires_grad for p in self._weight_list())
+        return any(p.requires_grad for p in self.parameters())
 
     def _hip_eval_ok(self):
         """The eval kernels cover every constructor variant with hid_dim == 64 and the category feature
@@ -254,11 +279,14 @@ class TempME(nn.Module):
         nn.Parameter(...)``, ``load_state_dict(..., assign=True)``) or moving the module rebuilds it."""
         c = self.__dict__.get("_wl_cache")
         if c is not None:
-            wl, links = c
+            wl, links, gen = c
+            if gen == _REG_GEN[0]:
+                return wl
             if all(d.get(k) is v for d, k, v in links):
+                self.__dict__["_wl_cache"] = (wl, links, _REG_GEN[0])
                 return wl
         wl, links = self._build_weight_list()
-        self.__dict__["_wl_cache"] = (wl, links)
+        self.__dict__["_wl_cache"] = (wl, links, _REG_GEN[0])
         return wl
 
     def _weight_paths(self):
@@ -318,6 +346,7 @@ class TempME(nn.Module):
             arr = (L.C.c_void_p * L.N_WEIGHTS)(*[w.data_ptr() for w in self._raw])
             L.check(L.lib().tm_weights_pack(self._packed.h, arr, L.stream_ptr(dev)), "tm_weights_pack")
             self._packed_key = key
+            self._prep_dirty = True
         return self._packed.h
 
     def feature_tables(self):
@@ -327,16 +356,17 @@ class TempME(nn.Module):
             self._n_tab = self.node_raw_embed.weight.detach().to(device=dev, dtype=torch.float32).contiguous()
             self._e_tab = self.edge_raw_embed.weight.detach().to(device=dev, dtype=torch.float32).contiguous()
             self._tables_key = key
+            self._prep_dirty = True
         return self._n_tab, self._e_tab
 
-    def dropin_edge_table(self):
+    def dropin_edge_table(self, w=None):
         """The drop-in forward's table mode: lin_event's edge-feature product W[:, :de] E(e) for every row of
         the edge-feature table (tm_edge_feature_table), rebuilt only when the weights or the table change;
         None when the encoder dims have no table mode or TEMPME_DROPIN_TABLE=0."""
         import os
         if os.environ.get("TEMPME_DROPIN_TABLE", "1") == "0":
             return None
-        w = self.packed_weights()
+        w = self.packed_weights() if w is None else w
         cols = L.lib().tm_edge_table_cols(w)
         if not cols:
             return None
@@ -348,46 +378,47 @@ class TempME(nn.Module):
             L.check(L.lib().tm_edge_feature_table(w, L.ptr(et), int(et.shape[0]), L.ptr(self._dropin_etab),
                                                   L.stream_ptr(dev)), "tm_edge_feature_table")
             self._dropin_etab_key = key
+            self._prep_dirty = True
         return self._dropin_etab
 
     def encoder_fwd(self, node6, eid3, ts3, cat, cut, cnt, n_groups, B, W, out=None, workspace=None, M=1,
-                    etab=None):
+                    etab=None, w=None):
         """tm_encoder_fwd on device tensors (int32 node6 [G,B,W,6], eid3, f32 ts3, int32 cat [G,B,W],
         f64 cut [G,B], f32 cnt [G,B,W,3,3]) -> f32 [G,B,W].  ``etab``: the per-edge-id table of
         tm_edge_tables (tm_encoder_fwd_tab: lin_event's edge-feature product read, not recomputed)."""
         dev = self._dev()
         nt, et = self.feature_tables()
+        w = self.packed_weights() if w is None else w
         n_walks = n_groups * B * W
         if out is None:
             out = torch.empty(max(n_walks, 1), dtype=torch.float32, device=dev)
         if workspace is None:
-            nbytes = L.lib().tm_encoder_workspace_bytes(self.packed_weights(), n_walks)
+            nbytes = L.lib().tm_encoder_workspace_bytes(w, n_walks)
             workspace = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        L.check(L.lib().tm_encoder_fwd_tab(self.packed_weights(), L.ptr(nt), L.ptr(et),
+        L.check(L.lib().tm_encoder_fwd_tab(w, L.ptr(nt), L.ptr(et),
                                            None if etab is None else L.ptr(etab), n_groups, B, W, M, L.ptr(node6),
                                            L.ptr(eid3), L.ptr(ts3), L.ptr(cat), L.ptr(cut), L.ptr(cnt),
                                            L.ptr(workspace), L.ptr(out), L.stream_ptr(dev)), "TempME.forward")
         return out
 
-    def edge_importance(self, eid3, ts3, imp, s1n, s1e, s2n, s2e, n_groups, B, W, N, out1=None, out2=None):
+    def edge_importance(self, eid3, ts3, imp, s1n, s1e, s2n, s2e, n_groups, B, W, N, out1=None, out2=None, w=None):
         dev = self._dev()
+        w = self.packed_weights() if w is None else w
         _, et = self.feature_tables()
         if out1 is None:
             out1 = torch.empty(max(n_groups * B * N, 1), dtype=torch.float32, device=dev)
             out2 = torch.empty(max(n_groups * B * N * N, 1), dtype=torch.float32, device=dev)
-        L.check(L.lib().tm_edge_importance(self.packed_weights(), L.ptr(et), n_groups, B, W, N, L.ptr(eid3),
+        L.check(L.lib().tm_edge_importance(w, L.ptr(et), n_groups, B, W, N, L.ptr(eid3),
                                            L.ptr(ts3), L.ptr(imp), L.ptr(s1n), L.ptr(s1e), L.ptr(s2n), L.ptr(s2e),
                                            L.ptr(out1), L.ptr(out2), L.stream_ptr(dev)), "retrieve_edge_imp_node")
         return out1, out2
 
     # ------------------------------------------------------------------ HIP training path (f3)
     def _encoder_params(self):
-        """The 22 tensors TempME.forward reads (tm_weights order minus the dependency gate)."""
-        at, ec, m = self.attention, self.event_conv, self.MLP
-        ts = []
-        for mod in (ec.lin_event, ec.MLP[0], ec.MLP[2], at.W1, at.W2, at.MLP[0], at.MLP[3], m[0], m[3], m[5]):
-            ts += [mod.weight, mod.bias]
-        return ts + [self.time_encoder.basis_freq, self.time_encoder.phase]
+        """The 22 tensors TempME.forward reads (tm_weights order minus the dependency gate): the cached
+        weight list's 10 Linear pairs and the time encoder's frequency and phase."""
+        ws = self._weight_list()
+        return ws[:20] + ws[-2:]
 
     def dropout_masks(self, n_walks):
         """Keep-masks of the three dropouts TempME.forward applies in training (explainer_new.py:839 alpha,
@@ -453,9 +484,9 @@ class TempME(nn.Module):
         return tuple(grads)
 
     def _gate_params(self):
-        d = self.edge_dependency_gcn
-        return [d[0].weight, d[0].bias, d[3].weight, d[3].bias, d[6].weight, d[6].bias,
-                self.time_encoder.basis_freq, self.time_encoder.phase]
+        """edge_dependency_gcn's three Linear pairs and the time encoder (the cached weight list)."""
+        ws = self._weight_list()
+        return ws[20:26] + ws[-2:]
 
     def gate_dropout_masks(self, n_pos):
         """Keep-masks of edge_dependency_gcn's Dropout(1.5p) [n_pos, h] and Dropout(p) [n_pos, h/2]
@@ -534,44 +565,97 @@ class TempME(nn.Module):
         assert np.shape(edge_identify)[-1] == 3 and np.shape(edge_idx)[-1] == 3, "event_dim mismatch (:180)"
         if not self._hip_eval_ok() or (self._needs_autograd() and not self._hip_ok()):
             return self._forward_torch(walks, cut_time_l, edge_identify)
-        if self._needs_autograd():
+        if self.training:
             out = self.forward_groups(_to(node_idx, dev, torch.int32), _to(edge_idx, dev, torch.int32),
                                       _to(time_idx, dev, torch.float32), _to(cat_feat, dev, torch.int32).reshape(B, W),
                                       _to(cut_time_l, dev, torch.float64), _to(edge_identify, dev, torch.float32), 1, B, W)
             return out.view(B, W, 1)
-        etab = self.dropin_edge_table()
+        wts = self.packed_weights()
+        etab = self.dropin_edge_table(wts)
         if etab is not None and isinstance(edge_idx, np.ndarray) and edge_idx.size and \
                 (edge_idx.max() >= etab.shape[0] or edge_idx.min() < 0):
             raise IndexError("index out of range in self")     # what the reference's embedding lookup raises
-        n6, e3, t3, ct, cu, ei = _to_many(dev, (node_idx, torch.int32), (edge_idx, torch.int32), (time_idx, torch.float32),
-                                          (cat_feat, torch.int32), (cut_time_l, torch.float64),
-                                          (edge_identify, torch.float32))
-        out = self.encoder_fwd(n6, e3, t3, ct.reshape(B, W), cu, ei, 1, B, W, etab=etab)
-        return out[:B * W].view(B, W, 1)
+        items = ((node_idx, torch.int32), (edge_idx, torch.int32), (time_idx, torch.float32), (cat_feat, torch.int32),
+                 (cut_time_l, torch.float64), (edge_identify, torch.float32))
+        side = self._side_stream(dev, items)
+        if side is None:
+            n6, e3, t3, ct, cu, ei = _to_many(dev, *items)
+            out = self.encoder_fwd(n6, e3, t3, ct.reshape(B, W), cu, ei, 1, B, W, etab=etab, w=wts)
+        else:
+            # eval_one_epoch's three per-side calls are independent: each runs on its own side stream (inputs
+            # staged there from host arrays, or device-pack views that are already resident), and the caller's
+            # stream waits for it, so the three walk kernels overlap instead of running one after another
+            cur = torch.cuda.current_stream(dev)
+            with torch.cuda.stream(side):
+                n6, e3, t3, ct, cu, ei = _to_many(dev, *items)
+                out = self.encoder_fwd(n6, e3, t3, ct.reshape(B, W), cu, ei, 1, B, W, etab=etab, w=wts)
+                done = torch.cuda.Event()
+                done.record(side)
+            cur.wait_event(done)
+            out.record_stream(cur)
+        out = out[:B * W]
+        if self._needs_autograd():
+            # eval mode with gradients enabled (temp_exp_main.py:446-452 calls the explainer outside no_grad):
+            # the eval kernel's output, with a backward that recomputes through the training kernels if asked
+            args = (n6, e3, t3, ct.reshape(B, W), cu, ei, 1, B, W)
+            out = _EvalEncoderFn.apply(self, args, out, *self._encoder_params())
+        return out.view(B, W, 1)
+
+    def _side_stream(self, dev, items):
+        """The next of three side streams for an eval forward whose inputs are host arrays or resident
+        device-pack views (``pack.DevicePack.get_item``), else None (run on the current stream).  Pending
+        weight / table preparation on the current stream is waited for through one recorded event."""
+        import os
+        if dev.type != "cuda" or os.environ.get("TEMPME_DROPIN_STREAMS", "1") == "0":
+            return None
+        for a, _ in items:
+            if isinstance(a, torch.Tensor) and not getattr(a, "_tm_resident", False):
+                return None
+            if not isinstance(a, (np.ndarray, torch.Tensor)):
+                return None
+        ss = self.__dict__.get("_side_streams")
+        if ss is None or ss[0].device != dev:
+            ss = self.__dict__["_side_streams"] = [torch.cuda.Stream(device=dev) for _ in range(3)]
+            self.__dict__["_side_i"] = 0
+            self._prep_dirty = True
+        if getattr(self, "_prep_dirty", True):
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+            self.__dict__["_prep_event"] = ev
+            self._prep_dirty = False
+        i = self.__dict__["_side_i"]
+        self.__dict__["_side_i"] = (i + 1) % len(ss)
+        ss[i].wait_event(self.__dict__["_prep_event"])
+        return ss[i]
 
     def retrieve_edge_imp_node(self, subgraph, graphlet_imp, walks, training=True):
         """explainer_new.py:354-406 -> (hop-1 [B,N], hop-2 [B,N^2])."""
         node_record, eidx_record, _ = subgraph
         dev = self._dev()
-        needs_grad = training or (graphlet_imp.requires_grad and torch.is_grad_enabled())
+        needs_grad = training or (torch.is_grad_enabled() and (graphlet_imp.requires_grad or any(
+            p.requires_grad for p in self._weight_list()[20:26])))
         if not self._hip_eval_ok() or (needs_grad and not self._hip_ok()):
             return self._edge_imp_torch(subgraph, graphlet_imp, walks, training)
-        if training or (graphlet_imp.requires_grad and torch.is_grad_enabled()):
-            B, N = np.shape(node_record[0])[0], np.shape(node_record[0])[1]
-            W = np.shape(walks[1])[1]
+        B, N = np.shape(node_record[0])[0], np.shape(node_record[0])[1]
+        W = np.shape(walks[1])[1]
+        if training:
             e0, e1 = self.explain_groups(graphlet_imp.reshape(1, B, W), _to(walks[1], dev, torch.int32),
                                          _to(walks[2], dev, torch.float32), _to(node_record[0], dev, torch.int32),
                                          _to(eidx_record[0], dev, torch.int32), _to(node_record[1], dev, torch.int32),
                                          _to(eidx_record[1], dev, torch.int32), 1, B, W, N, training)
             return e0.view(B, N), e1.view(B, N * N)
-        B, N = np.shape(node_record[0])[0], np.shape(node_record[0])[1]
-        W = np.shape(walks[1])[1]
         e3, t3, n1, x1, n2, x2 = _to_many(dev, (walks[1], torch.int32), (walks[2], torch.float32),
                                           (node_record[0], torch.int32), (eidx_record[0], torch.int32),
                                           (node_record[1], torch.int32), (eidx_record[1], torch.int32))
         o1, o2 = self.edge_importance(e3, t3, graphlet_imp.detach().to(dev, torch.float32).contiguous(), n1, x1, n2, x2,
                                       1, B, W, N)
-        return o1[:B * N].view(B, N), o2[:B * N * N].view(B, N * N)
+        o1, o2 = o1[:B * N].view(B, N), o2[:B * N * N].view(B, N * N)
+        if needs_grad:
+            # eval (Beta mean) with gradients enabled (eval_one_epoch, temp_exp_main.py:447-449): the eval
+            # kernels' values, backward through the HIP training kernels on demand
+            o1, o2 = _EvalExplainFn.apply(self, (e3, t3, n1, x1, n2, x2, B, W, N), graphlet_imp, o1, o2,
+                                          *self._gate_params())
+        return o1, o2
 
     def retrieve_explanation(self, subgraph_src, graphlet_imp_src, walks_src, subgraph_tgt, graphlet_imp_tgt,
                              walks_tgt, subgraph_bgd, graphlet_imp_bgd, walks_bgd, training=True):
@@ -712,6 +796,47 @@ class _EncoderFn(torch.autograd.Function):
         grads = ctx.ex._train_bwd(ctx.args, ctx.drop, ctx.drop_scale, ctx.ws, d_imp)
         ctx.ws = None
         return (None, None, None, None, *grads)
+
+
+class _EvalEncoderFn(torch.autograd.Function):
+    """Eval-mode TempME.forward with gradients enabled: forward = the eval kernel's output (no dropout in
+    eval, so it is the function the training kernels compute); backward recomputes through
+    tm_encoder_train_fwd (without dropout masks) and runs tm_encoder_bwd -- only if a backward is asked for."""
+
+    @staticmethod
+    def forward(ctx, ex, args, out, *params):
+        ctx.ex, ctx.args = ex, args
+        return out.detach()
+
+    @staticmethod
+    def backward(ctx, d_imp):
+        _, ws = ctx.ex._train_fwd(ctx.args, None, 1.0)
+        grads = ctx.ex._train_bwd(ctx.args, None, 1.0, ws, d_imp)
+        return (None, None, None, *grads)
+
+
+class _EvalExplainFn(torch.autograd.Function):
+    """retrieve_edge_imp_node(training=False) with gradients enabled: forward = the eval kernels' hop-1 /
+    hop-2 explanation; backward recomputes through explain_groups (HIP gate + scatter-max training kernels,
+    Beta mean) and differentiates that."""
+
+    @staticmethod
+    def forward(ctx, ex, args, imp, o1, o2, *params):
+        ctx.ex, ctx.args = ex, args
+        ctx.save_for_backward(imp)
+        return o1.detach(), o2.detach()
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        (imp,) = ctx.saved_tensors
+        e3, t3, n1, x1, n2, x2, B, W, N = ctx.args
+        params = ctx.ex._gate_params()
+        with torch.enable_grad():
+            imp_ = imp.detach().requires_grad_(True)
+            e0, e1 = ctx.ex.explain_groups(imp_.reshape(1, B, W), e3, t3, n1, x1, n2, x2, 1, B, W, N, False)
+            gs = torch.autograd.grad((e0, e1), [imp_] + list(params),
+                                     grad_outputs=(g1.reshape(e0.shape), g2.reshape(e1.shape)), allow_unused=True)
+        return (None, None, gs[0], None, None, *gs[1:])
 
 
 class _KLFn(torch.autograd.Function):

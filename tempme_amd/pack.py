@@ -129,9 +129,15 @@ def load_subgraph(args, file, batch_id):
     return (*subs, *walks)
 
 
-def load_subgraph_margin(args, file):
+def load_subgraph_margin(args, file, device=None):
     """utils/batch_loader.py:119-197: the whole ``{data}_{mode}_cat.h5`` pack ->
-    (subgraph_src, subgraph_tgt, subgraph_bgd, walks_src, walks_tgt, walks_bgd, dst_fake)."""
+    (subgraph_src, subgraph_tgt, subgraph_bgd, walks_src, walks_tgt, walks_bgd, dst_fake).
+
+    ``device`` (MI355X extension, default None = the reference's host arrays): upload the pack once into a
+    ``DevicePack``; ``get_item`` then hands out device views in the same tuple layout, so the eval / training
+    loop's per-batch slicing and TempME's inputs stay on the GPU."""
+    if device is not None:
+        return DevicePack(file, None, args.n_degree, device)
     subs = [_subgraph(file, s, args.n_degree) for s in SIDES]
     walks = []
     for s in SIDES:
@@ -153,7 +159,9 @@ def _as_slice(batch_id, n):
 
 
 def get_item(input_pack, batch_id):
-    """utils/batch_loader.py:200-235."""
+    """utils/batch_loader.py:200-235 (a ``DevicePack``: its device views, ``DevicePack.get_item``)."""
+    if isinstance(input_pack, DevicePack):
+        return input_pack.get_item(batch_id)
     *subs, ws, wt, wb, dst_fake = input_pack
     batch_id = _as_slice(batch_id, len(dst_fake))
     out = []
@@ -167,9 +175,38 @@ def get_item(input_pack, batch_id):
 
 
 def get_item_edge(edge_features, batch_id):
-    """utils/batch_loader.py:238-242: [3, n, W, 3, 3] -> (src_edge, tgt_edge, bgd_edge)."""
+    """utils/batch_loader.py:238-242: [3, n, W, 3, 3] -> (src_edge, tgt_edge, bgd_edge).  A device tensor
+    (``load_edge(..., device)``) or a ``DevicePack`` built with its edge counts gives device views."""
+    if isinstance(edge_features, DevicePack):
+        edge_features = edge_features.cnt
+    if isinstance(edge_features, torch.Tensor):
+        sl = _dev_index(batch_id, edge_features.shape[1], edge_features.device)
+        e = edge_features[:, sl]
+        return tuple(_resident(e[s]) for s in range(3))
     e = edge_features[:, _as_slice(batch_id, np.shape(edge_features)[1]), :, :, :]
     return e[0], e[1], e[2]
+
+
+def load_edge(edge, device):
+    """``np.load({data}_{mode}_edge.npy)`` uploaded once as float32 [3, n, W, 3, 3] for ``get_item_edge``."""
+    return torch.from_numpy(np.ascontiguousarray(np.asarray(edge), dtype=np.float32)).to(device)
+
+
+def _resident(t):
+    """Mark a device view as resident pack data (written once at upload, never by the caller's pending
+    work), so TempME's eval forward may read it from a side stream without waiting for the caller's."""
+    t._tm_resident = True
+    return t
+
+
+def _dev_index(batch_id, n, device):
+    sl = _as_slice(np.asarray(batch_id) if not isinstance(batch_id, slice) else batch_id, n)
+    if isinstance(sl, slice):
+        return sl
+    idx = np.asarray(sl)
+    if idx.size and (idx.min() < -n or idx.max() >= n):
+        raise IndexError(f"index {int(idx.max())} is out of bounds for axis 0 with size {n}")
+    return torch.from_numpy(idx.astype(np.int64)).to(device)
 
 
 # ---------------------------------------------------------------------------------- device side
@@ -214,15 +251,19 @@ class DevicePack(EventBuffers):
     hand the training loop, without per-batch host copies."""
 
     def __init__(self, file, edge, n_degree, device, walks_per_slot=3):
+        """``edge`` (the ``_edge.npy`` array) may be None: ``get_item_edge`` then reads a separate
+        ``load_edge`` tensor and ``cnt`` stays zero."""
         dst_fake = np.asarray(file["dst_fake"][:])
         n, N = int(dst_fake.shape[0]), int(n_degree)
         w0 = np.asarray(file["walks_src_new"][:])
         if w0.shape[1] % N:
             raise AssertionError(f"walks per side {w0.shape[1]} is not a multiple of n_degree {N}")
         super().__init__(n, N, w0.shape[1] // N if w0.shape[1] else walks_per_slot, device)
-        edge = np.asarray(edge)
-        if edge.shape != (3, n, self.W, 3, 3):
-            raise AssertionError(f"edge counts {edge.shape} != (3, {n}, {self.W}, 3, 3)")
+        if edge is not None:
+            edge = np.asarray(edge)
+            if edge.shape != (3, n, self.W, 3, 3):
+                raise AssertionError(f"edge counts {edge.shape} != (3, {n}, {self.W}, 3, 3)")
+        self.marg = torch.zeros(3, n, self.W, dtype=torch.float32, device=device)
         i32 = lambda a: torch.from_numpy(np.ascontiguousarray(a).astype(np.int32))  # noqa: E731
         f32 = lambda a: torch.from_numpy(np.ascontiguousarray(a).astype(np.float32))  # noqa: E731
         self.dst_fake.copy_(i32(dst_fake))
@@ -238,8 +279,30 @@ class DevicePack(EventBuffers):
             self.eid3[s].copy_(i32(w[:, :, 6:9]))
             self.ts3[s].copy_(f32(w[:, :, 9:12]))
             self.cat[s].copy_(i32(w[:, :, 12]))
-            self.cnt[s].copy_(f32(edge[s]))
+            self.marg[s].copy_(f32(w[:, :, 13]))
+            if edge is not None:
+                self.cnt[s].copy_(f32(edge[s]))
         self.hist.copy_(torch.bincount(self.cat.reshape(-1).long().cpu(), minlength=12))
+
+    def __len__(self):
+        return self.E
+
+    def get_item(self, batch_id):
+        """get_item (utils/batch_loader.py:200-235) on the device: the same tuple nesting -- per side
+        ([hop-1, hop-2] node, [..] eid, [..] ts), per side (node [B,W,6], eid [B,W,3], ts [B,W,3],
+        cat [B,W,1], marginal [B,W,1]), dst_fake [B] -- as int32 / float32 device views."""
+        sl = _dev_index(batch_id, self.E, self.dst_fake.device)
+        r = _resident
+        out = []
+        for s in range(3):
+            out.append(([r(self.sub1_node[s, sl]), r(self.sub2_node[s, sl])],
+                        [r(self.sub1_eid[s, sl]), r(self.sub2_eid[s, sl])],
+                        [r(self.sub1_ts[s, sl]), r(self.sub2_ts[s, sl])]))
+        for s in range(3):
+            out.append((r(self.node6[s, sl]), r(self.eid3[s, sl]), r(self.ts3[s, sl]),
+                        r(self.cat[s, sl].unsqueeze(-1)), r(self.marg[s, sl].unsqueeze(-1))))
+        out.append(r(self.dst_fake[:self.E][sl]))
+        return tuple(out)
 
     @classmethod
     def from_files(cls, cat_path, edge_path, n_degree, device):

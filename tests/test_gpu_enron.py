@@ -280,3 +280,71 @@ def test_dropin_equals_pipeline(dev, finder, g, z):
         assert torch.equal(x[..., 0], imp[k]), k
     assert torch.equal(expl[0], h1.reshape(3 * E, N))
     assert torch.equal(expl[1], h2.reshape(3 * E, N * N))
+
+
+@pytest.mark.parametrize("where", ["device_pack", "host_pack_grad"])
+def test_dropin_device_pack_and_grad_equal_pipeline(dev, finder, g, z, where):
+    """The same drop-in calls (a) through a device-resident pack (load_subgraph_margin(..., device=),
+    load_edge: get_item hands out device views and the three forward calls overlap on side streams) and
+    (b) from the host pack with gradients enabled (eval_one_epoch calls the explainer outside no_grad:
+    the eval kernel's output, backward on demand) are bit-identical to the fused pipeline."""
+    from tempme_amd import pack as P
+    from tempme_amd.pipeline import ExplainPipeline
+    N, E = 20, EI.SETS[20]
+    ex = _explainer(dev, g, z, "N20_base")
+    # the pipeline in reference batches of 25 events (the attention's time std is per batch = per call)
+    pipe = ExplainPipeline(ex, finder.graph, torch.from_numpy(z["test_sampler_dst"]), N, 3, 25, seed=0,
+                           split=px.SPLIT_TEST)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a[:E], dtype=dt)).to(dev)  # noqa: E731
+    imp, h1, h2 = [x.clone() for x in pipe.run(t(z["test_src"], np.int32), t(z["test_dst"], np.int32),
+                                                t(z["test_ts"], np.float64), t(z["test_eidx"], np.int32),
+                                                torch.arange(E, dtype=torch.int32, device=dev))]
+    _, cat_d, edge = P.buffers_to_arrays(pipe.buf, E)
+
+    class A:
+        n_degree = N
+    if where == "device_pack":
+        pk, ed = P.load_subgraph_margin(A(), cat_d, device=dev), P.load_edge(edge, dev)
+    else:
+        pk, ed = P.load_subgraph_margin(A(), cat_d), edge
+    cut = z["test_ts"][:E].astype(np.float64)
+    outs = []
+    for b0 in range(0, E, 25):                           # four reference batches, back to back
+        idx = np.arange(b0, b0 + 25)
+        sg_s, sg_t, sg_b, w_s, w_t, w_b, fake = P.get_item(pk, idx)
+        e_s, e_t, e_b = P.get_item_edge(ed, idx)
+        i_s, i_t, i_b = ex(w_s, cut[idx], e_s), ex(w_t, cut[idx], e_t), ex(w_b, cut[idx], e_b)
+        assert i_s.requires_grad                         # the reference calls the explainer with grad enabled
+        with torch.no_grad():
+            expl = ex.retrieve_explanation(sg_s, i_s, w_s, sg_t, i_t, w_t, sg_b, i_b, w_b, training=False)
+        outs.append((i_s.detach(), i_t.detach(), i_b.detach(), expl))
+        if where == "device_pack":
+            assert isinstance(fake, torch.Tensor) and fake.device == dev and w_s[0].dtype == torch.int32
+    for k in range(3):
+        got = torch.cat([o[k] for o in outs])[..., 0]
+        assert torch.equal(got, imp[k][:E]), k
+    # explanation rows are per side: [src batch | tgt batch | bgd batch] per reference batch
+    e1 = torch.cat([o[3][0].view(3, 25, N) for o in outs], 1).reshape(3 * E, N)
+    e2 = torch.cat([o[3][1].view(3, 25, N * N) for o in outs], 1).reshape(3 * E, N * N)
+    assert torch.equal(e1, h1.reshape(3 * E, N))
+    assert torch.equal(e2, h2.reshape(3 * E, N * N))
+
+
+def test_eval_forward_grad_matches_torch(dev, finder, g, z):
+    """Eval mode with gradients enabled: the eval kernel's output with the on-demand backward (recompute
+    through the training kernels) gives the torch formulation's weight gradients within 2e-4 rel-norm."""
+    from tests.encoder_inputs import SIDES  # noqa: F401  (same walk layout)
+    ex = _explainer(dev, g, z, "N20_base")
+    d = EI.walks(z, 20, 25)
+    x = d["src"]
+    w = (x["node"], x["eid"], x["ts"], x["cat"], x["marg"])
+    ex.zero_grad()
+    ex(w, d["ts_cut"], x["cnt"]).pow(2).sum().backward()
+    got = {n: p.grad.detach().clone() for n, p in ex.named_parameters() if p.grad is not None}
+    ex.zero_grad()
+    ex._forward_torch(w, d["ts_cut"], x["cnt"]).pow(2).sum().backward()
+    want = {n: p.grad.detach().clone() for n, p in ex.named_parameters() if p.grad is not None}
+    assert got.keys() == want.keys() and len(got) == 22
+    for n in want:
+        err = (got[n] - want[n]).norm() / max(want[n].norm(), 1e-12)
+        assert err < 2e-4, (n, float(err))
