@@ -144,9 +144,15 @@ int tm_gather_rows(const tm_gather_job *jobs, int32_t n_jobs, const int64_t *row
  *   6/7 attention.W1   8/9 attention.W2   10/11 attention.MLP.0   12/13 attention.MLP.3
  *   14/15 MLP.0   16/17 MLP.3   18/19 MLP.5   20/21 edge_dependency_gcn.0   22/23 .3   24/25 .6
  *   26 time_encoder.basis_freq   27 time_encoder.phase
- * de = edge feature dim, dn = node feature dim (= time dim), h = hid_dim (64 supported). */
+ * de = edge feature dim, dn = node feature dim (= time dim), h = hid_dim (a multiple of 16 up to 256;
+ * the fused register-resident walk kernel covers h = 64 with the category feature, every other shape
+ * runs the LDS-tiled kernels).  if_cat = if_cat_feature (explainer_new.py:121-125): 0 -> MLP.0 / MLP.3
+ * take h inputs (no one-hot category), tensors 14/15/16 shaped accordingly.
+ * Replaces the weights of TempME.__init__ (models/explainer_new.py:103-171; the reference keeps them as
+ * nn.Linear modules and calls them per forward). */
 #define TM_N_WEIGHTS 28
-int tm_weights_create(int32_t de, int32_t dn, int32_t h, int device, tm_weights **out);
+int tm_weights_create(int32_t de, int32_t dn, int32_t h, int device, tm_weights **out);   /* if_cat = 1 */
+int tm_weights_create_ex(int32_t de, int32_t dn, int32_t h, int32_t if_cat, int device, tm_weights **out);
 int tm_weights_pack(tm_weights *w, const float *const *tensors, void *stream);
 /* TempME constructor variants for the eval kernels (explainer_new.py:103-105, :121, :141-145, :367):
  * temporal_guidance = 0 -> the plain Attention (scores not time-weighted; the batch std is not needed),

@@ -29,7 +29,8 @@ def time_encode(sd, t):
     return torch.cos(m.to(w.dtype))
 
 
-def forward(sd, n_feat, e_feat, node, eid, ts, cat, cut, edge_count, drop=None, scale=1.0, temporal=True):
+def forward(sd, n_feat, e_feat, node, eid, ts, cat, cut, edge_count, drop=None, scale=1.0, temporal=True,
+            if_cat=True):
     """graphlet importance [B, W, 1] for one side (explainer_new.py:174-201).  temporal=False: the
     plain ``Attention`` of use_temporal_guidance=False (explainer_new.py:12-43, no time scaling).  drop: optional keep-masks
     [B, W, 144] of the training forward's three dropouts (alpha :839 -> cols 0..1, attention.MLP hidden :780
@@ -75,8 +76,11 @@ def forward(sd, n_feat, e_feat, node, eid, ts, cat, cut, edge_count, drop=None, 
         hid = hid * keep[..., 2:66]
     # TemporalAwareAttention.MLP has a Dropout at index 2 (:777-782), Attention.MLP does not (:18)
     out = _lin(sd, "attention.MLP.3" if "attention.MLP.3.weight" in sd else "attention.MLP.2", hid)
-    oh = F.one_hot(torch.as_tensor(np.asarray(cat), dtype=torch.long).reshape(B, W), 12).to(dty)
-    x = torch.cat([out, oh], dim=-1)
+    if if_cat:     # compute_catogory_feautres (:308-315); if_cat_feature=False feeds the attention output alone
+        oh = F.one_hot(torch.as_tensor(np.asarray(cat), dtype=torch.long).reshape(B, W), 12).to(dty)
+        x = torch.cat([out, oh], dim=-1)
+    else:
+        x = out
     x = torch.relu(_lin(sd, "MLP.0", x))
     if keep is not None:
         x = x * keep[..., 66:142]

@@ -69,7 +69,7 @@ __global__ void __launch_bounds__(256) gcn_kernel(EncW P, int64_t n_rows, const 
                                                   const float *__restrict__ cnt, float *__restrict__ F) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int de = P.de, dn = P.dn, kev = P.kev, kev16 = r16(kev), dn16 = r16(dn);
-    const int ldx = kev16 + 8, ldab = dn16 + 8, ldh = HID + 8;
+    const int h = P.h, ldx = kev16 + 8, ldab = dn16 + 8, ldh = r16(h) + 8;
     const int xsz = max(TILE_ROWS * ldx, 2 * TILE_ROWS * ldh);
     float *X = smem;                                  // [32][ldx]      event features
     float *AB = X + xsz;                              // [64][ldab]     A rows 0..31, B rows 32..63
@@ -133,7 +133,7 @@ __global__ void __launch_bounds__(256) gcn_kernel(EncW P, int64_t n_rows, const 
             const int row = erow(mt, r);
             const int rr = row & (TILE_ROWS - 1), half = row >> 5;
             const int64_t gr = row0 + rr;
-            if (gr < n_rows) F[gr * (2 * HID) + half * HID + c] = acc[r] + P.g2.b[c];
+            if (gr < n_rows && c < h) F[gr * (2 * h) + half * h + c] = acc[r] + P.g2.b[c];
         }
     });
 }
@@ -146,7 +146,7 @@ __global__ void __launch_bounds__(256) head_kernel(EncW P, int64_t n_walks, int6
                                                    const uint8_t *__restrict__ drop = nullptr, float dscale = 1.f) {
     // drop (training forward, nullable): keep-masks [n_walks][DROP_COLS]; kept values are scaled by dscale
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    constexpr int D2 = 2 * HID, LD = D2 + 8, LDM = r16(HID + 12) + 8, LDH = HID + 8;
+    const int h = P.h, D2 = 2 * h, LD = D2 + 8, LDM = r16(P.hm) + 8, LDH = r16(h) + 8;
     float *T = smem;                  // [64][LD]  positions 0,1 (rows p*32 + w)  -> later S, P
     float *Q = T + 2 * TILE_ROWS * LD;  // [64][LD]  W2(tgt)
     float *S = T;                     // [32][LD]  position 2
@@ -248,9 +248,11 @@ __global__ void __launch_bounds__(256) head_kernel(EncW P, int64_t n_walks, int6
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) X[erow(mt, r) * LDM + c] = acc[r] + P.a2.b[c];
     });
-    for (int i = tid; i < TILE_ROWS * 16; i += blockDim.x) {
-        const int w = i >> 4, c = i & 15;
-        X[w * LDM + HID + c] = (c < 12 && s_cat[w] == c) ? 1.f : 0.f;
+    if (P.cat) {   // one-hot category after the attention output (compute_catogory_feautres :308-315)
+        for (int i = tid; i < TILE_ROWS * 16; i += blockDim.x) {
+            const int w = i >> 4, c = i & 15;
+            X[w * LDM + h + c] = (c < 12 && s_cat[w] == c) ? 1.f : 0.f;
+        }
     }
     __syncthreads();
     gemm<2>(X, LDM, P.m1, [&](int mt, int nt, floatx4 acc) {
@@ -271,7 +273,7 @@ __global__ void __launch_bounds__(256) head_kernel(EncW P, int64_t n_walks, int6
     {
         const int w = tid >> 3, sub = tid & 7;
         float s = 0.f;
-        for (int c = sub; c < HID; c += 8) s += M2[w * LDH + c] * P.m3w[c];
+        for (int c = sub; c < h; c += 8) s += M2[w * LDH + c] * P.m3w[c];
         s += __shfl_xor(s, 1, 8);
         s += __shfl_xor(s, 2, 8);
         s += __shfl_xor(s, 4, 8);
@@ -294,7 +296,7 @@ __global__ void __launch_bounds__(256) gate_pos_kernel(EncW P, int64_t n_rows, i
                                                        const int32_t *__restrict__ eid3, const float *__restrict__ ts3,
                                                        const float *__restrict__ imp, float *__restrict__ wv) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int de = P.de, kdep = P.kdep, kd16 = r16(kdep), ldx = kd16 + 8, ldg = HID + 8, ldg2 = HID / 2 + 8;
+    const int de = P.de, kdep = P.kdep, kd16 = r16(kdep), ldx = kd16 + 8, ldg = r16(P.h) + 8, ldg2 = r16(P.h / 2) + 8;
     float *X = smem;                       // [32][ldx]
     float *G1 = X + TILE_ROWS * ldx;       // [32][ldg]
     float *G2 = G1 + TILE_ROWS * ldg;      // [32][ldg2]
@@ -337,7 +339,7 @@ __global__ void __launch_bounds__(256) gate_pos_kernel(EncW P, int64_t n_rows, i
     });
     __syncthreads();
     const int r = tid >> 3, sub = tid & 7;
-    const float sc = gate_logit_lds(G2 + r * ldg2, P.d3w, sub);
+    const float sc = gate_logit_lds(G2 + r * ldg2, P.d3w, sub, P.h / 2);
     const int64_t gr = c0 + r;
     if (sub == 0 && gr < n_rows) {
         const float gate = 1.f / (1.f + expf(-(sc + P.d3b[0])));
@@ -1141,7 +1143,7 @@ static bool walk_layout_ok(const EncW &P, int nqe) {
 __global__ void __launch_bounds__(256) gate_table_kernel(EncW P, int32_t n_ids, const double *__restrict__ ets,
                                                          const float *__restrict__ e_feat, float *__restrict__ gf) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int de = P.de, kdep = P.kdep, kd16 = r16(kdep), ldx = kd16 + 8, ldg = HID + 8, ldg2 = HID / 2 + 8;
+    const int de = P.de, kdep = P.kdep, kd16 = r16(kdep), ldx = kd16 + 8, ldg = r16(P.h) + 8, ldg2 = r16(P.h / 2) + 8;
     float *X = smem, *G1 = X + TILE_ROWS * ldx, *G2 = G1 + TILE_ROWS * ldg;
     const int tid = threadIdx.x;
     const int32_t e0 = blockIdx.x * TILE_ROWS;
@@ -1167,7 +1169,7 @@ __global__ void __launch_bounds__(256) gate_table_kernel(EncW P, int32_t n_ids, 
     });
     __syncthreads();
     const int r = tid >> 3, sub = tid & 7;
-    const float s = gate_logit_lds(G2 + r * ldg2, P.d3w, sub);
+    const float s = gate_logit_lds(G2 + r * ldg2, P.d3w, sub, P.h / 2);
     if (sub == 0 && e0 + r < n_ids) {
         const float z = s + P.d3b[0];
         gf[e0 + r] = P.dep ? 0.5f + 0.5f * (1.f / (1.f + expf(-z))) : 1.f;
@@ -1323,8 +1325,13 @@ using namespace tmk;
 
 
 extern "C" int tm_weights_create(int32_t de, int32_t dn, int32_t h, int device, tm_weights **out) {
-    if (!out || de <= 0 || dn <= 0) return fail(TM_E_ARG, "tm_weights_create: bad arguments");
-    if (h != HID) return fail(TM_E_UNSUPPORTED, "tm_weights_create: hid_dim must be 64 in this build");
+    return tm_weights_create_ex(de, dn, h, 1, device, out);
+}
+
+extern "C" int tm_weights_create_ex(int32_t de, int32_t dn, int32_t h, int32_t if_cat, int device, tm_weights **out) {
+    if (!out || de <= 0 || dn <= 0 || h <= 0) return fail(TM_E_ARG, "tm_weights_create: bad arguments");
+    if (h % 16 || h > 256)
+        return fail(TM_E_UNSUPPORTED, "tm_weights_create: hid_dim must be a multiple of 16 up to 256");
     *out = nullptr;
     tm_weights *w = new tm_weights();
     w->device = device;
@@ -1336,7 +1343,10 @@ extern "C" int tm_weights_create(int32_t de, int32_t dn, int32_t h, int device, 
     P.dn = dn;
     P.kev = de + 3 + dn;
     P.kdep = de + dn;
-    const int h2 = 2 * h, hm = h + 12;
+    P.h = h;
+    P.cat = if_cat ? 1 : 0;
+    P.hm = if_cat ? h + 12 : h;
+    const int h2 = 2 * h, hm = P.hm;
     struct L {
         Lin *lin;
         int wi, nout, k;
@@ -1358,9 +1368,9 @@ extern "C" int tm_weights_create(int32_t de, int32_t dn, int32_t h, int device, 
         total += (size_t)l.lin->nt * 16;
         w->specs.push_back({l.lin, l.wi, l.nout, l.k});
     }
-    const size_t m3w = total; total += 64;
+    const size_t m3w = total; total += r16(h);
     const size_t m3b = total; total += 4;
-    const size_t d3w = total; total += 64;
+    const size_t d3w = total; total += r16(h / 2);
     const size_t d3b = total; total += 4;
     const size_t fq = total; total += r16(dn);
     const size_t ph = total; total += r16(dn);
@@ -1456,11 +1466,11 @@ extern "C" int tm_weights_free(tm_weights *w) {
 
 extern "C" int64_t tm_encoder_workspace_bytes(const tm_weights *w, int64_t n_walks) {
     (void)w;
-    return n_walks * 3 * 2 * HID * (int64_t)sizeof(float) + (n_walks + 64) * (int64_t)sizeof(float) + 256;
+    return n_walks * 3 * 2 * (w ? w->h : HID) * (int64_t)sizeof(float) + (n_walks + 64) * (int64_t)sizeof(float) + 256;
 }
 
 static size_t gate_lds(const EncW &P) {
-    return sizeof(float) * (TILE_ROWS * (r16(P.kdep) + 8) + TILE_ROWS * (HID + 8) + TILE_ROWS * (HID / 2 + 8));
+    return sizeof(float) * (TILE_ROWS * (r16(P.kdep) + 8) + TILE_ROWS * (r16(P.h) + 8) + TILE_ROWS * (r16(P.h / 2) + 8));
 }
 
 // lin_event's K steps before the first one holding a count or time feature (= de / 16), when the
@@ -1468,6 +1478,7 @@ static size_t gate_lds(const EncW &P) {
 // Enron's 32; de = 160..175 with 21..22, as BASELINE configs[4]'s 172), else 0
 static int etab_q0(const EncW &P) {
     const int nqe = r16(P.kev) / 16, ntd = r16(P.dn) / 16, q0 = P.de / 16;
+    if (P.h != HID || !P.cat) return 0;
     if (ntd != 11 || P.dn % 4 || P.ev.nt != 11 || P.ev.nq != nqe || P.d1.nt != 4 || P.d2.nq != 4 || P.d2.nt != 2)
         return 0;
     if (q0 == 2 && nqe >= 11 && nqe <= 14 && P.d1.nq == 13) return 2;
@@ -1550,10 +1561,10 @@ extern "C" int tm_edge_importance_tab(const float *gf, int32_t n_ids, int32_t n_
 }
 
 static size_t gcn_lds(const EncW &P) {
-    const int xsz = std::max(TILE_ROWS * (r16(P.kev) + 8), 2 * TILE_ROWS * (HID + 8));
+    const int xsz = std::max(TILE_ROWS * (r16(P.kev) + 8), 2 * TILE_ROWS * (r16(P.h) + 8));
     return sizeof(float) * (xsz + 2 * TILE_ROWS * (r16(P.dn) + 8));
 }
-static size_t head_lds() { return sizeof(float) * (4 * TILE_ROWS * (2 * HID + 8)); }
+static size_t head_lds(const EncW &P) { return sizeof(float) * (4 * TILE_ROWS * (2 * P.h + 8)); }
 
 template <int NQE, bool SEF = false, int Q0 = 0>
 static void launch_walk(const WalkArgs &a, unsigned blocks, hipStream_t s) {
@@ -1579,11 +1590,11 @@ extern "C" int tm_encoder_fwd_tab(const tm_weights *w, const float *n_feat, cons
     if (!n_feat || !e_feat || !node6 || !eid3 || !ts3 || !cat || !cut || !cnt || !workspace || !out_imp)
         return fail(TM_E_ARG, "tm_encoder_fwd: NULL pointer");
     const EncW &P = w->P;
-    const size_t lds_g = gcn_lds(P), lds_h = head_lds();
+    const size_t lds_g = gcn_lds(P), lds_h = head_lds(P);
     if (lds_g > 160 * 1024) return fail(TM_E_UNSUPPORTED, "tm_encoder_fwd: feature dims too large for LDS tile");
     hipStream_t s = S_(stream);
     float *F = reinterpret_cast<float *>(workspace);
-    float *stdv = F + n_walks * 3 * 2 * HID;
+    float *stdv = F + n_walks * 3 * 2 * P.h;
     hipEvent_t pe = prof_begin(s);
     if (P.tg) std_kernel<<<dim3(n_groups), 1024, 0, s>>>(B, W, cut, ts3, stdv);
     TM_CHECK_LAUNCH();
@@ -1593,7 +1604,7 @@ extern "C" int tm_encoder_fwd_tab(const tm_weights *w, const float *n_feat, cons
     const bool narrow = nqe >= 11 && nqe <= 14 && P.de <= 16 * EQ_MAX;
     // wide edge features (e.g. BASELINE configs[4]: de = dn = 172): streamed per K step
     const bool wide = (nqe == 21 || nqe == 22) && P.de > 16 * EQ_MAX && P.de % 4 == 0;
-    if (ntd == 11 && P.dn % 4 == 0 && (narrow || wide)) {
+    if (ntd == 11 && P.dn % 4 == 0 && (narrow || wide) && P.h == HID && P.cat) {
         // fused register-resident path
         if (!walk_layout_ok(P, nqe)) return fail(TM_E_UNSUPPORTED, "tm_encoder_fwd: weight layout mismatch");
         const int64_t n_slots = n_walks / M;
@@ -1647,11 +1658,11 @@ extern "C" int tm_encoder_train_fwd(const tm_weights *w, const float *n_feat, co
     if (!n_feat || !e_feat || !node6 || !eid3 || !ts3 || !cat || !cut || !cnt || !workspace || !out_imp)
         return fail(TM_E_ARG, "tm_encoder_train_fwd: NULL pointer");
     const EncW &P = w->P;
-    const size_t lds_g = gcn_lds(P), lds_h = head_lds();
+    const size_t lds_g = gcn_lds(P), lds_h = head_lds(P);
     if (lds_g > 160 * 1024) return fail(TM_E_UNSUPPORTED, "tm_encoder_train_fwd: feature dims too large for LDS tile");
     hipStream_t s = S_(stream);
     float *F = reinterpret_cast<float *>(workspace);
-    float *stdv = F + n_walks * 3 * 2 * HID;
+    float *stdv = F + n_walks * 3 * 2 * P.h;
     hipEvent_t pe = prof_begin(s);
     if (P.tg) std_kernel<<<dim3(n_groups), 1024, 0, s>>>(B, W, cut, ts3, stdv);
     TM_CHECK_LAUNCH();
@@ -1683,7 +1694,7 @@ extern "C" int tm_edge_importance(const tm_weights *w, const float *e_feat, int3
     while ((1 << hbits) < 2 * 3 * W) ++hbits;
     if (hbits > 14) return fail(TM_E_UNSUPPORTED, "tm_edge_importance: too many walks per event");
     const EncW &P = w->P;
-    const size_t lds = sizeof(float) * (TILE_ROWS * (r16(P.kdep) + 8) + TILE_ROWS * (HID + 8) + TILE_ROWS * (HID / 2 + 8));
+    const size_t lds = gate_lds(P);
     const size_t hlds = 2 * sizeof(int32_t) * (1u << hbits);
     if (lds > 160 * 1024) return fail(TM_E_UNSUPPORTED, "tm_edge_importance: LDS budget exceeded");
     const int64_t n_pos = rows * 3 * W;

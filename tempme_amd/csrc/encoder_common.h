@@ -44,6 +44,9 @@ struct EncW {
     // constructor variants (explainer_new.py:103-105, :121, :141): tg = use_temporal_guidance (0: the plain
     // Attention, no time weighting of the scores), dep = use_dependency_aware_sampling (0: no gate)
     int tg = 1, dep = 1;
+    // hid_dim and the final MLP's width (hm = h + 12 with the one-hot category feature, h without:
+    // if_cat_feature, explainer_new.py:121-125); the fused walk kernel covers h = 64 with the category
+    int h = 64, hm = 76, cat = 1;
 };
 
 // ------------------------------------------------------------------ MFMA tile GEMM
@@ -109,21 +112,21 @@ __device__ __forceinline__ float time_cos(float t, float w, float phi) { return 
 
 __device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
 
-// The dependency gate's logit d3 . G2 over its h/2 = 32 features in ONE fixed order, shared by the
-// LDS-tiled kernels and the register-resident gate_reg_kernel so their gates agree bit for bit:
-// part k (k = 0..3) is an fma chain over features 16t + 4k + r (t = 0, 1; r = 0..3) and
+// The dependency gate's logit d3 . G2 over its h2 = h/2 features in ONE fixed order, shared by the
+// LDS-tiled kernels and the register-resident gate_reg_kernel (h2 = 32) so their gates agree bit for bit:
+// part k (k = 0..3) is an fma chain over features 16t + 4k + r (t < h2/16 rounded up, r = 0..3) and
 // z = (part0 + part1) + (part2 + part3).
-__device__ __forceinline__ float gate_part(const float *g2, const float *w3, int k) {
+__device__ __forceinline__ float gate_part(const float *g2, const float *w3, int k, int h2 = 32) {
     float p = 0.f;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; 16 * t < h2; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) p = __builtin_fmaf(g2[16 * t + 4 * k + r], w3[16 * t + 4 * k + r], p);
     return p;
 }
-// LDS form: 8 lanes per row (sub = lane & 7), the row's relu'd G2 at g2; the result in every lane
-__device__ __forceinline__ float gate_logit_lds(const float *g2, const float *w3, int sub) {
-    float v = sub < 4 ? gate_part(g2, w3, sub) : 0.f;
+// LDS form: 8 lanes per row (sub = lane & 7), the row's relu'd G2 at g2 (zero padded to a multiple of 16;
+// w3 likewise); the result in every lane
+__device__ __forceinline__ float gate_logit_lds(const float *g2, const float *w3, int sub, int h2 = 32) {
+    float v = sub < 4 ? gate_part(g2, w3, sub, h2) : 0.f;
     v += __shfl_xor(v, 1, 8);
     v += __shfl_xor(v, 2, 8);
     return v;

@@ -1004,7 +1004,7 @@ using namespace tmk;
 
 // ------------------------------------------------------------------ host side
 int train_packs_create(tm_weights *w) {
-    const int de = w->de, dn = w->dn, h = w->h, h2 = 2 * h, hm = h + 12, kev = de + 3 + dn;
+    const int de = w->de, dn = w->dn, h = w->h, h2 = 2 * h, hm = w->P.hm, kev = de + 3 + dn;
     (void)kev;
     struct D {
         Lin *lin;
@@ -1038,7 +1038,7 @@ int train_packs_create(tm_weights *w) {
 }
 
 void pack_all_weights(tm_weights *w, const float *const *t, hipStream_t s) {
-    const int de = w->de, dn = w->dn, h = w->h, h2 = 2 * h, hm = h + 12, kev = de + 3 + dn;
+    const int de = w->de, dn = w->dn, h = w->h, h2 = 2 * h, hm = w->P.hm, kev = de + 3 + dn;
     PackJobs P{};
     int64_t total = 0;
     auto frag = [&](const Lin &lin, const float *src, int so, int sc) {
@@ -1068,9 +1068,9 @@ void pack_all_weights(tm_weights *w, const float *const *t, hipStream_t s) {
         frag(*sp.lin, t[sp.wi], sp.k, 1);
         copy(t[sp.wi + 1], sp.lin->b, sp.nout, sp.lin->nt * 16);
     }
-    copy(t[18], w->P.m3w, h, 64);
+    copy(t[18], w->P.m3w, h, r16(h));
     copy(t[19], w->P.m3b, 1, 4);
-    copy(t[24], w->P.d3w, h / 2, 64);
+    copy(t[24], w->P.d3w, h / 2, r16(h / 2));
     copy(t[25], w->P.d3b, 1, 4);
     copy(t[26], w->P.freq, dn, r16(dn));
     copy(t[27], w->P.phase, dn, r16(dn));
@@ -1087,7 +1087,7 @@ void pack_all_weights(tm_weights *w, const float *const *t, hipStream_t s) {
     frag(w->T.d1T, t[20] + de, 1, de + dn);
     frag(w->T.d2T, t[22], 1, h);
     // the fused walk kernel's folded layers (hid_dim 64): fp64 products first, then packed with the rest
-    const bool fold = h == HID && w->fold64 && w->fold32;
+    const bool fold = h == HID && w->P.cat && w->fold64 && w->fold32;
     if (fold) {
         using L = FoldLay;
         const FoldIn F{t[4], t[5], t[6], t[7], t[8], t[9], t[10], t[11], t[12], t[13], t[14], t[15]};
@@ -1240,7 +1240,7 @@ extern "C" int tm_encoder_wgrad(const tm_weights *w, int32_t n_groups, int32_t B
         if (!grads[i]) return fail(TM_E_ARG, "tm_encoder_wgrad: NULL gradient " + std::to_string(i));
     const int64_t n64 = (int64_t)n_groups * B * W;
     if (n64 * 3 * 2 > INT32_MAX) return fail(TM_E_UNSUPPORTED, "tm_encoder_wgrad: too many walks per call");
-    const int n = (int)n64, R = 3 * n, h = w->h, h2 = 2 * h, hm = h + 12;
+    const int n = (int)n64, R = 3 * n, h = w->h, h2 = 2 * h, hm = w->P.hm;
     const int dn = w->dn, kev = w->P.kev, KE = r16(kev), DN = r16(dn), KM = r16(hm);
     const float *F = reinterpret_cast<const float *>(workspace);
     const tm_wgrad_job jobs[] = {

@@ -242,14 +242,14 @@ class TempME(nn.Module):
             return True
         if not torch.is_grad_enabled():
             return False
-        if self.if_cat and self.hid_dim == 64:
-            return any(p.requires_grad for p in self._weight_list())
-        return any(p.requires_grad for p in self.parameters())
+        return any(p.requires_grad for p in self._weight_list())
 
     def _hip_eval_ok(self):
-        """The eval kernels cover every constructor variant with hid_dim == 64 and the category feature
-        (use_temporal_guidance / use_dependency_aware_sampling through tm_weights_variant)."""
-        ok = self.if_cat and self.hid_dim == 64
+        """The eval kernels cover every constructor variant (use_temporal_guidance /
+        use_dependency_aware_sampling through tm_weights_variant, if_cat_feature and hid_dim through
+        tm_weights_create_ex) for hid_dim a multiple of 16 up to 256: the fused walk kernel for the default
+        shape (hid_dim 64 with the category feature), the LDS-tiled kernels for the others."""
+        ok = self.hid_dim % 16 == 0 and 0 < self.hid_dim <= 256
         if not ok and not getattr(self, "_warned_torch", False):
             warnings.warn("TempME(if_cat_feature=%s, hid_dim=%d): no HIP kernel instance for this constructor "
                           "variant; forward / retrieve_edge_imp_node run the torch-op formulation on the device"
@@ -337,8 +337,8 @@ class TempME(nn.Module):
         if self._packed is None or self._packed_key != key or force:
             if self._packed is None:
                 h = L.C.c_void_p()
-                L.check(L.lib().tm_weights_create(self.edge_dim, self.node_dim, self.hid_dim, dev.index,
-                                                  L.C.byref(h)), "tm_weights_create")
+                L.check(L.lib().tm_weights_create_ex(self.edge_dim, self.node_dim, self.hid_dim, int(bool(self.if_cat)),
+                                                     dev.index, L.C.byref(h)), "tm_weights_create")
                 self._packed = _Packed(h)
                 L.check(L.lib().tm_weights_variant(h, int(bool(self.use_temporal_guidance)),
                                                    int(bool(self.use_dependency_aware_sampling))), "tm_weights_variant")
@@ -563,7 +563,7 @@ class TempME(nn.Module):
         dev = self._dev()
         B, W = np.shape(edge_idx)[0], np.shape(edge_idx)[1]
         assert np.shape(edge_identify)[-1] == 3 and np.shape(edge_idx)[-1] == 3, "event_dim mismatch (:180)"
-        if not self._hip_eval_ok() or (self._needs_autograd() and not self._hip_ok()):
+        if not self._hip_eval_ok() or (self.training and not self._hip_ok()):
             return self._forward_torch(walks, cut_time_l, edge_identify)
         if self.training:
             out = self.forward_groups(_to(node_idx, dev, torch.int32), _to(edge_idx, dev, torch.int32),
@@ -634,7 +634,7 @@ class TempME(nn.Module):
         dev = self._dev()
         needs_grad = training or (torch.is_grad_enabled() and (graphlet_imp.requires_grad or any(
             p.requires_grad for p in self._weight_list()[20:26])))
-        if not self._hip_eval_ok() or (needs_grad and not self._hip_ok()):
+        if not self._hip_eval_ok() or (training and not self._hip_ok()):
             return self._edge_imp_torch(subgraph, graphlet_imp, walks, training)
         B, N = np.shape(node_record[0])[0], np.shape(node_record[0])[1]
         W = np.shape(walks[1])[1]
@@ -810,8 +810,17 @@ class _EvalEncoderFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, d_imp):
-        _, ws = ctx.ex._train_fwd(ctx.args, None, 1.0)
-        grads = ctx.ex._train_bwd(ctx.args, None, 1.0, ws, d_imp)
+        ex = ctx.ex
+        if ex._hip_ok():
+            _, ws = ex._train_fwd(ctx.args, None, 1.0)
+            grads = ex._train_bwd(ctx.args, None, 1.0, ws, d_imp)
+        else:   # constructor variants without HIP training kernels: recompute through the torch formulation
+            node6, eid3, ts3, cat, cut, cnt, G, B, W = ctx.args
+            params = ex._encoder_params()
+            with torch.enable_grad():
+                out = ex._forward_torch((node6, eid3, ts3, cat, None), cut, cnt)
+                grads = torch.autograd.grad(out.reshape(-1), params, grad_outputs=d_imp.reshape(-1).to(out.dtype),
+                                            allow_unused=True)
         return (None, None, None, *grads)
 
 
@@ -830,10 +839,15 @@ class _EvalExplainFn(torch.autograd.Function):
     def backward(ctx, g1, g2):
         (imp,) = ctx.saved_tensors
         e3, t3, n1, x1, n2, x2, B, W, N = ctx.args
-        params = ctx.ex._gate_params()
+        ex = ctx.ex
+        params = ex._gate_params()
         with torch.enable_grad():
             imp_ = imp.detach().requires_grad_(True)
-            e0, e1 = ctx.ex.explain_groups(imp_.reshape(1, B, W), e3, t3, n1, x1, n2, x2, 1, B, W, N, False)
+            if ex._hip_ok():
+                e0, e1 = ex.explain_groups(imp_.reshape(1, B, W), e3, t3, n1, x1, n2, x2, 1, B, W, N, False)
+            else:   # constructor variants without HIP training kernels: the torch formulation
+                e0, e1 = ex._edge_imp_torch(([n1, n2], [x1, x2], None), imp_.reshape(B, W, 1), (None, e3, t3),
+                                            False)
             gs = torch.autograd.grad((e0, e1), [imp_] + list(params),
                                      grad_outputs=(g1.reshape(e0.shape), g2.reshape(e1.shape)), allow_unused=True)
         return (None, None, gs[0], None, None, *gs[1:])

@@ -556,3 +556,41 @@ def test_edge_table_path(tm, de):
     np.testing.assert_allclose(a[0].cpu().numpy(), b[0].cpu().numpy(), rtol=RTOL, atol=ATOL)
     np.testing.assert_allclose(a[1].cpu().numpy(), b[1].cpu().numpy(), rtol=RTOL, atol=ATOL)
     np.testing.assert_allclose(a[2].cpu().numpy(), b[2].cpu().numpy(), rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.parametrize("hid,if_cat,tg", [(128, True, True), (64, False, True), (32, False, False), (48, True, True)])
+def test_constructor_shapes_on_hip(tm, hid, if_cat, tg):
+    """TempME(hid_dim, if_cat_feature, use_temporal_guidance) shapes outside the fused walk kernel run the
+    LDS-tiled HIP kernels (tm_weights_create_ex): forward and retrieve_explanation(eval) within 1e-5 of the
+    torch-fp32 oracle, and the HIP path (not the torch formulation) ran."""
+    from tests.encoder_inputs import SIDES, load
+    d = load("synth")
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(hid + 7 * if_cat)
+    ex = tm.TempME(_Base(d["n_feat"], d["e_feat"], dev), "tgn", "x", out_dim=40, hid_dim=hid, device=dev,
+                   if_cat_feature=if_cat, use_temporal_guidance=tg,
+                   null_model={k + 1: float(v) for k, v in enumerate(d["null"])}).to(dev).eval()
+    sd = {k: v.detach().cpu() for k, v in ex.state_dict().items()}
+    imps, subs, walks = [], [], []
+    for s in SIDES:
+        x = d[s]
+        w = (x["node"], x["eid"], x["ts"], x["cat"], x["marg"])
+        with torch.no_grad():
+            imp = ex(w, d["ts_cut"], x["cnt"])
+        ref = er.forward(sd, d["n_feat"].float(), d["e_feat"].float(), x["node"], x["eid"], x["ts"], x["cat"],
+                         d["ts_cut"], x["cnt"], temporal=tg, if_cat=if_cat)
+        np.testing.assert_allclose(imp.cpu().numpy(), ref.numpy(), rtol=RTOL, atol=ATOL, err_msg=s)
+        imps.append(imp)
+        subs.append((x["sub_node"], x["sub_eid"], x["sub_ts"]))
+        walks.append(w)
+    with torch.no_grad():
+        expl = ex.retrieve_explanation(subs[0], imps[0], walks[0], subs[1], imps[1], walks[1], subs[2], imps[2],
+                                       walks[2], training=False)
+    for k, s in enumerate(SIDES):
+        x = d[s]
+        r0, r1 = er.edge_importance(sd, d["e_feat"].float(), imps[k].cpu(), x["eid"], x["ts"], x["sub_node"],
+                                    x["sub_eid"])
+        B = r0.shape[0]
+        np.testing.assert_allclose(expl[0][k * B:(k + 1) * B].cpu().numpy(), r0.numpy(), rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(expl[1][k * B:(k + 1) * B].cpu().numpy(), r1.numpy(), rtol=RTOL, atol=ATOL)
+    assert ex._packed is not None, "the HIP encoder did not run"
