@@ -147,9 +147,10 @@ def aux_rows(finder, src, dst, ts, eidx, pool, graph_build_ms):
 
 def khop_alone(pipe, inputs, steps, N, group=8):
     """The (a) kernel measured alone (the >= 50 % HBM target applies to it): 2-hop
-    sampling of the three sides of ``group`` steps' events per call -- src and dst on the e_idx path, the
-    pipeline's fake dst on the time path -- as three tm_sample_khop calls on three streams, timed from the
-    first launch to the last completion (HIP events on the launch streams)."""
+    sampling of ``group`` steps' events per launch, one tm_sample_khop launch per side -- src and dst on the
+    e_idx path, the pipeline's fake dst on the time path -- serialised on one stream, each launch timed with
+    HIP events on that stream, so every khop2_kernel duration is its own (a rocprofv3 kernel trace of the
+    same run gives the same per-launch average: profiles/r03_*_kernel_stats.csv)."""
     from tempme_amd import _lib as L
     g = pipe.graph
     dev = inputs[0][0].device
@@ -164,32 +165,30 @@ def khop_alone(pipe, inputs, steps, N, group=8):
         plans.append((ts, ev, ((L.SIDE_SRC, src, eidx), (L.SIDE_TGT, dst, eidx), (L.SIDE_BGD, torch.cat(fakes), None))))
     E = int(plans[0][0].numel())
     tot = E * (N + N * N)
-    outs = [(torch.empty(tot, dtype=torch.int32, device=dev), torch.empty(tot, dtype=torch.int32, device=dev),
-             torch.empty(tot, dtype=torch.float32, device=dev)) for _ in range(3)]
+    on, oe, ot = (torch.empty(tot, dtype=torch.int32, device=dev), torch.empty(tot, dtype=torch.int32, device=dev),
+                  torch.empty(tot, dtype=torch.float32, device=dev))
     err = torch.zeros(1, dtype=torch.int32, device=dev)
-    streams = [torch.cuda.Stream(device=dev) for _ in range(3)]
     main = torch.cuda.current_stream(dev)
     torch.cuda.synchronize()
     ms = []
-    for ts, ev, sides in plans + plans:                # first pass warms the streams, second is timed
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(main)
-        for st, (side, root, ei), (on, oe, ot) in zip(streams, sides, outs):
-            st.wait_event(a)
+    for ts, ev, sides in plans + plans:                # first pass warms up, second is timed
+        for side, root, ei in sides:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(main)
             L.check(L.lib().tm_sample_khop(g.handle, L.TmRng(pipe.seed, pipe.split, side), 2, N, E, L.ptr(root),
                                            L.ptr(ts), L.ptr(ei), L.ptr(ev), L.ptr(on), L.ptr(oe), L.ptr(ot),
-                                           L.ptr(err), st.cuda_stream), "tm_sample_khop")
-            main.wait_stream(st)
-        b.record(main)
-        b.synchronize()
-        ms.append(a.elapsed_time(b))
-    ms = ms[len(plans):]
+                                           L.ptr(err), main.cuda_stream), "tm_sample_khop")
+            b.record(main)
+            ms.append((a, b))
+    torch.cuda.synchronize()
+    ms = [a.elapsed_time(b) for a, b in ms[3 * len(plans):]]
     L.raise_device_error(int(err.item()), "khop_alone")
-    per_call_ms = sum(ms) / len(ms)
-    ach = khop_bytes_per_event(N) * E / (per_call_ms * 1e-3) / 1e9
-    return {"kernel": "khop2_kernel (tm_sample_khop k=2), 3 sides on 3 streams", "roots_per_call": E,
-            "avg_ms": round(per_call_ms, 4), "launches": 3 * len(ms), "bound": "hbm", "achieved": round(ach, 1),
-            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_event": khop_bytes_per_event(N)}
+    per_launch_ms = sum(ms) / len(ms)
+    bytes_per_root = khop_bytes_per_event(N) // 3
+    ach = bytes_per_root * E / (per_launch_ms * 1e-3) / 1e9
+    return {"kernel": "khop2_kernel (tm_sample_khop k=2), one launch per side, serialised", "roots_per_launch": E,
+            "avg_ms": round(per_launch_ms, 4), "launches": len(ms), "bound": "hbm", "achieved": round(ach, 1),
+            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_root": bytes_per_root}
 
 
 def dropin_leg(ex, pipe, inputs, B, N, budget_s=3.0):

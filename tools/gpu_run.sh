@@ -25,6 +25,7 @@ for s in "$@"; do
         bench1) step bench_c1 600 python bench.py --config 1 --no-cpu-baseline ;;
         benchq) step bench 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
         prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --no-extras ;;
+        profx) step rocprof_x 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profx -o run --output-format csv -- python bench.py --no-cpu-baseline ;;
         prof4) step rocprof_c4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof4 -o run --output-format csv -- python bench.py --config 4 --no-cpu-baseline --no-extras ;;
         enron) step pytest_enron 900 python -u -m pytest tests/test_gpu_enron.py -v --timeout 300 --timeout-method thread ;;
         pmc1|pmc2|pmc4)  # PMC passes (one counter group per run) over a short bench of configs[1|2|4]
