@@ -633,9 +633,10 @@ struct WalkArgs {
 };
 
 // Phase timing (debug builds only, -DTM_STAMPS; tools/stamps.py): s_memtime deltas of lane 0 per
-// pass type accumulated for workgroups 512..1023 (past the first dispatch round).
+// pass type accumulated for every 16th workgroup (sampled over the whole launch).
 #ifdef TM_STAMPS
 __device__ unsigned long long g_st[3][10];
+__device__ unsigned long long g_live;   // waves inside the pass loop right now
 #define TM_STAMP(k)                                 \
     do {                                            \
         __builtin_amdgcn_sched_barrier(0);          \
@@ -1039,6 +1040,7 @@ __global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
     else load_et<QE0>(a, cur.e, et);
 #ifdef TM_STAMPS
     const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) atomicMax(&g_st[2][9], atomicAdd(&g_live, 1ull) + 1);   // waves resident at once (max)
 #endif
     // pass 0: position 2 once per slot (walk j*M carries it); then per walk m: position 0, position 1
 #pragma nounroll
@@ -1110,7 +1112,7 @@ __global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
         }
         TM_STAMP(8);
 #ifdef TM_STAMPS
-        if (lane == 0 && blockIdx.x >= 512 && blockIdx.x < 1024) {
+        if (lane == 0 && blockIdx.x % 16 == 5) {
             for (int k = 0; k < 8; ++k) atomicAdd(&g_st[p][k], T[k + 1] - T[k]);
             atomicAdd(&g_st[p][8], 1ull);
         }
@@ -1118,10 +1120,11 @@ __global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
     }
 #ifdef TM_STAMPS
     // in-kernel clock: shader-clock ticks over 100 MHz real-time ticks of the wave's pass loop
-    if (lane == 0 && blockIdx.x >= 512 && blockIdx.x < 1024) {
+    if (lane == 0 && blockIdx.x % 16 == 5) {
         atomicAdd(&g_st[0][9], __builtin_amdgcn_s_memtime() - clk_t0);
         atomicAdd(&g_st[1][9], __builtin_amdgcn_s_memrealtime() - clk_r0);
     }
+    if (lane == 0) atomicAdd(&g_live, ~0ull);
 #endif
 }
 

@@ -56,7 +56,7 @@ for s in "$@"; do
             for so in tempme_amd/lib/ab_st/*.so; do
                 n=$(basename "$so" .so)
                 TEMPME_LIB="$PWD/$so" step stamps_$n 300 python tools/stamps.py
-                { echo "== $n: $(grep -o '"walk_kernel": {"avg_ms": [0-9.]*' gpurun_out/stamps_$n.log)"; grep -E "^(slot|walk) |clock" gpurun_out/stamps_$n.log; } | tee -a gpurun_out/stamps.txt
+                { echo "== $n: $(grep -o '"walk_kernel": {"avg_ms": [0-9.]*' gpurun_out/stamps_$n.log)"; grep -E "^(slot|walk) |clock|wave pass-loop" gpurun_out/stamps_$n.log; } | tee -a gpurun_out/stamps.txt
             done ;;
         dist2)  # multi-rank rehearsal on one GPU: bench.py starts its own 2 ranks (gloo barrier/max), both on cuda:0
             TEMPME_DIST_BACKEND=gloo step dist2 300 python bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu-baseline ;;

@@ -24,3 +24,5 @@ for pt, pname in ((2, "slot p2"), (0, "walk p0"), (1, "walk p1")):
           "total=%.0f" % (sum(row[:8]) / n))
 print("walk_kernel in-kernel clock %.3f GHz (s_memtime / s_memrealtime over each wave's pass loop)"
       % (0.1 * buf[9] / max(1, buf[19])))
+print("walk_kernel mean wave pass-loop cycles %.0f over %d waves, %.1f us; max waves resident at once %d"
+      % (buf[9] / max(1, buf[28]), buf[28], buf[19] / max(1, buf[28]) * 0.01, buf[29]))
