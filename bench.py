@@ -497,6 +497,14 @@ def main():
 
     n_steps = args.warmup + args.steps
     strong = not args.weak
+    # distinct devices the ranks run on (a gloo rehearsal puts several ranks on one GPU): n_gpus counts
+    # devices, "ranks" the processes
+    if world > 1:
+        devs = [None] * world
+        dist.all_gather_object(devs, dev.index)
+        n_gpus = len(set(devs))
+    else:
+        n_gpus = 1
     if strong and args.batches % world:
         raise SystemExit(f"bench.py: --batches {args.batches} is not divisible by the {world} ranks")
     per_rank = (args.batches // world if strong else args.batches) * B
@@ -545,7 +553,7 @@ def main():
         if samp and traffic.get("events_kernel") is not None:
             samp["traffic"] = traffic["events_kernel"]
         total = world * args.steps * per_rank
-        out = {"metric": METRIC, "value": round(total / el, 2), "unit": "edges/s", "n_gpus": world,
+        out = {"metric": METRIC, "value": round(total / el, 2), "unit": "edges/s", "n_gpus": n_gpus, "ranks": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
                "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
                "dtype": "fp32",

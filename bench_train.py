@@ -4,12 +4,14 @@ target-edge batches sharded across GPUs with one RCCL gradient all-reduce per st
     python bench_train.py [--gpus N --steps K --warmup W --n-degree 20 --batch-size 100]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench_train.py --gpus N
 
-One step = temp_exp_main.py:593-632 for one batch of `--batch-size` target events per GPU: base
+One train step = temp_exp_main.py:593-632 for one batch of `--batch-size` target events per GPU: base
 contrast without explanation (no grad), TempME forward x3 (training mode: dropout, Beta rsample),
 retrieve_explanation, contrast with explanation weights, BCE + 0.5 KL, backward, gradient all-reduce,
 Adam.  The pack (k-hop subgraphs, walks, categories, edge counts of every training event) is sampled
 on the device before timing, as the reference samples it offline (processed/data_preprocess.py).
-Prints one JSON line (rank 0); value = trained target edges per second over all ranks.
+A timed step is `--global-batches` reference batches over all ranks (strong scaling: N ranks take
+global-batches / N train steps each, one all-reduced update per round of N batches; `--weak`: that
+many per rank).  Prints one JSON line (rank 0); value = trained target edges per second over all ranks.
 """
 import argparse
 import json
@@ -35,6 +37,13 @@ def main():
     ap.add_argument("--graph", action="store_true", help="capture the step as a HIP graph with several ranks "
                     "too (the RCCL all-reduce is then captured inside the graph)")
     ap.add_argument("--no-fused-adam", action="store_true", help="torch's default (foreach) Adam")
+    ap.add_argument("--global-batches", type=int, default=8,
+                    help="reference batches per timed step over ALL ranks (strong scaling: each rank steps through "
+                         "global-batches / N of them, one all-reduced Adam update per round of N batches)")
+    ap.add_argument("--weak", action="store_true", help="--global-batches per rank instead (weak scaling)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="eager multi-rank path: run the gradient all-reduce serially instead of overlapping it "
+                         "with the next batch's explainer-independent work")
     args = ap.parse_args()
 
     # one process per GPU: start our own ranks unless a launcher already did (before any GPU call)
@@ -68,7 +77,7 @@ def main():
     from tempme_amd.preprocess import sample_events
     from tempme_amd.sharding import max_over_ranks
     from tempme_amd.tgn import TGN
-    from tempme_amd.train import GradAllReduce, GraphedTrainStep, batch_from_pack, epoch_spans, train_step
+    from tempme_amd.train import GradAllReduce, GraphedTrainStep, batch_from_pack, epoch_spans, run_steps
     from tempme_amd.workload import enron_like, split
 
     N, M, B = args.n_degree, 3, args.batch_size
@@ -96,7 +105,10 @@ def main():
     sync = GradAllReduce(ex)
     ex.train()
 
-    n_steps = args.warmup + args.steps
+    if not args.weak and args.global_batches % world:
+        raise SystemExit(f"bench_train.py: --global-batches {args.global_batches} is not divisible by {world} ranks")
+    per_step = args.global_batches if args.weak else args.global_batches // world   # train_steps per rank per step
+    n_steps = (args.warmup + args.steps) * per_step
     gen = torch.Generator().manual_seed(args.seed)
     spans = []
     while len(spans) < n_steps + 4:     # a few spare in case the graphed path drops an epoch's tail batch
@@ -109,10 +121,19 @@ def main():
         n_steps = min(n_steps, len(rows))
         graphed = GraphedTrainStep(ex, base, opt, buf, s_d, d_d, t_d, e_d, rows[:max(args.warmup, 1)],
                                    grad_sync=sync)
-        step = lambda k: graphed(rows[k])  # noqa: E731
+
+        def step(k):   # one timed step = per_step replays
+            out = None
+            for i in range(k * per_step, (k + 1) * per_step):
+                out = graphed(rows[i])
+            return out
     else:
         batches = [batch_from_pack(buf, s_d, d_d, t_d, e_d, r) for r in rows]
-        step = lambda k: train_step(ex, base, opt, batches[k], grad_sync=sync)  # noqa: E731
+
+        def step(k):   # one timed step = per_step train_steps; the all-reduce overlaps the next batch's prep
+            outs = run_steps(ex, base, opt, batches[k * per_step:(k + 1) * per_step], grad_sync=sync,
+                             overlap=not args.no_overlap)
+            return outs[-1]
         for k in range(args.warmup):
             step(k)
     torch.cuda.synchronize()
@@ -123,7 +144,8 @@ def main():
     L.profile_enable(True)
     t0 = time.perf_counter()
     losses = []
-    for k in range(args.warmup, n_steps):
+    n_timed = n_steps // per_step
+    for k in range(args.warmup, n_timed):
         losses.append(step(k)["loss"].clone())
     torch.cuda.synchronize()
     if dist:
@@ -132,16 +154,25 @@ def main():
     prof = L.profile_read()
     L.profile_enable(False)
     el = max_over_ranks(el, dist, dev if backend == "nccl" else "cpu")
+    if world > 1:   # distinct devices (a gloo rehearsal puts the ranks on one GPU)
+        devs = [None] * world
+        dist.all_gather_object(devs, dev.index)
+        n_gpus = len(set(devs))
+    else:
+        n_gpus = 1
     losses = [float(x) for x in losses]
     if rank == 0:
-        edges = sum(int(rows[k].numel()) for k in range(args.warmup, n_steps)) * world
+        edges = sum(int(rows[k].numel()) for k in range(args.warmup * per_step, n_timed * per_step)) * world
+        timed = n_timed - args.warmup
         out = {"metric": "trained target-edges/sec (explainer training step, TGN + full-Enron-shaped graph)",
-               "value": round(edges / el, 2), "unit": "edges/s", "n_gpus": world, "steps": args.steps,
-               "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+               "value": round(edges / el, 2), "unit": "edges/s", "n_gpus": n_gpus, "ranks": world, "steps": timed,
+               "warmup": args.warmup, "ms_per_step": round(el / max(timed, 1) * 1e3, 3), "higher_is_better": True,
+               "scaling": "weak" if args.weak else "strong", "vs_baseline": None, "dtype": "fp32",
                "data": "synthetic (seeded Enron-shaped graph V=184 E=125,235, random-init TGN and TempME)",
                "config": {"workload": "configs[3]: full Enron + TGN explainer training step", "n_degree": N,
                           "batch_size": B, "train_events": int(len(src)), "parallelism": f"dp{world}",
+                          "global_batches_per_step": per_step * world, "train_steps_per_rank_per_step": per_step,
+                          "allreduce_overlap": (not args.no_overlap) and not use_graph,
                           "hip_graph": use_graph,
                           "grad_bucket_floats": sum(p.numel() for p in ex.parameters() if p.grad is not None)},
                "loss_first_last": [round(losses[0], 5), round(losses[-1], 5)],

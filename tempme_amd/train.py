@@ -16,7 +16,9 @@ step matches the reference statistically, not bit for bit; with ``Explainer.eval
 
 Data parallel: one process per GPU, each stepping its own whole batches; after
 backward the explainer's gradients (one flat fp32 bucket, ~0.46 MB at uslegis dims) are averaged
-with ONE all-reduce over RCCL before the optimizer step, so every rank keeps identical weights.
+with ONE all-reduce over RCCL before the optimizer step, so every rank keeps identical weights.  The
+all-reduce is issued asynchronously and the next batch's explainer-independent work (``prepare_step``)
+runs while it is in flight (``run_steps``).
 """
 import numpy as np
 import torch
@@ -119,14 +121,22 @@ def encode_sides(explainer, batch):
 
 
 class GradAllReduce:
-    """Average the explainer's gradients over the process group with one collective per step."""
+    """Average the explainer's gradients over the process group with one collective per step.
+
+    ``start()`` flattens the gradients into one bucket and launches the all-reduce asynchronously;
+    ``finish()`` waits for it and writes the averages back.  Work issued between the two (the next
+    batch's gather and the frozen base model's original-prediction contrast, which read neither the
+    explainer's gradients nor its weights) overlaps the collective.  ``__call__`` does
+    both back to back."""
 
     def __init__(self, module, group=None):
         self.module, self.group = module, group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self._flat = None
+        self._work = None
+        self._grads = None
 
-    def __call__(self):
+    def start(self):
         if self.world == 1:
             return
         grads = [p.grad for p in self.module.parameters() if p.grad is not None]
@@ -139,12 +149,24 @@ class GradAllReduce:
         for g in grads:
             self._flat[off:off + g.numel()].copy_(g.reshape(-1))
             off += g.numel()
-        dist.all_reduce(self._flat, op=dist.ReduceOp.SUM, group=self.group)
+        self._grads = grads
+        self._work = dist.all_reduce(self._flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
+    def finish(self):
+        if self._work is None:
+            return
+        self._work.wait()
+        self._work = None
         self._flat.div_(self.world)
         off = 0
-        for g in grads:
+        for g in self._grads:
             g.copy_(self._flat[off:off + g.numel()].view_as(g))
             off += g.numel()
+        self._grads = None
+
+    def __call__(self):
+        self.start()
+        self.finish()
 
 
 def explain_sides(explainer, batch, imps, training):
@@ -170,23 +192,31 @@ def explain_sides(explainer, batch, imps, training):
     return [e1.reshape(G * B, N)]
 
 
-def train_step(explainer, base_model, optimizer, batch, *, beta=0.5, prior_p=0.3, if_bern=True, criterion=None,
-               grad_sync=None):
-    """temp_exp_main.py:593-632 for one batch; returns the step's tensors (no host sync)."""
-    criterion = criterion or torch.nn.BCEWithLogitsLoss()
-    sg_s, sg_t, sg_b = batch.subgraphs
-    w_s, w_t, w_b = batch.walks
-    # the two contrasts of the batch (original and explained) share their derived inputs when the base
-    # model can prepare them (TGN: subgraph concatenations and time offsets built once per step)
+def prepare_step(base_model, batch):
+    """The explainer-independent part of a step (temp_exp_main.py:593-603): the base model's contrast
+    inputs (TGN: built once for both contrasts) and its original predictions -> y_ori, under no_grad.
+    Issued for batch k+1 while batch k's gradient all-reduce is in flight (``train_step(overlap=...)``)."""
     kw = {}
-    if hasattr(base_model, "prepare_contrast"):
-        with torch.no_grad():
-            kw["prepared"] = base_model.prepare_contrast(batch.src, batch.dst, batch.fake, batch.ts, sg_s, sg_t, sg_b)
+    sg_s, sg_t, sg_b = batch.subgraphs
     with torch.no_grad():
+        if hasattr(base_model, "prepare_contrast"):
+            kw["prepared"] = base_model.prepare_contrast(batch.src, batch.dst, batch.fake, batch.ts, sg_s, sg_t, sg_b)
         pos_out_ori, neg_out_ori = base_model.contrast(batch.src, batch.dst, batch.fake, batch.ts, batch.e_idx,
                                                        sg_s, sg_t, sg_b, **kw)
         y_pred = torch.cat([pos_out_ori, neg_out_ori], dim=0).sigmoid()
         y_ori = torch.where(y_pred > 0.5, 1., 0.).view(y_pred.size(0), 1)
+    return kw, pos_out_ori, neg_out_ori, y_ori
+
+
+def train_step(explainer, base_model, optimizer, batch, *, beta=0.5, prior_p=0.3, if_bern=True, criterion=None,
+               grad_sync=None, prepared=None, overlap=None):
+    """temp_exp_main.py:593-632 for one batch; returns the step's tensors (no host sync).  ``prepared``:
+    this batch's ``prepare_step`` output if it was issued earlier; ``overlap``: a callable run while the
+    gradient all-reduce is in flight (between ``grad_sync.start()`` and ``.finish()``)."""
+    criterion = criterion or torch.nn.BCEWithLogitsLoss()
+    sg_s, sg_t, sg_b = batch.subgraphs
+    w_s, w_t, w_b = batch.walks
+    kw, pos_out_ori, neg_out_ori, y_ori = prepared if prepared is not None else prepare_step(base_model, batch)
     optimizer.zero_grad()
     g_s, g_t, g_b = encode_sides(explainer, batch)
     explanation = explain_sides(explainer, batch, (g_s, g_t, g_b), if_bern)
@@ -204,12 +234,39 @@ def train_step(explainer, base_model, optimizer, batch, *, beta=0.5, prior_p=0.3
                    + explainer.kl_loss(g_b, w_b, target=prior_p))
     loss = pred_loss + beta * kl_loss
     loss.backward()
-    if grad_sync is not None:
+    if grad_sync is not None and hasattr(grad_sync, "start"):
+        grad_sync.start()
+    elif grad_sync is not None:
         grad_sync()
+    if overlap is not None:
+        overlap()
+    if grad_sync is not None and hasattr(grad_sync, "finish"):
+        grad_sync.finish()
     optimizer.step()
     return dict(loss=loss.detach(), pred_loss=pred_loss.detach(), kl_loss=kl_loss.detach(),
                 pos_logit=pos_logit.detach(), neg_logit=neg_logit.detach(), pos_out_ori=pos_out_ori,
                 neg_out_ori=neg_out_ori, y_ori=y_ori)
+
+
+def run_steps(explainer, base_model, optimizer, batches, *, grad_sync=None, overlap=True, **kw):
+    """``train_step`` over a list of batches; with ``overlap`` (and a process group), batch k+1's gather
+    result is prepared (``prepare_step``) while batch k's gradient all-reduce is in flight.  Same
+    updates as the serial loop (tests/test_multi_rank.py)."""
+    outs = []
+    nxt = prepare_step(base_model, batches[0]) if batches else None
+    for k, b in enumerate(batches):
+        cur, box = nxt, {}
+        if overlap and k + 1 < len(batches):
+            def pre(b1=batches[k + 1]):
+                box["p"] = prepare_step(base_model, b1)
+        else:
+            pre = None
+        outs.append(train_step(explainer, base_model, optimizer, b, grad_sync=grad_sync, prepared=cur, overlap=pre,
+                               **kw))
+        nxt = box.get("p") if k + 1 < len(batches) else None
+        if nxt is None and k + 1 < len(batches):
+            nxt = prepare_step(base_model, batches[k + 1])
+    return outs
 
 
 class GraphedTrainStep:
@@ -289,10 +346,8 @@ def train_epoch(explainer, base_model, optimizer, buf, src, dst, ts, e_idx, bs, 
     num_instance = int(src.shape[0]) - 1              # the reference leaves the last event out (:560-561)
     perm = torch.randperm(num_instance, generator=generator).to(src.device)
     explainer.train()
-    outs = []
-    for s_idx, e_end in epoch_spans(num_instance, bs, rank, world):
-        batch = batch_from_pack(buf, src, dst, ts, e_idx, perm[s_idx:e_end])
-        out = train_step(explainer, base_model, optimizer, batch, beta=beta, prior_p=prior_p, if_bern=if_bern,
-                         grad_sync=grad_sync)
-        outs.append(step_metrics(out) if metrics else out)
-    return outs
+    batches = [batch_from_pack(buf, src, dst, ts, e_idx, perm[s_idx:e_end])
+               for s_idx, e_end in epoch_spans(num_instance, bs, rank, world)]
+    outs = run_steps(explainer, base_model, optimizer, batches, grad_sync=grad_sync, beta=beta, prior_p=prior_p,
+                     if_bern=if_bern)
+    return [step_metrics(o) for o in outs] if metrics else outs

@@ -211,3 +211,59 @@ def test_bench_rejects_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--launch-check"],
                        capture_output=True, text=True, timeout=240, env=env, cwd=repo)
     assert r.returncode != 0 and "--gpus 2" in r.stderr
+
+
+def _overlap_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tempme_amd.train import GradAllReduce
+        nets, opts, syncs = [], [], []
+        for _ in range(2):
+            torch.manual_seed(0)
+            net = torch.nn.Sequential(torch.nn.Linear(5, 7), torch.nn.ReLU(), torch.nn.Linear(7, 1))
+            nets.append(net)
+            opts.append(torch.optim.Adam(net.parameters(), lr=1e-2))
+            syncs.append(GradAllReduce(net))
+        side = []
+        for step in range(4):
+            x = torch.randn(4, 5, generator=torch.Generator().manual_seed(100 * step + rank))
+            for i, (net, opt, sync) in enumerate(zip(nets, opts, syncs)):
+                opt.zero_grad()
+                net(x).pow(2).mean().backward()
+                if i == 0:
+                    sync()                                   # serial: all-reduce, then the optimizer
+                else:
+                    sync.start()                             # overlapped: the next batch's independent work
+                    side.append(torch.randn(64, 64).matmul(torch.randn(64, 64)).sum())   # runs in flight
+                    sync.finish()
+                opt.step()
+        for a, b in zip(nets[0].parameters(), nets[1].parameters()):
+            assert torch.equal(a, b)
+        got = [None] * world
+        dist.all_gather_object(got, [p.detach().clone() for p in nets[1].parameters()])
+        if rank == 0:
+            for a, b in zip(got[0], got[1]):
+                assert torch.equal(a, b)                     # replicas identical
+            q.put("ok")
+    except Exception as exc:
+        q.put(repr(exc))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_overlapped_all_reduce_equals_serial():
+    """GradAllReduce.start()/finish() with other work in between (train.run_steps overlaps the next
+    batch's prepare_step with the collective) gives exactly the serial step's gradients and updates."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == "ok", res
+    assert all(p.exitcode == 0 for p in procs)
