@@ -534,7 +534,8 @@ def main():
             # per row: projection N (C+T) C + per mixer channel FFN 2 N C HC + token FFN 2 N HT C MACs
             C_, T_, HT_, HC_ = gm.num_channels, gm.time_feat_dim, int(0.5 * N), int(4 * gm.num_channels)
             per_row = 2 * (N * (C_ + T_) * C_ + gm.num_layers * (2 * N * C_ * HC_ + 2 * N * HT_ * C_))
-            units["gm_embed_kernel"] = ("mfma", per_row * 3 * E)
+            units["gm_embed_kernel"] = ("mfma", per_row * 3 * E)   # LDS-tiled form (dims outside tm_gm_fused_ok)
+            units["gm_fused_kernel"] = ("mfma", per_row * 3 * E)   # register-resident form
         kernels = kernel_table(prof, units, executed)
         traffic, tsrc = load_traffic(cfg["name"])
         dom = max((k for k in kernels if "bound" in kernels[k]), key=lambda k: kernels[k]["avg_ms"])

@@ -423,6 +423,14 @@ int64_t tm_gm_packed_floats(int32_t n_out, int32_t k);
 /* W [n_out, k] row-major (nn.Linear.weight) -> MFMA B-operand fragments */
 int tm_gm_pack(const float *w, int32_t n_out, int32_t k, float *packed, void *stream);
 int tm_gm_embed(const tm_gm_embed_args *a, void *stream);
+/* 1 when tm_gm_embed runs the register-resident kernel for these dims (C % 4 == 0, T % 4 == 0, N <= 32,
+ * C <= 256); its weights are then packed by tm_gm_pack_a instead of tm_gm_pack: proj_w with
+ * (n_mult, k_mult) = (1, 4), channel ffn.0 with (2, 1), ffn.3 with (1, 2) */
+int tm_gm_fused_ok(int32_t N, int32_t C, int32_t T, int32_t HC);
+/* floats of tm_gm_pack_a's output: 16-row / 16-column tiles rounded up to multiples of n_mult / k_mult */
+int64_t tm_gm_packed_a_floats(int32_t n_out, int32_t k, int32_t n_mult, int32_t k_mult);
+/* W [n_out, k] row-major -> MFMA A-operand fragments (weights as the 16-output-row operand) */
+int tm_gm_pack_a(const float *w, int32_t n_out, int32_t k, int32_t n_mult, int32_t k_mult, float *packed, void *stream);
 
 #ifdef __cplusplus
 }

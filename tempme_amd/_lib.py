@@ -37,7 +37,7 @@ EXPORTS = (
     "tm_encoder_workspace_bytes",
     "tm_encoder_fwd", "tm_encoder_fwd_tab", "tm_encoder_train_fwd", "tm_encoder_bwd", "tm_encoder_wgrad", "tm_wgrad",
     "tm_explain_train_fwd", "tm_explain_train_bwd", "tm_kl_loss", "tm_edge_importance", "tm_edge_gate_table",
-    "tm_edge_table_cols", "tm_edge_tables", "tm_edge_feature_table", "tm_edge_importance_tab", "tm_tgn_attn_fwd", "tm_tgn_attn_bwd", "tm_gm_packed_floats", "tm_gm_pack", "tm_gm_embed",
+    "tm_edge_table_cols", "tm_edge_tables", "tm_edge_feature_table", "tm_edge_importance_tab", "tm_tgn_attn_fwd", "tm_tgn_attn_bwd", "tm_gm_packed_floats", "tm_gm_pack", "tm_gm_embed", "tm_gm_packed_a_floats", "tm_gm_pack_a", "tm_gm_fused_ok",
     "tm_mask_least_important", "tm_profile_enable", "tm_profile_sync", "tm_profile_entry",
 )
 
@@ -151,6 +151,10 @@ def _sig(L):
     L.tm_gm_packed_floats.argtypes = [i32, i32]
     L.tm_gm_pack.argtypes = [vp, i32, i32, vp, vp]
     L.tm_gm_embed.argtypes = [C.POINTER(GmEmbedArgs), vp]
+    L.tm_gm_packed_a_floats.restype = i64
+    L.tm_gm_packed_a_floats.argtypes = [i32, i32, i32, i32]
+    L.tm_gm_pack_a.argtypes = [vp, i32, i32, i32, i32, vp, vp]
+    L.tm_gm_fused_ok.argtypes = [i32, i32, i32, i32]
     L.tm_tgn_attn_fwd.argtypes = [C.POINTER(TgnAttn), vp, vp, vp]
     L.tm_tgn_attn_bwd.argtypes = [C.POINTER(TgnAttn), vp, vp, vp, vp, vp]
     L.tm_mask_least_important.argtypes = [vp, i32, i32, vp, i32, vp, vp, vp]

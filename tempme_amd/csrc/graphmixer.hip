@@ -405,6 +405,415 @@ __global__ void gm_pack_kernel(const float *__restrict__ w, int32_t n_out, int32
     }
 }
 
+// ================================================================== register-resident form (gm_fused_kernel)
+//
+// The walk kernel's orientation (encoder.hip): weights are the MFMA A operand (16 output features per
+// tile), a wave's 16 tokens are the B operand's columns, lane l holding features 16q + 4(l>>4) + {0..3}
+// of token l & 15 -- so the D tile of one GEMM is the B fragment of K tile q of the next and a token
+// tile's whole channel FFN, C -> 4C -> C, runs in registers: per pair of hidden tiles the first GEMM
+// (two interleaved accumulators over the C / 16 K tiles of the LayerNorm-ed input), GELU on the
+// accumulators, then the second GEMM accumulates the pair into the C / 16 output tiles.  No LDS in the
+// FFN, no hidden chunks, no barriers inside a layer's channel mix.  Weight fragments stream from L2
+// GF_PF ahead in one ring across the pair loop (the fragments of a pair: 4 C/16, a multiple of GF_PF).
+// LDS holds the X image [token][channel] (row stride 16 NC + 4) for what crosses tokens: the token
+// mixing (both token tiles of a row) and the residual; the projection input's edge-feature rows are
+// staged in the same image first (coalesced row loads), the time features computed in the K loop.
+constexpr int GF_PF = 4;
+
+// W [n_out][k] row-major -> A-operand fragments, tiles rounded up to multiples of n_mult / k_mult:
+// packed[((t * KT + q) * 64 + lane) * 4 + s] = W[16 t + (lane & 15)][16 q + 4 (lane >> 4) + s] (zero outside W)
+__global__ void gm_pack_a_kernel(const float *__restrict__ w, int32_t n_out, int32_t k, int32_t KT, int64_t total,
+                                 float *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int s = (int)(i & 3), lane = (int)((i >> 2) & 63);
+        const int64_t f = i >> 8;
+        const int q = (int)(f % KT), t = (int)(f / KT);
+        const int n = 16 * t + (lane & 15), kk = 16 * q + 4 * (lane >> 4) + s;
+        out[i] = (n < n_out && kk < k) ? w[(int64_t)n * k + kk] : 0.f;
+    }
+}
+
+// a pointer read from the device layer table is wave-uniform, but the compiler cannot prove it (the
+// table is ordinary global memory): without this, a buffer resource built from it sits in VGPRs and every
+// buffer load becomes a readfirstlane waterfall loop
+__device__ __forceinline__ const float *gf_uniform(const float *p) {
+    const uint64_t v = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return reinterpret_cast<const float *>(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gf_rsrc(const void *p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+
+// one 1-KB fragment: lane offset vo (VGPR), fragment byte offset so (wave-uniform, SGPR)
+__device__ __forceinline__ float4 gf_frag(__amdgpu_buffer_rsrc_t r, int vo, int so) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0));
+}
+
+__device__ __forceinline__ gmx4 gf_mfma4(const float4 &a, const float4 &b, gmx4 c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, c, 0, 0, 0);
+    return c;
+}
+
+// a [n] fp32 vector (n % 4 == 0) as a buffer resource: a float4 at byte offset 16 i (i < n / 4) is
+// one buffer load, and any float4 at or beyond n reads zero (the hardware range check on the
+// offset incl. the immediate) -- no clamped index, no select, no branch, no 64-bit address per lane
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gf_vrsrc(const float *v, int n) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(v), (short)0, n * 4, 0x00020000);
+}
+__device__ __forceinline__ float4 gf_vload(__amdgpu_buffer_rsrc_t r, int byte_off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+
+// A wave's place in the workgroup, recomputed at the start of every phase from the laundered thread id
+// (gm_tid): values derived once at kernel entry are loop-invariant to the compiler, which then hoists
+// every lane mask and LDS address of the layer loop out of it and holds them across all phases.
+template <int NC, int NTT>
+struct GfIds {
+    static constexpr int RPW = 4 / NTT, XS = 16 * NC + 4, C16 = 16 * NC;
+    int lane, m, j, tt, rl, tok;
+    float *Xr, *Xw, *colm, *colr, *sew, *sval;
+    __device__ __forceinline__ GfIds() {
+        extern __shared__ float gm_lds[];
+        const int t = gm_tid(), wave = t >> 6;
+        lane = t & 63;
+        m = lane & 15;
+        j = lane >> 4;
+        rl = wave / NTT;
+        tt = wave % NTT;
+        tok = 16 * tt + m;
+        Xr = gm_lds + rl * NTT * 16 * XS;                   // the row's image: token t at Xr + t * XS
+        Xw = Xr + tt * 16 * XS;                             // this wave's 16 tokens
+        colm = gm_lds + 64 * XS + rl * 2 * C16;
+        colr = colm + C16;
+        sew = gm_lds + 64 * XS + RPW * 2 * C16 + rl * 64;
+        sval = sew + 32;
+    }
+};
+
+// NC = channel tiles (C <= 16 NC), NTT = token tiles per row (N <= 16 NTT).  A workgroup of 4 waves takes
+// 4 / NTT rows, one wave per (row, token tile).  LDS plan (floats): X image [4 waves][16 tokens][XS] |
+// per row: token-LN column mean, rstd [2][16 NC] | ew_eff, valid [2][32].
+template <int NC, int NTT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 13 ? 3 : 2))) gm_fused_kernel(GmArgs a) {
+    typedef GfIds<NC, NTT> Ids;
+    constexpr int RPW = Ids::RPW, XS = Ids::XS, C16 = Ids::C16;
+    extern __shared__ float gm_lds[];
+    const int R = a.R, N = a.N, C = a.C, T = a.T;
+    const bool has_ew = a.ew != nullptr;
+    {
+        const int tid = gm_tid();
+        if (tid < RPW * 32) {
+            const int rl2 = tid >> 5, t = tid & 31, r2 = min((int)blockIdx.x * RPW + rl2, R - 1);
+            float *se = gm_lds + 64 * XS + RPW * 2 * C16 + rl2 * 64;
+            const bool v = t < N && a.nid[(size_t)r2 * N + t] != 0;
+            se[32 + t] = v ? 1.f : 0.f;
+            // exp_src * mask (:154-155); without explanation weights the mixer multiplies by nothing (1.0)
+            se[t] = t < N ? (has_ew ? a.ew[(size_t)r2 * N + t] * (v ? 1.f : 0.f) : 1.f) : 0.f;
+        }
+    }
+    // ---- projection input: the wave's 16 edge-feature rows into its image (padding neighbours zeroed
+    // unless edge_attr is given), one coalesced row load per token
+    {
+        const Ids I;
+        const int rr = min((int)blockIdx.x * RPW + I.rl, R - 1);
+        const size_t rowN = (size_t)rr * N;
+        const int nf4 = C >> 2;
+#pragma unroll 4
+        for (int mm = 0; mm < 16; ++mm) {
+            const int t = 16 * I.tt + mm, tc = min(t, N - 1);
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (I.lane < nf4) {
+                if (a.edge_attr) {
+                    v = reinterpret_cast<const float4 *>(a.edge_attr + (rowN + tc) * C)[I.lane];
+                    if (t >= N) v = make_float4(0.f, 0.f, 0.f, 0.f);
+                } else {
+                    const bool ok = t < N && a.nid[rowN + tc] != 0;
+                    v = reinterpret_cast<const float4 *>(a.e_feat + (size_t)a.eid[rowN + tc] * C)[I.lane];
+                    if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+                *reinterpret_cast<float4 *>(I.Xw + mm * XS + 4 * I.lane) = v;
+            }
+        }
+    }
+    __syncthreads();
+    // ---- projection (:156-167): X = [E(e) | cos(dt w + b)] Wp^T + bp over K tiles padded to a multiple
+    // of 4 (zero fragments); B fragment of K tile q: edge features from the image, time features computed
+    {
+        const Ids I;
+        const int m = I.m, j = I.j, vo = I.lane * 16;
+        const int rr = min((int)blockIdx.x * RPW + I.rl, R - 1), tokc = min(I.tok, N - 1);
+        const size_t rowN = (size_t)rr * N;
+        const bool tv = I.tok < N && a.nid[rowN + tokc] != 0;
+        const float dt = (float)(a.cut[rr] - a.ts[rowN + tokc]);
+        const int KP = ((C + T + 63) / 64) * 4;
+        const auto wr = gf_rsrc(a.proj_w);
+        const auto rtw = gf_vrsrc(a.time_w, T), rtb = gf_vrsrc(a.time_b, T), rb = gf_vrsrc(a.proj_b, C);
+        gmx4 y[NC];
+#pragma unroll
+        for (int o = 0; o < NC; ++o) {
+            const float4 b = gf_vload(rb, 64 * o + 16 * j);
+            y[o] = gmx4{b.x, b.y, b.z, b.w};
+        }
+        // fragment (o, q) at ((o * KP + q) * 64 + lane) * 16 B; the ring walks q-major, o-minor
+        float4 ring[GF_PF];
+#pragma unroll
+        for (int i = 0; i < GF_PF; ++i) ring[i] = gf_frag(wr, vo, ((i % NC) * KP + i / NC) * 1024);
+        for (int q0 = 0; q0 < KP; q0 += 4) {
+            // iteration bases opaque per iteration: loop strength reduction would otherwise keep every
+            // fragment's offset as its own SGPR induction variable
+            int qb = q0 * 1024, qn = min(q0 + 4, KP - 4) * 1024;
+            asm volatile("" : "+s"(qb), "+s"(qn));
+#pragma unroll
+            for (int dq = 0; dq < 4; ++dq) {
+                const int k0 = 16 * (q0 + dq) + 4 * j;
+                float4 bx;
+                if (k0 < C) {
+                    bx = *reinterpret_cast<const float4 *>(I.Xw + m * XS + k0);
+                } else {
+                    // Linear(1, d) on fp32 dt: one rounding of dt * w + b (the reference's CPU addmm); k >= T
+                    // reads w = b = 0 and is zeroed
+                    const int kt = k0 - C;
+                    const float4 fw = gf_vload(rtw, 4 * kt), fb = gf_vload(rtb, 4 * kt);
+                    const bool on = tv && kt < T;
+                    auto te = [&](float fr, float ph) {
+                        return on ? cos_rd((float)((double)dt * (double)fr + (double)ph)) : 0.f;
+                    };
+                    bx = make_float4(te(fw.x, fb.x), te(fw.y, fb.y), te(fw.z, fb.z), te(fw.w, fb.w));
+                }
+#pragma unroll
+                for (int o = 0; o < NC; ++o) {
+                    const int f = dq * NC + o, fn = f + GF_PF;   // this fragment, the one issued into its slot
+                    const float4 w = ring[f % GF_PF];
+                    const int dn = fn / NC, on = fn % NC;        // K tile q0 + dn (dn < 4) or the next iteration's
+                    ring[f % GF_PF] = dn < 4 ? gf_frag(wr, vo, qb + (on * KP + dn) * 1024)
+                                             : gf_frag(wr, vo, qn + (on * KP + dn - 4) * 1024);
+                    y[o] = gf_mfma4(w, bx, y[o]);
+                }
+            }
+        }
+        // X = projection, zero on padding tokens and channels (the image keeps them zero from here on)
+#pragma unroll
+        for (int o = 0; o < NC; ++o) {
+            const bool in = I.tok < N && 16 * o + 4 * j < C;
+            *reinterpret_cast<float4 *>(I.Xw + m * XS + 16 * o + 4 * j) =
+                in ? make_float4(y[o][0], y[o][1], y[o][2], y[o][3]) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+    __syncthreads();
+    const int NH2 = ((a.HC + 31) / 32) * 2;   // hidden tiles, rounded up to pairs (zero fragments)
+    for (int l = 0; l < a.L; ++l) {
+        const float *const *w = a.lw + 12 * l;
+        // ---- token mixing (:289-297), as gm_embed_kernel: column statistics of X * ew over the row's
+        // tokens, then per 16-channel tile W1 (HT x N) against the normalised column and W2 (N x HT)
+        // against H on MFMA (H's K order permuted so it stays in the registers the first MFMA left it in)
+        {
+            const Ids I;
+            for (int c = I.tt * 64 + I.lane; c < C; c += 64 * NTT) {
+                float sm = 0.f;
+                for (int t = 0; t < N; ++t) sm += I.Xr[t * XS + c] * I.sew[t];
+                const float mean = sm / (float)N;
+                float q = 0.f;
+                for (int t = 0; t < N; ++t) {
+                    const float d = I.Xr[t * XS + c] * I.sew[t] - mean;
+                    q += d * d;
+                }
+                I.colm[c] = mean;
+                I.colr[c] = 1.f / sqrtf(q / (float)N + 1e-5f);
+            }
+        }
+        __syncthreads();
+        {
+            const Ids I;
+            const int g = I.j, li = I.m, HT = a.HT;
+            const float *tw0 = gf_uniform(w[0]), *tw1 = gf_uniform(w[1]), *tw2 = gf_uniform(w[2]),
+                        *tw3 = gf_uniform(w[3]), *tw4 = gf_uniform(w[4]), *tw5 = gf_uniform(w[5]);
+            float a1[NTT][4], a2[NTT][4], lg[NTT][4], lb[NTT][4], b2v[NTT][4], b1v[4];
+#pragma unroll
+            for (int G = 0; G < NTT; ++G)
+#pragma unroll
+                for (int s2 = 0; s2 < 4; ++s2) {
+                    const int t = 16 * G + 4 * s2 + g;
+                    a1[G][s2] = (li < HT && t < N) ? tw2[li * N + t] : 0.f;
+                    lg[G][s2] = t < N ? tw0[t] : 0.f;
+                    lb[G][s2] = t < N ? tw1[t] : 0.f;
+                    const int tt2 = 16 * G + li, jj = 4 * g + s2;
+                    a2[G][s2] = (tt2 < N && jj < HT) ? tw4[tt2 * HT + jj] : 0.f;
+                    const int tr = 16 * G + 4 * g + s2;
+                    b2v[G][s2] = tr < N ? tw5[tr] : 0.f;
+                }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) b1v[i] = 4 * g + i < HT ? tw3[4 * g + i] : 0.f;
+            for (int nt = I.tt; nt < NC; nt += NTT) {
+                const int c = 16 * nt + li;
+                const bool cv = c < C;
+                const float mean = cv ? I.colm[c] : 0.f, rstd = cv ? I.colr[c] : 0.f;
+                gmx4 hacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int G = 0; G < NTT; ++G)
+#pragma unroll
+                    for (int s2 = 0; s2 < 4; ++s2) {
+                        const int t = 16 * G + 4 * s2 + g;
+                        const float xn = (cv && t < N) ? (I.Xr[t * XS + c] * I.sew[t] - mean) * rstd * lg[G][s2] + lb[G][s2] : 0.f;
+                        hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[G][s2], xn, hacc, 0, 0, 0);
+                    }
+                float h[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) h[i] = 4 * g + i < HT ? gm_gelu(hacc[i] + b1v[i]) : 0.f;
+#pragma unroll
+                for (int mt = 0; mt < NTT; ++mt) {
+                    gmx4 yy = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int s2 = 0; s2 < 4; ++s2) yy = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[mt][s2], h[s2], yy, 0, 0, 0);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int t = 16 * mt + 4 * g + i;
+                        if (cv && t < N) {
+                            const int ix = t * XS + c;
+                            I.Xr[ix] = (yy[i] + b2v[mt][i]) * I.sew[t] + I.Xr[ix] * I.sew[t];
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // ---- channel mixing (:300-305): the wave's token tile from the image; channel LayerNorm per
+        // token (column) in registers, then the FFN with the hidden features in registers
+        {
+            const Ids I;
+            const int m = I.m, j = I.j, vo = I.lane * 16;
+            gmx4 xn[NC], y[NC];
+            {
+                float4 xv[NC];
+                float s = 0.f;
+#pragma unroll
+                for (int q = 0; q < NC; ++q) {
+                    xv[q] = *reinterpret_cast<const float4 *>(I.Xw + m * XS + 16 * q + 4 * j);
+                    s += (xv[q].x + xv[q].y) + (xv[q].z + xv[q].w);
+                }
+                s += __shfl_xor(s, 16);
+                s += __shfl_xor(s, 32);
+                const float mean = s / (float)C;
+                float v = 0.f;
+#pragma unroll
+                for (int q = 0; q < NC; ++q) {
+                    const bool in = 16 * q + 4 * j < C;
+                    const float d0 = xv[q].x - mean, d1 = xv[q].y - mean, d2 = xv[q].z - mean, d3 = xv[q].w - mean;
+                    v += in ? (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3) : 0.f;
+                }
+                v += __shfl_xor(v, 16);
+                v += __shfl_xor(v, 32);
+                const float rstd = 1.f / sqrtf(v / (float)C + 1e-5f);
+                const auto rw = gf_vrsrc(gf_uniform(w[6]), C), rb = gf_vrsrc(gf_uniform(w[7]), C);
+#pragma unroll
+                for (int q = 0; q < NC; ++q) {
+                    const float4 lw = gf_vload(rw, 64 * q + 16 * j), lbv = gf_vload(rb, 64 * q + 16 * j);
+                    xn[q] = gmx4{(xv[q].x - mean) * rstd * lw.x + lbv.x, (xv[q].y - mean) * rstd * lw.y + lbv.y,
+                                 (xv[q].z - mean) * rstd * lw.z + lbv.z, (xv[q].w - mean) * rstd * lw.w + lbv.w};
+                }
+            }
+            {
+                const auto rb = gf_vrsrc(gf_uniform(w[11]), C);
+#pragma unroll
+                for (int o = 0; o < NC; ++o) {
+                    const float4 b = gf_vload(rb, 64 * o + 16 * j);
+                    y[o] = gmx4{b.x, b.y, b.z, b.w};
+                }
+            }
+            const auto r1 = gf_rsrc(gf_uniform(w[8])), r2 = gf_rsrc(gf_uniform(w[10]));
+            const auto rb1 = gf_vrsrc(gf_uniform(w[9]), a.HC);
+            const int NP = NH2 / 2;
+            // pair p's fragment f (compile-time) at the pair's base offset (opaque per pair, as in the
+            // projection) + a constant.  f < 2 NC: W1 tile 2p + (f & 1), K tile f >> 1 (pack [HC tiles][NC]);
+            // else g = f - 2 NC: W2 tile g >> 1, K tile 2p + (g & 1) (pack [NC][NH2])
+            auto issue = [&](int f, int pb1, int pb2) -> float4 {
+                if (f < 2 * NC) return gf_frag(r1, vo, pb1 + (((f & 1) * NC + (f >> 1)) * 64) * 16);
+                const int g = f - 2 * NC;
+                return gf_frag(r2, vo, pb2 + (((g >> 1) * NH2 + (g & 1)) * 64) * 16);
+            };
+            constexpr int F = 4 * NC;
+            float4 ring[GF_PF];
+#pragma unroll
+            for (int i = 0; i < GF_PF; ++i) ring[i] = issue(i, 0, 0);
+            for (int p = 0; p < NP; ++p) {
+                int pb1 = p * 2 * NC * 1024, pb2 = p * 2 * 1024;
+                int nb1 = min(p + 1, NP - 1) * 2 * NC * 1024, nb2 = min(p + 1, NP - 1) * 2 * 1024;
+                asm volatile("" : "+s"(pb1), "+s"(pb2), "+s"(nb1), "+s"(nb2));
+                const float4 c0 = gf_vload(rb1, 128 * p + 16 * j), c1 = gf_vload(rb1, 128 * p + 64 + 16 * j);
+                gmx4 h0 = {c0.x, c0.y, c0.z, c0.w}, h1 = {c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+                for (int q = 0; q < NC; ++q) {
+                    const int f = 2 * q;
+                    const float4 w0 = ring[f % GF_PF];
+                    ring[f % GF_PF] = f + GF_PF < F ? issue(f + GF_PF, pb1, pb2) : issue(f + GF_PF - F, nb1, nb2);
+                    const float4 w1 = ring[(f + 1) % GF_PF];
+                    ring[(f + 1) % GF_PF] = f + 1 + GF_PF < F ? issue(f + 1 + GF_PF, pb1, pb2) : issue(f + 1 + GF_PF - F, nb1, nb2);
+                    h0 = __builtin_amdgcn_mfma_f32_16x16x4f32(w0.x, xn[q][0], h0, 0, 0, 0);
+                    h1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.x, xn[q][0], h1, 0, 0, 0);
+                    h0 = __builtin_amdgcn_mfma_f32_16x16x4f32(w0.y, xn[q][1], h0, 0, 0, 0);
+                    h1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.y, xn[q][1], h1, 0, 0, 0);
+                    h0 = __builtin_amdgcn_mfma_f32_16x16x4f32(w0.z, xn[q][2], h0, 0, 0, 0);
+                    h1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.z, xn[q][2], h1, 0, 0, 0);
+                    h0 = __builtin_amdgcn_mfma_f32_16x16x4f32(w0.w, xn[q][3], h0, 0, 0, 0);
+                    h1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.w, xn[q][3], h1, 0, 0, 0);
+                }
+                // GELU (:303); padding hidden units have zero weights and bias, gelu(0) = 0
+                const float4 g0 = make_float4(gm_gelu(h0[0]), gm_gelu(h0[1]), gm_gelu(h0[2]), gm_gelu(h0[3]));
+                const float4 g1 = make_float4(gm_gelu(h1[0]), gm_gelu(h1[1]), gm_gelu(h1[2]), gm_gelu(h1[3]));
+#pragma unroll
+                for (int o = 0; o < NC; ++o) {
+                    const int f = 2 * NC + 2 * o;
+                    const float4 w0 = ring[f % GF_PF];
+                    ring[f % GF_PF] = f + GF_PF < F ? issue(f + GF_PF, pb1, pb2) : issue(f + GF_PF - F, nb1, nb2);
+                    const float4 w1 = ring[(f + 1) % GF_PF];
+                    ring[(f + 1) % GF_PF] = f + 1 + GF_PF < F ? issue(f + 1 + GF_PF, pb1, pb2) : issue(f + 1 + GF_PF - F, nb1, nb2);
+                    y[o] = gf_mfma4(w0, g0, y[o]);
+                    y[o] = gf_mfma4(w1, g1, y[o]);
+                }
+            }
+            // X = (Y + b2) * ew + X (:305, the explanation weight on the branch output)
+            const float e = I.sew[min(I.tok, 31)];
+#pragma unroll
+            for (int o = 0; o < NC; ++o) {
+                float *px = I.Xw + m * XS + 16 * o + 4 * j;
+                const float4 xo = *reinterpret_cast<const float4 *>(px);
+                const bool in = I.tok < N && 16 * o + 4 * j < C;
+                *reinterpret_cast<float4 *>(px) =
+                    in ? make_float4(y[o][0] * e + xo.x, y[o][1] * e + xo.y, y[o][2] * e + xo.z, y[o][3] * e + xo.w)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+        __syncthreads();
+    }
+    // ---- masked mean over the tokens (:176-178) and the neighbour-feature mean (:181-189), the row's
+    // NTT waves over channels / node features
+    const Ids I;
+    const int r = blockIdx.x * RPW + I.rl;
+    if (r < R) {
+        const int D = a.D;
+        for (int c = I.tt * 64 + I.lane; c < C; c += 64 * NTT) {
+            float s = 0.f;
+            for (int t = 0; t < N; ++t) s += I.Xr[t * XS + c] * I.sval[t] * (has_ew ? I.sew[t] : 1.f);
+            a.x_mean[(size_t)r * C + c] = s / (float)N;
+        }
+        float nvalid = 0.f;
+        for (int t = 0; t < N; ++t) nvalid += I.sval[t];
+        for (int d = I.tt * 64 + I.lane; d < D; d += 64 * NTT) {
+            float s = 0.f;
+            for (int t = 0; t < N; ++t) {
+                float sc = nvalid > 0.f ? I.sval[t] / nvalid : 1.f / (float)N;
+                if (has_ew) sc *= I.sew[t];
+                s += a.n_feat[(size_t)a.nid[(size_t)r * N + t] * D + d] * sc;
+            }
+            a.node_out[(size_t)r * D + d] = s / (float)N + a.n_feat[(size_t)a.node[r] * D + d];
+        }
+    }
+}
+
 }  // namespace tmk
 
 using namespace tmk;
@@ -429,6 +838,36 @@ extern "C" int tm_gm_pack(const float *w, int32_t n_out, int32_t k, float *packe
     return TM_OK;
 }
 
+static inline int64_t gm_pack_a_tiles(int32_t n, int32_t mult) { return (int64_t)((gm_r16(n) / 16 + mult - 1) / mult) * mult; }
+
+extern "C" int64_t tm_gm_packed_a_floats(int32_t n_out, int32_t k, int32_t n_mult, int32_t k_mult) {
+    if (n_out <= 0 || k <= 0 || n_mult <= 0 || k_mult <= 0) return 0;
+    return gm_pack_a_tiles(n_out, n_mult) * gm_pack_a_tiles(k, k_mult) * 256;
+}
+
+extern "C" int tm_gm_pack_a(const float *w, int32_t n_out, int32_t k, int32_t n_mult, int32_t k_mult, float *packed,
+                            void *stream) {
+    if (!w || !packed || n_out <= 0 || k <= 0 || n_mult <= 0 || k_mult <= 0) return fail(TM_E_ARG, "tm_gm_pack_a: bad arguments");
+    const int64_t total = tm_gm_packed_a_floats(n_out, k, n_mult, k_mult);
+    const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, 4096);
+    gm_pack_a_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(w, n_out, k, (int32_t)gm_pack_a_tiles(k, k_mult), total, packed);
+    TM_CHECK_LAUNCH();
+    return TM_OK;
+}
+
+static inline size_t gm_fused_lds_bytes(int32_t C, int32_t N) {
+    const size_t NC = gm_r16(C) / 16, XS = 16 * NC + 4, RPW = N > 16 ? 2 : 4;
+    return sizeof(float) * (64 * XS + RPW * (2 * 16 * NC + 64));
+}
+
+// the register-resident kernel's instances: channel tiles NC = C / 16 rounded up
+#define GM_FUSED_NC(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
+
+extern "C" int tm_gm_fused_ok(int32_t N, int32_t C, int32_t T, int32_t HC) {
+    return N > 0 && N <= GM_MT && C >= 4 && C <= 256 && C % 4 == 0 && T >= 4 && T % 4 == 0 && HC >= 4 && HC % 4 == 0 &&
+           gm_fused_lds_bytes(C, N) <= 80 * 1024;
+}
+
 extern "C" int tm_gm_embed(const tm_gm_embed_args *p, void *stream) {
     if (!p) return fail(TM_E_ARG, "tm_gm_embed: NULL arguments");
     const tm_gm_embed_args &q = *p;
@@ -451,6 +890,27 @@ extern "C" int tm_gm_embed(const tm_gm_embed_args *p, void *stream) {
     a.lw = q.layer_table;
     a.x_mean = q.x_mean;
     a.node_out = q.node_out;
+    if (tm_gm_fused_ok(q.N, q.C, q.T, q.HC)) {
+        // packs by tm_gm_pack_a: proj_w (1, 4), channel ffn.0 (2, 1), ffn.3 (1, 2)
+        const size_t lds = gm_fused_lds_bytes(q.C, q.N);
+        const int nc = gm_r16(q.C) / 16, rpw = q.N > 16 ? 2 : 4;
+        const unsigned grid = (unsigned)((q.R + rpw - 1) / rpw);
+        hipEvent_t pe = prof_begin((hipStream_t)stream);
+        auto launch = [&](auto kern) -> int {
+            TM_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            kern<<<grid, 256, lds, (hipStream_t)stream>>>(a);
+            return TM_OK;
+        };
+        int rc = TM_E_UNSUPPORTED;
+#define GM_CASE(X)                                                                                  \
+        if (nc == X) rc = q.N > 16 ? launch(gm_fused_kernel<X, 2>) : launch(gm_fused_kernel<X, 1>);
+        GM_FUSED_NC(GM_CASE)
+#undef GM_CASE
+        if (rc != TM_OK) return rc == TM_E_UNSUPPORTED ? fail(rc, "tm_gm_embed: no kernel instance") : rc;
+        TM_CHECK_LAUNCH();
+        prof_end("gm_fused_kernel", (hipStream_t)stream, pe);
+        return TM_OK;
+    }
     const size_t lds = gm_lds_bytes(q.C, q.T);
     if (lds > 160 * 1024) return fail(TM_E_UNSUPPORTED, "tm_gm_embed: edge + time dims too large for LDS");
     hipEvent_t pe = prof_begin((hipStream_t)stream);

@@ -160,11 +160,21 @@ class GraphMixer(nn.Module):
             st = L.stream_ptr(dev)
             keep = []
 
-            def pack(w):
+            N, C = self.num_tokens, self.num_channels
+            fused = bool(L.lib().tm_gm_fused_ok(N, C, self.time_feat_dim, int(self.channel_dim_expansion_factor * C)))
+
+            def pack(w, mult=(1, 1)):
+                # the register-resident kernel takes A-operand fragments (tm_gm_pack_a), the LDS-tiled one
+                # B-operand fragments (tm_gm_pack); tm_gm_embed picks the kernel by the same tm_gm_fused_ok
                 w = w.detach().to(dev, torch.float32).contiguous()
                 n_out, k = w.shape
-                out = torch.empty(int(L.lib().tm_gm_packed_floats(n_out, k)), dtype=torch.float32, device=dev)
-                L.check(L.lib().tm_gm_pack(L.ptr(w), n_out, k, L.ptr(out), st), "tm_gm_pack")
+                if fused:
+                    out = torch.empty(int(L.lib().tm_gm_packed_a_floats(n_out, k, *mult)), dtype=torch.float32,
+                                      device=dev)
+                    L.check(L.lib().tm_gm_pack_a(L.ptr(w), n_out, k, mult[0], mult[1], L.ptr(out), st), "tm_gm_pack_a")
+                else:
+                    out = torch.empty(int(L.lib().tm_gm_packed_floats(n_out, k)), dtype=torch.float32, device=dev)
+                    L.check(L.lib().tm_gm_pack(L.ptr(w), n_out, k, L.ptr(out), st), "tm_gm_pack")
                 keep.append(w)
                 return out
 
@@ -178,10 +188,11 @@ class GraphMixer(nn.Module):
                 tf, cf = m.token_feedforward.ffn, m.channel_feedforward.ffn
                 layers.append([flat(m.token_norm.weight), flat(m.token_norm.bias), flat(tf[0].weight), flat(tf[0].bias),
                                flat(tf[3].weight), flat(tf[3].bias), flat(m.channel_norm.weight),
-                               flat(m.channel_norm.bias), pack(cf[0].weight), flat(cf[0].bias), pack(cf[3].weight),
+                               flat(m.channel_norm.bias), pack(cf[0].weight, (2, 1)), flat(cf[0].bias),
+                               pack(cf[3].weight, (1, 2)),
                                flat(cf[3].bias)])
             table = torch.tensor([[t.data_ptr() for t in lw] for lw in layers] or [[0] * 12], dtype=torch.int64)
-            self._gm_pack = dict(proj_w=pack(self.projection_layer.weight), proj_b=flat(self.projection_layer.bias),
+            self._gm_pack = dict(proj_w=pack(self.projection_layer.weight, (1, 4)), proj_b=flat(self.projection_layer.bias),
                                  tw=flat(self.time_encoder.w.weight.reshape(-1)), tb=flat(self.time_encoder.w.bias),
                                  layers=layers, table=table.to(dev), keep=keep)
             self._gm_key = key
