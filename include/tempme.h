@@ -44,6 +44,7 @@ extern "C" {
 
 typedef struct tm_graph tm_graph;     /* opaque, immutable after build; device-resident */
 typedef struct tm_weights tm_weights; /* opaque, packed encoder weights on one device */
+typedef struct tm_dropin tm_dropin;   /* opaque, drop-in eval context: side streams, staging ring, workspaces */
 
 typedef struct {
     uint64_t seed;
@@ -305,6 +306,43 @@ int tm_edge_importance(const tm_weights *w, const float *e_feat, int32_t n_group
                        const int32_t *eid3, const float *ts3, const float *imp, const int32_t *sub1_node,
                        const int32_t *sub1_eid, const int32_t *sub2_node, const int32_t *sub2_eid, float *out_h1,
                        float *out_h2, void *stream);
+
+/* Drop-in eval context for the reference's per-side TempME.forward calls (temp_exp_main.py:446-453):
+ * three side streams, a device ring for the cut times (host values sent as kernel arguments),
+ * per-stream encoder workspaces. */
+int tm_dropin_create(int32_t device, tm_dropin **out);
+void tm_dropin_free(tm_dropin *d);
+/* Use the caller's stream as side stream k (0..2) -- e.g. a torch stream, so that the caller's allocator
+ * can hand out a call's outputs from that stream's pool -- instead of the context's own. */
+int tm_dropin_set_stream(tm_dropin *d, int32_t k, void *stream);
+/* TempME.forward (explainer_new.py:174-201) for one call (B events x W walks) in one library call on side
+ * stream k: with sync != 0 every side stream first waits (once) for `stream` (weights / tables prepared
+ * there, or a device cut tensor); the cut times come from the host (cut_host, sent as kernel arguments;
+ * an array equal to the previous call's is not sent again) or the device (cut_dev); std + encoder run
+ * there (tm_encoder_fwd_tab, M = 1, etab as there), and with out_gfac non-NULL the dependency-gate
+ * factor 0.5 + 0.5 * gate of every walk position [B, W, 3] (explainer_new.py:367-386) follows; `stream`
+ * then waits for the side stream.  out_imp [B*W] and out_gfac must be allocated on side stream k (or be
+ * otherwise free of pending work on other streams). */
+int tm_dropin_forward(tm_dropin *d, int32_t k, int32_t sync, const tm_weights *w, const float *n_feat,
+                      const float *e_feat, const float *etab, int32_t B, int32_t W, const int32_t *node6,
+                      const int32_t *eid3, const float *ts3, const int32_t *cat, const double *cut_host,
+                      const double *cut_dev, const float *cnt, float *out_imp, float *out_gfac, void *stream);
+/* tm_edge_importance from the gate factors of tm_dropin_forward (walk_imp = imp * gfac, the same
+ * roundings as tm_edge_importance): bit-identical outputs. */
+int tm_edge_importance_gf(const float *gfac, int32_t n_groups, int32_t B, int32_t W, int32_t N, const int32_t *eid3,
+                          const float *imp, const int32_t *sub1_node, const int32_t *sub1_eid,
+                          const int32_t *sub2_node, const int32_t *sub2_eid, float *out_h1, float *out_h2,
+                          void *stream);
+
+/* tm_edge_importance_gf for the three sides of one batch in one launch (retrieve_explanation,
+ * explainer_new.py:408-418): side s's gate factors / walk edge ids / graphlet importance / subgraph
+ * records at their own addresses (B events each), outputs concatenated: out_h1 [3B, N], out_h2 [3B, N^2]. */
+int tm_edge_importance_gf3(int32_t B, int32_t W, int32_t N, const float *gf0, const float *gf1, const float *gf2,
+                           const int32_t *e0, const int32_t *e1, const int32_t *e2, const float *i0, const float *i1,
+                           const float *i2, const int32_t *n10, const int32_t *n11, const int32_t *n12,
+                           const int32_t *x10, const int32_t *x11, const int32_t *x12, const int32_t *n20,
+                           const int32_t *n21, const int32_t *n22, const int32_t *x20, const int32_t *x21,
+                           const int32_t *x22, float *out_h1, float *out_h2, void *stream);
 
 /* Dependency-gate table (explainer_new.py:367-386 evaluated once per edge id): out_gf[e] =
  * 0.5 + 0.5*sigmoid(depMLP([e_feat[e] | cos(t_e * basis_freq + phase)])) for e in [0, max_eid],

@@ -16,6 +16,7 @@
 //                   gather at subgraph edge ids, Beta mean, node==0 mask
 // Every dense projection runs on MFMA with the packed weight stream read from L2 and the
 // activations staged in LDS (row stride K16+8 floats: conflict-free ds_read_b128).
+#include <cstring>
 #include <vector>
 
 #include "encoder_common.h"
@@ -308,7 +309,7 @@ __global__ void __launch_bounds__(256) gate_pos_kernel(EncW P, int64_t n_rows, i
     if (!P.dep) {                          // no dependency gate (tm_weights_variant): walk_imp = graphlet_imp
         if (tid < TILE_ROWS && c0 + tid < n_rows) {
             const int64_t r = c0 + tid;
-            wv[r] = imp[(r / W3) * W + (r % W3) / 3];
+            wv[r] = imp ? imp[(r / W3) * W + (r % W3) / 3] : 1.f;
         }
         return;
     }
@@ -343,26 +344,27 @@ __global__ void __launch_bounds__(256) gate_pos_kernel(EncW P, int64_t n_rows, i
     const int64_t gr = c0 + r;
     if (sub == 0 && gr < n_rows) {
         const float gate = 1.f / (1.f + expf(-(sc + P.d3b[0])));
-        wv[gr] = imp[(gr / W3) * W + (gr % W3) / 3] * (0.5f + 0.5f * gate);
+        // imp == nullptr: the gate factor alone (tm_dropin_forward), multiplied by graphlet_imp later in
+        // explain_hash_kernel -- the same two roundings in the same order
+        const float fac = 0.5f + 0.5f * gate;
+        wv[gr] = imp ? imp[(gr / W3) * W + (gr % W3) / 3] * fac : fac;
     }
 }
 
 // One workgroup per (group, event): scatter-max of the 3 W walk_imp values onto their edge ids (LDS
 // open-addressing table; atomicMax on the float bits, values >= 0), then the gather at the subgraph's
 // hop-1 / hop-2 edge ids, the Beta mean (eval) and the padding mask (:388-406, :420-430).
-__global__ void __launch_bounds__(256) explain_hash_kernel(int32_t W, int32_t N, int32_t hbits,
-                                                           const int32_t *__restrict__ eid3,
-                                                           const float *__restrict__ wv,
-                                                           const int32_t *__restrict__ sub1_node,
-                                                           const int32_t *__restrict__ sub1_eid,
-                                                           const int32_t *__restrict__ sub2_node,
-                                                           const int32_t *__restrict__ sub2_eid,
-                                                           float *__restrict__ out1, float *__restrict__ out2) {
+__device__ __forceinline__ void explain_hash_row(int64_t ge, int32_t W, int32_t N, int32_t hbits,
+                                                 const int32_t *__restrict__ eid3, const float *__restrict__ wv,
+                                                 const float *__restrict__ imp, const int32_t *__restrict__ sub1_node,
+                                                 const int32_t *__restrict__ sub1_eid,
+                                                 const int32_t *__restrict__ sub2_node,
+                                                 const int32_t *__restrict__ sub2_eid, float *__restrict__ out1,
+                                                 float *__restrict__ out2) {
     extern __shared__ __attribute__((aligned(16))) int32_t hsm[];
     const int hsize = 1 << hbits;
     int32_t *hkey = hsm;
     uint32_t *hval = reinterpret_cast<uint32_t *>(hkey + hsize);
-    const int64_t ge = blockIdx.x;
     const int tid = threadIdx.x, nrow = 3 * W;
     for (int i = tid; i < hsize; i += blockDim.x) {
         hkey[i] = -1;
@@ -371,7 +373,8 @@ __global__ void __launch_bounds__(256) explain_hash_kernel(int32_t W, int32_t N,
     __syncthreads();
     for (int i = tid; i < nrow; i += blockDim.x) {
         const int32_t key = eid3[ge * nrow + i];
-        const float v = wv[ge * nrow + i];
+        // wv = walk_imp, or (imp != nullptr) the gate factor of tm_dropin_forward times graphlet_imp
+        const float v = imp ? imp[ge * W + i / 3] * wv[ge * nrow + i] : wv[ge * nrow + i];
         uint32_t h = hash_eid(key) >> (32 - hbits);
         while (true) {
             const int32_t prev = atomicCAS(&hkey[h], -1, key);
@@ -404,6 +407,35 @@ __global__ void __launch_bounds__(256) explain_hash_kernel(int32_t W, int32_t N,
         if (h1) out1[o] = v;
         else out2[o] = v;
     }
+}
+
+__global__ void __launch_bounds__(256) explain_hash_kernel(int32_t W, int32_t N, int32_t hbits,
+                                                           const int32_t *__restrict__ eid3,
+                                                           const float *__restrict__ wv,
+                                                           const float *__restrict__ imp,
+                                                           const int32_t *__restrict__ sub1_node,
+                                                           const int32_t *__restrict__ sub1_eid,
+                                                           const int32_t *__restrict__ sub2_node,
+                                                           const int32_t *__restrict__ sub2_eid,
+                                                           float *__restrict__ out1, float *__restrict__ out2) {
+    explain_hash_row(blockIdx.x, W, N, hbits, eid3, wv, imp, sub1_node, sub1_eid, sub2_node, sub2_eid, out1, out2);
+}
+
+// the three sides of one reference batch in one launch (retrieve_explanation), each side's inputs at
+// their own addresses (device-pack views), the outputs concatenated [3 B, N] / [3 B, N^2]
+struct ExplainSides {
+    const float *gf[3], *imp[3];
+    const int32_t *eid3[3], *s1n[3], *s1e[3], *s2n[3], *s2e[3];
+};
+
+__global__ void __launch_bounds__(256) explain_hash3_kernel(ExplainSides a, int32_t B, int32_t W, int32_t N,
+                                                            int32_t hbits, float *__restrict__ out1,
+                                                            float *__restrict__ out2) {
+    const int s = blockIdx.x / B;
+    // per-side pointers shifted so that row index (s B + b) addresses row b of side s
+    const int64_t sh = (int64_t)s * B;
+    explain_hash_row(blockIdx.x, W, N, hbits, a.eid3[s] - sh * 3 * W, a.gf[s] - sh * 3 * W, a.imp[s] - sh * W,
+                     a.s1n[s] - sh * N, a.s1e[s] - sh * N, a.s2n[s] - sh * N * N, a.s2e[s] - sh * N * N, out1, out2);
 }
 
 // ------------------------------------------------------------------ fused register-resident walk encoder
@@ -1707,10 +1739,246 @@ extern "C" int tm_edge_importance(const tm_weights *w, const float *e_feat, int3
     gate_pos_kernel<<<dim3((unsigned)((n_pos + TILE_ROWS - 1) / TILE_ROWS)), 256, lds, S_(stream)>>>(P, n_pos, W, e_feat,
                                                                                                    eid3, ts3, imp, wv);
     TM_CHECK_LAUNCH();
-    explain_hash_kernel<<<dim3((unsigned)rows), 256, hlds, S_(stream)>>>(W, N, hbits, eid3, wv, sub1_node, sub1_eid,
-                                                                        sub2_node, sub2_eid, out_h1, out_h2);
+    explain_hash_kernel<<<dim3((unsigned)rows), 256, hlds, S_(stream)>>>(W, N, hbits, eid3, wv, nullptr, sub1_node,
+                                                                        sub1_eid, sub2_node, sub2_eid, out_h1, out_h2);
     TM_CHECK_LAUNCH();
     prof_end("explain_kernel", S_(stream), pe);
+    return TM_OK;
+}
+
+// ------------------------------------------------------------------ drop-in eval context
+// The reference's eval loop calls TempME.forward once per side, then retrieve_explanation
+// (temp_exp_main.py:446-453).  tm_dropin_forward is one such forward in ONE library call: the side
+// stream (three, round robin) is ordered after the caller's stream, the cut times are staged through a
+// device ring (sent as kernel arguments) (a repeated cut array -- the same ts_l_cut for the three sides -- is sent once), std +
+// encoder run on the side stream from a per-stream workspace, the dependency-gate factor of every walk
+// position (the part of retrieve_edge_imp_node that does not depend on graphlet_imp) follows on the
+// same stream, and the caller's stream waits for it.  tm_edge_importance_gf then finishes
+// retrieve_edge_imp_node from those factors.
+// up to 256 cut times as a kernel argument: the host values travel with the launch (asynchronous, no
+// host buffer to keep alive -- a small hipMemcpyAsync from host memory can block until the stream drains)
+struct CutChunk {
+    double v[256];
+};
+
+__global__ void put_cut_kernel(double *__restrict__ dst, int32_t n, CutChunk c) {
+    if ((int)threadIdx.x < n) dst[threadIdx.x] = c.v[threadIdx.x];
+}
+
+struct tm_dropin {
+    static constexpr int SIDES = 3, SLOTS = 64, SLOT_DOUBLES = 512;
+    int device = 0;
+    hipStream_t side[SIDES] = {};
+    hipEvent_t ev_cur = nullptr, ev_side[SIDES] = {};
+    bool prep_pending[SIDES] = {}, own[SIDES] = {};
+    double *hcopy = nullptr, *dring = nullptr;   // host copies of the slots (memo) | device ring
+    hipEvent_t copy_ev[SLOTS] = {}, read_ev[SLOTS][SIDES] = {};
+    bool read_used[SLOTS][SIDES] = {};
+    int slot_next = 0, last_slot = -1, last_n = 0, last_side = -1;
+    void *ws[SIDES] = {};
+    size_t ws_bytes[SIDES] = {};
+};
+
+extern "C" void tm_dropin_free(tm_dropin *d) {
+    if (!d) return;
+    int prev = 0;
+    hipGetDevice(&prev);
+    hipSetDevice(d->device);
+    for (int k = 0; k < tm_dropin::SIDES; ++k)
+        if (d->side[k]) hipStreamSynchronize(d->side[k]);
+    for (int k = 0; k < tm_dropin::SIDES; ++k) {
+        if (d->ws[k]) hipFree(d->ws[k]);
+        if (d->ev_side[k]) hipEventDestroy(d->ev_side[k]);
+        if (d->side[k] && d->own[k]) hipStreamDestroy(d->side[k]);
+    }
+    for (int i = 0; i < tm_dropin::SLOTS; ++i) {
+        if (d->copy_ev[i]) hipEventDestroy(d->copy_ev[i]);
+        for (int k = 0; k < tm_dropin::SIDES; ++k)
+            if (d->read_ev[i][k]) hipEventDestroy(d->read_ev[i][k]);
+    }
+    if (d->ev_cur) hipEventDestroy(d->ev_cur);
+    free(d->hcopy);
+    if (d->dring) hipFree(d->dring);
+    hipSetDevice(prev);
+    delete d;
+}
+
+extern "C" int tm_dropin_create(int32_t device, tm_dropin **out) {
+    if (!out) return fail(TM_E_ARG, "tm_dropin_create: NULL out");
+    *out = nullptr;
+    int prev = 0;
+    TM_HIP(hipGetDevice(&prev));
+    TM_HIP(hipSetDevice(device));
+    tm_dropin *d = new tm_dropin();
+    d->device = device;
+    bool ok = hipEventCreateWithFlags(&d->ev_cur, hipEventDisableTiming) == hipSuccess;
+    for (int k = 0; ok && k < tm_dropin::SIDES; ++k)
+        ok = (d->own[k] = hipStreamCreateWithFlags(&d->side[k], hipStreamNonBlocking) == hipSuccess) &&
+             hipEventCreateWithFlags(&d->ev_side[k], hipEventDisableTiming) == hipSuccess;
+    for (int i = 0; ok && i < tm_dropin::SLOTS; ++i) {
+        ok = hipEventCreateWithFlags(&d->copy_ev[i], hipEventDisableTiming) == hipSuccess;
+        for (int k = 0; ok && k < tm_dropin::SIDES; ++k)
+            ok = hipEventCreateWithFlags(&d->read_ev[i][k], hipEventDisableTiming) == hipSuccess;
+    }
+    const size_t ring = sizeof(double) * tm_dropin::SLOTS * tm_dropin::SLOT_DOUBLES;
+    d->hcopy = static_cast<double *>(malloc(ring));
+    ok = ok && d->hcopy && hipMalloc(reinterpret_cast<void **>(&d->dring), ring) == hipSuccess;
+    hipSetDevice(prev);
+    if (!ok) {
+        tm_dropin_free(d);
+        return fail(TM_E_HIP, "tm_dropin_create: stream / event / buffer allocation failed");
+    }
+    *out = d;
+    return TM_OK;
+}
+
+// side stream k from the caller (e.g. torch streams, so the caller's allocator can serve them); the
+// context's own stream k is destroyed once idle
+extern "C" int tm_dropin_set_stream(tm_dropin *d, int32_t k, void *stream) {
+    if (!d || k < 0 || k >= tm_dropin::SIDES || !stream) return fail(TM_E_ARG, "tm_dropin_set_stream: bad arguments");
+    if (d->own[k]) {
+        TM_HIP(hipStreamSynchronize(d->side[k]));
+        TM_HIP(hipStreamDestroy(d->side[k]));
+        d->own[k] = false;
+    }
+    d->side[k] = S_(stream);
+    d->prep_pending[k] = true;
+    return TM_OK;
+}
+
+extern "C" int tm_dropin_forward(tm_dropin *d, int32_t k, int32_t sync, const tm_weights *w, const float *n_feat,
+                                 const float *e_feat, const float *etab, int32_t B, int32_t W, const int32_t *node6,
+                                 const int32_t *eid3, const float *ts3, const int32_t *cat, const double *cut_host,
+                                 const double *cut_dev, const float *cnt, float *out_imp, float *out_gfac,
+                                 void *stream) {
+    if (!d || !w || B < 0 || W <= 0 || k < 0 || k >= tm_dropin::SIDES)
+        return fail(TM_E_ARG, "tm_dropin_forward: bad arguments");
+    if (B == 0) return TM_OK;
+    if (!cut_host == !cut_dev) return fail(TM_E_ARG, "tm_dropin_forward: exactly one of cut_host / cut_dev");
+    if (cut_host && B > tm_dropin::SLOT_DOUBLES) return fail(TM_E_UNSUPPORTED, "tm_dropin_forward: batch too large");
+    hipStream_t cur = S_(stream);
+    hipStream_t side = d->side[k];
+    // sync: work on the caller's stream this call depends on (weights / tables repacked there, a device
+    // cut tensor) -- every side stream waits for the caller's stream once, at its next use.  Otherwise
+    // the side stream is not ordered after the caller's: it reads resident pack data and writes buffers
+    // the caller allocated on the side stream itself.
+    if (sync) {
+        TM_HIP(hipEventRecord(d->ev_cur, cur));
+        for (int j = 0; j < tm_dropin::SIDES; ++j) d->prep_pending[j] = true;
+    }
+    if (d->prep_pending[k]) {
+        TM_HIP(hipStreamWaitEvent(side, d->ev_cur, 0));
+        d->prep_pending[k] = false;
+    }
+    const double *cut = cut_dev;
+    int slot = -1;
+    if (cut_host) {
+        const size_t bytes = sizeof(double) * (size_t)B;
+        if (d->last_slot >= 0 && d->last_n == B &&
+            memcmp(d->hcopy + (size_t)d->last_slot * tm_dropin::SLOT_DOUBLES, cut_host, bytes) == 0) {
+            slot = d->last_slot;   // the previous side's cut array again: already on the device
+            if (d->last_side != k) TM_HIP(hipStreamWaitEvent(side, d->copy_ev[slot], 0));
+        } else {
+            slot = d->slot_next;
+            d->slot_next = (slot + 1) % tm_dropin::SLOTS;
+            for (int j = 0; j < tm_dropin::SIDES; ++j)   // every kernel that read this slot's last contents done
+                if (d->read_used[slot][j]) {
+                    TM_HIP(hipEventSynchronize(d->read_ev[slot][j]));
+                    d->read_used[slot][j] = false;
+                }
+            double *h = d->hcopy + (size_t)slot * tm_dropin::SLOT_DOUBLES;
+            memcpy(h, cut_host, bytes);
+            for (int32_t i0 = 0; i0 < B; i0 += 256) {
+                CutChunk c;
+                const int32_t n = std::min<int32_t>(256, B - i0);
+                memcpy(c.v, cut_host + i0, sizeof(double) * (size_t)n);
+                put_cut_kernel<<<1, 256, 0, side>>>(d->dring + (size_t)slot * tm_dropin::SLOT_DOUBLES + i0, n, c);
+                TM_CHECK_LAUNCH();
+            }
+            TM_HIP(hipEventRecord(d->copy_ev[slot], side));
+            d->last_slot = slot;
+            d->last_n = B;
+            d->last_side = k;
+        }
+        cut = d->dring + (size_t)slot * tm_dropin::SLOT_DOUBLES;
+    }
+    const int64_t n_walks = (int64_t)B * W;
+    const size_t need = (size_t)tm_encoder_workspace_bytes(w, n_walks);
+    if (d->ws_bytes[k] < need) {
+        TM_HIP(hipStreamSynchronize(side));
+        if (d->ws[k]) TM_HIP(hipFree(d->ws[k]));
+        d->ws[k] = nullptr;
+        d->ws_bytes[k] = 0;
+        TM_HIP(hipMalloc(&d->ws[k], need));
+        d->ws_bytes[k] = need;
+    }
+    int rc = tm_encoder_fwd_tab(w, n_feat, e_feat, etab, 1, B, W, 1, node6, eid3, ts3, cat, cut, cnt, d->ws[k], out_imp,
+                                side);
+    if (rc != TM_OK) return rc;
+    if (out_gfac) {
+        const EncW &P = w->P;
+        const size_t lds = gate_lds(P);
+        if (lds > 160 * 1024) return fail(TM_E_UNSUPPORTED, "tm_dropin_forward: LDS budget exceeded");
+        const int64_t n_pos = n_walks * 3;
+        hipEvent_t pe = prof_begin(side);
+        gate_pos_kernel<<<dim3((unsigned)((n_pos + TILE_ROWS - 1) / TILE_ROWS)), 256, lds, side>>>(
+            P, n_pos, W, e_feat, eid3, ts3, nullptr, out_gfac);
+        TM_CHECK_LAUNCH();
+        prof_end("gate_pos_kernel", side, pe);
+    }
+    if (slot >= 0) {
+        TM_HIP(hipEventRecord(d->read_ev[slot][k], side));
+        d->read_used[slot][k] = true;
+    }
+    TM_HIP(hipEventRecord(d->ev_side[k], side));
+    TM_HIP(hipStreamWaitEvent(cur, d->ev_side[k], 0));
+    return TM_OK;
+}
+
+extern "C" int tm_edge_importance_gf3(int32_t B, int32_t W, int32_t N, const float *gf0, const float *gf1,
+                                      const float *gf2, const int32_t *e0, const int32_t *e1, const int32_t *e2,
+                                      const float *i0, const float *i1, const float *i2, const int32_t *n10,
+                                      const int32_t *n11, const int32_t *n12, const int32_t *x10, const int32_t *x11,
+                                      const int32_t *x12, const int32_t *n20, const int32_t *n21, const int32_t *n22,
+                                      const int32_t *x20, const int32_t *x21, const int32_t *x22, float *out_h1,
+                                      float *out_h2, void *stream) {
+    if (B < 0 || W <= 0 || N <= 0) return fail(TM_E_ARG, "tm_edge_importance_gf3: bad arguments");
+    if (B == 0) return TM_OK;
+    ExplainSides a{{gf0, gf1, gf2}, {i0, i1, i2}, {e0, e1, e2}, {n10, n11, n12}, {x10, x11, x12}, {n20, n21, n22},
+                   {x20, x21, x22}};
+    for (int s = 0; s < 3; ++s)
+        if (!a.gf[s] || !a.imp[s] || !a.eid3[s] || !a.s1n[s] || !a.s1e[s] || !a.s2n[s] || !a.s2e[s])
+            return fail(TM_E_ARG, "tm_edge_importance_gf3: NULL pointer");
+    if (!out_h1 || !out_h2) return fail(TM_E_ARG, "tm_edge_importance_gf3: NULL output");
+    int hbits = 6;
+    while ((1 << hbits) < 2 * 3 * W) ++hbits;
+    if (hbits > 14) return fail(TM_E_UNSUPPORTED, "tm_edge_importance_gf3: too many walks per event");
+    const size_t hlds = 2 * sizeof(int32_t) * (1u << hbits);
+    hipEvent_t pe = prof_begin(S_(stream));
+    explain_hash3_kernel<<<dim3((unsigned)(3 * B)), 256, hlds, S_(stream)>>>(a, B, W, N, hbits, out_h1, out_h2);
+    TM_CHECK_LAUNCH();
+    prof_end("explain_hash_kernel", S_(stream), pe);
+    return TM_OK;
+}
+
+extern "C" int tm_edge_importance_gf(const float *gfac, int32_t n_groups, int32_t B, int32_t W, int32_t N,
+                                     const int32_t *eid3, const float *imp, const int32_t *sub1_node,
+                                     const int32_t *sub1_eid, const int32_t *sub2_node, const int32_t *sub2_eid,
+                                     float *out_h1, float *out_h2, void *stream) {
+    if (n_groups < 0 || B < 0 || W <= 0 || N <= 0) return fail(TM_E_ARG, "tm_edge_importance_gf: bad arguments");
+    const int64_t rows = (int64_t)n_groups * B;
+    if (rows == 0) return TM_OK;
+    if (!gfac || !eid3 || !imp || !sub1_node || !sub1_eid || !sub2_node || !sub2_eid || !out_h1 || !out_h2)
+        return fail(TM_E_ARG, "tm_edge_importance_gf: NULL pointer");
+    int hbits = 6;
+    while ((1 << hbits) < 2 * 3 * W) ++hbits;
+    if (hbits > 14) return fail(TM_E_UNSUPPORTED, "tm_edge_importance_gf: too many walks per event");
+    const size_t hlds = 2 * sizeof(int32_t) * (1u << hbits);
+    hipEvent_t pe = prof_begin(S_(stream));
+    explain_hash_kernel<<<dim3((unsigned)rows), 256, hlds, S_(stream)>>>(W, N, hbits, eid3, gfac, imp, sub1_node,
+                                                                        sub1_eid, sub2_node, sub2_eid, out_h1, out_h2);
+    TM_CHECK_LAUNCH();
+    prof_end("explain_hash_kernel", S_(stream), pe);
     return TM_OK;
 }
 

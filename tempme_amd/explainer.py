@@ -15,6 +15,7 @@ gradients) run the HIP forward/backward kernels through autograd Functions
 (tm_encoder_train_fwd / tm_encoder_bwd / tm_encoder_wgrad, tm_explain_train_fwd / _bwd,
 tm_kl_loss); only Beta ``rsample`` and the padding mask are torch ops.
 """
+import operator
 import threading
 import warnings
 
@@ -346,7 +347,7 @@ class TempME(nn.Module):
             arr = (L.C.c_void_p * L.N_WEIGHTS)(*[w.data_ptr() for w in self._raw])
             L.check(L.lib().tm_weights_pack(self._packed.h, arr, L.stream_ptr(dev)), "tm_weights_pack")
             self._packed_key = key
-            self._prep_dirty = True
+            self._prep_dirty = self._prep_dirty_fast = True   # side streams must wait for this work
         return self._packed.h
 
     def feature_tables(self):
@@ -356,7 +357,7 @@ class TempME(nn.Module):
             self._n_tab = self.node_raw_embed.weight.detach().to(device=dev, dtype=torch.float32).contiguous()
             self._e_tab = self.edge_raw_embed.weight.detach().to(device=dev, dtype=torch.float32).contiguous()
             self._tables_key = key
-            self._prep_dirty = True
+            self._prep_dirty = self._prep_dirty_fast = True   # side streams must wait for this work
         return self._n_tab, self._e_tab
 
     def dropin_edge_table(self, w=None):
@@ -378,7 +379,7 @@ class TempME(nn.Module):
             L.check(L.lib().tm_edge_feature_table(w, L.ptr(et), int(et.shape[0]), L.ptr(self._dropin_etab),
                                                   L.stream_ptr(dev)), "tm_edge_feature_table")
             self._dropin_etab_key = key
-            self._prep_dirty = True
+            self._prep_dirty = self._prep_dirty_fast = True   # side streams must wait for this work
         return self._dropin_etab
 
     def encoder_fwd(self, node6, eid3, ts3, cat, cut, cnt, n_groups, B, W, out=None, workspace=None, M=1,
@@ -565,6 +566,10 @@ class TempME(nn.Module):
         assert np.shape(edge_identify)[-1] == 3 and np.shape(edge_idx)[-1] == 3, "event_dim mismatch (:180)"
         if not self._hip_eval_ok() or (self.training and not self._hip_ok()):
             return self._forward_torch(walks, cut_time_l, edge_identify)
+        if not self.training:
+            out = self._dropin_forward(node_idx, edge_idx, time_idx, cat_feat, cut_time_l, edge_identify, dev, B, W)
+            if out is not None:
+                return out
         if self.training:
             out = self.forward_groups(_to(node_idx, dev, torch.int32), _to(edge_idx, dev, torch.int32),
                                       _to(time_idx, dev, torch.float32), _to(cat_feat, dev, torch.int32).reshape(B, W),
@@ -600,6 +605,178 @@ class TempME(nn.Module):
             args = (n6, e3, t3, ct.reshape(B, W), cu, ei, 1, B, W)
             out = _EvalEncoderFn.apply(self, args, out, *self._encoder_params())
         return out.view(B, W, 1)
+
+    # ------------------------------------------------------------------ drop-in eval fast path
+    def _dropin_ctx(self, dev):
+        """(device, context, its three side streams -- torch streams, so outputs can come from their pools --,
+        next side) -- created on first use; a new context's side streams first wait for the caller's stream."""
+        c = self.__dict__.get("_dropin_c")
+        if c is None or c[0] != dev:
+            h = L.C.c_void_p()
+            L.check(L.lib().tm_dropin_create(dev.index, L.C.byref(h)), "tm_dropin_create")
+            ctx = _DropinCtx(h)
+            ext = [torch.cuda.Stream(device=dev) for _ in range(3)]
+            for k in range(3):
+                L.check(L.lib().tm_dropin_set_stream(h, k, ext[k].cuda_stream), "tm_dropin_set_stream")
+            ctx.streams = ext      # alive as long as the context
+            ctx.side_ids = [(x.stream_id, x.device_index, x.device_type) for x in ext]
+            ctx.cur_obj = None
+            c = self.__dict__["_dropin_c"] = (dev, ctx, ext, [0])
+            self._prep_dirty_fast = True
+        return c
+
+    def _fast_state(self):
+        """What the drop-in fast path derives from the weights and feature tables (packed weights, edge
+        table, table pointers, parameter bundles), rebuilt when one key over the packed parameters'
+        (data_ptr, version, requires_grad) and the two feature tables' (data_ptr, version) changes."""
+        ws = self._weight_list()
+        ne = self._modules["node_raw_embed"]._parameters["weight"]
+        ee = self._modules["edge_raw_embed"]._parameters["weight"]
+        key = (*map(_DP, ws), *map(_VER, ws), *map(_RG, ws), ne.data_ptr(), ne._version, ee.data_ptr(), ee._version)
+        fs = self.__dict__.get("_fs")
+        if fs is not None and fs[0] == key:
+            return fs[1]
+        wts = self.packed_weights()
+        etab = self.dropin_edge_table(wts)
+        nt, et = self.feature_tables()
+        st = _FastState(wts, None if etab is None else etab.data_ptr(), nt.data_ptr(), et.data_ptr(),
+                        any(map(_RG, ws[:20] + ws[-2:])), any(map(_RG, ws[20:26] + ws[-2:])), self._packed_key)
+        st.gate_key = self._gate_key(ws)
+        st.keep = (etab, nt, et)
+        self.__dict__["_fs"] = (key, st)
+        return st
+
+    @staticmethod
+    def _gate_key(ws):
+        """(data_ptr, version, requires_grad) of the tensors the dependency gate reads (the gate MLP and the
+        time encoder), which retrieve_explanation checks before using the gate factors of a forward."""
+        g = ws[20:26] + ws[-2:]
+        return (*map(_DP, g), *map(_VER, g), *map(_RG, g))
+
+    def _dropin_forward(self, node_idx, edge_idx, time_idx, cat_feat, cut_time_l, edge_identify, dev, B, W):
+        """Eval forward on resident device-pack views (``pack.DevicePack.get_item`` / ``get_item_edge``) in one
+        library call (tm_dropin_forward: side stream, staged cut times, encoder, and the dependency-gate
+        factors retrieve_edge_imp_node will need, cached by walk identity).  None when the inputs are not
+        such views (the general path below handles them)."""
+        for t in (node_idx, edge_idx, time_idx, cat_feat, edge_identify):
+            if t.__class__ is not torch.Tensor or not getattr(t, "_tm_resident", False):
+                return None
+        if node_idx.dtype is not torch.int32 or edge_idx.dtype is not torch.int32 or time_idx.dtype is not torch.float32 \
+                or cat_feat.dtype is not torch.int32 or edge_identify.dtype is not torch.float32 or B == 0:
+            return None
+        cut_h = cut_d = None
+        if cut_time_l.__class__ is np.ndarray:
+            c = cut_time_l if cut_time_l.dtype == np.float64 and cut_time_l.flags.c_contiguous else \
+                np.ascontiguousarray(cut_time_l, dtype=np.float64)
+            if c.size != B or B > 512:
+                return None
+            cut_h = c.__array_interface__["data"][0]
+        elif isinstance(cut_time_l, torch.Tensor) and cut_time_l.device == dev and cut_time_l.dtype is torch.float64 \
+                and cut_time_l.numel() == B and cut_time_l.is_contiguous():
+            cut_d = cut_time_l.data_ptr()
+        else:
+            return None
+        if not self._hip_eval_ok():
+            return None
+        fs = self._fast_state()
+        _, ctx, ext, nk = self._dropin_ctx(dev)
+        k = nk[0]
+        nk[0] = (k + 1) % 3
+        # the outputs come from the caching allocator's pool of side stream k (the kernels writing them run
+        # there) and are recorded as used by the caller's stream, which reads them after the wait
+        di = dev.index
+        cur = torch._C._cuda_getCurrentStream(di)
+        cobj = ctx.cur_obj
+        if cobj is None or cobj[0] != cur:
+            cobj = ctx.cur_obj = (cur, torch.cuda.Stream(stream_id=cur[0], device_index=cur[1], device_type=cur[2]))
+        torch._C._cuda_setStream(*ctx.side_ids[k])
+        try:
+            out = torch.empty(B * W * 4, dtype=torch.float32, device=dev)   # imp [B*W] | gate factors [B*W*3]
+        finally:
+            torch._C._cuda_setStream(*cur)
+        out.record_stream(cobj[1])
+        sync = 1 if (cut_d is not None or self.__dict__.get("_prep_dirty_fast", True)) else 0
+        if sync:
+            self._prep_dirty_fast = False
+        o = out.data_ptr()
+        L.check(L.lib().tm_dropin_forward(ctx.h, k, sync, fs.wts, fs.nt, fs.et, fs.etab, B, W, node_idx.data_ptr(),
+                                          edge_idx.data_ptr(), time_idx.data_ptr(), cat_feat.data_ptr(), cut_h, cut_d,
+                                          edge_identify.data_ptr(), o, o + 4 * B * W,
+                                          torch._C._cuda_getCurrentRawStream(di)), "TempME.forward")
+        imp = out[:B * W]
+        # the gate factors, for retrieve_explanation with these very walk tensors (identity + version)
+        gcache = self.__dict__.setdefault("_gf_cache", [])
+        gcache.append((edge_idx, time_idx, edge_idx._version, time_idx._version, fs.gate_key, out, B * W, B, W, fs))
+        if len(gcache) > 6:
+            del gcache[0]
+        if fs.enc_grad and torch.is_grad_enabled():
+            # the cut times as a host copy (moved to the device only if a backward runs)
+            args = (node_idx, edge_idx, time_idx, cat_feat.view(B, W),
+                    np.array(cut_time_l, dtype=np.float64) if cut_d is None else cut_time_l, edge_identify, 1, B, W)
+            imp = _apply(_EvalEncoderBundleFn, self, args, imp, fs.bundle(self, "enc"))
+        return imp.view(B, W, 1)
+
+    def _param_bundle(self, which):
+        return self._fast_state().bundle(self, which)
+
+    def _dropin_retrieve(self, sides):
+        """retrieve_explanation(training=False) for the three sides of one reference batch whose walks went
+        through _dropin_forward: one tm_edge_importance_gf3 launch from the gate factors cached with those
+        walk tensors (same objects, unmodified, gate weights unchanged), written straight into the
+        concatenated [3B, N] / [3B, N^2] outputs.  None if any side does not qualify."""
+        gc = self.__dict__.get("_gf_cache", ())
+        gk = None
+        got = []
+        for subgraph, imp, walks in sides:
+            e3, t3 = walks[1], walks[2]
+            h = None
+            for ent in reversed(gc):
+                if ent[0] is e3 and ent[1] is t3:
+                    h = ent
+                    break
+            if h is None or e3._version != h[2] or t3._version != h[3]:
+                return None
+            if gk is None:
+                gk = self._gate_key(self._weight_list())
+            if h[4] != gk:
+                return None
+            B, W = h[7], h[8]
+            n1, n2 = subgraph[0]
+            x1, x2 = subgraph[1]
+            for t in (n1, x1, n2, x2):
+                if not getattr(t, "_tm_resident", False):
+                    return None
+            N = n1.shape[1]
+            if imp.__class__ is not torch.Tensor or imp.dtype is not torch.float32 or imp.numel() != B * W or \
+                    not imp.is_contiguous() or n1.shape[0] != B or x1.shape != n1.shape or n2.shape != (B, N * N) or \
+                    x2.shape != n2.shape or n1.dtype is not torch.int32:
+                return None
+            got.append((h, e3, t3, imp, n1, x1, n2, x2, B, W, N))
+        B, W, N = got[0][8], got[0][9], got[0][10]
+        for g in got:
+            if g[8] != B or g[9] != W or g[10] != N:
+                return None
+        dev = self._dev()
+        o = torch.empty(3 * B * (N + N * N), dtype=torch.float32, device=dev)
+        p1 = o.data_ptr()
+        p2 = p1 + 4 * 3 * B * N
+        (ha, ea, _, ia, na1, xa1, na2, xa2, *_), (hb, eb, _, ib, nb1, xb1, nb2, xb2, *_), \
+            (hc, ec, _, ic, nc1, xc1, nc2, xc2, *_) = got
+        L.check(L.lib().tm_edge_importance_gf3(
+            B, W, N, ha[5].data_ptr() + 4 * ha[6], hb[5].data_ptr() + 4 * hb[6], hc[5].data_ptr() + 4 * hc[6],
+            ea.data_ptr(), eb.data_ptr(), ec.data_ptr(), ia.data_ptr(), ib.data_ptr(), ic.data_ptr(),
+            na1.data_ptr(), nb1.data_ptr(), nc1.data_ptr(), xa1.data_ptr(), xb1.data_ptr(), xc1.data_ptr(),
+            na2.data_ptr(), nb2.data_ptr(), nc2.data_ptr(), xa2.data_ptr(), xb2.data_ptr(), xc2.data_ptr(),
+            p1, p2, torch._C._cuda_getCurrentRawStream(dev.index)), "retrieve_explanation")
+        o1, o2 = o[:3 * B * N].view(3 * B, N), o[3 * B * N:].view(3 * B, N * N)
+        if torch.is_grad_enabled() and (any(gk[-8:]) or ia.requires_grad or ib.requires_grad or
+                                        ic.requires_grad):
+            args = tuple((g[1], g[2], g[4], g[5], g[6], g[7], B, W, N) for g in got)
+            # the gate bundle of the forward's state (its gate parameters are the current ones: gk matched)
+            o1, o2 = _apply(_EvalExplain3Fn, self, args, ia, ib, ic, o1, o2, ha[9].bundle(self, "gate"))
+        if self.base_type == "tgn":
+            return [o1, o2]
+        return [o1]
 
     def _side_stream(self, dev, items):
         """The next of three side streams for an eval forward whose inputs are host arrays or resident
@@ -660,6 +837,12 @@ class TempME(nn.Module):
     def retrieve_explanation(self, subgraph_src, graphlet_imp_src, walks_src, subgraph_tgt, graphlet_imp_tgt,
                              walks_tgt, subgraph_bgd, graphlet_imp_bgd, walks_bgd, training=True):
         """explainer_new.py:408-418."""
+        if not training and self.__dict__.get("_gf_cache") and self._hip_eval_ok():
+            r = self._dropin_retrieve(((subgraph_src, graphlet_imp_src, walks_src),
+                                       (subgraph_tgt, graphlet_imp_tgt, walks_tgt),
+                                       (subgraph_bgd, graphlet_imp_bgd, walks_bgd)))
+            if r is not None:
+                return r
         s0, s1 = self.retrieve_edge_imp_node(subgraph_src, graphlet_imp_src, walks_src, training=training)
         t0, t1 = self.retrieve_edge_imp_node(subgraph_tgt, graphlet_imp_tgt, walks_tgt, training=training)
         b0, b1 = self.retrieve_edge_imp_node(subgraph_bgd, graphlet_imp_bgd, walks_bgd, training=training)
@@ -822,6 +1005,114 @@ class _EvalEncoderFn(torch.autograd.Function):
                 grads = torch.autograd.grad(out.reshape(-1), params, grad_outputs=d_imp.reshape(-1).to(out.dtype),
                                             allow_unused=True)
         return (None, None, None, *grads)
+
+
+def _apply(fn, *args):
+    """fn.apply without the Python wrapper's per-argument pass (unwrap_dead_wrappers): the C++ apply of
+    torch.autograd.Function, used when no functorch transform is active (as Function.apply itself does)."""
+    if torch._C._are_functorch_transforms_active():
+        return fn.apply(*args)
+    return _C_APPLY(fn)(*args)
+
+
+def _C_APPLY(fn):
+    a = fn.__dict__.get("_c_apply")
+    if a is None:
+        a = super(torch.autograd.Function, fn).apply
+        setattr(fn, "_c_apply", a)
+    return a
+
+
+_DP = torch.Tensor.data_ptr
+_VER = operator.attrgetter("_version")
+_RG = operator.attrgetter("requires_grad")
+
+
+class _FastState:
+    """TempME._fast_state's derived objects for one weight / table version."""
+
+    def __init__(self, wts, etab, nt, et, enc_grad, gate_grad, packed_key):
+        self.wts, self.etab, self.nt, self.et = wts, etab, nt, et
+        self.enc_grad, self.gate_grad, self.packed_key = enc_grad, gate_grad, packed_key
+        self._bundles = {}
+
+    def bundle(self, ex, which):
+        """One tensor standing for the 22 encoder (or 8 gate) parameters in an eval call's autograd node:
+        the concatenation of their flattened values, built under grad mode once per weight version (its
+        CatBackward node -- no saved tensors -- routes a gradient of the bundle to every parameter), so
+        the per-call node has a few inputs instead of 22 (Function.apply costs per input)."""
+        b = self._bundles.get(which)
+        if b is None:
+            params = ex._encoder_params() if which == "enc" else ex._gate_params()
+            with torch.enable_grad():
+                b = self._bundles[which] = torch.cat([p.reshape(-1) for p in params])
+        return b
+
+
+class _DropinCtx:
+    def __init__(self, h):
+        self.h = h
+
+    def __del__(self):
+        try:
+            L.lib().tm_dropin_free(self.h)
+        except Exception:
+            pass
+
+
+def _flat_grads(grads, params):
+    return torch.cat([(torch.zeros_like(p) if g is None else g).reshape(-1) for g, p in zip(grads, params)])
+
+
+class _EvalEncoderBundleFn(torch.autograd.Function):
+    """_EvalEncoderFn with the 22 encoder parameters behind one bundle tensor (TempME._param_bundle):
+    backward returns the parameters' gradients flattened into the bundle's layout."""
+
+    @staticmethod
+    def forward(ctx, ex, args, out, bundle):
+        ctx.ex, ctx.args = ex, args
+        return out.detach()
+
+    @staticmethod
+    def backward(ctx, d_imp):
+        a = ctx.args
+        if isinstance(a[4], np.ndarray):
+            ctx.args = a[:4] + (torch.from_numpy(a[4]).to(a[0].device),) + a[5:]
+        grads = _EvalEncoderFn.backward(ctx, d_imp)[3:]
+        return None, None, None, _flat_grads(grads, ctx.ex._encoder_params())
+
+
+class _EvalExplain3Fn(torch.autograd.Function):
+    """retrieve_explanation(training=False) over the three sides with gradients enabled (_EvalExplainFn per
+    side, the 8 gate parameters behind one bundle tensor): outputs the concatenated hop-1 / hop-2."""
+
+    @staticmethod
+    def forward(ctx, ex, args, imp_s, imp_t, imp_b, o1, o2, bundle):
+        ctx.ex, ctx.args = ex, args
+        ctx.save_for_backward(imp_s, imp_t, imp_b)
+        return o1.detach(), o2.detach()
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        ex = ctx.ex
+        params = ex._gate_params()
+        d_imps, gsum = [], None
+        for s, imp in enumerate(ctx.saved_tensors):
+            e3, t3, n1, x1, n2, x2, B, W, N = ctx.args[s]
+            sub = _Ctx(ex, (e3, t3, n1, x1, n2, x2, B, W, N), imp)
+            gs = _EvalExplainFn.backward(sub, g1[s * B:(s + 1) * B], g2[s * B:(s + 1) * B])
+            d_imps.append(gs[2])
+            pg = [torch.zeros_like(p) if g is None else g for g, p in zip(gs[5:], params)]
+            gsum = pg if gsum is None else [a + b for a, b in zip(gsum, pg)]
+        return (None, None, *[None if d is None else d.reshape(ctx.saved_tensors[s].shape) for s, d in enumerate(d_imps)],
+                None, None, _flat_grads(gsum, params))
+
+
+class _Ctx:
+    """A stand-in ctx for calling _EvalExplainFn.backward per side."""
+
+    def __init__(self, ex, args, imp):
+        self.ex, self.args, self.saved_tensors = ex, args, (imp,)
 
 
 class _EvalExplainFn(torch.autograd.Function):

@@ -181,6 +181,15 @@ def get_item_edge(edge_features, batch_id):
         edge_features = edge_features.cnt
     if isinstance(edge_features, torch.Tensor):
         sl = _dev_index(batch_id, edge_features.shape[1], edge_features.device)
+        grid = getattr(edge_features, "_tm_grid", None)
+        if isinstance(sl, slice) and grid is not None:
+            n = sl.stop - sl.start
+            if not grid and n > 0:   # views of every batch on the first batch size's grid, as DevicePack.get_item
+                nb = edge_features.shape[1] // n
+                per = [[_resident(v) for v in edge_features[s].split(n, dim=0)][:nb] for s in range(3)]
+                grid[:] = [n, [tuple(per[s][k] for s in range(3)) for k in range(nb)]]
+            if n == grid[0] and sl.start % n == 0:
+                return grid[1][sl.start // n]
         e = edge_features[:, sl]
         return tuple(_resident(e[s]) for s in range(3))
     e = edge_features[:, _as_slice(batch_id, np.shape(edge_features)[1]), :, :, :]
@@ -189,7 +198,9 @@ def get_item_edge(edge_features, batch_id):
 
 def load_edge(edge, device):
     """``np.load({data}_{mode}_edge.npy)`` uploaded once as float32 [3, n, W, 3, 3] for ``get_item_edge``."""
-    return torch.from_numpy(np.ascontiguousarray(np.asarray(edge), dtype=np.float32)).to(device)
+    t = torch.from_numpy(np.ascontiguousarray(np.asarray(edge), dtype=np.float32)).to(device)
+    t._tm_grid = []   # get_item_edge's per-batch views, made on first use
+    return t
 
 
 def _resident(t):
@@ -290,8 +301,17 @@ class DevicePack(EventBuffers):
     def get_item(self, batch_id):
         """get_item (utils/batch_loader.py:200-235) on the device: the same tuple nesting -- per side
         ([hop-1, hop-2] node, [..] eid, [..] ts), per side (node [B,W,6], eid [B,W,3], ts [B,W,3],
-        cat [B,W,1], marginal [B,W,1]), dst_fake [B] -- as int32 / float32 device views."""
+        cat [B,W,1], marginal [B,W,1]), dst_fake [B] -- as int32 / float32 device views.  A batch on the
+        grid of the batch size seen first (the eval loop's np.arange(k * bs, (k + 1) * bs)) comes from views
+        of every batch made at once (torch.split, one call per array): the same view objects per batch."""
         sl = _dev_index(batch_id, self.E, self.dst_fake.device)
+        if isinstance(sl, slice):
+            n = sl.stop - sl.start
+            grid = self.__dict__.get("_grid")
+            if grid is None and n > 0:
+                grid = self._grid = (n, self._split_views(n))
+            if grid is not None and n == grid[0] and sl.start % n == 0:
+                return grid[1][sl.start // n]
         r = _resident
         out = []
         for s in range(3):
@@ -303,6 +323,22 @@ class DevicePack(EventBuffers):
                         r(self.cat[s, sl].unsqueeze(-1)), r(self.marg[s, sl].unsqueeze(-1))))
         out.append(r(self.dst_fake[:self.E][sl]))
         return tuple(out)
+
+    def _split_views(self, B):
+        """get_item's tuple for every batch [k B, (k + 1) B) that fits, from one torch.split per array."""
+        def sp(t):
+            return [_resident(v) for v in t[:self.E].split(B, dim=0)][:self.E // B]
+        s1n, s1e, s1t, s2n, s2e, s2t, n6, e3, t3, ct, mg = (
+            [sp(a[s]) for s in range(3)] for a in (self.sub1_node, self.sub1_eid, self.sub1_ts, self.sub2_node,
+                                                   self.sub2_eid, self.sub2_ts, self.node6, self.eid3, self.ts3,
+                                                   self.cat.unsqueeze(-1), self.marg.unsqueeze(-1)))
+        df = sp(self.dst_fake)
+        out = []
+        for k in range(self.E // B):
+            subs = tuple(([s1n[s][k], s2n[s][k]], [s1e[s][k], s2e[s][k]], [s1t[s][k], s2t[s][k]]) for s in range(3))
+            walks = tuple((n6[s][k], e3[s][k], t3[s][k], ct[s][k], mg[s][k]) for s in range(3))
+            out.append((*subs, *walks, df[k]))
+        return out
 
     @classmethod
     def from_files(cls, cat_path, edge_path, n_degree, device):

@@ -331,6 +331,53 @@ def test_dropin_device_pack_and_grad_equal_pipeline(dev, finder, g, z, where):
     assert torch.equal(e2, h2.reshape(3 * E, N * N))
 
 
+def test_dropin_fast_path_gradients_match_general_path(dev, finder, g, z):
+    """The device-pack fast path (tm_dropin_forward + tm_edge_importance_gf, parameters behind bundle
+    tensors in the autograd nodes) against the general path (host pack: per-side calls, every parameter
+    an input of its node): same outputs bit for bit, and the same gradients of a loss over the
+    explanation and the three graphlet importances, for every explainer parameter and the importances."""
+    from tempme_amd import pack as P
+    from tempme_amd.pipeline import ExplainPipeline
+    N, E = 20, 50
+    ex = _explainer(dev, g, z, "N20_base")
+    pipe = ExplainPipeline(ex, finder.graph, torch.from_numpy(z["test_sampler_dst"]), N, 3, 25, seed=0,
+                           split=px.SPLIT_TEST)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a[:E], dtype=dt)).to(dev)  # noqa: E731
+    pipe.run(t(z["test_src"], np.int32), t(z["test_dst"], np.int32), t(z["test_ts"], np.float64),
+             t(z["test_eidx"], np.int32), torch.arange(E, dtype=torch.int32, device=dev))
+    _, cat_d, edge = P.buffers_to_arrays(pipe.buf, E)
+
+    class A:
+        n_degree = N
+    cut = z["test_ts"][:E].astype(np.float64)
+    res = {}
+    for where in ("device", "host"):
+        pk, ed = ((P.load_subgraph_margin(A(), cat_d, device=dev), P.load_edge(edge, dev)) if where == "device"
+                  else (P.load_subgraph_margin(A(), cat_d), edge))
+        ex.zero_grad()
+        ex.__dict__.pop("_gf_cache", None)
+        idx = np.arange(25, 50)
+        sg_s, sg_t, sg_b, w_s, w_t, w_b, _ = P.get_item(pk, idx)
+        e_s, e_t, e_b = P.get_item_edge(ed, idx)
+        imps = [ex(w_s, cut[idx], e_s), ex(w_t, cut[idx], e_t), ex(w_b, cut[idx], e_b)]
+        for i in imps:
+            i.retain_grad()
+        expl = ex.retrieve_explanation(sg_s, imps[0], w_s, sg_t, imps[1], w_t, sg_b, imps[2], w_b, training=False)
+        assert (where == "device") == bool(ex.__dict__.get("_gf_cache")), "fast path taken only on device views"
+        loss = expl[0].pow(2).sum() + 0.5 * expl[1].sum() + (imps[0] * imps[1]).sum() + imps[2].pow(2).sum()
+        loss.backward()
+        res[where] = ([x.detach().clone() for x in expl], [i.grad.clone() for i in imps],
+                      {n: p.grad.detach().clone() for n, p in ex.named_parameters() if p.grad is not None})
+    (xd, gd, pd), (xh, gh, ph) = res["device"], res["host"]
+    for a_, b_ in zip(xd, xh):
+        assert torch.equal(a_, b_)
+    for a_, b_ in zip(gd, gh):
+        torch.testing.assert_close(a_, b_, rtol=1e-5, atol=1e-7)
+    assert pd.keys() == ph.keys() and len(pd) >= 26
+    for n in pd:
+        torch.testing.assert_close(pd[n], ph[n], rtol=1e-5, atol=1e-7, msg=n)
+
+
 def test_eval_forward_grad_matches_torch(dev, finder, g, z):
     """Eval mode with gradients enabled: the eval kernel's output with the on-demand backward (recompute
     through the training kernels) gives the torch formulation's weight gradients within 2e-4 rel-norm."""

@@ -8,7 +8,7 @@ for r in 1 2; do for so in tempme_amd/lib/ab/*.so; do
   python - "$so" <<'PY' | tee -a gpurun_out/gab.txt
 import json, sys, os
 d = json.loads([l for l in open("gpurun_out/gab.log") if l.startswith("{")][-1])
-k = d["kernels"]["gm_embed_kernel"]
+k = d["kernels"].get("gm_fused_kernel") or d["kernels"]["gm_embed_kernel"]
 print(os.path.basename(sys.argv[1]), "gm_embed", k["avg_ms"], k["frac"], "value", d["value"])
 PY
 done; done

@@ -70,6 +70,8 @@ for s in "$@"; do
         c2) step bench_c2 600 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config 2 ;;
         c4) step bench_c4 900 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config 4 ;;
         a3) step bench_a3 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --alpha 3.0 ;;
+        dropint) step dropint 300 python tools/dropin_timing.py ;;
+        dropintrace) step dropintrace 300 rocprofv3 --kernel-trace -d gpurun_out/ditrace -o run --output-format csv -- python tools/dropin_timing.py ;;
         dropinprof) TEMPME_DROPIN_PROFILE=1 step dropinprof 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
         k:*) step pytest_k 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread -k "${s#k:}" ;;
         micro:*) m=${s#micro:}; step micro_$m 200 ./micro/$m ;;   # a prebuilt micro-benchmark binary
