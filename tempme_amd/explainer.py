@@ -561,15 +561,15 @@ class TempME(nn.Module):
     def forward(self, walks, cut_time_l, edge_identify):
         """explainer_new.py:174-201 -> [bsz, n_walks, 1]."""
         node_idx, edge_idx, time_idx, cat_feat, _ = walks
+        if not self.training:
+            out = self._dropin_forward(node_idx, edge_idx, time_idx, cat_feat, cut_time_l, edge_identify)
+            if out is not None:
+                return out
         dev = self._dev()
         B, W = np.shape(edge_idx)[0], np.shape(edge_idx)[1]
         assert np.shape(edge_identify)[-1] == 3 and np.shape(edge_idx)[-1] == 3, "event_dim mismatch (:180)"
         if not self._hip_eval_ok() or (self.training and not self._hip_ok()):
             return self._forward_torch(walks, cut_time_l, edge_identify)
-        if not self.training:
-            out = self._dropin_forward(node_idx, edge_idx, time_idx, cat_feat, cut_time_l, edge_identify, dev, B, W)
-            if out is not None:
-                return out
         if self.training:
             out = self.forward_groups(_to(node_idx, dev, torch.int32), _to(edge_idx, dev, torch.int32),
                                       _to(time_idx, dev, torch.float32), _to(cat_feat, dev, torch.int32).reshape(B, W),
@@ -653,17 +653,22 @@ class TempME(nn.Module):
         g = ws[20:26] + ws[-2:]
         return (*map(_DP, g), *map(_VER, g), *map(_RG, g))
 
-    def _dropin_forward(self, node_idx, edge_idx, time_idx, cat_feat, cut_time_l, edge_identify, dev, B, W):
+    def _dropin_forward(self, node_idx, edge_idx, time_idx, cat_feat, cut_time_l, edge_identify):
         """Eval forward on resident device-pack views (``pack.DevicePack.get_item`` / ``get_item_edge``) in one
         library call (tm_dropin_forward: side stream, staged cut times, encoder, and the dependency-gate
         factors retrieve_edge_imp_node will need, cached by walk identity).  None when the inputs are not
-        such views (the general path below handles them)."""
-        for t in (node_idx, edge_idx, time_idx, cat_feat, edge_identify):
-            if t.__class__ is not torch.Tensor or not getattr(t, "_tm_resident", False):
-                return None
-        if node_idx.dtype is not torch.int32 or edge_idx.dtype is not torch.int32 or time_idx.dtype is not torch.float32 \
-                or cat_feat.dtype is not torch.int32 or edge_identify.dtype is not torch.float32 or B == 0:
+        such views of one batch (the general path handles them)."""
+        if not (getattr(edge_idx, "_tm_resident", False) and getattr(node_idx, "_tm_resident", False) and
+                getattr(time_idx, "_tm_resident", False) and getattr(cat_feat, "_tm_resident", False) and
+                getattr(edge_identify, "_tm_resident", False)):
             return None
+        # resident views are int32 / float32 slices of one pack: check that they are one batch's
+        B, W, three = edge_idx.shape
+        if three != 3 or B == 0 or node_idx.shape != (B, W, 6) or time_idx.shape != (B, W, 3) or \
+                cat_feat.shape[:2] != (B, W) or edge_identify.shape != (B, W, 3, 3) or \
+                edge_idx.dtype is not torch.int32 or time_idx.dtype is not torch.float32:
+            return None
+        dev = self._dev()
         cut_h = cut_d = None
         if cut_time_l.__class__ is np.ndarray:
             c = cut_time_l if cut_time_l.dtype == np.float64 and cut_time_l.flags.c_contiguous else \
@@ -703,18 +708,19 @@ class TempME(nn.Module):
                                           edge_idx.data_ptr(), time_idx.data_ptr(), cat_feat.data_ptr(), cut_h, cut_d,
                                           edge_identify.data_ptr(), o, o + 4 * B * W,
                                           torch._C._cuda_getCurrentRawStream(di)), "TempME.forward")
-        imp = out[:B * W]
+        imp = out.as_strided((B, W, 1), (W, 1, 1))
         # the gate factors, for retrieve_explanation with these very walk tensors (identity + version)
         gcache = self.__dict__.setdefault("_gf_cache", [])
         gcache.append((edge_idx, time_idx, edge_idx._version, time_idx._version, fs.gate_key, out, B * W, B, W, fs))
         if len(gcache) > 6:
             del gcache[0]
         if fs.enc_grad and torch.is_grad_enabled():
-            # the cut times as a host copy (moved to the device only if a backward runs)
-            args = (node_idx, edge_idx, time_idx, cat_feat.view(B, W),
+            # the cut times as a host copy (moved to the device only if a backward runs); cat [B, W, 1] is
+            # reshaped there too
+            args = (node_idx, edge_idx, time_idx, cat_feat,
                     np.array(cut_time_l, dtype=np.float64) if cut_d is None else cut_time_l, edge_identify, 1, B, W)
             imp = _apply(_EvalEncoderBundleFn, self, args, imp, fs.bundle(self, "enc"))
-        return imp.view(B, W, 1)
+        return imp
 
     def _param_bundle(self, which):
         return self._fast_state().bundle(self, which)
@@ -1076,8 +1082,10 @@ class _EvalEncoderBundleFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, d_imp):
         a = ctx.args
-        if isinstance(a[4], np.ndarray):
-            ctx.args = a[:4] + (torch.from_numpy(a[4]).to(a[0].device),) + a[5:]
+        B, W = a[7], a[8]
+        ctx.args = a[:3] + (a[3].reshape(B, W),
+                            torch.from_numpy(a[4]).to(a[0].device) if isinstance(a[4], np.ndarray) else a[4]) + a[5:]
+        d_imp = d_imp.reshape(-1)
         grads = _EvalEncoderFn.backward(ctx, d_imp)[3:]
         return None, None, None, _flat_grads(grads, ctx.ex._encoder_params())
 
