@@ -62,6 +62,37 @@ __global__ void __launch_bounds__(1024) std_kernel(int32_t B, int32_t W, const d
     if (threadIdx.x == 0) std_out[g] = n > 1 ? (float)sqrt(var / (double)(n - 1)) : __builtin_nanf("");
 }
 
+// std_kernel for one group whose B <= 256 cut times come as a kernel argument (tm_dropin_forward): the same
+// sums in the same order as std_kernel, and the cut times written to cut_out for the kernels that follow
+// on the stream
+struct CutArg {
+    double v[256];
+};
+
+__global__ void __launch_bounds__(1024) std_cut_kernel(int32_t B, int32_t W, CutArg c, const float *__restrict__ ts3,
+                                                       double *__restrict__ cut_out, float *__restrict__ std_out,
+                                                       int32_t do_std) {
+    __shared__ double red[16];
+    if ((int)threadIdx.x < B) cut_out[threadIdx.x] = c.v[threadIdx.x];
+    if (!do_std) return;
+    const int32_t nw = B * W;
+    const int64_t n = (int64_t)nw * 2;
+    double s = 0.0;
+    for (int32_t w = threadIdx.x; w < nw; w += blockDim.x) {
+        const float cc = (float)c.v[w / W];
+        s += (double)fabsf(cc - ts3[w * 3]) + (double)fabsf(cc - ts3[w * 3 + 1]);
+    }
+    const double mean = block_sum(s, red) / (double)n;
+    double v = 0.0;
+    for (int32_t w = threadIdx.x; w < nw; w += blockDim.x) {
+        const float cc = (float)c.v[w / W];
+        const double d0 = (double)fabsf(cc - ts3[w * 3]) - mean, d1 = (double)fabsf(cc - ts3[w * 3 + 1]) - mean;
+        v += d0 * d0 + d1 * d1;
+    }
+    const double var = block_sum(v, red);
+    if (threadIdx.x == 0) std_out[0] = n > 1 ? (float)sqrt(var / (double)(n - 1)) : __builtin_nanf("");
+}
+
 // ------------------------------------------------------------------ event_gcn: 32 walk-positions per block
 // F[row] = [MLP(x_s + relu(x_t + L)) | MLP(x_t + relu(x_s + L))],  L = lin_event([E(e) | cnt | cos(dt)])
 __global__ void __launch_bounds__(256) gcn_kernel(EncW P, int64_t n_rows, const float *__restrict__ n_feat,
@@ -1614,10 +1645,24 @@ extern "C" int tm_encoder_fwd(const tm_weights *w, const float *n_feat, const fl
                               workspace, out_imp, stream);
 }
 
+static int encoder_fwd_impl(const tm_weights *w, const float *n_feat, const float *e_feat, const float *etab,
+                            int32_t n_groups, int32_t B, int32_t W, int32_t M, const int32_t *node6, const int32_t *eid3,
+                            const float *ts3, const int32_t *cat, const double *cut, const float *cnt, void *workspace,
+                            float *out_imp, void *stream, bool do_std);
+
 extern "C" int tm_encoder_fwd_tab(const tm_weights *w, const float *n_feat, const float *e_feat, const float *etab,
                                   int32_t n_groups, int32_t B, int32_t W, int32_t M, const int32_t *node6,
                                   const int32_t *eid3, const float *ts3, const int32_t *cat, const double *cut,
                                   const float *cnt, void *workspace, float *out_imp, void *stream) {
+    return encoder_fwd_impl(w, n_feat, e_feat, etab, n_groups, B, W, M, node6, eid3, ts3, cat, cut, cnt, workspace,
+                            out_imp, stream, true);
+}
+
+// the encoder launches; do_std = false: the groups' std values are already in the workspace (std_cut_kernel)
+static int encoder_fwd_impl(const tm_weights *w, const float *n_feat, const float *e_feat, const float *etab,
+                            int32_t n_groups, int32_t B, int32_t W, int32_t M, const int32_t *node6, const int32_t *eid3,
+                            const float *ts3, const int32_t *cat, const double *cut, const float *cnt, void *workspace,
+                            float *out_imp, void *stream, bool do_std) {
     if (!w || n_groups < 0 || B < 0 || W < 0 || M <= 0) return fail(TM_E_ARG, "tm_encoder_fwd: bad arguments");
     if (W % M) return fail(TM_E_SHAPE, "tm_encoder_fwd: W must be a multiple of M (walks per hop-1 slot)");
     const int64_t n_walks = (int64_t)n_groups * B * W;
@@ -1630,10 +1675,13 @@ extern "C" int tm_encoder_fwd_tab(const tm_weights *w, const float *n_feat, cons
     hipStream_t s = S_(stream);
     float *F = reinterpret_cast<float *>(workspace);
     float *stdv = F + n_walks * 3 * 2 * P.h;
-    hipEvent_t pe = prof_begin(s);
-    if (P.tg) std_kernel<<<dim3(n_groups), 1024, 0, s>>>(B, W, cut, ts3, stdv);
-    TM_CHECK_LAUNCH();
-    prof_end("std_kernel", s, pe);
+    hipEvent_t pe = nullptr;
+    if (do_std) {
+        pe = prof_begin(s);
+        if (P.tg) std_kernel<<<dim3(n_groups), 1024, 0, s>>>(B, W, cut, ts3, stdv);
+        TM_CHECK_LAUNCH();
+        prof_end("std_kernel", s, pe);
+    }
     if (etab && etab_q0(P) == 0) return fail(TM_E_UNSUPPORTED, "tm_encoder_fwd_tab: no edge table for these dims");
     const int nqe = r16(P.kev) / 16, ntd = r16(P.dn) / 16;
     const bool narrow = nqe >= 11 && nqe <= 14 && P.de <= 16 * EQ_MAX;
@@ -1777,6 +1825,7 @@ struct tm_dropin {
     int slot_next = 0, last_slot = -1, last_n = 0, last_side = -1;
     void *ws[SIDES] = {};
     size_t ws_bytes[SIDES] = {};
+    double *dcut[SIDES] = {};   // per side stream: the cut times its std_cut_kernel writes (stream-ordered reuse)
 };
 
 extern "C" void tm_dropin_free(tm_dropin *d) {
@@ -1787,6 +1836,7 @@ extern "C" void tm_dropin_free(tm_dropin *d) {
     for (int k = 0; k < tm_dropin::SIDES; ++k)
         if (d->side[k]) hipStreamSynchronize(d->side[k]);
     for (int k = 0; k < tm_dropin::SIDES; ++k) {
+        if (d->dcut[k]) hipFree(d->dcut[k]);
         if (d->ws[k]) hipFree(d->ws[k]);
         if (d->ev_side[k]) hipEventDestroy(d->ev_side[k]);
         if (d->side[k] && d->own[k]) hipStreamDestroy(d->side[k]);
@@ -1823,6 +1873,8 @@ extern "C" int tm_dropin_create(int32_t device, tm_dropin **out) {
     const size_t ring = sizeof(double) * tm_dropin::SLOTS * tm_dropin::SLOT_DOUBLES;
     d->hcopy = static_cast<double *>(malloc(ring));
     ok = ok && d->hcopy && hipMalloc(reinterpret_cast<void **>(&d->dring), ring) == hipSuccess;
+    for (int k = 0; ok && k < tm_dropin::SIDES; ++k)
+        ok = hipMalloc(reinterpret_cast<void **>(&d->dcut[k]), sizeof(double) * 256) == hipSuccess;
     hipSetDevice(prev);
     if (!ok) {
         tm_dropin_free(d);
@@ -1872,7 +1924,30 @@ extern "C" int tm_dropin_forward(tm_dropin *d, int32_t k, int32_t sync, const tm
     }
     const double *cut = cut_dev;
     int slot = -1;
-    if (cut_host) {
+    const int64_t n_walks = (int64_t)B * W;
+    const size_t need = (size_t)tm_encoder_workspace_bytes(w, n_walks);
+    if (d->ws_bytes[k] < need) {
+        TM_HIP(hipStreamSynchronize(side));
+        if (d->ws[k]) TM_HIP(hipFree(d->ws[k]));
+        d->ws[k] = nullptr;
+        d->ws_bytes[k] = 0;
+        TM_HIP(hipMalloc(&d->ws[k], need));
+        d->ws_bytes[k] = need;
+    }
+    bool std_done = false;
+    if (cut_host && B <= 256) {
+        // the cut times travel as the std launch's argument; std_cut_kernel writes them to this side's
+        // buffer for the encoder (stream order keeps the buffer's previous readers ahead of it)
+        CutArg c;
+        memcpy(c.v, cut_host, sizeof(double) * (size_t)B);
+        float *stdv = reinterpret_cast<float *>(d->ws[k]) + n_walks * 3 * 2 * w->P.h;
+        hipEvent_t pe = prof_begin(side);
+        std_cut_kernel<<<1, 1024, 0, side>>>(B, W, c, ts3, d->dcut[k], stdv, w->P.tg ? 1 : 0);
+        TM_CHECK_LAUNCH();
+        prof_end("std_kernel", side, pe);
+        cut = d->dcut[k];
+        std_done = true;
+    } else if (cut_host) {
         const size_t bytes = sizeof(double) * (size_t)B;
         if (d->last_slot >= 0 && d->last_n == B &&
             memcmp(d->hcopy + (size_t)d->last_slot * tm_dropin::SLOT_DOUBLES, cut_host, bytes) == 0) {
@@ -1902,18 +1977,8 @@ extern "C" int tm_dropin_forward(tm_dropin *d, int32_t k, int32_t sync, const tm
         }
         cut = d->dring + (size_t)slot * tm_dropin::SLOT_DOUBLES;
     }
-    const int64_t n_walks = (int64_t)B * W;
-    const size_t need = (size_t)tm_encoder_workspace_bytes(w, n_walks);
-    if (d->ws_bytes[k] < need) {
-        TM_HIP(hipStreamSynchronize(side));
-        if (d->ws[k]) TM_HIP(hipFree(d->ws[k]));
-        d->ws[k] = nullptr;
-        d->ws_bytes[k] = 0;
-        TM_HIP(hipMalloc(&d->ws[k], need));
-        d->ws_bytes[k] = need;
-    }
-    int rc = tm_encoder_fwd_tab(w, n_feat, e_feat, etab, 1, B, W, 1, node6, eid3, ts3, cat, cut, cnt, d->ws[k], out_imp,
-                                side);
+    int rc = encoder_fwd_impl(w, n_feat, e_feat, etab, 1, B, W, 1, node6, eid3, ts3, cat, cut, cnt, d->ws[k], out_imp,
+                              side, !std_done);
     if (rc != TM_OK) return rc;
     if (out_gfac) {
         const EncW &P = w->P;
