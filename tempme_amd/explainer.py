@@ -621,6 +621,7 @@ class TempME(nn.Module):
             ctx.streams = ext      # alive as long as the context
             ctx.side_ids = [(x.stream_id, x.device_index, x.device_type) for x in ext]
             ctx.cur_obj = None
+            ctx.fwd, ctx.expl = L.lib().tm_dropin_forward, L.lib().tm_edge_importance_gf3
             c = self.__dict__["_dropin_c"] = (dev, ctx, ext, [0])
             self._prep_dirty_fast = True
         return c
@@ -689,11 +690,11 @@ class TempME(nn.Module):
         nk[0] = (k + 1) % 3
         # the outputs come from the caching allocator's pool of side stream k (the kernels writing them run
         # there) and are recorded as used by the caller's stream, which reads them after the wait
-        di = dev.index
-        cur = torch._C._cuda_getCurrentStream(di)
+        cur = torch._C._cuda_getCurrentStream(dev.index)
         cobj = ctx.cur_obj
         if cobj is None or cobj[0] != cur:
-            cobj = ctx.cur_obj = (cur, torch.cuda.Stream(stream_id=cur[0], device_index=cur[1], device_type=cur[2]))
+            st = torch.cuda.Stream(stream_id=cur[0], device_index=cur[1], device_type=cur[2])
+            cobj = ctx.cur_obj = (cur, st, st.cuda_stream)
         torch._C._cuda_setStream(*ctx.side_ids[k])
         try:
             out = torch.empty(B * W * 4, dtype=torch.float32, device=dev)   # imp [B*W] | gate factors [B*W*3]
@@ -704,10 +705,11 @@ class TempME(nn.Module):
         if sync:
             self._prep_dirty_fast = False
         o = out.data_ptr()
-        L.check(L.lib().tm_dropin_forward(ctx.h, k, sync, fs.wts, fs.nt, fs.et, fs.etab, B, W, node_idx.data_ptr(),
-                                          edge_idx.data_ptr(), time_idx.data_ptr(), cat_feat.data_ptr(), cut_h, cut_d,
-                                          edge_identify.data_ptr(), o, o + 4 * B * W,
-                                          torch._C._cuda_getCurrentRawStream(di)), "TempME.forward")
+        rc = ctx.fwd(ctx.h, k, sync, fs.wts, fs.nt, fs.et, fs.etab, B, W, node_idx.data_ptr(), edge_idx.data_ptr(),
+                     time_idx.data_ptr(), cat_feat.data_ptr(), cut_h, cut_d, edge_identify.data_ptr(), o, o + 4 * B * W,
+                     cobj[2])
+        if rc:
+            L.check(rc, "TempME.forward")
         imp = out.as_strided((B, W, 1), (W, 1, 1))
         # the gate factors, for retrieve_explanation with these very walk tensors (identity + version)
         gcache = self.__dict__.setdefault("_gf_cache", [])
@@ -763,18 +765,20 @@ class TempME(nn.Module):
             if g[8] != B or g[9] != W or g[10] != N:
                 return None
         dev = self._dev()
+        ctx = self.__dict__["_dropin_c"][1]
         o = torch.empty(3 * B * (N + N * N), dtype=torch.float32, device=dev)
         p1 = o.data_ptr()
         p2 = p1 + 4 * 3 * B * N
         (ha, ea, _, ia, na1, xa1, na2, xa2, *_), (hb, eb, _, ib, nb1, xb1, nb2, xb2, *_), \
             (hc, ec, _, ic, nc1, xc1, nc2, xc2, *_) = got
-        L.check(L.lib().tm_edge_importance_gf3(
-            B, W, N, ha[5].data_ptr() + 4 * ha[6], hb[5].data_ptr() + 4 * hb[6], hc[5].data_ptr() + 4 * hc[6],
-            ea.data_ptr(), eb.data_ptr(), ec.data_ptr(), ia.data_ptr(), ib.data_ptr(), ic.data_ptr(),
-            na1.data_ptr(), nb1.data_ptr(), nc1.data_ptr(), xa1.data_ptr(), xb1.data_ptr(), xc1.data_ptr(),
-            na2.data_ptr(), nb2.data_ptr(), nc2.data_ptr(), xa2.data_ptr(), xb2.data_ptr(), xc2.data_ptr(),
-            p1, p2, torch._C._cuda_getCurrentRawStream(dev.index)), "retrieve_explanation")
-        o1, o2 = o[:3 * B * N].view(3 * B, N), o[3 * B * N:].view(3 * B, N * N)
+        rc = ctx.expl(B, W, N, ha[5].data_ptr() + 4 * ha[6], hb[5].data_ptr() + 4 * hb[6], hc[5].data_ptr() + 4 * hc[6],
+                      ea.data_ptr(), eb.data_ptr(), ec.data_ptr(), ia.data_ptr(), ib.data_ptr(), ic.data_ptr(),
+                      na1.data_ptr(), nb1.data_ptr(), nc1.data_ptr(), xa1.data_ptr(), xb1.data_ptr(), xc1.data_ptr(),
+                      na2.data_ptr(), nb2.data_ptr(), nc2.data_ptr(), xa2.data_ptr(), xb2.data_ptr(), xc2.data_ptr(),
+                      p1, p2, torch._C._cuda_getCurrentRawStream(dev.index))
+        if rc:
+            L.check(rc, "retrieve_explanation")
+        o1, o2 = o.as_strided((3 * B, N), (N, 1)), o.as_strided((3 * B, N * N), (N * N, 1), 3 * B * N)
         if torch.is_grad_enabled() and (any(gk[-8:]) or ia.requires_grad or ib.requires_grad or
                                         ic.requires_grad):
             args = tuple((g[1], g[2], g[4], g[5], g[6], g[7], B, W, N) for g in got)
@@ -796,9 +800,11 @@ class TempME(nn.Module):
                 return None
             if not isinstance(a, (np.ndarray, torch.Tensor)):
                 return None
-        ss = self.__dict__.get("_side_streams")
-        if ss is None or ss[0].device != dev:
-            ss = self.__dict__["_side_streams"] = [torch.cuda.Stream(device=dev) for _ in range(3)]
+        # the drop-in context's three streams (shared with the fast path: more streams than the device's
+        # hardware queues -- 4 by default -- would be multiplexed onto them)
+        ss = self._dropin_ctx(dev)[2]
+        if self.__dict__.get("_side_streams") is not ss:
+            self.__dict__["_side_streams"] = ss
             self.__dict__["_side_i"] = 0
             self._prep_dirty = True
         if getattr(self, "_prep_dirty", True):
