@@ -880,7 +880,21 @@ class TempME(nn.Module):
         return self._null_dev
 
     def kl_loss(self, prob, walks, target=0.3):
-        """explainer_new.py:432-453."""
+        """explainer_new.py:432-453.  With the empirical prior over the 12 motif categories and a device
+        tensor prob [B, W(, 1)]: one tm_kl_loss launch (value and d/d prob; fp64 inside, within 1e-5 of the
+        torch formulation below, which serves other priors / category counts and host tensors)."""
+        _, _, _, cat_feat, _ = walks
+        if self.prior == "empirical" and len(self.null_model) == 12 and isinstance(prob, torch.Tensor) and \
+                prob.is_cuda and prob.dim() >= 2 and prob.numel() == prob.shape[0] * prob.shape[1] and \
+                prob.dtype == torch.float32:
+            B, W = prob.shape[0], prob.shape[1]
+            cat = _to(cat_feat, prob.device, torch.int32)
+            if cat.numel() == B * W:
+                return _KLFn.apply(prob.reshape(1, B, W), cat.reshape(1, B, W), self._null_vec(prob.device),
+                                   float(target))
+        return self._kl_loss_torch(prob, walks, target)
+
+    def _kl_loss_torch(self, prob, walks, target=0.3):
         _, _, _, cat_feat, _ = walks
         prob = torch.clamp(prob, 1e-6, 1 - 1e-6)
         if self.prior == "empirical":
@@ -903,7 +917,7 @@ class TempME(nn.Module):
         cat [G,B,W] int.  prior='empirical' only (the reference default); value and gradient from
         tm_kl_loss (fp64 inside), within 1e-5 of the per-side torch formulation."""
         if self.prior != "empirical" or not self._hip_ok():
-            return sum(self.kl_loss(prob[g].unsqueeze(-1), (None, None, None, cat[g], None), target=target)
+            return sum(self._kl_loss_torch(prob[g].unsqueeze(-1), (None, None, None, cat[g], None), target=target)
                        for g in range(prob.shape[0]))
         return _KLFn.apply(prob, cat, self._null_vec(prob.device), float(target))
 

@@ -93,11 +93,37 @@ def test_kl_loss_groups_matches_per_side(dev, W):
     p1 = prob.clone().to(dev).requires_grad_(True)
     p2 = prob.clone().to(dev).requires_grad_(True)
     a = ex.kl_loss_groups(p1, cat.to(dev), target=0.3)
-    b = sum(ex.kl_loss(p2[g].unsqueeze(-1), (None, None, None, cat[g].to(dev), None), target=0.3) for g in range(G))
+    b = sum(ex._kl_loss_torch(p2[g].unsqueeze(-1), (None, None, None, cat[g].to(dev), None), target=0.3)
+            for g in range(G))
     a.backward()
     b.backward()
     np.testing.assert_allclose(a.item(), b.item(), rtol=1e-5)
     np.testing.assert_allclose(p1.grad.cpu().numpy(), p2.grad.cpu().numpy(), rtol=1e-4, atol=1e-9)
+
+
+def test_dropin_kl_loss_on_hip_matches_torch(dev):
+    """TempME.kl_loss (the drop-in call, explainer_new.py:432-453) on a device tensor runs tm_kl_loss: value
+    and gradient equal the torch formulation within 1e-5, for [B, W, 1] importances with host or device
+    category arrays."""
+    from tempme_amd import TempME
+    base = TI.build_model("uslegis").to(dev)
+    ex = TempME(base, "tgn", "uslegis_sampled", out_dim=40, hid_dim=64, device=dev,
+                null_model={k: (k + 1.0) / 90 for k in range(1, 13)}).to(dev)
+    gen = torch.Generator().manual_seed(3)
+    B, W = 25, 60
+    prob = torch.rand(B, W, 1, generator=gen)
+    prob[0, :4] = 1.0
+    cat = torch.randint(0, 12, (B, W, 1), generator=gen, dtype=torch.int32)
+    for c in (cat.numpy().astype(np.float64), cat.to(dev)):
+        p1 = prob.clone().to(dev).requires_grad_(True)
+        p2 = prob.clone().to(dev).requires_grad_(True)
+        a = ex.kl_loss(p1, (None, None, None, c, None), target=0.3)
+        b = ex._kl_loss_torch(p2, (None, None, None, c, None), target=0.3)
+        assert a.grad_fn is not None and "KLFn" in type(a.grad_fn).__name__, "the HIP kernel did not run"
+        a.backward()
+        b.backward()
+        np.testing.assert_allclose(a.item(), b.item(), rtol=1e-5)
+        np.testing.assert_allclose(p1.grad.cpu().numpy(), p2.grad.cpu().numpy(), rtol=1e-4, atol=1e-9)
 
 
 def test_batch_from_pack_gather_equals_index_select(dev):
