@@ -476,7 +476,7 @@ template <int NC, int NTT>
 struct GfIds {
     static constexpr int RPW = 4 / NTT, XS = 16 * NC + 4, C16 = 16 * NC;
     int lane, m, j, tt, rl, tok;
-    float *Xr, *Xw, *colm, *colr, *sew, *sval;
+    float *Xr, *Xw, *sew, *sval;
     __device__ __forceinline__ GfIds() {
         extern __shared__ float gm_lds[];
         const int t = gm_tid(), wave = t >> 6;
@@ -488,20 +488,18 @@ struct GfIds {
         tok = 16 * tt + m;
         Xr = gm_lds + rl * NTT * 16 * XS;                   // the row's image: token t at Xr + t * XS
         Xw = Xr + tt * 16 * XS;                             // this wave's 16 tokens
-        colm = gm_lds + 64 * XS + rl * 2 * C16;
-        colr = colm + C16;
-        sew = gm_lds + 64 * XS + RPW * 2 * C16 + rl * 64;
+        sew = gm_lds + 64 * XS + rl * 64;
         sval = sew + 32;
     }
 };
 
 // NC = channel tiles (C <= 16 NC), NTT = token tiles per row (N <= 16 NTT).  A workgroup of 4 waves takes
 // 4 / NTT rows, one wave per (row, token tile).  LDS plan (floats): X image [4 waves][16 tokens][XS] |
-// per row: token-LN column mean, rstd [2][16 NC] | ew_eff, valid [2][32].
+// per row: ew_eff, valid [2][32].
 template <int NC, int NTT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 13 ? 3 : 2))) gm_fused_kernel(GmArgs a) {
     typedef GfIds<NC, NTT> Ids;
-    constexpr int RPW = Ids::RPW, XS = Ids::XS, C16 = Ids::C16;
+    constexpr int RPW = Ids::RPW, XS = Ids::XS;
     extern __shared__ float gm_lds[];
     const int R = a.R, N = a.N, C = a.C, T = a.T;
     const bool has_ew = a.ew != nullptr;
@@ -509,7 +507,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 
         const int tid = gm_tid();
         if (tid < RPW * 32) {
             const int rl2 = tid >> 5, t = tid & 31, r2 = min((int)blockIdx.x * RPW + rl2, R - 1);
-            float *se = gm_lds + 64 * XS + RPW * 2 * C16 + rl2 * 64;
+            float *se = gm_lds + 64 * XS + rl2 * 64;
             const bool v = t < N && a.nid[(size_t)r2 * N + t] != 0;
             se[32 + t] = v ? 1.f : 0.f;
             // exp_src * mask (:154-155); without explanation weights the mixer multiplies by nothing (1.0)
@@ -608,25 +606,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 
     const int NH2 = ((a.HC + 31) / 32) * 2;   // hidden tiles, rounded up to pairs (zero fragments)
     for (int l = 0; l < a.L; ++l) {
         const float *const *w = a.lw + 12 * l;
-        // ---- token mixing (:289-297), as gm_embed_kernel: column statistics of X * ew over the row's
-        // tokens, then per 16-channel tile W1 (HT x N) against the normalised column and W2 (N x HT)
-        // against H on MFMA (H's K order permuted so it stays in the registers the first MFMA left it in)
-        {
-            const Ids I;
-            for (int c = I.tt * 64 + I.lane; c < C; c += 64 * NTT) {
-                float sm = 0.f;
-                for (int t = 0; t < N; ++t) sm += I.Xr[t * XS + c] * I.sew[t];
-                const float mean = sm / (float)N;
-                float q = 0.f;
-                for (int t = 0; t < N; ++t) {
-                    const float d = I.Xr[t * XS + c] * I.sew[t] - mean;
-                    q += d * d;
-                }
-                I.colm[c] = mean;
-                I.colr[c] = 1.f / sqrtf(q / (float)N + 1e-5f);
-            }
-        }
-        __syncthreads();
+        // ---- token mixing (:289-297): per 16-channel tile, the token LayerNorm's column statistics of
+        // X * ew in registers (a lane holds 4 NTT of the column's tokens; the 4 lane groups combine by two
+        // shuffles), then W1 (HT x N) against the normalised column and W2 (N x HT) against H on MFMA (H's
+        // K order permuted so it stays in the registers the first MFMA left it in).  A wave's channel tiles
+        // are its own, so no barrier separates the statistics from the mixing.
         {
             const Ids I;
             const int g = I.j, li = I.m, HT = a.HT;
@@ -651,14 +635,36 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 
             for (int nt = I.tt; nt < NC; nt += NTT) {
                 const int c = 16 * nt + li;
                 const bool cv = c < C;
-                const float mean = cv ? I.colm[c] : 0.f, rstd = cv ? I.colr[c] : 0.f;
+                float v[NTT][4], sm = 0.f;
+#pragma unroll
+                for (int G = 0; G < NTT; ++G)
+#pragma unroll
+                    for (int s2 = 0; s2 < 4; ++s2) {
+                        const int t = 16 * G + 4 * s2 + g;
+                        v[G][s2] = (cv && t < N) ? I.Xr[t * XS + c] * I.sew[t] : 0.f;
+                        sm += v[G][s2];
+                    }
+                sm += __shfl_xor(sm, 16);
+                sm += __shfl_xor(sm, 32);
+                const float mean = sm / (float)N;
+                float q = 0.f;
+#pragma unroll
+                for (int G = 0; G < NTT; ++G)
+#pragma unroll
+                    for (int s2 = 0; s2 < 4; ++s2) {
+                        const float d = v[G][s2] - mean;
+                        q += 16 * G + 4 * s2 + g < N ? d * d : 0.f;
+                    }
+                q += __shfl_xor(q, 16);
+                q += __shfl_xor(q, 32);
+                const float rstd = 1.f / sqrtf(q / (float)N + 1e-5f);
                 gmx4 hacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int G = 0; G < NTT; ++G)
 #pragma unroll
                     for (int s2 = 0; s2 < 4; ++s2) {
                         const int t = 16 * G + 4 * s2 + g;
-                        const float xn = (cv && t < N) ? (I.Xr[t * XS + c] * I.sew[t] - mean) * rstd * lg[G][s2] + lb[G][s2] : 0.f;
+                        const float xn = (cv && t < N) ? (v[G][s2] - mean) * rstd * lg[G][s2] + lb[G][s2] : 0.f;
                         hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[G][s2], xn, hacc, 0, 0, 0);
                     }
                 float h[4];
@@ -857,7 +863,7 @@ extern "C" int tm_gm_pack_a(const float *w, int32_t n_out, int32_t k, int32_t n_
 
 static inline size_t gm_fused_lds_bytes(int32_t C, int32_t N) {
     const size_t NC = gm_r16(C) / 16, XS = 16 * NC + 4, RPW = N > 16 ? 2 : 4;
-    return sizeof(float) * (64 * XS + RPW * (2 * 16 * NC + 64));
+    return sizeof(float) * (64 * XS + RPW * 64);
 }
 
 // the register-resident kernel's instances: channel tiles NC = C / 16 rounded up
