@@ -189,17 +189,24 @@ int tm_encoder_fwd_tab(const tm_weights *w, const float *n_feat, const float *e_
 
 /* ---------------------------------------------------------------- encoder training (device)
  * Training forward of TempME.forward (explainer_new.py:174-201) with dropout active: drop (nullable
- * = eval) holds uint8 keep-masks [n_walks][144]: columns 0..1 the attention weights alpha (:839),
- * 2..65 attention.MLP's hidden layer (:780), 66..141 MLP's hidden layer (:122); kept values are
- * scaled by drop_scale = 1/(1-p).  `workspace` (tm_encoder_workspace_bytes) keeps the event_gcn
- * outputs F for tm_encoder_bwd.  Replaces the autograd forward of temp_exp_main.py:605-607. */
+ * = eval) holds uint8 keep-masks [n_walks][DC], DC = (2 + h + hm) rounded up to 16 (144 for the
+ * default h = 64, hm = h + 12 with the category feature, hm = h without): columns 0..1 the attention
+ * weights alpha (:839), the next h attention.MLP's hidden layer (:780), the next hm MLP's hidden layer
+ * (:122); kept values are scaled by drop_scale = 1/(1-p).  With use_temporal_guidance=False (the plain
+ * Attention, :12-43, no dropout) the first 2 + h columns are ignored.  `workspace`
+ * (tm_encoder_workspace_bytes) keeps the event_gcn outputs F for tm_encoder_bwd.  Replaces the autograd
+ * forward of temp_exp_main.py:605-607.  Every constructor variant (tm_weights_create_ex /
+ * tm_weights_variant) whose dims tm_encoder_train_supported accepts. */
+int tm_encoder_train_supported(int32_t de, int32_t dn, int32_t hid_dim, int32_t if_cat_feature);
 int tm_encoder_train_fwd(const tm_weights *w, const float *n_feat, const float *e_feat, int32_t n_groups, int32_t B,
                          int32_t W, const int32_t *node6, const int32_t *eid3, const float *ts3, const int32_t *cat,
                          const double *cut, const float *cnt, const uint8_t *drop, float drop_scale, void *workspace,
                          float *out_imp, void *stream);
 
 /* Buffers of tm_encoder_bwd (caller-allocated device memory; n = n_walks, R = 3n walk positions,
- * KE = kev rounded up to 16 (kev = de + 3 + dn), DN = dn rounded up to 16).  Each layer's
+ * KE = kev rounded up to 16 (kev = de + 3 + dn), DN = dn rounded up to 16).  Shapes below for the
+ * default hid_dim h = 64 with the category feature: in general 64 -> h, 128 -> 2h, 76 -> hm and
+ * 80 -> KM = hm rounded up to 16.  Each layer's
  * (d pre-activation, input) row pair is written so the weight gradients are dW = dY^T X over all rows
  * and the bias gradients sum(dY) (the caller runs those GEMMs / reductions).  Padding columns are 0. */
 typedef struct {

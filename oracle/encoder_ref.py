@@ -32,9 +32,11 @@ def time_encode(sd, t):
 def forward(sd, n_feat, e_feat, node, eid, ts, cat, cut, edge_count, drop=None, scale=1.0, temporal=True,
             if_cat=True):
     """graphlet importance [B, W, 1] for one side (explainer_new.py:174-201).  temporal=False: the
-    plain ``Attention`` of use_temporal_guidance=False (explainer_new.py:12-43, no time scaling).  drop: optional keep-masks
-    [B, W, 144] of the training forward's three dropouts (alpha :839 -> cols 0..1, attention.MLP hidden :780
-    -> 2..65, MLP hidden :122 -> 66..141), kept values scaled by `scale` (training-mode parity).
+    plain ``Attention`` of use_temporal_guidance=False (explainer_new.py:12-43, no time scaling, no dropout).
+    drop: optional keep-masks [B, W, >= 2 + h + hm] of the training forward's three dropouts (alpha :839 ->
+    cols 0..1, attention.MLP hidden :780 -> the next h, MLP hidden :122 -> the next hm = MLP.0's width;
+    144 columns = 2..65 and 66..141 for the default h = 64), kept values scaled by `scale`
+    (training-mode parity); the plain Attention ignores the first 2 + h.
     Computes in the dtype of sd's tensors (fp32, or fp64 for gradient references)."""
     node = torch.as_tensor(np.asarray(node), dtype=torch.long)
     eid = torch.as_tensor(np.asarray(eid), dtype=torch.long)
@@ -45,6 +47,7 @@ def forward(sd, n_feat, e_feat, node, eid, ts, cat, cut, edge_count, drop=None, 
     n_feat, e_feat, cnt = n_feat.to(dty), e_feat.to(dty), cnt.to(dty)
     keep = None if drop is None else torch.as_tensor(np.asarray(drop)).to(dty) * scale
     B, W = eid.shape[0], eid.shape[1]
+    h, hm = sd["MLP.3.weight"].shape[0], sd["MLP.0.weight"].shape[0]
     ef = e_feat[eid]                                             # [B,W,3,de]
     dt = t[:, :, 2:3] - t                                        # relative to position 2
     tf = time_encode(sd, dt.reshape(B, -1).to(dty)).reshape(B, W, 3, -1)
@@ -68,12 +71,12 @@ def forward(sd, n_feat, e_feat, node, eid, ts, cat, cut, edge_count, drop=None, 
         tw = torch.exp(-diff / (diff.std() + 1e-6)).to(dty)
         scores = scores * (1.0 - 0.3 + 0.3 * tw)
     alpha = torch.softmax(scores, dim=-1)
-    if keep is not None:
+    if keep is not None and temporal:
         alpha = alpha * keep[..., 0:2]
     out = src + (alpha.unsqueeze(-1) * wq).sum(2)
     hid = torch.relu(_lin(sd, "attention.MLP.0", out))
-    if keep is not None:
-        hid = hid * keep[..., 2:66]
+    if keep is not None and temporal:
+        hid = hid * keep[..., 2:2 + h]
     # TemporalAwareAttention.MLP has a Dropout at index 2 (:777-782), Attention.MLP does not (:18)
     out = _lin(sd, "attention.MLP.3" if "attention.MLP.3.weight" in sd else "attention.MLP.2", hid)
     if if_cat:     # compute_catogory_feautres (:308-315); if_cat_feature=False feeds the attention output alone
@@ -83,7 +86,7 @@ def forward(sd, n_feat, e_feat, node, eid, ts, cat, cut, edge_count, drop=None, 
         x = out
     x = torch.relu(_lin(sd, "MLP.0", x))
     if keep is not None:
-        x = x * keep[..., 66:142]
+        x = x * keep[..., 2 + h:2 + h + hm]
     x = torch.relu(_lin(sd, "MLP.3", x))
     return torch.sigmoid(_lin(sd, "MLP.5", x))
 
@@ -131,15 +134,23 @@ def kl_loss(imp, cat, null_vec, target=0.3):
             + emp * torch.log(emp / (null + 1e-6) + 1e-6)).mean()
 
 
-def edge_importance_train(sd, e_feat, imp, walk_eid, walk_ts, sub_eid, keep1=None, keep2=None, sc1=1.0, sc2=1.0):
+def edge_importance_train(sd, e_feat, imp, walk_eid, walk_ts, sub_eid, keep1=None, keep2=None, sc1=1.0, sc2=1.0,
+                          dependency=True):
     """retrieve_edge_imp_node up to the gathered scatter-max (explainer_new.py:354-393), with explicit keep-masks
-    for edge_dependency_gcn's two dropouts ([B, 3W, h] / [B, 3W, h/2]); autograd-able in the weights' dtype.
-    Returns (p1 [B, N], p2 [B, N^2]) before beta_sample and the padding mask."""
-    dty = sd["edge_dependency_gcn.0.weight"].dtype
+    for edge_dependency_gcn's two dropouts ([B, 3W, h] / [B, 3W, h/2]); autograd-able in imp's dtype.
+    dependency=False: use_dependency_aware_sampling=False (no gate).  Returns (p1 [B, N], p2 [B, N^2])
+    before beta_sample and the padding mask."""
     B = imp.shape[0]
     ew = torch.as_tensor(np.asarray(walk_eid), dtype=torch.long).reshape(B, -1)
     tw = torch.as_tensor(np.asarray(walk_ts, dtype=np.float64)).float().reshape(B, -1)
     wimp = imp.repeat(1, 1, 3).view(B, -1)
+    i0 = torch.as_tensor(np.asarray(sub_eid[0]), dtype=torch.long)
+    i1 = torch.as_tensor(np.asarray(sub_eid[1]), dtype=torch.long)
+    n_e = int(max(ew.max(), i0.max(), i1.max()) + 1)
+    if not dependency:
+        dense = torch.zeros(B, n_e, dtype=wimp.dtype).scatter_reduce(-1, ew, wimp, "amax", include_self=False)
+        return torch.gather(dense, -1, i0), torch.gather(dense, -1, i1)
+    dty = sd["edge_dependency_gcn.0.weight"].dtype
     g = torch.cat([e_feat.to(dty)[ew], time_encode(sd, tw)], dim=-1)
     g = torch.relu(_lin(sd, "edge_dependency_gcn.0", g))
     if keep1 is not None:
@@ -149,8 +160,5 @@ def edge_importance_train(sd, e_feat, imp, walk_eid, walk_ts, sub_eid, keep1=Non
         g = g * (torch.as_tensor(np.asarray(keep2)).to(dty) * sc2)
     g = _lin(sd, "edge_dependency_gcn.6", g).squeeze(-1)
     wimp = wimp * (0.5 + 0.5 * torch.sigmoid(g))
-    i0 = torch.as_tensor(np.asarray(sub_eid[0]), dtype=torch.long)
-    i1 = torch.as_tensor(np.asarray(sub_eid[1]), dtype=torch.long)
-    n_e = int(max(ew.max(), i0.max(), i1.max()) + 1)
     dense = torch.zeros(B, n_e, dtype=wimp.dtype).scatter_reduce(-1, ew, wimp, "amax", include_self=False)
     return torch.gather(dense, -1, i0), torch.gather(dense, -1, i1)

@@ -170,35 +170,39 @@ __global__ void __launch_bounds__(256) gcn_kernel(EncW P, int64_t n_rows, const 
     });
 }
 
-// ------------------------------------------------------------------ attention head + final MLP: 32 walks per block
+// ------------------------------------------------------------------ attention head + final MLP: TR walks per block
+// TR = 32, or 16 where the 32-walk tiles exceed the LDS (hid_dim above 152)
+template <int TR>
 __global__ void __launch_bounds__(256) head_kernel(EncW P, int64_t n_walks, int64_t walks_per_group, int32_t W,
                                                    const float *__restrict__ F, const float *__restrict__ ts3,
                                                    const double *__restrict__ cut, const int32_t *__restrict__ cat,
                                                    const float *__restrict__ stdv, float *__restrict__ out,
                                                    const uint8_t *__restrict__ drop = nullptr, float dscale = 1.f) {
     // drop (training forward, nullable): keep-masks [n_walks][DROP_COLS]; kept values are scaled by dscale
+    static_assert(TR == 32 || TR == 16, "head_kernel: 16 or 32 walks per workgroup");
+    constexpr int MT1 = TR / 16, MT2 = TR / 8;   // row tiles of TR and 2 TR rows
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int h = P.h, D2 = 2 * h, LD = D2 + 8, LDM = r16(P.hm) + 8, LDH = r16(h) + 8;
     float *T = smem;                  // [64][LD]  positions 0,1 (rows p*32 + w)  -> later S, P
-    float *Q = T + 2 * TILE_ROWS * LD;  // [64][LD]  W2(tgt)
+    float *Q = T + 2 * TR * LD;  // [64][LD]  W2(tgt)
     float *S = T;                     // [32][LD]  position 2
-    float *Pp = T + TILE_ROWS * LD;   // [32][LD]  W1(src) -> later O
+    float *Pp = T + TR * LD;   // [32][LD]  W1(src) -> later O
     float *H1 = Q;                    // [32][LDH]
     float *X = S;                     // [32][LDM]
     float *M1 = Pp;                   // [32][LDM]
     float *M2 = Q;                    // [32][LDH]
-    __shared__ float s_score[TILE_ROWS * 2], s_tw[TILE_ROWS * 2], s_alpha[TILE_ROWS * 2];
-    __shared__ int32_t s_cat[TILE_ROWS];
-    const int64_t w0 = (int64_t)blockIdx.x * TILE_ROWS;
+    __shared__ float s_score[TR * 2], s_tw[TR * 2], s_alpha[TR * 2];
+    __shared__ int32_t s_cat[TR];
+    const int64_t w0 = (int64_t)blockIdx.x * TR;
     const int tid = threadIdx.x;
     // stage positions 0,1
-    for (int i = tid; i < 2 * TILE_ROWS * (D2 / 4); i += blockDim.x) {
-        const int row = i / (D2 / 4), c4 = i % (D2 / 4), p = row / TILE_ROWS, w = row % TILE_ROWS;
+    for (int i = tid; i < 2 * TR * (D2 / 4); i += blockDim.x) {
+        const int row = i / (D2 / 4), c4 = i % (D2 / 4), p = row / TR, w = row % TR;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (w0 + w < n_walks) v = reinterpret_cast<const float4 *>(F + ((w0 + w) * 3 + p) * D2)[c4];
         *reinterpret_cast<float4 *>(T + row * LD + 4 * c4) = v;
     }
-    if (tid < TILE_ROWS * 2) {
+    if (tid < TR * 2) {
         const int w = tid >> 1, p = tid & 1;
         const int64_t gw = w0 + w;
         float tw = 0.f;
@@ -210,22 +214,22 @@ __global__ void __launch_bounds__(256) head_kernel(EncW P, int64_t n_walks, int6
         }
         s_tw[tid] = tw;
     }
-    if (tid < TILE_ROWS) s_cat[tid] = (w0 + tid < n_walks) ? cat[w0 + tid] : -1;
+    if (tid < TR) s_cat[tid] = (w0 + tid < n_walks) ? cat[w0 + tid] : -1;
     __syncthreads();
-    gemm<4>(T, LD, P.w2, [&](int mt, int nt, floatx4 acc) {
+    gemm<MT2>(T, LD, P.w2, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) Q[erow(mt, r) * LD + c] = acc[r] + P.w2.b[c];
     });
     __syncthreads();
     // stage position 2 into S (T is dead)
-    for (int i = tid; i < TILE_ROWS * (D2 / 4); i += blockDim.x) {
+    for (int i = tid; i < TR * (D2 / 4); i += blockDim.x) {
         const int w = i / (D2 / 4), c4 = i % (D2 / 4);
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (w0 + w < n_walks) v = reinterpret_cast<const float4 *>(F + ((w0 + w) * 3 + 2) * D2)[c4];
         *reinterpret_cast<float4 *>(S + w * LD + 4 * c4) = v;
     }
     __syncthreads();
-    gemm<2>(S, LD, P.w1, [&](int mt, int nt, floatx4 acc) {
+    gemm<MT1>(S, LD, P.w1, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) Pp[erow(mt, r) * LD + c] = acc[r] + P.w1.b[c];
     });
@@ -233,23 +237,24 @@ __global__ void __launch_bounds__(256) head_kernel(EncW P, int64_t n_walks, int6
     // scores[w][p] = <W1 src, W2 tgt_p>, 4 lanes per dot product
     {
         const int pair = tid >> 2, sub = tid & 3, w = pair >> 1, p = pair & 1;
+        const int cend = w < TR ? D2 : 0;   // lane groups past TR walks sum nothing
         float s = 0.f;
-        for (int c = sub; c < D2; c += 4) s += Pp[w * LD + c] * Q[(p * TILE_ROWS + w) * LD + c];
+        for (int c = sub; c < cend; c += 4) s += Pp[w * LD + c] * Q[(p * TR + w) * LD + c];
         s += __shfl_xor(s, 1, 4);
         s += __shfl_xor(s, 2, 4);
-        if (sub == 0) {
+        if (sub == 0 && w < TR) {
             // scores * (1.0 - 0.3 + 0.3 * time_weight)   (:835-836)
             const float m = __fadd_rn(0.7f, __fmul_rn(0.3f, s_tw[pair]));
             s_score[pair] = s * m;
         }
     }
     __syncthreads();
-    if (tid < TILE_ROWS) {
+    if (tid < TR) {
         const float s0 = s_score[2 * tid], s1 = s_score[2 * tid + 1], mx = fmaxf(s0, s1);
         const float e0 = expf(s0 - mx), e1 = expf(s1 - mx), sum = e0 + e1;
         float a0 = e0 / sum, a1 = e1 / sum;
-        if (drop) {   // alpha = self.dropout(alpha)  (:839)
-            const uint8_t *dm = drop + (w0 + tid < n_walks ? w0 + tid : 0) * DROP_COLS + DROP_A;
+        if (drop && P.tg) {   // alpha = self.dropout(alpha)  (:839); the plain Attention has no dropout
+            const uint8_t *dm = drop + (w0 + tid < n_walks ? w0 + tid : 0) * drop_cols(h, P.hm) + DROP_A;
             a0 = dm[0] ? a0 * dscale : 0.f;
             a1 = dm[1] ? a1 * dscale : 0.f;
         }
@@ -258,58 +263,60 @@ __global__ void __launch_bounds__(256) head_kernel(EncW P, int64_t n_walks, int6
     }
     __syncthreads();
     // O = src + alpha . Wq   (into Pp)
-    for (int i = tid; i < TILE_ROWS * D2; i += blockDim.x) {
+    for (int i = tid; i < TR * D2; i += blockDim.x) {
         const int w = i / D2, c = i % D2;
-        const float o = s_alpha[2 * w] * Q[w * LD + c] + s_alpha[2 * w + 1] * Q[(TILE_ROWS + w) * LD + c];
+        const float o = s_alpha[2 * w] * Q[w * LD + c] + s_alpha[2 * w + 1] * Q[(TR + w) * LD + c];
         Pp[w * LD + c] = S[w * LD + c] + o;
     }
     __syncthreads();
-    gemm<2>(Pp, LD, P.a1, [&](int mt, int nt, floatx4 acc) {
+    gemm<MT1>(Pp, LD, P.a1, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) {
             const int row = erow(mt, r);
             float v = relu(acc[r] + P.a1.b[c]);
-            if (drop && !drop[(w0 + row < n_walks ? w0 + row : 0) * DROP_COLS + DROP_H + c]) v = 0.f;
-            else if (drop) v *= dscale;
+            if (drop && P.tg)   // TemporalAwareAttention.MLP's Dropout (:780); Attention.MLP has none (:18)
+                v = drop[(w0 + row < n_walks ? w0 + row : 0) * drop_cols(h, P.hm) + DROP_H + c] ? v * dscale : 0.f;
             H1[row * LDH + c] = v;
         }
     });
     __syncthreads();
     // X = [attention MLP out | one-hot(cat)]
-    gemm<2>(H1, LDH, P.a2, [&](int mt, int nt, floatx4 acc) {
+    gemm<MT1>(H1, LDH, P.a2, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) X[erow(mt, r) * LDM + c] = acc[r] + P.a2.b[c];
     });
     if (P.cat) {   // one-hot category after the attention output (compute_catogory_feautres :308-315)
-        for (int i = tid; i < TILE_ROWS * 16; i += blockDim.x) {
+        for (int i = tid; i < TR * 16; i += blockDim.x) {
             const int w = i >> 4, c = i & 15;
             X[w * LDM + h + c] = (c < 12 && s_cat[w] == c) ? 1.f : 0.f;
         }
     }
     __syncthreads();
-    gemm<2>(X, LDM, P.m1, [&](int mt, int nt, floatx4 acc) {
+    gemm<MT1>(X, LDM, P.m1, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) {
             const int row = erow(mt, r);
             float v = c < P.m1.nout ? relu(acc[r] + P.m1.b[c]) : 0.f;
-            if (drop && c < P.m1.nout) v = drop[(w0 + row < n_walks ? w0 + row : 0) * DROP_COLS + DROP_M + c] ? v * dscale : 0.f;
+            if (drop && c < P.m1.nout)
+                v = drop[(w0 + row < n_walks ? w0 + row : 0) * drop_cols(h, P.hm) + DROP_H + h + c] ? v * dscale : 0.f;
             M1[row * LDM + c] = v;
         }
     });
     __syncthreads();
-    gemm<2>(M1, LDM, P.m2, [&](int mt, int nt, floatx4 acc) {
+    gemm<MT1>(M1, LDM, P.m2, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) M2[erow(mt, r) * LDH + c] = relu(acc[r] + P.m2.b[c]);
     });
     __syncthreads();
     {
         const int w = tid >> 3, sub = tid & 7;
+        const int cend = w < TR ? h : 0;
         float s = 0.f;
-        for (int c = sub; c < h; c += 8) s += M2[w * LDH + c] * P.m3w[c];
+        for (int c = sub; c < cend; c += 8) s += M2[w * LDH + c] * P.m3w[c];
         s += __shfl_xor(s, 1, 8);
         s += __shfl_xor(s, 2, 8);
         s += __shfl_xor(s, 4, 8);
-        if (sub == 0 && w0 + w < n_walks) {
+        if (sub == 0 && w < TR && w0 + w < n_walks) {
             const float z = s + P.m3b[0];
             out[w0 + w] = 1.f / (1.f + expf(-z));
         }
@@ -1630,7 +1637,20 @@ static size_t gcn_lds(const EncW &P) {
     const int xsz = std::max(TILE_ROWS * (r16(P.kev) + 8), 2 * TILE_ROWS * (r16(P.h) + 8));
     return sizeof(float) * (xsz + 2 * TILE_ROWS * (r16(P.dn) + 8));
 }
-static size_t head_lds(const EncW &P) { return sizeof(float) * (4 * TILE_ROWS * (2 * P.h + 8)); }
+static size_t head_lds(const EncW &P, int tr) { return sizeof(float) * (4 * tr * (2 * P.h + 8)); }
+// walks per head_kernel workgroup: 32 where the tiles fit the LDS, else 16
+static int head_tr(const EncW &P) { return head_lds(P, 32) <= 160 * 1024 ? 32 : 16; }
+static void launch_head(const EncW &P, int64_t n_walks, int64_t walks_per_group, int32_t W, const float *F,
+                        const float *ts3, const double *cut, const int32_t *cat, const float *stdv, float *out,
+                        const uint8_t *drop, float dscale, hipStream_t s) {
+    const int tr = head_tr(P);
+    if (tr == 32)
+        head_kernel<32><<<dim3((unsigned)((n_walks + 31) / 32)), 256, head_lds(P, 32), s>>>(
+            P, n_walks, walks_per_group, W, F, ts3, cut, cat, stdv, out, drop, dscale);
+    else
+        head_kernel<16><<<dim3((unsigned)((n_walks + 15) / 16)), 256, head_lds(P, 16), s>>>(
+            P, n_walks, walks_per_group, W, F, ts3, cut, cat, stdv, out, drop, dscale);
+}
 
 template <int NQE, bool SEF = false, int Q0 = 0>
 static void launch_walk(const WalkArgs &a, unsigned blocks, hipStream_t s) {
@@ -1670,7 +1690,7 @@ static int encoder_fwd_impl(const tm_weights *w, const float *n_feat, const floa
     if (!n_feat || !e_feat || !node6 || !eid3 || !ts3 || !cat || !cut || !cnt || !workspace || !out_imp)
         return fail(TM_E_ARG, "tm_encoder_fwd: NULL pointer");
     const EncW &P = w->P;
-    const size_t lds_g = gcn_lds(P), lds_h = head_lds(P);
+    const size_t lds_g = gcn_lds(P);
     if (lds_g > 160 * 1024) return fail(TM_E_UNSUPPORTED, "tm_encoder_fwd: feature dims too large for LDS tile");
     hipStream_t s = S_(stream);
     float *F = reinterpret_cast<float *>(workspace);
@@ -1722,8 +1742,7 @@ static int encoder_fwd_impl(const tm_weights *w, const float *n_feat, const floa
     TM_CHECK_LAUNCH();
     prof_end("gcn_kernel", s, pe);
     pe = prof_begin(s);
-    head_kernel<<<dim3((unsigned)((n_walks + TILE_ROWS - 1) / TILE_ROWS)), 256, lds_h, s>>>(
-        P, n_walks, (int64_t)B * W, W, F, ts3, cut, cat, stdv, out_imp);
+    launch_head(P, n_walks, (int64_t)B * W, W, F, ts3, cut, cat, stdv, out_imp, nullptr, 1.f, s);
     TM_CHECK_LAUNCH();
     prof_end("head_kernel", s, pe);
     return TM_OK;
@@ -1741,7 +1760,7 @@ extern "C" int tm_encoder_train_fwd(const tm_weights *w, const float *n_feat, co
     if (!n_feat || !e_feat || !node6 || !eid3 || !ts3 || !cat || !cut || !cnt || !workspace || !out_imp)
         return fail(TM_E_ARG, "tm_encoder_train_fwd: NULL pointer");
     const EncW &P = w->P;
-    const size_t lds_g = gcn_lds(P), lds_h = head_lds(P);
+    const size_t lds_g = gcn_lds(P);
     if (lds_g > 160 * 1024) return fail(TM_E_UNSUPPORTED, "tm_encoder_train_fwd: feature dims too large for LDS tile");
     hipStream_t s = S_(stream);
     float *F = reinterpret_cast<float *>(workspace);
@@ -1757,8 +1776,7 @@ extern "C" int tm_encoder_train_fwd(const tm_weights *w, const float *n_feat, co
     TM_CHECK_LAUNCH();
     prof_end("gcn_kernel", s, pe);
     pe = prof_begin(s);
-    head_kernel<<<dim3((unsigned)((n_walks + TILE_ROWS - 1) / TILE_ROWS)), 256, lds_h, s>>>(
-        P, n_walks, (int64_t)B * W, W, F, ts3, cut, cat, stdv, out_imp, drop, drop_scale);
+    launch_head(P, n_walks, (int64_t)B * W, W, F, ts3, cut, cat, stdv, out_imp, drop, drop_scale, s);
     TM_CHECK_LAUNCH();
     prof_end("head_kernel", s, pe);
     return TM_OK;

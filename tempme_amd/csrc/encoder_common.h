@@ -154,11 +154,15 @@ struct EncWT {
     Lin d1T, d2T;   // dependency gate: d1T holds only the time-feature columns of edge_dependency_gcn.0
 };
 
-// Dropout keep-masks of the training forward, uint8 [n_walks][DROP_COLS]: attention weights alpha
-// (TemporalAwareAttention.dropout, explainer_new.py:839), the attention MLP's hidden layer (:780) and
-// the final MLP's hidden layer (:122); 1 = kept (scaled by 1/(1-p)), 0 = dropped.
-constexpr int DROP_A = 0, DROP_H = 2, DROP_M = DROP_H + HID, DROP_COLS = 144;
-static_assert(DROP_M + HID + 12 <= DROP_COLS, "dropout mask columns");
+// Dropout keep-masks of the training forward, uint8 [n_walks][drop_cols(h, hm)]: attention weights alpha
+// (TemporalAwareAttention.dropout, explainer_new.py:839) in columns 0..1, the attention MLP's hidden layer
+// (:780) in the h columns from DROP_H and the final MLP's hidden layer (:122) in the hm columns from
+// DROP_H + h; 1 = kept (scaled by 1/(1-p)), 0 = dropped.  Rows padded to 16 columns (144 for the default
+// hid_dim 64 with the category feature).  The plain Attention (use_temporal_guidance=False, :12-43) has
+// neither of the first two dropouts: their columns are ignored then.
+constexpr int DROP_A = 0, DROP_H = 2;
+__host__ __device__ constexpr int drop_cols(int h, int hm) { return r16(DROP_H + h + hm); }
+static_assert(drop_cols(HID, HID + 12) == 144, "dropout mask columns");
 
 }  // namespace tmk
 

@@ -215,164 +215,183 @@ __global__ void __launch_bounds__(256) fold2_kernel(FoldIn F, const double *__re
 }
 
 // ------------------------------------------------------------------ head backward
+// Row strides for hid_dim h and the final MLP's width hm (h + 12 with the category feature, h without);
+// KM = r16(hm).  The default constructor: h = 64, KM = 80.
 struct HeadBwdOut {
     float *imp;     // [n]          recomputed sigmoid output (nullable)
     float *dlogit;  // [n]          d logit                         (MLP.5: with M2)
-    float *M2;      // [n][64]      relu(MLP.3 ...)
-    float *dM2;     // [n][64]      d MLP.3 pre-activation          (with M1d)
-    float *M1d;     // [n][80]      dropout(relu(MLP.0 x))
-    float *dM1;     // [n][80]      d MLP.0 pre-activation          (with X)
-    float *X;       // [n][80]      [attention out | one-hot(cat)]
-    float *dY2;     // [n][64]      d attention.MLP.3 output        (with H1d)
-    float *H1d;     // [n][64]      dropout(relu(attention.MLP.0 O))
-    float *dH1;     // [n][64]      d attention.MLP.0 pre-activation (with O)
-    float *O;       // [n][128]     src + sum alpha' Wq
-    float *dP;      // [n][128]     d W1(src)                       (with F[:, 2])
-    float *dQ;      // [2][n][128]  d W2(tgt_k)                     (with F[:, k])
-    float *dF;      // [n][3][128]  d [U_s | U_t] per walk position
+    float *M2;      // [n][h]       relu(MLP.3 ...)
+    float *dM2;     // [n][h]       d MLP.3 pre-activation          (with M1d)
+    float *M1d;     // [n][KM]      dropout(relu(MLP.0 x))
+    float *dM1;     // [n][KM]      d MLP.0 pre-activation          (with X)
+    float *X;       // [n][KM]      [attention out | one-hot(cat)]  (attention out alone without the category)
+    float *dY2;     // [n][h]       d attention.MLP.3 output        (with H1d)
+    float *H1d;     // [n][h]       dropout(relu(attention.MLP.0 O))
+    float *dH1;     // [n][h]       d attention.MLP.0 pre-activation (with O)
+    float *O;       // [n][2h]      src + sum alpha' Wq
+    float *dP;      // [n][2h]      d W1(src)                       (with F[:, 2])
+    float *dQ;      // [2][n][2h]   d W2(tgt_k)                     (with F[:, k])
+    float *dF;      // [n][3][2h]   d [U_s | U_t] per walk position
 };
 
+// LDS of head_bwd_kernel<TR> (TR walks per workgroup): Qb [2TR][LD], Wp / Ob [TR][LD], H1 / M2 [TR][LDH],
+// Xb / M1 [TR][LDM]
+__host__ __device__ constexpr size_t head_bwd_lds_floats(int h, int hm, int TR) {
+    return (size_t)TR * (4 * (2 * h + 8) + 2 * (h + 8) + 2 * (r16(hm) + 8));
+}
+
+// TR = 32 walks per workgroup, or 16 where the 32-walk tiles exceed the LDS (hid_dim > 64 or so)
+template <int TR>
 __global__ void __launch_bounds__(256) head_bwd_kernel(EncW P, EncWT T, int64_t n_walks, int64_t walks_per_group,
                                                        int32_t W, const float *__restrict__ F,
                                                        const float *__restrict__ ts3, const double *__restrict__ cut,
                                                        const int32_t *__restrict__ cat, const float *__restrict__ stdv,
                                                        const uint8_t *__restrict__ drop, float dscale,
                                                        const float *__restrict__ d_imp, HeadBwdOut o) {
+    static_assert(TR == 32 || TR == 16, "head_bwd_kernel: 16 or 32 walks per workgroup");
+    constexpr int MT1 = TR / 16, MT2 = TR / 8;   // row tiles of TR and 2 TR rows
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    constexpr int D2 = 2 * HID, LD = D2 + 8, LDH = HID + 8, KM = r16(HID + 12), LDM = KM + 8;
-    float *Qb = smem;              // [64][LD]  W2(F0 | F1)            -> dQ
-    float *Wp = Qb + 64 * LD;      // [32][LD]  W1(F2)                 -> dP      (Wp..Ob: F0|F1 staging)
-    float *Ob = Wp + 32 * LD;      // [32][LD]  F2 -> O                -> dO
-    float *H1 = Ob + 32 * LD;      // [32][LDH] H1d                    -> dH1
-    float *Xb = H1 + 32 * LDH;     // [32][LDM] X                      -> dY2
-    float *M1 = Xb + 32 * LDM;     // [32][LDM] M1d                    -> dM1
-    float *M2 = M1 + 32 * LDM;     // [32][LDH] M2                     -> dM2
+    const int h = P.h, D2 = 2 * h, LD = D2 + 8, LDH = h + 8, KM = r16(P.hm), LDM = KM + 8;
+    const int dcols = drop_cols(h, P.hm), DM = DROP_H + h;
+    float *Qb = smem;              // [2TR][LD] W2(F0 | F1)            -> dQ
+    float *Wp = Qb + 2 * TR * LD;  // [TR][LD]  W1(F2)                 -> dP      (Wp..Ob: F0|F1 staging)
+    float *Ob = Wp + TR * LD;      // [TR][LD]  F2 -> O                -> dO
+    float *H1 = Ob + TR * LD;      // [TR][LDH] H1d                    -> dH1
+    float *Xb = H1 + TR * LDH;     // [TR][LDM] X                      -> dY2
+    float *M1 = Xb + TR * LDM;     // [TR][LDM] M1d                    -> dM1
+    float *M2 = M1 + TR * LDM;     // [TR][LDH] M2                     -> dM2
     __shared__ float s_mult[64], s_score[64], s_alpha[64], s_alphad[64], s_dsr[64], s_dl[32];
     __shared__ int32_t s_cat[32];
-    const int64_t w0 = (int64_t)blockIdx.x * TILE_ROWS;
+    const int64_t w0 = (int64_t)blockIdx.x * TR;
     const int tid = threadIdx.x;
-    const float kscale = drop ? dscale : 1.f;   // d(dropout(relu(z)))/dz where the output is > 0
+    const float kscale = drop ? dscale : 1.f;              // d(dropout(relu(z)))/dz where the output is > 0
+    const float kscale_h = drop && P.tg ? dscale : 1.f;    // attention.MLP hidden: no Dropout in plain Attention
     auto valid = [&](int w) { return w0 + w < n_walks; };
     auto keep = [&](int w, int col) -> float {
         if (!drop) return 1.f;
-        return (valid(w) && drop[(w0 + w) * DROP_COLS + col]) ? dscale : 0.f;
+        return (valid(w) && drop[(w0 + w) * dcols + col]) ? dscale : 0.f;
     };
+    auto keep_att = [&](int w, int col) -> float { return P.tg ? keep(w, col) : 1.f; };
 
     // ---- forward again: Q = W2 [F0; F1], Wp = W1 F2, scores, softmax, dropout, O
     float *Tb = Wp;
-    for (int i = tid; i < 2 * TILE_ROWS * (D2 / 4); i += blockDim.x) {
-        const int row = i / (D2 / 4), c4 = i % (D2 / 4), p = row / TILE_ROWS, w = row % TILE_ROWS;
+    for (int i = tid; i < 2 * TR * (D2 / 4); i += blockDim.x) {
+        const int row = i / (D2 / 4), c4 = i % (D2 / 4), p = row / TR, w = row % TR;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (valid(w)) v = reinterpret_cast<const float4 *>(F + ((w0 + w) * 3 + p) * D2)[c4];
         *reinterpret_cast<float4 *>(Tb + row * LD + 4 * c4) = v;
     }
-    if (tid < 2 * TILE_ROWS) {
+    if (tid < 2 * TR) {
         const int w = tid >> 1, p = tid & 1;
-        float tw = 0.f;
-        if (valid(w)) {
+        float tw = 1.f;   // plain Attention: the scores unscaled
+        if (P.tg && valid(w)) {
             const int64_t gw = w0 + w, g = gw / walks_per_group, b = (gw % walks_per_group) / W;
             const float c = (float)cut[g * (walks_per_group / W) + b];
             tw = expf(-fabsf(c - ts3[gw * 3 + p]) / (stdv[g] + 1e-6f));
         }
-        s_mult[tid] = __fadd_rn(0.7f, __fmul_rn(0.3f, tw));   // 1.0 - 0.3 + 0.3 * time_weight (:835-836)
+        s_mult[tid] = P.tg ? __fadd_rn(0.7f, __fmul_rn(0.3f, tw)) : 1.f;   // 1.0 - 0.3 + 0.3 * time_weight (:835-836)
     }
-    if (tid < TILE_ROWS) s_cat[tid] = valid(tid) ? cat[w0 + tid] : -1;
+    if (tid < TR) s_cat[tid] = valid(tid) ? cat[w0 + tid] : -1;
     __syncthreads();
-    gemm<4>(Tb, LD, P.w2, [&](int mt, int nt, floatx4 acc) {
+    gemm<MT2>(Tb, LD, P.w2, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) Qb[erow(mt, r) * LD + c] = acc[r] + P.w2.b[c];
     });
     __syncthreads();
-    for (int i = tid; i < TILE_ROWS * (D2 / 4); i += blockDim.x) {
+    for (int i = tid; i < TR * (D2 / 4); i += blockDim.x) {
         const int w = i / (D2 / 4), c4 = i % (D2 / 4);
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (valid(w)) v = reinterpret_cast<const float4 *>(F + ((w0 + w) * 3 + 2) * D2)[c4];
         *reinterpret_cast<float4 *>(Ob + w * LD + 4 * c4) = v;
     }
     __syncthreads();
-    gemm<2>(Ob, LD, P.w1, [&](int mt, int nt, floatx4 acc) {
+    gemm<MT1>(Ob, LD, P.w1, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) Wp[erow(mt, r) * LD + c] = acc[r] + P.w1.b[c];
     });
     __syncthreads();
-    {
+    {   // 4 lanes per (walk, position); groups past TR walks sum nothing
         const int pair = tid >> 2, sub = tid & 3, w = pair >> 1, p = pair & 1;
+        const int cend = w < TR ? D2 : 0;
         float s = 0.f;
-        for (int c = sub; c < D2; c += 4) s += Wp[w * LD + c] * Qb[(p * TILE_ROWS + w) * LD + c];
+        for (int c = sub; c < cend; c += 4) s += Wp[w * LD + c] * Qb[(p * TR + w) * LD + c];
         s += __shfl_xor(s, 1, 4);
         s += __shfl_xor(s, 2, 4);
-        if (sub == 0) s_score[pair] = s * s_mult[pair];
+        if (sub == 0 && w < TR) s_score[pair] = s * s_mult[pair];
     }
     __syncthreads();
-    if (tid < TILE_ROWS) {
+    if (tid < TR) {
         const float s0 = s_score[2 * tid], s1 = s_score[2 * tid + 1], mx = fmaxf(s0, s1);
         const float e0 = expf(s0 - mx), e1 = expf(s1 - mx), sum = e0 + e1;
         const float a0 = e0 / sum, a1 = e1 / sum;
         s_alpha[2 * tid] = a0;
         s_alpha[2 * tid + 1] = a1;
-        s_alphad[2 * tid] = a0 * keep(tid, DROP_A);
-        s_alphad[2 * tid + 1] = a1 * keep(tid, DROP_A + 1);
+        s_alphad[2 * tid] = a0 * keep_att(tid, DROP_A);
+        s_alphad[2 * tid + 1] = a1 * keep_att(tid, DROP_A + 1);
     }
     __syncthreads();
-    for (int i = tid; i < TILE_ROWS * D2; i += blockDim.x) {
+    for (int i = tid; i < TR * D2; i += blockDim.x) {
         const int w = i / D2, c = i % D2;
-        const float a = s_alphad[2 * w] * Qb[w * LD + c] + s_alphad[2 * w + 1] * Qb[(TILE_ROWS + w) * LD + c];
+        const float a = s_alphad[2 * w] * Qb[w * LD + c] + s_alphad[2 * w + 1] * Qb[(TR + w) * LD + c];
         const float v = Ob[w * LD + c] + a;
         Ob[w * LD + c] = v;
         if (valid(w)) o.O[(w0 + w) * D2 + c] = v;
     }
     __syncthreads();
-    gemm<2>(Ob, LD, P.a1, [&](int mt, int nt, floatx4 acc) {
+    gemm<MT1>(Ob, LD, P.a1, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) {
             const int row = erow(mt, r);
-            const float v = relu(acc[r] + P.a1.b[c]) * keep(row, DROP_H + c);
+            const float v = relu(acc[r] + P.a1.b[c]) * keep_att(row, DROP_H + c);
             H1[row * LDH + c] = v;
-            if (valid(row)) o.H1d[(w0 + row) * HID + c] = v;
+            if (valid(row)) o.H1d[(w0 + row) * h + c] = v;
         }
     });
     __syncthreads();
-    gemm<2>(H1, LDH, P.a2, [&](int mt, int nt, floatx4 acc) {
+    gemm<MT1>(H1, LDH, P.a2, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) Xb[erow(mt, r) * LDM + c] = acc[r] + P.a2.b[c];
     });
-    for (int i = tid; i < TILE_ROWS * 16; i += blockDim.x) {
-        const int w = i >> 4, c = i & 15;
-        Xb[w * LDM + HID + c] = (c < 12 && s_cat[w] == c) ? 1.f : 0.f;
+    if (P.cat) {   // one-hot category after the attention output (:308-315)
+        for (int i = tid; i < TR * 16; i += blockDim.x) {
+            const int w = i >> 4, c = i & 15;
+            Xb[w * LDM + h + c] = (c < 12 && s_cat[w] == c) ? 1.f : 0.f;
+        }
     }
     __syncthreads();
-    for (int i = tid; i < TILE_ROWS * KM; i += blockDim.x) {
+    for (int i = tid; i < TR * KM; i += blockDim.x) {
         const int w = i / KM, c = i % KM;
         if (valid(w)) o.X[(w0 + w) * KM + c] = Xb[w * LDM + c];
     }
-    gemm<2>(Xb, LDM, P.m1, [&](int mt, int nt, floatx4 acc) {
+    gemm<MT1>(Xb, LDM, P.m1, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) {
             const int row = erow(mt, r);
-            const float v = c < P.m1.nout ? relu(acc[r] + P.m1.b[c]) * keep(row, DROP_M + c) : 0.f;
+            const float v = c < P.m1.nout ? relu(acc[r] + P.m1.b[c]) * keep(row, DM + c) : 0.f;
             M1[row * LDM + c] = v;
             if (valid(row)) o.M1d[(w0 + row) * KM + c] = v;
         }
     });
     __syncthreads();
-    gemm<2>(M1, LDM, P.m2, [&](int mt, int nt, floatx4 acc) {
+    gemm<MT1>(M1, LDM, P.m2, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) {
             const int row = erow(mt, r);
             const float v = relu(acc[r] + P.m2.b[c]);
             M2[row * LDH + c] = v;
-            if (valid(row)) o.M2[(w0 + row) * HID + c] = v;
+            if (valid(row)) o.M2[(w0 + row) * h + c] = v;
         }
     });
     __syncthreads();
     {
         const int w = tid >> 3, sub = tid & 7;
+        const int cend = w < TR ? h : 0;
         float s = 0.f;
-        for (int c = sub; c < HID; c += 8) s += M2[w * LDH + c] * P.m3w[c];
+        for (int c = sub; c < cend; c += 8) s += M2[w * LDH + c] * P.m3w[c];
         s += __shfl_xor(s, 1, 8);
         s += __shfl_xor(s, 2, 8);
         s += __shfl_xor(s, 4, 8);
-        if (sub == 0) {
+        if (sub == 0 && w < TR) {
             float dl = 0.f;
             if (valid(w)) {
                 const float y = 1.f / (1.f + expf(-(s + P.m3b[0])));
@@ -386,14 +405,14 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(EncW P, EncWT T, int64_t 
     __syncthreads();
 
     // ---- backward through the MLP head
-    for (int i = tid; i < TILE_ROWS * HID; i += blockDim.x) {
-        const int w = i / HID, c = i % HID;
+    for (int i = tid; i < TR * h; i += blockDim.x) {
+        const int w = i / h, c = i % h;
         const float v = M2[w * LDH + c] > 0.f ? s_dl[w] * P.m3w[c] : 0.f;
         M2[w * LDH + c] = v;
-        if (valid(w)) o.dM2[(w0 + w) * HID + c] = v;
+        if (valid(w)) o.dM2[(w0 + w) * h + c] = v;
     }
     __syncthreads();
-    gemm<2>(M2, LDH, T.m2T, [&](int mt, int nt, floatx4 acc) {   // d M1d = dM2 P3
+    gemm<MT1>(M2, LDH, T.m2T, [&](int mt, int nt, floatx4 acc) {   // d M1d = dM2 P3
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) {
             const int row = erow(mt, r);
@@ -403,57 +422,58 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(EncW P, EncWT T, int64_t 
         }
     });
     __syncthreads();
-    gemm<2>(M1, LDM, T.m1T, [&](int mt, int nt, floatx4 acc) {   // d X = dM1 P0; keep the attention part
+    gemm<MT1>(M1, LDM, T.m1T, [&](int mt, int nt, floatx4 acc) {   // d X = dM1 P0; keep the attention part
         const int c = ecol(nt);
-        if (c < HID) {
+        if (c < h) {
             for (int r = 0; r < 4; ++r) {
                 const int row = erow(mt, r);
                 Xb[row * LDM + c] = acc[r];
-                if (valid(row)) o.dY2[(w0 + row) * HID + c] = acc[r];
+                if (valid(row)) o.dY2[(w0 + row) * h + c] = acc[r];
             }
         }
     });
     __syncthreads();
-    gemm<2>(Xb, LDM, T.a2T, [&](int mt, int nt, floatx4 acc) {   // d H1d = dY2 A3
+    gemm<MT1>(Xb, LDM, T.a2T, [&](int mt, int nt, floatx4 acc) {   // d H1d = dY2 A3
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) {
             const int row = erow(mt, r);
-            const float v = H1[row * LDH + c] > 0.f ? acc[r] * kscale : 0.f;
+            const float v = H1[row * LDH + c] > 0.f ? acc[r] * kscale_h : 0.f;
             H1[row * LDH + c] = v;
-            if (valid(row)) o.dH1[(w0 + row) * HID + c] = v;
+            if (valid(row)) o.dH1[(w0 + row) * h + c] = v;
         }
     });
     __syncthreads();
-    gemm<2>(H1, LDH, T.a1T, [&](int mt, int nt, floatx4 acc) {   // d O = dH1 A0
+    gemm<MT1>(H1, LDH, T.a1T, [&](int mt, int nt, floatx4 acc) {   // d O = dH1 A0
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) Ob[erow(mt, r) * LD + c] = acc[r];
     });
     __syncthreads();
     {   // d alpha'_k = dO . Wq_k
         const int pair = tid >> 2, sub = tid & 3, w = pair >> 1, p = pair & 1;
+        const int cend = w < TR ? D2 : 0;
         float s = 0.f;
-        for (int c = sub; c < D2; c += 4) s += Ob[w * LD + c] * Qb[(p * TILE_ROWS + w) * LD + c];
+        for (int c = sub; c < cend; c += 4) s += Ob[w * LD + c] * Qb[(p * TR + w) * LD + c];
         s += __shfl_xor(s, 1, 4);
         s += __shfl_xor(s, 2, 4);
-        if (sub == 0) s_score[pair] = s;
+        if (sub == 0 && w < TR) s_score[pair] = s;
     }
     __syncthreads();
-    if (tid < TILE_ROWS) {   // dropout, softmax and temporal-scaling backward
+    if (tid < TR) {   // dropout, softmax and temporal-scaling backward
         const float a0 = s_alpha[2 * tid], a1 = s_alpha[2 * tid + 1];
-        const float g0 = s_score[2 * tid] * keep(tid, DROP_A), g1 = s_score[2 * tid + 1] * keep(tid, DROP_A + 1);
+        const float g0 = s_score[2 * tid] * keep_att(tid, DROP_A), g1 = s_score[2 * tid + 1] * keep_att(tid, DROP_A + 1);
         const float dot = g0 * a0 + g1 * a1;
         s_dsr[2 * tid] = (g0 - dot) * a0 * s_mult[2 * tid];
         s_dsr[2 * tid + 1] = (g1 - dot) * a1 * s_mult[2 * tid + 1];
     }
     __syncthreads();
-    for (int i = tid; i < TILE_ROWS * D2; i += blockDim.x) {
+    for (int i = tid; i < TR * D2; i += blockDim.x) {
         const int w = i / D2, c = i % D2;
-        const float q0 = Qb[w * LD + c], q1 = Qb[(TILE_ROWS + w) * LD + c], wp = Wp[w * LD + c], dO = Ob[w * LD + c];
+        const float q0 = Qb[w * LD + c], q1 = Qb[(TR + w) * LD + c], wp = Wp[w * LD + c], dO = Ob[w * LD + c];
         const float ds0 = s_dsr[2 * w], ds1 = s_dsr[2 * w + 1];
         const float dq0 = s_alphad[2 * w] * dO + ds0 * wp, dq1 = s_alphad[2 * w + 1] * dO + ds1 * wp;
         const float dp = ds0 * q0 + ds1 * q1;
         Qb[w * LD + c] = dq0;
-        Qb[(TILE_ROWS + w) * LD + c] = dq1;
+        Qb[(TR + w) * LD + c] = dq1;
         Wp[w * LD + c] = dp;
         if (valid(w)) {
             o.dQ[(w0 + w) * D2 + c] = dq0;
@@ -462,14 +482,14 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(EncW P, EncWT T, int64_t 
         }
     }
     __syncthreads();
-    gemm<4>(Qb, LD, T.w2T, [&](int mt, int nt, floatx4 acc) {   // dF0, dF1 = dQ W2
+    gemm<MT2>(Qb, LD, T.w2T, [&](int mt, int nt, floatx4 acc) {   // dF0, dF1 = dQ W2
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) {
-            const int row = erow(mt, r), p = row / TILE_ROWS, w = row % TILE_ROWS;
+            const int row = erow(mt, r), p = row / TR, w = row % TR;
             if (valid(w)) o.dF[((w0 + w) * 3 + p) * D2 + c] = acc[r];
         }
     });
-    gemm<2>(Wp, LD, T.w1T, [&](int mt, int nt, floatx4 acc) {   // dF2 = dO + dP W1
+    gemm<MT1>(Wp, LD, T.w1T, [&](int mt, int nt, floatx4 acc) {   // dF2 = dO + dP W1
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) {
             const int row = erow(mt, r);
@@ -496,7 +516,7 @@ __global__ void __launch_bounds__(256) gcn_bwd_kernel(EncW P, EncWT T, int64_t n
                                                       const float *__restrict__ dF, GcnBwdOut o) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int de = P.de, dn = P.dn, kev = P.kev, kev16 = r16(kev), dn16 = r16(dn);
-    const int ldx = kev16 + 8, ldab = dn16 + 8, ldh = HID + 8;
+    const int h = P.h, ldx = kev16 + 8, ldab = dn16 + 8, ldh = h + 8;
     const int xsz = max(TILE_ROWS * ldx, 2 * TILE_ROWS * ldh);
     float *X = smem;                                     // [32][ldx]  event features -> dU [64][ldh]
     float *dU = X;
@@ -563,9 +583,9 @@ __global__ void __launch_bounds__(256) gcn_bwd_kernel(EncW P, EncWT T, int64_t n
         }
     });
     __syncthreads();
-    for (int i = tid; i < 2 * TILE_ROWS * HID; i += blockDim.x) {   // dU: d U_s rows 0..31, d U_t rows 32..63
-        const int row = i / HID, c = i % HID, r = row % TILE_ROWS, half = row / TILE_ROWS;
-        dU[row * ldh + c] = valid(r) ? dF[(row0 + r) * (2 * HID) + half * HID + c] : 0.f;
+    for (int i = tid; i < 2 * TILE_ROWS * h; i += blockDim.x) {   // dU: d U_s rows 0..31, d U_t rows 32..63
+        const int row = i / h, c = i % h, r = row % TILE_ROWS, half = row / TILE_ROWS;
+        dU[row * ldh + c] = valid(r) ? dF[(row0 + r) * (2 * h) + half * h + c] : 0.f;
     }
     gemm<4>(AB, ldab, P.g1, [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
@@ -573,7 +593,7 @@ __global__ void __launch_bounds__(256) gcn_bwd_kernel(EncW P, EncWT T, int64_t n
             const int row = erow(mt, r), rr = row % TILE_ROWS, half = row / TILE_ROWS;
             const float v = relu(acc[r] + P.g1.b[c]);
             Hb[row * ldh + c] = v;
-            if (valid(rr)) o.H[((row0 + rr) * 2 + half) * HID + c] = v;
+            if (valid(rr)) o.H[((row0 + rr) * 2 + half) * h + c] = v;
         }
     });
     __syncthreads();
@@ -583,7 +603,7 @@ __global__ void __launch_bounds__(256) gcn_bwd_kernel(EncW P, EncWT T, int64_t n
             const int row = erow(mt, r), rr = row % TILE_ROWS, half = row / TILE_ROWS;
             const float v = Hb[row * ldh + c] > 0.f ? acc[r] : 0.f;
             Hb[row * ldh + c] = v;
-            if (valid(rr)) o.dZ[((row0 + rr) * 2 + half) * HID + c] = v;
+            if (valid(rr)) o.dZ[((row0 + rr) * 2 + half) * h + c] = v;
         }
     });
     __syncthreads();
@@ -776,14 +796,18 @@ __global__ void __launch_bounds__(256) gate_train_fwd_kernel(EncW P, int64_t n_r
                                                              const uint8_t *__restrict__ keep2, float sc1, float sc2,
                                                              ExplIO o) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    constexpr int H2 = HID / 2;
-    const int de = P.de, kdep = P.kdep, kd16 = r16(kdep), ldx = kd16 + 8, ldg = HID + 8, ldg2 = H2 + 8;
+    const int h = P.h, H2 = h / 2;
+    const int de = P.de, kdep = P.kdep, kd16 = r16(kdep), ldx = kd16 + 8, ldg = r16(h) + 8, ldg2 = r16(H2) + 8;
     float *X = smem, *G1 = X + TILE_ROWS * ldx, *G2 = G1 + TILE_ROWS * ldg;
     __shared__ int32_t s_e[TILE_ROWS];
     __shared__ float s_t[TILE_ROWS];
     const int64_t r0 = (int64_t)blockIdx.x * TILE_ROWS;
     const int tid = threadIdx.x;
     auto valid = [&](int r) { return r0 + r < n_rows; };
+    if (!P.dep) {   // use_dependency_aware_sampling=False: no gate (:366-386 skipped), walk_imp = graphlet_imp
+        if (tid < TILE_ROWS && valid(tid)) o.gate[r0 + tid] = 1.f;
+        return;
+    }
     if (tid < TILE_ROWS) {
         s_e[tid] = valid(tid) ? eid3[r0 + tid] : 0;
         s_t[tid] = valid(tid) ? ts3[r0 + tid] : 0.f;    // raw event time (:371)
@@ -806,9 +830,9 @@ __global__ void __launch_bounds__(256) gate_train_fwd_kernel(EncW P, int64_t n_r
         for (int r = 0; r < 4; ++r) {
             const int row = erow(mt, r);
             float v = relu(acc[r] + P.d1.b[c]);
-            if (keep1) v = (valid(row) && keep1[(r0 + row) * HID + c]) ? v * sc1 : 0.f;
+            if (keep1) v = (valid(row) && keep1[(r0 + row) * h + c]) ? v * sc1 : 0.f;
             G1[row * ldg + c] = v;
-            if (valid(row)) o.G1[(r0 + row) * HID + c] = v;
+            if (valid(row)) o.G1[(r0 + row) * h + c] = v;
         }
     });
     __syncthreads();
@@ -817,14 +841,14 @@ __global__ void __launch_bounds__(256) gate_train_fwd_kernel(EncW P, int64_t n_r
         for (int r = 0; r < 4; ++r) {
             const int row = erow(mt, r);
             float v = relu(acc[r] + P.d2.b[c]);
-            if (keep2) v = (valid(row) && keep2[(r0 + row) * H2 + c]) ? v * sc2 : 0.f;
+            if (keep2) v = (valid(row) && c < H2 && keep2[(r0 + row) * H2 + c]) ? v * sc2 : 0.f;
             G2[row * ldg2 + c] = v;
-            if (valid(row)) o.G2[(r0 + row) * H2 + c] = v;
+            if (valid(row) && c < H2) o.G2[(r0 + row) * H2 + c] = v;
         }
     });
     __syncthreads();
     const int r = tid >> 3, sub = tid & 7;
-    const float sv = gate_logit_lds(G2 + r * ldg2, P.d3w, sub);
+    const float sv = gate_logit_lds(G2 + r * ldg2, P.d3w, sub, H2);
     if (sub == 0 && valid(r)) {
         const float z = sv + P.d3b[0];
         o.z[r0 + r] = z;
@@ -944,8 +968,8 @@ __global__ void __launch_bounds__(256) explain_train_bwd_kernel(int32_t W, int32
 __global__ void __launch_bounds__(256) gate_train_bwd_kernel(EncW P, EncWT T, int64_t n_rows, const uint8_t *keep1,
                                                              const uint8_t *keep2, float sc1, float sc2, ExplIO o) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    constexpr int H2 = HID / 2;
-    const int dn = P.dn, dn16 = r16(dn), ldg = HID + 8, ldg2 = H2 + 8;
+    const int h = P.h, H2 = h / 2, H2p = r16(H2);
+    const int dn = P.dn, dn16 = r16(dn), ldg = r16(h) + 8, ldg2 = H2p + 8;
     float *G1 = smem, *G2 = G1 + TILE_ROWS * ldg;
     __shared__ float s_dz[TILE_ROWS], s_t[TILE_ROWS];
     const int64_t r0 = (int64_t)blockIdx.x * TILE_ROWS;
@@ -963,17 +987,17 @@ __global__ void __launch_bounds__(256) gate_train_bwd_kernel(EncW P, EncWT T, in
         s_dz[tid] = dz;
         s_t[tid] = t;
     }
-    for (int i = tid; i < TILE_ROWS * HID; i += blockDim.x) {
-        const int r = i / HID, c = i % HID;
-        G1[r * ldg + c] = valid(r) ? o.G1[(r0 + r) * HID + c] : 0.f;
+    for (int i = tid; i < TILE_ROWS * h; i += blockDim.x) {
+        const int r = i / h, c = i % h;
+        G1[r * ldg + c] = valid(r) ? o.G1[(r0 + r) * h + c] : 0.f;
     }
     __syncthreads();
-    for (int i = tid; i < TILE_ROWS * H2; i += blockDim.x) {   // dG2 = dz d3 * [G2 > 0] * keep
-        const int r = i / H2, c = i % H2;
-        const float g2 = valid(r) ? o.G2[(r0 + r) * H2 + c] : 0.f;
+    for (int i = tid; i < TILE_ROWS * H2p; i += blockDim.x) {   // dG2 = dz d3 * [G2 > 0] * keep (K padding 0)
+        const int r = i / H2p, c = i % H2p;
+        const float g2 = (valid(r) && c < H2) ? o.G2[(r0 + r) * H2 + c] : 0.f;
         const float v = g2 > 0.f ? s_dz[r] * P.d3w[c] * k2 : 0.f;
         G2[r * ldg2 + c] = v;
-        if (valid(r)) o.dG2[(r0 + r) * H2 + c] = v;
+        if (valid(r) && c < H2) o.dG2[(r0 + r) * H2 + c] = v;
     }
     __syncthreads();
     gemm<2>(G2, ldg2, T.d2T, [&](int mt, int nt, floatx4 acc) {   // dG1 = (dG2 W.3) * [G1 > 0] * keep
@@ -982,7 +1006,7 @@ __global__ void __launch_bounds__(256) gate_train_bwd_kernel(EncW P, EncWT T, in
             const int row = erow(mt, r);
             const float v = G1[row * ldg + c] > 0.f ? acc[r] * k1 : 0.f;
             G1[row * ldg + c] = v;
-            if (valid(row)) o.dG1[(r0 + row) * HID + c] = v;
+            if (valid(row)) o.dG1[(r0 + row) * h + c] = v;
         }
     });
     __syncthreads();
@@ -1109,14 +1133,32 @@ void train_packs_free(tm_weights *w) {
     w->tbuf = nullptr;
 }
 
-static size_t head_bwd_lds() {
-    constexpr int D2 = 2 * HID, LD = D2 + 8, LDH = HID + 8, LDM = r16(HID + 12) + 8;
-    return sizeof(float) * (128 * LD + 2 * TILE_ROWS * LDH + 2 * TILE_ROWS * LDM);
+// walks per head_bwd_kernel workgroup: 32 where the tiles fit the LDS, else 16; 0 = no instance
+static int head_bwd_tr(const EncW &P) {
+    if (sizeof(float) * head_bwd_lds_floats(P.h, P.hm, 32) <= 160 * 1024) return 32;
+    if (sizeof(float) * head_bwd_lds_floats(P.h, P.hm, 16) <= 160 * 1024) return 16;
+    return 0;
 }
 static size_t gcn_bwd_lds(const EncW &P) {
-    const int ldx = r16(P.kev) + 8, ldab = r16(P.dn) + 8, ldh = HID + 8;
+    const int ldx = r16(P.kev) + 8, ldab = r16(P.dn) + 8, ldh = r16(P.h) + 8;
     const size_t xsz = std::max(TILE_ROWS * ldx, 2 * TILE_ROWS * ldh);
     return sizeof(float) * (xsz + 2 * TILE_ROWS * ldab + 2 * TILE_ROWS * ldh) + 2 * TILE_ROWS * r16(P.dn);
+}
+
+// Whether the training kernels (tm_encoder_train_fwd / _bwd, tm_explain_train_fwd / _bwd) have an
+// instance for these encoder dims: hid_dim a multiple of 16 up to 256 whose tiles fit the LDS.
+extern "C" int tm_encoder_train_supported(int32_t de, int32_t dn, int32_t h, int32_t cat) {
+    if (de <= 0 || dn <= 0 || h <= 0 || h % 16 || h > 256) return 0;
+    EncW P{};
+    P.de = de;
+    P.dn = dn;
+    P.kev = de + 3 + dn;
+    P.kdep = de + dn;
+    P.h = h;
+    P.hm = cat ? h + 12 : h;
+    const size_t lim = 160 * 1024;
+    const size_t gate = sizeof(float) * TILE_ROWS * (r16(P.kdep) + 8 + r16(h) + 8 + r16(h / 2) + 8);
+    return head_bwd_tr(P) && gcn_bwd_lds(P) <= lim && gate <= lim ? 1 : 0;
 }
 
 extern "C" int tm_encoder_bwd(const tm_weights *w, const float *n_feat, const float *e_feat, int32_t n_groups,
@@ -1135,16 +1177,21 @@ extern "C" int tm_encoder_bwd(const tm_weights *w, const float *n_feat, const fl
         return fail(TM_E_ARG, "tm_encoder_bwd: NULL output buffer");
     if (!w->tbuf) return fail(TM_E_ARG, "tm_encoder_bwd: weights have no transposed packs");
     const EncW &P = w->P;
-    const size_t lh = head_bwd_lds(), lg = gcn_bwd_lds(P);
-    if (lh > 160 * 1024 || lg > 160 * 1024) return fail(TM_E_UNSUPPORTED, "tm_encoder_bwd: LDS budget exceeded");
+    const int tr = head_bwd_tr(P);
+    const size_t lh = sizeof(float) * head_bwd_lds_floats(P.h, P.hm, tr), lg = gcn_bwd_lds(P);
+    if (P.h % 16 || !tr || lg > 160 * 1024) return fail(TM_E_UNSUPPORTED, "tm_encoder_bwd: LDS budget exceeded");
     hipStream_t s = S_(stream);
     const float *F = reinterpret_cast<const float *>(workspace);
-    const float *stdv = F + n_walks * 3 * 2 * HID;
+    const float *stdv = F + n_walks * 3 * 2 * P.h;
     HeadBwdOut ho{io->imp, io->dlogit, io->M2, io->dM2, io->M1d, io->dM1, io->X, io->dY2, io->H1d, io->dH1, io->O,
                   io->dP,  io->dQ,     io->dF};
     hipEvent_t pe = prof_begin(s);
-    head_bwd_kernel<<<dim3((unsigned)((n_walks + TILE_ROWS - 1) / TILE_ROWS)), 256, lh, s>>>(
-        P, w->T, n_walks, (int64_t)B * W, W, F, ts3, cut, cat, stdv, drop, drop_scale, d_imp, ho);
+    if (tr == 32)
+        head_bwd_kernel<32><<<dim3((unsigned)((n_walks + 31) / 32)), 256, lh, s>>>(
+            P, w->T, n_walks, (int64_t)B * W, W, F, ts3, cut, cat, stdv, drop, drop_scale, d_imp, ho);
+    else
+        head_bwd_kernel<16><<<dim3((unsigned)((n_walks + 15) / 16)), 256, lh, s>>>(
+            P, w->T, n_walks, (int64_t)B * W, W, F, ts3, cut, cat, stdv, drop, drop_scale, d_imp, ho);
     TM_CHECK_LAUNCH();
     prof_end("head_bwd_kernel", s, pe);
     const int64_t n_rows = n_walks * 3;
@@ -1290,7 +1337,8 @@ extern "C" int tm_explain_train_fwd(const tm_weights *w, const float *e_feat, in
     hipStream_t s = S_(stream);
     const int64_t R = rows * 3 * W;
     ExplIO o{io->X, io->G1, io->G2, io->z, io->gate, io->d_gate, io->dz, io->dG2, io->dG1, io->g, io->t};
-    const size_t lds = sizeof(float) * (TILE_ROWS * (r16(P.kdep) + 8) + TILE_ROWS * (HID + 8) + TILE_ROWS * (HID / 2 + 8));
+    const size_t lds = sizeof(float) * (TILE_ROWS * (r16(P.kdep) + 8) + TILE_ROWS * (r16(P.h) + 8) + TILE_ROWS * (r16(P.h / 2) + 8));
+    if (lds > 160 * 1024) return fail(TM_E_UNSUPPORTED, "tm_explain_train_fwd: LDS budget exceeded");
     hipEvent_t pe = prof_begin(s);
     gate_train_fwd_kernel<<<dim3((unsigned)((R + TILE_ROWS - 1) / TILE_ROWS)), 256, lds, s>>>(
         P, R, e_feat, eid3, ts3, keep1, keep2, scale1, scale2, o);
@@ -1331,14 +1379,17 @@ extern "C" int tm_explain_train_bwd(const tm_weights *w, int32_t n_groups, int32
             W, N, hb, eid3, imp, io->gate, sub1_eid, sub2_eid, dp1, dp2, d_imp, io->d_gate);
         TM_CHECK_LAUNCH();
         prof_end("explain_train_bwd_kernel", s, pe);
-        const size_t lds = sizeof(float) * (TILE_ROWS * (HID + 8) + TILE_ROWS * (HID / 2 + 8));
-        pe = prof_begin(s);
-        gate_train_bwd_kernel<<<dim3((unsigned)((R64 + TILE_ROWS - 1) / TILE_ROWS)), 256, lds, s>>>(
-            P, w->T, R64, keep1, keep2, scale1, scale2, o);
-        TM_CHECK_LAUNCH();
-        prof_end("gate_train_bwd_kernel", s, pe);
+        if (P.dep) {   // no gate without dependency-aware sampling: d imp is the whole backward
+            const size_t lds = sizeof(float) * (TILE_ROWS * (r16(P.h) + 8) + TILE_ROWS * (r16(P.h / 2) + 8));
+            pe = prof_begin(s);
+            gate_train_bwd_kernel<<<dim3((unsigned)((R64 + TILE_ROWS - 1) / TILE_ROWS)), 256, lds, s>>>(
+                P, w->T, R64, keep1, keep2, scale1, scale2, o);
+            TM_CHECK_LAUNCH();
+            prof_end("gate_train_bwd_kernel", s, pe);
+        }
     }
-    const int R = (int)R64, h = w->h, dn = w->dn, kdep = P.kdep;
+    // without the gate its tensors and the time encoder get no gradient from this path: zero rows below
+    const int R = P.dep ? (int)R64 : 0, h = w->h, dn = w->dn, kdep = P.kdep;
     const tm_wgrad_job jobs[] = {
         {io->dG1, io->X, h, r16(kdep), h, kdep, R},        // edge_dependency_gcn.0
         {io->dG2, io->G1, h / 2, h, h / 2, h, R},          // .3

@@ -259,15 +259,20 @@ class TempME(nn.Module):
         return ok
 
     def _hip_ok(self):
-        """The training kernels (f3): the default constructor only."""
-        ok = (self.use_temporal_guidance and self.use_dependency_aware_sampling and self.if_cat
-              and self.hid_dim == 64)
+        """The training kernels (f3) cover every constructor variant (use_temporal_guidance,
+        use_dependency_aware_sampling, if_cat_feature) for the dims tm_encoder_train_supported accepts:
+        hid_dim a multiple of 16 whose tiles fit the LDS (every hid_dim up to 192 at Enron / Wikipedia
+        feature dims)."""
+        key = (self.edge_dim, self.node_dim, self.hid_dim, bool(self.if_cat))
+        c = self.__dict__.get("_train_ok")
+        if c is None or c[0] != key:
+            ok = self._hip_eval_ok() and bool(L.lib().tm_encoder_train_supported(*[int(x) for x in key]))
+            c = self.__dict__["_train_ok"] = (key, ok)
+        ok = c[1]
         if not ok and not getattr(self, "_warned_torch_train", False):
-            warnings.warn("TempME(use_temporal_guidance=%s, use_dependency_aware_sampling=%s, if_cat_feature=%s, "
-                          "hid_dim=%d): the HIP training kernels cover the default constructor; gradients run "
-                          "through the torch-op formulation on the device"
-                          % (self.use_temporal_guidance, self.use_dependency_aware_sampling, self.if_cat,
-                             self.hid_dim), RuntimeWarning, stacklevel=3)
+            warnings.warn("TempME(if_cat_feature=%s, hid_dim=%d, edge_dim=%d, node_dim=%d): no HIP training kernel "
+                          "instance for these dims; gradients run through the torch-op formulation on the device"
+                          % (self.if_cat, self.hid_dim, self.edge_dim, self.node_dim), RuntimeWarning, stacklevel=3)
             self._warned_torch_train = True
         return ok
 
@@ -421,15 +426,22 @@ class TempME(nn.Module):
         ws = self._weight_list()
         return ws[:20] + ws[-2:]
 
+    def dropout_cols(self):
+        """Columns of a dropout keep-mask row (include/tempme.h, tm_encoder_train_fwd): alpha 2, attention.MLP
+        hidden h, MLP hidden mlp_dim, rounded up to 16 -- 144 for the default constructor."""
+        return -(-(2 + self.hid_dim + self.mlp_dim) // 16) * 16
+
     def dropout_masks(self, n_walks):
         """Keep-masks of the three dropouts TempME.forward applies in training (explainer_new.py:839 alpha,
-        :780 attention.MLP hidden, :122 MLP hidden), uint8 [n_walks, 144] from torch's device RNG, or
-        None when they are inactive (eval mode or p = 0)."""
+        :780 attention.MLP hidden, :122 MLP hidden), uint8 [n_walks, dropout_cols()] from torch's device
+        RNG, or None when they are inactive (eval mode or p = 0).  The plain Attention
+        (use_temporal_guidance=False) has no alpha / hidden dropout: the kernels ignore those columns."""
         p = self.dropout_p
         if not self.training or p <= 0:
             return None, 1.0
         dev = self._dev()
-        return torch.empty(n_walks, 144, dtype=torch.uint8, device=dev).bernoulli_(1.0 - p), 1.0 / (1.0 - p)
+        return (torch.empty(n_walks, self.dropout_cols(), dtype=torch.uint8, device=dev).bernoulli_(1.0 - p),
+                1.0 / (1.0 - p))
 
     def forward_groups(self, node6, eid3, ts3, cat, cut, cnt, n_groups, B, W, drop=None, drop_scale=1.0,
                        use_module_dropout=True):
@@ -467,7 +479,7 @@ class TempME(nn.Module):
         R = 3 * n
         de, dn, h = self.edge_dim, self.node_dim, self.hid_dim
         kev = de + 3 + dn
-        KE, DN, KM = -(-kev // 16) * 16, -(-dn // 16) * 16, -(-(h + 12) // 16) * 16
+        KE, DN, KM = -(-kev // 16) * 16, -(-dn // 16) * 16, -(-self.mlp_dim // 16) * 16
         e = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
         b = dict(imp=None, dlogit=e(n), M2=e(n, h), dM2=e(n, h), M1d=e(n, KM), dM1=e(n, KM), X=e(n, KM), dY2=e(n, h),
                  H1d=e(n, h), dH1=e(n, h), O=e(n, 2 * h), dP=e(n, 2 * h), dQ=e(2, n, 2 * h), dF=e(n, 3, 2 * h),
@@ -493,7 +505,7 @@ class TempME(nn.Module):
         """Keep-masks of edge_dependency_gcn's Dropout(1.5p) [n_pos, h] and Dropout(p) [n_pos, h/2]
         (explainer_new.py:136-140) from torch's device RNG, or None in eval mode."""
         p = self.dropout_p
-        if not self.training or p <= 0:
+        if not self.training or p <= 0 or not self.use_dependency_aware_sampling:
             return None, None, 1.0, 1.0
         dev = self._dev()
         p1 = min(1.5 * p, 1.0)

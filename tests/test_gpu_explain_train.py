@@ -101,3 +101,75 @@ def test_explain_backward_matches_autograd(dev, de, G, B, N, train):
             assert ga.shape == gr.shape, k
             assert float((ga - gr).norm()) <= tol * float(gr.norm()) + 1e-9, (dty, k, float((ga - gr).norm()),
                                                                                float(gr.norm()))
+
+
+@pytest.mark.parametrize("var", ["nodep", "h32", "h128"])
+def test_explain_backward_variants_match_autograd(dev, var):
+    """use_dependency_aware_sampling=False (no gate: d imp through the scatter-max alone, no gradient to the
+    time encoder from this path) and the gate at hid_dim 32 / 128."""
+    from tempme_amd import TempME
+    from tempme_amd.explainer import _ExplainFn
+    kw = {"nodep": dict(hid_dim=64, use_dependency_aware_sampling=False), "h32": dict(hid_dim=32),
+          "h128": dict(hid_dim=128)}[var]
+    h = kw.pop("hid_dim")
+    rng = np.random.RandomState(h)
+    de, G, B, N = 32, 2, 6, 10
+    V, E, W = 50, 400, 3 * N
+    n_feat = rng.uniform(0, 1, (V + 1, 172)).astype(np.float32)
+    e_feat = rng.uniform(0, 1, (E + 1, de)).astype(np.float32)
+    n_feat[0] = 0
+    e_feat[0] = 0
+    eid3 = rng.randint(0, E + 1, (G, B, W, 3)).astype(np.int32)
+    ts3 = rng.uniform(0, 1e6, (G, B, W, 3)).astype(np.float32)
+    dup = rng.uniform(size=(G, B, W)) < 0.3
+    eid3[..., 2][dup] = eid3[..., 0][dup]
+    ts3[..., 2][dup] = ts3[..., 0][dup]
+    s1e = rng.randint(0, E + 1, (G, B, N)).astype(np.int32)
+    s1e[..., : N // 2] = eid3[..., : N // 2, 0]
+    s2e = rng.randint(0, E + 1, (G, B, N * N)).astype(np.int32)
+    m2 = min(N * N // 2, 3 * W)
+    s2e[..., :m2] = eid3.reshape(G, B, -1)[..., :m2]
+    imp_np = rng.uniform(0.05, 0.95, (G, B, W)).astype(np.float32)
+    torch.manual_seed(3)
+    ex = TempME(_Base(n_feat, e_feat), "tgn", "synth", 40, h, device=dev,
+                null_model={k: 1 / 12 for k in range(1, 13)}, **kw).to(dev)
+    ex.train(True)
+    assert ex._hip_ok(), var
+    dep = ex.use_dependency_aware_sampling
+    masks = ex.gate_dropout_masks(G * B * 3 * W)
+    assert (masks[0] is None) == (not dep)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    imp = t(imp_np).requires_grad_(True)
+    p1, p2 = _ExplainFn.apply(ex, (t(eid3), t(ts3), t(s1e), t(s2e), masks, G, B, W, N), imp.reshape(-1),
+                              *ex._gate_params())
+    w1 = torch.from_numpy(rng.uniform(-1, 1, G * B * N).astype(np.float32))
+    w2 = torch.from_numpy(rng.uniform(-1, 1, G * B * N * N).astype(np.float32))
+    ((p1 * w1.to(dev)).sum() + (p2 * w2.to(dev)).sum()).backward()
+    names = GATE if dep else GATE[-2:]
+    named = dict(ex.named_parameters())
+    got = {k: named[k].grad.detach().cpu().double() for k in names}
+    sd = {k: v.detach().cpu().float().requires_grad_(k in names) for k, v in ex.state_dict().items()}
+    imp_ref = torch.from_numpy(imp_np).requires_grad_(True)
+    k1 = None if masks[0] is None else masks[0].cpu().numpy().reshape(G, B, 3 * W, -1)
+    k2 = None if masks[1] is None else masks[1].cpu().numpy().reshape(G, B, 3 * W, -1)
+    loss = 0
+    for g in range(G):
+        r1, r2 = er.edge_importance_train(sd, torch.from_numpy(e_feat), imp_ref[g].unsqueeze(-1), eid3[g], ts3[g],
+                                          [s1e[g], s2e[g]], None if k1 is None else k1[g],
+                                          None if k2 is None else k2[g], masks[2], masks[3], dependency=dep)
+        np.testing.assert_allclose(p1.detach().cpu().numpy().reshape(G, B, N)[g], r1.detach().numpy(), rtol=1e-5,
+                                   atol=1e-6)
+        np.testing.assert_allclose(p2.detach().cpu().numpy().reshape(G, B, N * N)[g], r2.detach().numpy(),
+                                   rtol=1e-5, atol=1e-6)
+        loss = loss + (r1.reshape(-1) * w1.reshape(G, -1)[g]).sum() + (r2.reshape(-1) * w2.reshape(G, -1)[g]).sum()
+    loss.backward()
+    gi = imp_ref.grad.double().reshape(-1)
+    assert float((imp.grad.detach().cpu().double().reshape(-1) - gi).norm()) <= 2e-4 * float(gi.norm()) + 1e-9
+    for k in names:
+        ga = got[k]
+        if not dep:      # the time encoder is not on this path without the gate
+            assert float(ga.abs().max()) == 0.0, k
+            continue
+        gr = sd[k].grad.double()
+        assert ga.shape == gr.shape, k
+        assert float((ga - gr).norm()) <= 2e-5 * float(gr.norm()) + 1e-9, (var, k)
