@@ -582,24 +582,60 @@ struct WalkLay {
 };
 
 // out[t] += W tile t * x over the K steps [0, NQ) of a pack with NQL K steps at float offset BASE (the
-// caller initialises out: bias rows from LDS, a table row, or zero); weights streamed PF fragments ahead
+// caller initialises out: bias rows from LDS, a table row, or zero); weights streamed PFP fragments ahead.
+// Fragments go in tile pairs (t, t+1) with the K steps inside and the pair's two fragments' MFMAs
+// interleaved, so no MFMA waits on the one before it (v_mfma_f32_16x16x4_f32: 32-cycle issue, 40-cycle
+// dependent-accumulator latency); an odd last tile runs alone.  Each tile still accumulates its K steps
+// in the same order (the results do not change).
+#ifndef TM_PFP
+#define TM_PFP 4
+#endif
+constexpr int PFP = TM_PFP;
+template <int NTO, int NQ>
+struct PairOrder {   // fragment i of the pair order -> (tile, K step)
+    static constexpr int NP = NTO / 2, NPF = 2 * NP * NQ;
+    static constexpr int t(int i) { return i < NPF ? 2 * (i / (2 * NQ)) + (i & 1) : NTO - 1; }
+    static constexpr int q(int i) { return i < NPF ? (i % (2 * NQ)) / 2 : i - NPF; }
+};
+
 template <int NTO, int NQ, int NQL, int BASE>
 __device__ __forceinline__ void cgemm(__amdgpu_buffer_rsrc_t wr, const floatx4 (&x)[NQ], floatx4 (&o)[NTO]) {
+    using O = PairOrder<NTO, NQ>;
     const int vo = lane_id() * 16;
-    constexpr int N = NTO * NQ, D = PF < N ? PF : N;
+    constexpr int N = NTO * NQ, D = PFP < N ? PFP : N;
+    auto off = [](int i) { return BASE / 4 + (O::t(i) * NQL + O::q(i)) * 64; };
     float4 buf[D];
 #pragma unroll
-    for (int i = 0; i < D; ++i) buf[i] = wload(wr, vo, BASE / 4 + ((i / NQ) * NQL + i % NQ) * 64);
+    for (int i = 0; i < D; ++i) buf[i] = wload(wr, vo, off(i));
 #pragma unroll
-    for (int i = 0; i < N; ++i) {
-        const int t = i / NQ, q = i % NQ;
-        const float4 w = buf[i % D];
-        if (i + D < N) buf[i % D] = wload(wr, vo, BASE / 4 + (((i + D) / NQ) * NQL + (i + D) % NQ) * 64);
-        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, x[q].x, o[t], 0, 0, 0);
-        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, x[q].y, o[t], 0, 0, 0);
-        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, x[q].z, o[t], 0, 0, 0);
-        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, x[q].w, o[t], 0, 0, 0);
+    for (int k = 0; k < O::NP * NQ; ++k) {
+        const int i = 2 * k, t = O::t(i), q = O::q(i);
+        const float4 w0 = buf[i % D];
+        if (i + D < N) buf[i % D] = wload(wr, vo, off(i + D));
+        const float4 w1 = buf[(i + 1) % D];
+        if (i + 1 + D < N) buf[(i + 1) % D] = wload(wr, vo, off(i + 1 + D));
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0.x, x[q].x, o[t], 0, 0, 0);
+        o[t + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.x, x[q].x, o[t + 1], 0, 0, 0);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0.y, x[q].y, o[t], 0, 0, 0);
+        o[t + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.y, x[q].y, o[t + 1], 0, 0, 0);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0.z, x[q].z, o[t], 0, 0, 0);
+        o[t + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.z, x[q].z, o[t + 1], 0, 0, 0);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0.w, x[q].w, o[t], 0, 0, 0);
+        o[t + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.w, x[q].w, o[t + 1], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (NTO % 2) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int i = O::NPF + q;
+            const float4 w = buf[i % D];
+            if (i + D < N) buf[i % D] = wload(wr, vo, off(i + D));
+            o[NTO - 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, x[q].x, o[NTO - 1], 0, 0, 0);
+            o[NTO - 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, x[q].y, o[NTO - 1], 0, 0, 0);
+            o[NTO - 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, x[q].z, o[NTO - 1], 0, 0, 0);
+            o[NTO - 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, x[q].w, o[NTO - 1], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
     }
 }
 
@@ -883,7 +919,7 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
     {
         const int vo = lane_id() * 16;
         constexpr int nq = NQE;
-        constexpr int N = NTD * (NQE - Q0), D = PF;
+        constexpr int N = NTD * (NQE - Q0), D = PFP;
         constexpr int EVF4 = LY::EV / 4;
         float4 buf[D];
 #pragma unroll
@@ -939,21 +975,47 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
                     const float wq[4] = {w4.x, w4.y, w4.z, w4.w}, pq[4] = {p4.x, p4.y, p4.z, p4.w};
                     constexpr bool pure_next_ok = ETAB;   // table mode: steps >= Q0 + 2 hold only time features
                     floatx4 xn = xq;
-#pragma unroll
-                    for (int t = 0; t < NTD; ++t) {
-                        const int i = (q - Q0) * NTD + t;
-                        const float4 w = buf[i % D];
-                        if (i + D < N) buf[i % D] = wload(wr, vo, EVF4 + (((i + D) % NTD) * nq + Q0 + (i + D) / NTD) * 64);
-                        L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, xq.x, L[t], 0, 0, 0);
-                        L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, xq.y, L[t], 0, 0, 0);
-                        L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, xq.z, L[t], 0, 0, 0);
-                        L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, xq.w, L[t], 0, 0, 0);
+                    auto gen = [&](int t) {
                         if (q + 1 < NQE && t < 4) {
                             if (pure_next_ok && q + 1 >= Q0 + 2)
                                 xn[t] = gen_one<ETAB, true>(q + 1, t, wq[t], pq[t], ef, g, de, dt, c0, c1, c2);
                             else
                                 xn[t] = gen_one<ETAB, false>(q + 1, t, wq[t], pq[t], ef, g, de, dt, c0, c1, c2);
                         }
+                    };
+                    auto wnext = [&](int i) {   // fragment i + D of the ring into slot i % D
+                        if (i + D < N) buf[i % D] = wload(wr, vo, EVF4 + (((i + D) % NTD) * nq + Q0 + (i + D) / NTD) * 64);
+                    };
+                    // tile pairs with interleaved MFMAs (no MFMA waits on its predecessor); an odd last tile alone
+#pragma unroll
+                    for (int t = 0; t + 1 < NTD; t += 2) {
+                        const int i = (q - Q0) * NTD + t;
+                        const float4 w0 = buf[i % D];
+                        wnext(i);
+                        const float4 w1 = buf[(i + 1) % D];
+                        wnext(i + 1);
+                        L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0.x, xq.x, L[t], 0, 0, 0);
+                        L[t + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.x, xq.x, L[t + 1], 0, 0, 0);
+                        L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0.y, xq.y, L[t], 0, 0, 0);
+                        L[t + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.y, xq.y, L[t + 1], 0, 0, 0);
+                        L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0.z, xq.z, L[t], 0, 0, 0);
+                        L[t + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.z, xq.z, L[t + 1], 0, 0, 0);
+                        L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0.w, xq.w, L[t], 0, 0, 0);
+                        L[t + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.w, xq.w, L[t + 1], 0, 0, 0);
+                        gen(t);
+                        gen(t + 1);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                    if constexpr (NTD % 2) {
+                        constexpr int t = NTD - 1;
+                        const int i = (q - Q0) * NTD + t;
+                        const float4 w = buf[i % D];
+                        wnext(i);
+                        L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, xq.x, L[t], 0, 0, 0);
+                        L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, xq.y, L[t], 0, 0, 0);
+                        L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, xq.z, L[t], 0, 0, 0);
+                        L[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, xq.w, L[t], 0, 0, 0);
+                        gen(t);
                         __builtin_amdgcn_sched_barrier(0);
                     }
                     xq = xn;
