@@ -468,6 +468,15 @@ int64_t tm_gm_packed_floats(int32_t n_out, int32_t k);
 /* W [n_out, k] row-major (nn.Linear.weight) -> MFMA B-operand fragments */
 int tm_gm_pack(const float *w, int32_t n_out, int32_t k, float *packed, void *stream);
 int tm_gm_embed(const tm_gm_embed_args *a, void *stream);
+/* Backward of tm_gm_embed with respect to the explanation weights (the explainer's training signal through a
+ * frozen base GraphMixer, temp_exp_main.py:614-632 with base_type 'graphmixer'; GM/graphmixer.py:142-193,
+ * :273-315): d_ew [R, N] from d_x_mean [R, C] and d_node_out [R, D]; zero on padding neighbours.  `a` as for
+ * tm_gm_embed with a->ew set, every weight pack by tm_gm_pack (B-operand fragments), and layer_table holding
+ * L x 14 pointers: tm_gm_embed's 12, then channel ffn.3 transposed ([HC, C]) and ffn.0 transposed
+ * ([C, HC]), both packed by tm_gm_pack.  x_mean / node_out unused.  No parameter gradients. */
+int tm_gm_embed_bwd_ok(int32_t N, int32_t C, int32_t T, int32_t L, int32_t HT);
+int tm_gm_embed_bwd(const tm_gm_embed_args *a, const float *d_x_mean, const float *d_node_out, float *d_ew,
+                    void *stream);
 /* 1 when tm_gm_embed runs the register-resident kernel for these dims (C % 4 == 0, T % 4 == 0, N <= 32,
  * C <= 256); its weights are then packed by tm_gm_pack_a instead of tm_gm_pack: proj_w with
  * (n_mult, k_mult) = (1, 4), channel ffn.0 with (2, 1), ffn.3 with (1, 2) */

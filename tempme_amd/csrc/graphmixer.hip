@@ -820,6 +820,489 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 
     }
 }
 
+
+// ================================================================== backward: d explanation weights
+//
+// The explainer's training signal through a frozen base GraphMixer (temp_exp_main.py:614-632 with
+// base_type == 'graphmixer'): d ew [R, N] from d x_mean [R, C] and d node_out [R, D].  One workgroup per
+// row, the LDS-tiled layout of gm_embed_kernel.  The row's forward runs first, keeping every mixer's
+// input image XL[l]; then per layer, last first, with G = d(layer output) in LDS:
+//   out1 = (Y_tok + b) * ew + X * ew      recomputed per channel (thread per channel, VALU, N <= 32 tokens)
+//   channel branch, per hidden chunk: Z2 = W1 LN(out1) + b1 (MFMA, LN applied to the A fragments), H = gelu(Z2)
+//     -> Y_ch += W2 H (for the ew term), dG2 = (G ew) W2 (MFMA on the transposed pack), dZ2 = dG2 gelu'(Z2),
+//     dV += dZ2 W1 (MFMA on the transposed pack, the chunk's K slice)
+//   d ew_t += sum_c G (Y_ch + b2);  G <- G + LN_backward(dV)          (= d out1)
+//   token branch per channel: d ew_t += sum_c G (Y_tok + b) + da X, da = G + LN_tok_backward(FFN_tok_backward(G ew)),
+//     G <- da * ew                                                     (= d layer input)
+// Per-token sums over channels go through an LDS image and one wave per token (fixed order, deterministic).
+struct GmBwd {
+    const float *d_xm, *d_no;   // [R][C], [R][D]
+    float *d_ew;                // [R][N]
+    const float *const *lw;     // [L][14]: tm_gm_embed's 12 (B-operand packs) + ffn.3^T, ffn.0^T packs
+};
+constexpr int GMB_LW = 14;
+
+__device__ __forceinline__ float gm_gelu_d(float x) {
+    return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * expf(-0.5f * x * x);
+}
+
+// token LayerNorm / FFN weights of one layer, staged in LDS
+struct GmTokW {
+    float *lg, *lb, *w1, *b1, *w2, *b2;
+};
+constexpr int GMB_TW = 2 * GM_MT + 2 * (GM_MT / 2) * GM_MT + GM_MT / 2 + GM_MT;   // its LDS floats
+
+// LDS plan (floats): XL [L][32][XP] | X/G [32][XP] | O1 [32][XP] | DY [32][XP] | U [ulen] (projection
+// input halves, hidden chunks) | token-FFN weights [GMB_TW] | tmean, trstd, sew, sval, dsew [5][32] |
+// lnw, lnb [2][C16].  ~147 KB at C = T = 172 with 2 layers: one workgroup per CU.
+static __host__ __device__ inline int gmb_ulen(int C, int T) {
+    const int KG = gm_r16(C + T) / 16, K0P = 16 * ((KG + 1) / 2) + 4, HP = GM_HCH + 4;
+    return GM_MT * K0P > GM_MT * HP ? GM_MT * K0P : GM_MT * HP;
+}
+static __host__ __device__ inline size_t gmb_lds_floats(int C, int T, int L) {
+    const int XP = gm_r16(C) + 4;
+    return (size_t)(L + 3) * GM_MT * XP + gmb_ulen(C, T) + GMB_TW + 5 * GM_MT + 2 * gm_r16(C);
+}
+
+// one channel's token mixing, recomputed: av[t] = X[t][c] ew_t, LayerNorm over the N tokens, FFN N -> HT -> N
+// (GELU); y[t] = FFN output + b2 (tokens t < N).  Weights from LDS: lg, lb [N], w1 [HT][N], b1 [HT], w2 [N][HT], b2 [N]
+__device__ __forceinline__ void gmb_tok_fwd(int N, int HT, const GmTokW &tw, const float (&av)[GM_MT], float &mean,
+                                            float &rstd, float (&z1)[GM_MT / 2], float (&y)[GM_MT]) {
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < GM_MT; ++t) s += t < N ? av[t] : 0.f;
+    mean = s / (float)N;
+    float q = 0.f;
+#pragma unroll
+    for (int t = 0; t < GM_MT; ++t) {
+        const float d = t < N ? av[t] - mean : 0.f;
+        q += d * d;
+    }
+    rstd = 1.f / sqrtf(q / (float)N + 1e-5f);
+#pragma unroll
+    for (int k = 0; k < GM_MT / 2; ++k) {
+        float acc = 0.f;
+        if (k < HT) {
+            acc = tw.b1[k];
+#pragma unroll
+            for (int t = 0; t < GM_MT; ++t)
+                if (t < N) acc += tw.w1[k * N + t] * ((av[t] - mean) * rstd * tw.lg[t] + tw.lb[t]);
+        }
+        z1[k] = acc;
+    }
+#pragma unroll
+    for (int t = 0; t < GM_MT; ++t) {
+        float acc = 0.f;
+        if (t < N) {
+            acc = tw.b2[t];
+#pragma unroll
+            for (int k = 0; k < GM_MT / 2; ++k)
+                if (k < HT) acc += tw.w2[t * HT + k] * gm_gelu(z1[k]);
+        }
+        y[t] = acc;
+    }
+}
+
+// sum over c < C of the LDS image V[t][c], one wave per token, added to out[t]
+__device__ __forceinline__ void gmb_token_sums(const float *V, int XP, int N, int C, float *out) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int t = wave; t < N; t += 4) {
+        float s = 0.f;
+        for (int c = lane; c < C; c += 64) s += V[gm_idx(t, c, XP)];
+        s = gm_wsum(s);
+        if (lane == 0) out[t] += s;
+    }
+}
+
+template <int NMT, int NTW>
+__global__ void __launch_bounds__(256) gm_bwd_kernel(GmArgs a, GmBwd b) {
+    extern __shared__ float gm_lds[];
+    const int r = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int N = a.N, C = a.C, T = a.T, D = a.D, L = a.L, HT = a.HT;
+    const int C16 = gm_r16(C), KG = gm_r16(C + T) / 16, KH = (KG + 1) / 2;
+    const int XP = C16 + 4, HP = GM_HCH + 4, K0P = 16 * KH + 4, IMG = GM_MT * XP;
+    float *XL = gm_lds, *X = XL + L * IMG, *G = X, *O1 = X + IMG, *DY = O1 + IMG, *U = DY + IMG;
+    float *TW = U + gmb_ulen(C, T);
+    float *tmean = TW + GMB_TW, *trstd = tmean + GM_MT, *sew = trstd + GM_MT, *sval = sew + GM_MT;
+    float *dsew = sval + GM_MT, *lnw = dsew + GM_MT, *lnb = lnw + C16;
+    float *X0 = U, *H = U;
+    if (tid < GM_MT) {
+        const bool v = tid < N && a.nid[(size_t)r * N + tid] != 0;
+        sval[tid] = v ? 1.f : 0.f;
+        sew[tid] = tid < N ? a.ew[(size_t)r * N + tid] * (v ? 1.f : 0.f) : 0.f;
+        dsew[tid] = 0.f;
+    }
+    __syncthreads();
+    const int NT = C16 / 16, ntw = (NT - wave + 3) / 4;
+    const int NH = gm_r16(a.HC) / 16;
+    float mr[2] = {0.f, 0.f}, rr[2] = {0.f, 0.f};
+    // ---- forward: projection (as gm_embed_kernel)
+    const double cut = a.cut[r];
+    for (int h = 0; h < 2; ++h) {
+        const int G0 = h * KH, nG = min(KH, KG - G0), W16 = 16 * nG;
+        if (nG <= 0) break;
+        for (int i = tid; i < GM_MT * W16; i += blockDim.x) {
+            const int t = i / W16, k = 16 * G0 + (i - t * W16);
+            float v = 0.f;
+            if (t < N) {
+                const bool valid = sval[t] != 0.f;
+                if (k < C) {
+                    if (a.edge_attr) v = a.edge_attr[((size_t)r * N + t) * C + k];
+                    else if (valid) v = a.e_feat[(size_t)a.eid[(size_t)r * N + t] * C + k];
+                } else if (k < C + T && valid) {
+                    const float dt = (float)(cut - a.ts[(size_t)r * N + t]);
+                    const float arg = (float)((double)dt * (double)a.time_w[k - C] + (double)a.time_b[k - C]);
+                    v = cos_rd(arg);
+                }
+            }
+            X0[gm_idx(t, k - 16 * G0, K0P)] = v;
+        }
+        __syncthreads();
+        {
+            gmx4 acc[NTW][2];
+#pragma unroll
+            for (int i = 0; i < NTW; ++i) acc[i][0] = acc[i][1] = gmx4{0.f, 0.f, 0.f, 0.f};
+            gm_gemm_mt<NMT, NTW, false>(X0, K0P, G0, a.proj_w, NT, wave, ntw, G0, nG, acc, nullptr, nullptr, mr, rr);
+#pragma unroll
+            for (int i = 0; i < NTW; ++i) {
+                if (i >= ntw) break;
+                const int n = 16 * (wave + 4 * i) + (lane & 15);
+                const float bv = n < C ? a.proj_b[n] : 0.f;
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int t = 16 * mt + 4 * (lane >> 4) + e;
+                        const int ix = gm_idx(t, n, XP);
+                        const bool in = mt < NMT && n < C && t < N;
+                        if (h == 0) X[ix] = in ? acc[i][mt][e] : 0.f;
+                        else if (in) X[ix] = X[ix] + acc[i][mt][e] + bv;
+                    }
+            }
+        }
+        __syncthreads();
+    }
+    if (KG == 1) {
+        for (int i = tid; i < GM_MT * C16; i += blockDim.x) {
+            const int t = i / C16, n = i - t * C16;
+            if (t < N && n < C) X[gm_idx(t, n, XP)] += a.proj_b[n];
+        }
+        __syncthreads();
+    }
+    // stage layer l's token LayerNorm / FFN weights into TW; channel LN parameters (permuted K order) into
+    // lnw / lnb
+    auto stage_layer = [&](int l) -> GmTokW {
+        const float *const *w = b.lw + GMB_LW * l;
+        GmTokW tw{TW, TW + GM_MT, TW + 2 * GM_MT, TW + 2 * GM_MT + (GM_MT / 2) * GM_MT,
+                  TW + 2 * GM_MT + (GM_MT / 2) * GM_MT + GM_MT / 2, TW + 2 * GM_MT + GM_MT * GM_MT + GM_MT / 2};
+        for (int i = tid; i < N; i += blockDim.x) {
+            tw.lg[i] = w[0][i];
+            tw.lb[i] = w[1][i];
+            tw.b2[i] = w[5][i];
+        }
+        for (int i = tid; i < HT * N; i += blockDim.x) {
+            tw.w1[i] = w[2][i];
+            tw.w2[i] = w[4][i];
+        }
+        for (int i = tid; i < HT; i += blockDim.x) tw.b1[i] = w[3][i];
+        for (int k = tid; k < C16; k += blockDim.x) {
+            const int pk = (k & ~15) + 4 * (k & 3) + ((k >> 2) & 3);
+            lnw[pk] = k < C ? w[6][k] : 0.f;
+            lnb[pk] = k < C ? w[7][k] : 0.f;
+        }
+        return tw;
+    };
+    // token mixing of one channel c from image S into image Dst: Dst = (y) * ew + S * ew (thread per channel)
+    auto token_mix = [&](const GmTokW &tw, const float *S, float *Dst) {
+        for (int c = tid; c < C; c += blockDim.x) {
+            float av[GM_MT], z1[GM_MT / 2], y[GM_MT], mean, rstd;
+#pragma unroll
+            for (int t = 0; t < GM_MT; ++t) av[t] = t < N ? S[gm_idx(t, c, XP)] * sew[t] : 0.f;
+            gmb_tok_fwd(N, HT, tw, av, mean, rstd, z1, y);
+#pragma unroll
+            for (int t = 0; t < GM_MT; ++t)
+                if (t < N) Dst[gm_idx(t, c, XP)] = y[t] * sew[t] + av[t];
+        }
+    };
+    // channel LayerNorm statistics of image S (one wave per token) into tmean / trstd, then this lane's rows
+    auto chan_stats = [&](const float *S) {
+        for (int t = wave; t < GM_MT; t += 4) {
+            float mean = 0.f, rstd = 0.f;
+            if (t < N) {
+                float s = 0.f, q = 0.f;
+                for (int c = lane; c < C; c += 64) s += S[gm_idx(t, c, XP)];
+                mean = gm_wsum(s) / (float)C;
+                for (int c = lane; c < C; c += 64) {
+                    const float d = S[gm_idx(t, c, XP)] - mean;
+                    q += d * d;
+                }
+                rstd = 1.f / sqrtf(gm_wsum(q) / (float)C + 1e-5f);
+            }
+            if (lane == 0) {
+                tmean[t] = mean;
+                trstd[t] = rstd;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+            mr[mt] = tmean[16 * mt + (lane & 15)];
+            rr[mt] = trstd[16 * mt + (lane & 15)];
+        }
+    };
+    // ---- forward through the mixers, keeping each layer's input
+    for (int l = 0; l < L; ++l) {
+        const float *const *w = b.lw + GMB_LW * l;
+        for (int i = tid; i < IMG; i += blockDim.x) XL[l * IMG + i] = X[i];
+        const GmTokW tw = stage_layer(l);
+        __syncthreads();
+        token_mix(tw, X, X);
+        __syncthreads();
+        chan_stats(X);
+        const float4 *W1 = reinterpret_cast<const float4 *>(w[8]), *W2 = reinterpret_cast<const float4 *>(w[10]);
+        gmx4 acc2[NTW][2];
+#pragma unroll
+        for (int i = 0; i < NTW; ++i) acc2[i][0] = acc2[i][1] = gmx4{0.f, 0.f, 0.f, 0.f};
+        for (int h0 = 0; h0 < NH; h0 += GM_HCH / 16) {
+            const int nh = min(GM_HCH / 16, NH - h0), nw1 = (nh - wave + 3) / 4;
+            gmx4 acc[GM_HCH / 64][2];
+#pragma unroll
+            for (int i = 0; i < GM_HCH / 64; ++i) acc[i][0] = acc[i][1] = gmx4{0.f, 0.f, 0.f, 0.f};
+            gm_gemm_mt<NMT, GM_HCH / 64, true>(X, XP, 0, W1, NH, h0 + wave, nw1, 0, C16 / 16, acc, lnw, lnb, mr, rr);
+#pragma unroll
+            for (int i = 0; i < GM_HCH / 64; ++i) {
+                if (i >= nw1) break;
+                const int ht = wave + 4 * i, n = 16 * (h0 + ht) + (lane & 15);
+                const float bv = n < a.HC ? w[9][n] : 0.f;
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int t = 16 * mt + 4 * (lane >> 4) + e;
+                        H[gm_idx(t, 16 * ht + (lane & 15), HP)] = (mt < NMT && n < a.HC) ? gm_gelu(acc[i][mt][e] + bv) : 0.f;
+                    }
+            }
+            __syncthreads();
+            gm_gemm_mt<NMT, NTW, false>(H, HP, h0, W2, NT, wave, ntw, h0, nh, acc2, nullptr, nullptr, mr, rr);
+            __syncthreads();
+        }
+#pragma unroll
+        for (int i = 0; i < NTW; ++i) {
+            const int nt = wave + 4 * i;
+            if (nt >= NT) break;
+            const int n = 16 * nt + (lane & 15);
+            const float bv = n < C ? w[11][n] : 0.f;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int t = 16 * mt + 4 * (lane >> 4) + e;
+                    if (mt < NMT && t < N && n < C) {
+                        const int ix = gm_idx(t, n, XP);
+                        X[ix] = (acc2[i][mt][e] + bv) * sew[t] + X[ix];
+                    }
+                }
+        }
+        __syncthreads();
+    }
+    // ---- d of the masked token mean (:176-178) and the neighbour-feature mean (:181-189)
+    float nvalid = 0.f;
+    for (int t = 0; t < N; ++t) nvalid += sval[t];
+    const float *dxm = b.d_xm + (size_t)r * C;
+    // DY <- dxm_c X[t][c] sval_t / N (per-token sums give the x_mean part of d sew); G <- dxm_c sval_t sew_t / N
+    for (int i = tid; i < GM_MT * C16; i += blockDim.x) {
+        const int t = i / C16, c = i - t * C16;
+        const int ix = gm_idx(t, c, XP);
+        const bool in = t < N && c < C;
+        const float g = in ? dxm[c] : 0.f;
+        DY[ix] = in ? g * X[ix] * sval[t] / (float)N : 0.f;
+        G[ix] = in ? g * sval[t] * sew[t] / (float)N : 0.f;
+    }
+    __syncthreads();
+    gmb_token_sums(DY, XP, N, C, dsew);
+    {   // node_out: d sew_t += sum_d dno_d n_feat[nid_t][d] sc_t / N, one wave per token
+        const float *dno = b.d_no + (size_t)r * D;
+        for (int t = wave; t < N; t += 4) {
+            const float sc = nvalid > 0.f ? sval[t] / nvalid : 1.f / (float)N;
+            const float *nf = a.n_feat + (size_t)a.nid[(size_t)r * N + t] * D;
+            float s = 0.f;
+            for (int d = lane; d < D; d += 64) s += dno[d] * nf[d];
+            s = gm_wsum(s);
+            if (lane == 0) dsew[t] += s * sc / (float)N;
+        }
+    }
+    __syncthreads();
+    // ---- the mixers backwards
+    for (int l = L - 1; l >= 0; --l) {
+        const float *const *w = b.lw + GMB_LW * l;
+        const float *XI = XL + l * IMG;
+        const GmTokW tw = stage_layer(l);
+        __syncthreads();
+        token_mix(tw, XI, O1);                                    // out1
+        // DY = G ew (d channel-FFN output)
+        for (int i = tid; i < GM_MT * C16; i += blockDim.x) {
+            const int t = i / C16, c = i - t * C16;
+            const int ix = gm_idx(t, c, XP);
+            DY[ix] = (t < N && c < C) ? G[ix] * sew[t] : 0.f;
+        }
+        __syncthreads();
+        chan_stats(O1);
+        const float4 *W1 = reinterpret_cast<const float4 *>(w[8]), *W2 = reinterpret_cast<const float4 *>(w[10]);
+        const float4 *W2T = reinterpret_cast<const float4 *>(w[12]), *W1T = reinterpret_cast<const float4 *>(w[13]);
+        gmx4 acc2[NTW][2], accv[NTW][2];
+#pragma unroll
+        for (int i = 0; i < NTW; ++i) acc2[i][0] = acc2[i][1] = accv[i][0] = accv[i][1] = gmx4{0.f, 0.f, 0.f, 0.f};
+        for (int h0 = 0; h0 < NH; h0 += GM_HCH / 16) {
+            const int nh = min(GM_HCH / 16, NH - h0), nw1 = (nh - wave + 3) / 4;
+            gmx4 acc[GM_HCH / 64][2], accd[GM_HCH / 64][2];
+#pragma unroll
+            for (int i = 0; i < GM_HCH / 64; ++i)
+                acc[i][0] = acc[i][1] = accd[i][0] = accd[i][1] = gmx4{0.f, 0.f, 0.f, 0.f};
+            gm_gemm_mt<NMT, GM_HCH / 64, true>(O1, XP, 0, W1, NH, h0 + wave, nw1, 0, C16 / 16, acc, lnw, lnb, mr, rr);
+            gm_gemm_mt<NMT, GM_HCH / 64, false>(DY, XP, 0, W2T, NH, h0 + wave, nw1, 0, C16 / 16, accd, nullptr, nullptr,
+                                                mr, rr);
+            // H = gelu(Z2) for Y_ch; dZ2 = dG2 gelu'(Z2) kept in accd for the second pass through U
+#pragma unroll
+            for (int i = 0; i < GM_HCH / 64; ++i) {
+                if (i >= nw1) break;
+                const int ht = wave + 4 * i, n = 16 * (h0 + ht) + (lane & 15);
+                const float bv = n < a.HC ? w[9][n] : 0.f;
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int t = 16 * mt + 4 * (lane >> 4) + e;
+                        const bool in = mt < NMT && n < a.HC;
+                        const float z = acc[i][mt][e] + bv;
+                        H[gm_idx(t, 16 * ht + (lane & 15), HP)] = in ? gm_gelu(z) : 0.f;
+                        accd[i][mt][e] = in ? accd[i][mt][e] * gm_gelu_d(z) : 0.f;
+                    }
+            }
+            __syncthreads();
+            gm_gemm_mt<NMT, NTW, false>(H, HP, h0, W2, NT, wave, ntw, h0, nh, acc2, nullptr, nullptr, mr, rr);
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < GM_HCH / 64; ++i) {
+                if (i >= nw1) break;
+                const int ht = wave + 4 * i;
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int t = 16 * mt + 4 * (lane >> 4) + e;
+                        H[gm_idx(t, 16 * ht + (lane & 15), HP)] = accd[i][mt][e];
+                    }
+            }
+            __syncthreads();
+            gm_gemm_mt<NMT, NTW, false>(H, HP, h0, W1T, NT, wave, ntw, h0, nh, accv, nullptr, nullptr, mr, rr);
+            __syncthreads();
+        }
+        // d sew_t += sum_c G (Y_ch + b2)
+#pragma unroll
+        for (int i = 0; i < NTW; ++i) {
+            const int nt = wave + 4 * i;
+            if (nt >= NT) break;
+            const int n = 16 * nt + (lane & 15);
+            const float bv = n < C ? w[11][n] : 0.f;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int t = 16 * mt + 4 * (lane >> 4) + e;
+                    const int ix = gm_idx(t, n, XP);
+                    DY[ix] = (mt < NMT && t < N && n < C) ? G[ix] * (acc2[i][mt][e] + bv) : 0.f;
+                }
+        }
+        __syncthreads();
+        gmb_token_sums(DY, XP, N, C, dsew);
+        __syncthreads();
+        // channel LayerNorm backward: DY = dV * ln weight; G += rstd (DY - mean_c DY - xhat mean_c(DY xhat))
+#pragma unroll
+        for (int i = 0; i < NTW; ++i) {
+            const int nt = wave + 4 * i;
+            if (nt >= NT) break;
+            const int n = 16 * nt + (lane & 15);
+            const float gw = n < C ? w[6][n] : 0.f;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int t = 16 * mt + 4 * (lane >> 4) + e;
+                    DY[gm_idx(t, n, XP)] = (mt < NMT && t < N && n < C) ? accv[i][mt][e] * gw : 0.f;
+                }
+        }
+        __syncthreads();
+        for (int t = wave; t < N; t += 4) {
+            const float mean = tmean[t], rstd = trstd[t];
+            float s1 = 0.f, s2 = 0.f;
+            for (int c = lane; c < C; c += 64) {
+                const int ix = gm_idx(t, c, XP);
+                const float dv = DY[ix], xh = (O1[ix] - mean) * rstd;
+                s1 += dv;
+                s2 += dv * xh;
+            }
+            s1 = gm_wsum(s1) / (float)C;
+            s2 = gm_wsum(s2) / (float)C;
+            for (int c = lane; c < C; c += 64) {
+                const int ix = gm_idx(t, c, XP);
+                const float xh = (O1[ix] - mean) * rstd;
+                G[ix] += rstd * (DY[ix] - s1 - xh * s2);
+            }
+        }
+        __syncthreads();
+        // token branch, thread per channel: G = d out1 -> d layer input; DY = the channel's terms of d sew
+        for (int c = tid; c < C; c += blockDim.x) {
+            float av[GM_MT], z1[GM_MT / 2], y[GM_MT], mean, rstd;
+#pragma unroll
+            for (int t = 0; t < GM_MT; ++t) av[t] = t < N ? XI[gm_idx(t, c, XP)] * sew[t] : 0.f;
+            gmb_tok_fwd(N, HT, tw, av, mean, rstd, z1, y);
+            float g[GM_MT], dz[GM_MT / 2];
+#pragma unroll
+            for (int t = 0; t < GM_MT; ++t) g[t] = t < N ? G[gm_idx(t, c, XP)] : 0.f;
+            // dh = W2^T (g ew), dz1 = dh gelu'(z1)
+#pragma unroll
+            for (int k = 0; k < GM_MT / 2; ++k) {
+                float s = 0.f;
+                if (k < HT) {
+#pragma unroll
+                    for (int t = 0; t < GM_MT; ++t)
+                        if (t < N) s += tw.w2[t * HT + k] * g[t] * sew[t];
+                }
+                dz[k] = k < HT ? s * gm_gelu_d(z1[k]) : 0.f;
+            }
+            // dT = W1^T dz1; LayerNorm-over-tokens backward
+            float s1 = 0.f, s2 = 0.f, dtg[GM_MT];
+#pragma unroll
+            for (int t = 0; t < GM_MT; ++t) {
+                float s = 0.f;
+                if (t < N) {
+#pragma unroll
+                    for (int k = 0; k < GM_MT / 2; ++k)
+                        if (k < HT) s += tw.w1[k * N + t] * dz[k];
+                }
+                dtg[t] = t < N ? s * tw.lg[t] : 0.f;
+                s1 += dtg[t];
+                s2 += t < N ? dtg[t] * (av[t] - mean) * rstd : 0.f;
+            }
+            s1 /= (float)N;
+            s2 /= (float)N;
+#pragma unroll
+            for (int t = 0; t < GM_MT; ++t) {
+                if (t < N) {
+                    const int ix = gm_idx(t, c, XP);
+                    const float da = g[t] + rstd * (dtg[t] - s1 - (av[t] - mean) * rstd * s2);
+                    DY[ix] = g[t] * y[t] + da * XI[ix];
+                    G[ix] = da * sew[t];
+                }
+            }
+        }
+        __syncthreads();
+        gmb_token_sums(DY, XP, N, C, dsew);
+        __syncthreads();
+    }
+    if (tid < N) b.d_ew[(size_t)r * N + tid] = dsew[tid] * sval[tid];
+}
+
 }  // namespace tmk
 
 using namespace tmk;
@@ -933,5 +1416,49 @@ extern "C" int tm_gm_embed(const tm_gm_embed_args *p, void *stream) {
     if (rc != TM_OK) return rc;
     TM_CHECK_LAUNCH();
     prof_end("gm_embed_kernel", (hipStream_t)stream, pe);
+    return TM_OK;
+}
+
+extern "C" int tm_gm_embed_bwd_ok(int32_t N, int32_t C, int32_t T, int32_t L, int32_t HT) {
+    return N > 0 && N <= GM_MT && HT >= 0 && HT <= GM_MT / 2 && L >= 0 && L <= GM_MAXL && C > 0 && C <= 256 && T >= 0 &&
+           sizeof(float) * gmb_lds_floats(C, T, L) <= 160 * 1024;
+}
+
+extern "C" int tm_gm_embed_bwd(const tm_gm_embed_args *p, const float *d_x_mean, const float *d_node_out, float *d_ew,
+                               void *stream) {
+    if (!p) return fail(TM_E_ARG, "tm_gm_embed_bwd: NULL arguments");
+    const tm_gm_embed_args &q = *p;
+    if (q.R < 0 || q.N <= 0 || q.C <= 0 || q.T < 0 || q.D <= 0 || q.L < 0 || q.HT < 0 || q.HC <= 0)
+        return fail(TM_E_ARG, "tm_gm_embed_bwd: bad dimensions");
+    if (q.N > GM_MT || q.HT > GM_MT / 2 || q.L > GM_MAXL || q.C > 256)
+        return fail(TM_E_UNSUPPORTED, "tm_gm_embed_bwd: needs num_tokens <= 32, token hidden <= 16, <= 4 layers, "
+                                      "channels <= 256");
+    if (q.R == 0) return TM_OK;
+    if (!q.node || !q.nid || !q.cut || !q.ts || !q.n_feat || (!q.e_feat && !q.edge_attr) || (q.T && (!q.time_w || !q.time_b)) ||
+        !q.proj_w || !q.proj_b || (!q.eid && !q.edge_attr) || !q.ew || !d_x_mean || !d_node_out || !d_ew ||
+        (q.L > 0 && !q.layer_table))
+        return fail(TM_E_ARG, "tm_gm_embed_bwd: NULL pointer");
+    const size_t lds = sizeof(float) * gmb_lds_floats(q.C, q.T, q.L);
+    if (lds > 160 * 1024) return fail(TM_E_UNSUPPORTED, "tm_gm_embed_bwd: dims too large for the LDS tile");
+    GmArgs a{};
+    a.R = q.R; a.N = q.N; a.C = q.C; a.T = q.T; a.D = q.D; a.L = q.L; a.HT = q.HT; a.HC = q.HC;
+    a.node = q.node; a.nid = q.nid; a.eid = q.eid; a.cut = q.cut; a.ts = q.ts; a.ew = q.ew; a.edge_attr = q.edge_attr;
+    a.n_feat = q.n_feat; a.e_feat = q.e_feat; a.time_w = q.time_w; a.time_b = q.time_b;
+    a.proj_w = reinterpret_cast<const float4 *>(q.proj_w);
+    a.proj_b = q.proj_b;
+    GmBwd b{d_x_mean, d_node_out, d_ew, q.layer_table};
+    hipEvent_t pe = prof_begin((hipStream_t)stream);
+    const bool t3 = gm_r16(q.C) / 16 <= 12;
+    auto launch = [&](auto kern) -> int {
+        TM_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        kern<<<q.R, 256, lds, (hipStream_t)stream>>>(a, b);
+        return TM_OK;
+    };
+    int rc;
+    if (q.N > 16) rc = t3 ? launch(gm_bwd_kernel<2, 3>) : launch(gm_bwd_kernel<2, 4>);
+    else rc = t3 ? launch(gm_bwd_kernel<1, 3>) : launch(gm_bwd_kernel<1, 4>);
+    if (rc != TM_OK) return rc;
+    TM_CHECK_LAUNCH();
+    prof_end("gm_bwd_kernel", (hipStream_t)stream, pe);
     return TM_OK;
 }

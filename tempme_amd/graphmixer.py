@@ -90,6 +90,29 @@ class MLPMixer(nn.Module):
         return h + out
 
 
+class _GmEmbedFn(torch.autograd.Function):
+    """(x_mean, node_out) of tm_gm_embed as a function of the explanation weights: forward passes the
+    kernel's outputs through, backward is tm_gm_embed_bwd (d ew [R, N]; zero on padding neighbours)."""
+
+    @staticmethod
+    def forward(ctx, ew, x_mean, node_out, args, keep):
+        ctx.args, ctx.keep = args, keep
+        ctx.shape = ew.shape
+        return x_mean.detach(), node_out.detach()
+
+    @staticmethod
+    def backward(ctx, d_xm, d_no):
+        a = ctx.args
+        dev = ctx.keep[1].device
+        R, N = a.R, a.N
+        d_xm = (torch.zeros(R, a.C, device=dev) if d_xm is None else d_xm).float().contiguous()
+        d_no = (torch.zeros(R, a.D, device=dev) if d_no is None else d_no).float().contiguous()
+        d_ew = torch.empty(max(R, 1), N, dtype=torch.float32, device=dev)
+        L.check(L.lib().tm_gm_embed_bwd(ctypes.byref(a), L.ptr(d_xm), L.ptr(d_no), L.ptr(d_ew), L.stream_ptr(dev)),
+                "GraphMixer explanation-weight backward")
+        return d_ew[:R].reshape(ctx.shape), None, None, None, None
+
+
 class GraphMixer(nn.Module):
     """graphmixer.py:53-101 constructor."""
 
@@ -138,18 +161,29 @@ class GraphMixer(nn.Module):
         return self._ntab, self._etab
 
     # ------------------------------------------------------------------ HIP path (tm_gm_embed)
-    def _hip_ok(self, explain_weight, N):
-        """Eval forward without gradients (threshold_test, scoring): the fused HIP embedding.  With
-        gradients (explainer training through the base model) or dropout active, the torch formulation
-        below runs under autograd."""
+    def _hip_mode(self, explain_weight, N):
+        """"eval": the fused HIP embedding, no gradients (threshold_test, scoring).  "grad": explanation
+        weights that require a gradient (the explainer's training step through the frozen base model,
+        temp_exp_main.py:614-632): the HIP forward plus tm_gm_embed_bwd for d ew; the base model's
+        parameters get no .grad (as the TGN base, tgn.py).  None: the torch formulation below (dropout
+        active, unsupported dims, or gradients wanted for the base model's own parameters only)."""
         import os
         if os.environ.get("TEMPME_GM_TORCH") == "1" or self.training:
-            return False
-        if torch.is_grad_enabled() and ((explain_weight is not None and explain_weight.requires_grad)
-                                        or any(p.requires_grad for p in self.parameters())):
-            return False
+            return None
         ht = int(self.mlp_mixers[0].token_feedforward.dim_expansion_factor * N) if self.num_layers else 0
-        return (N <= 32 and ht <= 16 and self.num_layers <= 4 and self.num_channels <= 256 and N == self.num_tokens)
+        if not (N <= 32 and ht <= 16 and self.num_layers <= 4 and self.num_channels <= 256 and N == self.num_tokens):
+            return None
+        if not torch.is_grad_enabled():
+            return "eval"
+        if explain_weight is not None and explain_weight.requires_grad:
+            ok = L.lib().tm_gm_embed_bwd_ok(N, self.num_channels, self.time_feat_dim, self.num_layers, ht)
+            return "grad" if ok else None
+        if any(p.requires_grad for p in self.parameters()):
+            return None
+        return "eval"
+
+    def _hip_ok(self, explain_weight, N):
+        return self._hip_mode(explain_weight, N) is not None
 
     def _gm_packed(self, dev):
         """Packed MFMA fragments of projection_layer and every channel FFN (tm_gm_pack), rebuilt when a
@@ -198,8 +232,58 @@ class GraphMixer(nn.Module):
             self._gm_key = key
         return self._gm_pack
 
-    def _embed_hip(self, dev, node_ids, cut, nid, eid, t, explain_weight, edge_attr):
+    def _gm_packed_bwd(self, dev):
+        """B-operand packs (tm_gm_pack) for tm_gm_embed_bwd: the projection, each channel FFN's two weights
+        and their transposes; layer table [L][14]; rebuilt when a parameter changes."""
+        ps = list(self.parameters())
+        key = (dev, tuple((p.data_ptr(), p._version) for p in ps))
+        if getattr(self, "_gmb_key", None) != key:
+            st = L.stream_ptr(dev)
+            keep = []
+
+            def pack(w):
+                w = w.detach().to(dev, torch.float32).contiguous()
+                n_out, k = w.shape
+                out = torch.empty(int(L.lib().tm_gm_packed_floats(n_out, k)), dtype=torch.float32, device=dev)
+                L.check(L.lib().tm_gm_pack(L.ptr(w), n_out, k, L.ptr(out), st), "tm_gm_pack")
+                keep.append(w)
+                return out
+
+            def flat(t):
+                t = t.detach().to(dev, torch.float32).contiguous()
+                keep.append(t)
+                return t
+
+            layers = []
+            for m in self.mlp_mixers:
+                tf, cf = m.token_feedforward.ffn, m.channel_feedforward.ffn
+                layers.append([flat(m.token_norm.weight), flat(m.token_norm.bias), flat(tf[0].weight), flat(tf[0].bias),
+                               flat(tf[3].weight), flat(tf[3].bias), flat(m.channel_norm.weight),
+                               flat(m.channel_norm.bias), pack(cf[0].weight), flat(cf[0].bias), pack(cf[3].weight),
+                               flat(cf[3].bias), pack(cf[3].weight.t()), pack(cf[0].weight.t())])
+            table = torch.tensor([[t.data_ptr() for t in lw] for lw in layers] or [[0] * 14], dtype=torch.int64)
+            self._gmb_pack = dict(proj_w=pack(self.projection_layer.weight), layers=layers, table=table.to(dev),
+                                  keep=keep)
+            self._gmb_key = key
+        return self._gmb_pack
+
+    def _embed_args(self, dev, node, nid32, eid32, cut64, t64, ew, ea, proj_w, proj_b, tw, tb, table):
         ntab, etab = self._tables(dev)
+        R, N = nid32.shape
+        a = L.GmEmbedArgs()
+        a.R, a.N, a.C, a.T, a.D, a.L = R, N, self.num_channels, self.time_feat_dim, self.node_feat_dim, self.num_layers
+        a.HT = int(self.mlp_mixers[0].token_feedforward.dim_expansion_factor * N) if self.num_layers else 0
+        a.HC = int(self.channel_dim_expansion_factor * self.num_channels)
+        a.node, a.nid, a.eid, a.cut, a.ts = L.ptr(node), L.ptr(nid32), L.ptr(eid32), L.ptr(cut64), L.ptr(t64)
+        a.ew = None if ew is None else L.ptr(ew)
+        a.edge_attr = None if ea is None else L.ptr(ea)
+        a.n_feat, a.e_feat = L.ptr(ntab), L.ptr(etab)
+        a.time_w, a.time_b = L.ptr(tw), L.ptr(tb)
+        a.proj_w, a.proj_b = L.ptr(proj_w), L.ptr(proj_b)
+        a.layer_table = L.ptr(table)
+        return a
+
+    def _embed_hip(self, dev, node_ids, cut, nid, eid, t, explain_weight, edge_attr, mode="eval"):
         R, N = nid.shape
         pk = self._gm_packed(dev)
         i32 = lambda x: x.to(dev, torch.int32).contiguous()  # noqa: E731
@@ -212,32 +296,34 @@ class GraphMixer(nn.Module):
         C, D = self.num_channels, self.node_feat_dim
         x_mean = torch.empty(max(R, 1), C, dtype=torch.float32, device=dev)
         node_out = torch.empty(max(R, 1), D, dtype=torch.float32, device=dev)
-        a = L.GmEmbedArgs()
-        a.R, a.N, a.C, a.T, a.D, a.L = R, N, C, self.time_feat_dim, D, self.num_layers
-        a.HT = int(self.mlp_mixers[0].token_feedforward.dim_expansion_factor * N) if self.num_layers else 0
-        a.HC = int(self.channel_dim_expansion_factor * C)
-        a.node, a.nid, a.eid, a.cut, a.ts = L.ptr(node), L.ptr(nid32), L.ptr(eid32), L.ptr(cut64), L.ptr(t64)
-        a.ew = None if ew is None else L.ptr(ew)
-        a.edge_attr = None if ea is None else L.ptr(ea)
-        a.n_feat, a.e_feat = L.ptr(ntab), L.ptr(etab)
-        a.time_w, a.time_b = L.ptr(pk["tw"]), L.ptr(pk["tb"])
-        a.proj_w, a.proj_b = L.ptr(pk["proj_w"]), L.ptr(pk["proj_b"])
-        a.layer_table = L.ptr(pk["table"])
+        a = self._embed_args(dev, node, nid32, eid32, cut64, t64, ew, ea, pk["proj_w"], pk["proj_b"], pk["tw"], pk["tb"],
+                             pk["table"])
         a.x_mean, a.node_out = L.ptr(x_mean), L.ptr(node_out)
         L.check(L.lib().tm_gm_embed(ctypes.byref(a), L.stream_ptr(dev)), "GraphMixer.compute_node_temporal_embeddings")
-        return F.linear(torch.cat([x_mean[:R], node_out[:R]], dim=1), self.output_layer.weight.to(dev),
-                        self.output_layer.bias.to(dev))
+        xm, no = x_mean[:R], node_out[:R]
+        if mode == "grad":
+            # d ew through tm_gm_embed_bwd; the rest of the graph (output layer, MergeLayer) is torch autograd
+            # with the base model's weights detached (frozen base: no parameter gradients)
+            bk = self._gm_packed_bwd(dev)
+            ab = self._embed_args(dev, node, nid32, eid32, cut64, t64, ew, ea, bk["proj_w"], pk["proj_b"], pk["tw"],
+                                  pk["tb"], bk["table"])
+            keep = (node, nid32, eid32, cut64, t64, ew, ea, bk, pk)
+            xm, no = _GmEmbedFn.apply(explain_weight, xm, no, ab, keep)
+            return F.linear(torch.cat([xm, no], dim=1), self.output_layer.weight.detach().to(dev),
+                            self.output_layer.bias.detach().to(dev))
+        return F.linear(torch.cat([xm, no], dim=1), self.output_layer.weight.to(dev), self.output_layer.bias.to(dev))
 
     def node_embeddings(self, node_ids, cut_time, nid, eid, times, explain_weight=None, edge_attr=None):
         """compute_node_temporal_embeddings (graphmixer.py:142-193) for R rows at once:
         node_ids [R], cut_time [R] (f64), nid/eid/times [R, N] (hop-1 records), explain_weight [R, N]."""
         dev = self._dev()
         N0 = np.shape(nid)[-1]
-        if self._hip_ok(explain_weight, N0):
+        mode = self._hip_mode(explain_weight, N0)
+        if mode is not None:
             return self._embed_hip(dev, _as_dev(node_ids, dev, torch.long).reshape(-1),
                                    _as_dev(cut_time, dev, torch.float64).reshape(-1), _as_dev(nid, dev, torch.long),
                                    _as_dev(eid, dev, torch.long), _as_dev(times, dev, torch.float64), explain_weight,
-                                   None if edge_attr is None else _as_dev(edge_attr, dev, torch.float32))
+                                   None if edge_attr is None else _as_dev(edge_attr, dev, torch.float32), mode)
         ntab, etab = self._tables(dev)
         node_ids = _as_dev(node_ids, dev, torch.long).reshape(-1)
         nid = _as_dev(nid, dev, torch.long)

@@ -97,6 +97,50 @@ def test_config5_dims_and_gradient_vs_oracle(dev):
                                atol=ATOL, rtol=RTOL)
     ga, gb = ew.grad.double().cpu(), ew64.grad
     assert torch.linalg.norm(ga - gb) <= 1e-4 * torch.linalg.norm(gb)
+    assert getattr(m, "_gmb_key", None) is not None, "the HIP explanation-weight backward did not run"
+
+
+@pytest.mark.parametrize("N,C,L", [(30, 172, 2), (12, 172, 2), (20, 32, 1), (16, 100, 3)])
+def test_hip_ew_gradient_vs_oracle(dev, N, C, L):
+    """tm_gm_embed_bwd (the explainer's training signal through a frozen GraphMixer): d ew of a BCE loss on
+    contrast's logits vs fp64 autograd through the oracle, for one / two token tiles, channel counts with and
+    without padding, 1-3 mixer layers, padding neighbours and a row without any valid neighbour; the embedding's
+    parameters get no gradient (frozen base, as the TGN base; the MergeLayer score stays torch autograd)."""
+    from tempme_amd.graphmixer import GraphMixer
+    rng = np.random.default_rng(N + C + L)
+    V, E, B = 300, 2000, 20
+    nf = rng.uniform(0, 1, (V, C)).astype(np.float32)
+    ef = rng.uniform(0, 1, (E + 1, C)).astype(np.float32)
+    nf[0] = ef[0] = 0
+    torch.manual_seed(N + L)
+    m = GraphMixer(nf, ef, n_neighbors=N, device=dev, num_tokens=N, num_layers=L, dropout=0.1).to(dev).eval()
+    cut = np.floor(rng.uniform(5e7, 1e8, B))
+    sgs = []
+    for _ in range(3):
+        node = rng.integers(1, V, (B, N))
+        node[rng.uniform(size=node.shape) < 0.25] = 0
+        node[1] = 0
+        eid = np.where(node > 0, rng.integers(1, E + 1, node.shape), 0)
+        ts = np.where(node > 0, np.floor(cut[:, None] - rng.uniform(0, 5e7, node.shape)), 0.0)
+        sgs.append(([node.astype(np.float64), None], [eid.astype(np.float64), None], [ts, None]))
+    src, dst, fake = (rng.integers(1, V, B) for _ in range(3))
+    ew0 = rng.uniform(0, 1, (3 * B, N)).astype(np.float32)
+    y = torch.cat([torch.ones(B, 1), torch.zeros(B, 1)])
+    ew = torch.from_numpy(ew0).to(dev).requires_grad_(True)
+    p, n = m.contrast(src, dst, fake, cut, None, *sgs, explain_weights=[ew])
+    torch.nn.functional.binary_cross_entropy_with_logits(torch.cat([p, n]), y.to(dev)).backward()
+    assert getattr(m, "_gmb_key", None) is not None, "the HIP explanation-weight backward did not run"
+    assert all(q.grad is None for k, q in m.named_parameters() if not k.startswith("affinity_score"))
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    ew64 = torch.from_numpy(ew0).double().requires_grad_(True)
+    p64, n64 = O.contrast(sd, L, src, dst, fake, cut, *sgs, explain_weights=[ew64], dtype=torch.float64)
+    torch.nn.functional.binary_cross_entropy_with_logits(torch.cat([p64, n64]), y.double()).backward()
+    np.testing.assert_allclose(torch.cat([p, n]).detach().cpu().double().numpy(), torch.cat([p64, n64]).detach().numpy(),
+                               atol=ATOL, rtol=RTOL)
+    ga, gb = ew.grad.double().cpu(), ew64.grad
+    assert float(torch.linalg.norm(ga - gb)) <= 1e-4 * float(torch.linalg.norm(gb)), \
+        (float(torch.linalg.norm(ga - gb)), float(torch.linalg.norm(gb)))
+    assert float(ga.abs()[torch.from_numpy(np.concatenate([sg[0][0] for sg in sgs]) == 0)].max()) == 0.0
 
 
 @pytest.mark.parametrize("case", CASES)
