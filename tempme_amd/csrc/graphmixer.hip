@@ -879,6 +879,9 @@ __device__ __forceinline__ void gmb_tok_fwd(int N, int HT, const GmTokW &tw, con
         q += d * d;
     }
     rstd = 1.f / sqrtf(q / (float)N + 1e-5f);
+    float xn[GM_MT], h[GM_MT / 2];
+#pragma unroll
+    for (int t = 0; t < GM_MT; ++t) xn[t] = t < N ? (av[t] - mean) * rstd * tw.lg[t] + tw.lb[t] : 0.f;
 #pragma unroll
     for (int k = 0; k < GM_MT / 2; ++k) {
         float acc = 0.f;
@@ -886,9 +889,10 @@ __device__ __forceinline__ void gmb_tok_fwd(int N, int HT, const GmTokW &tw, con
             acc = tw.b1[k];
 #pragma unroll
             for (int t = 0; t < GM_MT; ++t)
-                if (t < N) acc += tw.w1[k * N + t] * ((av[t] - mean) * rstd * tw.lg[t] + tw.lb[t]);
+                if (t < N) acc += tw.w1[k * N + t] * xn[t];
         }
         z1[k] = acc;
+        h[k] = k < HT ? gm_gelu(acc) : 0.f;
     }
 #pragma unroll
     for (int t = 0; t < GM_MT; ++t) {
@@ -897,7 +901,7 @@ __device__ __forceinline__ void gmb_tok_fwd(int N, int HT, const GmTokW &tw, con
             acc = tw.b2[t];
 #pragma unroll
             for (int k = 0; k < GM_MT / 2; ++k)
-                if (k < HT) acc += tw.w2[t * HT + k] * gm_gelu(z1[k]);
+                if (k < HT) acc += tw.w2[t * HT + k] * h[k];
         }
         y[t] = acc;
     }
