@@ -591,6 +591,25 @@ struct WalkLay {
 #define TM_PFP 4
 #endif
 constexpr int PFP = TM_PFP;
+// walk_kernel: node-feature rows loaded tile by tile inside event_gcn's first layer (1) or all before
+// lin_event's K loop (0); waves per SIMD the kernel is compiled for
+#ifndef TM_JIT_NODES
+#define TM_JIT_NODES 1
+#endif
+#ifndef TM_WALK_WAVES
+#define TM_WALK_WAVES 2
+#endif
+// waves per walk_kernel workgroup: each wave owns its 16 slots and a 12.25 KB LDS stash, the workgroup one
+// constant table; 3 waves per SIMD need one 12-wave workgroup per CU (three 4-wave ones exceed the LDS)
+// table mode: the next pass's edge-table row requested a pass ahead (1; 44 VGPRs live through the head) or
+// at the start of its own pass (0)
+#ifndef TM_ET_PREFETCH
+#define TM_ET_PREFETCH 1
+#endif
+#ifndef TM_WALK_WPB
+#define TM_WALK_WPB 4
+#endif
+constexpr int WALK_WPB = TM_WALK_WPB;
 template <int NTO, int NQ>
 struct PairOrder {   // fragment i of the pair order -> (tile, K step)
     static constexpr int NP = NTO / 2, NPF = 2 * NP * NQ;
@@ -891,7 +910,9 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
     const float dt = pi.dt, c0 = pi.c0, c1 = pi.c1, c2 = pi.c2;
     const float4 *nrow_s = reinterpret_cast<const float4 *>(a.n_feat + (int64_t)pi.ns * dn);
     const float4 *nrow_t = reinterpret_cast<const float4 *>(a.n_feat + (int64_t)pi.nt * dn);
+#if !TM_JIT_NODES
     float4 xs[NTD], xt[NTD];
+#endif
     floatx4 L[NTD];
     if constexpr (ETAB) {
 #pragma unroll
@@ -905,6 +926,7 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
 #pragma unroll
         for (int t = 0; t < NTD; ++t) L[t] = ldsx4(bias, t);
     }
+#if !TM_JIT_NODES
 #pragma unroll
     for (int t = 0; t < NTD; ++t) {
         const int f4 = (t < NTD - 1) ? 4 * t + g : min(4 * t + g, dn / 4 - 1);
@@ -915,6 +937,7 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
         const int f4 = (t < NTD - 1) ? 4 * t + g : min(4 * t + g, dn / 4 - 1);
         xt[t] = nrow_t[f4];
     }
+#endif
     TM_STAMP(1);
     {
         const int vo = lane_id() * 16;
@@ -1024,6 +1047,65 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
         }
     }
     TM_STAMP(2);
+#if TM_JIT_NODES
+    // event_gcn's first layer K-outer: K step q of A = x_s + relu(x_t + L), B = x_t + relu(x_s + L) (:93-96,
+    // lin_event shared) is built from node-row tile q just before its MFMAs, the node tiles requested
+    // JN - 1 steps ahead and the step's 4 weight fragments one step ahead (the two branches share them).
+    // The node rows are never all live at once (and not during lin_event's K loop).  Each output tile
+    // accumulates its K steps in the same order as cgemm2 (same results).
+    floatx4 Hs[4], Ht[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        Hs[t] = ldsx4(cs + C::G1, t);
+        Ht[t] = ldsx4(cs + C::G1C, t);
+    }
+    {
+        constexpr int JN = 3;
+        const int vo = lane_id() * 16;
+        float4 rs[JN], rt[JN], wq[2][4];
+        auto nload = [&](int q) {
+            const int f4 = (q < NTD - 1) ? 4 * q + g : min(4 * q + g, dn / 4 - 1);
+            rs[q % JN] = nrow_s[f4];
+            rt[q % JN] = nrow_t[f4];
+        };
+#pragma unroll
+        for (int q = 0; q < JN - 1 && q < NTD; ++q) nload(q);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) wq[0][t] = wload(wr, vo, LY::G1 / 4 + (t * NTD) * 64);
+#pragma unroll
+        for (int q = 0; q < NTD; ++q) {
+            if (q + JN - 1 < NTD) nload(q + JN - 1);
+            if (q + 1 < NTD) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) wq[(q + 1) & 1][t] = wload(wr, vo, LY::G1 / 4 + (t * NTD + q + 1) * 64);
+            }
+            const float4 xs4 = rs[q % JN], xt4 = rt[q % JN];
+            const float sv[4] = {xs4.x, xs4.y, xs4.z, xs4.w}, tv[4] = {xt4.x, xt4.y, xt4.z, xt4.w};
+            floatx4 A, Bq;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float l = L[q][r];
+                A[r] = sv[r] + relu(tv[r] + l);
+                Bq[r] = tv[r] + relu(sv[r] + l);
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float4 w = wq[q & 1][t];
+                Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, A.x, Hs[t], 0, 0, 0);
+                Ht[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, Bq.x, Ht[t], 0, 0, 0);
+                Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, A.y, Hs[t], 0, 0, 0);
+                Ht[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, Bq.y, Ht[t], 0, 0, 0);
+                Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, A.z, Hs[t], 0, 0, 0);
+                Ht[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, Bq.z, Ht[t], 0, 0, 0);
+                Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, A.w, Hs[t], 0, 0, 0);
+                Ht[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, Bq.w, Ht[t], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    TM_STAMP(3);
+    TM_STAMP(4);
+#else
     // A = x_s + relu(x_t + L), B = x_t + relu(x_s + L)   (event_gcn :93-96, lin_event shared)
     floatx4 A[NTD], Bv[NTD];
 #pragma unroll
@@ -1045,6 +1127,7 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
     }
     cgemm2<4, NTD, LY::G1>(wr, A, Bv, Hs, Ht);
     TM_STAMP(4);
+#endif
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         H[t] = relu4(Hs[t]);
@@ -1142,7 +1225,7 @@ __device__ __forceinline__ float score_dot(const Stash &st, const floatx4 (&H)[8
 }
 
 template <int NQE, int NTD, bool SEF = false, int QE0 = 0>
-__global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
+__global__ void __launch_bounds__(64 * WALK_WPB, 4 * TM_WALK_WAVES / WALK_WPB) walk_kernel(WalkArgs a) {
     using C = WalkConsts<NQE, NTD>;
     const EncW &P = a.P;
     const int lane = threadIdx.x & 63, col = lane & 15;
@@ -1153,7 +1236,7 @@ __global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
     const int64_t eg = valid ? gs / NS : 0;             // (group, event) row
     const int32_t j = valid ? (int32_t)(gs % NS) : 0;
     // LDS: per-wave stash of the slot's position-2 results (12.25 KB per wave), then the constant table
-    __shared__ Stash stash[4];
+    __shared__ Stash stash[WALK_WPB];
     __shared__ float4 cs4[(C::SIZE + 3) / 4];
     float *cs = reinterpret_cast<float *>(cs4);
     load_consts<NQE, NTD>(P, cs);
@@ -1169,7 +1252,7 @@ __global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
     float ef[EQ_MAX][4] = {};
     float4 et[ETAB_N(QE0)];
     if constexpr (QE0 == 0) load_ef(a, cur.e, ef);
-    else load_et<QE0>(a, cur.e, et);
+    else if (TM_ET_PREFETCH) load_et<QE0>(a, cur.e, et);
 #ifdef TM_STAMPS
     const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) atomicMax(&g_st[2][9], atomicAdd(&g_live, 1ull) + 1);   // waves resident at once (max)
@@ -1195,9 +1278,10 @@ __global__ void __launch_bounds__(256, 2) walk_kernel(WalkArgs a) {
         floatx4 H[8];
         unsigned long long T[10];
         TM_STAMP(0);
+        if constexpr (QE0 > 0 && !TM_ET_PREFETCH) load_et<QE0>(a, cur.e, et);
         encode_position<NQE, NTD, SEF, QE0>(a, wr, cs, cur, ef, et, p, H, T);
         if constexpr (QE0 == 0) load_ef(a, nxt.e, ef);
-        else load_et<QE0>(a, nxt.e, et);
+        else if (TM_ET_PREFETCH) load_et<QE0>(a, nxt.e, et);
         cur = nxt;
         TM_STAMP(6);
         if (p == 2) {
@@ -1716,7 +1800,7 @@ static void launch_head(const EncW &P, int64_t n_walks, int64_t walks_per_group,
 
 template <int NQE, bool SEF = false, int Q0 = 0>
 static void launch_walk(const WalkArgs &a, unsigned blocks, hipStream_t s) {
-    walk_kernel<NQE, 11, SEF, Q0><<<dim3(blocks), 256, 0, s>>>(a);
+    walk_kernel<NQE, 11, SEF, Q0><<<dim3(blocks), 64 * WALK_WPB, 0, s>>>(a);
 }
 
 extern "C" int tm_encoder_fwd(const tm_weights *w, const float *n_feat, const float *e_feat, int32_t n_groups,
@@ -1775,7 +1859,7 @@ static int encoder_fwd_impl(const tm_weights *w, const float *n_feat, const floa
         const int64_t n_slots = n_walks / M;
         const int64_t units = (n_slots + 15) / 16;
         WalkArgs a{P, n_slots, W, M, B * W, n_feat, e_feat, node6, eid3, cat, ts3, cnt, stdv, cut, out_imp, etab};
-        const unsigned blocks = (unsigned)((units + 3) / 4);
+        const unsigned blocks = (unsigned)((units + WALK_WPB - 1) / WALK_WPB);
         const int q0 = etab ? etab_q0(P) : 0;
         pe = prof_begin(s);
         if (q0 == 2) {        // edge table: lin_event from K step 2
