@@ -1141,6 +1141,9 @@ __global__ void __launch_bounds__(256) gm_bwd_kernel(GmArgs a, GmBwd b) {
         const float *const *w = b.lw + GMB_LW * l;
         const float *XI = XL + l * IMG;
         const GmTokW tw = stage_layer(l);
+        // out1's padding (tokens >= N, channels >= C) must read as 0: the channel FFN's A fragments and its
+        // LayerNorm (weight 0 there) multiply whatever the LDS holds
+        for (int i = tid; i < IMG; i += blockDim.x) O1[i] = 0.f;
         __syncthreads();
         token_mix(tw, XI, O1);                                    // out1
         // DY = G ew (d channel-FFN output)

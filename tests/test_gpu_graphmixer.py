@@ -100,7 +100,7 @@ def test_config5_dims_and_gradient_vs_oracle(dev):
     assert getattr(m, "_gmb_key", None) is not None, "the HIP explanation-weight backward did not run"
 
 
-@pytest.mark.parametrize("N,C,L", [(30, 172, 2), (12, 172, 2), (20, 32, 1), (16, 100, 3)])
+@pytest.mark.parametrize("N,C,L", [(30, 172, 2), (12, 172, 2), (20, 32, 1), (16, 100, 3), (20, 1, 3)])
 def test_hip_ew_gradient_vs_oracle(dev, N, C, L):
     """tm_gm_embed_bwd (the explainer's training signal through a frozen GraphMixer): d ew of a BCE loss on
     contrast's logits vs fp64 autograd through the oracle, for one / two token tiles, channel counts with and

@@ -272,3 +272,39 @@ def test_run_steps_overlap_equals_serial(dev):
     np.testing.assert_allclose(runs[1][0], runs[0][0], rtol=2e-3)
     for k, v in runs[0][1].items():
         assert float((runs[1][1][k] - v).abs().max()) <= 1e-2, k
+
+
+@pytest.mark.parametrize("if_bern", [False, True])
+def test_train_step_through_graphmixer_hip_equals_torch(dev, if_bern):
+    """The explainer's training step with a GraphMixer base (temp_exp_main.py:605-632, base_type
+    'graphmixer'): the explanation weights' gradient through tm_gm_embed_bwd gives the same losses and
+    explainer gradients as the torch formulation of the frozen base under autograd (TEMPME_GM_TORCH=1),
+    deterministic (Beta mean) and with rsample (same RNG state both times)."""
+    from tests.test_graphmixer_oracle import build
+    from tempme_amd.train import train_step
+    _, ex, batch, opt = _setup("uslegis", dev)
+    gm = build("uslegis").to(dev)
+    p0 = {k: v.detach().clone() for k, v in ex.named_parameters()}
+    res = {}
+    for mode in ("hip", "torch"):
+        with torch.no_grad():
+            for k, v in ex.named_parameters():
+                v.copy_(p0[k])
+        opt.zero_grad(set_to_none=True)
+        ex.eval()
+        os.environ["TEMPME_GM_TORCH"] = "1" if mode == "torch" else "0"
+        try:
+            torch.manual_seed(123)
+            out = train_step(ex, gm, opt, batch, beta=0.5, prior_p=0.3, if_bern=if_bern)
+        finally:
+            os.environ.pop("TEMPME_GM_TORCH", None)
+        res[mode] = (out["loss"].item(), {k: v.grad.detach().clone() for k, v in ex.named_parameters()
+                                          if v.grad is not None})
+        if mode == "hip":
+            assert getattr(gm, "_gmb_key", None) is not None, "the HIP explanation-weight backward did not run"
+    (lh, gh), (lt, gt) = res["hip"], res["torch"]
+    np.testing.assert_allclose(lh, lt, rtol=1e-5, atol=1e-6)
+    assert gh.keys() == gt.keys() and len(gh) > 0
+    for k in gh:
+        d, n = float((gh[k] - gt[k]).norm()), float(gt[k].norm())
+        assert d <= 1e-4 * n + 1e-9, (k, d, n)
