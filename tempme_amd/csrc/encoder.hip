@@ -610,6 +610,13 @@ constexpr int PFP = TM_PFP;
 #define TM_WALK_WPB 4
 #endif
 constexpr int WALK_WPB = TM_WALK_WPB;
+// persistent walk_kernel waves (1: the grid is one round of resident workgroups looping over the units)
+#ifndef TM_WALK_PERSIST
+#define TM_WALK_PERSIST 0
+#endif
+#ifndef TM_WALK_OFFSET
+#define TM_WALK_OFFSET 0
+#endif
 template <int NTO, int NQ>
 struct PairOrder {   // fragment i of the pair order -> (tile, K step)
     static constexpr int NP = NTO / 2, NPF = 2 * NP * NQ;
@@ -656,6 +663,71 @@ __device__ __forceinline__ void cgemm(__amdgpu_buffer_rsrc_t wr, const floatx4 (
             __builtin_amdgcn_sched_barrier(0);
         }
     }
+}
+
+// Cross-phase weight prefetch: every GEMM phase of a pass starts with its first PFP fragments already in
+// registers.  The previous phase loads them into its ring slots as they free up (its last PFP refills), so
+// the L2 latency of a phase's first fragments overlaps the previous phase's MFMAs instead of stalling at
+// every phase start; the pass's last GEMM prefetches the next pass's lin_event fragments.
+static_assert(PFP == 4, "the phase hand-off carries 4 fragments (pair order: (t0,q0) (t1,q0) (t0,q1) (t1,q1))");
+struct NextFr {
+    int o[PFP];   // float4 offsets of the next phase's first PFP fragments (wave-uniform)
+};
+// fragment k < 4 of a cgemm in pair order, pack with NQL K steps at float4 offset base
+template <int NQL>
+__device__ __forceinline__ NextFr pair_first(int base) {
+    return NextFr{{base, base + NQL * 64, base + 64, base + NQL * 64 + 64}};
+}
+
+// cgemm whose first PFP fragments come in `pre`; on return `pre` holds the next phase's first PFP fragments
+// (nx), loaded into the ring slots of this GEMM's last PFP fragments
+template <int NTO, int NQ, int NQL, int BASE>
+__device__ __forceinline__ void cgemm_p(__amdgpu_buffer_rsrc_t wr, const floatx4 (&x)[NQ], floatx4 (&o)[NTO],
+                                        float4 (&pre)[PFP], const NextFr &nx) {
+    using O = PairOrder<NTO, NQ>;
+    const int vo = lane_id() * 16;
+    constexpr int N = NTO * NQ, D = PFP;
+    static_assert(N >= D, "a phase shorter than the ring");
+    auto off = [](int i) { return BASE / 4 + (O::t(i) * NQL + O::q(i)) * 64; };
+    float4 buf[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) buf[i] = pre[i];
+    auto refill = [&](int i) {   // slot i % D: fragment i + D of this GEMM, else the next phase's
+        if (i + D < N) buf[i % D] = wload(wr, vo, off(i + D));
+        else buf[i % D] = wload(wr, vo, nx.o[i + D - N]);
+    };
+#pragma unroll
+    for (int k = 0; k < O::NP * NQ; ++k) {
+        const int i = 2 * k, t = O::t(i), q = O::q(i);
+        const float4 w0 = buf[i % D];
+        refill(i);
+        const float4 w1 = buf[(i + 1) % D];
+        refill(i + 1);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0.x, x[q].x, o[t], 0, 0, 0);
+        o[t + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.x, x[q].x, o[t + 1], 0, 0, 0);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0.y, x[q].y, o[t], 0, 0, 0);
+        o[t + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.y, x[q].y, o[t + 1], 0, 0, 0);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0.z, x[q].z, o[t], 0, 0, 0);
+        o[t + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.z, x[q].z, o[t + 1], 0, 0, 0);
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0.w, x[q].w, o[t], 0, 0, 0);
+        o[t + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.w, x[q].w, o[t + 1], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (NTO % 2) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int i = O::NPF + q;
+            const float4 w = buf[i % D];
+            refill(i);
+            o[NTO - 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, x[q].x, o[NTO - 1], 0, 0, 0);
+            o[NTO - 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, x[q].y, o[NTO - 1], 0, 0, 0);
+            o[NTO - 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, x[q].z, o[NTO - 1], 0, 0, 0);
+            o[NTO - 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, x[q].w, o[NTO - 1], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) pre[k] = buf[(N + k) % D];
 }
 
 // two column sets through the same weight fragments (one load feeds 8 MFMAs)
@@ -899,7 +971,7 @@ template <int NQE, int NTD, bool SEF, int Q0 = 0>
 __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buffer_rsrc_t wr, const float *cs,
                                                 const PosIn &pi, const float (&ef)[EQ_MAX][4],
                                                 const float4 (&et)[ETAB_N(Q0)], int p, floatx4 (&H)[8],
-                                                unsigned long long (&T)[10]) {
+                                                float4 (&pre)[PFP], const NextFr &nx, unsigned long long (&T)[10]) {
     constexpr bool ETAB = Q0 > 0;
     static_assert(!(ETAB && SEF), "table mode replaces the streamed edge features");
     using C = WalkConsts<NQE, NTD>;
@@ -944,9 +1016,12 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
         constexpr int nq = NQE;
         constexpr int N = NTD * (NQE - Q0), D = PFP;
         constexpr int EVF4 = LY::EV / 4;
+        // the first D fragments (EVF4 + ((i % NTD) * nq + Q0 + i / NTD) * 64) come in pre, requested during
+        // the previous pass; the ring's last D refills request event_gcn's first K step (G1 tiles 0..3)
         float4 buf[D];
 #pragma unroll
-        for (int i = 0; i < D; ++i) buf[i] = wload(wr, vo, EVF4 + ((i % NTD) * nq + Q0 + i / NTD) * 64);
+        for (int i = 0; i < D; ++i) buf[i] = pre[i];
+        auto g1f = [](int k) { return LY::G1 / 4 + k * NTD * 64; };
         const int qend = p == 2 ? P.qt : NQE;            // slot pass: steps >= qt folded into evc / devc
         if constexpr (SEF) {
             const float4 *erow4 = reinterpret_cast<const float4 *>(a.e_feat + (int64_t)pi.e * de);
@@ -1006,8 +1081,9 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
                                 xn[t] = gen_one<ETAB, false>(q + 1, t, wq[t], pq[t], ef, g, de, dt, c0, c1, c2);
                         }
                     };
-                    auto wnext = [&](int i) {   // fragment i + D of the ring into slot i % D
+                    auto wnext = [&](int i) {   // fragment i + D of the ring into slot i % D (past N: G1's)
                         if (i + D < N) buf[i % D] = wload(wr, vo, EVF4 + (((i + D) % NTD) * nq + Q0 + (i + D) / NTD) * 64);
+                        else buf[i % D] = wload(wr, vo, g1f(i + D - N));
                     };
                     // tile pairs with interleaved MFMAs (no MFMA waits on its predecessor); an odd last tile alone
 #pragma unroll
@@ -1045,6 +1121,14 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
                 }
             }
         }
+        // G1's first fragments: in the ring's slots after a full K loop; the slot pass (K loop cut at qt) and
+        // the streamed-edge-feature loop request them now
+        if (SEF || p == 2) {
+#pragma unroll
+            for (int k = 0; k < D; ++k) buf[(N + k) % D] = wload(wr, vo, g1f(k));
+        }
+#pragma unroll
+        for (int k = 0; k < D; ++k) pre[k] = buf[(N + k) % D];
     }
     TM_STAMP(2);
 #if TM_JIT_NODES
@@ -1071,13 +1155,16 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
 #pragma unroll
         for (int q = 0; q < JN - 1 && q < NTD; ++q) nload(q);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) wq[0][t] = wload(wr, vo, LY::G1 / 4 + (t * NTD) * 64);
+        for (int t = 0; t < 4; ++t) wq[0][t] = pre[t];
 #pragma unroll
         for (int q = 0; q < NTD; ++q) {
             if (q + JN - 1 < NTD) nload(q + JN - 1);
             if (q + 1 < NTD) {
 #pragma unroll
                 for (int t = 0; t < 4; ++t) wq[(q + 1) & 1][t] = wload(wr, vo, LY::G1 / 4 + (t * NTD + q + 1) * 64);
+            } else {                                     // the last step: the next phase's first fragments
+#pragma unroll
+                for (int t = 0; t < 4; ++t) wq[(q + 1) & 1][t] = wload(wr, vo, nx.o[t]);
             }
             const float4 xs4 = rs[q % JN], xt4 = rt[q % JN];
             const float sv[4] = {xs4.x, xs4.y, xs4.z, xs4.w}, tv[4] = {xt4.x, xt4.y, xt4.z, xt4.w};
@@ -1102,6 +1189,8 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
             }
             __builtin_amdgcn_sched_barrier(0);
         }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) pre[t] = wq[NTD & 1][t];
     }
     TM_STAMP(3);
     TM_STAMP(4);
@@ -1126,6 +1215,11 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
         Ht[t] = ldsx4(cs + C::G1C, t);
     }
     cgemm2<4, NTD, LY::G1>(wr, A, Bv, Hs, Ht);
+    {
+        const int vo = lane_id() * 16;
+#pragma unroll
+        for (int k = 0; k < PFP; ++k) pre[k] = wload(wr, vo, nx.o[k]);
+    }
     TM_STAMP(4);
 #endif
 #pragma unroll
@@ -1163,7 +1257,8 @@ struct Stash {
 template <int NQE, int NTD>
 __device__ __forceinline__ void walk_head(const WalkArgs &a, __amdgpu_buffer_rsrc_t wr, const float *cs, int64_t gw,
                                           bool valid, const HeadIn &hi, const Stash &st, float s0, float s1,
-                                          const floatx4 (&R0)[4], const floatx4 (&R1)[4]) {
+                                          const floatx4 (&R0)[4], const floatx4 (&R1)[4], float4 (&pre)[PFP],
+                                          const NextFr &nx_end) {
     using C = WalkConsts<NQE, NTD>;
     using LY = WalkLay<NQE>;
     const EncW &P = a.P;
@@ -1194,13 +1289,13 @@ __device__ __forceinline__ void walk_head(const WalkArgs &a, __amdgpu_buffer_rsr
         const float4 b = *reinterpret_cast<const float4 *>(cs + C::TC + 80 * c + 16 * t + 4 * g);
         M1[t] = floatx4{b.x, b.y, b.z, b.w};
     }
-    cgemm<5, 4, 4, FoldLay::M1A2>(wr, X, M1);
+    cgemm_p<5, 4, 4, FoldLay::M1A2>(wr, X, M1, pre, pair_first<5>(LY::M2 / 4));
 #pragma unroll
     for (int t = 0; t < 5; ++t) M1[t] = relu4(M1[t]);
     floatx4 M2[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) M2[t] = ldsx4(cs + C::M2, t);
-    cgemm<4, 5, 5, LY::M2>(wr, M1, M2);
+    cgemm_p<4, 5, 5, LY::M2>(wr, M1, M2, pre, nx_end);
     float z = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -1229,19 +1324,43 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * TM_WALK_WAVES / WALK_WPB) w
     using C = WalkConsts<NQE, NTD>;
     const EncW &P = a.P;
     const int lane = threadIdx.x & 63, col = lane & 15;
-    const int64_t unit = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const int64_t gs = unit * 16 + col;                 // this column's hop-1 slot
-    const bool valid = gs < a.n_slots;
     const int32_t NS = a.W / a.M;
-    const int64_t eg = valid ? gs / NS : 0;             // (group, event) row
-    const int32_t j = valid ? (int32_t)(gs % NS) : 0;
+    const int64_t n_units = (a.n_slots + 15) / 16;
+#if TM_WALK_PERSIST
+    // persistent waves: the grid is one round of resident workgroups; wave w takes units w, w + stride, ...
+    // (the constant table is loaded once per workgroup, the next unit's first scalars and table row are
+    // requested during the last pass of the current one)
+    const int64_t ustride = (int64_t)gridDim.x * (blockDim.x >> 6);
+#else
+    const int64_t ustride = n_units;                    // one unit per wave
+#endif
+    int64_t unit = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    // this column's hop-1 slot of unit u: (group, event) row and slot within it
+    auto coords = [&](int64_t u, bool &v, int64_t &eg_, int32_t &j_) {
+        const int64_t gs = u * 16 + col;
+        v = u < n_units && gs < a.n_slots;
+        eg_ = v ? gs / NS : 0;
+        j_ = v ? (int32_t)(gs % NS) : 0;
+    };
+    bool valid;
+    int64_t eg;
+    int32_t j;
+    coords(unit, valid, eg, j);
     // LDS: per-wave stash of the slot's position-2 results (12.25 KB per wave), then the constant table
     __shared__ Stash stash[WALK_WPB];
     __shared__ float4 cs4[(C::SIZE + 3) / 4];
     float *cs = reinterpret_cast<float *>(cs4);
     load_consts<NQE, NTD>(P, cs);
     __syncthreads();
-    if (unit * 16 >= a.n_slots) return;                 // whole wave idle (wave-uniform)
+    if (unit >= n_units) return;                        // whole wave idle (wave-uniform)
+#if TM_WALK_PERSIST && TM_WALK_OFFSET
+    // the upper half of a workgroup's waves (wave w shares its SIMD with wave w - WPB/2) starts
+    // TM_WALK_OFFSET real-time ticks (100 MHz) late, so the two waves of a SIMD run out of phase
+    if ((threadIdx.x >> 6) >= WALK_WPB / 2) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)TM_WALK_OFFSET) __builtin_amdgcn_s_sleep(127);
+    }
+#endif
     Stash &st = stash[threadIdx.x >> 6];
     // every weight fragment off one buffer resource (WalkLay offsets from the folded region's base)
     const auto wr = wrsrc(P.kv.w);
@@ -1251,12 +1370,26 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * TM_WALK_WAVES / WALK_WPB) w
     PosIn cur = load_pos(a, eg * a.W + (int64_t)j * a.M, 2, valid);
     float ef[EQ_MAX][4] = {};
     float4 et[ETAB_N(QE0)];
+    // lin_event's first PFP fragments (ring order: tile k % NTD, K step QE0 + k / NTD), carried pass to pass
+    NextFr lin0;
+#pragma unroll
+    for (int k = 0; k < PFP; ++k) lin0.o[k] = WalkLay<NQE>::EV / 4 + ((k % NTD) * NQE + QE0 + k / NTD) * 64;
+    float4 pre[PFP];
+#pragma unroll
+    for (int k = 0; k < PFP; ++k) pre[k] = wload(wr, lane_id() * 16, lin0.o[k]);
     if constexpr (QE0 == 0) load_ef(a, cur.e, ef);
     else if (TM_ET_PREFETCH) load_et<QE0>(a, cur.e, et);
 #ifdef TM_STAMPS
     const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) atomicMax(&g_st[2][9], atomicAdd(&g_live, 1ull) + 1);   // waves resident at once (max)
 #endif
+#pragma nounroll
+    for (;;) {
+    const int64_t unext = unit + ustride;
+    bool vn;
+    int64_t egn;
+    int32_t jn;
+    coords(unext, vn, egn, jn);
     // pass 0: position 2 once per slot (walk j*M carries it); then per walk m: position 0, position 1
 #pragma nounroll
     for (int pass = 0; pass < n_pass; ++pass) {
@@ -1271,15 +1404,18 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * TM_WALK_WAVES / WALK_WPB) w
             hi.t1 = a.ts3[gw * 3 + 1];
             hi.c = a.cat[gw];
         }
-        // next pass's scalars now; its edge features / table row once this pass's lin_event is done
-        const int pn = pass + 1 < n_pass ? ((pass & 1) == 0 ? 0 : 1) : 0;
-        const int64_t gwn = eg * a.W + (int64_t)j * a.M + (pass >> 1);
-        const PosIn nxt = load_pos(a, gwn, pn, valid && pass + 1 < n_pass);
+        // next pass's scalars now (after the last pass: the next unit's slot pass); its edge features / table
+        // row once this pass's lin_event is done
+        const bool last = pass + 1 == n_pass;
+        const int pn = !last ? ((pass & 1) == 0 ? 0 : 1) : 2;
+        const int64_t gwn = !last ? eg * a.W + (int64_t)j * a.M + (pass >> 1) : egn * a.W + (int64_t)jn * a.M;
+        const PosIn nxt = load_pos(a, gwn, pn, !last ? valid : vn);
         floatx4 H[8];
         unsigned long long T[10];
         TM_STAMP(0);
         if constexpr (QE0 > 0 && !TM_ET_PREFETCH) load_et<QE0>(a, cur.e, et);
-        encode_position<NQE, NTD, SEF, QE0>(a, wr, cs, cur, ef, et, p, H, T);
+        encode_position<NQE, NTD, SEF, QE0>(a, wr, cs, cur, ef, et, p, H, pre,
+                                            pair_first<8>(p == 2 ? FoldLay::A1D / 4 : FoldLay::A1G / 4), T);
         if constexpr (QE0 == 0) load_ef(a, nxt.e, ef);
         else if (TM_ET_PREFETCH) load_et<QE0>(a, nxt.e, et);
         cur = nxt;
@@ -1289,11 +1425,11 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * TM_WALK_WAVES / WALK_WPB) w
             floatx4 P2[4];
 #pragma unroll
             for (int t = 0; t < 4; ++t) P2[t] = ldsx4(cs + C::CP, t);
-            cgemm<4, 8, 8, FoldLay::A1D>(wr, H, P2);
+            cgemm_p<4, 8, 8, FoldLay::A1D>(wr, H, P2, pre, pair_first<8>(FoldLay::KV / 4));
             floatx4 V[8];
 #pragma unroll
             for (int t = 0; t < 8; ++t) V[t] = ldsx4(cs + C::V0, t);
-            cgemm<8, 8, 8, FoldLay::KV>(wr, H, V);
+            cgemm_p<8, 8, 8, FoldLay::KV>(wr, H, V, pre, lin0);
             TM_STAMP(7);
             float cw = 0.f;
 #pragma unroll
@@ -1315,7 +1451,7 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * TM_WALK_WAVES / WALK_WPB) w
             floatx4 R[4];
 #pragma unroll
             for (int t = 0; t < 4; ++t) R[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-            cgemm<4, 8, 8, FoldLay::A1G>(wr, H, R);
+            cgemm_p<4, 8, 8, FoldLay::A1G>(wr, H, R, pre, p == 1 ? pair_first<4>(FoldLay::M1A2 / 4) : lin0);
             const float s = score_dot(st, H);
             TM_STAMP(7);
             if (p == 0) {
@@ -1323,7 +1459,7 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * TM_WALK_WAVES / WALK_WPB) w
                 for (int t = 0; t < 4; ++t) R0[t] = R[t];
                 s0 = s;
             } else {
-                walk_head<NQE, NTD>(a, wr, cs, gw, valid, hi, st, s0, s, R0, R);
+                walk_head<NQE, NTD>(a, wr, cs, gw, valid, hi, st, s0, s, R0, R, pre, lin0);
             }
         }
         TM_STAMP(8);
@@ -1333,6 +1469,12 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * TM_WALK_WAVES / WALK_WPB) w
             atomicAdd(&g_st[p][8], 1ull);
         }
 #endif
+    }
+    unit = unext;
+    if (unit >= n_units) break;                         // wave-uniform: every wave leaves after its last unit
+    valid = vn;
+    eg = egn;
+    j = jn;
     }
 #ifdef TM_STAMPS
     // in-kernel clock: shader-clock ticks over 100 MHz real-time ticks of the wave's pass loop
@@ -1800,6 +1942,24 @@ static void launch_head(const EncW &P, int64_t n_walks, int64_t walks_per_group,
 
 template <int NQE, bool SEF = false, int Q0 = 0>
 static void launch_walk(const WalkArgs &a, unsigned blocks, hipStream_t s) {
+#if TM_WALK_PERSIST
+    // one round of resident workgroups (occupancy x CUs of the current device), cached per instance
+    static int cap[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+        if (cap[dev] == 0) {
+            int per_cu = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, walk_kernel<NQE, 11, SEF, Q0>, 64 * WALK_WPB, 0) ==
+                    hipSuccess &&
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && per_cu > 0 &&
+                cus > 0)
+                cap[dev] = per_cu * cus;
+            else
+                cap[dev] = -1;
+        }
+        if (cap[dev] > 0 && blocks > (unsigned)cap[dev]) blocks = (unsigned)cap[dev];
+    }
+#endif
     walk_kernel<NQE, 11, SEF, Q0><<<dim3(blocks), 64 * WALK_WPB, 0, s>>>(a);
 }
 

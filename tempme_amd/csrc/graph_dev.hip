@@ -372,9 +372,10 @@ int tm_graph_build_edges_device(int32_t V, int64_t n_edges, const int64_t *src, 
             e = e ? e : incl_scan(t, hpos, bstart, n, rocprim::maximum<int32_t>(), s);
             e = e ? e : incl_scan(t, hflag, bincl, n, rocprim::plus<int32_t>(), s);
             int32_t nb = 0;
-            e = e ? e : hipMemcpyAsync(&nb, bincl + (n - 1), sizeof(int32_t), hipMemcpyDeviceToHost, s);
-            e = e ? e : hipStreamSynchronize(s);
-            if (n == 0) nb = 0;
+            if (n > 0) {
+                e = e ? e : hipMemcpyAsync(&nb, bincl + (n - 1), sizeof(int32_t), hipMemcpyDeviceToHost, s);
+                e = e ? e : hipStreamSynchronize(s);
+            }
             int32_t *bn = t.get<int32_t>(nb), *bu = t.get<int32_t>(nb), *bx = t.get<int32_t>(nb), *bs = t.get<int32_t>(nb),
                     *rl = t.get<int32_t>(nb), *rbase = t.get<int32_t>(nb);
             e = e ? e : t.e;

@@ -73,6 +73,10 @@ for s in "$@"; do
         dropint) step dropint 300 python tools/dropin_timing.py ;;
         dropintrace) step dropintrace 300 rocprofv3 --kernel-trace -d gpurun_out/ditrace -o run --output-format csv -- python tools/dropin_timing.py ;;
         dropinprof) TEMPME_DROPIN_PROFILE=1 step dropinprof 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+        abtests:*)  # the GPU suite against tempme_amd/lib/ab/<name>.so
+            n=${s#abtests:}
+            TEMPME_LIB="$PWD/tempme_amd/lib/ab/$n.so" step pytest_ab_$n 600 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread ;;
+        wab) step wab 1200 ./tools/walk_ab.sh ;;
         k:*) step pytest_k 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread -k "${s#k:}" ;;
         micro:*) m=${s#micro:}; step micro_$m 200 ./micro/$m ;;   # a prebuilt micro-benchmark binary
         *) echo "unknown step $s"; exit 2 ;;
