@@ -609,6 +609,22 @@ constexpr int PFP = TM_PFP;
 #ifndef TM_WALK_WPB
 #define TM_WALK_WPB 4
 #endif
+// table mode: the next pass's edge-table row is requested inside event_gcn's K loop at this step (its
+// weights are requested a whole step ahead there, so the row's latency does not stall the weight ring
+// behind it); -1: after the position's encoding (before the folded GEMMs)
+#ifndef TM_ET_STEP
+#define TM_ET_STEP -1
+#endif
+// the next pass's scalars (and the head's inputs of a position-1 pass) are requested inside event_gcn's K
+// loop at this step instead of at the top of the pass, where lin_event's weight refills waited behind them
+#ifndef TM_POS_STEP
+#define TM_POS_STEP 0
+#endif
+static_assert(TM_JIT_NODES || (TM_ET_STEP < 0 && TM_POS_STEP < 0), "in-G1 loads need the K-outer event_gcn loop");
+// lin_event's weight ring depth (fragments in flight; the first PFP come from the previous pass)
+#ifndef TM_LIN_D
+#define TM_LIN_D PFP
+#endif
 constexpr int WALK_WPB = TM_WALK_WPB;
 // persistent walk_kernel waves (1: the grid is one round of resident workgroups looping over the units)
 #ifndef TM_WALK_PERSIST
@@ -616,6 +632,9 @@ constexpr int WALK_WPB = TM_WALK_WPB;
 #endif
 #ifndef TM_WALK_OFFSET
 #define TM_WALK_OFFSET 0
+#endif
+#ifndef TM_WALK_PRIO
+#define TM_WALK_PRIO 0
 #endif
 template <int NTO, int NQ>
 struct PairOrder {   // fragment i of the pair order -> (tile, K step)
@@ -967,10 +986,10 @@ __device__ __forceinline__ void load_et(const WalkArgs &a, int32_t e, float4 (&e
 // zero for those inputs, so they contribute nothing.
 // SEF (streamed edge features, EQ_MAX*16 < de <= 176): ef holds K steps 0 and 1 (loaded during the
 // previous pass); step q + 2's float4 is loaded while step q's MFMAs run.
-template <int NQE, int NTD, bool SEF, int Q0 = 0>
+template <int NQE, int NTD, bool SEF, int Q0, class Extra>
 __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buffer_rsrc_t wr, const float *cs,
                                                 const PosIn &pi, const float (&ef)[EQ_MAX][4],
-                                                const float4 (&et)[ETAB_N(Q0)], int p, floatx4 (&H)[8],
+                                                float4 (&et)[ETAB_N(Q0)], Extra &&extra, int p, floatx4 (&H)[8],
                                                 float4 (&pre)[PFP], const NextFr &nx, unsigned long long (&T)[10]) {
     constexpr bool ETAB = Q0 > 0;
     static_assert(!(ETAB && SEF), "table mode replaces the streamed edge features");
@@ -1014,13 +1033,14 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
     {
         const int vo = lane_id() * 16;
         constexpr int nq = NQE;
-        constexpr int N = NTD * (NQE - Q0), D = PFP;
+        constexpr int N = NTD * (NQE - Q0), D = (SEF ? PFP : TM_LIN_D);
+        static_assert(D >= PFP && D <= N, "lin_event ring depth");
         constexpr int EVF4 = LY::EV / 4;
         // the first D fragments (EVF4 + ((i % NTD) * nq + Q0 + i / NTD) * 64) come in pre, requested during
         // the previous pass; the ring's last D refills request event_gcn's first K step (G1 tiles 0..3)
         float4 buf[D];
 #pragma unroll
-        for (int i = 0; i < D; ++i) buf[i] = pre[i];
+        for (int i = 0; i < D; ++i) buf[i] = i < PFP ? pre[i] : wload(wr, vo, EVF4 + ((i % NTD) * nq + Q0 + i / NTD) * 64);
         auto g1f = [](int k) { return LY::G1 / 4 + k * NTD * 64; };
         const int qend = p == 2 ? P.qt : NQE;            // slot pass: steps >= qt folded into evc / devc
         if constexpr (SEF) {
@@ -1083,7 +1103,7 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
                     };
                     auto wnext = [&](int i) {   // fragment i + D of the ring into slot i % D (past N: G1's)
                         if (i + D < N) buf[i % D] = wload(wr, vo, EVF4 + (((i + D) % NTD) * nq + Q0 + (i + D) / NTD) * 64);
-                        else buf[i % D] = wload(wr, vo, g1f(i + D - N));
+                        else if (i + D - N < PFP) buf[i % D] = wload(wr, vo, g1f(i + D - N));
                     };
                     // tile pairs with interleaved MFMAs (no MFMA waits on its predecessor); an odd last tile alone
 #pragma unroll
@@ -1125,10 +1145,10 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
         // the streamed-edge-feature loop request them now
         if (SEF || p == 2) {
 #pragma unroll
-            for (int k = 0; k < D; ++k) buf[(N + k) % D] = wload(wr, vo, g1f(k));
+            for (int k = 0; k < PFP; ++k) buf[(N + k) % D] = wload(wr, vo, g1f(k));
         }
 #pragma unroll
-        for (int k = 0; k < D; ++k) pre[k] = buf[(N + k) % D];
+        for (int k = 0; k < PFP; ++k) pre[k] = buf[(N + k) % D];
     }
     TM_STAMP(2);
 #if TM_JIT_NODES
@@ -1166,6 +1186,7 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
 #pragma unroll
                 for (int t = 0; t < 4; ++t) wq[(q + 1) & 1][t] = wload(wr, vo, nx.o[t]);
             }
+            extra(q);                                    // the caller's loads placed at step q
             const float4 xs4 = rs[q % JN], xt4 = rt[q % JN];
             const float sv[4] = {xs4.x, xs4.y, xs4.z, xs4.w}, tv[4] = {xt4.x, xt4.y, xt4.z, xt4.w};
             floatx4 A, Bq;
@@ -1361,6 +1382,12 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * TM_WALK_WAVES / WALK_WPB) w
         while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)TM_WALK_OFFSET) __builtin_amdgcn_s_sleep(127);
     }
 #endif
+#if TM_WALK_PRIO == 1
+    // static arbitration priority for one wave of each SIMD pair (the upper half of the workgroup)
+    if ((threadIdx.x >> 6) >= WALK_WPB / 2) __builtin_amdgcn_s_setprio(1);
+#elif TM_WALK_PRIO == 2
+    if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);
+#endif
     Stash &st = stash[threadIdx.x >> 6];
     // every weight fragment off one buffer resource (WalkLay offsets from the folded region's base)
     const auto wr = wrsrc(P.kv.w);
@@ -1397,27 +1424,46 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * TM_WALK_WAVES / WALK_WPB) w
         const int p = pass == 0 ? 2 : ((pass - 1) & 1);
         const int64_t gw = eg * a.W + (int64_t)j * a.M + m;
         HeadIn hi{0.f, 1.f, 0.f, 0.f, -1};
-        if (p == 1 && valid) {                           // issued early, consumed by the head
-            hi.cu = (float)a.cut[eg];
-            hi.sd = a.stdv[gw / a.BW] + 1e-6f;
-            hi.t0 = a.ts3[gw * 3 + 0];
-            hi.t1 = a.ts3[gw * 3 + 1];
-            hi.c = a.cat[gw];
-        }
-        // next pass's scalars now (after the last pass: the next unit's slot pass); its edge features / table
+        auto load_hi = [&]() {                           // consumed by the head
+            if (p == 1 && valid) {
+                hi.cu = (float)a.cut[eg];
+                hi.sd = a.stdv[gw / a.BW] + 1e-6f;
+                hi.t0 = a.ts3[gw * 3 + 0];
+                hi.t1 = a.ts3[gw * 3 + 1];
+                hi.c = a.cat[gw];
+            }
+        };
+        // next pass's scalars (after the last pass: the next unit's slot pass); its edge features / table
         // row once this pass's lin_event is done
         const bool last = pass + 1 == n_pass;
         const int pn = !last ? ((pass & 1) == 0 ? 0 : 1) : 2;
         const int64_t gwn = !last ? eg * a.W + (int64_t)j * a.M + (pass >> 1) : egn * a.W + (int64_t)jn * a.M;
-        const PosIn nxt = load_pos(a, gwn, pn, !last ? valid : vn);
+        PosIn nxt;
+        if constexpr (TM_POS_STEP < 0) {
+            load_hi();
+            nxt = load_pos(a, gwn, pn, !last ? valid : vn);
+        }
+        // loads issued inside event_gcn's K loop (its weights are requested a whole step ahead)
+        auto extra = [&](int q) {
+            if constexpr (TM_POS_STEP >= 0) {
+                if (q == TM_POS_STEP) {
+                    load_hi();
+                    nxt = load_pos(a, gwn, pn, !last ? valid : vn);
+                }
+            }
+            if constexpr (QE0 > 0 && TM_ET_STEP >= 0) {
+                static_assert(TM_ET_STEP > TM_POS_STEP, "the table row needs the next pass's edge id");
+                if (q == TM_ET_STEP) load_et<QE0>(a, nxt.e, et);   // the next pass's table row
+            }
+        };
         floatx4 H[8];
         unsigned long long T[10];
         TM_STAMP(0);
         if constexpr (QE0 > 0 && !TM_ET_PREFETCH) load_et<QE0>(a, cur.e, et);
-        encode_position<NQE, NTD, SEF, QE0>(a, wr, cs, cur, ef, et, p, H, pre,
+        encode_position<NQE, NTD, SEF, QE0>(a, wr, cs, cur, ef, et, extra, p, H, pre,
                                             pair_first<8>(p == 2 ? FoldLay::A1D / 4 : FoldLay::A1G / 4), T);
         if constexpr (QE0 == 0) load_ef(a, nxt.e, ef);
-        else if (TM_ET_PREFETCH) load_et<QE0>(a, nxt.e, et);
+        else if (TM_ET_PREFETCH && !(TM_JIT_NODES && TM_ET_STEP >= 0)) load_et<QE0>(a, nxt.e, et);
         cur = nxt;
         TM_STAMP(6);
         if (p == 2) {
