@@ -2201,25 +2201,25 @@ struct tm_dropin {
 extern "C" void tm_dropin_free(tm_dropin *d) {
     if (!d) return;
     int prev = 0;
-    hipGetDevice(&prev);
-    hipSetDevice(d->device);
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(d->device);
     for (int k = 0; k < tm_dropin::SIDES; ++k)
-        if (d->side[k]) hipStreamSynchronize(d->side[k]);
+        if (d->side[k]) (void)hipStreamSynchronize(d->side[k]);
     for (int k = 0; k < tm_dropin::SIDES; ++k) {
-        if (d->dcut[k]) hipFree(d->dcut[k]);
-        if (d->ws[k]) hipFree(d->ws[k]);
-        if (d->ev_side[k]) hipEventDestroy(d->ev_side[k]);
-        if (d->side[k] && d->own[k]) hipStreamDestroy(d->side[k]);
+        if (d->dcut[k]) (void)hipFree(d->dcut[k]);
+        if (d->ws[k]) (void)hipFree(d->ws[k]);
+        if (d->ev_side[k]) (void)hipEventDestroy(d->ev_side[k]);
+        if (d->side[k] && d->own[k]) (void)hipStreamDestroy(d->side[k]);
     }
     for (int i = 0; i < tm_dropin::SLOTS; ++i) {
-        if (d->copy_ev[i]) hipEventDestroy(d->copy_ev[i]);
+        if (d->copy_ev[i]) (void)hipEventDestroy(d->copy_ev[i]);
         for (int k = 0; k < tm_dropin::SIDES; ++k)
-            if (d->read_ev[i][k]) hipEventDestroy(d->read_ev[i][k]);
+            if (d->read_ev[i][k]) (void)hipEventDestroy(d->read_ev[i][k]);
     }
-    if (d->ev_cur) hipEventDestroy(d->ev_cur);
+    if (d->ev_cur) (void)hipEventDestroy(d->ev_cur);
     free(d->hcopy);
-    if (d->dring) hipFree(d->dring);
-    hipSetDevice(prev);
+    if (d->dring) (void)hipFree(d->dring);
+    (void)hipSetDevice(prev);
     delete d;
 }
 
@@ -2245,7 +2245,7 @@ extern "C" int tm_dropin_create(int32_t device, tm_dropin **out) {
     ok = ok && d->hcopy && hipMalloc(reinterpret_cast<void **>(&d->dring), ring) == hipSuccess;
     for (int k = 0; ok && k < tm_dropin::SIDES; ++k)
         ok = hipMalloc(reinterpret_cast<void **>(&d->dcut[k]), sizeof(double) * 256) == hipSuccess;
-    hipSetDevice(prev);
+    (void)hipSetDevice(prev);
     if (!ok) {
         tm_dropin_free(d);
         return fail(TM_E_HIP, "tm_dropin_create: stream / event / buffer allocation failed");
