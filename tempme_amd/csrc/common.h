@@ -127,6 +127,25 @@ __device__ __forceinline__ T *vptr(T *p) {
     asm volatile("" : "+v"(v));
     return reinterpret_cast<T *>(v);
 }
+// The same, typed as a global-address-space pointer: a pointer laundered through the asm loses its
+// address space, and stores through a generic pointer are FLAT stores, which count on lgkmcnt as well
+// as vmcnt (out of order), so every later LDS wait also waited for them.
+template <class T>
+using gptr = __attribute__((address_space(1))) T *;
+template <class T>
+__device__ __forceinline__ gptr<T> gvptr(T *p) {
+    uint64_t v = reinterpret_cast<uint64_t>(p);
+    asm volatile("" : "+v"(v));
+    return (gptr<T>)v;
+}
+#ifndef TM_GLOBAL_OUT
+#define TM_GLOBAL_OUT 1
+#endif
+#if TM_GLOBAL_OUT
+#define TM_OUTP(p) gvptr(p)
+#else
+#define TM_OUTP(p) vptr(p)
+#endif
 
 // ------------------------------------------------------------------ Philox4x32-10
 // all four output words of one Philox4x32-10 block

@@ -620,6 +620,11 @@ constexpr int PFP = TM_PFP;
 #ifndef TM_POS_STEP
 #define TM_POS_STEP 0
 #endif
+// event_gcn's first node-row tiles are requested this many K steps before the end of lin_event's K loop (the
+// tiles' L2 latency then overlaps lin_event instead of opening event_gcn); 0: at event_gcn's start
+#ifndef TM_NODE_EARLY
+#define TM_NODE_EARLY 0
+#endif
 static_assert(TM_JIT_NODES || (TM_ET_STEP < 0 && TM_POS_STEP < 0), "in-G1 loads need the K-outer event_gcn loop");
 // lin_event's weight ring depth (fragments in flight; the first PFP come from the previous pass)
 #ifndef TM_LIN_D
@@ -1030,6 +1035,16 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
     }
 #endif
     TM_STAMP(1);
+#if TM_JIT_NODES
+    constexpr int JN = 3;                                // node tiles in flight in event_gcn's K loop
+    float4 rs[JN], rt[JN];
+    auto nload = [&](int q) {
+        const int f4 = (q < NTD - 1) ? 4 * q + g : min(4 * q + g, dn / 4 - 1);
+        rs[q % JN] = nrow_s[f4];
+        rt[q % JN] = nrow_t[f4];
+    };
+    bool node_early = false;
+#endif
     {
         const int vo = lane_id() * 16;
         constexpr int nq = NQE;
@@ -1091,6 +1106,13 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
                         p4 = lds4(cp, q + 1);
                     }
                     const float wq[4] = {w4.x, w4.y, w4.z, w4.w}, pq[4] = {p4.x, p4.y, p4.z, p4.w};
+#if TM_JIT_NODES
+                    if (TM_NODE_EARLY > 0 && q == NQE - TM_NODE_EARLY) {
+#pragma unroll
+                        for (int k = 0; k < JN - 1 && k < NTD; ++k) nload(k);
+                        node_early = true;
+                    }
+#endif
                     constexpr bool pure_next_ok = ETAB;   // table mode: steps >= Q0 + 2 hold only time features
                     floatx4 xn = xq;
                     auto gen = [&](int t) {
@@ -1164,16 +1186,12 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
         Ht[t] = ldsx4(cs + C::G1C, t);
     }
     {
-        constexpr int JN = 3;
         const int vo = lane_id() * 16;
-        float4 rs[JN], rt[JN], wq[2][4];
-        auto nload = [&](int q) {
-            const int f4 = (q < NTD - 1) ? 4 * q + g : min(4 * q + g, dn / 4 - 1);
-            rs[q % JN] = nrow_s[f4];
-            rt[q % JN] = nrow_t[f4];
-        };
+        float4 wq[2][4];
+        if (!node_early) {
 #pragma unroll
-        for (int q = 0; q < JN - 1 && q < NTD; ++q) nload(q);
+            for (int q = 0; q < JN - 1 && q < NTD; ++q) nload(q);
+        }
 #pragma unroll
         for (int t = 0; t < 4; ++t) wq[0][t] = pre[t];
 #pragma unroll
@@ -1659,6 +1677,10 @@ __global__ void __launch_bounds__(256) gate_reg_kernel(EncW P, int32_t n_ids, co
     if (gf && valid && g == 0) gf[e] = P.dep ? 0.5f + 0.5f * (1.f / (1.f + expf(-z))) : 1.f;
 }
 
+// threads per (group, event) workgroup of explain_tab_kernel (its loops stride by blockDim.x)
+#ifndef TM_EXPLAIN_TPB
+#define TM_EXPLAIN_TPB 256
+#endif
 // retrieve_edge_imp_node with the gate table: per (group, event) the LDS hash keeps, per edge id,
 // the max graphlet importance of the walks through it; edge_imp = that max * gf(e), which equals
 // max_w(imp_w * gf(e)) bit for bit (rounding is monotone).
@@ -1960,7 +1982,7 @@ extern "C" int tm_edge_importance_tab(const float *gf, int32_t n_ids, int32_t n_
     while ((1 << hbits) < 2 * 3 * W) ++hbits;
     if (hbits > 14) return fail(TM_E_UNSUPPORTED, "tm_edge_importance_tab: too many walks per event");
     hipEvent_t pe = prof_begin(S_(stream));
-    explain_tab_kernel<<<dim3((unsigned)rows), 256, 2 * sizeof(int32_t) * (1u << hbits), S_(stream)>>>(
+    explain_tab_kernel<<<dim3((unsigned)rows), TM_EXPLAIN_TPB, 2 * sizeof(int32_t) * (1u << hbits), S_(stream)>>>(
         W, N, hbits, n_ids, gf, eid3, imp, sub1_node, sub1_eid, sub2_node, sub2_eid, out_h1, out_h2, err_flag);
     TM_CHECK_LAUNCH();
     prof_end("explain_tab_kernel", S_(stream), pe);

@@ -50,6 +50,12 @@ struct GmArgs {
 
 __host__ __device__ inline int32_t gm_r16(int32_t x) { return (x + 15) & ~15; }
 
+// row `off` of the device layer table as a global-address-space table of global pointers: loads through
+// generic pointers are FLAT loads, which also count on lgkmcnt (every later LDS wait waited for them)
+__device__ __forceinline__ gptr<const gptr<const float>> gm_layer(const float *const *lw, int off) {
+    return (gptr<const gptr<const float>>)(lw + off);
+}
+
 // LDS index of (token m, feature k) in a [32][P] image: inside each 16-wide K block the position of
 // k = 16G + 4s + j is 16G + 4j + s, so lane group j's four K values of one MFMA block are one float4
 __device__ __forceinline__ int gm_idx(int m, int k, int P) { return m * P + (k & ~15) + 4 * (k & 3) + ((k >> 2) & 3); }
@@ -216,7 +222,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
         __syncthreads();
     }
     for (int l = 0; l < a.L; ++l) {
-        const float *const *w = a.lw + 12 * l;
+        const auto w = gm_layer(a.lw, 12 * l);
         // ---- token mixing (:289-297).  Per channel c: H = gelu(W1 LN_t(X[:, c] * ew) + b1), Y = W2 H + b2,
         // X[:, c] = (Y + ... ) * ew + X[:, c] * ew -- two tiny GEMMs per 16-channel tile on MFMA: W1 (HT x N) as
         // the A operand against the normalised column (B, K = tokens), then W2 (N x HT) against H, whose
@@ -319,7 +325,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) g
         }
         // ---- channel FFN (:302-305): hidden chunks of GM_HCH through LDS (GELU in the first GEMM's epilogue)
         const int NH = gm_r16(a.HC) / 16;
-        const float4 *W1 = reinterpret_cast<const float4 *>(w[8]), *W2 = reinterpret_cast<const float4 *>(w[10]);
+        const float4 *W1 = (const float4 *)(w[8]), *W2 = (const float4 *)(w[10]);
         // every chunk's first GEMM normalises the layer's input X, so the second GEMM accumulates its
         // output tiles in registers across the chunks and X is updated once, after them
         gmx4 acc2[NTW][2];
@@ -436,10 +442,20 @@ __global__ void gm_pack_a_kernel(const float *__restrict__ w, int32_t n_out, int
 // a pointer read from the device layer table is wave-uniform, but the compiler cannot prove it (the
 // table is ordinary global memory): without this, a buffer resource built from it sits in VGPRs and every
 // buffer load becomes a readfirstlane waterfall loop
-__device__ __forceinline__ const float *gf_uniform(const float *p) {
-    const uint64_t v = reinterpret_cast<uint64_t>(p);
+template <class P>
+__device__ __forceinline__ const float *gf_uniform(P p) {
+    const uint64_t v = (uint64_t)p;
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
     return reinterpret_cast<const float *>(((uint64_t)hi << 32) | lo);
+}
+
+// the same as a global-address-space pointer, for plain loads (a generic pointer makes them FLAT loads,
+// which count on lgkmcnt too: the next LDS wait would also wait for them)
+template <class P>
+__device__ __forceinline__ gptr<const float> gf_uniform_g(P p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (gptr<const float>)(((uint64_t)hi << 32) | lo);
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t gf_rsrc(const void *p) {
@@ -605,7 +621,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 
     __syncthreads();
     const int NH2 = ((a.HC + 31) / 32) * 2;   // hidden tiles, rounded up to pairs (zero fragments)
     for (int l = 0; l < a.L; ++l) {
-        const float *const *w = a.lw + 12 * l;
+        const auto w = gm_layer(a.lw, 12 * l);
         // ---- token mixing (:289-297): per 16-channel tile, the token LayerNorm's column statistics of
         // X * ew in registers (a lane holds 4 NTT of the column's tokens; the 4 lane groups combine by two
         // shuffles), then W1 (HT x N) against the normalised column and W2 (N x HT) against H on MFMA (H's
@@ -614,8 +630,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 
         {
             const Ids I;
             const int g = I.j, li = I.m, HT = a.HT;
-            const float *tw0 = gf_uniform(w[0]), *tw1 = gf_uniform(w[1]), *tw2 = gf_uniform(w[2]),
-                        *tw3 = gf_uniform(w[3]), *tw4 = gf_uniform(w[4]), *tw5 = gf_uniform(w[5]);
+            const auto tw0 = gf_uniform_g(w[0]), tw1 = gf_uniform_g(w[1]), tw2 = gf_uniform_g(w[2]),
+                       tw3 = gf_uniform_g(w[3]), tw4 = gf_uniform_g(w[4]), tw5 = gf_uniform_g(w[5]);
             float a1[NTT][4], a2[NTT][4], lg[NTT][4], lb[NTT][4], b2v[NTT][4], b1v[4];
 #pragma unroll
             for (int G = 0; G < NTT; ++G)
@@ -996,7 +1012,7 @@ __global__ void __launch_bounds__(256) gm_bwd_kernel(GmArgs a, GmBwd b) {
     // stage layer l's token LayerNorm / FFN weights into TW; channel LN parameters (permuted K order) into
     // lnw / lnb
     auto stage_layer = [&](int l) -> GmTokW {
-        const float *const *w = b.lw + GMB_LW * l;
+        const auto w = gm_layer(b.lw, GMB_LW * l);
         GmTokW tw{TW, TW + GM_MT, TW + 2 * GM_MT, TW + 2 * GM_MT + (GM_MT / 2) * GM_MT,
                   TW + 2 * GM_MT + (GM_MT / 2) * GM_MT + GM_MT / 2, TW + 2 * GM_MT + GM_MT * GM_MT + GM_MT / 2};
         for (int i = tid; i < N; i += blockDim.x) {
@@ -1056,14 +1072,14 @@ __global__ void __launch_bounds__(256) gm_bwd_kernel(GmArgs a, GmBwd b) {
     };
     // ---- forward through the mixers, keeping each layer's input
     for (int l = 0; l < L; ++l) {
-        const float *const *w = b.lw + GMB_LW * l;
+        const auto w = gm_layer(b.lw, GMB_LW * l);
         for (int i = tid; i < IMG; i += blockDim.x) XL[l * IMG + i] = X[i];
         const GmTokW tw = stage_layer(l);
         __syncthreads();
         token_mix(tw, X, X);
         __syncthreads();
         chan_stats(X);
-        const float4 *W1 = reinterpret_cast<const float4 *>(w[8]), *W2 = reinterpret_cast<const float4 *>(w[10]);
+        const float4 *W1 = (const float4 *)(w[8]), *W2 = (const float4 *)(w[10]);
         gmx4 acc2[NTW][2];
 #pragma unroll
         for (int i = 0; i < NTW; ++i) acc2[i][0] = acc2[i][1] = gmx4{0.f, 0.f, 0.f, 0.f};
@@ -1138,7 +1154,7 @@ __global__ void __launch_bounds__(256) gm_bwd_kernel(GmArgs a, GmBwd b) {
     __syncthreads();
     // ---- the mixers backwards
     for (int l = L - 1; l >= 0; --l) {
-        const float *const *w = b.lw + GMB_LW * l;
+        const auto w = gm_layer(b.lw, GMB_LW * l);
         const float *XI = XL + l * IMG;
         const GmTokW tw = stage_layer(l);
         // out1's padding (tokens >= N, channels >= C) must read as 0: the channel FFN's A fragments and its
@@ -1154,8 +1170,8 @@ __global__ void __launch_bounds__(256) gm_bwd_kernel(GmArgs a, GmBwd b) {
         }
         __syncthreads();
         chan_stats(O1);
-        const float4 *W1 = reinterpret_cast<const float4 *>(w[8]), *W2 = reinterpret_cast<const float4 *>(w[10]);
-        const float4 *W2T = reinterpret_cast<const float4 *>(w[12]), *W1T = reinterpret_cast<const float4 *>(w[13]);
+        const float4 *W1 = (const float4 *)(w[8]), *W2 = (const float4 *)(w[10]);
+        const float4 *W2T = (const float4 *)(w[12]), *W1T = (const float4 *)(w[13]);
         gmx4 acc2[NTW][2], accv[NTW][2];
 #pragma unroll
         for (int i = 0; i < NTW; ++i) acc2[i][0] = acc2[i][1] = accv[i][0] = accv[i][1] = gmx4{0.f, 0.f, 0.f, 0.f};

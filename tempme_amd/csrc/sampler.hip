@@ -571,9 +571,10 @@ __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t
     uint32_t *ev1 = reinterpret_cast<uint32_t *>(o1 + EPB);
     const int32_t e0 = blockIdx.x * EPB, ne = min(EPB, B - e0), tid = threadIdx.x;
     const bool time_path = eidx == nullptr;
-    on = vptr(on);   // output pointers in VGPRs (scalar file pressure, see events_kernel)
-    oe = vptr(oe);
-    ot = vptr(ot);
+    // output pointers in VGPRs (scalar file pressure, see events_kernel), global address space
+    const auto gon = TM_OUTP(on);
+    const auto goe = TM_OUTP(oe);
+    const auto got = TM_OUTP(ot);
     // hop-1 rows
     if (tid < ne) {
         const int32_t u = root[e0 + tid];
@@ -612,9 +613,9 @@ __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t
     __syncthreads();
     for (int32_t x = tid; x < ne * N; x += blockDim.x) {                 // hop-1 rows, coalesced
         const int64_t o = (int64_t)e0 * N + x;
-        on[o] = h1n[x];
-        oe[o] = h1e[x];
-        ot[o] = h1t[x];
+        gon[o] = h1n[x];
+        goe[o] = h1e[x];
+        got[o] = h1t[x];
     }
     // hop-2 rows (e_idx path, graph.py:247-250): cut length and record offset once per row
     for (int32_t x = tid; x < ne * N; x += blockDim.x) {
@@ -681,9 +682,9 @@ __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t
         for (int k = 0; k < 4; ++k) {
             const int32_t q = q0 + k * (int32_t)blockDim.x;
             if (q >= tot) break;
-            on[base2 + q] = rc[k].ngh;
-            oe[base2 + q] = rc[k].eid;
-            ot[base2 + q] = rc[k].ts;
+            gon[base2 + q] = rc[k].ngh;
+            goe[base2 + q] = rc[k].eid;
+            got[base2 + q] = rc[k].ts;
         }
     }
 }
@@ -900,13 +901,13 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
     const DevGraph &g = a.g;
     // output pointers live in VGPRs (vptr): kept as uniform SGPR pairs next to the graph and input
     // pointers they overflow the scalar file and spill through v_readlane in every phase
-    int32_t *const o_dst_fake = vptr(a.dst_fake), *const o_sub1_node = vptr(a.sub1_node),
-                  *const o_sub1_eid = vptr(a.sub1_eid), *const o_sub2_node = vptr(a.sub2_node),
-                  *const o_sub2_eid = vptr(a.sub2_eid), *const o_node6 = vptr(a.node6), *const o_eid3 = vptr(a.eid3),
-                  *const o_cat = vptr(a.cat);
-    float *const o_sub1_ts = vptr(a.sub1_ts), *const o_sub2_ts = vptr(a.sub2_ts), *const o_ts3 = vptr(a.ts3),
-                *const o_cnt = vptr(a.cnt);
-    uint32_t *const o_bins = vptr(a.bins_out);
+    // (global address space: TM_OUTP)
+    const auto o_dst_fake = TM_OUTP(a.dst_fake), o_sub1_node = TM_OUTP(a.sub1_node), o_sub1_eid = TM_OUTP(a.sub1_eid),
+               o_sub2_node = TM_OUTP(a.sub2_node), o_sub2_eid = TM_OUTP(a.sub2_eid), o_node6 = TM_OUTP(a.node6),
+               o_eid3 = TM_OUTP(a.eid3), o_cat = TM_OUTP(a.cat);
+    const auto o_sub1_ts = TM_OUTP(a.sub1_ts), o_sub2_ts = TM_OUTP(a.sub2_ts), o_ts3 = TM_OUTP(a.ts3),
+               o_cnt = TM_OUTP(a.cnt);
+    const auto o_bins = TM_OUTP(a.bins_out);
     const int32_t e = blockIdx.x, s = blockIdx.y, tid = threadIdx.x;
     const uint32_t ev = a.event_ids[e];
     const Key key = make_key(a.seed, a.split, (uint32_t)(s + 1));
@@ -1052,7 +1053,7 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
         const Step2 s2 = next_step<MC>(g, key, ev, j, M, m, u, v1, s2c[j]);
         const Step3 s3 = final_step(g, key, ev, w, u, v1, s2.src, s2.ngh, s2.eid, s2.pos, s2.rank);
         const int64_t o = se * W + w;
-        int32_t *nd = o_node6 + o * 6;
+        const auto nd = o_node6 + o * 6;
         // per-lane row stores (24 / 12 B per walk); staging them in LDS for contiguous runs measured
         // slower (0.170 -> 0.178 ms: the extra LDS costs resident workgroups)
         TM_ST(nd[0], s3.src); TM_ST(nd[1], s3.ngh); TM_ST(nd[2], s2.src); TM_ST(nd[3], s2.ngh); TM_ST(nd[4], u); TM_ST(nd[5], v1);
@@ -1078,7 +1079,7 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
     __syncthreads();
     TM_EST(4);
     // new_edge_info (data_preprocess.py:327-343): count of walk w's id p in column q
-    float *const oc = o_cnt + se * W * 9;
+    const auto oc = o_cnt + se * W * 9;
     for (int32_t w = tid; w < W; w += blockDim.x) {
 #pragma unroll
         for (int p = 0; p < 3; ++p) {

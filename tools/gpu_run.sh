@@ -77,6 +77,7 @@ for s in "$@"; do
             n=${s#abtests:}
             TEMPME_LIB="$PWD/tempme_amd/lib/ab/$n.so" step pytest_ab_$n 600 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread ;;
         wab) step wab 1200 ./tools/walk_ab.sh ;;
+        wabx) WAB_EXTRAS=" " step wab 1200 ./tools/walk_ab.sh ;;
         sab) step sab 1200 ./tools/streams_ab2.sh ;;
         k:*) step pytest_k 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread -k "${s#k:}" ;;
         micro:*) m=${s#micro:}; step micro_$m 200 ./micro/$m ;;   # a prebuilt micro-benchmark binary
