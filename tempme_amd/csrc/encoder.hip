@@ -1677,9 +1677,11 @@ __global__ void __launch_bounds__(256) gate_reg_kernel(EncW P, int32_t n_ids, co
     if (gf && valid && g == 0) gf[e] = P.dep ? 0.5f + 0.5f * (1.f / (1.f + expf(-z))) : 1.f;
 }
 
-// threads per (group, event) workgroup of explain_tab_kernel (its loops stride by blockDim.x)
+// threads per (group, event) workgroup of explain_tab_kernel (its loops stride by blockDim.x): one wave
+// (256 -> 64: 0.136 -> 0.110 ms per 19,200 x 3 rows at the metric config; a workgroup is a short chain of
+// dependent loads and LDS atomics, so four times as many of them in flight per CU hide that latency)
 #ifndef TM_EXPLAIN_TPB
-#define TM_EXPLAIN_TPB 256
+#define TM_EXPLAIN_TPB 64
 #endif
 // retrieve_edge_imp_node with the gate table: per (group, event) the LDS hash keeps, per edge id,
 // the max graphlet importance of the walks through it; edge_imp = that max * gf(e), which equals
