@@ -10,6 +10,6 @@ import json, sys, os
 d = json.loads([l for l in open("gpurun_out/wab.log") if l.startswith("{")][-1])
 k = d["kernels"]["walk_kernel"]
 print(os.path.basename(sys.argv[1]), "round", sys.argv[2], "walk_kernel", k["avg_ms"], k["frac"],
-      "events", d["kernels"]["events_kernel"]["avg_ms"], "explain_tab", d["kernels"].get("explain_tab_kernel", {}).get("avg_ms"), "khop", (d.get("khop_roofline") or {}).get("avg_ms"), "ms_per_step", d["ms_per_step"], "value", d["value"])
+      "events", d["kernels"]["events_kernel"]["avg_ms"], "explain_tab", d["kernels"].get("explain_tab_kernel", {}).get("avg_ms"), "khop", (d.get("khop_roofline") or {}).get("avg_ms"), "gate", d["kernels"].get("gate_table_kernel", {}).get("avg_ms"), "ms_per_step", d["ms_per_step"], "value", d["value"])
 PY
 done; done
