@@ -209,13 +209,13 @@ def dropin_leg(ex, pipe, inputs, B, N, budget_s=3.0):
     cut = ts.cpu().numpy()
     n_b = int(src.numel()) // B
 
-    def run(pk, ed):
+    def run(pk, ed, training=False):
         def one(b):
             idx = np.arange(b * B, (b + 1) * B)
             sg_s, sg_t, sg_b, w_s, w_t, w_b, _ = P.get_item(pk, idx)
             e_s, e_t, e_b = P.get_item_edge(ed, idx)
             i_s, i_t, i_b = ex(w_s, cut[idx], e_s), ex(w_t, cut[idx], e_t), ex(w_b, cut[idx], e_b)
-            return ex.retrieve_explanation(sg_s, i_s, w_s, sg_t, i_t, w_t, sg_b, i_b, w_b, training=False)
+            return ex.retrieve_explanation(sg_s, i_s, w_s, sg_t, i_t, w_t, sg_b, i_b, w_b, training=training)
 
         for b in range(min(n_b, 4)):
             one(b)
@@ -242,8 +242,11 @@ def dropin_leg(ex, pipe, inputs, B, N, budget_s=3.0):
         pr.disable()
         pstats.Stats(pr, stream=sys.stderr).sort_stats("tottime").print_stats(30)
     devp = run(dpk, ded)
+    bern = run(dpk, ded, training=True)
     return {"value": devp["value"], "unit": "edges/s", "batch_size": B, "batches": devp["batches"],
             "ms_per_batch": devp["ms_per_batch"], "host_pack": host,
+            "bern": dict(bern, what="the same calls with retrieve_explanation(training=True): the reference's default "
+                                    "eval call (--if_bern defaults to True, temp_exp_main.py:46, :450-453), Beta rsample"),
             "what": "eval_one_epoch pattern: get_item / get_item_edge, TempME.forward x3 (grad enabled, eval mode), "
                     "retrieve_explanation(training=False) per reference batch; value = device pack "
                     "(load_subgraph_margin(..., device=)), host_pack = the reference's host float64 arrays"}

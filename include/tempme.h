@@ -350,6 +350,18 @@ int tm_edge_importance_gf3(int32_t B, int32_t W, int32_t N, const float *gf0, co
                            const int32_t *x10, const int32_t *x11, const int32_t *x12, const int32_t *n20,
                            const int32_t *n21, const int32_t *n22, const int32_t *x20, const int32_t *x21,
                            const int32_t *x22, float *out_h1, float *out_h2, void *stream);
+/* retrieve_explanation(training=True) (explainer_new.py:408-418 with beta_sample's rsample branch :420-430,
+ * as eval_one_epoch calls it under --if_bern, temp_exp_main.py:450-453): the same three-side launch, but
+ * out_p1 / out_p2 receive the gathered maxima p (before the Beta draw) and keep_h1 / keep_h2 the padding
+ * mask (0 where the subgraph node is 0, else 1); the caller draws Beta(max(10p,1), max(10(1-p),1)) and
+ * multiplies by keep (= masked_fill(node == 0, 0)). */
+int tm_edge_importance_gf3_bern(int32_t B, int32_t W, int32_t N, const float *gf0, const float *gf1, const float *gf2,
+                                const int32_t *e0, const int32_t *e1, const int32_t *e2, const float *i0,
+                                const float *i1, const float *i2, const int32_t *n10, const int32_t *n11,
+                                const int32_t *n12, const int32_t *x10, const int32_t *x11, const int32_t *x12,
+                                const int32_t *n20, const int32_t *n21, const int32_t *n22, const int32_t *x20,
+                                const int32_t *x21, const int32_t *x22, float *out_p1, float *out_p2, float *keep_h1,
+                                float *keep_h2, void *stream);
 
 /* Dependency-gate table (explainer_new.py:367-386 evaluated once per edge id): out_gf[e] =
  * 0.5 + 0.5*sigmoid(depMLP([e_feat[e] | cos(t_e * basis_freq + phase)])) for e in [0, max_eid],

@@ -398,7 +398,8 @@ __device__ __forceinline__ void explain_hash_row(int64_t ge, int32_t W, int32_t 
                                                  const int32_t *__restrict__ sub1_eid,
                                                  const int32_t *__restrict__ sub2_node,
                                                  const int32_t *__restrict__ sub2_eid, float *__restrict__ out1,
-                                                 float *__restrict__ out2) {
+                                                 float *__restrict__ out2, float *__restrict__ keep1 = nullptr,
+                                                 float *__restrict__ keep2 = nullptr) {
     extern __shared__ __attribute__((aligned(16))) int32_t hsm[];
     const int hsize = 1 << hbits;
     int32_t *hkey = hsm;
@@ -440,6 +441,16 @@ __device__ __forceinline__ void explain_hash_row(int64_t ge, int32_t W, int32_t 
             if (k == -1) break;
             h = (h + 1) & (hsize - 1);
         }
+        if (keep1) {   // training=True (beta_sample's rsample follows in torch): p and the padding mask
+            if (h1) {
+                out1[o] = p;
+                keep1[o] = nd == 0 ? 0.f : 1.f;
+            } else {
+                out2[o] = p;
+                keep2[o] = nd == 0 ? 0.f : 1.f;
+            }
+            continue;
+        }
         const float a = fmaxf(p * 10.f, 1.f), b = fmaxf((1.f - p) * 10.f, 1.f);
         const float v = nd == 0 ? 0.f : a / (a + b);
         if (h1) out1[o] = v;
@@ -468,12 +479,14 @@ struct ExplainSides {
 
 __global__ void __launch_bounds__(256) explain_hash3_kernel(ExplainSides a, int32_t B, int32_t W, int32_t N,
                                                             int32_t hbits, float *__restrict__ out1,
-                                                            float *__restrict__ out2) {
+                                                            float *__restrict__ out2, float *__restrict__ keep1,
+                                                            float *__restrict__ keep2) {
     const int s = blockIdx.x / B;
     // per-side pointers shifted so that row index (s B + b) addresses row b of side s
     const int64_t sh = (int64_t)s * B;
     explain_hash_row(blockIdx.x, W, N, hbits, a.eid3[s] - sh * 3 * W, a.gf[s] - sh * 3 * W, a.imp[s] - sh * W,
-                     a.s1n[s] - sh * N, a.s1e[s] - sh * N, a.s2n[s] - sh * N * N, a.s2e[s] - sh * N * N, out1, out2);
+                     a.s1n[s] - sh * N, a.s1e[s] - sh * N, a.s2n[s] - sh * N * N, a.s2e[s] - sh * N * N, out1, out2,
+                     keep1, keep2);
 }
 
 // ------------------------------------------------------------------ fused register-resident walk encoder
@@ -1382,7 +1395,11 @@ __device__ __forceinline__ float score_dot(const Stash &st, const floatx4 (&H)[8
     return col_sum(s) + st.cw[lane];
 }
 
-template <int NQE, int NTD, bool SEF = false, int QE0 = 0>
+// SPLIT (small grids, e.g. one reference batch per call in the drop-in surface): a wave takes one walk m of
+// its unit's 16 slots -- the slot pass, then that walk's positions 0 and 1 (3 passes instead of 1 + 2M) --
+// so a unit's M walks run on M waves at once.  The slot pass is repeated by each of them (same values);
+// the chip is far from full at these sizes, and the latency of a call is one wave's pass chain.
+template <int NQE, int NTD, bool SEF = false, int QE0 = 0, bool SPLIT = false>
 __global__ void __launch_bounds__(64 * WALK_WPB, 4 * TM_WALK_WAVES / WALK_WPB) walk_kernel(WalkArgs a) {
     using C = WalkConsts<NQE, NTD>;
     const EncW &P = a.P;
@@ -1398,6 +1415,12 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * TM_WALK_WAVES / WALK_WPB) w
     const int64_t ustride = n_units;                    // one unit per wave
 #endif
     int64_t unit = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    int m0 = 0;                                         // SPLIT: this wave's walk within each slot
+    if constexpr (SPLIT) {
+        static_assert(!TM_WALK_PERSIST, "split waves take one unit each");
+        m0 = (int)(unit % a.M);
+        unit /= a.M;
+    }
     // this column's hop-1 slot of unit u: (group, event) row and slot within it
     auto coords = [&](int64_t u, bool &v, int64_t &eg_, int32_t &j_) {
         const int64_t gs = u * 16 + col;
@@ -1435,7 +1458,7 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * TM_WALK_WAVES / WALK_WPB) w
     const auto wr = wrsrc(P.kv.w);
     floatx4 R0[4];                                      // A1G H_0, carried to the position-1 pass
     float s0 = 0.f;
-    const int n_pass = 1 + 2 * a.M;
+    const int n_pass = SPLIT ? 3 : 1 + 2 * a.M;
     PosIn cur = load_pos(a, eg * a.W + (int64_t)j * a.M, 2, valid);
     float ef[EQ_MAX][4] = {};
     float4 et[ETAB_N(QE0)];
@@ -1462,7 +1485,7 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * TM_WALK_WAVES / WALK_WPB) w
     // pass 0: position 2 once per slot (walk j*M carries it); then per walk m: position 0, position 1
 #pragma nounroll
     for (int pass = 0; pass < n_pass; ++pass) {
-        const int m = pass == 0 ? 0 : (pass - 1) >> 1;
+        const int m = SPLIT ? m0 : pass == 0 ? 0 : (pass - 1) >> 1;
         const int p = pass == 0 ? 2 : ((pass - 1) & 1);
         const int64_t gw = eg * a.W + (int64_t)j * a.M + m;
         HeadIn hi{0.f, 1.f, 0.f, 0.f, -1};
@@ -1479,7 +1502,7 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * TM_WALK_WAVES / WALK_WPB) w
         // row once this pass's lin_event is done
         const bool last = pass + 1 == n_pass;
         const int pn = !last ? ((pass & 1) == 0 ? 0 : 1) : 2;
-        const int64_t gwn = !last ? eg * a.W + (int64_t)j * a.M + (pass >> 1) : egn * a.W + (int64_t)jn * a.M;
+        const int64_t gwn = !last ? eg * a.W + (int64_t)j * a.M + (SPLIT ? m0 : pass >> 1) : egn * a.W + (int64_t)jn * a.M;
         PosIn nxt;
         if constexpr (TM_POS_STEP < 0) {
             load_hi();
@@ -1632,17 +1655,23 @@ __global__ void __launch_bounds__(256) gate_table_kernel(EncW P, int32_t n_ids, 
 // lin_event.W[:, :de] . E[e] + lin_event.b (16 * 11 features; the walk kernel starts lin_event's
 // accumulators from it), from lin_event's pack (NQL K steps): the first NQX K steps with the lanes past
 // de zeroed.
+// Per-position mode (row_eid != nullptr, tm_dropin_forward): column = walk position r of the call, its edge
+// id row_eid[r] and raw time row_t[r] (:371) instead of edge id r and its timestamp; gf[r] = the position's
+// gate factor (the same arithmetic as per edge id: the drop-in equals the pipeline bit for bit).
 template <int NQ, int NQX = 0, int NQL = 1>
 __global__ void __launch_bounds__(256) gate_reg_kernel(EncW P, int32_t n_ids, const double *__restrict__ ets,
                                                        const float *__restrict__ e_feat, float *__restrict__ gf,
-                                                       float *__restrict__ etab = nullptr) {
+                                                       float *__restrict__ etab = nullptr,
+                                                       const int32_t *__restrict__ row_eid = nullptr,
+                                                       const float *__restrict__ row_t = nullptr) {
     const int lane = threadIdx.x & 63, col = lane & 15, g = lane_id() >> 4;
     const int64_t e = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + col;
     if (((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 >= n_ids) return;   // wave-uniform
     const bool valid = e < n_ids;
-    const int64_t ec = valid ? e : 0;
+    const int64_t ec = !valid ? 0 : row_eid ? (int64_t)row_eid[e] : e;
     const int de = P.de, kdep = P.kdep;
-    const float t = ets ? (float)ets[ec] : 0.f;        // no timestamps: edge table only (gf is null too)
+    // no timestamps: edge table only (gf is null too)
+    const float t = row_eid ? (valid ? row_t[e] : 0.f) : ets ? (float)ets[ec] : 0.f;
     const float *erow = e_feat + ec * de;
     floatx4 X[NQ];
 #pragma unroll
@@ -2034,8 +2063,18 @@ static void launch_head(const EncW &P, int64_t n_walks, int64_t walks_per_group,
             P, n_walks, walks_per_group, W, F, ts3, cut, cat, stdv, out, drop, dscale);
 }
 
+// a grid of fewer units than this runs split (one wave per (unit, walk)): at most one round of resident
+// waves either way (1024 SIMDs x 2 waves), so the call's latency is the shorter pass chain
+constexpr int64_t WALK_SPLIT_UNITS = 512;
+
 template <int NQE, bool SEF = false, int Q0 = 0>
 static void launch_walk(const WalkArgs &a, unsigned blocks, hipStream_t s) {
+    const int64_t units = (a.n_slots + 15) / 16;
+    if (!TM_WALK_PERSIST && units * a.M <= 3 * WALK_SPLIT_UNITS && units < WALK_SPLIT_UNITS) {
+        const unsigned sb = (unsigned)((units * a.M + WALK_WPB - 1) / WALK_WPB);
+        walk_kernel<NQE, 11, SEF, Q0, true><<<dim3(sb), 64 * WALK_WPB, 0, s>>>(a);
+        return;
+    }
 #if TM_WALK_PERSIST
     // one round of resident workgroups (occupancy x CUs of the current device), cached per instance
     static int cap[64] = {};
@@ -2404,8 +2443,23 @@ extern "C" int tm_dropin_forward(tm_dropin *d, int32_t k, int32_t sync, const tm
         if (lds > 160 * 1024) return fail(TM_E_UNSUPPORTED, "tm_dropin_forward: LDS budget exceeded");
         const int64_t n_pos = n_walks * 3;
         hipEvent_t pe = prof_begin(side);
-        gate_pos_kernel<<<dim3((unsigned)((n_pos + TILE_ROWS - 1) / TILE_ROWS)), 256, lds, side>>>(
-            P, n_pos, W, e_feat, eid3, ts3, nullptr, out_gfac);
+        // hid_dim 64: the register-resident gate (one wave per 16 positions, MFMA chain in registers); other
+        // dims: the LDS-tiled one
+        const unsigned rblocks = (unsigned)((n_pos + 63) / 64);
+        const int nq = P.d1.nq;
+        const bool reg = P.dep && P.d2.nq == 4 && P.d1.nt == 4 && P.d2.nt == 2 && n_pos < INT32_MAX &&
+                         (nq == 11 || nq == 12 || nq == 13 || nq == 22);
+        if (reg && nq == 11)
+            gate_reg_kernel<11><<<dim3(rblocks), 256, 0, side>>>(P, (int32_t)n_pos, nullptr, e_feat, out_gfac, nullptr, eid3, ts3);
+        else if (reg && nq == 12)
+            gate_reg_kernel<12><<<dim3(rblocks), 256, 0, side>>>(P, (int32_t)n_pos, nullptr, e_feat, out_gfac, nullptr, eid3, ts3);
+        else if (reg && nq == 13)
+            gate_reg_kernel<13><<<dim3(rblocks), 256, 0, side>>>(P, (int32_t)n_pos, nullptr, e_feat, out_gfac, nullptr, eid3, ts3);
+        else if (reg)
+            gate_reg_kernel<22><<<dim3(rblocks), 256, 0, side>>>(P, (int32_t)n_pos, nullptr, e_feat, out_gfac, nullptr, eid3, ts3);
+        else
+            gate_pos_kernel<<<dim3((unsigned)((n_pos + TILE_ROWS - 1) / TILE_ROWS)), 256, lds, side>>>(
+                P, n_pos, W, e_feat, eid3, ts3, nullptr, out_gfac);
         TM_CHECK_LAUNCH();
         prof_end("gate_pos_kernel", side, pe);
     }
@@ -2418,6 +2472,14 @@ extern "C" int tm_dropin_forward(tm_dropin *d, int32_t k, int32_t sync, const tm
     return TM_OK;
 }
 
+static int edge_importance_gf3(int32_t B, int32_t W, int32_t N, const float *gf0, const float *gf1, const float *gf2,
+                               const int32_t *e0, const int32_t *e1, const int32_t *e2, const float *i0, const float *i1,
+                               const float *i2, const int32_t *n10, const int32_t *n11, const int32_t *n12,
+                               const int32_t *x10, const int32_t *x11, const int32_t *x12, const int32_t *n20,
+                               const int32_t *n21, const int32_t *n22, const int32_t *x20, const int32_t *x21,
+                               const int32_t *x22, float *out_h1, float *out_h2, float *keep_h1, float *keep_h2,
+                               void *stream);
+
 extern "C" int tm_edge_importance_gf3(int32_t B, int32_t W, int32_t N, const float *gf0, const float *gf1,
                                       const float *gf2, const int32_t *e0, const int32_t *e1, const int32_t *e2,
                                       const float *i0, const float *i1, const float *i2, const int32_t *n10,
@@ -2425,6 +2487,30 @@ extern "C" int tm_edge_importance_gf3(int32_t B, int32_t W, int32_t N, const flo
                                       const int32_t *x12, const int32_t *n20, const int32_t *n21, const int32_t *n22,
                                       const int32_t *x20, const int32_t *x21, const int32_t *x22, float *out_h1,
                                       float *out_h2, void *stream) {
+    return edge_importance_gf3(B, W, N, gf0, gf1, gf2, e0, e1, e2, i0, i1, i2, n10, n11, n12, x10, x11, x12, n20, n21,
+                               n22, x20, x21, x22, out_h1, out_h2, nullptr, nullptr, stream);
+}
+
+extern "C" int tm_edge_importance_gf3_bern(int32_t B, int32_t W, int32_t N, const float *gf0, const float *gf1,
+                                           const float *gf2, const int32_t *e0, const int32_t *e1, const int32_t *e2,
+                                           const float *i0, const float *i1, const float *i2, const int32_t *n10,
+                                           const int32_t *n11, const int32_t *n12, const int32_t *x10,
+                                           const int32_t *x11, const int32_t *x12, const int32_t *n20,
+                                           const int32_t *n21, const int32_t *n22, const int32_t *x20,
+                                           const int32_t *x21, const int32_t *x22, float *out_p1, float *out_p2,
+                                           float *keep_h1, float *keep_h2, void *stream) {
+    if (!keep_h1 || !keep_h2) return fail(TM_E_ARG, "tm_edge_importance_gf3_bern: NULL keep output");
+    return edge_importance_gf3(B, W, N, gf0, gf1, gf2, e0, e1, e2, i0, i1, i2, n10, n11, n12, x10, x11, x12, n20, n21,
+                               n22, x20, x21, x22, out_p1, out_p2, keep_h1, keep_h2, stream);
+}
+
+static int edge_importance_gf3(int32_t B, int32_t W, int32_t N, const float *gf0, const float *gf1, const float *gf2,
+                               const int32_t *e0, const int32_t *e1, const int32_t *e2, const float *i0, const float *i1,
+                               const float *i2, const int32_t *n10, const int32_t *n11, const int32_t *n12,
+                               const int32_t *x10, const int32_t *x11, const int32_t *x12, const int32_t *n20,
+                               const int32_t *n21, const int32_t *n22, const int32_t *x20, const int32_t *x21,
+                               const int32_t *x22, float *out_h1, float *out_h2, float *keep_h1, float *keep_h2,
+                               void *stream) {
     if (B < 0 || W <= 0 || N <= 0) return fail(TM_E_ARG, "tm_edge_importance_gf3: bad arguments");
     if (B == 0) return TM_OK;
     ExplainSides a{{gf0, gf1, gf2}, {i0, i1, i2}, {e0, e1, e2}, {n10, n11, n12}, {x10, x11, x12}, {n20, n21, n22},
@@ -2438,7 +2524,8 @@ extern "C" int tm_edge_importance_gf3(int32_t B, int32_t W, int32_t N, const flo
     if (hbits > 14) return fail(TM_E_UNSUPPORTED, "tm_edge_importance_gf3: too many walks per event");
     const size_t hlds = 2 * sizeof(int32_t) * (1u << hbits);
     hipEvent_t pe = prof_begin(S_(stream));
-    explain_hash3_kernel<<<dim3((unsigned)(3 * B)), 256, hlds, S_(stream)>>>(a, B, W, N, hbits, out_h1, out_h2);
+    explain_hash3_kernel<<<dim3((unsigned)(3 * B)), 256, hlds, S_(stream)>>>(a, B, W, N, hbits, out_h1, out_h2,
+                                                                            keep_h1, keep_h2);
     TM_CHECK_LAUNCH();
     prof_end("explain_hash_kernel", S_(stream), pe);
     return TM_OK;

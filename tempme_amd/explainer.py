@@ -610,6 +610,11 @@ class TempME(nn.Module):
                 done.record(side)
             cur.wait_event(done)
             out.record_stream(cur)
+            if self._needs_autograd():
+                # the backward reads the staged inputs on the caller's stream (ctx.args): their blocks came
+                # from the side stream's pool, so they must not return to it before that stream is done
+                for t in (n6, e3, t3, ct, cu, ei):
+                    t.record_stream(cur)
         out = out[:B * W]
         if self._needs_autograd():
             # eval mode with gradients enabled (temp_exp_main.py:446-452 calls the explainer outside no_grad):
@@ -634,6 +639,7 @@ class TempME(nn.Module):
             ctx.side_ids = [(x.stream_id, x.device_index, x.device_type) for x in ext]
             ctx.cur_obj = None
             ctx.fwd, ctx.expl = L.lib().tm_dropin_forward, L.lib().tm_edge_importance_gf3
+            ctx.bern = L.lib().tm_edge_importance_gf3_bern
             c = self.__dict__["_dropin_c"] = (dev, ctx, ext, [0])
             self._prep_dirty_fast = True
         return c
@@ -739,11 +745,17 @@ class TempME(nn.Module):
     def _param_bundle(self, which):
         return self._fast_state().bundle(self, which)
 
-    def _dropin_retrieve(self, sides):
+    def _dropin_retrieve(self, sides, bern=False):
         """retrieve_explanation(training=False) for the three sides of one reference batch whose walks went
         through _dropin_forward: one tm_edge_importance_gf3 launch from the gate factors cached with those
         walk tensors (same objects, unmodified, gate weights unchanged), written straight into the
-        concatenated [3B, N] / [3B, N^2] outputs.  None if any side does not qualify."""
+        concatenated [3B, N] / [3B, N^2] outputs.  None if any side does not qualify.
+
+        bern (training=True on an eval-mode module, eval_one_epoch under --if_bern, temp_exp_main.py:46,
+        :450-453): the launch writes the gathered maxima p and the padding mask of the three sides, and
+        beta_sample's rsample (explainer_new.py:420-430) runs ONCE over the concatenated [3B, N + N^2]
+        (the reference draws per side; the draws are i.i.d. either way -- parity is statistical, SURVEY.md
+        §8(c)), then masked_fill(node == 0, 0) as a multiply by the mask."""
         gc = self.__dict__.get("_gf_cache", ())
         gk = None
         got = []
@@ -778,18 +790,33 @@ class TempME(nn.Module):
                 return None
         dev = self._dev()
         ctx = self.__dict__["_dropin_c"][1]
-        o = torch.empty(3 * B * (N + N * N), dtype=torch.float32, device=dev)
+        n_out = 3 * B * (N + N * N)
+        o = torch.empty(n_out * (2 if bern else 1), dtype=torch.float32, device=dev)
         p1 = o.data_ptr()
         p2 = p1 + 4 * 3 * B * N
         (ha, ea, _, ia, na1, xa1, na2, xa2, *_), (hb, eb, _, ib, nb1, xb1, nb2, xb2, *_), \
             (hc, ec, _, ic, nc1, xc1, nc2, xc2, *_) = got
-        rc = ctx.expl(B, W, N, ha[5].data_ptr() + 4 * ha[6], hb[5].data_ptr() + 4 * hb[6], hc[5].data_ptr() + 4 * hc[6],
-                      ea.data_ptr(), eb.data_ptr(), ec.data_ptr(), ia.data_ptr(), ib.data_ptr(), ic.data_ptr(),
-                      na1.data_ptr(), nb1.data_ptr(), nc1.data_ptr(), xa1.data_ptr(), xb1.data_ptr(), xc1.data_ptr(),
-                      na2.data_ptr(), nb2.data_ptr(), nc2.data_ptr(), xa2.data_ptr(), xb2.data_ptr(), xc2.data_ptr(),
-                      p1, p2, torch._C._cuda_getCurrentRawStream(dev.index))
+        args = (B, W, N, ha[5].data_ptr() + 4 * ha[6], hb[5].data_ptr() + 4 * hb[6], hc[5].data_ptr() + 4 * hc[6],
+                ea.data_ptr(), eb.data_ptr(), ec.data_ptr(), ia.data_ptr(), ib.data_ptr(), ic.data_ptr(),
+                na1.data_ptr(), nb1.data_ptr(), nc1.data_ptr(), xa1.data_ptr(), xb1.data_ptr(), xc1.data_ptr(),
+                na2.data_ptr(), nb2.data_ptr(), nc2.data_ptr(), xa2.data_ptr(), xb2.data_ptr(), xc2.data_ptr(), p1, p2)
+        if bern:
+            k1 = p1 + 4 * n_out
+            rc = ctx.bern(*args, k1, k1 + 4 * 3 * B * N, torch._C._cuda_getCurrentRawStream(dev.index))
+        else:
+            rc = ctx.expl(*args, torch._C._cuda_getCurrentRawStream(dev.index))
         if rc:
             L.check(rc, "retrieve_explanation")
+        if bern:
+            p, keep = o[:n_out], o[n_out:]
+            if torch.is_grad_enabled() and (any(gk[-8:]) or ia.requires_grad or ib.requires_grad or ic.requires_grad):
+                args = tuple((g[1], g[2], g[5], g[7], B, W, N) for g in got)
+                p = _apply(_EvalExplain3RawFn, self, args, ia, ib, ic, p, ha[9].bundle(self, "gate"))
+            x = self.beta_sample(p, True) * keep
+            o1, o2 = x[:3 * B * N].view(3 * B, N), x[3 * B * N:].view(3 * B, N * N)
+            if self.base_type == "tgn":
+                return [o1, o2]
+            return [o1]
         o1, o2 = o.as_strided((3 * B, N), (N, 1)), o.as_strided((3 * B, N * N), (N * N, 1), 3 * B * N)
         if torch.is_grad_enabled() and (any(gk[-8:]) or ia.requires_grad or ib.requires_grad or
                                         ic.requires_grad):
@@ -861,10 +888,11 @@ class TempME(nn.Module):
     def retrieve_explanation(self, subgraph_src, graphlet_imp_src, walks_src, subgraph_tgt, graphlet_imp_tgt,
                              walks_tgt, subgraph_bgd, graphlet_imp_bgd, walks_bgd, training=True):
         """explainer_new.py:408-418."""
-        if not training and self.__dict__.get("_gf_cache") and self._hip_eval_ok():
+        # the gate factors cached by eval-mode forwards (dropout off, as in the module's eval mode)
+        if not self.training and self.__dict__.get("_gf_cache") and self._hip_eval_ok():
             r = self._dropin_retrieve(((subgraph_src, graphlet_imp_src, walks_src),
                                        (subgraph_tgt, graphlet_imp_tgt, walks_tgt),
-                                       (subgraph_bgd, graphlet_imp_bgd, walks_bgd)))
+                                       (subgraph_bgd, graphlet_imp_bgd, walks_bgd)), bern=bool(training))
             if r is not None:
                 return r
         s0, s1 = self.retrieve_edge_imp_node(subgraph_src, graphlet_imp_src, walks_src, training=training)
@@ -1146,6 +1174,40 @@ class _EvalExplain3Fn(torch.autograd.Function):
             gsum = pg if gsum is None else [a + b for a, b in zip(gsum, pg)]
         return (None, None, *[None if d is None else d.reshape(ctx.saved_tensors[s].shape) for s, d in enumerate(d_imps)],
                 None, None, _flat_grads(gsum, params))
+
+
+class _EvalExplain3RawFn(torch.autograd.Function):
+    """The gathered maxima p of retrieve_edge_imp_node for the three sides, concatenated [3B*N | 3B*N^2]
+    (tm_edge_importance_gf3_bern, eval-mode module), with gradients: backward recomputes each side through
+    the HIP training kernels (gate + scatter-max, no dropout in eval mode) and differentiates p."""
+
+    @staticmethod
+    def forward(ctx, ex, args, imp_s, imp_t, imp_b, p, bundle):
+        ctx.ex, ctx.args = ex, args
+        ctx.save_for_backward(imp_s, imp_t, imp_b)
+        return p.detach()
+
+    @staticmethod
+    def backward(ctx, gp):
+        ex = ctx.ex
+        params = ex._gate_params()
+        d_imps, gsum = [], None
+        B, N = ctx.args[0][4], ctx.args[0][6]
+        g1, g2 = gp[:3 * B * N].view(3, B * N), gp[3 * B * N:].view(3, B * N * N)
+        for s, imp in enumerate(ctx.saved_tensors):
+            e3, t3, x1, x2, B, W, N = ctx.args[s]
+            with torch.enable_grad():
+                imp_ = imp.detach().reshape(-1).to(torch.float32).requires_grad_(True)
+                a = (e3.contiguous(), t3.contiguous(), x1.contiguous(), x2.contiguous(), (None, None, 1.0, 1.0),
+                     1, B, W, N)
+                p1, p2 = _ExplainFn.apply(ex, a, imp_, *params)
+                gs = torch.autograd.grad((p1, p2), [imp_] + list(params), grad_outputs=(g1[s], g2[s]),
+                                         allow_unused=True)
+            d_imps.append(gs[0])
+            pg = [torch.zeros_like(q) if g is None else g for g, q in zip(gs[1:], params)]
+            gsum = pg if gsum is None else [a_ + b_ for a_, b_ in zip(gsum, pg)]
+        return (None, None, *[d.reshape(ctx.saved_tensors[s].shape) for s, d in enumerate(d_imps)], None,
+                _flat_grads(gsum, params))
 
 
 class _Ctx:

@@ -177,7 +177,21 @@ class GraphMixer(nn.Module):
             return "eval"
         if explain_weight is not None and explain_weight.requires_grad:
             ok = L.lib().tm_gm_embed_bwd_ok(N, self.num_channels, self.time_feat_dim, self.num_layers, ht)
-            return "grad" if ok else None
+            if not ok:
+                return None
+            if any(p.requires_grad for p in self.parameters()):
+                # the reference's training loop leaves the base's parameters requiring grad but never steps
+                # them (its optimizer holds the explainer's only, temp_exp_main.py:555); the HIP backward
+                # returns d ew alone.  frozen_base = False asks for their gradients: the torch formulation
+                if not getattr(self, "frozen_base", True):
+                    return None
+                if not getattr(self, "_warned_frozen", False):
+                    import warnings
+                    warnings.warn("GraphMixer: explanation-weight gradients on HIP; the base model's own "
+                                  "parameters get no .grad (set model.frozen_base = False for the torch "
+                                  "formulation, which computes them)", stacklevel=3)
+                    self._warned_frozen = True
+            return "grad"
         if any(p.requires_grad for p in self.parameters()):
             return None
         return "eval"

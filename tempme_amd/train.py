@@ -253,20 +253,41 @@ def run_steps(explainer, base_model, optimizer, batches, *, grad_sync=None, over
     result is prepared (``prepare_step``) while batch k's gradient all-reduce is in flight.  Same
     updates as the serial loop (tests/test_multi_rank.py)."""
     outs = []
-    nxt = prepare_step(base_model, batches[0]) if batches else None
-    for k, b in enumerate(batches):
-        cur, box = nxt, {}
-        if overlap and k + 1 < len(batches):
-            def pre(b1=batches[k + 1]):
+    n = len(batches)
+    # each batch is fetched once (``batches`` may gather lazily, e.g. _LazyBatches): at most the current and
+    # the next gathered batch are alive at a time
+    b_next = batches[0] if n else None
+    nxt = prepare_step(base_model, b_next) if n else None
+    for k in range(n):
+        b, cur, box = b_next, nxt, {}
+        b_next = batches[k + 1] if k + 1 < n else None
+        if overlap and b_next is not None:
+            def pre(b1=b_next):
                 box["p"] = prepare_step(base_model, b1)
         else:
             pre = None
         outs.append(train_step(explainer, base_model, optimizer, b, grad_sync=grad_sync, prepared=cur, overlap=pre,
                                **kw))
-        nxt = box.get("p") if k + 1 < len(batches) else None
-        if nxt is None and k + 1 < len(batches):
-            nxt = prepare_step(base_model, batches[k + 1])
+        del b, cur
+        nxt = box.get("p") if b_next is not None else None
+        if nxt is None and b_next is not None:
+            nxt = prepare_step(base_model, b_next)
     return outs
+
+
+class _LazyBatches:
+    """The epoch's batches gathered from the pack on access (``batch_from_pack`` per index), so an epoch
+    does not hold a permuted device copy of the whole rank-local pack."""
+
+    def __init__(self, buf, src, dst, ts, e_idx, perm, spans):
+        self.args, self.perm, self.spans = (buf, src, dst, ts, e_idx), perm, spans
+
+    def __len__(self):
+        return len(self.spans)
+
+    def __getitem__(self, k):
+        s_idx, e_end = self.spans[k]
+        return batch_from_pack(*self.args, self.perm[s_idx:e_end])
 
 
 class GraphedTrainStep:
@@ -346,8 +367,7 @@ def train_epoch(explainer, base_model, optimizer, buf, src, dst, ts, e_idx, bs, 
     num_instance = int(src.shape[0]) - 1              # the reference leaves the last event out (:560-561)
     perm = torch.randperm(num_instance, generator=generator).to(src.device)
     explainer.train()
-    batches = [batch_from_pack(buf, src, dst, ts, e_idx, perm[s_idx:e_end])
-               for s_idx, e_end in epoch_spans(num_instance, bs, rank, world)]
+    batches = _LazyBatches(buf, src, dst, ts, e_idx, perm, epoch_spans(num_instance, bs, rank, world))
     outs = run_steps(explainer, base_model, optimizer, batches, grad_sync=grad_sync, beta=beta, prior_p=prior_p,
                      if_bern=if_bern)
     return [step_metrics(o) for o in outs] if metrics else outs

@@ -396,3 +396,89 @@ def test_eval_forward_grad_matches_torch(dev, finder, g, z):
     for n in want:
         err = (got[n] - want[n]).norm() / max(want[n].norm(), 1e-12)
         assert err < 2e-4, (n, float(err))
+
+
+def _bern_setup(dev, finder, g, z, E=50):
+    from tempme_amd import pack as P
+    from tempme_amd.pipeline import ExplainPipeline
+    N = 20
+    ex = _explainer(dev, g, z, "N20_base")
+    pipe = ExplainPipeline(ex, finder.graph, torch.from_numpy(z["test_sampler_dst"]), N, 3, 25, seed=0,
+                           split=px.SPLIT_TEST)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a[:E], dtype=dt)).to(dev)  # noqa: E731
+    pipe.run(t(z["test_src"], np.int32), t(z["test_dst"], np.int32), t(z["test_ts"], np.float64),
+             t(z["test_eidx"], np.int32), torch.arange(E, dtype=torch.int32, device=dev))
+    _, cat_d, edge = P.buffers_to_arrays(pipe.buf, E)
+
+    class A:
+        n_degree = N
+    return ex, P, A, cat_d, edge, z["test_ts"][:E].astype(np.float64)
+
+
+def test_dropin_bern_fast_path_matches_general_path(dev, finder, g, z):
+    """retrieve_explanation(training=True) on the eval-mode module (eval_one_epoch under --if_bern,
+    temp_exp_main.py:46, :450-453) through the device-pack fast path (tm_edge_importance_gf3_bern: the
+    gathered maxima and the padding mask of the three sides in one launch, one rsample over all of them)
+    against the general path (per side: HIP training kernels, rsample, masked_fill).  With beta_sample's
+    draw replaced by the identity (the draw is random; everything around it is deterministic): outputs
+    bit-identical and the gradients of a loss over them equal for every parameter and importance."""
+    ex, P, A, cat_d, edge, cut = _bern_setup(dev, finder, g, z)
+    ex.beta_sample = lambda prob, training: prob     # instance attribute: both paths call self.beta_sample
+    res = {}
+    for where in ("device", "host"):
+        pk, ed = ((P.load_subgraph_margin(A(), cat_d, device=dev), P.load_edge(edge, dev)) if where == "device"
+                  else (P.load_subgraph_margin(A(), cat_d), edge))
+        ex.zero_grad()
+        ex.__dict__.pop("_gf_cache", None)
+        idx = np.arange(25, 50)
+        sg_s, sg_t, sg_b, w_s, w_t, w_b, _ = P.get_item(pk, idx)
+        e_s, e_t, e_b = P.get_item_edge(ed, idx)
+        imps = [ex(w_s, cut[idx], e_s), ex(w_t, cut[idx], e_t), ex(w_b, cut[idx], e_b)]
+        for i in imps:
+            i.retain_grad()
+        expl = ex.retrieve_explanation(sg_s, imps[0], w_s, sg_t, imps[1], w_t, sg_b, imps[2], w_b, training=True)
+        assert (where == "device") == bool(ex.__dict__.get("_gf_cache"))
+        loss = expl[0].pow(2).sum() + 0.5 * expl[1].sum() + (imps[0] * imps[1]).sum()
+        loss.backward()
+        res[where] = ([x.detach().clone() for x in expl], [i.grad.clone() for i in imps],
+                      {n: p.grad.detach().clone() for n, p in ex.named_parameters() if p.grad is not None})
+    (xd, gd, pd), (xh, gh, ph) = res["device"], res["host"]
+    for a_, b_ in zip(xd, xh):
+        assert torch.equal(a_, b_)
+    for a_, b_ in zip(gd, gh):
+        torch.testing.assert_close(a_, b_, rtol=1e-5, atol=1e-7)
+    assert pd.keys() == ph.keys() and len(pd) >= 26
+    for n in pd:
+        torch.testing.assert_close(pd[n], ph[n], rtol=1e-5, atol=1e-7, msg=n)
+
+
+def test_dropin_bern_draws_are_beta(dev, finder, g, z):
+    """The fast path's real draws: zero on padding entries, in (0, 1) elsewhere, and over 400 calls their
+    per-entry mean and variance match Beta(max(10p,1), max(10(1-p),1)) (explainer_new.py:420-430) with p
+    the eval path's maxima (parity for the rsample branch is statistical)."""
+    ex, P, A, cat_d, edge, cut = _bern_setup(dev, finder, g, z, E=25)
+    pk, ed = P.load_subgraph_margin(A(), cat_d, device=dev), P.load_edge(edge, dev)
+    idx = np.arange(25)
+    sg_s, sg_t, sg_b, w_s, w_t, w_b, _ = P.get_item(pk, idx)
+    e_s, e_t, e_b = P.get_item_edge(ed, idx)
+    torch.manual_seed(0)
+    with torch.no_grad():
+        imps = [ex(w_s, cut[idx], e_s), ex(w_t, cut[idx], e_t), ex(w_b, cut[idx], e_b)]
+        draws = [torch.cat([x.reshape(-1) for x in
+                            ex.retrieve_explanation(sg_s, imps[0], w_s, sg_t, imps[1], w_t, sg_b, imps[2], w_b,
+                                                    training=True)]) for _ in range(400)]
+        mean_eval = torch.cat([x.reshape(-1) for x in ex.retrieve_explanation(
+            sg_s, imps[0], w_s, sg_t, imps[1], w_t, sg_b, imps[2], w_b, training=False)])
+    d = torch.stack(draws).double()
+    pad = mean_eval == 0
+    assert bool((d[:, pad] == 0).all())
+    live = d[:, ~pad]
+    assert bool((live > 0).all() and (live < 1).all())
+    m = mean_eval[~pad].double()                      # = a / (a + b), the eval branch
+    # a + b = max(10p,1) + max(10(1-p),1) >= 10, so var = m(1-m)/(a+b+1) <= 1/44; the 400-draw mean's
+    # standard error is <= 0.0075 per entry: check the average deviation and the worst entry loosely
+    dev_mean = (live.mean(0) - m).abs()
+    assert float(dev_mean.mean()) < 0.004 and float(dev_mean.max()) < 0.05
+    # Beta variance m(1-m)/(a+b+1) with a+b+1 in [11, 12]: the pooled ratio lies in [1/12, 1/11] up to noise
+    ratio = float(live.var(0).sum() / (m * (1 - m)).sum())
+    assert 1 / 12.6 < ratio < 1 / 10.5, ratio

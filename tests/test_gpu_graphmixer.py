@@ -195,3 +195,34 @@ def test_hip_embedding_config5_dims_vs_oracle(dev, N):
         np.testing.assert_allclose(torch.cat([p, n]).cpu().double().numpy(), torch.cat([p64, n64]).numpy(),
                                    atol=ATOL, rtol=RTOL)
     assert getattr(m, "_gm_key", None) is not None, "the HIP embedding did not run"
+
+
+def test_frozen_base_false_takes_torch_gradients(dev):
+    """frozen_base = False: gradients wanted for the base model's own parameters as well -> the torch
+    formulation (autograd), so they get a .grad; the default (frozen) HIP backward leaves them None."""
+    from tempme_amd.graphmixer import GraphMixer
+    rng = np.random.default_rng(5)
+    V, E, B, N, C = 100, 500, 8, 12, 32
+    nf = rng.uniform(0, 1, (V, C)).astype(np.float32)
+    ef = rng.uniform(0, 1, (E + 1, C)).astype(np.float32)
+    cut = np.floor(rng.uniform(5e7, 1e8, B))
+    sgs = []
+    for _ in range(3):
+        node = rng.integers(1, V, (B, N))
+        eid = rng.integers(1, E + 1, node.shape)
+        ts = np.floor(cut[:, None] - rng.uniform(0, 5e7, node.shape))
+        sgs.append(([node.astype(np.float64), None], [eid.astype(np.float64), None], [ts, None]))
+    src, dst, fake = (rng.integers(1, V, B) for _ in range(3))
+    grads = {}
+    for frozen in (True, False):
+        torch.manual_seed(1)
+        m = GraphMixer(nf, ef, n_neighbors=N, device=dev, num_tokens=N, num_layers=1, dropout=0.1).to(dev).eval()
+        m.frozen_base = frozen
+        ew = torch.full((3 * B, N), 0.5, device=dev, requires_grad=True)
+        p, n = m.contrast(src, dst, fake, cut, None, *sgs, explain_weights=[ew])
+        torch.cat([p, n]).sum().backward()
+        assert (getattr(m, "_gmb_key", None) is not None) == frozen
+        assert (m.projection_layer.weight.grad is None) == frozen
+        grads[frozen] = ew.grad.detach().clone()
+    d = float((grads[True] - grads[False]).norm())
+    assert d <= 1e-4 * float(grads[False].norm()) + 1e-9

@@ -252,26 +252,49 @@ def test_run_steps_overlap_equals_serial(dev):
     base.forbidden_memory_update = True
     base = base.to(dev).eval()
     B = 40
+
+    class Rec:
+        """grad_sync stand-in: records each step's gradients between backward and the optimizer step
+        (run_steps issues the next batch's prepare_step between start() and finish())."""
+        def __init__(self, ex):
+            self.ex, self.steps = ex, []
+
+        def start(self):
+            self.steps.append([p.grad.detach().clone() for p in self.ex.parameters() if p.grad is not None])
+
+        def finish(self):
+            pass
+
     runs = []
     for overlap in (False, True):
         torch.manual_seed(5)
         ex = tm.TempME(base, "tgn", "enron", out_dim=40, hid_dim=64, device=dev,
                        null_model={k: 1.0 / 12 for k in range(1, 13)}).to(dev).eval()
         opt = torch.optim.Adam(ex.parameters(), lr=1e-3)
+        rec = Rec(ex)
         batches = [batch_from_pack(buf, s_d, d_d, t_d, e_d, torch.arange(k * B, (k + 1) * B, device=dev))
                    for k in range(4)]
         if overlap:
-            outs = run_steps(ex, base, opt, batches, overlap=True, if_bern=False)
+            outs = run_steps(ex, base, opt, batches, overlap=True, if_bern=False, grad_sync=rec)
         else:
-            outs = [train_step(ex, base, opt, b, if_bern=False) for b in batches]
-        runs.append(([float(o["loss"]) for o in outs], {k: v.detach().clone() for k, v in ex.named_parameters()}))
-    # the same computation in a different launch order; the runs drift apart only through torch's atomic
-    # scatter/gather backward (nondeterministic summation order) amplified by Adam's early ~lr*sign(g)
-    # updates of near-zero gradients (as in test_graphed_step_equals_eager): a few lr units at most
+            outs = [train_step(ex, base, opt, b, if_bern=False, grad_sync=rec) for b in batches]
+        runs.append(([float(o["loss"]) for o in outs], {k: v.detach().clone() for k, v in ex.named_parameters()},
+                     rec.steps))
+    # step 1 is the same computation from the same parameters: its gradients agree to summation order
+    assert len(runs[0][2]) == len(runs[1][2]) == 4
+    for a, b in zip(runs[0][2][0], runs[1][2][0]):
+        assert float((a - b).norm()) <= 1e-5 * float(a.norm()) + 1e-9
+    # later steps drift apart only through torch's atomic scatter/gather backward (nondeterministic
+    # summation order), which Adam's early ~lr*sign(g) updates amplify for near-zero gradients (as in
+    # test_graphed_step_equals_eager): measured ~30 % of the parameters differ by more than 1e-6 after 4
+    # steps, but by far less than lr.  A step run on the wrong batch or on another batch's prepared inputs
+    # moves the losses by far more than 2e-4 and most parameters by ~lr per step
     np.testing.assert_allclose(runs[1][0][0], runs[0][0][0], rtol=2e-5)
-    np.testing.assert_allclose(runs[1][0], runs[0][0], rtol=2e-3)
-    for k, v in runs[0][1].items():
-        assert float((runs[1][1][k] - v).abs().max()) <= 1e-2, k
+    np.testing.assert_allclose(runs[1][0], runs[0][0], rtol=2e-4)
+    lr = 1e-3
+    far = sum(int(((runs[1][1][k] - v).abs() > 0.5 * lr).sum()) for k, v in runs[0][1].items())
+    total = sum(v.numel() for v in runs[0][1].values())
+    assert far <= 0.01 * total, (far, total)
 
 
 @pytest.mark.parametrize("if_bern", [False, True])

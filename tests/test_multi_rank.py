@@ -267,3 +267,85 @@ def test_overlapped_all_reduce_equals_serial():
         p.join(timeout=60)
     assert res == "ok", res
     assert all(p.exitcode == 0 for p in procs)
+
+
+def _run_steps_worker(rank, world, port, q):
+    """train.run_steps with a GradAllReduce over gloo (the orchestration: each batch fetched once, batch
+    k+1's prepare_step issued while batch k's all-reduce is in flight) against the serial loop.  The
+    step body is a CPU stand-in with train_step's structure (the real one needs the HIP library; its
+    multi-rank run on the device is tests/test_gpu_multi_rank.py)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import tempme_amd.train as T
+
+        def prepare_step(base, batch):
+            return ("prepared", batch["i"])
+
+        def train_step(ex, base, opt, batch, *, grad_sync=None, prepared=None, overlap=None, **kw):
+            assert prepared == ("prepared", batch["i"]), (prepared, batch["i"])
+            opt.zero_grad()
+            ex(batch["x"]).pow(2).mean().backward()
+            grad_sync.start()
+            if overlap is not None:
+                overlap()
+            grad_sync.finish()
+            opt.step()
+            return batch["i"]
+
+        T.prepare_step, T.train_step = prepare_step, train_step
+
+        class Lazy:
+            def __init__(self):
+                self.fetched = []
+
+            def __len__(self):
+                return 5
+
+            def __getitem__(self, k):
+                self.fetched.append(k)
+                return {"i": k, "x": torch.randn(6, 5, generator=torch.Generator().manual_seed(10 * k + rank))}
+
+        nets = []
+        for mode in ("serial", "run_steps"):
+            torch.manual_seed(0)
+            net = torch.nn.Sequential(torch.nn.Linear(5, 7), torch.nn.ReLU(), torch.nn.Linear(7, 1))
+            opt = torch.optim.Adam(net.parameters(), lr=1e-2)
+            sync = T.GradAllReduce(net)
+            lazy = Lazy()
+            if mode == "serial":
+                for k in range(len(lazy)):
+                    b = lazy[k]
+                    train_step(net, None, opt, b, grad_sync=sync, prepared=prepare_step(None, b))
+            else:
+                outs = T.run_steps(net, None, opt, lazy, grad_sync=sync, overlap=True)
+                assert outs == list(range(5))
+            assert lazy.fetched == list(range(5)), lazy.fetched      # each batch gathered once, in order
+            nets.append(net)
+        for a, b in zip(nets[0].parameters(), nets[1].parameters()):
+            assert torch.equal(a, b)
+        got = [None] * world
+        dist.all_gather_object(got, [p.detach().clone() for p in nets[1].parameters()])
+        if rank == 0:
+            for a, b in zip(got[0], got[1]):
+                assert torch.equal(a, b)
+            q.put("ok")
+    except Exception as exc:
+        q.put(repr(exc))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_run_steps_grad_all_reduce_two_ranks():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_run_steps_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == "ok", res
+    assert all(p.exitcode == 0 for p in procs)

@@ -4,7 +4,10 @@ different kernels): mean counter value per dispatch and the dispatch count.  FET
 (rocprofv3); on gfx950 FETCH_SIZE reads 1/2 of a wide coalesced stream's bytes (MI355X_MICROARCH.md §HBM)
 -- reported raw and x2.
 
-    python tools/pmc_summary.py gpurun_out --glob 'pmc_enron_*' [--traffic profiles/pmc_traffic_enron.json]
+    python tools/pmc_summary.py gpurun_out --glob 'pmc_enron_*' [--out SUMMARY.json] [--traffic profiles/pmc_traffic_enron.json]
+
+The summary JSON goes to --out (or stdout); every status message goes to stderr, so a redirected stdout
+stays valid JSON.
 """
 import csv
 import glob
@@ -40,7 +43,11 @@ for k, d in acc.items():
         x["lds_conflict_cycles_per_lds_inst"] = x["SQ_LDS_BANK_CONFLICT"] / max(1.0, x["SQ_INSTS_LDS"])
     if "SQ_WAIT_INST_ANY" in x and "SQ_WAVE_CYCLES" in x:
         x["wait_inst_any_per_wave_cycle"] = x["SQ_WAIT_INST_ANY"] / max(1.0, x["SQ_WAVE_CYCLES"])
-print(json.dumps(out, indent=1))
+if "--out" in sys.argv:
+    with open(sys.argv[sys.argv.index("--out") + 1], "w") as fh:
+        json.dump(out, fh, indent=1)
+else:
+    print(json.dumps(out, indent=1))
 # --traffic FILE: per-launch HBM bytes (FETCH_SIZE x2 + WRITE_SIZE) of every instance, and for each name
 # bench.py times the instance launched most often in this run (the bench kernel, not a one-off like the
 # null model's), which bench.py reports as roofline.traffic for the config this PMC run measured
@@ -57,4 +64,4 @@ if "--traffic" in sys.argv:
         by[BENCH_ALIAS.get(short, short)] = v["bytes"]          # the most-dispatched instance wins
     with open(dest, "w") as fh:
         json.dump({"source": f"{root}/{pat}", "kernels": inst, "by_bench_name": by}, fh, indent=1)
-    print("wrote", dest, by)
+    print("wrote", dest, by, file=sys.stderr)
