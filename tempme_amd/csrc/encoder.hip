@@ -958,10 +958,19 @@ __device__ __forceinline__ void load_ef(const WalkArgs &a, int32_t e, float (&ef
 // the polynomial in an exec-mask branch, which serialised it against the MFMAs) and the count / edge
 // lanes select their values.  Padding lanes (k >= kev) keep cos(0) = 1: lin_event's packed weights are
 // zero there.  In table mode the edge lanes are 0 (their product comes from the table row).
+// TM_ABL (A/B ablation builds only, outputs meaningless): bit 1 = time features without the cos (one fma),
+// bit 2 = every node-feature row read at node 0, bit 4 = every edge-table row read at edge 0
+#ifndef TM_ABL
+#define TM_ABL 0
+#endif
 template <bool ETAB, bool PURE>
 __device__ __forceinline__ float gen_one(int q, int s, float w, float ph, const float (&ef)[EQ_MAX][4], int g,
                                          int de, float dt, float c0, float c1, float c2) {
+#if TM_ABL & 1
+    float c = __builtin_fmaf(dt, w, ph);
+#else
     float c = time_cos(dt, w, ph);
+#endif
     if constexpr (PURE) return c;
     const int k = 16 * q + 4 * g + s;
     const int qe = q < EQ_MAX ? q : 0;
@@ -1010,7 +1019,11 @@ __device__ __forceinline__ float4 ef_step(const float4 *erow4, int q, int g, int
 template <int Q0>
 __device__ __forceinline__ void load_et(const WalkArgs &a, int32_t e, float4 (&et)[ETAB_N(Q0)]) {
     if constexpr (Q0 > 0) {
+#if TM_ABL & 4
+        const float4 *trow = reinterpret_cast<const float4 *>(a.etab) + 0 * e;
+#else
         const float4 *trow = reinterpret_cast<const float4 *>(a.etab + (int64_t)e * 176);
+#endif
         const int g = lane_id() >> 4;
 #pragma unroll
         for (int t = 0; t < 11; ++t) et[t] = trow[4 * t + g];
@@ -1041,8 +1054,12 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
     const int g = lane_id() >> 4;
     const int de = P.de, dn = P.dn, kev = P.kev;
     const float dt = pi.dt, c0 = pi.c0, c1 = pi.c1, c2 = pi.c2;
+#if TM_ABL & 2
+    const float4 *nrow_s = reinterpret_cast<const float4 *>(a.n_feat), *nrow_t = nrow_s;
+#else
     const float4 *nrow_s = reinterpret_cast<const float4 *>(a.n_feat + (int64_t)pi.ns * dn);
     const float4 *nrow_t = reinterpret_cast<const float4 *>(a.n_feat + (int64_t)pi.nt * dn);
+#endif
 #if !TM_JIT_NODES
     float4 xs[NTD], xt[NTD];
 #endif

@@ -169,6 +169,33 @@ torch.nn.modules.module.register_module_parameter_registration_hook(_bump_gen)
 torch.nn.modules.module.register_module_module_registration_hook(_bump_gen)
 
 
+_EXT = [None, False]
+
+
+def _dropin_ext():
+    """tempme_amd/lib/_dropin_ext*.so (csrc/dropin_ext.cpp, built by __graft_entry__.build()): the C++ host
+    side of the drop-in fast path.  Without it the same fast path runs its host side in Python (same
+    kernels, same results), with a warning."""
+    if not _EXT[1]:
+        _EXT[1] = True
+        import importlib.machinery
+        import importlib.util
+        import os
+        import sysconfig
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                            "_dropin_ext" + sysconfig.get_config_var("EXT_SUFFIX"))
+        if os.path.exists(path) and os.environ.get("TEMPME_DROPIN_EXT", "1") != "0":
+            loader = importlib.machinery.ExtensionFileLoader("tempme_amd._dropin_ext", path)
+            spec = importlib.util.spec_from_file_location("tempme_amd._dropin_ext", path, loader=loader)
+            mod = importlib.util.module_from_spec(spec)
+            loader.exec_module(mod)
+            _EXT[0] = mod
+        elif os.environ.get("TEMPME_DROPIN_EXT", "1") != "0":
+            warnings.warn("tempme_amd/lib/_dropin_ext*.so not built (python tempme_amd/_build_ext.py): the drop-in "
+                          "fast path's host side runs in Python", RuntimeWarning, stacklevel=3)
+    return _EXT[0]
+
+
 def _to_many(device, *items):
     """[_to(a, device, dtype) for (a, dtype) in items], staged through one pinned copy when every
     array is a host numpy array and the device is a GPU."""
@@ -677,6 +704,20 @@ class TempME(nn.Module):
         library call (tm_dropin_forward: side stream, staged cut times, encoder, and the dependency-gate
         factors retrieve_edge_imp_node will need, cached by walk identity).  None when the inputs are not
         such views of one batch (the general path handles them)."""
+        fx = self.__dict__.get("_fastx")
+        if fx is not None:
+            r = fx[0].forward(node_idx, edge_idx, time_idx, cat_feat, cut_time_l, edge_identify)
+            if r is not None:
+                imp, rc, grad = r
+                if rc:
+                    L.check(rc, "TempME.forward")
+                if grad:
+                    B, W = edge_idx.shape[0], edge_idx.shape[1]
+                    args = (node_idx, edge_idx, time_idx, cat_feat,
+                            np.array(cut_time_l, dtype=np.float64) if cut_time_l.__class__ is np.ndarray else cut_time_l,
+                            edge_identify, 1, B, W)
+                    imp = _apply(_EvalEncoderBundleFn, self, args, imp, fx[1].bundle(self, "enc"))
+                return imp
         if not (getattr(edge_idx, "_tm_resident", False) and getattr(node_idx, "_tm_resident", False) and
                 getattr(time_idx, "_tm_resident", False) and getattr(cat_feat, "_tm_resident", False) and
                 getattr(edge_identify, "_tm_resident", False)):
@@ -740,7 +781,31 @@ class TempME(nn.Module):
             args = (node_idx, edge_idx, time_idx, cat_feat,
                     np.array(cut_time_l, dtype=np.float64) if cut_d is None else cut_time_l, edge_identify, 1, B, W)
             imp = _apply(_EvalEncoderBundleFn, self, args, imp, fs.bundle(self, "enc"))
+        self._make_fastx(fs, ctx, dev, (edge_idx, time_idx, out, B, W))
         return imp
+
+    def _make_fastx(self, fs, ctx, dev, entry):
+        """The C++ host side of this fast path (csrc/dropin_ext.cpp) for the current weights / tables / context:
+        later forwards and retrieves on device-pack views take one C++ call each; any change of the weights,
+        tables or module registrations sends the next call back here."""
+        ext = _dropin_ext()
+        if ext is None:
+            return
+        fx = self.__dict__.get("_fastx")
+        if fx is not None and fx[1] is fs and fx[2] is ctx and fx[0].current():
+            fx[0].push(*entry)
+            return
+        ws = self._weight_list()
+        ne = self._modules["node_raw_embed"]._parameters["weight"]
+        ee = self._modules["edge_raw_embed"]._parameters["weight"]
+        addr = lambda f: L.C.cast(f, L.C.c_void_p).value  # noqa: E731
+        lib = L.lib()
+        fast = ext.Fast(list(ws) + [ne, ee], [True] * len(ws) + [False, False], _REG_GEN, _REG_GEN[0], ctx.h.value,
+                        addr(lib.tm_dropin_forward), addr(lib.tm_edge_importance_gf3),
+                        addr(lib.tm_edge_importance_gf3_bern), fs.wts if isinstance(fs.wts, int) else fs.wts.value,
+                        fs.nt, fs.et, fs.etab or 0, list(ctx.side_ids), dev.index, bool(fs.enc_grad))
+        fast.push(*entry)
+        self.__dict__["_fastx"] = (fast, fs, ctx)
 
     def _param_bundle(self, which):
         return self._fast_state().bundle(self, which)
@@ -807,22 +872,29 @@ class TempME(nn.Module):
             rc = ctx.expl(*args, torch._C._cuda_getCurrentRawStream(dev.index))
         if rc:
             L.check(rc, "retrieve_explanation")
+        # the gate bundle of the forward's state (its gate parameters are the current ones: gk matched)
+        return self._retrieve_tail(o, [(g[1], g[2], g[4], g[5], g[6], g[7], B, W, N) for g in got], (ia, ib, ic),
+                                   any(gk[-8:]), ha[9], bern)
+
+    def _retrieve_tail(self, o, sides, imps, gate_grad, fs, bern):
+        """The fast retrieve's outputs from its one launch's buffer o ([hop-1 | hop-2], with bern [p | keep]):
+        views [3B, N] / [3B, N^2], the Beta draw for bern, and the autograd node when gradients are wanted.
+        sides: per side (e3, t3, n1, x1, n2, x2, B, W, N)."""
+        B, N = sides[0][6], sides[0][8]
+        ia, ib, ic = imps
+        grad = torch.is_grad_enabled() and (gate_grad or ia.requires_grad or ib.requires_grad or ic.requires_grad)
         if bern:
+            n_out = 3 * B * (N + N * N)
             p, keep = o[:n_out], o[n_out:]
-            if torch.is_grad_enabled() and (any(gk[-8:]) or ia.requires_grad or ib.requires_grad or ic.requires_grad):
-                args = tuple((g[1], g[2], g[5], g[7], B, W, N) for g in got)
-                p = _apply(_EvalExplain3RawFn, self, args, ia, ib, ic, p, ha[9].bundle(self, "gate"))
+            if grad:
+                args = tuple((g[0], g[1], g[3], g[5], g[6], g[7], g[8]) for g in sides)
+                p = _apply(_EvalExplain3RawFn, self, args, ia, ib, ic, p, fs.bundle(self, "gate"))
             x = self.beta_sample(p, True) * keep
             o1, o2 = x[:3 * B * N].view(3 * B, N), x[3 * B * N:].view(3 * B, N * N)
-            if self.base_type == "tgn":
-                return [o1, o2]
-            return [o1]
-        o1, o2 = o.as_strided((3 * B, N), (N, 1)), o.as_strided((3 * B, N * N), (N * N, 1), 3 * B * N)
-        if torch.is_grad_enabled() and (any(gk[-8:]) or ia.requires_grad or ib.requires_grad or
-                                        ic.requires_grad):
-            args = tuple((g[1], g[2], g[4], g[5], g[6], g[7], B, W, N) for g in got)
-            # the gate bundle of the forward's state (its gate parameters are the current ones: gk matched)
-            o1, o2 = _apply(_EvalExplain3Fn, self, args, ia, ib, ic, o1, o2, ha[9].bundle(self, "gate"))
+        else:
+            o1, o2 = o.as_strided((3 * B, N), (N, 1)), o.as_strided((3 * B, N * N), (N * N, 1), 3 * B * N)
+            if grad:
+                o1, o2 = _apply(_EvalExplain3Fn, self, tuple(sides), ia, ib, ic, o1, o2, fs.bundle(self, "gate"))
         if self.base_type == "tgn":
             return [o1, o2]
         return [o1]
@@ -889,12 +961,23 @@ class TempME(nn.Module):
                              walks_tgt, subgraph_bgd, graphlet_imp_bgd, walks_bgd, training=True):
         """explainer_new.py:408-418."""
         # the gate factors cached by eval-mode forwards (dropout off, as in the module's eval mode)
-        if not self.training and self.__dict__.get("_gf_cache") and self._hip_eval_ok():
-            r = self._dropin_retrieve(((subgraph_src, graphlet_imp_src, walks_src),
-                                       (subgraph_tgt, graphlet_imp_tgt, walks_tgt),
-                                       (subgraph_bgd, graphlet_imp_bgd, walks_bgd)), bern=bool(training))
-            if r is not None:
-                return r
+        if not self.training:
+            sides = ((subgraph_src, graphlet_imp_src, walks_src), (subgraph_tgt, graphlet_imp_tgt, walks_tgt),
+                     (subgraph_bgd, graphlet_imp_bgd, walks_bgd))
+            fx = self.__dict__.get("_fastx")
+            if fx is not None and fx[0].cached:
+                r = fx[0].retrieve(sides, bool(training))
+                if r is not None:
+                    o, rc, args = r
+                    if rc:
+                        L.check(rc, "retrieve_explanation")
+                    fs = fx[1]
+                    return self._retrieve_tail(o, args, (graphlet_imp_src, graphlet_imp_tgt, graphlet_imp_bgd),
+                                               fs.gate_grad, fs, bool(training))
+            if self.__dict__.get("_gf_cache") and self._hip_eval_ok():
+                r = self._dropin_retrieve(sides, bern=bool(training))
+                if r is not None:
+                    return r
         s0, s1 = self.retrieve_edge_imp_node(subgraph_src, graphlet_imp_src, walks_src, training=training)
         t0, t1 = self.retrieve_edge_imp_node(subgraph_tgt, graphlet_imp_tgt, walks_tgt, training=training)
         b0, b1 = self.retrieve_edge_imp_node(subgraph_bgd, graphlet_imp_bgd, walks_bgd, training=training)

@@ -427,13 +427,25 @@ class TGN(nn.Module):
         return pack
 
     # -------------------------------------------------------------- forward pieces
-    def _layer(self, pk, li, src_feat, R, N, node_idx, ngh_dense, edge_idx, edge_dense, dt, mask_node, ew, seg=0):
-        """One TemporalAttentionLayer over R source rows (embedding_module.py:181-216)."""
+    def _layer(self, pk, li, src_feat, R, N, node_idx, ngh_dense, edge_idx, edge_dense, dt, mask_node, ew, seg=0,
+               cache=None):
+        """One TemporalAttentionLayer over R source rows (embedding_module.py:181-216).  ``cache`` (the
+        prepared inputs' dict): the query and its folded projection depend on the source rows and the frozen
+        weights only, so the training step's two contrasts of one batch (temp_exp_main.py:597, :611) compute
+        them once."""
         lw = pk["layers"][li]
         H, dk = lw["H"], lw["dk"]
         dn = self.n_node_features
-        query = torch.cat([src_feat, pk["cosb"].expand(R, dn)], dim=1)        # [R, dq]
-        qf = query @ lw["P"].t()                                             # [R, H*dk]
+        key = ("qf", li, id(pk))
+        hit = cache.get(key) if cache is not None else None
+        if hit is not None and hit[0] is pk:
+            query, qf = hit[1], hit[2]
+        else:
+            query = torch.cat([src_feat(), pk["cosb"].expand(R, dn)], dim=1)    # [R, dq]
+            qf = (query @ lw["P"].t()).contiguous()                            # [R, H*dk]
+            if cache is not None:
+                cache[key] = (pk, query, qf)
+        src_feat = query[:, :dn]
         de = edge_dense.shape[-1] if edge_dense is not None else self.n_edge_features
         if dn + de + dn != dk:
             raise AssertionError(f"key dim {dn}+{de}+{dn} != {dk}")
@@ -443,7 +455,7 @@ class TGN(nn.Module):
                     edge_tab=edge_dense if edge_dense is not None else pk["etab"],
                     edge_idx=None if edge_dense is not None else edge_idx, dt=dt, time_w=pk["tw"],
                     time_b=pk["tb"], mask_node=mask_node, err=pk["err"], seg_rows=seg)
-        z = _TgnAttnFn.apply(qf.contiguous(), ngh_dense, ew, spec)
+        z = _TgnAttnFn.apply(qf, ngh_dense, ew, spec)
         out = torch.addmm(lw["fcb"], z, lw["G"].t())
         h = F.layer_norm(out + query, (query.shape[1],), lw["lnw"], lw["lnb"], 1e-5)
         x = torch.cat([h, src_feat], dim=1)
@@ -470,11 +482,12 @@ class TGN(nn.Module):
             ew2 = explain_weights[1].to(dev, torch.float32).reshape(R1 * N, N).contiguous()
         tab = pk["tab"]
         # layer 0 (attention_models[0]): hop-1 nodes attend over their hop-2 neighbours
-        y0 = self._layer(pk, 0, tab[x["n1l"]], R1 * N, N, x["n2f"], None, x["e2"], x["ed2"], x["dt2"], x["n2f"],
-                         ew2, seg1 * N)
+        cache = x if prepared is not None else None
+        y0 = self._layer(pk, 0, lambda: tab[x["n1l"]], R1 * N, N, x["n2f"], None, x["e2"], x["ed2"], x["dt2"],
+                         x["n2f"], ew2, seg1 * N, cache)
         # layer 1 (attention_models[1]): roots attend over the hop-1 embeddings
-        y1 = self._layer(pk, 1, tab[x["n0"]], R1, N, None, y0.contiguous(), x["e1"], x["ed1"], x["dt1"], x["n1f"],
-                         ew1, seg1)
+        y1 = self._layer(pk, 1, lambda: tab[x["n0"]], R1, N, None, y0.contiguous(), x["e1"], x["ed1"], x["dt1"],
+                         x["n1f"], ew1, seg1, cache)
         return y1
 
     def _prep_inputs(self, nodes, eids, times, cut_time, edge_attr=None, n_segments=1):

@@ -356,6 +356,7 @@ def test_dropin_fast_path_gradients_match_general_path(dev, finder, g, z):
                   else (P.load_subgraph_margin(A(), cat_d), edge))
         ex.zero_grad()
         ex.__dict__.pop("_gf_cache", None)
+        ex.__dict__.pop("_fastx", None)
         idx = np.arange(25, 50)
         sg_s, sg_t, sg_b, w_s, w_t, w_b, _ = P.get_item(pk, idx)
         e_s, e_t, e_b = P.get_item_edge(ed, idx)
@@ -364,6 +365,8 @@ def test_dropin_fast_path_gradients_match_general_path(dev, finder, g, z):
             i.retain_grad()
         expl = ex.retrieve_explanation(sg_s, imps[0], w_s, sg_t, imps[1], w_t, sg_b, imps[2], w_b, training=False)
         assert (where == "device") == bool(ex.__dict__.get("_gf_cache")), "fast path taken only on device views"
+        if where == "device":    # the first forward built the C++ host side; the other calls went through it
+            assert ex.__dict__["_fastx"][0].hits == 3
         loss = expl[0].pow(2).sum() + 0.5 * expl[1].sum() + (imps[0] * imps[1]).sum() + imps[2].pow(2).sum()
         loss.backward()
         res[where] = ([x.detach().clone() for x in expl], [i.grad.clone() for i in imps],
@@ -430,6 +433,7 @@ def test_dropin_bern_fast_path_matches_general_path(dev, finder, g, z):
                   else (P.load_subgraph_margin(A(), cat_d), edge))
         ex.zero_grad()
         ex.__dict__.pop("_gf_cache", None)
+        ex.__dict__.pop("_fastx", None)
         idx = np.arange(25, 50)
         sg_s, sg_t, sg_b, w_s, w_t, w_b, _ = P.get_item(pk, idx)
         e_s, e_t, e_b = P.get_item_edge(ed, idx)
@@ -438,6 +442,8 @@ def test_dropin_bern_fast_path_matches_general_path(dev, finder, g, z):
             i.retain_grad()
         expl = ex.retrieve_explanation(sg_s, imps[0], w_s, sg_t, imps[1], w_t, sg_b, imps[2], w_b, training=True)
         assert (where == "device") == bool(ex.__dict__.get("_gf_cache"))
+        if where == "device":
+            assert ex.__dict__["_fastx"][0].hits == 3
         loss = expl[0].pow(2).sum() + 0.5 * expl[1].sum() + (imps[0] * imps[1]).sum()
         loss.backward()
         res[where] = ([x.detach().clone() for x in expl], [i.grad.clone() for i in imps],
@@ -482,3 +488,51 @@ def test_dropin_bern_draws_are_beta(dev, finder, g, z):
     # Beta variance m(1-m)/(a+b+1) with a+b+1 in [11, 12]: the pooled ratio lies in [1/12, 1/11] up to noise
     ratio = float(live.var(0).sum() / (m * (1 - m)).sum())
     assert 1 / 12.6 < ratio < 1 / 10.5, ratio
+
+
+def test_dropin_cpp_host_side_equals_python_host_side(dev, finder, g, z):
+    """The C++ host side of the drop-in fast path (csrc/dropin_ext.cpp) against its Python host side (the
+    same library calls): four reference batches each way, retrieve_explanation eval and bern (identity
+    draw), outputs bit-identical; a weight update between batches sends the next call back through
+    Python (new version key) and the results follow the new weights."""
+    from tempme_amd import explainer as X
+    ex, P, A, cat_d, edge, cut = _bern_setup(dev, finder, g, z, E=100)
+    assert X._dropin_ext() is not None, "tempme_amd/lib/_dropin_ext*.so missing (python tempme_amd/_build_ext.py)"
+    ex.beta_sample = lambda prob, training: prob
+    pk, ed = P.load_subgraph_margin(A(), cat_d, device=dev), P.load_edge(edge, dev)
+
+    def run(force_python):
+        outs = []
+        for b0 in range(0, 100, 25):
+            idx = np.arange(b0, b0 + 25)
+            sg_s, sg_t, sg_b, w_s, w_t, w_b, _ = P.get_item(pk, idx)
+            e_s, e_t, e_b = P.get_item_edge(ed, idx)
+            imps = []
+            for w, e in ((w_s, e_s), (w_t, e_t), (w_b, e_b)):
+                if force_python:
+                    ex.__dict__.pop("_fastx", None)
+                imps.append(ex(w, cut[idx], e))
+            if force_python:
+                ex.__dict__.pop("_fastx", None)
+            with torch.no_grad():
+                a = ex.retrieve_explanation(sg_s, imps[0], w_s, sg_t, imps[1], w_t, sg_b, imps[2], w_b, training=False)
+                b = ex.retrieve_explanation(sg_s, imps[0], w_s, sg_t, imps[1], w_t, sg_b, imps[2], w_b, training=True)
+            outs.append([x.detach().clone() for x in imps + a + b])
+        return outs
+
+    cpp = run(False)
+    assert ex.__dict__["_fastx"][0].hits >= 4 * 4
+    py_ = run(True)
+    for u, v in zip(cpp, py_):
+        for x, y in zip(u, v):
+            assert torch.equal(x, y)
+    # a weight update: the C++ state's key no longer matches, the call goes through Python and rebuilds it
+    with torch.no_grad():
+        ex.MLP[0].weight.mul_(1.5)
+    upd = run(False)
+    assert not torch.equal(upd[0][0], cpp[0][0])
+    ex.__dict__.pop("_fastx", None)
+    ref = run(True)
+    for u, v in zip(upd, ref):
+        for x, y in zip(u, v):
+            assert torch.equal(x, y)

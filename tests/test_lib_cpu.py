@@ -74,3 +74,13 @@ def test_flops_model_matches_survey():
     assert abs(fm["per_walk"] - 631_000) / 631_000 < 1e-3
     assert bench.sampling_bytes_per_event(20, 3) == 78_816
     assert bench.sampling_bytes_per_event(30, 3) == 143_376
+
+
+def test_dropin_extension_loads():
+    """The drop-in fast path's C++ host side (csrc/dropin_ext.cpp, built by build()) imports on the CPU and
+    exposes its entry points (constructing one needs a HIP device)."""
+    from tempme_amd import explainer as X
+    m = X._dropin_ext()
+    assert m is not None, "tempme_amd/lib/_dropin_ext*.so missing: python tempme_amd/_build_ext.py"
+    for name in ("forward", "retrieve", "push", "current"):
+        assert hasattr(m.Fast, name)
