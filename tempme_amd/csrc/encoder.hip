@@ -496,86 +496,7 @@ __global__ void __launch_bounds__(256) explain_hash3_kernel(ExplainSides a, int3
 // next layer, so the whole chain stays in registers.  A wave owns 16 hop-1 slots (columns):
 // position 2 (shared by the M walks of a slot: same e1, t1, v1, root, edge counts, dt = 0) is
 // encoded once per slot, positions 0/1 once per walk.
-// out[t] = W tile t * x  over the flattened (t, q) sequence, weights prefetched PF steps ahead in
-// a rotating register buffer; sched_barrier pins each step so the loads stay PF steps ahead instead
-// of being hoisted (which would need NTO*NQ registers).
-constexpr int PF = 3;
-
 #define TM_W_ADDR(i) ((((i) / NQ) * nq + ((i) % NQ)) * 64)
-
-// The lane index laundered through an opaque asm: loads addressed with it cannot be hoisted out of
-// the pass loop by LICM (hoisting every loop-invariant weight/bias load costs ~300 registers).
-__device__ __forceinline__ int lane_id() {
-    int l = threadIdx.x & 63;
-    asm volatile("" : "+v"(l));
-    return l;
-}
-
-// Weight fragments are read with buffer loads: the fragment's byte offset is a compile-time SGPR
-// operand (s_mov, scalar pipe) instead of a 64-bit VGPR address add per fragment.  The lane offset
-// goes through lane_id() so the loads stay inside the pass loop.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t wrsrc(const float4 *w) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float4 *>(w), (short)0, 0x7fffffff, 0x00020000);
-}
-
-__device__ __forceinline__ float4 wload(__amdgpu_buffer_rsrc_t r, int vo, int f4) {
-    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, f4 * 16, 0));
-}
-
-template <int NTO, int NQ>
-struct PairOrder {   // fragment i of the pair order -> (tile, K step)
-    static constexpr int NP = NTO / 2, NPF = 2 * NP * NQ;
-    static constexpr int t(int i) { return i < NPF ? 2 * (i / (2 * NQ)) + (i & 1) : NTO - 1; }
-    static constexpr int q(int i) { return i < NPF ? (i % (2 * NQ)) / 2 : i - NPF; }
-};
-
-// NQL = the pack's K steps (L.nq); NQ <= NQL of them are multiplied (the leading ones).  Tile pairs (t, t+1)
-// with their K steps inside and the two tiles' MFMAs interleaved (no MFMA waits on the accumulator of the one
-// before it: 32-cycle issue, 40-cycle dependent latency); an odd last tile alone.  Every tile accumulates its
-// K steps in the same order as a tile-by-tile loop (same results).
-template <int NTO, int NQ, int NQL = NQ>
-__device__ __forceinline__ void rgemm(const Lin &L, const floatx4 (&x)[NQ], floatx4 (&o)[NTO]) {
-    using O = PairOrder<NTO, NQ>;
-    const auto wr = wrsrc(L.w);
-    const int vo = lane_id() * 16;
-    constexpr int N = NTO * NQ, D = PF < N ? PF : N;
-    auto off = [](int i) { return (O::t(i) * NQL + O::q(i)) * 64; };
-#pragma unroll
-    for (int t = 0; t < NTO; ++t) o[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    float4 buf[D];
-#pragma unroll
-    for (int i = 0; i < D; ++i) buf[i] = wload(wr, vo, off(i));
-#pragma unroll
-    for (int k = 0; k < O::NP * NQ; ++k) {
-        const int i = 2 * k, t = O::t(i), q = O::q(i);
-        const float4 w0 = buf[i % D];
-        if (i + D < N) buf[i % D] = wload(wr, vo, off(i + D));
-        const float4 w1 = buf[(i + 1) % D];
-        if (i + 1 + D < N) buf[(i + 1) % D] = wload(wr, vo, off(i + 1 + D));
-        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0.x, x[q].x, o[t], 0, 0, 0);
-        o[t + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.x, x[q].x, o[t + 1], 0, 0, 0);
-        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0.y, x[q].y, o[t], 0, 0, 0);
-        o[t + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.y, x[q].y, o[t + 1], 0, 0, 0);
-        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0.z, x[q].z, o[t], 0, 0, 0);
-        o[t + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.z, x[q].z, o[t + 1], 0, 0, 0);
-        o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0.w, x[q].w, o[t], 0, 0, 0);
-        o[t + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1.w, x[q].w, o[t + 1], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    if constexpr (NTO % 2) {
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const int i = O::NPF + q;
-            const float4 w = buf[i % D];
-            if (i + D < N) buf[i % D] = wload(wr, vo, off(i + D));
-            o[NTO - 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, x[q].x, o[NTO - 1], 0, 0, 0);
-            o[NTO - 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, x[q].y, o[NTO - 1], 0, 0, 0);
-            o[NTO - 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, x[q].z, o[NTO - 1], 0, 0, 0);
-            o[NTO - 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, x[q].w, o[NTO - 1], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-}
 
 // two column sets through the same weights (one weight load feeds both)
 template <int NTO, int NQ>

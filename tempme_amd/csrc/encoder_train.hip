@@ -18,6 +18,8 @@
 // alongside the forward packs).  Each kernel also writes, per layer, the (dY, X) row pairs of its tile;
 // wgrad_partial_kernel + wgrad_reduce_kernel then form every weight gradient dW = dY^T X (and bias
 // gradient, a column of ones appended to X) over all rows in two launches (tm_encoder_wgrad).
+#include <cstdlib>
+
 #include "encoder_common.h"
 
 namespace tmk {
@@ -639,6 +641,221 @@ __global__ void __launch_bounds__(256) gcn_bwd_kernel(EncW P, EncWT T, int64_t n
 }
 
 
+// Register-resident event_gcn backward (hid_dim 64, dn with 11 tiles, lin_event with NQE K steps): the same
+// computation as gcn_bwd_kernel in the fused walk kernel's orientation -- weights are the MFMA A operand
+// (forward packs P.ev / P.g1 and the transposed packs T.g2T / T.g1T / T.evT), one wave's 16 walk positions the
+// B operand's columns, so the whole chain (recomputed lin_event, both event_gcn branches, dZ, d lev, the
+// time-feature gradient) stays in registers with no LDS and no barriers; the (d pre-activation, input) row
+// pairs the weight gradients need are stored as they are produced.  Every tile accumulates its K steps in
+// the LDS kernel's order; the time-feature gradient's sin is the branch-free sin_rd (common.h, |error| ~1e-7;
+// ocml's sinf carries a Payne-Hanek slow path).
+template <int NQE>
+__global__ void __launch_bounds__(256, 2) gcn_bwd_reg_kernel(EncW P, EncWT T, int64_t n_rows,
+                                                              const float *__restrict__ n_feat,
+                                                              const float *__restrict__ e_feat,
+                                                              const int32_t *__restrict__ node6,
+                                                              const int32_t *__restrict__ eid3,
+                                                              const float *__restrict__ ts3,
+                                                              const float *__restrict__ cnt,
+                                                              const float *__restrict__ dF, GcnBwdOut o) {
+    constexpr int NTD = 11, KE = 16 * NQE, DN = 16 * NTD, H = HID;
+    const int lane = threadIdx.x & 63, col = lane & 15, g = lane_id() >> 4;
+    const int64_t r0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16;
+    const int64_t r = r0 + col;
+    const bool valid = r < n_rows;                       // a wave past the end computes row n_rows - 1, stores nothing
+    const int64_t rc = valid ? r : n_rows - 1;           // clamped: every load in bounds, stores skipped
+    const int64_t w = rc / 3;
+    const int p = (int)(rc % 3);
+    const int de = P.de, dn = P.dn, kev = P.kev;
+    const int32_t e = eid3[rc], ns = node6[w * 6 + 2 * p], nt = node6[w * 6 + 2 * p + 1];
+    const float dt = ts3[w * 3 + 2] - ts3[w * 3 + p];
+    const float c0 = cnt[rc * 3], c1 = cnt[rc * 3 + 1], c2 = cnt[rc * 3 + 2];
+    if (valid && g == 0) o.dt[r] = dt;
+    // 1. event features (B fragments: lane group g holds features 16 q + 4 g + s of column col) -> lin_event.
+    // Branch-free: the edge-feature float4 (clamped index), the counts and the cos are all formed and the
+    // lane's value selected; the time encoder's frequency / phase come from an LDS table laid out on the
+    // event-feature axis (zero outside the time block)
+    __shared__ float4 tabw[NQE * 4], tabp[NQE * 4];
+    for (int i = threadIdx.x; i < NQE * 16; i += blockDim.x) {
+        const int ti = i - de - 3;
+        reinterpret_cast<float *>(tabw)[i] = (ti >= 0 && ti < dn) ? P.freq[ti] : 0.f;
+        reinterpret_cast<float *>(tabp)[i] = (ti >= 0 && ti < dn) ? P.phase[ti] : 0.f;
+    }
+    __syncthreads();
+    const float4 *er = reinterpret_cast<const float4 *>(e_feat + (int64_t)e * de);
+    floatx4 X[NQE];
+#pragma unroll
+    for (int q = 0; q < NQE; ++q) {
+        const float4 ef4 = er[min(4 * q + g, de / 4 - 1)], w4 = tabw[4 * q + g], p4 = tabp[4 * q + g];
+        const float ef[4] = {ef4.x, ef4.y, ef4.z, ef4.w}, wv[4] = {w4.x, w4.y, w4.z, w4.w}, pv[4] = {p4.x, p4.y, p4.z, p4.w};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int k = 16 * q + 4 * g + s;
+            float c = time_cos(dt, wv[s], pv[s]);
+            asm volatile("" : "+v"(c));
+            float v = k < kev ? c : 0.f;
+            if (k < de + 3) v = k == de ? c0 : k == de + 1 ? c1 : c2;
+            if (k < de) v = ef[s];
+            X[q][s] = v;
+        }
+        if (valid)
+            *reinterpret_cast<float4 *>(o.ev + r * KE + 16 * q + 4 * g) = make_float4(X[q][0], X[q][1], X[q][2], X[q][3]);
+    }
+    floatx4 L[NTD];
+    rgemm<NTD, NQE, NQE>(P.ev, X, L);
+#pragma unroll
+    for (int t = 0; t < NTD; ++t) {
+        const float4 b = *reinterpret_cast<const float4 *>(P.ev.b + 16 * t + 4 * g);
+        L[t] = floatx4{L[t][0] + b.x, L[t][1] + b.y, L[t][2] + b.z, L[t][3] + b.w};
+    }
+    // 2. A = x_s + relu(x_t + L), B = x_t + relu(x_s + L) (:93-96) K step by K step into event_gcn's first
+    // layer for both branches (one weight fragment feeds both); relu masks of a / b kept as bits
+    const float4 *nrs = reinterpret_cast<const float4 *>(n_feat + (int64_t)ns * dn);
+    const float4 *nrt = reinterpret_cast<const float4 *>(n_feat + (int64_t)nt * dn);
+    const auto wg1 = wrsrc(P.g1.w);
+    const int vo = lane_id() * 16;
+    floatx4 Hs[4], Ht[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) Hs[t] = Ht[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    uint64_t ma = 0, mb = 0;
+    float4 wq[2][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) wq[0][t] = wload(wg1, vo, (t * NTD + 0) * 64);
+#pragma unroll
+    for (int q = 0; q < NTD; ++q) {
+        if (q + 1 < NTD) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) wq[(q + 1) & 1][t] = wload(wg1, vo, (t * NTD + q + 1) * 64);
+        }
+        const int f4 = min(4 * q + g, dn / 4 - 1);
+        const float4 xs4 = nrs[f4], xt4 = nrt[f4];
+        const float xs[4] = {xs4.x, xs4.y, xs4.z, xs4.w}, xt[4] = {xt4.x, xt4.y, xt4.z, xt4.w};
+        floatx4 A, Bq;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int c = 16 * q + 4 * g + s;
+            const float l = L[q][s], a = xt[s] + l, b = xs[s] + l;
+            const bool in = q < NTD - 1 || c < dn;     // 161 <= dn <= 176: only the last tile has padding
+            A[s] = in ? xs[s] + relu(a) : 0.f;
+            Bq[s] = in ? xt[s] + relu(b) : 0.f;
+            ma |= (uint64_t)(in && a > 0.f) << (4 * q + s);
+            mb |= (uint64_t)(in && b > 0.f) << (4 * q + s);
+        }
+        if (valid) {
+            *reinterpret_cast<float4 *>(o.AB + (r * 2) * DN + 16 * q + 4 * g) = make_float4(A[0], A[1], A[2], A[3]);
+            *reinterpret_cast<float4 *>(o.AB + (r * 2 + 1) * DN + 16 * q + 4 * g) = make_float4(Bq[0], Bq[1], Bq[2], Bq[3]);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const float4 wv = wq[q & 1][t];
+            Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv.x, A.x, Hs[t], 0, 0, 0);
+            Ht[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv.x, Bq.x, Ht[t], 0, 0, 0);
+            Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv.y, A.y, Hs[t], 0, 0, 0);
+            Ht[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv.y, Bq.y, Ht[t], 0, 0, 0);
+            Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv.z, A.z, Hs[t], 0, 0, 0);
+            Ht[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv.z, Bq.z, Ht[t], 0, 0, 0);
+            Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv.w, A.w, Hs[t], 0, 0, 0);
+            Ht[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv.w, Bq.w, Ht[t], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // the relu masks as VGPR bit fields (opaque to the compiler: it would otherwise keep every compare's lane
+    // mask alive in SGPR pairs until step 6 and spill the scalar file)
+    uint32_t ma0 = (uint32_t)ma, ma1 = (uint32_t)(ma >> 32), mb0 = (uint32_t)mb, mb1 = (uint32_t)(mb >> 32);
+    asm volatile("" : "+v"(ma0), "+v"(ma1), "+v"(mb0), "+v"(mb1));
+    ma = ((uint64_t)ma1 << 32) | ma0;
+    mb = ((uint64_t)mb1 << 32) | mb0;
+    // 3. z = relu(MLP.0 . + b) of both branches (stored: MLP.2's inputs); 4. dU = dF (the head's gradient);
+    // 5. dZ = (M2^T dU) * [z > 0]
+    uint32_t mz = 0;
+    floatx4 dUs[4], dUt[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const float4 b = *reinterpret_cast<const float4 *>(P.g1.b + 16 * t + 4 * g);
+        const float bb[4] = {b.x, b.y, b.z, b.w};
+        floatx4 zs, zt;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            zs[s] = relu(Hs[t][s] + bb[s]);
+            zt[s] = relu(Ht[t][s] + bb[s]);
+            mz |= (uint32_t)(zs[s] > 0.f) << (4 * t + s);
+            mz |= (uint32_t)(zt[s] > 0.f) << (16 + 4 * t + s);
+        }
+        if (valid) {
+            *reinterpret_cast<float4 *>(o.H + (r * 2) * H + 16 * t + 4 * g) = make_float4(zs[0], zs[1], zs[2], zs[3]);
+            *reinterpret_cast<float4 *>(o.H + (r * 2 + 1) * H + 16 * t + 4 * g) = make_float4(zt[0], zt[1], zt[2], zt[3]);
+        }
+        const float4 us = *reinterpret_cast<const float4 *>(dF + rc * (2 * H) + 16 * t + 4 * g);
+        const float4 ut = *reinterpret_cast<const float4 *>(dF + rc * (2 * H) + H + 16 * t + 4 * g);
+        dUs[t] = floatx4{valid ? us.x : 0.f, valid ? us.y : 0.f, valid ? us.z : 0.f, valid ? us.w : 0.f};
+        dUt[t] = floatx4{valid ? ut.x : 0.f, valid ? ut.y : 0.f, valid ? ut.z : 0.f, valid ? ut.w : 0.f};
+    }
+    asm volatile("" : "+v"(mz));
+    floatx4 dZs[4], dZt[4];
+    rgemm<4, 4, 4>(T.g2T, dUs, dZs);
+    rgemm<4, 4, 4>(T.g2T, dUt, dZt);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            dZs[t][s] = (mz >> (4 * t + s)) & 1u ? dZs[t][s] : 0.f;
+            dZt[t][s] = (mz >> (16 + 4 * t + s)) & 1u ? dZt[t][s] : 0.f;
+        }
+        if (valid) {
+            *reinterpret_cast<float4 *>(o.dZ + (r * 2) * H + 16 * t + 4 * g) = make_float4(dZs[t][0], dZs[t][1], dZs[t][2], dZs[t][3]);
+            *reinterpret_cast<float4 *>(o.dZ + (r * 2 + 1) * H + 16 * t + 4 * g) = make_float4(dZt[t][0], dZt[t][1], dZt[t][2], dZt[t][3]);
+        }
+    }
+    // 6. d lev = (M0^T dZ_s) * [a > 0] + (M0^T dZ_t) * [b > 0], tile by tile (one fragment feeds both branches)
+    const auto wg1t = wrsrc(T.g1T.w);
+    floatx4 DL[NTD];
+#pragma unroll
+    for (int t = 0; t < NTD; ++t) {
+        float4 wf[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) wf[q] = wload(wg1t, vo, (t * 4 + q) * 64);
+        floatx4 as = floatx4{0.f, 0.f, 0.f, 0.f}, at = as;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            as = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q].x, dZs[q].x, as, 0, 0, 0);
+            at = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q].x, dZt[q].x, at, 0, 0, 0);
+            as = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q].y, dZs[q].y, as, 0, 0, 0);
+            at = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q].y, dZt[q].y, at, 0, 0, 0);
+            as = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q].z, dZs[q].z, as, 0, 0, 0);
+            at = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q].z, dZt[q].z, at, 0, 0, 0);
+            as = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q].w, dZs[q].w, as, 0, 0, 0);
+            at = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q].w, dZt[q].w, at, 0, 0, 0);
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const float vs = (ma >> (4 * t + s)) & 1u ? as[s] : 0.f, vt = (mb >> (4 * t + s)) & 1u ? at[s] : 0.f;
+            DL[t][s] = vs + vt;
+        }
+        if (valid)
+            *reinterpret_cast<float4 *>(o.dlev + r * DN + 16 * t + 4 * g) = make_float4(DL[t][0], DL[t][1], DL[t][2], DL[t][3]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // 7. d time features = lin_event's time columns^T d lev, times -sin(dt w + phi)
+    floatx4 GT[NTD];
+    rgemm<NTD, NTD, NTD>(T.evT, DL, GT);
+    if (valid) {
+#pragma unroll
+        for (int t = 0; t < NTD; ++t) {
+            float gv[4];
+            const float4 f4 = *reinterpret_cast<const float4 *>(P.freq + 16 * t + 4 * g);
+            const float4 h4 = *reinterpret_cast<const float4 *>(P.phase + 16 * t + 4 * g);
+            const float fv[4] = {f4.x, f4.y, f4.z, f4.w}, hv[4] = {h4.x, h4.y, h4.z, h4.w};
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int j = 16 * t + 4 * g + s;
+                gv[s] = (t < NTD - 1 || j < dn) ? -GT[t][s] * sin_rd(__fadd_rn(__fmul_rn(dt, fv[s]), hv[s])) : 0.f;
+            }
+            *reinterpret_cast<float4 *>(o.g + r * DN + 16 * t + 4 * g) = make_float4(gv[0], gv[1], gv[2], gv[3]);
+        }
+    }
+}
+
+
 // ------------------------------------------------------------------ weight gradients: dW = dY^T X over rows
 // One launch computes every weight / bias gradient of the encoder from the (dY, X) row pairs the two
 // backward kernels wrote: job j covers a 64 x 64 block of dW_j (its bias gradient = a virtual column of
@@ -1197,8 +1414,22 @@ extern "C" int tm_encoder_bwd(const tm_weights *w, const float *n_feat, const fl
     const int64_t n_rows = n_walks * 3;
     GcnBwdOut go{io->ev, io->AB, io->H, io->dZ, io->dlev, io->g, io->dt};
     pe = prof_begin(s);
-    gcn_bwd_kernel<<<dim3((unsigned)((n_rows + TILE_ROWS - 1) / TILE_ROWS)), 256, lg, s>>>(
-        P, w->T, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, io->dF, go);
+    const int nqe = r16(P.kev) / 16;
+    // register-resident instance: hid_dim 64, 11 node-feature tiles (dn 161..176, a multiple of 4), lin_event
+    // with 11..14 K steps; the LDS-tiled kernel otherwise
+    const bool reg = P.h == HID && r16(P.dn) == 176 && P.dn % 4 == 0 && P.de % 4 == 0 && nqe >= 11 && nqe <= 14 &&
+                     P.g1.nt == 4 && P.g1.nq == 11 && w->T.g2T.nt == 4 && w->T.g1T.nt == 11 && w->T.g1T.nq == 4 &&
+                     w->T.evT.nt == 11 && w->T.evT.nq == 11 && P.ev.nq == nqe && std::getenv("TEMPME_GCN_BWD_LDS") == nullptr;
+    if (reg) {
+        const unsigned blocks = (unsigned)((n_rows + 63) / 64);
+        if (nqe == 11) gcn_bwd_reg_kernel<11><<<dim3(blocks), 256, 0, s>>>(P, w->T, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, io->dF, go);
+        else if (nqe == 12) gcn_bwd_reg_kernel<12><<<dim3(blocks), 256, 0, s>>>(P, w->T, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, io->dF, go);
+        else if (nqe == 13) gcn_bwd_reg_kernel<13><<<dim3(blocks), 256, 0, s>>>(P, w->T, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, io->dF, go);
+        else gcn_bwd_reg_kernel<14><<<dim3(blocks), 256, 0, s>>>(P, w->T, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, io->dF, go);
+    } else {
+        gcn_bwd_kernel<<<dim3((unsigned)((n_rows + TILE_ROWS - 1) / TILE_ROWS)), 256, lg, s>>>(
+            P, w->T, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, io->dF, go);
+    }
     TM_CHECK_LAUNCH();
     prof_end("gcn_bwd_kernel", s, pe);
     return TM_OK;

@@ -38,6 +38,8 @@ class Batch:
         # (node6 [3,B,W,6], eid3, ts3, cat [3,B,W], cnt [3,B,W,3,3]) device tensors: the three sides of the
         # batch stacked, so the explainer encodes them in one call (per-side walks are views of these)
         self.stacked = stacked
+        self.sub_stacked = None   # (hop-1 nodes, hop-1 eids, hop-2 nodes, hop-2 eids) [3, B, ...] when gathered
+        self.imp_all = None       # encode_sides' [3 B W] importances and their per-side views
 
     def __len__(self):
         return int(self.src.shape[0])
@@ -93,7 +95,10 @@ def _batch(src, dst, ts, e_idx, fake, node6, eid3, ts3, cat, cnt, s1, s2):
         subgraphs.append(([s1[0][s], s2[0][s]], [s1[1][s], s2[1][s]], [s1[2][s], s2[2][s]]))
         walks.append((node6[s], eid3[s], ts3[s], cat[s].unsqueeze(-1), None))
         edges.append(cnt[s])
-    return Batch(src, dst, ts, e_idx, fake, subgraphs, walks, edges, stacked=(node6, eid3, ts3, cat, cnt))
+    b = Batch(src, dst, ts, e_idx, fake, subgraphs, walks, edges, stacked=(node6, eid3, ts3, cat, cnt))
+    # the three sides' hop-1 / hop-2 node and edge ids as the gathered [3, B, ...] tensors (explain_sides)
+    b.sub_stacked = (s1[0], s1[1], s2[0], s2[1])
+    return b
 
 
 def _as_dev(x, dev, dtype):
@@ -117,7 +122,18 @@ def encode_sides(explainer, batch):
     G, B, W = node6.shape[0], node6.shape[1], node6.shape[2]
     cut = _as_dev(batch.ts, dev, torch.float64).reshape(1, B).expand(G, B)
     imp = explainer.forward_groups(node6, eid3, ts3, cat.reshape(G, B, W), cut, cnt, G, B, W)
-    return list(imp.view(G, B, W, 1).unbind(0))
+    sides = list(imp.view(G, B, W, 1).unbind(0))
+    batch.imp_all = (imp, sides)      # the three sides' importances as one tensor (explain_sides, kl_loss)
+    return sides
+
+
+def _stacked_imp(batch, imps, G, B, W):
+    """[G, B, W] importances: encode_sides' single output when ``imps`` are its per-side views (no copy),
+    else a stack of them."""
+    ia = getattr(batch, "imp_all", None)
+    if ia is not None and len(imps) == len(ia[1]) and all(a is b for a, b in zip(imps, ia[1])):
+        return ia[0].view(G, B, W)
+    return torch.stack([x.reshape(B, W) for x in imps])
 
 
 class GradAllReduce:
@@ -180,12 +196,16 @@ def explain_sides(explainer, batch, imps, training):
     dev = explainer._dev()
     node6, eid3, ts3, cat, cnt = batch.stacked
     G, B, W = eid3.shape[0], eid3.shape[1], eid3.shape[2]
-    s1n = torch.stack([_as_dev(sg[0][0], dev, torch.int32) for sg in batch.subgraphs])
-    s1e = torch.stack([_as_dev(sg[1][0], dev, torch.int32) for sg in batch.subgraphs])
-    s2n = torch.stack([_as_dev(sg[0][1], dev, torch.int32) for sg in batch.subgraphs])
-    s2e = torch.stack([_as_dev(sg[1][1], dev, torch.int32) for sg in batch.subgraphs])
+    ss = getattr(batch, "sub_stacked", None)
+    if ss is not None and all(x.is_cuda and x.dtype == torch.int32 and x.is_contiguous() for x in ss):
+        s1n, s1e, s2n, s2e = ss
+    else:
+        s1n = torch.stack([_as_dev(sg[0][0], dev, torch.int32) for sg in batch.subgraphs])
+        s1e = torch.stack([_as_dev(sg[1][0], dev, torch.int32) for sg in batch.subgraphs])
+        s2n = torch.stack([_as_dev(sg[0][1], dev, torch.int32) for sg in batch.subgraphs])
+        s2e = torch.stack([_as_dev(sg[1][1], dev, torch.int32) for sg in batch.subgraphs])
     N = s1n.shape[-1]
-    imp = torch.stack([x.reshape(B, W) for x in imps])
+    imp = _stacked_imp(batch, imps, G, B, W)
     e1, e2 = explainer.explain_groups(imp, eid3, ts3, s1n, s1e, s2n, s2e, G, B, W, N, training)
     if explainer.base_type == "tgn":
         return [e1.reshape(G * B, N), e2.reshape(G * B, N * N)]
@@ -227,7 +247,7 @@ def train_step(explainer, base_model, optimizer, batch, *, beta=0.5, prior_p=0.3
     if batch.stacked is not None and explainer._hip_ok() and explainer.prior == "empirical":
         # the three per-side kl_loss calls as one tm_kl_loss launch (value and gradient)
         B, W = g_s.shape[0], g_s.shape[1]
-        prob = torch.stack([g.reshape(B, W) for g in (g_s, g_t, g_b)])
+        prob = _stacked_imp(batch, (g_s, g_t, g_b), 3, B, W)
         kl_loss = explainer.kl_loss_groups(prob, batch.stacked[3].reshape(3, B, W), target=prior_p)
     else:
         kl_loss = (explainer.kl_loss(g_s, w_s, target=prior_p) + explainer.kl_loss(g_t, w_t, target=prior_p)
