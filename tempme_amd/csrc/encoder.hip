@@ -2148,8 +2148,9 @@ extern "C" int tm_encoder_train_fwd(const tm_weights *w, const float *n_feat, co
     prof_end("std_kernel", s, pe);
     const int64_t n_rows = n_walks * 3;
     pe = prof_begin(s);
-    gcn_kernel<<<dim3((unsigned)((n_rows + TILE_ROWS - 1) / TILE_ROWS)), 256, lds_g, s>>>(
-        P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, F);
+    if (!launch_gcn_fwd_reg(P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, F, s))
+        gcn_kernel<<<dim3((unsigned)((n_rows + TILE_ROWS - 1) / TILE_ROWS)), 256, lds_g, s>>>(
+            P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, F);
     TM_CHECK_LAUNCH();
     prof_end("gcn_kernel", s, pe);
     pe = prof_begin(s);

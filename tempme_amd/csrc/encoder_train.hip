@@ -649,16 +649,24 @@ __global__ void __launch_bounds__(256) gcn_bwd_kernel(EncW P, EncWT T, int64_t n
 // pairs the weight gradients need are stored as they are produced.  Every tile accumulates its K steps in
 // the LDS kernel's order; the time-feature gradient's sin is the branch-free sin_rd (common.h, |error| ~1e-7;
 // ocml's sinf carries a Payne-Hanek slow path).
-template <int NQE>
-__global__ void __launch_bounds__(256, 2) gcn_bwd_reg_kernel(EncW P, EncWT T, int64_t n_rows,
-                                                              const float *__restrict__ n_feat,
-                                                              const float *__restrict__ e_feat,
-                                                              const int32_t *__restrict__ node6,
-                                                              const int32_t *__restrict__ eid3,
-                                                              const float *__restrict__ ts3,
-                                                              const float *__restrict__ cnt,
-                                                              const float *__restrict__ dF, GcnBwdOut o) {
-    constexpr int NTD = 11, KE = 16 * NQE, DN = 16 * NTD, H = HID;
+struct GcnRow {
+    int64_t r, rc;   // this lane's row (walk position) and its clamped index
+    bool valid;
+    float dt;
+};
+
+// The front of the register-resident event_gcn kernels for one wave's 16 walk positions: event features,
+// lin_event, A / B and event_gcn's first layer (pre-activation) of both branches; BWD also stores the event
+// features and A / B rows and dt for the weight gradients and returns the relu masks of a / b as bits.
+// tabw / tabp: the workgroup's LDS tables of the time encoder's frequency / phase on the event-feature axis.
+template <int NQE, bool BWD>
+__device__ __forceinline__ GcnRow gcn_front(const EncW &P, int64_t n_rows, const float *__restrict__ n_feat,
+                                            const float *__restrict__ e_feat, const int32_t *__restrict__ node6,
+                                            const int32_t *__restrict__ eid3, const float *__restrict__ ts3,
+                                            const float *__restrict__ cnt, float4 *tabw, float4 *tabp,
+                                            const GcnBwdOut *o, floatx4 (&Hs)[4], floatx4 (&Ht)[4], uint64_t &ma,
+                                            uint64_t &mb) {
+    constexpr int NTD = 11, KE = 16 * NQE, DN = 16 * NTD;
     const int lane = threadIdx.x & 63, col = lane & 15, g = lane_id() >> 4;
     const int64_t r0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16;
     const int64_t r = r0 + col;
@@ -670,12 +678,11 @@ __global__ void __launch_bounds__(256, 2) gcn_bwd_reg_kernel(EncW P, EncWT T, in
     const int32_t e = eid3[rc], ns = node6[w * 6 + 2 * p], nt = node6[w * 6 + 2 * p + 1];
     const float dt = ts3[w * 3 + 2] - ts3[w * 3 + p];
     const float c0 = cnt[rc * 3], c1 = cnt[rc * 3 + 1], c2 = cnt[rc * 3 + 2];
-    if (valid && g == 0) o.dt[r] = dt;
+    if (BWD && valid && g == 0) o->dt[r] = dt;
     // 1. event features (B fragments: lane group g holds features 16 q + 4 g + s of column col) -> lin_event.
     // Branch-free: the edge-feature float4 (clamped index), the counts and the cos are all formed and the
     // lane's value selected; the time encoder's frequency / phase come from an LDS table laid out on the
     // event-feature axis (zero outside the time block)
-    __shared__ float4 tabw[NQE * 4], tabp[NQE * 4];
     for (int i = threadIdx.x; i < NQE * 16; i += blockDim.x) {
         const int ti = i - de - 3;
         reinterpret_cast<float *>(tabw)[i] = (ti >= 0 && ti < dn) ? P.freq[ti] : 0.f;
@@ -698,8 +705,8 @@ __global__ void __launch_bounds__(256, 2) gcn_bwd_reg_kernel(EncW P, EncWT T, in
             if (k < de) v = ef[s];
             X[q][s] = v;
         }
-        if (valid)
-            *reinterpret_cast<float4 *>(o.ev + r * KE + 16 * q + 4 * g) = make_float4(X[q][0], X[q][1], X[q][2], X[q][3]);
+        if (BWD && valid)
+            *reinterpret_cast<float4 *>(o->ev + r * KE + 16 * q + 4 * g) = make_float4(X[q][0], X[q][1], X[q][2], X[q][3]);
     }
     floatx4 L[NTD];
     rgemm<NTD, NQE, NQE>(P.ev, X, L);
@@ -714,10 +721,9 @@ __global__ void __launch_bounds__(256, 2) gcn_bwd_reg_kernel(EncW P, EncWT T, in
     const float4 *nrt = reinterpret_cast<const float4 *>(n_feat + (int64_t)nt * dn);
     const auto wg1 = wrsrc(P.g1.w);
     const int vo = lane_id() * 16;
-    floatx4 Hs[4], Ht[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) Hs[t] = Ht[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    uint64_t ma = 0, mb = 0;
+    ma = mb = 0;
     float4 wq[2][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) wq[0][t] = wload(wg1, vo, (t * NTD + 0) * 64);
@@ -738,12 +744,14 @@ __global__ void __launch_bounds__(256, 2) gcn_bwd_reg_kernel(EncW P, EncWT T, in
             const bool in = q < NTD - 1 || c < dn;     // 161 <= dn <= 176: only the last tile has padding
             A[s] = in ? xs[s] + relu(a) : 0.f;
             Bq[s] = in ? xt[s] + relu(b) : 0.f;
-            ma |= (uint64_t)(in && a > 0.f) << (4 * q + s);
-            mb |= (uint64_t)(in && b > 0.f) << (4 * q + s);
+            if (BWD) {
+                ma |= (uint64_t)(in && a > 0.f) << (4 * q + s);
+                mb |= (uint64_t)(in && b > 0.f) << (4 * q + s);
+            }
         }
-        if (valid) {
-            *reinterpret_cast<float4 *>(o.AB + (r * 2) * DN + 16 * q + 4 * g) = make_float4(A[0], A[1], A[2], A[3]);
-            *reinterpret_cast<float4 *>(o.AB + (r * 2 + 1) * DN + 16 * q + 4 * g) = make_float4(Bq[0], Bq[1], Bq[2], Bq[3]);
+        if (BWD && valid) {
+            *reinterpret_cast<float4 *>(o->AB + (r * 2) * DN + 16 * q + 4 * g) = make_float4(A[0], A[1], A[2], A[3]);
+            *reinterpret_cast<float4 *>(o->AB + (r * 2 + 1) * DN + 16 * q + 4 * g) = make_float4(Bq[0], Bq[1], Bq[2], Bq[3]);
         }
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -761,10 +769,36 @@ __global__ void __launch_bounds__(256, 2) gcn_bwd_reg_kernel(EncW P, EncWT T, in
     }
     // the relu masks as VGPR bit fields (opaque to the compiler: it would otherwise keep every compare's lane
     // mask alive in SGPR pairs until step 6 and spill the scalar file)
-    uint32_t ma0 = (uint32_t)ma, ma1 = (uint32_t)(ma >> 32), mb0 = (uint32_t)mb, mb1 = (uint32_t)(mb >> 32);
-    asm volatile("" : "+v"(ma0), "+v"(ma1), "+v"(mb0), "+v"(mb1));
-    ma = ((uint64_t)ma1 << 32) | ma0;
-    mb = ((uint64_t)mb1 << 32) | mb0;
+    if (BWD) {
+        uint32_t ma0 = (uint32_t)ma, ma1 = (uint32_t)(ma >> 32), mb0 = (uint32_t)mb, mb1 = (uint32_t)(mb >> 32);
+        asm volatile("" : "+v"(ma0), "+v"(ma1), "+v"(mb0), "+v"(mb1));
+        ma = ((uint64_t)ma1 << 32) | ma0;
+        mb = ((uint64_t)mb1 << 32) | mb0;
+    }
+    return GcnRow{r, rc, valid, dt};
+}
+
+template <int NQE>
+__global__ void __launch_bounds__(256, 2) gcn_bwd_reg_kernel(EncW P, EncWT T, int64_t n_rows,
+                                                              const float *__restrict__ n_feat,
+                                                              const float *__restrict__ e_feat,
+                                                              const int32_t *__restrict__ node6,
+                                                              const int32_t *__restrict__ eid3,
+                                                              const float *__restrict__ ts3,
+                                                              const float *__restrict__ cnt,
+                                                              const float *__restrict__ dF, GcnBwdOut o) {
+    constexpr int NTD = 11, DN = 16 * NTD, H = HID;
+    __shared__ float4 tabw[NQE * 4], tabp[NQE * 4];
+    const int g = lane_id() >> 4;
+    const int vo = lane_id() * 16;
+    const int dn = P.dn;
+    floatx4 Hs[4], Ht[4];
+    uint64_t ma, mb;
+    const GcnRow rw = gcn_front<NQE, true>(P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, tabw, tabp, &o, Hs, Ht,
+                                           ma, mb);
+    const int64_t r = rw.r, rc = rw.rc;
+    const bool valid = rw.valid;
+    const float dt = rw.dt;
     // 3. z = relu(MLP.0 . + b) of both branches (stored: MLP.2's inputs); 4. dU = dF (the head's gradient);
     // 5. dZ = (M2^T dU) * [z > 0]
     uint32_t mz = 0;
@@ -855,6 +889,44 @@ __global__ void __launch_bounds__(256, 2) gcn_bwd_reg_kernel(EncW P, EncWT T, in
     }
 }
 
+
+// Register-resident event_gcn forward for the training step (hid_dim 64, 11 node tiles): F = [MLP(A) | MLP(B)]
+// per walk position (explainer_new.py:79-96), the front of gcn_bwd_reg_kernel plus MLP.2, with gcn_kernel's
+// accumulation order (the same F; tm_encoder_train_fwd keeps it for the head and the backward).
+template <int NQE>
+__global__ void __launch_bounds__(256, 2) gcn_fwd_reg_kernel(EncW P, int64_t n_rows, const float *__restrict__ n_feat,
+                                                              const float *__restrict__ e_feat,
+                                                              const int32_t *__restrict__ node6,
+                                                              const int32_t *__restrict__ eid3,
+                                                              const float *__restrict__ ts3,
+                                                              const float *__restrict__ cnt, float *__restrict__ F) {
+    constexpr int H = HID;
+    __shared__ float4 tabw[NQE * 4], tabp[NQE * 4];
+    const int g = lane_id() >> 4;
+    floatx4 Hs[4], Ht[4];
+    uint64_t ma, mb;
+    const GcnRow rw = gcn_front<NQE, false>(P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, tabw, tabp, nullptr, Hs,
+                                            Ht, ma, mb);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const float4 b = *reinterpret_cast<const float4 *>(P.g1.b + 16 * t + 4 * g);
+        Hs[t] = floatx4{relu(Hs[t][0] + b.x), relu(Hs[t][1] + b.y), relu(Hs[t][2] + b.z), relu(Hs[t][3] + b.w)};
+        Ht[t] = floatx4{relu(Ht[t][0] + b.x), relu(Ht[t][1] + b.y), relu(Ht[t][2] + b.z), relu(Ht[t][3] + b.w)};
+    }
+    floatx4 Fs[4], Ft[4];
+    rgemm<4, 4, 4>(P.g2, Hs, Fs);
+    rgemm<4, 4, 4>(P.g2, Ht, Ft);
+    if (rw.valid) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const float4 b = *reinterpret_cast<const float4 *>(P.g2.b + 16 * t + 4 * g);
+            *reinterpret_cast<float4 *>(F + rw.r * (2 * H) + 16 * t + 4 * g) =
+                make_float4(Fs[t][0] + b.x, Fs[t][1] + b.y, Fs[t][2] + b.z, Fs[t][3] + b.w);
+            *reinterpret_cast<float4 *>(F + rw.r * (2 * H) + H + 16 * t + 4 * g) =
+                make_float4(Ft[t][0] + b.x, Ft[t][1] + b.y, Ft[t][2] + b.z, Ft[t][3] + b.w);
+        }
+    }
+}
 
 // ------------------------------------------------------------------ weight gradients: dW = dY^T X over rows
 // One launch computes every weight / bias gradient of the encoder from the (dY, X) row pairs the two
@@ -968,6 +1040,83 @@ __global__ void __launch_bounds__(256) wgrad_partial_kernel(WgPlan P, float *__r
     for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) out[(16 * wave + 4 * g + r) * 64 + 16 * t + m] = acc[t][r];
+}
+
+// The same partial blocks with the row slabs staged TRANSPOSED in LDS ([column][row], pitch WG_TP): a lane's
+// four K values (four consecutive rows of one column) are one ds_read_b128, so a 16-row K block of a wave's
+// 2 x 2 tiles (32 x 32 of the 64 x 64 block) takes 4 LDS reads for 16 MFMAs instead of 5 reads per 4 MFMAs.
+// The rows inside a 16-row block go to the MFMAs in a different order than wgrad_partial_kernel's
+// (deterministic either way).
+constexpr int WG_TP = 68;
+__global__ void __launch_bounds__(256) wgrad_partial_t_kernel(WgPlan P, float *__restrict__ part) {
+    __shared__ __attribute__((aligned(16))) float Yt[2][64 * WG_TP], Xt[2][64 * WG_TP];
+    const int64_t bid = blockIdx.x;
+    int j = 0;
+    while (j + 1 < P.njob && bid >= P.job[j + 1].wg_begin) ++j;
+    const WgJob &J = P.job[j];
+    const int64_t local = bid - J.wg_begin;
+    const int nb = J.OB * J.IB;
+    const int chunk = (int)(local / nb), tb = (int)(local % nb), ob = tb / J.IB, ib = tb % J.IB;
+    const int o0 = ob * 64, i0 = ib * 64;
+    const int r_begin = chunk * WG_CHUNK, r_end = min(J.R, r_begin + WG_CHUNK);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, m = lane & 15;
+    const int wo = 32 * (wave >> 1), wi = 32 * (wave & 1);   // this wave's 32 x 32 quarter of the block
+    floatx4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+    auto store_t = [&](const Slab &sl, float *Ys, float *Xs) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int e = tid + 256 * k, row = e >> 4, c = (e & 15) * 4;
+            const float yv[4] = {sl.y[k].x, sl.y[k].y, sl.y[k].z, sl.y[k].w};
+            const float xv[4] = {sl.x[k].x, sl.x[k].y, sl.x[k].z, sl.x[k].w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                Ys[(c + q) * WG_TP + row] = yv[q];
+                Xs[(c + q) * WG_TP + row] = xv[q];
+            }
+        }
+    };
+    Slab sl;
+    slab_load(J, r_begin, r_end, o0, i0, sl);
+    store_t(sl, Yt[0], Xt[0]);
+    __syncthreads();
+    int buf = 0;
+    for (int r0 = r_begin; r0 < r_end; r0 += 64) {
+        const bool more = r0 + 64 < r_end;
+        if (more) slab_load(J, r0 + 64, r_end, o0, i0, sl);
+        const float *Y = Yt[buf], *X = Xt[buf];
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+            float4 a[2], b[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                a[t] = *reinterpret_cast<const float4 *>(Y + (wo + 16 * t + m) * WG_TP + 16 * kb + 4 * g);
+                b[t] = *reinterpret_cast<const float4 *>(X + (wi + 16 * t + m) * WG_TP + 16 * kb + 4 * g);
+            }
+#pragma unroll
+            for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+                for (int it = 0; it < 2; ++it) {
+                    acc[ot][it] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ot].x, b[it].x, acc[ot][it], 0, 0, 0);
+                    acc[ot][it] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ot].y, b[it].y, acc[ot][it], 0, 0, 0);
+                    acc[ot][it] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ot].z, b[it].z, acc[ot][it], 0, 0, 0);
+                    acc[ot][it] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ot].w, b[it].w, acc[ot][it], 0, 0, 0);
+                }
+        }
+        if (more) store_t(sl, Yt[buf ^ 1], Xt[buf ^ 1]);
+        __syncthreads();
+        buf ^= 1;
+    }
+    float *out = part + J.part_begin + local * 4096;
+#pragma unroll
+    for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+        for (int it = 0; it < 2; ++it)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) out[(wo + 16 * ot + 4 * g + r) * 64 + wi + 16 * it + m] = acc[ot][it][r];
 }
 
 __global__ void wgrad_reduce_kernel(WgPlan P, const float *__restrict__ part) {
@@ -1435,6 +1584,22 @@ extern "C" int tm_encoder_bwd(const tm_weights *w, const float *n_feat, const fl
     return TM_OK;
 }
 
+bool tmk::launch_gcn_fwd_reg(const EncW &P, int64_t n_rows, const float *n_feat, const float *e_feat,
+                             const int32_t *node6, const int32_t *eid3, const float *ts3, const float *cnt, float *F,
+                             hipStream_t s) {
+    const int nqe = r16(P.kev) / 16;
+    if (!(P.h == HID && r16(P.dn) == 176 && P.dn % 4 == 0 && P.de % 4 == 0 && nqe >= 11 && nqe <= 14 &&
+          P.ev.nt == 11 && P.ev.nq == nqe && P.g1.nt == 4 && P.g1.nq == 11 && P.g2.nt == 4 && P.g2.nq == 4) ||
+        std::getenv("TEMPME_GCN_LDS") != nullptr)
+        return false;
+    const unsigned blocks = (unsigned)((n_rows + 63) / 64);
+    if (nqe == 11) gcn_fwd_reg_kernel<11><<<dim3(blocks), 256, 0, s>>>(P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, F);
+    else if (nqe == 12) gcn_fwd_reg_kernel<12><<<dim3(blocks), 256, 0, s>>>(P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, F);
+    else if (nqe == 13) gcn_fwd_reg_kernel<13><<<dim3(blocks), 256, 0, s>>>(P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, F);
+    else gcn_fwd_reg_kernel<14><<<dim3(blocks), 256, 0, s>>>(P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, F);
+    return true;
+}
+
 // Shared driver of the weight-gradient launches: jobs (dY, X, rows) and targets (dW, db, job range).
 static int run_wgrad(const tm_wgrad_job *jobs, int njob, const tm_wgrad_target *tgts, int ntgt, hipStream_t s,
                      const char *what) {
@@ -1493,7 +1658,10 @@ static int run_wgrad(const tm_wgrad_job *jobs, int njob, const tm_wgrad_target *
     float *part = reinterpret_cast<float *>(scratch((size_t)pb * sizeof(float), s));
     if (!part) return fail(TM_E_HIP, std::string(what) + ": scratch allocation failed");
     hipEvent_t pe = prof_begin(s);
-    wgrad_partial_kernel<<<dim3((unsigned)wg), 256, 0, s>>>(P, part);
+    if (std::getenv("TEMPME_WGRAD_ROWMAJOR"))
+        wgrad_partial_kernel<<<dim3((unsigned)wg), 256, 0, s>>>(P, part);
+    else
+        wgrad_partial_t_kernel<<<dim3((unsigned)wg), 256, 0, s>>>(P, part);
     TM_CHECK_LAUNCH();
     prof_end("wgrad_partial_kernel", s, pe);
     pe = prof_begin(s);
