@@ -288,6 +288,14 @@ int tm_explain_train_fwd(const tm_weights *w, const float *e_feat, int32_t n_gro
                          const int32_t *eid3, const float *ts3, const float *imp, const int32_t *sub1_eid,
                          const int32_t *sub2_eid, const uint8_t *keep1, const uint8_t *keep2, float scale1,
                          float scale2, const tm_explain_grad_io *io, float *p1, float *p2, void *stream);
+/* tm_explain_train_fwd plus the padding mask of explainer_new.py:400-404 as factors: pad1 [G,B,N] / pad2
+ * [G,B,N^2] = 0 where sub1_node / sub2_node is 0, else 1 (beta_sample's output times the mask = the
+ * reference's masked_fill). */
+int tm_explain_train_fwd_pad(const tm_weights *w, const float *e_feat, int32_t n_groups, int32_t B, int32_t W,
+                             int32_t N, const int32_t *eid3, const float *ts3, const float *imp, const int32_t *sub1_eid,
+                             const int32_t *sub2_eid, const uint8_t *keep1, const uint8_t *keep2, float scale1,
+                             float scale2, const tm_explain_grad_io *io, float *p1, float *p2, const int32_t *sub1_node,
+                             const int32_t *sub2_node, float *pad1, float *pad2, void *stream);
 /* Backward given dp1 / dp2: d_imp [G,B,W] (the scatter-max gradient is split evenly among tied walk
  * positions, as torch's scatter_reduce amax backward does) and the gate's weight gradients
  * grads = 8 DEVICE pointers: edge_dependency_gcn.0 w/b, .3 w/b, .6 w/b, time_encoder.basis_freq, .phase

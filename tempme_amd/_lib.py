@@ -36,7 +36,7 @@ EXPORTS = (
     "tm_sample_events", "tm_gather_rows", "tm_weights_create", "tm_weights_create_ex", "tm_weights_pack", "tm_weights_variant", "tm_weights_free",
     "tm_encoder_workspace_bytes",
     "tm_encoder_fwd", "tm_encoder_fwd_tab", "tm_encoder_train_supported", "tm_encoder_train_fwd", "tm_encoder_bwd", "tm_encoder_wgrad", "tm_wgrad",
-    "tm_explain_train_fwd", "tm_explain_train_bwd", "tm_kl_loss", "tm_edge_importance", "tm_edge_gate_table",
+    "tm_explain_train_fwd", "tm_explain_train_fwd_pad", "tm_explain_train_bwd", "tm_kl_loss", "tm_edge_importance", "tm_edge_gate_table",
     "tm_edge_table_cols", "tm_edge_tables", "tm_edge_feature_table", "tm_edge_importance_tab", "tm_tgn_attn_fwd", "tm_tgn_attn_bwd", "tm_gm_packed_floats", "tm_gm_pack", "tm_gm_embed", "tm_gm_embed_bwd_ok", "tm_gm_embed_bwd", "tm_gm_packed_a_floats", "tm_gm_pack_a", "tm_gm_fused_ok", "tm_dropin_create", "tm_dropin_free", "tm_dropin_forward", "tm_dropin_set_stream", "tm_edge_importance_gf", "tm_edge_importance_gf3", "tm_edge_importance_gf3_bern",
     "tm_mask_least_important", "tm_profile_enable", "tm_profile_sync", "tm_profile_entry",
 )
@@ -137,6 +137,8 @@ def _sig(L):
     L.tm_wgrad.argtypes = [C.POINTER(WgradJob), i32, C.POINTER(WgradTarget), i32, vp]
     L.tm_explain_train_fwd.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, C.c_float, C.c_float,
                                        C.POINTER(ExplainGradIO), vp, vp, vp]
+    L.tm_explain_train_fwd_pad.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, C.c_float,
+                                           C.c_float, C.POINTER(ExplainGradIO), vp, vp, vp, vp, vp, vp, vp]
     L.tm_explain_train_bwd.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, C.c_float, C.c_float, vp, vp,
                                        C.POINTER(ExplainGradIO), vp, C.POINTER(vp), vp]
     L.tm_edge_importance.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]

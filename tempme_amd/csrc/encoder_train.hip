@@ -1262,7 +1262,11 @@ __global__ void __launch_bounds__(256) explain_train_kernel(int32_t W, int32_t N
                                                             const float *__restrict__ gate,
                                                             const int32_t *__restrict__ sub1_eid,
                                                             const int32_t *__restrict__ sub2_eid,
-                                                            float *__restrict__ p1, float *__restrict__ p2) {
+                                                            float *__restrict__ p1, float *__restrict__ p2,
+                                                            const int32_t *__restrict__ sub1_node = nullptr,
+                                                            const int32_t *__restrict__ sub2_node = nullptr,
+                                                            float *__restrict__ keep1 = nullptr,
+                                                            float *__restrict__ keep2 = nullptr) {
     extern __shared__ __attribute__((aligned(16))) int32_t hkey[];
     uint32_t *hval = reinterpret_cast<uint32_t *>(hkey + (1 << hbits));
     const int64_t ge = blockIdx.x;
@@ -1276,6 +1280,10 @@ __global__ void __launch_bounds__(256) explain_train_kernel(int32_t W, int32_t N
         const float p = hh >= 0 ? __uint_as_float(hval[hh]) : 0.f;   // ids no walk passes through: 0
         if (h1) p1[o] = p;
         else p2[o] = p;
+        if (keep1) {   // the padding mask of :400-404 (node 0 -> weight 0), as a factor
+            if (h1) keep1[o] = sub1_node[o] == 0 ? 0.f : 1.f;
+            else keep2[o] = sub2_node[o] == 0 ? 0.f : 1.f;
+        }
     }
 }
 
@@ -1719,11 +1727,38 @@ static int expl_hbits(int W) {
     return hb;
 }
 
+static int explain_train_fwd(const tm_weights *w, const float *e_feat, int32_t n_groups, int32_t B, int32_t W,
+                             int32_t N, const int32_t *eid3, const float *ts3, const float *imp, const int32_t *sub1_eid,
+                             const int32_t *sub2_eid, const uint8_t *keep1, const uint8_t *keep2, float scale1,
+                             float scale2, const tm_explain_grad_io *io, float *p1, float *p2, const int32_t *sub1_node,
+                             const int32_t *sub2_node, float *pad1, float *pad2, void *stream);
+
 extern "C" int tm_explain_train_fwd(const tm_weights *w, const float *e_feat, int32_t n_groups, int32_t B, int32_t W,
                                     int32_t N, const int32_t *eid3, const float *ts3, const float *imp,
                                     const int32_t *sub1_eid, const int32_t *sub2_eid, const uint8_t *keep1,
                                     const uint8_t *keep2, float scale1, float scale2, const tm_explain_grad_io *io,
                                     float *p1, float *p2, void *stream) {
+    return explain_train_fwd(w, e_feat, n_groups, B, W, N, eid3, ts3, imp, sub1_eid, sub2_eid, keep1, keep2, scale1,
+                             scale2, io, p1, p2, nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+extern "C" int tm_explain_train_fwd_pad(const tm_weights *w, const float *e_feat, int32_t n_groups, int32_t B,
+                                        int32_t W, int32_t N, const int32_t *eid3, const float *ts3, const float *imp,
+                                        const int32_t *sub1_eid, const int32_t *sub2_eid, const uint8_t *keep1,
+                                        const uint8_t *keep2, float scale1, float scale2,
+                                        const tm_explain_grad_io *io, float *p1, float *p2,
+                                        const int32_t *sub1_node, const int32_t *sub2_node, float *pad1, float *pad2,
+                                        void *stream) {
+    if (!sub1_node || !sub2_node || !pad1 || !pad2) return fail(TM_E_ARG, "tm_explain_train_fwd_pad: NULL pointer");
+    return explain_train_fwd(w, e_feat, n_groups, B, W, N, eid3, ts3, imp, sub1_eid, sub2_eid, keep1, keep2, scale1,
+                             scale2, io, p1, p2, sub1_node, sub2_node, pad1, pad2, stream);
+}
+
+static int explain_train_fwd(const tm_weights *w, const float *e_feat, int32_t n_groups, int32_t B, int32_t W,
+                             int32_t N, const int32_t *eid3, const float *ts3, const float *imp, const int32_t *sub1_eid,
+                             const int32_t *sub2_eid, const uint8_t *keep1, const uint8_t *keep2, float scale1,
+                             float scale2, const tm_explain_grad_io *io, float *p1, float *p2, const int32_t *sub1_node,
+                             const int32_t *sub2_node, float *pad1, float *pad2, void *stream) {
     if (!w || !io || n_groups < 0 || B < 0 || W <= 0 || N <= 0) return fail(TM_E_ARG, "tm_explain_train_fwd: bad arguments");
     const int64_t rows = (int64_t)n_groups * B;
     if (rows == 0) return TM_OK;
@@ -1745,7 +1780,7 @@ extern "C" int tm_explain_train_fwd(const tm_weights *w, const float *e_feat, in
     prof_end("gate_train_fwd_kernel", s, pe);
     pe = prof_begin(s);
     explain_train_kernel<<<dim3((unsigned)rows), 256, 2 * sizeof(int32_t) * (1u << hb), s>>>(
-        W, N, hb, eid3, imp, io->gate, sub1_eid, sub2_eid, p1, p2);
+        W, N, hb, eid3, imp, io->gate, sub1_eid, sub2_eid, p1, p2, sub1_node, sub2_node, pad1, pad2);
     TM_CHECK_LAUNCH();
     prof_end("explain_train_kernel", s, pe);
     return TM_OK;

@@ -548,16 +548,15 @@ class TempME(nn.Module):
         dev = self._dev()
         if masks is None:
             masks = self.gate_dropout_masks(n_groups * B * 3 * W)
-        args = (eid3.to(dev, torch.int32).contiguous(), ts3.to(dev, torch.float32).contiguous(),
-                s1e.to(dev, torch.int32).contiguous(), s2e.to(dev, torch.int32).contiguous(), masks,
-                int(n_groups), int(B), int(W), int(N))
-        p1, p2 = _ExplainFn.apply(self, args, imp.reshape(-1).to(dev, torch.float32).contiguous(),
+        i32 = lambda x: x.to(dev, torch.int32).contiguous()  # noqa: E731
+        args = (i32(eid3), ts3.to(dev, torch.float32).contiguous(), i32(s1e), i32(s2e), masks,
+                int(n_groups), int(B), int(W), int(N), i32(s1n), i32(s2n))
+        # p = [hop-1 | hop-2] maxima of the G groups in one buffer (one Beta draw below), pad = the padding mask
+        p, pad = _ExplainFn.apply(self, args, imp.reshape(-1).to(dev, torch.float32).contiguous(),
                                   *self._gate_params())
-        e1 = self.beta_sample(p1.view(n_groups, B, N), training)
-        e2 = self.beta_sample(p2.view(n_groups, B, N * N), training)
-        e1 = e1.masked_fill(s1n.to(dev).view(n_groups, B, N) == 0, 0)
-        e2 = e2.masked_fill(s2n.to(dev).view(n_groups, B, N * N) == 0, 0)
-        return e1, e2
+        n1 = n_groups * B * N
+        e = self.beta_sample(p, training) * pad    # beta_sample then masked_fill(node == 0, 0) (:400-404, :420-430)
+        return e[:n1].view(n_groups, B, N), e[n1:].view(n_groups, B, N * N)
 
     def _expl_io(self, R):
         dev = self._dev()
@@ -569,20 +568,32 @@ class TempME(nn.Module):
         return b, L.ExplainGradIO(*[b[k].data_ptr() for k in L.EXPL_IO_FIELDS])
 
     def _explain_fwd(self, args, imp):
-        eid3, ts3, s1e, s2e, (k1, k2, sc1, sc2), G, B, W, N = args
+        """-> p [G B N | G B N^2] (hop-1 then hop-2 maxima), and with the subgraph node ids in args their
+        padding mask in the same layout (else None), and the backward's buffers."""
+        eid3, ts3, s1e, s2e, (k1, k2, sc1, sc2), G, B, W, N = args[:9]
         dev = self._dev()
         _, et = self.feature_tables()
         b, io = self._expl_io(G * B * 3 * W)
-        p1 = torch.empty(max(G * B * N, 1), dtype=torch.float32, device=dev)
-        p2 = torch.empty(max(G * B * N * N, 1), dtype=torch.float32, device=dev)
-        L.check(L.lib().tm_explain_train_fwd(self.packed_weights(), L.ptr(et), G, B, W, N, L.ptr(eid3), L.ptr(ts3),
-                                             L.ptr(imp), L.ptr(s1e), L.ptr(s2e), L.ptr(k1), L.ptr(k2), sc1, sc2,
-                                             L.C.byref(io), L.ptr(p1), L.ptr(p2), L.stream_ptr(dev)),
-                "retrieve_edge_imp_node (training)")
-        return p1[:G * B * N], p2[:G * B * N * N], (b, io)
+        n1, n2 = G * B * N, G * B * N * N
+        pad = len(args) > 9
+        p = torch.empty(max((n1 + n2) * (2 if pad else 1), 1), dtype=torch.float32, device=dev)
+        pp = p.data_ptr()
+        if pad:
+            s1n, s2n = args[9], args[10]
+            q = pp + 4 * (n1 + n2)
+            rc = L.lib().tm_explain_train_fwd_pad(self.packed_weights(), L.ptr(et), G, B, W, N, L.ptr(eid3), L.ptr(ts3),
+                                                  L.ptr(imp), L.ptr(s1e), L.ptr(s2e), L.ptr(k1), L.ptr(k2), sc1, sc2,
+                                                  L.C.byref(io), pp, pp + 4 * n1, L.ptr(s1n), L.ptr(s2n), q,
+                                                  q + 4 * n1, L.stream_ptr(dev))
+        else:
+            rc = L.lib().tm_explain_train_fwd(self.packed_weights(), L.ptr(et), G, B, W, N, L.ptr(eid3), L.ptr(ts3),
+                                              L.ptr(imp), L.ptr(s1e), L.ptr(s2e), L.ptr(k1), L.ptr(k2), sc1, sc2,
+                                              L.C.byref(io), pp, pp + 4 * n1, L.stream_ptr(dev))
+        L.check(rc, "retrieve_edge_imp_node (training)")
+        return p[:n1 + n2], (p[n1 + n2:2 * (n1 + n2)] if pad else None), (b, io)
 
     def _explain_bwd(self, args, imp, bufs, dp1, dp2):
-        eid3, ts3, s1e, s2e, (k1, k2, sc1, sc2), G, B, W, N = args
+        eid3, ts3, s1e, s2e, (k1, k2, sc1, sc2), G, B, W, N = args[:9]
         dev = self._dev()
         b, io = bufs
         d_imp = torch.empty(max(G * B * W, 1), dtype=torch.float32, device=dev)
@@ -1283,8 +1294,8 @@ class _EvalExplain3RawFn(torch.autograd.Function):
                 imp_ = imp.detach().reshape(-1).to(torch.float32).requires_grad_(True)
                 a = (e3.contiguous(), t3.contiguous(), x1.contiguous(), x2.contiguous(), (None, None, 1.0, 1.0),
                      1, B, W, N)
-                p1, p2 = _ExplainFn.apply(ex, a, imp_, *params)
-                gs = torch.autograd.grad((p1, p2), [imp_] + list(params), grad_outputs=(g1[s], g2[s]),
+                p, _ = _ExplainFn.apply(ex, a, imp_, *params)
+                gs = torch.autograd.grad((p,), [imp_] + list(params), grad_outputs=(torch.cat([g1[s], g2[s]]),),
                                          allow_unused=True)
             d_imps.append(gs[0])
             pg = [torch.zeros_like(q) if g is None else g for g, q in zip(gs[1:], params)]
@@ -1353,18 +1364,24 @@ class _KLFn(torch.autograd.Function):
 
 
 class _ExplainFn(torch.autograd.Function):
-    """retrieve_edge_imp_node's gate + scatter-max + gather (training) on the HIP kernels."""
+    """retrieve_edge_imp_node's gate + scatter-max + gather (training) on the HIP kernels: p = [hop-1 | hop-2]
+    maxima in one tensor, and (with the subgraph node ids in args) the padding mask (no gradient)."""
 
     @staticmethod
     def forward(ctx, ex, args, imp, *params):
-        p1, p2, bufs = ex._explain_fwd(args, imp)
+        p, pad, bufs = ex._explain_fwd(args, imp)
         ctx.ex, ctx.args, ctx.bufs = ex, args, bufs
         ctx.save_for_backward(imp)
-        return p1, p2
+        if pad is not None:
+            ctx.mark_non_differentiable(pad)
+        return p, pad
 
     @staticmethod
-    def backward(ctx, dp1, dp2):
+    def backward(ctx, dp, _dpad):
         (imp,) = ctx.saved_tensors
-        d_imp, grads = ctx.ex._explain_bwd(ctx.args, imp, ctx.bufs, dp1, dp2)
+        G, B, N = ctx.args[5], ctx.args[6], ctx.args[8]
+        n1 = G * B * N
+        dp = dp.contiguous()
+        d_imp, grads = ctx.ex._explain_bwd(ctx.args, imp, ctx.bufs, dp[:n1], dp[n1:])
         ctx.bufs = None
         return (None, None, d_imp, *grads)

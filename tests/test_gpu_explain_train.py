@@ -65,7 +65,8 @@ def test_explain_backward_matches_autograd(dev, de, G, B, N, train):
     imp = t(imp_np).requires_grad_(True)
     args = (t(eid3), t(ts3), t(s1e), t(s2e), masks, G, B, W, N)
     from tempme_amd.explainer import _ExplainFn
-    p1, p2 = _ExplainFn.apply(ex, args, imp.reshape(-1), *ex._gate_params())
+    p, _ = _ExplainFn.apply(ex, args, imp.reshape(-1), *ex._gate_params())
+    p1, p2 = p[:G * B * N], p[G * B * N:]
     w1 = torch.from_numpy(rng.uniform(-1, 1, G * B * N).astype(np.float32))
     w2 = torch.from_numpy(rng.uniform(-1, 1, G * B * N * N).astype(np.float32))
     ((p1 * w1.to(dev)).sum() + (p2 * w2.to(dev)).sum()).backward()
@@ -140,8 +141,9 @@ def test_explain_backward_variants_match_autograd(dev, var):
     assert (masks[0] is None) == (not dep)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
     imp = t(imp_np).requires_grad_(True)
-    p1, p2 = _ExplainFn.apply(ex, (t(eid3), t(ts3), t(s1e), t(s2e), masks, G, B, W, N), imp.reshape(-1),
-                              *ex._gate_params())
+    p, _ = _ExplainFn.apply(ex, (t(eid3), t(ts3), t(s1e), t(s2e), masks, G, B, W, N), imp.reshape(-1),
+                            *ex._gate_params())
+    p1, p2 = p[:G * B * N], p[G * B * N:]
     w1 = torch.from_numpy(rng.uniform(-1, 1, G * B * N).astype(np.float32))
     w2 = torch.from_numpy(rng.uniform(-1, 1, G * B * N * N).astype(np.float32))
     ((p1 * w1.to(dev)).sum() + (p2 * w2.to(dev)).sum()).backward()
