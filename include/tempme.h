@@ -73,6 +73,15 @@ int tm_graph_info(const tm_graph *g, int32_t *n_nodes, int64_t *n_entries, int32
 /* host copy of node_idx_l / edge_idx_l / node_ts_l / off_set_l (utils/graph.py:23-27) and
  * per-entry nodeedge2idx[owner][eid] raw value (may be negative, see get_ts2idx). */
 int tm_graph_export(const tm_graph *g, int64_t *off, int32_t *ngh, int32_t *eid, double *ts, int32_t *dict_val);
+/* strict_temporal view (SURVEY §7/§8(b) opt-in; the reference has no such mode -- its NeighborFinder is
+ * parity mode, which every other entry point reproduces).  The view shares g's device buffers and
+ * differs in two lookups: an e_idx slice of node u is bisect_left(ts_u, t(e)) -- every record strictly
+ * earlier than the edge -- instead of get_ts2idx's trailing-tie value (utils/graph.py:77-101), and
+ * get_final_step's lookup of an edge u does not hold cuts at t(e) instead of taking u's whole list
+ * (graph.py:357/:366, a future leak).  Pass the view wherever a tm_graph is taken (tm_sample_khop,
+ * tm_sample_walks, tm_sample_events).  TM_E_UNSUPPORTED when an edge id carries more than one timestamp.
+ * Free the view (tm_graph_free) before g; export/info of a view report g's CSR. */
+int tm_graph_strict_view(const tm_graph *g, tm_graph **out);
 
 /* ---------------------------------------------------------------- sampling (device)
  * find_k_hop (utils/graph.py:233-262) + get_temporal_neighbor (:197-231) for B rows.

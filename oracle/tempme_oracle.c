@@ -65,6 +65,9 @@ typedef struct {
     double *ts;
     int64_t *doff;             /* per-node dict: [V+1] offsets into dkey/dval */
     int32_t *dkey, *dval;      /* sorted unique eids of the node, final dict value */
+    int strict;                /* strict_temporal: see or_graph_set_strict */
+    int32_t max_eid;
+    double *ets;               /* [max_eid+1] timestamp of each edge id (strict mode only) */
 } or_graph;
 
 typedef struct { double ts; int64_t ord; int32_t ngh, eid; } ent_t;
@@ -154,6 +157,7 @@ or_graph *or_graph_build(int32_t n_nodes, const int64_t *in_off, const int32_t *
 void or_graph_free(or_graph *g) {
     if (!g) return;
     free(g->off); free(g->ngh); free(g->eid); free(g->ts); free(g->doff); free(g->dkey); free(g->dval);
+    free(g->ets);
     free(g);
 }
 
@@ -162,6 +166,43 @@ void or_graph_export(const or_graph *g, int64_t *off, int32_t *ngh, int32_t *eid
     memcpy(ngh, g->ngh, sizeof(int32_t) * g->n_entries);
     memcpy(eid, g->eid, sizeof(int32_t) * g->n_entries);
     memcpy(ts, g->ts, sizeof(double) * g->n_entries);
+}
+
+static int64_t bisect_left(const double *a, int64_t n, double x) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        int64_t mid = (lo + hi) / 2;
+        if (a[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+/* strict_temporal mode (SURVEY §7 opt-in; not in the reference): the slice of node u's list before edge e
+ * is every record strictly earlier than e's own timestamp, bisect_left(ts_u, t(e)), instead of
+ * get_ts2idx's trailing-tie value (graph.py:77-101); and a get_final_step lookup of an edge the node does
+ * not hold (graph.py:357/:366 .get -> None -> the whole list, a future leak) is cut at t(e) too.
+ * Requires one timestamp per edge id; returns -1 otherwise (nothing changed). */
+int or_graph_set_strict(or_graph *g, int strict) {
+    if (!strict) { g->strict = 0; return 0; }
+    int32_t mx = 0;
+    for (int64_t i = 0; i < g->n_entries; ++i) if (g->eid[i] > mx) mx = g->eid[i];
+    double *ets = malloc(sizeof(double) * ((size_t)mx + 1));
+    char *seen = calloc((size_t)mx + 1, 1);
+    for (int64_t i = 0; i < g->n_entries; ++i) {
+        int32_t e = g->eid[i];
+        if (e < 0) continue;
+        if (seen[e] && ets[e] != g->ts[i]) { free(ets); free(seen); return -1; }
+        ets[e] = g->ts[i]; seen[e] = 1;
+    }
+    for (int32_t e = 0; e <= mx; ++e) if (!seen[e]) ets[e] = 0.0;
+    free(seen);
+    free(g->ets);
+    g->ets = ets; g->max_eid = mx; g->strict = 1;
+    return 0;
+}
+
+static double edge_ts(const or_graph *g, int32_t e) {
+    return (e >= 0 && e <= g->max_eid) ? g->ets[e] : 0.0;
 }
 
 /* raw nodeedge2idx[u][e]; *found = 0 for None */
@@ -177,20 +218,12 @@ int32_t or_dict_raw(const or_graph *g, int32_t u, int32_t e, int32_t *found) {
 int32_t or_lookup(const or_graph *g, int32_t u, int32_t e) {
     int32_t found, v = or_dict_raw(g, u, e, &found);
     if (!found) return -1;
+    if (g->strict) return (int32_t)bisect_left(g->ts + g->off[u], g->off[u + 1] - g->off[u], edge_ts(g, e));
     if (v < 0) {
         int64_t d = g->off[u + 1] - g->off[u] + v;
         v = d > 0 ? (int32_t)d : 0;
     }
     return v;
-}
-
-static int64_t bisect_left(const double *a, int64_t n, double x) {
-    int64_t lo = 0, hi = n;
-    while (lo < hi) {
-        int64_t mid = (lo + hi) / 2;
-        if (a[mid] < x) lo = mid + 1; else hi = mid;
-    }
-    return lo;
 }
 
 /* find_before (graph.py:103-146): returns cut length, or -1 (IndexError). */
@@ -251,6 +284,7 @@ int or_khop(const or_graph *g, or_rng rng, int32_t k, int32_t N, int32_t B, cons
 static int64_t final_cut(const or_graph *g, int32_t u, int32_t e) {
     if (!(u > 0)) return 0;
     int32_t p = or_lookup(g, u, e);
+    if (p < 0 && g->strict) return bisect_left(g->ts + g->off[u], g->off[u + 1] - g->off[u], edge_ts(g, e));
     return p < 0 ? (g->off[u + 1] - g->off[u]) : p;
 }
 

@@ -32,6 +32,7 @@ N_WEIGHTS = 28
 # every symbol include/tempme.h declares
 EXPORTS = (
     "tm_last_error", "tm_version", "tm_graph_build", "tm_graph_build_edges", "tm_graph_free", "tm_graph_info", "tm_graph_export",
+    "tm_graph_strict_view",
     "tm_sample_khop", "tm_sample_walks", "tm_neg_sample", "tm_perm_keys", "tm_motif_hist", "tm_edge_counts",
     "tm_sample_events", "tm_gather_rows", "tm_weights_create", "tm_weights_create_ex", "tm_weights_pack", "tm_weights_variant", "tm_weights_free",
     "tm_encoder_workspace_bytes",
@@ -114,6 +115,7 @@ def _sig(L):
     L.tm_graph_free.argtypes = [vp]
     L.tm_graph_info.argtypes = [vp, C.POINTER(i32), C.POINTER(i64), C.POINTER(i32)]
     L.tm_graph_export.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.tm_graph_strict_view.argtypes = [vp, C.POINTER(vp)]
     L.tm_sample_khop.argtypes = [vp, TmRng, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.tm_sample_walks.argtypes = [vp, TmRng, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.tm_neg_sample.argtypes = [TmRng, vp, i64, vp, i32, i32, vp, vp]

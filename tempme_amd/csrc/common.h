@@ -117,6 +117,8 @@ struct DevGraph {
     int32_t ts_unique;      // every record of an edge id carries the same timestamp
     const PairBlk *pblk;    // [pblk_mask+1] (node, neighbour) block table
     uint32_t pblk_mask;
+    int32_t strict;         // strict_temporal view (tm_graph_strict_view): ends hold bisect_left(ts_u, t(e)),
+                            // and final_step cuts an edge the node does not hold at t(e), not the whole list
 };
 
 // A uniform pointer moved into VGPRs: kernels with many pointer arguments otherwise overflow the
@@ -276,6 +278,8 @@ struct tm_graph {
     // until tm_graph_export asks for them
     int32_t *d_hngh, *d_heid, *d_dict;
     int dev_built;
+    // a strict_temporal view (tm_graph_strict_view) owns only d_ends; everything else is the parent's
+    const tm_graph *parent;
     // host copies (export)
     int64_t *h_off;
     int32_t *h_ngh, *h_eid, *h_dict;

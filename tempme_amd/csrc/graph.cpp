@@ -522,6 +522,7 @@ extern "C" int tm_graph_info(const tm_graph *g, int32_t *n_nodes, int64_t *n_ent
 extern "C" int tm_graph_export(const tm_graph *gc, int64_t *off, int32_t *ngh, int32_t *eid, double *ts,
                                int32_t *dict_val) {
     if (!gc) return fail(TM_E_ARG, "tm_graph_export: NULL graph");
+    if (gc->parent) return tm_graph_export(gc->parent, off, ngh, eid, ts, dict_val);
     tm_graph *g = const_cast<tm_graph *>(gc);
     const int64_t n = g->d.n_entries;
     if (g->dev_built) {   // host copies of a device-built graph, made once (the first export publishes them)

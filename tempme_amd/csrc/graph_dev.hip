@@ -100,6 +100,17 @@ __global__ void k_fill_ends(int64_t n, EdgeEnds *ends) {
     GS_LOOP(i, n) ends[i] = EdgeEnds{-1, 0, -1, 0};
 }
 
+// strict_temporal slice lengths: every record of the owner strictly earlier than the edge's own time
+__global__ void k_strict_ends(int64_t n, DevGraph g, EdgeEnds *ends) {
+    GS_LOOP(i, n) {
+        EdgeEnds x = g.ends[i];
+        const double t = g.ets[i];
+        if (x.node_a >= 0) x.len_a = bisect_ts(g, x.node_a, t);
+        if (x.node_b >= 0) x.len_b = bisect_ts(g, x.node_b, t);
+        ends[i] = x;
+    }
+}
+
 __global__ void k_fill_i32(int64_t n, int32_t *a, int32_t v) {
     GS_LOOP(i, n) a[i] = v;
 }
@@ -421,5 +432,43 @@ int tm_graph_build_edges_device(int32_t V, int64_t n_edges, const int64_t *src, 
         return rc;
     }
     *out = g;
+    return TM_OK;
+}
+
+// A strict_temporal view of g (SURVEY §7 opt-in; the reference has no such mode): the same device CSR,
+// timestamps, block trees and pair table, with its own e_idx -> slice-length table holding
+// bisect_left(ts_u, t(e)) instead of get_ts2idx's trailing-tie values (utils/graph.py:77-101), and the
+// strict flag that makes get_final_step cut a None lookup at t(e2) (graph.py:357/:366).  The view shares
+// the parent's buffers: free it (tm_graph_free) before the parent.
+extern "C" int tm_graph_strict_view(const tm_graph *g, tm_graph **out) {
+    using namespace tmk;
+    using namespace tmk::gdev;
+    if (!g || !out) return fail(TM_E_ARG, "tm_graph_strict_view: bad arguments");
+    *out = nullptr;
+    if (g->parent) g = g->parent;
+    if (!g->d.ts_unique)
+        return fail(TM_E_UNSUPPORTED, "tm_graph_strict_view: an edge id carries more than one timestamp");
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess) prev = 0;
+    hipError_t e = hipSetDevice(g->device);
+    tm_graph *v = new tm_graph();
+    v->device = g->device;
+    v->parent = g;
+    const int64_t n = (int64_t)g->d.max_eid + 1;
+    e = e ? e : hipMalloc(&v->d_ends, sizeof(EdgeEnds) * n);
+    if (e == hipSuccess) {
+        k_strict_ends<<<grid(n), TB, 0, 0>>>(n, g->d, v->d_ends);
+        e = hipGetLastError();
+    }
+    e = e ? e : hipDeviceSynchronize();
+    (void)hipSetDevice(prev);
+    if (e != hipSuccess) {
+        tm_graph_free(v);
+        return fail(TM_E_HIP, std::string("tm_graph_strict_view: ") + hipGetErrorString(e));
+    }
+    v->d = g->d;
+    v->d.ends = v->d_ends;
+    v->d.strict = 1;
+    *out = v;
     return TM_OK;
 }

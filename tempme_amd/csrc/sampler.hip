@@ -214,8 +214,13 @@ __device__ Step3 final_step(const DevGraph &g, Key key, uint32_t ev, uint32_t w,
     const EdgeEnds x2 = (e2 >= 0 && e2 <= g.max_eid) ? g.ends[e2] : EdgeEnds{-1, 0, -1, 0};
     const int2 oa = va ? g.span[a_node] : make_int2(0, 0), ob = vb ? g.span[b_node] : make_int2(0, 0);
     const int32_t oa0 = oa.x, oa1 = oa.y, ob0 = ob.x, ob1 = ob.y;
-    const int32_t ca = !va ? 0 : x2.node_a == a_node ? x2.len_a : x2.node_b == a_node ? x2.len_b : oa1 - oa0;
-    const int32_t cb = !vb ? 0 : x2.node_a == b_node ? x2.len_a : x2.node_b == b_node ? x2.len_b : ob1 - ob0;
+    int32_t ca = !va ? 0 : x2.node_a == a_node ? x2.len_a : x2.node_b == a_node ? x2.len_b : oa1 - oa0;
+    int32_t cb = !vb ? 0 : x2.node_a == b_node ? x2.len_a : x2.node_b == b_node ? x2.len_b : ob1 - ob0;
+    if (g.strict) {   // strict_temporal: the None lookup cuts at e2's own time instead of leaking the future
+        const double t2 = (e2 >= 0 && e2 <= g.max_eid) ? g.ets[e2] : 0.0;
+        if (va && x2.node_a != a_node && x2.node_b != a_node) ca = bisect_ts(g, a_node, t2);
+        if (vb && x2.node_a != b_node && x2.node_b != b_node) cb = bisect_ts(g, b_node, t2);
+    }
     int32_t na, nb, k1 = 0, n1 = 0, k2 = 0, n2 = 0, kb = 0;
     if (filt) {
         // filtered counts: the (node, neighbour) block of each of the three neighbours from the block

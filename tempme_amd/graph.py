@@ -99,6 +99,11 @@ class DeviceGraph:
         m = self.n_entries
         return off, ngh[:m], eid[:m], ts[:m], dv[:m]
 
+    def strict_view(self):
+        """strict_temporal view (tm_graph_strict_view): the same device CSR with slice lengths
+        bisect_left(ts_u, t(e)) and no get_final_step future leak (SURVEY §7 opt-in)."""
+        return _StrictGraph(self)
+
     def __del__(self):
         h = getattr(self, "handle", None)
         if h is not None and L._lib is not None:
@@ -106,9 +111,25 @@ class DeviceGraph:
             self.handle = None
 
 
+class _StrictGraph(DeviceGraph):
+    """A ``tm_graph`` view sharing ``parent``'s buffers (held here, so the view is freed first)."""
+
+    def __init__(self, parent):
+        self.parent = parent
+        self.device = parent.device
+        self.n_nodes, self.n_entries, self.max_eid = parent.n_nodes, parent.n_entries, parent.max_eid
+        h = C.c_void_p()
+        L.check(L.lib().tm_graph_strict_view(parent.handle, C.byref(h)), "tm_graph_strict_view")
+        self.handle = h
+
+
 class NeighborFinder:
     def __init__(self, adj_list, bias=0, ts_precision=PRECISION, use_cache=False, sample_method="multinomial",
-                 device=None, *, seed=0, split=L.SPLIT_TEST, _flat=None, _edges=None):
+                 device=None, *, seed=0, split=L.SPLIT_TEST, strict_temporal=False, _flat=None, _edges=None):
+        """graph.py:13-27.  strict_temporal=True (not in the reference, off by default) fixes two of its
+        temporal quirks: an e_idx slice keeps exactly the records strictly earlier than the edge (no
+        trailing-tie get_ts2idx value, graph.py:77-101), and get_final_step's None lookup cuts at the
+        edge's time instead of taking the whole list (graph.py:357/:366)."""
         if not math.isclose(bias, 0) or sample_method != "multinomial":
             # graph.py:219-227 (bias != 0, 'binary') are unreachable from every reference caller
             raise NotImplementedError("only bias=0, sample_method='multinomial' (the reference's only live path)")
@@ -124,6 +145,9 @@ class NeighborFinder:
         else:
             off, ngh, eid, ts = _flat if _flat is not None else _flatten_adj(adj_list)
             self.graph = DeviceGraph(off, ngh, eid, ts, device)
+        self.strict_temporal = bool(strict_temporal)
+        if self.strict_temporal:
+            self.graph = self.graph.strict_view()
         self.device = self.graph.device
         self._host = None
         self._ne2i = None
@@ -172,6 +196,8 @@ class NeighborFinder:
             cut = self.nodeedge2idx[src_idx].get(e_idx) if src_idx > 0 else 0
             if cut is None:
                 raise IndexError("e_idx {} not found in edge list of {}".format(e_idx, src_idx))
+            if self.strict_temporal and src_idx > 0:
+                cut = int(np.searchsorted(n_t, n_t[n_e == e_idx][0], side="left"))
         if return_binary_prob:
             raise NotImplementedError("binary_prob is only used by the dead 'binary' sample method")
         return n_i[:cut], n_e[:cut], n_t[:cut], None

@@ -594,3 +594,40 @@ def test_constructor_shapes_on_hip(tm, hid, if_cat, tg):
         np.testing.assert_allclose(expl[0][k * B:(k + 1) * B].cpu().numpy(), r0.numpy(), rtol=RTOL, atol=ATOL)
         np.testing.assert_allclose(expl[1][k * B:(k + 1) * B].cpu().numpy(), r1.numpy(), rtol=RTOL, atol=ATOL)
     assert ex._packed is not None, "the HIP encoder did not run"
+
+
+def test_strict_temporal_view_vs_oracle(tm):
+    """strict_temporal (tm_graph_strict_view, SURVEY §7 opt-in): the fused sampler on the strict view vs the
+    C oracle in strict mode, bit-exact, on uslegis's late events (long lists, many ties); the parity-mode
+    graph it views is unchanged, and the host find_before of a strict finder agrees."""
+    from tempme_amd.preprocess import sample_events
+    df = pd.read_csv(os.path.join(G, "data", "ml_uslegis_sampled.csv"))
+    src, dst, eidx, ts = df.u.values, df.i.values, df.idx.values, df.ts.values
+    f = tm.NeighborFinder.from_edges(src, dst, eidx, ts, 224, strict_temporal=True)
+    fp = _finder(tm, src, dst, eidx, ts, 224)
+    rows = np.arange(len(src) - 64, len(src))
+    pool = np.unique(dst)
+    og = orc.OracleGraph(src, dst, eidx, ts, 224, strict_temporal=True)
+    dev = f.device
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a[rows], dtype=dt)).to(dev)  # noqa: E731
+    h = lambda x: x.cpu().numpy()  # noqa: E731
+    for N, M in ((20, 3), (8, 1)):
+        o = orc.event_pipeline(og, 0, px.SPLIT_TEST, N, M, src[rows], dst[rows], ts[rows], eidx[rows],
+                               np.arange(len(rows)), pool, 8)
+        outs = []
+        for g in (f.graph, fp.graph):
+            outs.append(sample_events(g, 0, px.SPLIT_TEST, N, M, t(src, np.int32), t(dst, np.int32),
+                                      t(ts, np.float64), t(eidx, np.int32),
+                                      torch.arange(len(rows), dtype=torch.int32, device=dev),
+                                      torch.from_numpy(pool.astype(np.int32)).to(dev)))
+        b, bp = outs
+        for name in ("node6", "eid3", "ts3", "cat", "sub1_node", "sub1_eid", "sub1_ts", "sub2_node", "sub2_eid",
+                     "sub2_ts"):
+            assert np.array_equal(h(getattr(b, name)).swapaxes(0, 1), o[name]), name
+        assert np.array_equal(h(b.cnt).swapaxes(0, 1).astype(np.int32), o["cnt"])
+        assert not torch.equal(b.eid3, bp.eid3)        # the view changed the walks, not the parent graph
+    ref = orc.event_pipeline(orc.OracleGraph(src, dst, eidx, ts, 224), 0, px.SPLIT_TEST, 8, 1, src[rows],
+                             dst[rows], ts[rows], eidx[rows], np.arange(len(rows)), pool, 8)
+    assert np.array_equal(h(bp.eid3).swapaxes(0, 1), ref["eid3"])
+    for u, e in ((int(src[-1]), int(eidx[-1])), (int(dst[-5]), int(eidx[-5]))):
+        assert len(f.find_before(u, 0.0, e_idx=e)[0]) == og.find_before(u, 0.0, e)
