@@ -26,6 +26,7 @@
 // mixing, LayerNorm statistics and the masked means are VALU / wave reductions.  The output layer and
 // the MergeLayer score are plain [rows x 2C] GEMMs left to the library (tempme_amd/graphmixer.py).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -923,10 +924,10 @@ __device__ __forceinline__ void gmb_tok_fwd(int N, int HT, const GmTokW &tw, con
     }
 }
 
-// sum over c < C of the LDS image V[t][c], one wave per token, added to out[t]
-__device__ __forceinline__ void gmb_token_sums(const float *V, int XP, int N, int C, float *out) {
+// sum over c < C of the LDS image V[t][c], one wave per token (nw waves), added to out[t]
+__device__ __forceinline__ void gmb_token_sums(const float *V, int XP, int N, int C, int nw, float *out) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int t = wave; t < N; t += 4) {
+    for (int t = wave; t < N; t += nw) {
         float s = 0.f;
         for (int c = lane; c < C; c += 64) s += V[gm_idx(t, c, XP)];
         s = gm_wsum(s);
@@ -934,10 +935,15 @@ __device__ __forceinline__ void gmb_token_sums(const float *V, int XP, int N, in
     }
 }
 
-template <int NMT, int NTW>
-__global__ void __launch_bounds__(256) gm_bwd_kernel(GmArgs a, GmBwd b) {
+// TS8 with NMT == 2 (N > 16): 8 waves, wave = 4 mh + wq runs token tile mh of output tiles wq + 4i in every
+// GEMM (the workgroup's 147 KB of LDS allows one per CU: 8 waves give each SIMD two); otherwise 4 waves.
+template <int NMT, int NTW, bool TS8>
+__global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmArgs a, GmBwd b) {
     extern __shared__ float gm_lds[];
+    constexpr bool TS = NMT == 2 && TS8;
+    constexpr int NWV = TS ? 8 : 4, GMT = TS ? 1 : NMT;
     const int r = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int wq = TS ? (wave & 3) : wave, mh = TS ? (wave >> 2) : 0;
     const int N = a.N, C = a.C, T = a.T, D = a.D, L = a.L, HT = a.HT;
     const int C16 = gm_r16(C), KG = gm_r16(C + T) / 16, KH = (KG + 1) / 2;
     const int XP = C16 + 4, HP = GM_HCH + 4, K0P = 16 * KH + 4, IMG = GM_MT * XP;
@@ -953,7 +959,7 @@ __global__ void __launch_bounds__(256) gm_bwd_kernel(GmArgs a, GmBwd b) {
         dsew[tid] = 0.f;
     }
     __syncthreads();
-    const int NT = C16 / 16, ntw = (NT - wave + 3) / 4;
+    const int NT = C16 / 16, ntw = (NT - wq + 3) / 4;
     const int NH = gm_r16(a.HC) / 16;
     float mr[2] = {0.f, 0.f}, rr[2] = {0.f, 0.f};
     // ---- forward: projection (as gm_embed_kernel)
@@ -982,21 +988,22 @@ __global__ void __launch_bounds__(256) gm_bwd_kernel(GmArgs a, GmBwd b) {
             gmx4 acc[NTW][2];
 #pragma unroll
             for (int i = 0; i < NTW; ++i) acc[i][0] = acc[i][1] = gmx4{0.f, 0.f, 0.f, 0.f};
-            gm_gemm_mt<NMT, NTW, false>(X0, K0P, G0, a.proj_w, NT, wave, ntw, G0, nG, acc, nullptr, nullptr, mr, rr);
+            gm_gemm_mt<GMT, NTW, false>(X0 + 16 * mh * K0P, K0P, G0, a.proj_w, NT, wq, ntw, G0, nG, acc, nullptr, nullptr,
+                                        mr, rr);
 #pragma unroll
             for (int i = 0; i < NTW; ++i) {
                 if (i >= ntw) break;
-                const int n = 16 * (wave + 4 * i) + (lane & 15);
+                const int n = 16 * (wq + 4 * i) + (lane & 15);
                 const float bv = n < C ? a.proj_b[n] : 0.f;
 #pragma unroll
-                for (int mt = 0; mt < 2; ++mt)
+                for (int q = 0; q < GMT; ++q)
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        const int t = 16 * mt + 4 * (lane >> 4) + e;
+                        const int mt = mh + q, t = 16 * mt + 4 * (lane >> 4) + e;
                         const int ix = gm_idx(t, n, XP);
                         const bool in = mt < NMT && n < C && t < N;
-                        if (h == 0) X[ix] = in ? acc[i][mt][e] : 0.f;
-                        else if (in) X[ix] = X[ix] + acc[i][mt][e] + bv;
+                        if (h == 0) X[ix] = in ? acc[i][q][e] : 0.f;
+                        else if (in) X[ix] = X[ix] + acc[i][q][e] + bv;
                     }
             }
         }
@@ -1046,7 +1053,7 @@ __global__ void __launch_bounds__(256) gm_bwd_kernel(GmArgs a, GmBwd b) {
     };
     // channel LayerNorm statistics of image S (one wave per token) into tmean / trstd, then this lane's rows
     auto chan_stats = [&](const float *S) {
-        for (int t = wave; t < GM_MT; t += 4) {
+        for (int t = wave; t < GM_MT; t += NWV) {
             float mean = 0.f, rstd = 0.f;
             if (t < N) {
                 float s = 0.f, q = 0.f;
@@ -1065,9 +1072,9 @@ __global__ void __launch_bounds__(256) gm_bwd_kernel(GmArgs a, GmBwd b) {
         }
         __syncthreads();
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-            mr[mt] = tmean[16 * mt + (lane & 15)];
-            rr[mt] = trstd[16 * mt + (lane & 15)];
+        for (int q = 0; q < GMT; ++q) {
+            mr[q] = tmean[16 * (mh + q) + (lane & 15)];
+            rr[q] = trstd[16 * (mh + q) + (lane & 15)];
         }
     };
     // ---- forward through the mixers, keeping each layer's input
@@ -1084,42 +1091,43 @@ __global__ void __launch_bounds__(256) gm_bwd_kernel(GmArgs a, GmBwd b) {
 #pragma unroll
         for (int i = 0; i < NTW; ++i) acc2[i][0] = acc2[i][1] = gmx4{0.f, 0.f, 0.f, 0.f};
         for (int h0 = 0; h0 < NH; h0 += GM_HCH / 16) {
-            const int nh = min(GM_HCH / 16, NH - h0), nw1 = (nh - wave + 3) / 4;
+            const int nh = min(GM_HCH / 16, NH - h0), nw1 = (nh - wq + 3) / 4;
             gmx4 acc[GM_HCH / 64][2];
 #pragma unroll
             for (int i = 0; i < GM_HCH / 64; ++i) acc[i][0] = acc[i][1] = gmx4{0.f, 0.f, 0.f, 0.f};
-            gm_gemm_mt<NMT, GM_HCH / 64, true>(X, XP, 0, W1, NH, h0 + wave, nw1, 0, C16 / 16, acc, lnw, lnb, mr, rr);
+            gm_gemm_mt<GMT, GM_HCH / 64, true>(X + 16 * mh * XP, XP, 0, W1, NH, h0 + wq, nw1, 0, C16 / 16, acc, lnw, lnb,
+                                               mr, rr);
 #pragma unroll
             for (int i = 0; i < GM_HCH / 64; ++i) {
                 if (i >= nw1) break;
-                const int ht = wave + 4 * i, n = 16 * (h0 + ht) + (lane & 15);
+                const int ht = wq + 4 * i, n = 16 * (h0 + ht) + (lane & 15);
                 const float bv = n < a.HC ? w[9][n] : 0.f;
 #pragma unroll
-                for (int mt = 0; mt < 2; ++mt)
+                for (int q = 0; q < GMT; ++q)
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        const int t = 16 * mt + 4 * (lane >> 4) + e;
-                        H[gm_idx(t, 16 * ht + (lane & 15), HP)] = (mt < NMT && n < a.HC) ? gm_gelu(acc[i][mt][e] + bv) : 0.f;
+                        const int mt = mh + q, t = 16 * mt + 4 * (lane >> 4) + e;
+                        H[gm_idx(t, 16 * ht + (lane & 15), HP)] = (mt < NMT && n < a.HC) ? gm_gelu(acc[i][q][e] + bv) : 0.f;
                     }
             }
             __syncthreads();
-            gm_gemm_mt<NMT, NTW, false>(H, HP, h0, W2, NT, wave, ntw, h0, nh, acc2, nullptr, nullptr, mr, rr);
+            gm_gemm_mt<GMT, NTW, false>(H + 16 * mh * HP, HP, h0, W2, NT, wq, ntw, h0, nh, acc2, nullptr, nullptr, mr, rr);
             __syncthreads();
         }
 #pragma unroll
         for (int i = 0; i < NTW; ++i) {
-            const int nt = wave + 4 * i;
+            const int nt = wq + 4 * i;
             if (nt >= NT) break;
             const int n = 16 * nt + (lane & 15);
             const float bv = n < C ? w[11][n] : 0.f;
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
+            for (int q = 0; q < GMT; ++q)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const int t = 16 * mt + 4 * (lane >> 4) + e;
+                    const int mt = mh + q, t = 16 * mt + 4 * (lane >> 4) + e;
                     if (mt < NMT && t < N && n < C) {
                         const int ix = gm_idx(t, n, XP);
-                        X[ix] = (acc2[i][mt][e] + bv) * sew[t] + X[ix];
+                        X[ix] = (acc2[i][q][e] + bv) * sew[t] + X[ix];
                     }
                 }
         }
@@ -1139,10 +1147,10 @@ __global__ void __launch_bounds__(256) gm_bwd_kernel(GmArgs a, GmBwd b) {
         G[ix] = in ? g * sval[t] * sew[t] / (float)N : 0.f;
     }
     __syncthreads();
-    gmb_token_sums(DY, XP, N, C, dsew);
+    gmb_token_sums(DY, XP, N, C, NWV, dsew);
     {   // node_out: d sew_t += sum_d dno_d n_feat[nid_t][d] sc_t / N, one wave per token
         const float *dno = b.d_no + (size_t)r * D;
-        for (int t = wave; t < N; t += 4) {
+        for (int t = wave; t < N; t += NWV) {
             const float sc = nvalid > 0.f ? sval[t] / nvalid : 1.f / (float)N;
             const float *nf = a.n_feat + (size_t)a.nid[(size_t)r * N + t] * D;
             float s = 0.f;
@@ -1176,86 +1184,88 @@ __global__ void __launch_bounds__(256) gm_bwd_kernel(GmArgs a, GmBwd b) {
 #pragma unroll
         for (int i = 0; i < NTW; ++i) acc2[i][0] = acc2[i][1] = accv[i][0] = accv[i][1] = gmx4{0.f, 0.f, 0.f, 0.f};
         for (int h0 = 0; h0 < NH; h0 += GM_HCH / 16) {
-            const int nh = min(GM_HCH / 16, NH - h0), nw1 = (nh - wave + 3) / 4;
+            const int nh = min(GM_HCH / 16, NH - h0), nw1 = (nh - wq + 3) / 4;
             gmx4 acc[GM_HCH / 64][2], accd[GM_HCH / 64][2];
 #pragma unroll
             for (int i = 0; i < GM_HCH / 64; ++i)
                 acc[i][0] = acc[i][1] = accd[i][0] = accd[i][1] = gmx4{0.f, 0.f, 0.f, 0.f};
-            gm_gemm_mt<NMT, GM_HCH / 64, true>(O1, XP, 0, W1, NH, h0 + wave, nw1, 0, C16 / 16, acc, lnw, lnb, mr, rr);
-            gm_gemm_mt<NMT, GM_HCH / 64, false>(DY, XP, 0, W2T, NH, h0 + wave, nw1, 0, C16 / 16, accd, nullptr, nullptr,
-                                                mr, rr);
+            gm_gemm_mt<GMT, GM_HCH / 64, true>(O1 + 16 * mh * XP, XP, 0, W1, NH, h0 + wq, nw1, 0, C16 / 16, acc, lnw, lnb,
+                                               mr, rr);
+            gm_gemm_mt<GMT, GM_HCH / 64, false>(DY + 16 * mh * XP, XP, 0, W2T, NH, h0 + wq, nw1, 0, C16 / 16, accd,
+                                                nullptr, nullptr, mr, rr);
             // H = gelu(Z2) for Y_ch; dZ2 = dG2 gelu'(Z2) kept in accd for the second pass through U
 #pragma unroll
             for (int i = 0; i < GM_HCH / 64; ++i) {
                 if (i >= nw1) break;
-                const int ht = wave + 4 * i, n = 16 * (h0 + ht) + (lane & 15);
+                const int ht = wq + 4 * i, n = 16 * (h0 + ht) + (lane & 15);
                 const float bv = n < a.HC ? w[9][n] : 0.f;
 #pragma unroll
-                for (int mt = 0; mt < 2; ++mt)
+                for (int q = 0; q < GMT; ++q)
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        const int t = 16 * mt + 4 * (lane >> 4) + e;
+                        const int mt = mh + q, t = 16 * mt + 4 * (lane >> 4) + e;
                         const bool in = mt < NMT && n < a.HC;
-                        const float z = acc[i][mt][e] + bv;
+                        const float z = acc[i][q][e] + bv;
                         H[gm_idx(t, 16 * ht + (lane & 15), HP)] = in ? gm_gelu(z) : 0.f;
-                        accd[i][mt][e] = in ? accd[i][mt][e] * gm_gelu_d(z) : 0.f;
+                        accd[i][q][e] = in ? accd[i][q][e] * gm_gelu_d(z) : 0.f;
                     }
             }
             __syncthreads();
-            gm_gemm_mt<NMT, NTW, false>(H, HP, h0, W2, NT, wave, ntw, h0, nh, acc2, nullptr, nullptr, mr, rr);
+            gm_gemm_mt<GMT, NTW, false>(H + 16 * mh * HP, HP, h0, W2, NT, wq, ntw, h0, nh, acc2, nullptr, nullptr, mr, rr);
             __syncthreads();
 #pragma unroll
             for (int i = 0; i < GM_HCH / 64; ++i) {
                 if (i >= nw1) break;
-                const int ht = wave + 4 * i;
+                const int ht = wq + 4 * i;
 #pragma unroll
-                for (int mt = 0; mt < 2; ++mt)
+                for (int q = 0; q < GMT; ++q)
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        const int t = 16 * mt + 4 * (lane >> 4) + e;
-                        H[gm_idx(t, 16 * ht + (lane & 15), HP)] = accd[i][mt][e];
+                        const int t = 16 * (mh + q) + 4 * (lane >> 4) + e;
+                        H[gm_idx(t, 16 * ht + (lane & 15), HP)] = accd[i][q][e];
                     }
             }
             __syncthreads();
-            gm_gemm_mt<NMT, NTW, false>(H, HP, h0, W1T, NT, wave, ntw, h0, nh, accv, nullptr, nullptr, mr, rr);
+            gm_gemm_mt<GMT, NTW, false>(H + 16 * mh * HP, HP, h0, W1T, NT, wq, ntw, h0, nh, accv, nullptr, nullptr, mr,
+                                        rr);
             __syncthreads();
         }
         // d sew_t += sum_c G (Y_ch + b2)
 #pragma unroll
         for (int i = 0; i < NTW; ++i) {
-            const int nt = wave + 4 * i;
+            const int nt = wq + 4 * i;
             if (nt >= NT) break;
             const int n = 16 * nt + (lane & 15);
             const float bv = n < C ? w[11][n] : 0.f;
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
+            for (int q = 0; q < GMT; ++q)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const int t = 16 * mt + 4 * (lane >> 4) + e;
+                    const int mt = mh + q, t = 16 * mt + 4 * (lane >> 4) + e;
                     const int ix = gm_idx(t, n, XP);
-                    DY[ix] = (mt < NMT && t < N && n < C) ? G[ix] * (acc2[i][mt][e] + bv) : 0.f;
+                    DY[ix] = (mt < NMT && t < N && n < C) ? G[ix] * (acc2[i][q][e] + bv) : 0.f;
                 }
         }
         __syncthreads();
-        gmb_token_sums(DY, XP, N, C, dsew);
+        gmb_token_sums(DY, XP, N, C, NWV, dsew);
         __syncthreads();
         // channel LayerNorm backward: DY = dV * ln weight; G += rstd (DY - mean_c DY - xhat mean_c(DY xhat))
 #pragma unroll
         for (int i = 0; i < NTW; ++i) {
-            const int nt = wave + 4 * i;
+            const int nt = wq + 4 * i;
             if (nt >= NT) break;
             const int n = 16 * nt + (lane & 15);
             const float gw = n < C ? w[6][n] : 0.f;
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
+            for (int q = 0; q < GMT; ++q)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const int t = 16 * mt + 4 * (lane >> 4) + e;
-                    DY[gm_idx(t, n, XP)] = (mt < NMT && t < N && n < C) ? accv[i][mt][e] * gw : 0.f;
+                    const int mt = mh + q, t = 16 * mt + 4 * (lane >> 4) + e;
+                    DY[gm_idx(t, n, XP)] = (mt < NMT && t < N && n < C) ? accv[i][q][e] * gw : 0.f;
                 }
         }
         __syncthreads();
-        for (int t = wave; t < N; t += 4) {
+        for (int t = wave; t < N; t += NWV) {
             const float mean = tmean[t], rstd = trstd[t];
             float s1 = 0.f, s2 = 0.f;
             for (int c = lane; c < C; c += 64) {
@@ -1320,7 +1330,7 @@ __global__ void __launch_bounds__(256) gm_bwd_kernel(GmArgs a, GmBwd b) {
             }
         }
         __syncthreads();
-        gmb_token_sums(DY, XP, N, C, dsew);
+        gmb_token_sums(DY, XP, N, C, NWV, dsew);
         __syncthreads();
     }
     if (tid < N) b.d_ew[(size_t)r * N + tid] = dsew[tid] * sval[tid];
@@ -1472,14 +1482,16 @@ extern "C" int tm_gm_embed_bwd(const tm_gm_embed_args *p, const float *d_x_mean,
     GmBwd b{d_x_mean, d_node_out, d_ew, q.layer_table};
     hipEvent_t pe = prof_begin((hipStream_t)stream);
     const bool t3 = gm_r16(q.C) / 16 <= 12;
-    auto launch = [&](auto kern) -> int {
+    static const bool four = getenv("TEMPME_GM_BWD4") != nullptr;   // A/B: the round-3 four-wave form
+    auto launch = [&](auto kern, int threads) -> int {
         TM_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        kern<<<q.R, 256, lds, (hipStream_t)stream>>>(a, b);
+        kern<<<q.R, threads, lds, (hipStream_t)stream>>>(a, b);
         return TM_OK;
     };
     int rc;
-    if (q.N > 16) rc = t3 ? launch(gm_bwd_kernel<2, 3>) : launch(gm_bwd_kernel<2, 4>);
-    else rc = t3 ? launch(gm_bwd_kernel<1, 3>) : launch(gm_bwd_kernel<1, 4>);
+    if (q.N > 16 && !four) rc = t3 ? launch(gm_bwd_kernel<2, 3, true>, 512) : launch(gm_bwd_kernel<2, 4, true>, 512);
+    else if (q.N > 16) rc = t3 ? launch(gm_bwd_kernel<2, 3, false>, 256) : launch(gm_bwd_kernel<2, 4, false>, 256);
+    else rc = t3 ? launch(gm_bwd_kernel<1, 3, false>, 256) : launch(gm_bwd_kernel<1, 4, false>, 256);
     if (rc != TM_OK) return rc;
     TM_CHECK_LAUNCH();
     prof_end("gm_bwd_kernel", (hipStream_t)stream, pe);
