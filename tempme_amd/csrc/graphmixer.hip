@@ -557,7 +557,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 
     }
     __syncthreads();
     // ---- projection (:156-167): X = [E(e) | cos(dt w + b)] Wp^T + bp over K tiles padded to a multiple
-    // of 4 (zero fragments); B fragment of K tile q: edge features from the image, time features computed
+    // of 2 (zero fragments); B fragment of K tile q: edge features from the image, time features computed
     {
         const Ids I;
         const int m = I.m, j = I.j, vo = I.lane * 16;
@@ -565,7 +565,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 
         const size_t rowN = (size_t)rr * N;
         const bool tv = I.tok < N && a.nid[rowN + tokc] != 0;
         const float dt = (float)(a.cut[rr] - a.ts[rowN + tokc]);
-        const int KP = ((C + T + 63) / 64) * 4;
+        // K tiles per loop iteration (and the pack's multiple): the GF_PF-deep ring must stay within the
+        // next iteration's QG * NC fragments
+        constexpr int QG = NC >= 2 ? 2 : 4;
+        const int KP = ((C + T + 16 * QG - 1) / (16 * QG)) * QG;
         const auto wr = gf_rsrc(a.proj_w);
         const auto rtw = gf_vrsrc(a.time_w, T), rtb = gf_vrsrc(a.time_b, T), rb = gf_vrsrc(a.proj_b, C);
         gmx4 y[NC];
@@ -578,13 +581,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 
         float4 ring[GF_PF];
 #pragma unroll
         for (int i = 0; i < GF_PF; ++i) ring[i] = gf_frag(wr, vo, ((i % NC) * KP + i / NC) * 1024);
-        for (int q0 = 0; q0 < KP; q0 += 4) {
+        for (int q0 = 0; q0 < KP; q0 += QG) {
             // iteration bases opaque per iteration: loop strength reduction would otherwise keep every
             // fragment's offset as its own SGPR induction variable
-            int qb = q0 * 1024, qn = min(q0 + 4, KP - 4) * 1024;
+            int qb = q0 * 1024, qn = min(q0 + QG, KP - QG) * 1024;
             asm volatile("" : "+s"(qb), "+s"(qn));
 #pragma unroll
-            for (int dq = 0; dq < 4; ++dq) {
+            for (int dq = 0; dq < QG; ++dq) {
                 const int k0 = 16 * (q0 + dq) + 4 * j;
                 float4 bx;
                 if (k0 < C) {
@@ -604,9 +607,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 
                 for (int o = 0; o < NC; ++o) {
                     const int f = dq * NC + o, fn = f + GF_PF;   // this fragment, the one issued into its slot
                     const float4 w = ring[f % GF_PF];
-                    const int dn = fn / NC, on = fn % NC;        // K tile q0 + dn (dn < 4) or the next iteration's
-                    ring[f % GF_PF] = dn < 4 ? gf_frag(wr, vo, qb + (on * KP + dn) * 1024)
-                                             : gf_frag(wr, vo, qn + (on * KP + dn - 4) * 1024);
+                    const int dn = fn / NC, on = fn % NC;        // K tile q0 + dn (dn < QG) or the next iteration's
+                    ring[f % GF_PF] = dn < QG ? gf_frag(wr, vo, qb + (on * KP + dn) * 1024)
+                                              : gf_frag(wr, vo, qn + (on * KP + dn - QG) * 1024);
                     y[o] = gf_mfma4(w, bx, y[o]);
                 }
             }
@@ -924,10 +927,17 @@ __device__ __forceinline__ void gmb_tok_fwd(int N, int HT, const GmTokW &tw, con
     }
 }
 
+// phase ablation of gm_bwd_kernel for timing builds only (wrong results): bit 1 skips the per-channel token
+// mixing (forward, recompute and backward), bit 2 the channel-FFN GEMMs, bit 4 the projection GEMM, bit 8 the
+// LayerNorm statistics / backward and per-token sums
+#ifndef TM_GMB_ABL
+#define TM_GMB_ABL 0
+#endif
+
 // sum over c < C of the LDS image V[t][c], one wave per token (nw waves), added to out[t]
 __device__ __forceinline__ void gmb_token_sums(const float *V, int XP, int N, int C, int nw, float *out) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int t = wave; t < N; t += nw) {
+    for (int t = wave; t < N && !(TM_GMB_ABL & 8); t += nw) {
         float s = 0.f;
         for (int c = lane; c < C; c += 64) s += V[gm_idx(t, c, XP)];
         s = gm_wsum(s);
@@ -988,8 +998,9 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
             gmx4 acc[NTW][2];
 #pragma unroll
             for (int i = 0; i < NTW; ++i) acc[i][0] = acc[i][1] = gmx4{0.f, 0.f, 0.f, 0.f};
-            gm_gemm_mt<GMT, NTW, false>(X0 + 16 * mh * K0P, K0P, G0, a.proj_w, NT, wq, ntw, G0, nG, acc, nullptr, nullptr,
-                                        mr, rr);
+            if (!(TM_GMB_ABL & 4))
+                gm_gemm_mt<GMT, NTW, false>(X0 + 16 * mh * K0P, K0P, G0, a.proj_w, NT, wq, ntw, G0, nG, acc, nullptr,
+                                            nullptr, mr, rr);
 #pragma unroll
             for (int i = 0; i < NTW; ++i) {
                 if (i >= ntw) break;
@@ -1041,6 +1052,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
     };
     // token mixing of one channel c from image S into image Dst: Dst = (y) * ew + S * ew (thread per channel)
     auto token_mix = [&](const GmTokW &tw, const float *S, float *Dst) {
+        if (TM_GMB_ABL & 1) return;
         for (int c = tid; c < C; c += blockDim.x) {
             float av[GM_MT], z1[GM_MT / 2], y[GM_MT], mean, rstd;
 #pragma unroll
@@ -1053,7 +1065,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
     };
     // channel LayerNorm statistics of image S (one wave per token) into tmean / trstd, then this lane's rows
     auto chan_stats = [&](const float *S) {
-        for (int t = wave; t < GM_MT; t += NWV) {
+        for (int t = wave; t < GM_MT && !(TM_GMB_ABL & 8); t += NWV) {
             float mean = 0.f, rstd = 0.f;
             if (t < N) {
                 float s = 0.f, q = 0.f;
@@ -1095,7 +1107,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
             gmx4 acc[GM_HCH / 64][2];
 #pragma unroll
             for (int i = 0; i < GM_HCH / 64; ++i) acc[i][0] = acc[i][1] = gmx4{0.f, 0.f, 0.f, 0.f};
-            gm_gemm_mt<GMT, GM_HCH / 64, true>(X + 16 * mh * XP, XP, 0, W1, NH, h0 + wq, nw1, 0, C16 / 16, acc, lnw, lnb,
+            if (!(TM_GMB_ABL & 2)) gm_gemm_mt<GMT, GM_HCH / 64, true>(X + 16 * mh * XP, XP, 0, W1, NH, h0 + wq, nw1, 0, C16 / 16, acc, lnw, lnb,
                                                mr, rr);
 #pragma unroll
             for (int i = 0; i < GM_HCH / 64; ++i) {
@@ -1111,7 +1123,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
                     }
             }
             __syncthreads();
-            gm_gemm_mt<GMT, NTW, false>(H + 16 * mh * HP, HP, h0, W2, NT, wq, ntw, h0, nh, acc2, nullptr, nullptr, mr, rr);
+            if (!(TM_GMB_ABL & 2)) gm_gemm_mt<GMT, NTW, false>(H + 16 * mh * HP, HP, h0, W2, NT, wq, ntw, h0, nh, acc2, nullptr, nullptr, mr, rr);
             __syncthreads();
         }
 #pragma unroll
@@ -1189,9 +1201,9 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
 #pragma unroll
             for (int i = 0; i < GM_HCH / 64; ++i)
                 acc[i][0] = acc[i][1] = accd[i][0] = accd[i][1] = gmx4{0.f, 0.f, 0.f, 0.f};
-            gm_gemm_mt<GMT, GM_HCH / 64, true>(O1 + 16 * mh * XP, XP, 0, W1, NH, h0 + wq, nw1, 0, C16 / 16, acc, lnw, lnb,
+            if (!(TM_GMB_ABL & 2)) gm_gemm_mt<GMT, GM_HCH / 64, true>(O1 + 16 * mh * XP, XP, 0, W1, NH, h0 + wq, nw1, 0, C16 / 16, acc, lnw, lnb,
                                                mr, rr);
-            gm_gemm_mt<GMT, GM_HCH / 64, false>(DY + 16 * mh * XP, XP, 0, W2T, NH, h0 + wq, nw1, 0, C16 / 16, accd,
+            if (!(TM_GMB_ABL & 2)) gm_gemm_mt<GMT, GM_HCH / 64, false>(DY + 16 * mh * XP, XP, 0, W2T, NH, h0 + wq, nw1, 0, C16 / 16, accd,
                                                 nullptr, nullptr, mr, rr);
             // H = gelu(Z2) for Y_ch; dZ2 = dG2 gelu'(Z2) kept in accd for the second pass through U
 #pragma unroll
@@ -1211,7 +1223,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
                     }
             }
             __syncthreads();
-            gm_gemm_mt<GMT, NTW, false>(H + 16 * mh * HP, HP, h0, W2, NT, wq, ntw, h0, nh, acc2, nullptr, nullptr, mr, rr);
+            if (!(TM_GMB_ABL & 2)) gm_gemm_mt<GMT, NTW, false>(H + 16 * mh * HP, HP, h0, W2, NT, wq, ntw, h0, nh, acc2, nullptr, nullptr, mr, rr);
             __syncthreads();
 #pragma unroll
             for (int i = 0; i < GM_HCH / 64; ++i) {
@@ -1226,7 +1238,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
                     }
             }
             __syncthreads();
-            gm_gemm_mt<GMT, NTW, false>(H + 16 * mh * HP, HP, h0, W1T, NT, wq, ntw, h0, nh, accv, nullptr, nullptr, mr,
+            if (!(TM_GMB_ABL & 2)) gm_gemm_mt<GMT, NTW, false>(H + 16 * mh * HP, HP, h0, W1T, NT, wq, ntw, h0, nh, accv, nullptr, nullptr, mr,
                                         rr);
             __syncthreads();
         }
@@ -1265,7 +1277,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
                 }
         }
         __syncthreads();
-        for (int t = wave; t < N; t += NWV) {
+        for (int t = wave; t < N && !(TM_GMB_ABL & 8); t += NWV) {
             const float mean = tmean[t], rstd = trstd[t];
             float s1 = 0.f, s2 = 0.f;
             for (int c = lane; c < C; c += 64) {
@@ -1284,7 +1296,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
         }
         __syncthreads();
         // token branch, thread per channel: G = d out1 -> d layer input; DY = the channel's terms of d sew
-        for (int c = tid; c < C; c += blockDim.x) {
+        for (int c = tid; c < C && !(TM_GMB_ABL & 1); c += blockDim.x) {
             float av[GM_MT], z1[GM_MT / 2], y[GM_MT], mean, rstd;
 #pragma unroll
             for (int t = 0; t < GM_MT; ++t) av[t] = t < N ? XI[gm_idx(t, c, XP)] * sew[t] : 0.f;
@@ -1413,7 +1425,7 @@ extern "C" int tm_gm_embed(const tm_gm_embed_args *p, void *stream) {
     a.x_mean = q.x_mean;
     a.node_out = q.node_out;
     if (tm_gm_fused_ok(q.N, q.C, q.T, q.HC)) {
-        // packs by tm_gm_pack_a: proj_w (1, 4), channel ffn.0 (2, 1), ffn.3 (1, 2)
+        // packs by tm_gm_pack_a: proj_w (1, 2) ((1, 4) for C <= 16), channel ffn.0 (2, 1), ffn.3 (1, 2)
         const size_t lds = gm_fused_lds_bytes(q.C, q.N);
         const int nc = gm_r16(q.C) / 16, rpw = q.N > 16 ? 2 : 4;
         const unsigned grid = (unsigned)((q.R + rpw - 1) / rpw);

@@ -228,18 +228,47 @@ def prepare_step(base_model, batch):
     return kw, pos_out_ori, neg_out_ori, y_ori
 
 
+def _record_stream(obj, stream):
+    """record_stream(stream) on every tensor inside obj (dicts, lists, tuples)."""
+    if isinstance(obj, torch.Tensor):
+        if obj.is_cuda:
+            obj.record_stream(stream)
+    elif isinstance(obj, dict):
+        for v in obj.values():
+            _record_stream(v, stream)
+    elif isinstance(obj, (list, tuple)):
+        for v in obj:
+            _record_stream(v, stream)
+
+
 def train_step(explainer, base_model, optimizer, batch, *, beta=0.5, prior_p=0.3, if_bern=True, criterion=None,
-               grad_sync=None, prepared=None, overlap=None):
+               grad_sync=None, prepared=None, overlap=None, side_stream=None):
     """temp_exp_main.py:593-632 for one batch; returns the step's tensors (no host sync).  ``prepared``:
     this batch's ``prepare_step`` output if it was issued earlier; ``overlap``: a callable run while the
-    gradient all-reduce is in flight (between ``grad_sync.start()`` and ``.finish()``)."""
+    gradient all-reduce is in flight (between ``grad_sync.start()`` and ``.finish()``); ``side_stream``:
+    without ``prepared``, the base model's original-prediction contrast (``prepare_step``, independent of
+    the explainer) runs on this stream concurrently with the explainer's encoder and explanation, joined
+    before the explained contrast."""
     criterion = criterion or torch.nn.BCEWithLogitsLoss()
     sg_s, sg_t, sg_b = batch.subgraphs
     w_s, w_t, w_b = batch.walks
-    kw, pos_out_ori, neg_out_ori, y_ori = prepared if prepared is not None else prepare_step(base_model, batch)
+    fork = prepared is None and side_stream is not None
+    if fork:
+        cur = torch.cuda.current_stream(side_stream.device)
+        side_stream.wait_stream(cur)
+        with torch.cuda.stream(side_stream):
+            prepared = prepare_step(base_model, batch)
+    elif prepared is None:
+        prepared = prepare_step(base_model, batch)
+    kw, pos_out_ori, neg_out_ori, y_ori = prepared
     optimizer.zero_grad()
     g_s, g_t, g_b = encode_sides(explainer, batch)
     explanation = explain_sides(explainer, batch, (g_s, g_t, g_b), if_bern)
+    if fork:
+        cur.wait_stream(side_stream)
+        if not torch.cuda.is_current_stream_capturing():
+            # the side stream's allocations are read here: keep them from its pool until this stream is done
+            _record_stream(prepared, cur)
     pos_logit, neg_logit = base_model.contrast(batch.src, batch.dst, batch.fake, batch.ts, batch.e_idx, sg_s, sg_t,
                                                sg_b, explain_weights=explanation, **kw)
     pred = torch.cat([pos_logit, neg_logit], dim=0)
@@ -321,10 +350,14 @@ class GraphedTrainStep:
     first ``len(warmup_rows)`` batches are run eagerly on the capture stream first (they are real
     training steps).  Returns the static output dict of ``train_step`` (overwritten by every call)."""
 
-    def __init__(self, explainer, base_model, optimizer, buf, src, dst, ts, e_idx, warmup_rows, **kw):
+    def __init__(self, explainer, base_model, optimizer, buf, src, dst, ts, e_idx, warmup_rows, *,
+                 overlap_prepare=True, **kw):
         dev = src.device
         self.args = (explainer, base_model, optimizer, buf, src, dst, ts, e_idx)
         self.kw = kw
+        if overlap_prepare and "prepared" not in kw:
+            # the captured graph gets two branches: the base model's original contrast beside the explainer
+            self.kw = dict(kw, side_stream=torch.cuda.Stream(device=dev))
         self.rows = torch.empty_like(warmup_rows[0])
         self.stream = torch.cuda.Stream(device=dev)
         self.stream.wait_stream(torch.cuda.current_stream(dev))

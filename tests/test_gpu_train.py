@@ -331,3 +331,24 @@ def test_train_step_through_graphmixer_hip_equals_torch(dev, if_bern):
     for k in gh:
         d, n = float((gh[k] - gt[k]).norm()), float(gt[k].norm())
         assert d <= 1e-4 * n + 1e-9, (k, d, n)
+
+
+def test_side_stream_prepare_equals_inline(dev):
+    """train_step(side_stream=...) -- the base model's original-prediction contrast on a second stream,
+    concurrent with the explainer's encoder and explanation, joined before the explained contrast -- takes
+    the same step as the inline order: losses, y_ori and every explainer gradient (deterministic config)."""
+    from tempme_amd.train import train_step
+    res = []
+    for side in (None, torch.cuda.Stream(device=dev)):
+        base, ex, batch, opt = _setup("uslegis", dev)
+        ex.eval()
+        out = train_step(ex, base, opt, batch, beta=0.5, prior_p=0.3, if_bern=False, side_stream=side)
+        torch.cuda.synchronize()
+        res.append((out["loss"].item(), out["y_ori"].clone(),
+                    {k: v.grad.detach().clone() for k, v in ex.named_parameters() if v.grad is not None}))
+    (l0, y0, g0), (l1, y1, g1) = res
+    np.testing.assert_allclose(l1, l0, rtol=1e-6)
+    assert torch.equal(y0, y1)
+    assert g0.keys() == g1.keys() and len(g0) > 0
+    for k in g0:
+        assert float((g0[k] - g1[k]).norm()) <= 1e-5 * float(g0[k].norm()) + 1e-9, k

@@ -7,6 +7,7 @@ cd "$(dirname "$0")/.."
 name=$1; enc=$2
 out=ab_src/$name; mkdir -p "$out" tempme_amd/lib/ab
 cp tempme_amd/csrc/*.h tempme_amd/csrc/*.cpp tempme_amd/csrc/*.hip "$out/"
+rm -f "$out/dropin_ext.cpp"   # the torch host extension, not part of the library
 cp "$enc" "$out/encoder.hip"
 [ -n "$SAMPLER" ] && cp "$SAMPLER" "$out/sampler.hip"
 [ -n "$TRAIN" ] && cp "$TRAIN" "$out/encoder_train.hip"

@@ -54,6 +54,15 @@ def main():
         dt = (time.perf_counter() - t0) / reps
         res[mode] = g.detach().clone()
         print("%-5s forward + d ew backward: %.2f ms per %d rows (%d events x 3 sides)" % (mode, dt * 1e3, 3 * B, B))
+        if mode == "hip":
+            from tempme_amd import _lib as L
+            L.profile_enable(True)
+            for _ in range(reps):
+                step()
+            prof = L.profile_read()
+            L.profile_enable(False)
+            for k, (ms, cnt) in sorted(prof.items()):
+                print("  kernel %-16s %.3f ms per launch (%d launches)" % (k, ms / max(cnt, 1), cnt))
     err = float(torch.linalg.norm(res["hip"] - res["torch"]) / torch.linalg.norm(res["torch"]))
     print("relative difference of d ew, HIP vs torch formulation: %.2e" % err)
 
