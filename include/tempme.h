@@ -322,6 +322,15 @@ int tm_explain_train_bwd(const tm_weights *w, int32_t n_groups, int32_t B, int32
 int tm_kl_loss(const float *prob, const int32_t *cat, const float *null12, float target, int32_t n_groups, int32_t B,
                int32_t W, float *partial, float *dprob, void *stream);
 
+/* beta_sample(p, training=True) (explainer_new.py:420-430) around torch's own Dirichlet sampler and its
+ * gradient: tm_beta_params writes conc [n,2] = (clamp(10p, min=1), clamp(10(1-p), min=1)) and total [n,2]
+ * = their sum (the inputs of torch._sample_dirichlet / torch._dirichlet_grad); tm_beta_rsample_bwd gives dp
+ * [n] from g = d(x[:,0] * pad), the sample x [n,2] and d = torch._dirichlet_grad(x, conc, total) -- the
+ * same fp32 operations as torch's autograd graph of Beta(...).rsample() * pad. */
+int tm_beta_params(const float *p, int64_t n, float *conc, float *total, void *stream);
+int tm_beta_rsample_bwd(const float *g, const float *pad, const float *x, const float *d, const float *p, int64_t n,
+                        float *dp, void *stream);
+
 /* retrieve_edge_imp_node, eval (explainer_new.py:354-406, :420-430) for each of the G*B
  * (group, event) rows: dependency gate, walk->edge scatter-max, gather at the subgraph eids,
  * Beta mean, node==0 mask.  sub1_* [G,B,N], sub2_* [G,B,N*N]; out_h1 [G,B,N], out_h2 [G,B,N*N]

@@ -11,6 +11,7 @@ the library).
 """
 import ctypes as C
 import os
+import types
 
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
@@ -40,6 +41,7 @@ EXPORTS = (
     "tm_explain_train_fwd", "tm_explain_train_fwd_pad", "tm_explain_train_bwd", "tm_kl_loss", "tm_edge_importance", "tm_edge_gate_table",
     "tm_edge_table_cols", "tm_edge_tables", "tm_edge_feature_table", "tm_edge_importance_tab", "tm_tgn_attn_fwd", "tm_tgn_attn_bwd", "tm_gm_packed_floats", "tm_gm_pack", "tm_gm_embed", "tm_gm_embed_bwd_ok", "tm_gm_embed_bwd", "tm_gm_packed_a_floats", "tm_gm_pack_a", "tm_gm_fused_ok", "tm_dropin_create", "tm_dropin_free", "tm_dropin_forward", "tm_dropin_set_stream", "tm_edge_importance_gf", "tm_edge_importance_gf3", "tm_edge_importance_gf3_bern",
     "tm_mask_least_important", "tm_profile_enable", "tm_profile_sync", "tm_profile_entry",
+    "tm_beta_params", "tm_beta_rsample_bwd",
 )
 
 
@@ -174,10 +176,25 @@ def _sig(L):
     L.tm_tgn_attn_bwd.argtypes = [C.POINTER(TgnAttn), vp, vp, vp, vp, vp]
     L.tm_mask_least_important.argtypes = [vp, i32, i32, vp, i32, vp, vp, vp]
     L.tm_profile_enable.argtypes = [C.c_int]
+    L.tm_beta_params.argtypes = [vp, i64, vp, vp, vp]
+    L.tm_beta_rsample_bwd.argtypes = [vp, vp, vp, vp, vp, i64, vp, vp]
     L.tm_profile_entry.argtypes = [C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(i64)]
     for name in EXPORTS:
         if name not in ("tm_last_error", "tm_encoder_workspace_bytes"):
             getattr(L, name).restype = C.c_int
+
+
+class _Lenient:
+    """Attribute access on a CDLL that yields a throwaway object for symbols the library lacks."""
+
+    def __init__(self, L):
+        self.__dict__["_L"] = L
+
+    def __getattr__(self, name):
+        try:
+            return getattr(self._L, name)
+        except AttributeError:
+            return types.SimpleNamespace()
 
 
 def lib():
@@ -189,7 +206,9 @@ def lib():
                 f"tempme_amd: HIP library not built ({LIB_PATH} missing); run __graft_entry__.build() "
                 "or `make -C tempme_amd/csrc`")
         L = C.CDLL(LIB_PATH)
-        _sig(L)
+        # an A/B build (TEMPME_LIB) may predate newer entry points: their signatures are skipped, and a call
+        # to one of them fails with AttributeError
+        _sig(_Lenient(L) if os.environ.get("TEMPME_LIB") else L)
         _lib = L
     return _lib
 

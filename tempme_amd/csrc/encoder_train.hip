@@ -1908,6 +1908,63 @@ __global__ void __launch_bounds__(64) kl_loss_kernel(int32_t B, int32_t W, const
     }
 }
 
+// ------------------------------------------------------------------ Beta rsample glue (explainer_new.py:420-430)
+// Beta(clamp(10 p, min=1), clamp(10 (1 - p), min=1)).rsample() as torch evaluates it, minus its chain of small
+// launches: the concentrations (and the Dirichlet total) of the [n, 2] Dirichlet torch samples, in one
+// launch; and the backward after torch._dirichlet_grad, in one launch.  Same fp32 operations and order as
+// torch's autograd graph, so the results are bitwise the torch path's (tests/test_gpu_explain_train.py).
+__global__ void beta_params_kernel(int64_t n, const float *__restrict__ p, float2 *__restrict__ conc,
+                                   float2 *__restrict__ total) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float a0 = p[i] * 10.f, b0 = (1.f - p[i]) * 10.f;
+        const float a = a0 < 1.f ? 1.f : a0, b = b0 < 1.f ? 1.f : b0;   // clamp(min=1), NaN propagates
+        conc[i] = make_float2(a, b);
+        const float t = a + b;
+        total[i] = make_float2(t, t);
+    }
+}
+
+// dp from d out (out = x0 * pad), x [n, 2] the Dirichlet sample, d [n, 2] = torch._dirichlet_grad(x, conc, total):
+// Dirichlet backward with grad_output (g0, 0), select, clamp (self >= min) and the two scalings
+__global__ void beta_rsample_bwd_kernel(int64_t n, const float *__restrict__ g, const float *__restrict__ pad,
+                                        const float2 *__restrict__ x, const float2 *__restrict__ d,
+                                        const float *__restrict__ p, float *__restrict__ dp) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float g0 = g[i] * pad[i];
+        const float2 xv = x[i], dv = d[i];
+        const float sx = xv.x * g0 + xv.y * 0.f;
+        const float gc0 = dv.x * (g0 - sx), gc1 = dv.y * (0.f - sx);
+        const float pv = p[i];
+        const float ga = (pv * 10.f >= 1.f) ? gc0 : 0.f;
+        const float gb = ((1.f - pv) * 10.f >= 1.f) ? gc1 : 0.f;
+        dp[i] = ga * 10.f + -(gb * 10.f);
+    }
+}
+
+extern "C" int tm_beta_params(const float *p, int64_t n, float *conc, float *total, void *stream) {
+    if (n < 0) return fail(TM_E_ARG, "tm_beta_params: bad size");
+    if (n == 0) return TM_OK;
+    if (!p || !conc || !total) return fail(TM_E_ARG, "tm_beta_params: NULL pointer");
+    hipStream_t s = S_(stream);
+    const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+    beta_params_kernel<<<grid, 256, 0, s>>>(n, p, reinterpret_cast<float2 *>(conc), reinterpret_cast<float2 *>(total));
+    TM_CHECK_LAUNCH();
+    return TM_OK;
+}
+
+extern "C" int tm_beta_rsample_bwd(const float *g, const float *pad, const float *x, const float *d, const float *p,
+                                   int64_t n, float *dp, void *stream) {
+    if (n < 0) return fail(TM_E_ARG, "tm_beta_rsample_bwd: bad size");
+    if (n == 0) return TM_OK;
+    if (!g || !pad || !x || !d || !p || !dp) return fail(TM_E_ARG, "tm_beta_rsample_bwd: NULL pointer");
+    hipStream_t s = S_(stream);
+    const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+    beta_rsample_bwd_kernel<<<grid, 256, 0, s>>>(n, g, pad, reinterpret_cast<const float2 *>(x),
+                                                 reinterpret_cast<const float2 *>(d), p, dp);
+    TM_CHECK_LAUNCH();
+    return TM_OK;
+}
+
 extern "C" int tm_kl_loss(const float *prob, const int32_t *cat, const float *null12, float target, int32_t n_groups,
                           int32_t B, int32_t W, float *partial, float *dprob, void *stream) {
     if (n_groups < 0 || B < 0 || W <= 0) return fail(TM_E_ARG, "tm_kl_loss: bad arguments");

@@ -16,6 +16,7 @@ gradients) run the HIP forward/backward kernels through autograd Functions
 tm_kl_loss); only Beta ``rsample`` and the padding mask are torch ops.
 """
 import operator
+import os
 import threading
 import warnings
 
@@ -26,6 +27,9 @@ import torch.nn.functional as F
 
 from . import _lib as L
 from .null_model import get_null_distribution
+
+# TEMPME_BETA_TORCH=1: the training explanation's Beta draw through torch.distributions (A/B of _BetaRsampleFn)
+_BETA_TORCH = os.environ.get("TEMPME_BETA_TORCH", "0") == "1"
 
 
 class TimeEncode(nn.Module):
@@ -555,7 +559,10 @@ class TempME(nn.Module):
         p, pad = _ExplainFn.apply(self, args, imp.reshape(-1).to(dev, torch.float32).contiguous(),
                                   *self._gate_params())
         n1 = n_groups * B * N
-        e = self.beta_sample(p, training) * pad    # beta_sample then masked_fill(node == 0, 0) (:400-404, :420-430)
+        if training and pad is not None and not _BETA_TORCH:
+            e = _BetaRsampleFn.apply(p, pad)
+        else:
+            e = self.beta_sample(p, training) * pad    # beta_sample then masked_fill(node == 0, 0) (:400-404, :420-430)
         return e[:n1].view(n_groups, B, N), e[n1:].view(n_groups, B, N * N)
 
     def _expl_io(self, R):
@@ -1361,6 +1368,35 @@ class _KLFn(torch.autograd.Function):
     def backward(ctx, g):
         (dprob,) = ctx.saved_tensors
         return dprob * g, None, None, None
+
+
+class _BetaRsampleFn(torch.autograd.Function):
+    """beta_sample(p, training=True) * pad (explainer_new.py:400-404, :420-430) with torch's own Dirichlet
+    sampler and reparameterized gradient (torch._sample_dirichlet / torch._dirichlet_grad, the kernels
+    Beta.rsample runs, same RNG stream) and the elementwise rest in one launch each way (tm_beta_params,
+    tm_beta_rsample_bwd): bitwise the torch formulation, ~6 launches instead of ~25."""
+
+    @staticmethod
+    def forward(ctx, p, pad):
+        dev = p.device
+        n = p.numel()
+        conc = torch.empty(n, 2, dtype=torch.float32, device=dev)
+        total = torch.empty_like(conc)
+        st = L.stream_ptr(dev)
+        L.check(L.lib().tm_beta_params(L.ptr(p), n, L.ptr(conc), L.ptr(total), st), "beta_sample")
+        x = torch._sample_dirichlet(conc)
+        ctx.save_for_backward(p, pad, x, conc, total)
+        return x[:, 0] * pad
+
+    @staticmethod
+    def backward(ctx, g):
+        p, pad, x, conc, total = ctx.saved_tensors
+        d = torch._dirichlet_grad(x, conc, total)
+        g = g.contiguous()
+        dp = torch.empty_like(p)
+        L.check(L.lib().tm_beta_rsample_bwd(L.ptr(g), L.ptr(pad), L.ptr(x.contiguous()), L.ptr(d.contiguous()),
+                                            L.ptr(p), p.numel(), L.ptr(dp), L.stream_ptr(p.device)), "beta_sample")
+        return dp, None
 
 
 class _ExplainFn(torch.autograd.Function):

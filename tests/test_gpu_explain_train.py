@@ -175,3 +175,29 @@ def test_explain_backward_variants_match_autograd(dev, var):
         gr = sd[k].grad.double()
         assert ga.shape == gr.shape, k
         assert float((ga - gr).norm()) <= 2e-5 * float(gr.norm()) + 1e-9, (var, k)
+
+
+def test_fused_beta_rsample_equals_torch(dev):
+    """_BetaRsampleFn (tm_beta_params + torch._sample_dirichlet, torch._dirichlet_grad + tm_beta_rsample_bwd)
+    = Beta(clamp(10p, 1), clamp(10(1-p), 1)).rsample() * pad under autograd, bitwise: same RNG draws, same
+    sample, same gradient -- p includes values at the clamp boundaries (10p = 1, 10(1-p) = 1) and 0 / 1."""
+    from tempme_amd import TempME
+    from tempme_amd.explainer import _BetaRsampleFn
+    rng = np.random.RandomState(3)
+    n = 50000
+    p_np = rng.uniform(0, 1, n).astype(np.float32)
+    p_np[:6] = [0.1, 0.9, 0.0, 1.0, 0.05, 0.95]
+    pad_np = (rng.uniform(size=n) < 0.8).astype(np.float32)
+    g_np = rng.uniform(-1, 1, n).astype(np.float32)
+    ex = TempME(_Base(np.zeros((3, 172), np.float32), np.zeros((3, 4), np.float32)), "tgn", "synth", 40, 64, device=dev,
+                null_model={k: 1 / 12 for k in range(1, 13)}).to(dev)
+    t = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
+    outs = []
+    for fused in (True, False):
+        p = t(p_np).requires_grad_(True)
+        torch.manual_seed(11)
+        e = _BetaRsampleFn.apply(p, t(pad_np)) if fused else ex.beta_sample(p, True) * t(pad_np)
+        (e * t(g_np)).sum().backward()
+        outs.append((e.detach().clone(), p.grad.detach().clone()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1]), float((outs[0][1] - outs[1][1]).abs().max())
