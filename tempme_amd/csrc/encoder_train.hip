@@ -19,6 +19,7 @@
 // wgrad_partial_kernel + wgrad_reduce_kernel then form every weight gradient dW = dY^T X (and bias
 // gradient, a column of ones appended to X) over all rows in two launches (tm_encoder_wgrad).
 #include <cstdlib>
+#include <string>
 
 #include "encoder_common.h"
 
@@ -1573,10 +1574,11 @@ extern "C" int tm_encoder_bwd(const tm_weights *w, const float *n_feat, const fl
     pe = prof_begin(s);
     const int nqe = r16(P.kev) / 16;
     // register-resident instance: hid_dim 64, 11 node-feature tiles (dn 161..176, a multiple of 4), lin_event
-    // with 11..14 K steps; the LDS-tiled kernel otherwise
+    // with 11..14 K steps; the LDS-tiled kernel otherwise.  Opt-in (TEMPME_GCN_REG=1) until it has been
+    // checked on the GPU (written in round 4 while the GPU pool was unavailable to this build)
     const bool reg = P.h == HID && r16(P.dn) == 176 && P.dn % 4 == 0 && P.de % 4 == 0 && nqe >= 11 && nqe <= 14 &&
                      P.g1.nt == 4 && P.g1.nq == 11 && w->T.g2T.nt == 4 && w->T.g1T.nt == 11 && w->T.g1T.nq == 4 &&
-                     w->T.evT.nt == 11 && w->T.evT.nq == 11 && P.ev.nq == nqe && std::getenv("TEMPME_GCN_BWD_LDS") == nullptr;
+                     w->T.evT.nt == 11 && w->T.evT.nq == 11 && P.ev.nq == nqe && gcn_reg_enabled();
     if (reg) {
         const unsigned blocks = (unsigned)((n_rows + 63) / 64);
         if (nqe == 11) gcn_bwd_reg_kernel<11><<<dim3(blocks), 256, 0, s>>>(P, w->T, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, io->dF, go);
@@ -1592,13 +1594,19 @@ extern "C" int tm_encoder_bwd(const tm_weights *w, const float *n_feat, const fl
     return TM_OK;
 }
 
+// TEMPME_GCN_REG=1: the register-resident event_gcn forward / backward (gcn_fwd_reg_kernel, gcn_bwd_reg_kernel)
+bool tmk::gcn_reg_enabled() {   // read per launch (tests switch it inside one process)
+    const char *v = std::getenv("TEMPME_GCN_REG");
+    return v != nullptr && std::string(v) == "1";
+}
+
 bool tmk::launch_gcn_fwd_reg(const EncW &P, int64_t n_rows, const float *n_feat, const float *e_feat,
                              const int32_t *node6, const int32_t *eid3, const float *ts3, const float *cnt, float *F,
                              hipStream_t s) {
     const int nqe = r16(P.kev) / 16;
     if (!(P.h == HID && r16(P.dn) == 176 && P.dn % 4 == 0 && P.de % 4 == 0 && nqe >= 11 && nqe <= 14 &&
           P.ev.nt == 11 && P.ev.nq == nqe && P.g1.nt == 4 && P.g1.nq == 11 && P.g2.nt == 4 && P.g2.nq == 4) ||
-        std::getenv("TEMPME_GCN_LDS") != nullptr)
+        !gcn_reg_enabled())
         return false;
     const unsigned blocks = (unsigned)((n_rows + 63) / 64);
     if (nqe == 11) gcn_fwd_reg_kernel<11><<<dim3(blocks), 256, 0, s>>>(P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, F);
@@ -1666,10 +1674,12 @@ static int run_wgrad(const tm_wgrad_job *jobs, int njob, const tm_wgrad_target *
     float *part = reinterpret_cast<float *>(scratch((size_t)pb * sizeof(float), s));
     if (!part) return fail(TM_E_HIP, std::string(what) + ": scratch allocation failed");
     hipEvent_t pe = prof_begin(s);
-    if (std::getenv("TEMPME_WGRAD_ROWMAJOR"))
-        wgrad_partial_kernel<<<dim3((unsigned)wg), 256, 0, s>>>(P, part);
-    else
+    // the transposed-LDS form is opt-in (TEMPME_WGRAD_T=1) until it has been checked on the GPU
+    const char *wt = std::getenv("TEMPME_WGRAD_T");
+    if (wt != nullptr && std::string(wt) == "1")
         wgrad_partial_t_kernel<<<dim3((unsigned)wg), 256, 0, s>>>(P, part);
+    else
+        wgrad_partial_kernel<<<dim3((unsigned)wg), 256, 0, s>>>(P, part);
     TM_CHECK_LAUNCH();
     prof_end("wgrad_partial_kernel", s, pe);
     pe = prof_begin(s);

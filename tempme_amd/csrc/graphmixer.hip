@@ -557,7 +557,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 
     }
     __syncthreads();
     // ---- projection (:156-167): X = [E(e) | cos(dt w + b)] Wp^T + bp over K tiles padded to a multiple
-    // of 2 (zero fragments); B fragment of K tile q: edge features from the image, time features computed
+    // of 4 (zero fragments); B fragment of K tile q: edge features from the image, time features computed
     {
         const Ids I;
         const int m = I.m, j = I.j, vo = I.lane * 16;
@@ -565,9 +565,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 
         const size_t rowN = (size_t)rr * N;
         const bool tv = I.tok < N && a.nid[rowN + tokc] != 0;
         const float dt = (float)(a.cut[rr] - a.ts[rowN + tokc]);
-        // K tiles per loop iteration (and the pack's multiple): the GF_PF-deep ring must stay within the
-        // next iteration's QG * NC fragments
-        constexpr int QG = NC >= 2 ? 2 : 4;
+        // K tiles per loop iteration (and the pack's multiple, tm_gm_pack_a k_mult); the GF_PF-deep ring stays
+        // within the next iteration's QG * NC fragments
+        constexpr int QG = 4;
         const int KP = ((C + T + 16 * QG - 1) / (16 * QG)) * QG;
         const auto wr = gf_rsrc(a.proj_w);
         const auto rtw = gf_vrsrc(a.time_w, T), rtb = gf_vrsrc(a.time_b, T), rb = gf_vrsrc(a.proj_b, C);
@@ -1425,7 +1425,7 @@ extern "C" int tm_gm_embed(const tm_gm_embed_args *p, void *stream) {
     a.x_mean = q.x_mean;
     a.node_out = q.node_out;
     if (tm_gm_fused_ok(q.N, q.C, q.T, q.HC)) {
-        // packs by tm_gm_pack_a: proj_w (1, 2) ((1, 4) for C <= 16), channel ffn.0 (2, 1), ffn.3 (1, 2)
+        // packs by tm_gm_pack_a: proj_w (1, 4), channel ffn.0 (2, 1), ffn.3 (1, 2)
         const size_t lds = gm_fused_lds_bytes(q.C, q.N);
         const int nc = gm_r16(q.C) / 16, rpw = q.N > 16 ? 2 : 4;
         const unsigned grid = (unsigned)((q.R + rpw - 1) / rpw);
@@ -1494,7 +1494,9 @@ extern "C" int tm_gm_embed_bwd(const tm_gm_embed_args *p, const float *d_x_mean,
     GmBwd b{d_x_mean, d_node_out, d_ew, q.layer_table};
     hipEvent_t pe = prof_begin((hipStream_t)stream);
     const bool t3 = gm_r16(q.C) / 16 <= 12;
-    static const bool four = getenv("TEMPME_GM_BWD4") != nullptr;   // A/B: the round-3 four-wave form
+    // the eight-wave form is opt-in (TEMPME_GM_BWD8=1) until it has been checked on the GPU
+    const char *w8 = getenv("TEMPME_GM_BWD8");
+    const bool four = !(w8 != nullptr && w8[0] == '1');
     auto launch = [&](auto kern, int threads) -> int {
         TM_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         kern<<<q.R, threads, lds, (hipStream_t)stream>>>(a, b);

@@ -30,6 +30,9 @@ from .null_model import get_null_distribution
 
 # TEMPME_BETA_TORCH=1: the training explanation's Beta draw through torch.distributions (A/B of _BetaRsampleFn)
 _BETA_TORCH = os.environ.get("TEMPME_BETA_TORCH", "0") == "1"
+# TEMPME_EXPLAIN_PAD=1: the padding mask from the explanation kernel (tm_explain_train_fwd_pad) instead of a
+# torch comparison; opt-in until it has been checked on the GPU
+_EXPLAIN_PAD = os.environ.get("TEMPME_EXPLAIN_PAD", "0") == "1"
 
 
 class TimeEncode(nn.Module):
@@ -188,13 +191,14 @@ def _dropin_ext():
         import sysconfig
         path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
                             "_dropin_ext" + sysconfig.get_config_var("EXT_SUFFIX"))
-        if os.path.exists(path) and os.environ.get("TEMPME_DROPIN_EXT", "1") != "0":
+        # opt-in (TEMPME_DROPIN_EXT=1) until the extension has been checked on the GPU
+        if os.path.exists(path) and os.environ.get("TEMPME_DROPIN_EXT", "0") == "1":
             loader = importlib.machinery.ExtensionFileLoader("tempme_amd._dropin_ext", path)
             spec = importlib.util.spec_from_file_location("tempme_amd._dropin_ext", path, loader=loader)
             mod = importlib.util.module_from_spec(spec)
             loader.exec_module(mod)
             _EXT[0] = mod
-        elif os.environ.get("TEMPME_DROPIN_EXT", "1") != "0":
+        elif os.environ.get("TEMPME_DROPIN_EXT", "0") == "1":
             warnings.warn("tempme_amd/lib/_dropin_ext*.so not built (python tempme_amd/_build_ext.py): the drop-in "
                           "fast path's host side runs in Python", RuntimeWarning, stacklevel=3)
     return _EXT[0]
@@ -554,10 +558,14 @@ class TempME(nn.Module):
             masks = self.gate_dropout_masks(n_groups * B * 3 * W)
         i32 = lambda x: x.to(dev, torch.int32).contiguous()  # noqa: E731
         args = (i32(eid3), ts3.to(dev, torch.float32).contiguous(), i32(s1e), i32(s2e), masks,
-                int(n_groups), int(B), int(W), int(N), i32(s1n), i32(s2n))
+                int(n_groups), int(B), int(W), int(N))
+        if _EXPLAIN_PAD:
+            args = args + (i32(s1n), i32(s2n))
         # p = [hop-1 | hop-2] maxima of the G groups in one buffer (one Beta draw below), pad = the padding mask
         p, pad = _ExplainFn.apply(self, args, imp.reshape(-1).to(dev, torch.float32).contiguous(),
                                   *self._gate_params())
+        if pad is None:
+            pad = torch.cat([s1n.reshape(-1), s2n.reshape(-1)]).to(dev).ne(0).to(torch.float32)
         n1 = n_groups * B * N
         if training and pad is not None and not _BETA_TORCH:
             e = _BetaRsampleFn.apply(p, pad)

@@ -240,7 +240,7 @@ class GraphMixer(nn.Module):
                                pack(cf[3].weight, (1, 2)),
                                flat(cf[3].bias)])
             table = torch.tensor([[t.data_ptr() for t in lw] for lw in layers] or [[0] * 12], dtype=torch.int64)
-            self._gm_pack = dict(proj_w=pack(self.projection_layer.weight, (1, 2 if C > 16 else 4)), proj_b=flat(self.projection_layer.bias),
+            self._gm_pack = dict(proj_w=pack(self.projection_layer.weight, (1, 4)), proj_b=flat(self.projection_layer.bias),
                                  tw=flat(self.time_encoder.w.weight.reshape(-1)), tb=flat(self.time_encoder.w.bias),
                                  layers=layers, table=table.to(dev), keep=keep)
             self._gm_key = key

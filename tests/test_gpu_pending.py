@@ -1,0 +1,87 @@
+"""GPU validation of the round-4 paths that are opt-in until they have run on an MI355X (they were written
+while the GPU pool was closed to this build): each against the validated default path or the oracle.
+Skipped unless TEMPME_VALIDATE_PENDING=1 (``tools/gpu_run.sh pending``); once green, the flags become
+defaults.
+
+* TEMPME_GCN_REG=1 -- gcn_fwd_reg_kernel / gcn_bwd_reg_kernel (register-resident event_gcn training
+  forward and backward) and TEMPME_WGRAD_T=1 -- wgrad_partial_t_kernel: the encoder backward test against
+  fp64 autograd through the oracle, with the flags on.
+* TEMPME_EXPLAIN_PAD=1 -- the padding mask from tm_explain_train_fwd_pad: bitwise the torch mask.
+* TEMPME_GM_BWD8=1 -- gm_bwd_kernel with 8 waves (N > 16): the d ew test against fp64 autograd through
+  the oracle, with the flag on.
+* GraphedTrainStep(overlap_prepare=True): the graph with the base contrast on a second branch = eager.
+* TEMPME_DROPIN_EXT=1 -- the C++ drop-in host side: tests/test_gpu_enron.py's cpp test runs instead of
+  skipping when the runner sets it."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(os.environ.get("TEMPME_VALIDATE_PENDING") != "1",
+                                 reason="round-4 opt-in paths: TEMPME_VALIDATE_PENDING=1 runs them")]
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a HIP device")
+    return torch.device("cuda", 0)
+
+
+@pytest.mark.parametrize("de,G,B,N,train", [(32, 3, 20, 20, True), (32, 1, 9, 20, False), (172, 2, 11, 20, True)])
+def test_gcn_reg_and_wgrad_t_match_autograd(dev, monkeypatch, de, G, B, N, train):
+    from tests.test_gpu_encoder_train import test_encoder_backward_matches_autograd as check
+    monkeypatch.setenv("TEMPME_GCN_REG", "1")
+    monkeypatch.setenv("TEMPME_WGRAD_T", "1")
+    check(dev, de, G, B, N, train)
+
+
+def test_explain_pad_kernel_equals_torch_mask(dev, monkeypatch):
+    from tempme_amd import TempME
+    from tempme_amd import explainer as X
+    from tests.test_gpu_explain_train import _Base
+    rng = np.random.RandomState(5)
+    G, B, N, de = 3, 9, 20, 32
+    W, V, E = 3 * N, 50, 400
+    n_feat = rng.uniform(0, 1, (V + 1, 172)).astype(np.float32)
+    e_feat = rng.uniform(0, 1, (E + 1, de)).astype(np.float32)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    eid3 = t(rng.randint(0, E + 1, (G, B, W, 3)).astype(np.int32))
+    ts3 = t(rng.uniform(0, 1e6, (G, B, W, 3)).astype(np.float32))
+    s1e, s2e = t(rng.randint(0, E + 1, (G, B, N)).astype(np.int32)), t(rng.randint(0, E + 1, (G, B, N * N)).astype(np.int32))
+    s1n, s2n = t(rng.randint(0, 3, (G, B, N)).astype(np.int32)), t(rng.randint(0, 3, (G, B, N * N)).astype(np.int32))
+    imp_np = rng.uniform(0.05, 0.95, (G, B, W)).astype(np.float32)
+    torch.manual_seed(9)
+    ex = TempME(_Base(n_feat, e_feat), "tgn", "synth", 40, 64, device=dev,
+                null_model={k: 1 / 12 for k in range(1, 13)}).to(dev).eval()
+    ex.beta_sample = lambda prob, training: prob
+    outs = []
+    for on in (False, True):
+        monkeypatch.setattr(X, "_EXPLAIN_PAD", on)
+        imp = t(imp_np).requires_grad_(True)
+        e1, e2 = ex.explain_groups(imp, eid3, ts3, s1n, s1e, s2n, s2e, G, B, W, N, True)
+        (e1.sum() + 2 * e2.sum()).backward()
+        outs.append((e1.detach().clone(), e2.detach().clone(), imp.grad.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("N,C,L", [(30, 172, 2), (20, 32, 1), (20, 1, 3)])
+def test_gm_bwd_8_waves_vs_oracle(dev, monkeypatch, N, C, L):
+    from tests.test_gpu_graphmixer import test_hip_ew_gradient_vs_oracle as check
+    monkeypatch.setenv("TEMPME_GM_BWD8", "1")
+    check(dev, N, C, L)
+
+
+def test_graphed_step_with_prepare_branch_equals_eager(dev, monkeypatch):
+    from tempme_amd import train as T
+    from tests import test_gpu_train as TT
+    orig = T.GraphedTrainStep.__init__
+
+    def init(self, *a, **kw):
+        kw.setdefault("overlap_prepare", True)
+        orig(self, *a, **kw)
+    monkeypatch.setattr(T.GraphedTrainStep, "__init__", init)
+    TT.test_graphed_step_equals_eager(dev)

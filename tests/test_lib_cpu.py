@@ -76,10 +76,13 @@ def test_flops_model_matches_survey():
     assert bench.sampling_bytes_per_event(30, 3) == 143_376
 
 
-def test_dropin_extension_loads():
-    """The drop-in fast path's C++ host side (csrc/dropin_ext.cpp, built by build()) imports on the CPU and
-    exposes its entry points (constructing one needs a HIP device)."""
+def test_dropin_extension_loads(monkeypatch):
+    """The drop-in fast path's C++ host side (csrc/dropin_ext.cpp, built by build(); opt-in at run time,
+    TEMPME_DROPIN_EXT=1) imports on the CPU and exposes its entry points (constructing one needs a HIP
+    device)."""
     from tempme_amd import explainer as X
+    monkeypatch.setenv("TEMPME_DROPIN_EXT", "1")
+    monkeypatch.setattr(X, "_EXT", [None, False])
     m = X._dropin_ext()
     assert m is not None, "tempme_amd/lib/_dropin_ext*.so missing: python tempme_amd/_build_ext.py"
     for name in ("forward", "retrieve", "push", "current"):
