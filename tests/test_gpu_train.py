@@ -287,14 +287,18 @@ def test_run_steps_overlap_equals_serial(dev):
     # later steps drift apart only through torch's atomic scatter/gather backward (nondeterministic
     # summation order), which Adam's early ~lr*sign(g) updates amplify for near-zero gradients (as in
     # test_graphed_step_equals_eager): measured ~30 % of the parameters differ by more than 1e-6 after 4
-    # steps, and the later losses by up to ~4e-4 relative, but by far less than lr.  A step run on the wrong
-    # batch or on another batch's prepared inputs moves the losses by percents and most parameters by ~lr
+    # steps, and the later losses by up to ~4e-4 relative.  A step run on the wrong batch or on another
+    # batch's prepared inputs moves the losses by percents
     np.testing.assert_allclose(runs[1][0][0], runs[0][0][0], rtol=2e-5)
     np.testing.assert_allclose(runs[1][0], runs[0][0], rtol=2e-3)
-    lr = 1e-3
-    far = sum(int(((runs[1][1][k] - v).abs() > 0.5 * lr).sum()) for k, v in runs[0][1].items())
-    total = sum(v.numel() for v in runs[0][1].values())
-    assert far <= 0.01 * total, (far, total)
+    # every later step's gradients (recorded between backward and the optimizer step) agree with the serial
+    # loop's to a few percent of their norm -- near-zero gradients flip sign under the nondeterministic
+    # summation, so parameters are compared through the gradients they produce; a step on the wrong batch
+    # or on another batch's prepared inputs gives gradients that differ by O(1) of their norm
+    for k in range(1, 4):
+        a = torch.cat([g.reshape(-1) for g in runs[0][2][k]])
+        b = torch.cat([g.reshape(-1) for g in runs[1][2][k]])
+        assert float((a - b).norm()) <= 5e-2 * float(a.norm()), (k, float((a - b).norm()), float(a.norm()))
 
 
 @pytest.mark.parametrize("if_bern", [False, True])
