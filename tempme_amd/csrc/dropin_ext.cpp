@@ -44,6 +44,11 @@ constexpr int kSides = 3, kCache = 6, kMaxHostCut = 512;
 
 bool is_tensor(PyObject *o) { return THPVariable_Check(o); }
 
+// contiguous, on the context's device, of the given type: what the kernels' pointer arithmetic assumes
+bool plain(const at::Tensor &t, int device, at::ScalarType ty) {
+    return t.is_cuda() && t.get_device() == device && t.scalar_type() == ty && t.is_contiguous();
+}
+
 // a tensor the device pack handed out (pack.DevicePack views carry _tm_resident = True)
 bool resident(PyObject *o) {
     if (!is_tensor(o)) return false;
@@ -122,8 +127,8 @@ class Fast {
         if (B == 0 || n6.dim() != 3 || n6.size(0) != B || n6.size(1) != W || n6.size(2) != 6 || t3.dim() != 3 ||
             t3.size(0) != B || t3.size(1) != W || t3.size(2) != 3 || ct.dim() < 2 || ct.size(0) != B ||
             ct.size(1) != W || cn.dim() != 4 || cn.size(0) != B || cn.size(1) != W || cn.size(2) != 3 ||
-            cn.size(3) != 3 || e3.scalar_type() != at::kInt || t3.scalar_type() != at::kFloat ||
-            n6.scalar_type() != at::kInt || ct.scalar_type() != at::kInt || cn.scalar_type() != at::kFloat)
+            cn.size(3) != 3 || !plain(e3, device_, at::kInt) || !plain(t3, device_, at::kFloat) ||
+            !plain(n6, device_, at::kInt) || !plain(ct, device_, at::kInt) || !plain(cn, device_, at::kFloat))
             return py::none();
         // cut times: a host float64 array (sent as kernel arguments) or a device float64 tensor
         const double *cut_h = nullptr, *cut_d = nullptr;
@@ -213,10 +218,11 @@ class Fast {
         const int64_t N = sd[0].n1.size(1);
         for (int s = 0; s < kSides; ++s) {
             const Side &x = sd[s];
-            if (x.h->B != B || x.h->W != W || x.imp.scalar_type() != at::kFloat || x.imp.numel() != B * W ||
-                !x.imp.is_contiguous() || x.n1.dim() != 2 || x.n1.size(0) != B || x.n1.size(1) != N ||
-                x.n1.scalar_type() != at::kInt || !x.x1.sizes().equals(x.n1.sizes()) || x.n2.dim() != 2 ||
-                x.n2.size(0) != B || x.n2.size(1) != N * N || !x.x2.sizes().equals(x.n2.sizes()))
+            if (x.h->B != B || x.h->W != W || !plain(x.imp, device_, at::kFloat) || x.imp.numel() != B * W ||
+                x.n1.dim() != 2 || x.n1.size(0) != B || x.n1.size(1) != N || !plain(x.n1, device_, at::kInt) ||
+                !x.x1.sizes().equals(x.n1.sizes()) || !plain(x.x1, device_, at::kInt) || x.n2.dim() != 2 ||
+                x.n2.size(0) != B || x.n2.size(1) != N * N || !plain(x.n2, device_, at::kInt) ||
+                !x.x2.sizes().equals(x.n2.sizes()) || !plain(x.x2, device_, at::kInt))
                 return py::none();
         }
         const int64_t n_out = 3 * B * (N + N * N);
