@@ -1925,6 +1925,7 @@ __global__ void __launch_bounds__(64) kl_loss_kernel(int32_t B, int32_t W, const
 // torch's autograd graph, so the results are bitwise the torch path's (tests/test_gpu_explain_train.py).
 __global__ void beta_params_kernel(int64_t n, const float *__restrict__ p, float2 *__restrict__ conc,
                                    float2 *__restrict__ total) {
+#pragma clang fp contract(off)   // torch rounds every product and sum separately: no fma contraction
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const float a0 = p[i] * 10.f, b0 = (1.f - p[i]) * 10.f;
         const float a = a0 < 1.f ? 1.f : a0, b = b0 < 1.f ? 1.f : b0;   // clamp(min=1), NaN propagates
@@ -1939,6 +1940,7 @@ __global__ void beta_params_kernel(int64_t n, const float *__restrict__ p, float
 __global__ void beta_rsample_bwd_kernel(int64_t n, const float *__restrict__ g, const float *__restrict__ pad,
                                         const float2 *__restrict__ x, const float2 *__restrict__ d,
                                         const float *__restrict__ p, float *__restrict__ dp) {
+#pragma clang fp contract(off)   // ga * 10 + -(gb * 10) would otherwise become one fma (autograd adds two rounded terms)
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const float g0 = g[i] * pad[i];
         const float2 xv = x[i], dv = d[i];
