@@ -426,6 +426,10 @@ __global__ void gm_pack_kernel(const float *__restrict__ w, int32_t n_out, int32
 // mixing (both token tiles of a row) and the residual; the projection input's edge-feature rows are
 // staged in the same image first (coalesced row loads), the time features computed in the K loop.
 constexpr int GF_PF = 4;
+// A/B knob: token mixing two channel tiles per iteration (gm_fused_kernel), default off until measured
+#ifndef TM_GF_TOKPAIR
+#define TM_GF_TOKPAIR 0
+#endif
 
 // W [n_out][k] row-major -> A-operand fragments, tiles rounded up to multiples of n_mult / k_mult:
 // packed[((t * KT + q) * 64 + lane) * 4 + s] = W[16 t + (lane & 15)][16 q + 4 (lane >> 4) + s] (zero outside W)
@@ -652,6 +656,103 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 
                 }
 #pragma unroll
             for (int i = 0; i < 4; ++i) b1v[i] = 4 * g + i < HT ? tw3[4 * g + i] : 0.f;
+#if TM_GF_TOKPAIR
+            // two of the wave's channel tiles per iteration: two independent MFMA / shuffle chains in flight
+            // (the same operations per tile, so the same results).  Branch-free: the image's rows past N and
+            // columns past C hold zeros (the projection wrote them), lg / lb are zero past N, so loads and xn
+            // need no select; the token mask of the variance is a float in a VGPR (a compare per element would
+            // hold a lane mask in SGPRs); writes keep the lane's channel test (padding columns stay zero).
+            float tmk[NTT][4];
+#pragma unroll
+            for (int G = 0; G < NTT; ++G)
+#pragma unroll
+                for (int s2 = 0; s2 < 4; ++s2) {
+                    float m = 16 * G + 4 * s2 + g < N ? 1.f : 0.f;
+                    asm volatile("" : "+v"(m));
+                    tmk[G][s2] = m;
+                }
+            for (int nt0 = I.tt; nt0 < NC; nt0 += 2 * NTT) {
+                float v[2][NTT][4], mean[2], rstd[2];
+                int c[2];
+                bool cv[2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int ntu = min(nt0 + u * NTT, NC - 1);
+                    c[u] = 16 * ntu + li;
+                    cv[u] = nt0 + u * NTT < NC && c[u] < C;
+                    float sm = 0.f;
+#pragma unroll
+                    for (int G = 0; G < NTT; ++G)
+#pragma unroll
+                        for (int s2 = 0; s2 < 4; ++s2) {
+                            const int t = 16 * G + 4 * s2 + g;
+                            v[u][G][s2] = I.Xr[t * XS + c[u]] * I.sew[t];
+                            sm += v[u][G][s2];
+                        }
+                    mean[u] = sm;
+                }
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    float sm = mean[u];
+                    sm += __shfl_xor(sm, 16);
+                    sm += __shfl_xor(sm, 32);
+                    mean[u] = sm / (float)N;
+                }
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    float q = 0.f;
+#pragma unroll
+                    for (int G = 0; G < NTT; ++G)
+#pragma unroll
+                        for (int s2 = 0; s2 < 4; ++s2) {
+                            const float d = (v[u][G][s2] - mean[u]) * tmk[G][s2];
+                            q += d * d;
+                        }
+                    rstd[u] = q;
+                }
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    float q = rstd[u];
+                    q += __shfl_xor(q, 16);
+                    q += __shfl_xor(q, 32);
+                    rstd[u] = 1.f / sqrtf(q / (float)N + 1e-5f);
+                }
+                gmx4 hacc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+                for (int G = 0; G < NTT; ++G)
+#pragma unroll
+                    for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+                        for (int u = 0; u < 2; ++u) {
+                            const float xn = (v[u][G][s2] - mean[u]) * rstd[u] * lg[G][s2] + lb[G][s2];
+                            hacc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[G][s2], xn, hacc[u], 0, 0, 0);
+                        }
+                float h[2][4];
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) h[u][i] = 4 * g + i < HT ? gm_gelu(hacc[u][i] + b1v[i]) : 0.f;
+#pragma unroll
+                for (int mt = 0; mt < NTT; ++mt) {
+                    gmx4 yy[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+                    for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+                        for (int u = 0; u < 2; ++u)
+                            yy[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[mt][s2], h[u][s2], yy[u], 0, 0, 0);
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        if (!cv[u]) continue;
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int t = 16 * mt + 4 * g + i;
+                            const int ix = t * XS + c[u];
+                            I.Xr[ix] = (yy[u][i] + b2v[mt][i]) * I.sew[t] + I.Xr[ix] * I.sew[t];
+                        }
+                    }
+                }
+            }
+#else
             for (int nt = I.tt; nt < NC; nt += NTT) {
                 const int c = 16 * nt + li;
                 const bool cv = c < C;
@@ -705,6 +806,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 
                     }
                 }
             }
+#endif
         }
         __syncthreads();
         // ---- channel mixing (:300-305): the wave's token tile from the image; channel LayerNorm per
