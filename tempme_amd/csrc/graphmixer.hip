@@ -430,6 +430,10 @@ constexpr int GF_PF = 4;
 #ifndef TM_GF_TOKPAIR
 #define TM_GF_TOKPAIR 0
 #endif
+// A/B knob: the projection's K loop over pairs of K tiles (see gm_fused_kernel), default off until measured
+#ifndef TM_GF_QG2
+#define TM_GF_QG2 0
+#endif
 
 // W [n_out][k] row-major -> A-operand fragments, tiles rounded up to multiples of n_mult / k_mult:
 // packed[((t * KT + q) * 64 + lane) * 4 + s] = W[16 t + (lane & 15)][16 q + 4 (lane >> 4) + s] (zero outside W)
@@ -569,10 +573,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 
         const size_t rowN = (size_t)rr * N;
         const bool tv = I.tok < N && a.nid[rowN + tokc] != 0;
         const float dt = (float)(a.cut[rr] - a.ts[rowN + tokc]);
-        // K tiles per loop iteration (and the pack's multiple, tm_gm_pack_a k_mult); the GF_PF-deep ring stays
-        // within the next iteration's QG * NC fragments
-        constexpr int QG = 4;
-        const int KP = ((C + T + 16 * QG - 1) / (16 * QG)) * QG;
+        // KP = the pack's K tiles per output tile (tm_gm_pack_a k_mult 4: the fragment pitch); the loop runs
+        // QG K tiles per iteration up to KL.  TM_GF_QG2 (A/B knob): QG = 2, so the loop stops at the K tiles
+        // C + T needs rounded to pairs (22 instead of 24 at C = T = 172); the GF_PF-deep ring must stay within
+        // the next iteration's QG * NC fragments, hence QG = 4 for a single channel tile
+        constexpr int QG = (TM_GF_QG2 && NC >= 2) ? 2 : 4;
+        const int KP = ((C + T + 63) / 64) * 4;
+        const int KL = ((C + T + 16 * QG - 1) / (16 * QG)) * QG;
         const auto wr = gf_rsrc(a.proj_w);
         const auto rtw = gf_vrsrc(a.time_w, T), rtb = gf_vrsrc(a.time_b, T), rb = gf_vrsrc(a.proj_b, C);
         gmx4 y[NC];
@@ -585,10 +592,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 
         float4 ring[GF_PF];
 #pragma unroll
         for (int i = 0; i < GF_PF; ++i) ring[i] = gf_frag(wr, vo, ((i % NC) * KP + i / NC) * 1024);
-        for (int q0 = 0; q0 < KP; q0 += QG) {
+        for (int q0 = 0; q0 < KL; q0 += QG) {
             // iteration bases opaque per iteration: loop strength reduction would otherwise keep every
             // fragment's offset as its own SGPR induction variable
-            int qb = q0 * 1024, qn = min(q0 + QG, KP - QG) * 1024;
+            int qb = q0 * 1024, qn = min(q0 + QG, KL - QG) * 1024;
             asm volatile("" : "+s"(qb), "+s"(qn));
 #pragma unroll
             for (int dq = 0; dq < QG; ++dq) {
