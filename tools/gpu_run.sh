@@ -68,6 +68,7 @@ for s in "$@"; do
         n30) step bench_n30 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --n-degree 30 ;;
         phases) step phases 300 python tools/train_phases.py ;;
         pending) TEMPME_VALIDATE_PENDING=1 TEMPME_DROPIN_EXT=1 step pytest_pending 600 python -u -m pytest tests/test_gpu_pending.py tests/test_gpu_enron.py -x -v -m gpu --timeout 300 --timeout-method thread -k "pending or cpp_host" ;;
+        trainflags) step train_flags 1100 ./tools/train_flags_ab.sh ;;
         gmab) step gm_ab 900 ./tools/gm_ab.sh ;;
         gmbab) step gmb_ab 900 ./tools/gmb_ab.sh ;;
         gmbwd) step gm_bwd 300 python tools/gm_bwd_timing.py && TEMPME_GM_BWD4=1 step gm_bwd4 300 python tools/gm_bwd_timing.py ;;
