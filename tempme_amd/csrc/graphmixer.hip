@@ -1060,7 +1060,9 @@ template <int NMT, int NTW, bool TS8>
 __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmArgs a, GmBwd b) {
     extern __shared__ float gm_lds[];
     constexpr bool TS = NMT == 2 && TS8;
-    constexpr int NWV = TS ? 8 : 4, GMT = TS ? 1 : NMT;
+    // GMT: token tiles per wave in the GEMMs; WT: token tiles per wave in the epilogues (the 4-wave form writes
+    // both tiles, zeros past NMT, as before the 8-wave form existed)
+    constexpr int NWV = TS ? 8 : 4, GMT = TS ? 1 : NMT, WT = TS ? 1 : 2;
     const int r = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int wq = TS ? (wave & 3) : wave, mh = TS ? (wave >> 2) : 0;
     const int N = a.N, C = a.C, T = a.T, D = a.D, L = a.L, HT = a.HT;
@@ -1116,7 +1118,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
                 const int n = 16 * (wq + 4 * i) + (lane & 15);
                 const float bv = n < C ? a.proj_b[n] : 0.f;
 #pragma unroll
-                for (int q = 0; q < GMT; ++q)
+                for (int q = 0; q < WT; ++q)
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const int mt = mh + q, t = 16 * mt + 4 * (lane >> 4) + e;
@@ -1193,7 +1195,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
         }
         __syncthreads();
 #pragma unroll
-        for (int q = 0; q < GMT; ++q) {
+        for (int q = 0; q < WT; ++q) {
             mr[q] = tmean[16 * (mh + q) + (lane & 15)];
             rr[q] = trstd[16 * (mh + q) + (lane & 15)];
         }
@@ -1224,7 +1226,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
                 const int ht = wq + 4 * i, n = 16 * (h0 + ht) + (lane & 15);
                 const float bv = n < a.HC ? w[9][n] : 0.f;
 #pragma unroll
-                for (int q = 0; q < GMT; ++q)
+                for (int q = 0; q < WT; ++q)
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const int mt = mh + q, t = 16 * mt + 4 * (lane >> 4) + e;
@@ -1242,7 +1244,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
             const int n = 16 * nt + (lane & 15);
             const float bv = n < C ? w[11][n] : 0.f;
 #pragma unroll
-            for (int q = 0; q < GMT; ++q)
+            for (int q = 0; q < WT; ++q)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int mt = mh + q, t = 16 * mt + 4 * (lane >> 4) + e;
@@ -1321,7 +1323,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
                 const int ht = wq + 4 * i, n = 16 * (h0 + ht) + (lane & 15);
                 const float bv = n < a.HC ? w[9][n] : 0.f;
 #pragma unroll
-                for (int q = 0; q < GMT; ++q)
+                for (int q = 0; q < WT; ++q)
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const int mt = mh + q, t = 16 * mt + 4 * (lane >> 4) + e;
@@ -1339,7 +1341,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
                 if (i >= nw1) break;
                 const int ht = wq + 4 * i;
 #pragma unroll
-                for (int q = 0; q < GMT; ++q)
+                for (int q = 0; q < WT; ++q)
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const int t = 16 * (mh + q) + 4 * (lane >> 4) + e;
@@ -1359,7 +1361,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
             const int n = 16 * nt + (lane & 15);
             const float bv = n < C ? w[11][n] : 0.f;
 #pragma unroll
-            for (int q = 0; q < GMT; ++q)
+            for (int q = 0; q < WT; ++q)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int mt = mh + q, t = 16 * mt + 4 * (lane >> 4) + e;
@@ -1378,7 +1380,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
             const int n = 16 * nt + (lane & 15);
             const float gw = n < C ? w[6][n] : 0.f;
 #pragma unroll
-            for (int q = 0; q < GMT; ++q)
+            for (int q = 0; q < WT; ++q)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int mt = mh + q, t = 16 * mt + 4 * (lane >> 4) + e;
