@@ -567,7 +567,7 @@ class TempME(nn.Module):
         if pad is None:
             pad = torch.cat([s1n.reshape(-1), s2n.reshape(-1)]).to(dev).ne(0).to(torch.float32)
         n1 = n_groups * B * N
-        if training and pad is not None and not _BETA_TORCH:
+        if training and pad is not None and self._fused_beta():
             e = _BetaRsampleFn.apply(p, pad)
         else:
             e = self.beta_sample(p, training) * pad    # beta_sample then masked_fill(node == 0, 0) (:400-404, :420-430)
@@ -915,7 +915,7 @@ class TempME(nn.Module):
             if grad:
                 args = tuple((g[0], g[1], g[3], g[5], g[6], g[7], g[8]) for g in sides)
                 p = _apply(_EvalExplain3RawFn, self, args, ia, ib, ic, p, fs.bundle(self, "gate"))
-            x = self.beta_sample(p, True) * keep
+            x = _BetaRsampleFn.apply(p.contiguous(), keep) if self._fused_beta() else self.beta_sample(p, True) * keep
             o1, o2 = x[:3 * B * N].view(3 * B, N), x[3 * B * N:].view(3 * B, N * N)
         else:
             o1, o2 = o.as_strided((3 * B, N), (N, 1)), o.as_strided((3 * B, N * N), (N * N, 1), 3 * B * N)
@@ -1010,6 +1010,11 @@ class TempME(nn.Module):
         if self.base_type == "tgn":
             return [torch.cat([s0, t0, b0], dim=0), torch.cat([s1, t1, b1], dim=0)]
         return [torch.cat([s0, t0, b0], dim=0)]
+
+    def _fused_beta(self):
+        """beta_sample(p, True) * mask may go through _BetaRsampleFn (bitwise the same as torch's Beta rsample):
+        not when the module's beta_sample is overridden (an instance attribute) or TEMPME_BETA_TORCH=1."""
+        return not _BETA_TORCH and "beta_sample" not in self.__dict__ and type(self).beta_sample is TempME.beta_sample
 
     def beta_sample(self, prob, training):
         """explainer_new.py:420-430."""
