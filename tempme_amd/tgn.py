@@ -271,6 +271,28 @@ def _as_dev(x, device, dtype):
     return torch.from_numpy(np.ascontiguousarray(np.asarray(x))).to(device=device, dtype=dtype)
 
 
+def _cat_rows(xs):
+    """torch.cat(xs) along dim 0 -- as a view when the tensors are consecutive row blocks of one contiguous
+    tensor (a gathered pack's three sides, [3, B, ...]), else a copy.  Only for tensors without autograd
+    history (the view would route gradients through the first one's base)."""
+    a = xs[0]
+    if all(isinstance(x, torch.Tensor) for x in xs) and not any(x.requires_grad for x in xs):
+        st = a.untyped_storage().data_ptr()
+        adjacent = all(x.is_contiguous() and x.dtype == a.dtype and x.device == a.device and x.dim() == a.dim()
+                       and x.shape[1:] == a.shape[1:] and x.untyped_storage().data_ptr() == st for x in xs)
+        if adjacent:
+            off = a.storage_offset()
+            for x in xs:
+                if x.storage_offset() != off:
+                    adjacent = False
+                    break
+                off += x.numel()
+        if adjacent:
+            return a.as_strided((sum(int(x.shape[0]) for x in xs),) + tuple(a.shape[1:]), a.stride(),
+                                a.storage_offset())
+    return torch.cat(list(xs))
+
+
 # ------------------------------------------------------------------ the model
 class TGN(nn.Module):
     """TGN/tgn.py:14-97 constructor (same arguments, submodules and initialisation order)."""
@@ -550,7 +572,12 @@ class TGN(nn.Module):
         roots = torch.cat([_as_dev(x, dev, torch.long).reshape(-1) for x in (src_idx, tgt_idx, bgd_idx)])
 
         def cat(i, h, dtype):
-            return torch.cat([_as_dev(sg[i][h], dev, dtype) for sg in (subgraph_src, subgraph_tgt, subgraph_bgd)])
+            xs = [sg[i][h] for sg in (subgraph_src, subgraph_tgt, subgraph_bgd)]
+            if all(isinstance(x, torch.Tensor) and x.device == dev for x in xs):
+                # the three sides of a gathered pack are consecutive rows of one tensor: one view, and one
+                # dtype conversion instead of three (elementwise, so the same values as convert-then-cat)
+                return _as_dev(_cat_rows(xs), dev, dtype)
+            return torch.cat([_as_dev(x, dev, dtype) for x in xs])
         nodes = [roots, cat(0, 0, torch.int32), cat(0, 1, torch.int32)]
         eids = [cat(1, 0, torch.int32), cat(1, 1, torch.int32)] if edge_attr is None else [None, None]
         times = [cat(2, 0, torch.float64), cat(2, 1, torch.float64)]
