@@ -595,7 +595,7 @@ class TGN(nn.Module):
         B = len(src_idx)
         s, d, n = self.get_node_emb(src_idx, tgt_idx, bgd_idx, cut_time, e_idx, subgraph_src, subgraph_tgt,
                                     subgraph_bgd, explain_weights, edge_attr, prepared=prepared)
-        score = self.affinity(torch.cat([s, s], dim=0), torch.cat([d, n])).squeeze(dim=0)
+        score = self.affinity(torch.cat([s, s], dim=0), _cat_rows([d, n])).squeeze(dim=0)   # d, n: rows of one emb
         return score[:B], score[B:]
 
     def retrieve_edge_features(self, subgraph_src, subgraph_tgt, subgraph_bgd):
