@@ -64,3 +64,26 @@ def test_strict_pipeline_has_no_future(strict):
         assert future == 0
     else:
         assert future > 0    # the reference's ties and step-3 leak show up on this data
+
+
+def test_strict_equals_parity_without_ties():
+    """On a graph whose timestamps are all distinct, get_ts2idx's value is the record's position, which is
+    bisect_left of its own time: the e_idx slices of the two modes agree, so the k-hop samples (e_idx path
+    for hop 1 and hop 2) are identical; parity mode is pinned to the reference's goldens, so this pins
+    strict mode's slices to the reference's wherever the reference has no tie."""
+    rng = np.random.default_rng(4)
+    V, E = 40, 600
+    src = rng.integers(1, V, E)
+    dst = 1 + (src - 1 + rng.integers(1, V - 1, E)) % (V - 1)  # in 1..V-1, never src: no self-loop ties
+    assert not (dst == src).any()
+    ts = rng.permutation(E).astype(np.float64) + 1.0          # distinct times
+    eidx = np.arange(1, E + 1)
+    gp = orc.OracleGraph(src, dst, eidx, ts, V)
+    gs = orc.OracleGraph(src, dst, eidx, ts, V, strict_temporal=True)
+    rows = np.arange(E - 80, E)
+    for e_l in (eidx[rows], None):
+        a = orc.khop(gp, 3, px.SPLIT_TEST, px.SIDE_SRC, 2, 10, src[rows], ts[rows], e_l, np.arange(len(rows)))
+        b = orc.khop(gs, 3, px.SPLIT_TEST, px.SIDE_SRC, 2, 10, src[rows], ts[rows], e_l, np.arange(len(rows)))
+        for x, y in zip(a, b):
+            for u, v in zip(x, y):
+                assert np.array_equal(u, v)
