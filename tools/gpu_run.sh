@@ -77,6 +77,10 @@ for s in "$@"; do
         c4) step bench_c4 900 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config 4 ;;
         a3) step bench_a3 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --alpha 3.0 ;;
         dropint) step dropint 300 python tools/dropin_timing.py ;;
+        dropintx) TEMPME_DROPIN_EXT=1 step dropintx 300 python tools/dropin_timing.py ;;
+        diag) step overlap_diag 300 python -u tools/overlap_diag.py ;;
+        testsall) step pytest_gpu_all 1100 python -u -m pytest tests -q -m gpu -rfEs --timeout 300 --timeout-method thread ;;
+        pendingall) TEMPME_VALIDATE_PENDING=1 TEMPME_DROPIN_EXT=1 step pytest_pending 600 python -u -m pytest tests/test_gpu_pending.py tests/test_gpu_enron.py -v -m gpu -rfEs --timeout 300 --timeout-method thread -k "pending or cpp_host" ;;
         dropintrace) step dropintrace 300 rocprofv3 --kernel-trace -d gpurun_out/ditrace -o run --output-format csv -- python tools/dropin_timing.py ;;
         dropinprof) TEMPME_DROPIN_PROFILE=1 step dropinprof 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
         abtests:*)  # the GPU suite against tempme_amd/lib/ab/<name>.so
