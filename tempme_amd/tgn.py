@@ -288,8 +288,14 @@ def _cat_rows(xs):
                     break
                 off += x.numel()
         if adjacent:
-            return a.as_strided((sum(int(x.shape[0]) for x in xs),) + tuple(a.shape[1:]), a.stride(),
-                                a.storage_offset())
+            # explicit contiguous strides: is_contiguous() ignores the stride of a size-1 dim, so a.stride()
+            # may not describe consecutive rows when a has one row
+            shape = (sum(int(x.shape[0]) for x in xs),) + tuple(a.shape[1:])
+            strides, acc = [], 1
+            for d in reversed(shape):
+                strides.append(acc)
+                acc *= int(d)
+            return a.as_strided(shape, tuple(reversed(strides)), a.storage_offset())
     return torch.cat(list(xs))
 
 

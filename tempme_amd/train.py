@@ -143,17 +143,19 @@ class GradAllReduce:
     ``finish()`` waits for it and writes the averages back.  Work issued between the two (the next
     batch's gather and the frozen base model's original-prediction contrast, which read neither the
     explainer's gradients nor its weights) overlaps the collective.  ``__call__`` does
-    both back to back."""
+    both back to back.  ``force``: run the collective even in a group of one (exercises the backend's
+    path, e.g. RCCL on one GPU; at world size 1 the average is the gradient itself)."""
 
-    def __init__(self, module, group=None):
+    def __init__(self, module, group=None, force=False):
         self.module, self.group = module, group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.force = bool(force) and dist.is_initialized()
         self._flat = None
         self._work = None
         self._grads = None
 
     def start(self):
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             return
         grads = [p.grad for p in self.module.parameters() if p.grad is not None]
         if not grads:
@@ -292,6 +294,7 @@ def train_step(explainer, base_model, optimizer, batch, *, beta=0.5, prior_p=0.3
     if grad_sync is not None and hasattr(grad_sync, "finish"):
         grad_sync.finish()
     optimizer.step()
+    batch.imp_all = None      # drop the importances' autograd graph with the step (callers may keep the batch)
     return dict(loss=loss.detach(), pred_loss=pred_loss.detach(), kl_loss=kl_loss.detach(),
                 pos_logit=pos_logit.detach(), neg_logit=neg_logit.detach(), pos_out_ori=pos_out_ori,
                 neg_out_ori=neg_out_ori, y_ori=y_ori)

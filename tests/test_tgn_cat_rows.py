@@ -32,3 +32,14 @@ def test_other_layouts_are_copied():
     ys = list(g.unbind(0))
     out = _cat_rows(ys)
     assert out.grad_fn is not None and torch.equal(out, torch.cat(ys))
+
+
+def test_single_row_blocks_with_odd_leading_stride():
+    """B == 1: a [1, N] block is contiguous whatever its leading stride (is_contiguous ignores size-1 dims);
+    the view must still lay the blocks out as consecutive rows, like torch.cat."""
+    base = torch.arange(3 * 7, dtype=torch.int32).reshape(3, 7)
+    xs = [base[k].as_strided((1, 7), (99, 1), base[k].storage_offset()) for k in range(3)]
+    assert all(x.is_contiguous() for x in xs)
+    out = _cat_rows(xs)
+    assert torch.equal(out, torch.cat(xs))
+    assert out.stride() == (7, 1)
