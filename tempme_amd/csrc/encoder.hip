@@ -595,15 +595,11 @@ static_assert(TM_JIT_NODES || (TM_ET_STEP < 0 && TM_POS_STEP < 0), "in-G1 loads 
 #define TM_LIN_D PFP
 #endif
 constexpr int WALK_WPB = TM_WALK_WPB;
-// persistent walk_kernel waves (1: the grid is one round of resident workgroups looping over the units)
+// persistent walk_kernel waves: the grid is one round of resident workgroups looping over the units;
+// 1: static striding (wave w takes units w, w + stride, ...), 2: dynamic (each wave takes its next unit
+// from an atomic counter, requested at the start of its current unit)
 #ifndef TM_WALK_PERSIST
 #define TM_WALK_PERSIST 0
-#endif
-#ifndef TM_WALK_OFFSET
-#define TM_WALK_OFFSET 0
-#endif
-#ifndef TM_WALK_PRIO
-#define TM_WALK_PRIO 0
 #endif
 
 template <int NTO, int NQ, int NQL, int BASE>
@@ -809,6 +805,7 @@ struct WalkArgs {
     const double *cut;
     float *out;
     const float *etab;    // [n_ids][16*NTD] lin_event's edge-feature part + bias per edge id (Q0 > 0)
+    uint32_t *ticket;     // TM_WALK_PERSIST == 2: the launch's unit counter (zeroed before the launch)
 };
 
 // Phase timing (debug builds only, -DTM_STAMPS; tools/stamps.py): s_memtime deltas of lane 0 per
@@ -1344,18 +1341,20 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * TM_WALK_WAVES / WALK_WPB) w
     const int lane = threadIdx.x & 63, col = lane & 15;
     const int32_t NS = a.W / a.M;
     const int64_t n_units = (a.n_slots + 15) / 16;
-#if TM_WALK_PERSIST
-    // persistent waves: the grid is one round of resident workgroups; wave w takes units w, w + stride, ...
-    // (the constant table is loaded once per workgroup, the next unit's first scalars and table row are
-    // requested during the last pass of the current one)
-    const int64_t ustride = (int64_t)gridDim.x * (blockDim.x >> 6);
-#else
-    const int64_t ustride = n_units;                    // one unit per wave
-#endif
+    // persistent waves (not SPLIT): the grid is one round of resident workgroups; wave w takes units w,
+    // w + stride, ... or (dynamic) its next unit from the launch's counter (the constant table is loaded once per
+    // workgroup, the next unit's first scalars and table row are requested during the last pass of the current one)
+    constexpr int PERSIST = SPLIT ? 0 : TM_WALK_PERSIST;
+    const int64_t ustride = PERSIST ? (int64_t)gridDim.x * (blockDim.x >> 6) : n_units;
     int64_t unit = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    // the next unit (dynamic): a ticket from the launch's counter, offset by the first round (the grid's waves)
+    auto ticket = [&]() -> int64_t {
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(a.ticket, 1u);
+        return ustride + (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+    };
     int m0 = 0;                                         // SPLIT: this wave's walk within each slot
     if constexpr (SPLIT) {
-        static_assert(!TM_WALK_PERSIST, "split waves take one unit each");
         m0 = (int)(unit % a.M);
         unit /= a.M;
     }
@@ -1377,20 +1376,6 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * TM_WALK_WAVES / WALK_WPB) w
     load_consts<NQE, NTD>(P, cs);
     __syncthreads();
     if (unit >= n_units) return;                        // whole wave idle (wave-uniform)
-#if TM_WALK_PERSIST && TM_WALK_OFFSET
-    // the upper half of a workgroup's waves (wave w shares its SIMD with wave w - WPB/2) starts
-    // TM_WALK_OFFSET real-time ticks (100 MHz) late, so the two waves of a SIMD run out of phase
-    if ((threadIdx.x >> 6) >= WALK_WPB / 2) {
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)TM_WALK_OFFSET) __builtin_amdgcn_s_sleep(127);
-    }
-#endif
-#if TM_WALK_PRIO == 1
-    // static arbitration priority for one wave of each SIMD pair (the upper half of the workgroup)
-    if ((threadIdx.x >> 6) >= WALK_WPB / 2) __builtin_amdgcn_s_setprio(1);
-#elif TM_WALK_PRIO == 2
-    if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);
-#endif
     Stash &st = stash[threadIdx.x >> 6];
     // every weight fragment off one buffer resource (WalkLay offsets from the folded region's base)
     const auto wr = wrsrc(P.kv.w);
@@ -1415,7 +1400,7 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * TM_WALK_WAVES / WALK_WPB) w
 #endif
 #pragma nounroll
     for (;;) {
-    const int64_t unext = unit + ustride;
+    const int64_t unext = PERSIST == 2 ? ticket() : unit + ustride;
     bool vn;
     int64_t egn;
     int32_t jn;
@@ -2030,6 +2015,9 @@ static void launch_walk(const WalkArgs &a, unsigned blocks, hipStream_t s) {
         }
         if (cap[dev] > 0 && blocks > (unsigned)cap[dev]) blocks = (unsigned)cap[dev];
     }
+#if TM_WALK_PERSIST == 2
+    if (!a.ticket || hipMemsetAsync(a.ticket, 0, sizeof(uint32_t), s) != hipSuccess) return;
+#endif
 #endif
     walk_kernel<NQE, 11, SEF, Q0><<<dim3(blocks), 64 * WALK_WPB, 0, s>>>(a);
 }
@@ -2089,7 +2077,9 @@ static int encoder_fwd_impl(const tm_weights *w, const float *n_feat, const floa
         if (!walk_layout_ok(P, nqe)) return fail(TM_E_UNSUPPORTED, "tm_encoder_fwd: weight layout mismatch");
         const int64_t n_slots = n_walks / M;
         const int64_t units = (n_slots + 15) / 16;
-        WalkArgs a{P, n_slots, W, M, B * W, n_feat, e_feat, node6, eid3, cat, ts3, cnt, stdv, cut, out_imp, etab};
+        // the unit counter of a dynamic persistent launch lives in the workspace's F region (unused by this path)
+        WalkArgs a{P, n_slots, W, M, B * W, n_feat, e_feat, node6, eid3, cat, ts3, cnt, stdv, cut, out_imp, etab,
+                   reinterpret_cast<uint32_t *>(F)};
         const unsigned blocks = (unsigned)((units + WALK_WPB - 1) / WALK_WPB);
         const int q0 = etab ? etab_q0(P) : 0;
         pe = prof_begin(s);

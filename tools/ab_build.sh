@@ -13,8 +13,9 @@ cp "$enc" "$out/encoder.hip"
 [ -n "$TRAIN" ] && cp "$TRAIN" "$out/encoder_train.hip"
 [ -n "$GM" ] && cp "$GM" "$out/graphmixer.hip"
 F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -mcode-object-version=5 -Wno-unused-result -Iinclude $EXTRA"
-for s in $(cd "$out" && ls *.cpp *.hip); do /opt/rocm/bin/hipcc $F -x hip -c "$out/$s" -o "$out/$s.o" & done
-wait
+pids=()
+for s in $(cd "$out" && ls *.cpp *.hip); do /opt/rocm/bin/hipcc $F -x hip -c "$out/$s" -o "$out/$s.o" & pids+=($!); done
+for p in "${pids[@]}"; do wait "$p" || { echo "compile failed"; rm -rf "$out"; exit 1; }; done
 /opt/rocm/bin/hipcc $F -shared -o "tempme_amd/lib/ab/$name.so" "$out"/*.o
 rm -rf "$out"; rmdir ab_src 2>/dev/null || true
 echo "built tempme_amd/lib/ab/$name.so"
