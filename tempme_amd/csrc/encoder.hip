@@ -551,50 +551,11 @@ struct WalkLay {
 // interleaved, so no MFMA waits on the one before it (v_mfma_f32_16x16x4_f32: 32-cycle issue, 40-cycle
 // dependent-accumulator latency); an odd last tile runs alone.  Each tile still accumulates its K steps
 // in the same order (the results do not change).
-#ifndef TM_PFP
-#define TM_PFP 4
-#endif
-constexpr int PFP = TM_PFP;
-// walk_kernel: node-feature rows loaded tile by tile inside event_gcn's first layer (1) or all before
-// lin_event's K loop (0); waves per SIMD the kernel is compiled for
-#ifndef TM_JIT_NODES
-#define TM_JIT_NODES 1
-#endif
-#ifndef TM_WALK_WAVES
-#define TM_WALK_WAVES 2
-#endif
-// waves per walk_kernel workgroup: each wave owns its 16 slots and a 12.25 KB LDS stash, the workgroup one
-// constant table; 3 waves per SIMD need one 12-wave workgroup per CU (three 4-wave ones exceed the LDS)
-// table mode: the next pass's edge-table row requested a pass ahead (1; 44 VGPRs live through the head) or
-// at the start of its own pass (0)
-#ifndef TM_ET_PREFETCH
-#define TM_ET_PREFETCH 1
-#endif
-#ifndef TM_WALK_WPB
-#define TM_WALK_WPB 4
-#endif
-// table mode: the next pass's edge-table row is requested inside event_gcn's K loop at this step (its
-// weights are requested a whole step ahead there, so the row's latency does not stall the weight ring
-// behind it); -1: after the position's encoding (before the folded GEMMs)
-#ifndef TM_ET_STEP
-#define TM_ET_STEP -1
-#endif
-// the next pass's scalars (and the head's inputs of a position-1 pass) are requested inside event_gcn's K
-// loop at this step instead of at the top of the pass, where lin_event's weight refills waited behind them
-#ifndef TM_POS_STEP
-#define TM_POS_STEP 0
-#endif
-// event_gcn's first node-row tiles are requested this many K steps before the end of lin_event's K loop (the
-// tiles' L2 latency then overlaps lin_event instead of opening event_gcn); 0: at event_gcn's start
-#ifndef TM_NODE_EARLY
-#define TM_NODE_EARLY 0
-#endif
-static_assert(TM_JIT_NODES || (TM_ET_STEP < 0 && TM_POS_STEP < 0), "in-G1 loads need the K-outer event_gcn loop");
-// lin_event's weight ring depth (fragments in flight; the first PFP come from the previous pass)
-#ifndef TM_LIN_D
-#define TM_LIN_D PFP
-#endif
-constexpr int WALK_WPB = TM_WALK_WPB;
+constexpr int PFP = 4;     // weight-fragment ring depth (2, 4, 6 measured: 4 best)
+// waves per SIMD walk_kernel is compiled for, and waves per workgroup (each wave owns its 16 slots and a
+// 12.25 KB LDS stash, the workgroup one constant table; 3 waves per SIMD and 8-wave workgroups measured slower)
+constexpr int WALK_WAVES = 2;
+constexpr int WALK_WPB = 4;
 // persistent walk_kernel waves: the grid is one round of resident workgroups looping over the units;
 // 1: static striding (wave w takes units w, w + stride, ...), 2: dynamic (each wave takes its next unit
 // from an atomic counter, requested at the start of its current unit)
@@ -876,19 +837,10 @@ __device__ __forceinline__ void load_ef(const WalkArgs &a, int32_t e, float (&ef
 // the polynomial in an exec-mask branch, which serialised it against the MFMAs) and the count / edge
 // lanes select their values.  Padding lanes (k >= kev) keep cos(0) = 1: lin_event's packed weights are
 // zero there.  In table mode the edge lanes are 0 (their product comes from the table row).
-// TM_ABL (A/B ablation builds only, outputs meaningless): bit 1 = time features without the cos (one fma),
-// bit 2 = every node-feature row read at node 0, bit 4 = every edge-table row read at edge 0
-#ifndef TM_ABL
-#define TM_ABL 0
-#endif
 template <bool ETAB, bool PURE>
 __device__ __forceinline__ float gen_one(int q, int s, float w, float ph, const float (&ef)[EQ_MAX][4], int g,
                                          int de, float dt, float c0, float c1, float c2) {
-#if TM_ABL & 1
-    float c = __builtin_fmaf(dt, w, ph);
-#else
     float c = time_cos(dt, w, ph);
-#endif
     if constexpr (PURE) return c;
     const int k = 16 * q + 4 * g + s;
     const int qe = q < EQ_MAX ? q : 0;
@@ -937,11 +889,7 @@ __device__ __forceinline__ float4 ef_step(const float4 *erow4, int q, int g, int
 template <int Q0>
 __device__ __forceinline__ void load_et(const WalkArgs &a, int32_t e, float4 (&et)[ETAB_N(Q0)]) {
     if constexpr (Q0 > 0) {
-#if TM_ABL & 4
-        const float4 *trow = reinterpret_cast<const float4 *>(a.etab) + 0 * e;
-#else
         const float4 *trow = reinterpret_cast<const float4 *>(a.etab + (int64_t)e * 176);
-#endif
         const int g = lane_id() >> 4;
 #pragma unroll
         for (int t = 0; t < 11; ++t) et[t] = trow[4 * t + g];
@@ -972,15 +920,8 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
     const int g = lane_id() >> 4;
     const int de = P.de, dn = P.dn, kev = P.kev;
     const float dt = pi.dt, c0 = pi.c0, c1 = pi.c1, c2 = pi.c2;
-#if TM_ABL & 2
-    const float4 *nrow_s = reinterpret_cast<const float4 *>(a.n_feat), *nrow_t = nrow_s;
-#else
     const float4 *nrow_s = reinterpret_cast<const float4 *>(a.n_feat + (int64_t)pi.ns * dn);
     const float4 *nrow_t = reinterpret_cast<const float4 *>(a.n_feat + (int64_t)pi.nt * dn);
-#endif
-#if !TM_JIT_NODES
-    float4 xs[NTD], xt[NTD];
-#endif
     floatx4 L[NTD];
     if constexpr (ETAB) {
 #pragma unroll
@@ -994,20 +935,7 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
 #pragma unroll
         for (int t = 0; t < NTD; ++t) L[t] = ldsx4(bias, t);
     }
-#if !TM_JIT_NODES
-#pragma unroll
-    for (int t = 0; t < NTD; ++t) {
-        const int f4 = (t < NTD - 1) ? 4 * t + g : min(4 * t + g, dn / 4 - 1);
-        xs[t] = nrow_s[f4];
-    }
-#pragma unroll
-    for (int t = 0; t < NTD; ++t) {
-        const int f4 = (t < NTD - 1) ? 4 * t + g : min(4 * t + g, dn / 4 - 1);
-        xt[t] = nrow_t[f4];
-    }
-#endif
     TM_STAMP(1);
-#if TM_JIT_NODES
     constexpr int JN = 3;                                // node tiles in flight in event_gcn's K loop
     float4 rs[JN], rt[JN];
     auto nload = [&](int q) {
@@ -1015,12 +943,10 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
         rs[q % JN] = nrow_s[f4];
         rt[q % JN] = nrow_t[f4];
     };
-    bool node_early = false;
-#endif
     {
         const int vo = lane_id() * 16;
         constexpr int nq = NQE;
-        constexpr int N = NTD * (NQE - Q0), D = (SEF ? PFP : TM_LIN_D);
+        constexpr int N = NTD * (NQE - Q0), D = PFP;
         static_assert(D >= PFP && D <= N, "lin_event ring depth");
         constexpr int EVF4 = LY::EV / 4;
         // the first D fragments (EVF4 + ((i % NTD) * nq + Q0 + i / NTD) * 64) come in pre, requested during
@@ -1078,13 +1004,6 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
                         p4 = lds4(cp, q + 1);
                     }
                     const float wq[4] = {w4.x, w4.y, w4.z, w4.w}, pq[4] = {p4.x, p4.y, p4.z, p4.w};
-#if TM_JIT_NODES
-                    if (TM_NODE_EARLY > 0 && q == NQE - TM_NODE_EARLY) {
-#pragma unroll
-                        for (int k = 0; k < JN - 1 && k < NTD; ++k) nload(k);
-                        node_early = true;
-                    }
-#endif
                     constexpr bool pure_next_ok = ETAB;   // table mode: steps >= Q0 + 2 hold only time features
                     floatx4 xn = xq;
                     auto gen = [&](int t) {
@@ -1145,7 +1064,6 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
         for (int k = 0; k < PFP; ++k) pre[k] = buf[(N + k) % D];
     }
     TM_STAMP(2);
-#if TM_JIT_NODES
     // event_gcn's first layer K-outer: K step q of A = x_s + relu(x_t + L), B = x_t + relu(x_s + L) (:93-96,
     // lin_event shared) is built from node-row tile q just before its MFMAs, the node tiles requested
     // JN - 1 steps ahead and the step's 4 weight fragments one step ahead (the two branches share them).
@@ -1160,10 +1078,8 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
     {
         const int vo = lane_id() * 16;
         float4 wq[2][4];
-        if (!node_early) {
 #pragma unroll
-            for (int q = 0; q < JN - 1 && q < NTD; ++q) nload(q);
-        }
+        for (int q = 0; q < JN - 1 && q < NTD; ++q) nload(q);
 #pragma unroll
         for (int t = 0; t < 4; ++t) wq[0][t] = pre[t];
 #pragma unroll
@@ -1205,34 +1121,6 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
     }
     TM_STAMP(3);
     TM_STAMP(4);
-#else
-    // A = x_s + relu(x_t + L), B = x_t + relu(x_s + L)   (event_gcn :93-96, lin_event shared)
-    floatx4 A[NTD], Bv[NTD];
-#pragma unroll
-    for (int t = 0; t < NTD; ++t) {
-        const float sv[4] = {xs[t].x, xs[t].y, xs[t].z, xs[t].w}, tv[4] = {xt[t].x, xt[t].y, xt[t].z, xt[t].w};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const float l = L[t][r];
-            A[t][r] = sv[r] + relu(tv[r] + l);
-            Bv[t][r] = tv[r] + relu(sv[r] + l);
-        }
-    }
-    TM_STAMP(3);
-    floatx4 Hs[4], Ht[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        Hs[t] = ldsx4(cs + C::G1, t);
-        Ht[t] = ldsx4(cs + C::G1C, t);
-    }
-    cgemm2<4, NTD, LY::G1>(wr, A, Bv, Hs, Ht);
-    {
-        const int vo = lane_id() * 16;
-#pragma unroll
-        for (int k = 0; k < PFP; ++k) pre[k] = wload(wr, vo, nx.o[k]);
-    }
-    TM_STAMP(4);
-#endif
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         H[t] = relu4(Hs[t]);
@@ -1335,7 +1223,7 @@ __device__ __forceinline__ float score_dot(const Stash &st, const floatx4 (&H)[8
 // so a unit's M walks run on M waves at once.  The slot pass is repeated by each of them (same values);
 // the chip is far from full at these sizes, and the latency of a call is one wave's pass chain.
 template <int NQE, int NTD, bool SEF = false, int QE0 = 0, bool SPLIT = false>
-__global__ void __launch_bounds__(64 * WALK_WPB, 4 * TM_WALK_WAVES / WALK_WPB) walk_kernel(WalkArgs a) {
+__global__ void __launch_bounds__(64 * WALK_WPB, 4 * WALK_WAVES / WALK_WPB) walk_kernel(WalkArgs a) {
     using C = WalkConsts<NQE, NTD>;
     const EncW &P = a.P;
     const int lane = threadIdx.x & 63, col = lane & 15;
@@ -1393,7 +1281,7 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * TM_WALK_WAVES / WALK_WPB) w
 #pragma unroll
     for (int k = 0; k < PFP; ++k) pre[k] = wload(wr, lane_id() * 16, lin0.o[k]);
     if constexpr (QE0 == 0) load_ef(a, cur.e, ef);
-    else if (TM_ET_PREFETCH) load_et<QE0>(a, cur.e, et);
+    else load_et<QE0>(a, cur.e, et);
 #ifdef TM_STAMPS
     const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) atomicMax(&g_st[2][9], atomicAdd(&g_live, 1ull) + 1);   // waves resident at once (max)
@@ -1427,31 +1315,22 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * TM_WALK_WAVES / WALK_WPB) w
         const int pn = !last ? ((pass & 1) == 0 ? 0 : 1) : 2;
         const int64_t gwn = !last ? eg * a.W + (int64_t)j * a.M + (SPLIT ? m0 : pass >> 1) : egn * a.W + (int64_t)jn * a.M;
         PosIn nxt;
-        if constexpr (TM_POS_STEP < 0) {
-            load_hi();
-            nxt = load_pos(a, gwn, pn, !last ? valid : vn);
-        }
-        // loads issued inside event_gcn's K loop (its weights are requested a whole step ahead)
+        // the next pass's scalars (and the head's inputs of a position-1 pass) are requested inside event_gcn's
+        // K loop at its first step (its weights are requested a whole step ahead there), not at the top of the
+        // pass where lin_event's weight refills waited behind them
         auto extra = [&](int q) {
-            if constexpr (TM_POS_STEP >= 0) {
-                if (q == TM_POS_STEP) {
-                    load_hi();
-                    nxt = load_pos(a, gwn, pn, !last ? valid : vn);
-                }
-            }
-            if constexpr (QE0 > 0 && TM_ET_STEP >= 0) {
-                static_assert(TM_ET_STEP > TM_POS_STEP, "the table row needs the next pass's edge id");
-                if (q == TM_ET_STEP) load_et<QE0>(a, nxt.e, et);   // the next pass's table row
+            if (q == 0) {
+                load_hi();
+                nxt = load_pos(a, gwn, pn, !last ? valid : vn);
             }
         };
         floatx4 H[8];
         unsigned long long T[10];
         TM_STAMP(0);
-        if constexpr (QE0 > 0 && !TM_ET_PREFETCH) load_et<QE0>(a, cur.e, et);
         encode_position<NQE, NTD, SEF, QE0>(a, wr, cs, cur, ef, et, extra, p, H, pre,
                                             pair_first<8>(p == 2 ? FoldLay::A1D / 4 : FoldLay::A1G / 4), T);
         if constexpr (QE0 == 0) load_ef(a, nxt.e, ef);
-        else if (TM_ET_PREFETCH && !(TM_JIT_NODES && TM_ET_STEP >= 0)) load_et<QE0>(a, nxt.e, et);
+        else load_et<QE0>(a, nxt.e, et);
         cur = nxt;
         TM_STAMP(6);
         if (p == 2) {
@@ -1656,9 +1535,7 @@ __global__ void __launch_bounds__(256) gate_reg_kernel(EncW P, int32_t n_ids, co
 // threads per (group, event) workgroup of explain_tab_kernel (its loops stride by blockDim.x): one wave
 // (256 -> 64: 0.136 -> 0.110 ms per 19,200 x 3 rows at the metric config; a workgroup is a short chain of
 // dependent loads and LDS atomics, so four times as many of them in flight per CU hide that latency)
-#ifndef TM_EXPLAIN_TPB
-#define TM_EXPLAIN_TPB 64
-#endif
+constexpr int EXPLAIN_TPB = 64;   // one wave per (group, event); 128 / 256 threads measured within noise / slower
 // retrieve_edge_imp_node with the gate table: per (group, event) the LDS hash keeps, per edge id,
 // the max graphlet importance of the walks through it; edge_imp = that max * gf(e), which equals
 // max_w(imp_w * gf(e)) bit for bit (rounding is monotone).
@@ -1960,7 +1837,7 @@ extern "C" int tm_edge_importance_tab(const float *gf, int32_t n_ids, int32_t n_
     while ((1 << hbits) < 2 * 3 * W) ++hbits;
     if (hbits > 14) return fail(TM_E_UNSUPPORTED, "tm_edge_importance_tab: too many walks per event");
     hipEvent_t pe = prof_begin(S_(stream));
-    explain_tab_kernel<<<dim3((unsigned)rows), TM_EXPLAIN_TPB, 2 * sizeof(int32_t) * (1u << hbits), S_(stream)>>>(
+    explain_tab_kernel<<<dim3((unsigned)rows), EXPLAIN_TPB, 2 * sizeof(int32_t) * (1u << hbits), S_(stream)>>>(
         W, N, hbits, n_ids, gf, eid3, imp, sub1_node, sub1_eid, sub2_node, sub2_eid, out_h1, out_h2, err_flag);
     TM_CHECK_LAUNCH();
     prof_end("explain_tab_kernel", S_(stream), pe);

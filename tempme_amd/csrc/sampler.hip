@@ -20,16 +20,9 @@
 
 namespace tmk {
 
-#ifndef TM_NT_STORES
-#define TM_NT_STORES 0
-#endif
-// TM_NT_STORES=1 streams the sampled outputs (non-temporal); measured slower (events_kernel 0.170 ->
-// 0.175 ms, and the k-hop kernel's in-row scattered outputs 2.4x slower), so plain stores by default
-#if TM_NT_STORES
-#define TM_ST(dst, v) __builtin_nontemporal_store((v), &(dst))
-#else
+// output stores are plain (write-back) stores: streamed non-temporal stores measured slower (events_kernel
+// 0.170 -> 0.175 ms, the k-hop kernel's in-row scattered outputs 2.4x slower)
 #define TM_ST(dst, v) ((dst) = (v))
-#endif
 
 constexpr int kMaxN = 64;   // n_degree supported by the sampling kernels (reference: 20..60)
 constexpr int kMaxM = 8;    // walks per hop-1 slot (reference: 3, null model 1)
