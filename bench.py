@@ -75,7 +75,7 @@ def self_launch(n):
 
 
 # ----------------------------------------------------------------------------------------------- models
-def flops_model(de, dn, h, N, M, etab=False):
+def flops_model(de, dn, h, N, M, etab=False, zn=False):
     """MACs x2 per unit for each encoder kernel.  ``walk_kernel``: the SURVEY.md §8(a) a12 model (3 walk
     positions + head), minus the 3 de x dn edge-feature MACs per walk that the edge table (``etab``) does once
     per edge id.  ``walk_kernel_executed``: what the kernel actually issues (folded form) --
@@ -83,7 +83,8 @@ def flops_model(de, dn, h, N, M, etab=False):
     product A1G (h x 2h) and the score dot (2h); per hop-1 slot (shared by its M walks): position 2's
     lin_event over the K steps below qt (the all-time-feature steps are a bias at dt = 0), event_gcn's
     first layer, the folded kv = G^T W1D (2h x 2h), A1D (h x 2h) and the u dot; per walk the head:
-    MLP.0 folded with attention.MLP.3 (h+12 x h), MLP.3 (h x h+12) and the last row (h)."""
+    MLP.0 folded with attention.MLP.3 (h+12 x h), MLP.3 (h x h+12) and the last row (h).  ``zn`` (zero node
+    features, tm_weights_set_node_zero): event_gcn's first layer runs on one branch (the two are bit-identical)."""
     kev = de + 3 + dn
     per_pos_gcn = kev * dn + 2 * (dn * h + h * h)                       # lin_event + event_gcn MLP x2
     per_walk_head = 3 * (2 * h) ** 2 + (2 * h) * h + h * h + (h + 12) ** 2 + (h + 12) * h + h + 2 * 2 * h
@@ -91,8 +92,9 @@ def flops_model(de, dn, h, N, M, etab=False):
     W = N * M
     qt = (de + 3 + 15) // 16
     edge = de * dn if etab else 0
-    pos = kev * dn - edge + 2 * dn * h
-    slot = kev * dn - max(kev - 16 * qt, 0) * dn - edge + 2 * dn * h + h * 2 * h + (2 * h) ** 2 + 2 * h
+    br = 1 if zn else 2
+    pos = kev * dn - edge + br * dn * h
+    slot = kev * dn - max(kev - 16 * qt, 0) * dn - edge + br * dn * h + h * 2 * h + (2 * h) ** 2 + 2 * h
     exec_walk = 2 * (2 * (pos + h * 2 * h + 2 * h) + slot / M + (h + 12) * h + h * (h + 12) + h)
     walk = 2 * (3 * per_pos_gcn + per_walk_head)
     if etab:
@@ -398,6 +400,8 @@ def main():
     ap.add_argument("--no-edge-table", action="store_true",
                     help="lin_event's edge-feature product per walk position instead of per edge id")
     ap.add_argument("--streams", type=int, default=1, help="steps in flight (PipelinedExplainer)")
+    ap.add_argument("--no-node-zero", action="store_true",
+                    help="do not specialise the walk kernel for an all-zero node-feature table (A/B)")
     ap.add_argument("--contrast", choices=("auto", "graphmixer", "none"), default="auto",
                     help="base-model contrast with the explanation (auto: GraphMixer for --config 4, as configs[4] "
                          "names it; none elsewhere: SURVEY §8(d) excludes the base contrast from the scoring unit)")
@@ -470,6 +474,7 @@ def main():
     torch.manual_seed(args.seed)
     ex = tm.TempME(Base(), "tgn", cfg["name"], out_dim=40, hid_dim=64, device=dev,
                    null_model={k: 1.0 / 12 for k in range(1, 13)}).to(dev).eval()
+    ex.node_zero_specialization = not args.no_node_zero
     S = max(1, args.streams)
     contrast = args.contrast if args.contrast != "auto" else ("graphmixer" if args.config == 4 else "none")
     gm = None
@@ -527,7 +532,8 @@ def main():
 
     if rank == 0:
         E = per_rank
-        fm = flops_model(g["e_feat"].shape[1], g["n_feat"].shape[1], 64, N, M, etab=pipe.etab is not None)
+        zn = bool(getattr(ex, "_node_zero", False)) and ex.node_zero_specialization and pipe.etab is not None
+        fm = flops_model(g["e_feat"].shape[1], g["n_feat"].shape[1], 64, N, M, etab=pipe.etab is not None, zn=zn)
         W = fm["W"]
         units = {"events_kernel": ("hbm", sampling_bytes_per_event(N, M) * E),
                  "gate_table_kernel": ("mfma", fm["gate_per_edge"] * (int(g["eidx"].max()) + 1)),
@@ -566,7 +572,8 @@ def main():
                           "metric (full Enron + TGN, n_degree=20)", "n_degree": N, "walks_per_slot": M,
                           "batch_size": B, "global_batches_per_step": per_rank * world // B,
                           "events_per_step_per_gpu": per_rank, "parallelism": f"dp{world} (whole batches per rank)",
-                          "steps_in_flight": S, "base_contrast": contrast},
+                          "steps_in_flight": S, "base_contrast": contrast,
+                          "walk_kernel_zero_node_features": zn},
                "roofline": roof, "kernels": kernels, "sampling_roofline": samp or None}
         if weak is not None:
             out["weak" if strong else "strong"] = weak

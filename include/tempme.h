@@ -169,6 +169,12 @@ int tm_weights_pack(tm_weights *w, const float *const *tensors, void *stream);
  * dependency_gate = 0 -> no dependency gate in retrieve_edge_imp_node (walk importance used as is).
  * Defaults 1, 1.  The training kernels support the defaults only. */
 int tm_weights_variant(tm_weights *w, int32_t temporal_guidance, int32_t dependency_gate);
+/* The node-feature table the caller passes to the eval encoder calls is all zeros (the TGN-format datasets
+ * Enron, UCI, Wikipedia, Reddit and USLegis ship zero node features).  event_gcn's two branches
+ * (explainer_new.py:93-96, src + relu(tgt + event) and tgt + relu(src + event)) are then the same expression of
+ * the event projection, bit for bit, and tm_encoder_fwd_tab computes one of them and reads no node row.  The
+ * caller re-asserts it whenever the table changes; 0 (the default) makes no assumption. */
+int tm_weights_set_node_zero(tm_weights *w, int32_t node_zero);
 int tm_weights_free(tm_weights *w);
 
 /* Workspace bytes tm_encoder_fwd needs for n_walks walks. */

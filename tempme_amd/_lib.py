@@ -35,7 +35,7 @@ EXPORTS = (
     "tm_last_error", "tm_version", "tm_graph_build", "tm_graph_build_edges", "tm_graph_free", "tm_graph_info", "tm_graph_export",
     "tm_graph_strict_view",
     "tm_sample_khop", "tm_sample_walks", "tm_neg_sample", "tm_perm_keys", "tm_motif_hist", "tm_edge_counts",
-    "tm_sample_events", "tm_gather_rows", "tm_weights_create", "tm_weights_create_ex", "tm_weights_pack", "tm_weights_variant", "tm_weights_free",
+    "tm_sample_events", "tm_gather_rows", "tm_weights_create", "tm_weights_create_ex", "tm_weights_pack", "tm_weights_variant", "tm_weights_set_node_zero", "tm_weights_free",
     "tm_encoder_workspace_bytes",
     "tm_encoder_fwd", "tm_encoder_fwd_tab", "tm_encoder_train_supported", "tm_encoder_train_fwd", "tm_encoder_bwd", "tm_encoder_wgrad", "tm_wgrad",
     "tm_explain_train_fwd", "tm_explain_train_fwd_pad", "tm_explain_train_bwd", "tm_kl_loss", "tm_edge_importance", "tm_edge_gate_table",
@@ -129,6 +129,7 @@ def _sig(L):
     L.tm_weights_create_ex.argtypes = [i32, i32, i32, i32, C.c_int, C.POINTER(vp)]
     L.tm_weights_pack.argtypes = [vp, C.POINTER(vp), vp]
     L.tm_weights_variant.argtypes = [vp, i32, i32]
+    L.tm_weights_set_node_zero.argtypes = [vp, i32]
     L.tm_weights_free.argtypes = [vp]
     L.tm_encoder_workspace_bytes.restype = i64
     L.tm_encoder_workspace_bytes.argtypes = [vp, i64]

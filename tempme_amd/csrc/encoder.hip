@@ -907,7 +907,7 @@ __device__ __forceinline__ void load_et(const WalkArgs &a, int32_t e, float4 (&e
 // zero for those inputs, so they contribute nothing.
 // SEF (streamed edge features, EQ_MAX*16 < de <= 176): ef holds K steps 0 and 1 (loaded during the
 // previous pass); step q + 2's float4 is loaded while step q's MFMAs run.
-template <int NQE, int NTD, bool SEF, int Q0, class Extra>
+template <int NQE, int NTD, bool SEF, int Q0, bool ZN, class Extra>
 __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buffer_rsrc_t wr, const float *cs,
                                                 const PosIn &pi, const float (&ef)[EQ_MAX][4],
                                                 float4 (&et)[ETAB_N(Q0)], Extra &&extra, int p, floatx4 (&H)[8],
@@ -1069,22 +1069,26 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
     // JN - 1 steps ahead and the step's 4 weight fragments one step ahead (the two branches share them).
     // The node rows are never all live at once (and not during lin_event's K loop).  Each output tile
     // accumulates its K steps in the same order as cgemm2 (same results).
+    // ZN (every node-feature row zero, tm_weights_set_node_zero): A and B are the same expression of L,
+    // 0 + relu(0 + L), so both branches are bit-identical: one branch is computed (and no node row read)
     floatx4 Hs[4], Ht[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         Hs[t] = ldsx4(cs + C::G1, t);
-        Ht[t] = ldsx4(cs + C::G1C, t);
+        if constexpr (!ZN) Ht[t] = ldsx4(cs + C::G1C, t);
     }
     {
         const int vo = lane_id() * 16;
         float4 wq[2][4];
+        if constexpr (!ZN) {
 #pragma unroll
-        for (int q = 0; q < JN - 1 && q < NTD; ++q) nload(q);
+            for (int q = 0; q < JN - 1 && q < NTD; ++q) nload(q);
+        }
 #pragma unroll
         for (int t = 0; t < 4; ++t) wq[0][t] = pre[t];
 #pragma unroll
         for (int q = 0; q < NTD; ++q) {
-            if (q + JN - 1 < NTD) nload(q + JN - 1);
+            if (!ZN && q + JN - 1 < NTD) nload(q + JN - 1);
             if (q + 1 < NTD) {
 #pragma unroll
                 for (int t = 0; t < 4; ++t) wq[(q + 1) & 1][t] = wload(wr, vo, LY::G1 / 4 + (t * NTD + q + 1) * 64);
@@ -1093,6 +1097,23 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
                 for (int t = 0; t < 4; ++t) wq[(q + 1) & 1][t] = wload(wr, vo, nx.o[t]);
             }
             extra(q);                                    // the caller's loads placed at step q
+            if constexpr (ZN) {
+                floatx4 A;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) A[r] = 0.f + relu(0.f + L[q][r]);
+                // the 4 tiles' chains interleaved (no MFMA waits on its predecessor); each tile accumulates
+                // its k values in the same order as below
+#pragma unroll
+                for (int t = 0; t < 4; ++t) Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[q & 1][t].x, A.x, Hs[t], 0, 0, 0);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[q & 1][t].y, A.y, Hs[t], 0, 0, 0);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[q & 1][t].z, A.z, Hs[t], 0, 0, 0);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[q & 1][t].w, A.w, Hs[t], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                continue;
+            }
             const float4 xs4 = rs[q % JN], xt4 = rt[q % JN];
             const float sv[4] = {xs4.x, xs4.y, xs4.z, xs4.w}, tv[4] = {xt4.x, xt4.y, xt4.z, xt4.w};
             floatx4 A, Bq;
@@ -1124,7 +1145,7 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         H[t] = relu4(Hs[t]);
-        H[4 + t] = relu4(Ht[t]);
+        H[4 + t] = ZN ? H[t] : relu4(Ht[t]);
     }
     TM_STAMP(5);
 }
@@ -1222,7 +1243,7 @@ __device__ __forceinline__ float score_dot(const Stash &st, const floatx4 (&H)[8
 // its unit's 16 slots -- the slot pass, then that walk's positions 0 and 1 (3 passes instead of 1 + 2M) --
 // so a unit's M walks run on M waves at once.  The slot pass is repeated by each of them (same values);
 // the chip is far from full at these sizes, and the latency of a call is one wave's pass chain.
-template <int NQE, int NTD, bool SEF = false, int QE0 = 0, bool SPLIT = false>
+template <int NQE, int NTD, bool SEF = false, int QE0 = 0, bool SPLIT = false, bool ZN = false>
 __global__ void __launch_bounds__(64 * WALK_WPB, 4 * WALK_WAVES / WALK_WPB) walk_kernel(WalkArgs a) {
     using C = WalkConsts<NQE, NTD>;
     const EncW &P = a.P;
@@ -1327,7 +1348,7 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * WALK_WAVES / WALK_WPB) walk
         floatx4 H[8];
         unsigned long long T[10];
         TM_STAMP(0);
-        encode_position<NQE, NTD, SEF, QE0>(a, wr, cs, cur, ef, et, extra, p, H, pre,
+        encode_position<NQE, NTD, SEF, QE0, ZN>(a, wr, cs, cur, ef, et, extra, p, H, pre,
                                             pair_first<8>(p == 2 ? FoldLay::A1D / 4 : FoldLay::A1G / 4), T);
         if constexpr (QE0 == 0) load_ef(a, nxt.e, ef);
         else load_et<QE0>(a, nxt.e, et);
@@ -1721,6 +1742,12 @@ extern "C" int tm_weights_create_ex(int32_t de, int32_t dn, int32_t h, int32_t i
     return TM_OK;
 }
 
+extern "C" int tm_weights_set_node_zero(tm_weights *w, int32_t node_zero) {
+    if (!w) return fail(TM_E_ARG, "tm_weights_set_node_zero: NULL weights");
+    w->node_zero = node_zero ? 1 : 0;
+    return TM_OK;
+}
+
 extern "C" int tm_weights_variant(tm_weights *w, int32_t temporal_guidance, int32_t dependency_gate) {
     if (!w) return fail(TM_E_ARG, "tm_weights_variant: NULL weights");
     w->P.tg = temporal_guidance ? 1 : 0;
@@ -1867,12 +1894,12 @@ static void launch_head(const EncW &P, int64_t n_walks, int64_t walks_per_group,
 // waves either way (1024 SIMDs x 2 waves), so the call's latency is the shorter pass chain
 constexpr int64_t WALK_SPLIT_UNITS = 512;
 
-template <int NQE, bool SEF = false, int Q0 = 0>
+template <int NQE, bool SEF = false, int Q0 = 0, bool ZN = false>
 static void launch_walk(const WalkArgs &a, unsigned blocks, hipStream_t s) {
     const int64_t units = (a.n_slots + 15) / 16;
     if (!TM_WALK_PERSIST && units * a.M <= 3 * WALK_SPLIT_UNITS && units < WALK_SPLIT_UNITS) {
         const unsigned sb = (unsigned)((units * a.M + WALK_WPB - 1) / WALK_WPB);
-        walk_kernel<NQE, 11, SEF, Q0, true><<<dim3(sb), 64 * WALK_WPB, 0, s>>>(a);
+        walk_kernel<NQE, 11, SEF, Q0, true, ZN><<<dim3(sb), 64 * WALK_WPB, 0, s>>>(a);
         return;
     }
 #if TM_WALK_PERSIST
@@ -1882,7 +1909,7 @@ static void launch_walk(const WalkArgs &a, unsigned blocks, hipStream_t s) {
     if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
         if (cap[dev] == 0) {
             int per_cu = 0, cus = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, walk_kernel<NQE, 11, SEF, Q0>, 64 * WALK_WPB, 0) ==
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, walk_kernel<NQE, 11, SEF, Q0, false, ZN>, 64 * WALK_WPB, 0) ==
                     hipSuccess &&
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && per_cu > 0 &&
                 cus > 0)
@@ -1896,7 +1923,7 @@ static void launch_walk(const WalkArgs &a, unsigned blocks, hipStream_t s) {
     if (!a.ticket || hipMemsetAsync(a.ticket, 0, sizeof(uint32_t), s) != hipSuccess) return;
 #endif
 #endif
-    walk_kernel<NQE, 11, SEF, Q0><<<dim3(blocks), 64 * WALK_WPB, 0, s>>>(a);
+    walk_kernel<NQE, 11, SEF, Q0, false, ZN><<<dim3(blocks), 64 * WALK_WPB, 0, s>>>(a);
 }
 
 extern "C" int tm_encoder_fwd(const tm_weights *w, const float *n_feat, const float *e_feat, int32_t n_groups,
@@ -1960,7 +1987,12 @@ static int encoder_fwd_impl(const tm_weights *w, const float *n_feat, const floa
         const unsigned blocks = (unsigned)((units + WALK_WPB - 1) / WALK_WPB);
         const int q0 = etab ? etab_q0(P) : 0;
         pe = prof_begin(s);
-        if (q0 == 2) {        // edge table: lin_event from K step 2
+        if (q0 == 2 && w->node_zero) {   // edge table, zero node features: one event_gcn branch (ZN)
+            if (nqe == 11) launch_walk<11, false, 2, true>(a, blocks, s);
+            else if (nqe == 12) launch_walk<12, false, 2, true>(a, blocks, s);
+            else if (nqe == 13) launch_walk<13, false, 2, true>(a, blocks, s);
+            else launch_walk<14, false, 2, true>(a, blocks, s);
+        } else if (q0 == 2) {        // edge table: lin_event from K step 2
             if (nqe == 11) launch_walk<11, false, 2>(a, blocks, s);
             else if (nqe == 12) launch_walk<12, false, 2>(a, blocks, s);
             else if (nqe == 13) launch_walk<13, false, 2>(a, blocks, s);

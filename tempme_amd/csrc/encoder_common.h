@@ -262,6 +262,9 @@ struct tm_weights {
     float *buf;
     size_t n_floats;
     EncW P;
+    // the caller's node-feature table is all zeros (tm_weights_set_node_zero): the fused eval kernel computes
+    // one event_gcn branch, the other being bit-identical
+    int node_zero = 0;
     // per linear: raw tensor index, nout, k
     struct Spec {
         Lin *lin;

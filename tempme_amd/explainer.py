@@ -383,6 +383,8 @@ class TempME(nn.Module):
                 self._packed = _Packed(h)
                 L.check(L.lib().tm_weights_variant(h, int(bool(self.use_temporal_guidance)),
                                                    int(bool(self.use_dependency_aware_sampling))), "tm_weights_variant")
+                self.feature_tables()
+                self._set_node_zero(h)
             self._raw = [w.detach().to(device=dev, dtype=torch.float32).contiguous() for w in ws]
             arr = (L.C.c_void_p * L.N_WEIGHTS)(*[w.data_ptr() for w in self._raw])
             L.check(L.lib().tm_weights_pack(self._packed.h, arr, L.stream_ptr(dev)), "tm_weights_pack")
@@ -392,13 +394,23 @@ class TempME(nn.Module):
 
     def feature_tables(self):
         dev = self._dev()
-        key = (self.node_raw_embed.weight.data_ptr(), self.edge_raw_embed.weight.data_ptr())
+        nw, ew = self.node_raw_embed.weight, self.edge_raw_embed.weight
+        key = (nw.data_ptr(), nw._version, ew.data_ptr(), ew._version)
         if getattr(self, "_tables_key", None) != key:
-            self._n_tab = self.node_raw_embed.weight.detach().to(device=dev, dtype=torch.float32).contiguous()
-            self._e_tab = self.edge_raw_embed.weight.detach().to(device=dev, dtype=torch.float32).contiguous()
+            self._n_tab = nw.detach().to(device=dev, dtype=torch.float32).contiguous()
+            self._e_tab = ew.detach().to(device=dev, dtype=torch.float32).contiguous()
+            # every node-feature bit zero (the TGN-format datasets): the eval encoder computes one event_gcn
+            # branch, the other being bit-identical (tm_weights_set_node_zero); one device reduction per table
+            self._node_zero = bool((self._n_tab.view(torch.int32) == 0).all().item())
             self._tables_key = key
             self._prep_dirty = self._prep_dirty_fast = True   # side streams must wait for this work
+            if getattr(self, "_packed", None) is not None:
+                self._set_node_zero(self._packed.h)
         return self._n_tab, self._e_tab
+
+    def _set_node_zero(self, h):
+        zero = bool(getattr(self, "_node_zero", False)) and getattr(self, "node_zero_specialization", True)
+        L.check(L.lib().tm_weights_set_node_zero(h, int(zero)), "tm_weights_set_node_zero")
 
     def dropin_edge_table(self, w=None):
         """The drop-in forward's table mode: lin_event's edge-feature product W[:, :de] E(e) for every row of
