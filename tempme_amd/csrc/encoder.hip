@@ -709,7 +709,7 @@ struct WalkConsts {
                          C0 = M3B + 1, SIZE = M3B + 4;
 };
 
-template <int NQE, int NTD>
+template <int NQE, int NTD, bool ZN = false>
 __device__ __forceinline__ void load_consts(const EncW &P, float *cs) {
     using C = WalkConsts<NQE, NTD>;
     for (int i = threadIdx.x; i < C::SIZE; i += blockDim.x) {
@@ -722,9 +722,9 @@ __device__ __forceinline__ void load_consts(const EncW &P, float *cs) {
         else if (i < C::G1) v = P.devc[i - C::DEVC];
         else if (i < C::G1C) v = P.g1.b[i - C::G1];
         else if (i < C::V0) v = P.g1.b[i - C::G1C];
-        else if (i < C::CP) v = P.v0[i - C::V0];
+        else if (i < C::CP) v = ZN ? (i - C::V0 < HID ? P.v0z[i - C::V0] : 0.f) : P.v0[i - C::V0];
         else if (i < C::U) v = P.cp[i - C::CP];
-        else if (i < C::M2) v = P.u[i - C::U];
+        else if (i < C::M2) v = ZN ? (i - C::U < HID ? P.uz[i - C::U] : 0.f) : P.u[i - C::U];
         else if (i < C::M3) v = P.m2.b[i - C::M2];
         else if (i < C::TC) v = P.m3w[i - C::M3];
         else if (i < C::M3B) v = P.tc[i - C::TC];
@@ -1226,12 +1226,13 @@ __device__ __forceinline__ void walk_head(const WalkArgs &a, __amdgpu_buffer_rsr
     if (valid && g == 0) a.out[gw] = 1.f / (1.f + expf(-z));
 }
 
-// this column's V . H (the 4 lane groups' parts summed)
+// this column's V . H (the 4 lane groups' parts summed); ZN: VZ . U over the first 4 tiles
+template <bool ZN = false>
 __device__ __forceinline__ float score_dot(const Stash &st, const floatx4 (&H)[8]) {
     const int lane = threadIdx.x & 63;
     float s = 0.f;
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
+    for (int t = 0; t < (ZN ? 4 : 8); ++t) {
         const floatx4 v = st.V[t][lane];
 #pragma unroll
         for (int r = 0; r < 4; ++r) s = __builtin_fmaf(v[r], H[t][r], s);
@@ -1282,7 +1283,7 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * WALK_WAVES / WALK_WPB) walk
     __shared__ Stash stash[WALK_WPB];
     __shared__ float4 cs4[(C::SIZE + 3) / 4];
     float *cs = reinterpret_cast<float *>(cs4);
-    load_consts<NQE, NTD>(P, cs);
+    load_consts<NQE, NTD, ZN>(P, cs);
     __syncthreads();
     if (unit >= n_units) return;                        // whole wave idle (wave-uniform)
     Stash &st = stash[threadIdx.x >> 6];
@@ -1349,12 +1350,41 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * WALK_WAVES / WALK_WPB) walk
         unsigned long long T[10];
         TM_STAMP(0);
         encode_position<NQE, NTD, SEF, QE0, ZN>(a, wr, cs, cur, ef, et, extra, p, H, pre,
-                                            pair_first<8>(p == 2 ? FoldLay::A1D / 4 : FoldLay::A1G / 4), T);
+                                            ZN ? pair_first<4>(p == 2 ? FoldLay::A1DZ / 4 : FoldLay::A1GZ / 4)
+                                               : pair_first<8>(p == 2 ? FoldLay::A1D / 4 : FoldLay::A1G / 4), T);
         if constexpr (QE0 == 0) load_ef(a, nxt.e, ef);
         else load_et<QE0>(a, nxt.e, et);
         cur = nxt;
         TM_STAMP(6);
-        if (p == 2) {
+        // ZN: H = [U; U]: the layers reading H as their 64-column-folded forms on U (FoldLay KVZ ...)
+        floatx4 Uv[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) Uv[t] = H[t];
+        if (ZN && p == 2) {
+            floatx4 P2[4], V[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) P2[t] = ldsx4(cs + C::CP, t);
+            cgemm_p<4, 4, 4, FoldLay::A1DZ>(wr, Uv, P2, pre, pair_first<4>(FoldLay::KVZ / 4));
+#pragma unroll
+            for (int t = 0; t < 4; ++t) V[t] = ldsx4(cs + C::V0, t);
+            cgemm_p<4, 4, 4, FoldLay::KVZ>(wr, Uv, V, pre, lin0);
+            TM_STAMP(7);
+            float cw = 0.f;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float4 b = lds4(cs + C::U, t);
+                cw = __builtin_fmaf(Uv[t][0], b.x, cw);
+                cw = __builtin_fmaf(Uv[t][1], b.y, cw);
+                cw = __builtin_fmaf(Uv[t][2], b.z, cw);
+                cw = __builtin_fmaf(Uv[t][3], b.w, cw);
+            }
+            cw = col_sum(cw) + cs[C::C0];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) st.V[t][lane] = V[t];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) st.P2[t][lane] = P2[t];
+            st.cw[lane] = cw;
+        } else if (p == 2) {
             // P2 = A1D H_2 + cp; V = kv H_2 + v0 (= G^T Wp); cw = u . H_2 + c0 (= Wp . beta)
             floatx4 P2[4];
 #pragma unroll
@@ -1385,8 +1415,9 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * WALK_WAVES / WALK_WPB) walk
             floatx4 R[4];
 #pragma unroll
             for (int t = 0; t < 4; ++t) R[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-            cgemm_p<4, 8, 8, FoldLay::A1G>(wr, H, R, pre, p == 1 ? pair_first<4>(FoldLay::M1A2 / 4) : lin0);
-            const float s = score_dot(st, H);
+            if constexpr (ZN) cgemm_p<4, 4, 4, FoldLay::A1GZ>(wr, Uv, R, pre, p == 1 ? pair_first<4>(FoldLay::M1A2 / 4) : lin0);
+            else cgemm_p<4, 8, 8, FoldLay::A1G>(wr, H, R, pre, p == 1 ? pair_first<4>(FoldLay::M1A2 / 4) : lin0);
+            const float s = score_dot<ZN>(st, H);
             TM_STAMP(7);
             if (p == 0) {
 #pragma unroll
@@ -1428,7 +1459,8 @@ static bool walk_layout_ok(const EncW &P, int nqe) {
                                                                      2 * (8 * 8 * 256 + 128) + 4 * 8 * 256 + 64 +
                                                                      4 * 4 * 256 + 64 + 5 * 5 * 256 + 80;
     return at(P.ev.w, ev) && at(P.g1.w, g1) && at(P.m2.w, m2) && at(P.a1d.w, FoldLay::A1D) &&
-           at(P.a1g.w, FoldLay::A1G) && at(P.m1a2.w, FoldLay::M1A2) && P.g1.nt == 4 && P.g1.nq == 11 && P.m2.nt == 4 && P.m2.nq == 5 && P.ev.nt == 11 && P.ev.nq == nqe;
+           at(P.a1g.w, FoldLay::A1G) && at(P.m1a2.w, FoldLay::M1A2) && at(P.kvz.w, FoldLay::KVZ) &&
+           at(P.a1dz.w, FoldLay::A1DZ) && at(P.a1gz.w, FoldLay::A1GZ) && P.g1.nt == 4 && P.g1.nq == 11 && P.m2.nt == 4 && P.m2.nq == 5 && P.ev.nt == 11 && P.ev.nq == nqe;
 }
 
 // ------------------------------------------------------------------ per-edge dependency gate table
@@ -1710,7 +1742,9 @@ extern "C" int tm_weights_create_ex(int32_t de, int32_t dn, int32_t h, int32_t i
         struct FL {
             Lin *lin;
             int off, nout, k;
-        } fl[] = {{&P.kv, F::KV, h2, h2}, {&P.a1d, F::A1D, h, h2}, {&P.a1g, F::A1G, h, h2}, {&P.m1a2, F::M1A2, hm, h}};
+        } fl[] = {{&P.kv, F::KV, h2, h2},     {&P.a1d, F::A1D, h, h2},   {&P.a1g, F::A1G, h, h2},
+                  {&P.m1a2, F::M1A2, hm, h},  {&P.kvz, F::KVZ, h, h},    {&P.a1dz, F::A1DZ, h, h},
+                  {&P.a1gz, F::A1GZ, h, h}};
         for (auto &f : fl) {
             f.lin->w = reinterpret_cast<const float4 *>(w->buf + f.off);
             f.lin->b = nullptr;
@@ -1724,6 +1758,8 @@ extern "C" int tm_weights_create_ex(int32_t de, int32_t dn, int32_t h, int32_t i
         P.c0 = w->buf + F::C0;
         P.cp = w->buf + F::CP;
         P.tc = w->buf + F::TC;
+        P.v0z = w->buf + F::V0Z;
+        P.uz = w->buf + F::UZ;
         (void)hipGetDevice(&prev);
         const bool ok = hipSetDevice(device) == hipSuccess &&
                         hipMalloc(&w->fold64, sizeof(double) * F::S64_SIZE) == hipSuccess &&

@@ -41,6 +41,9 @@ struct EncW {
     // M1A2 = MLP.0[:, :h] a2, tc[c] = MLP.0[:, h + c] + bm1 + MLP.0[:, :h] ba2 (row 12: no category).
     Lin kv, a1d, a1g, m1a2;
     const float *v0, *u, *c0, *cp, *tc;
+    // zero node features (tm_weights_set_node_zero; FoldLay KVZ ...): the same layers on U = H[:64] = H[64:]
+    Lin kvz, a1dz, a1gz;
+    const float *v0z, *uz;
     // constructor variants (explainer_new.py:103-105, :121, :141): tg = use_temporal_guidance (0: the plain
     // Attention, no time weighting of the scores), dep = use_dependency_aware_sampling (0: no gate)
     int tg = 1, dep = 1;
@@ -137,10 +140,15 @@ __device__ __forceinline__ float gate_logit_lds(const float *g2, const float *w3
 struct FoldLay {
     static constexpr int KV = 0, V0 = KV + 8 * 8 * 256, U = V0 + 128, C0 = U + 128, A1D = C0 + 4, CP = A1D + 4 * 8 * 256,
                          A1G = CP + 64, M1A2 = A1G + 4 * 8 * 256, TC = M1A2 + 5 * 4 * 256,
-                         SIZE = (TC + 13 * 80 + 63) & ~63;
+                         // the zero-node-feature forms (H_s = H_t = U, so H = [U; U] and every layer reading H
+                         // takes the sum of its two column halves; kv and v0 also sum their two row halves, the
+                         // score V . H_i becoming VZ . U_i with VZ = V[:64] + V[64:])
+                         KVZ = (TC + 13 * 80 + 63) & ~63, A1DZ = KVZ + 4 * 4 * 256, A1GZ = A1DZ + 4 * 4 * 256,
+                         V0Z = A1GZ + 4 * 4 * 256, UZ = V0Z + 64, SIZE = (UZ + 64 + 63) & ~63;
     // fold32 scratch (row-major fp32 matrices before packing)
     static constexpr int S_KV = 0, S_A1D = S_KV + 128 * 128, S_A1G = S_A1D + 64 * 128, S_M1A2 = S_A1G + 64 * 128,
-                         S_SIZE = S_M1A2 + 76 * 64;
+                         S_KVZ = S_M1A2 + 76 * 64, S_A1DZ = S_KVZ + 64 * 64, S_A1GZ = S_A1DZ + 64 * 64,
+                         S_SIZE = S_A1GZ + 64 * 64;
     // fold64 scratch (stage 1): a1 W2, a1 b2, W1D = W1 blockdiag(g2,g2), G = W2 blockdiag(g2,g2), b1d, beta
     static constexpr int S64_A1W2 = 0, S64_A1B2 = S64_A1W2 + 64 * 128, S64_W1D = S64_A1B2 + 64,
                          S64_G = S64_W1D + 128 * 128, S64_B1D = S64_G + 128 * 128, S64_BETA = S64_B1D + 128,

@@ -142,7 +142,7 @@ __global__ void __launch_bounds__(256) fold1_kernel(FoldIn F, double *__restrict
 }
 
 // stage 2: the packed matrices (fp32 row-major into s32, packed afterwards) and the vectors (into buf)
-constexpr int FOLD2_N = 128 * 128 + 2 * 64 * 128 + 76 * 64 + 128 + 128 + 1 + 64 + 13 * 80;
+constexpr int FOLD2_N = 128 * 128 + 2 * 64 * 128 + 76 * 64 + 128 + 128 + 1 + 64 + 13 * 80 + 3 * 64 * 64 + 64 + 64;
 __global__ void __launch_bounds__(256) fold2_kernel(FoldIn F, const double *__restrict__ s64, float *__restrict__ s32,
                                                     float *__restrict__ buf) {
     using L = FoldLay;
@@ -214,6 +214,45 @@ __global__ void __launch_bounds__(256) fold2_kernel(FoldIn F, const double *__re
             v = (float)acc;
         }
         buf[L::TC + i] = v;
+        return;
+    }
+    i -= 13 * 80;
+    // zero-node-feature forms: U = H[:64] = H[64:], so a layer X reading H is X[:, :64] + X[:, 64:] on U;
+    // kv and v0 also fold their row halves (the score V . H = (V[:64] + V[64:]) . U).  fp64 sums, one rounding
+    if (i < 64 * 64) {                                   // KVZ = (G[:, o] + G[:, o+64])^T (W1D[:, k] + W1D[:, k+64])
+        const int o = i / 64, k = i % 64;
+        double acc = 0.0;
+        for (int j = 0; j < 128; ++j)
+            acc += (G[j * 128 + o] + G[j * 128 + o + 64]) * (W1D[j * 128 + k] + W1D[j * 128 + k + 64]);
+        s32[L::S_KVZ + i] = (float)acc;
+        return;
+    }
+    i -= 64 * 64;
+    if (i < 64 * 64) {                                   // A1DZ = A1D[:, :64] + A1D[:, 64:]
+        const int o = i / 64, k = i % 64;
+        const auto row = [&](int j) { return F.a1[o * 128 + j]; };
+        s32[L::S_A1DZ + i] = (float)(fold_bd(F, row, k) + fold_bd(F, row, k + 64));
+        return;
+    }
+    i -= 64 * 64;
+    if (i < 64 * 64) {                                   // A1GZ = A1G[:, :64] + A1G[:, 64:]
+        const int o = i / 64, k = i % 64;
+        const auto row = [&](int j) { return s64[L::S64_A1W2 + o * 128 + j]; };
+        s32[L::S_A1GZ + i] = (float)(fold_bd(F, row, k) + fold_bd(F, row, k + 64));
+        return;
+    }
+    i -= 64 * 64;
+    if (i < 64) {                                        // v0z = v0[:64] + v0[64:]
+        double acc = 0.0;
+        for (int j = 0; j < 128; ++j) acc += (G[j * 128 + i] + G[j * 128 + i + 64]) * b1d[j];
+        buf[L::V0Z + i] = (float)acc;
+        return;
+    }
+    i -= 64;
+    if (i < 64) {                                        // uz = u[:64] + u[64:]
+        double acc = 0.0;
+        for (int j = 0; j < 128; ++j) acc += (W1D[j * 128 + i] + W1D[j * 128 + i + 64]) * beta[j];
+        buf[L::UZ + i] = (float)acc;
     }
 }
 
@@ -1496,6 +1535,9 @@ void pack_all_weights(tm_weights *w, const float *const *t, hipStream_t s) {
         frag(w->P.a1d, w->fold32 + L::S_A1D, h2, 1);
         frag(w->P.a1g, w->fold32 + L::S_A1G, h2, 1);
         frag(w->P.m1a2, w->fold32 + L::S_M1A2, h, 1);
+        frag(w->P.kvz, w->fold32 + L::S_KVZ, h, 1);
+        frag(w->P.a1dz, w->fold32 + L::S_A1DZ, h, 1);
+        frag(w->P.a1gz, w->fold32 + L::S_A1GZ, h, 1);
     }
     P.total = total;
     pack_jobs_kernel<<<dim3((unsigned)std::min<int64_t>((total + 255) / 256, 1024)), 256, 0, s>>>(P);

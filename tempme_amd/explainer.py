@@ -410,7 +410,9 @@ class TempME(nn.Module):
 
     def _set_node_zero(self, h):
         zero = bool(getattr(self, "_node_zero", False)) and getattr(self, "node_zero_specialization", True)
-        L.check(L.lib().tm_weights_set_node_zero(h, int(zero)), "tm_weights_set_node_zero")
+        fn = getattr(L.lib(), "tm_weights_set_node_zero", None)    # absent in an older A/B build (TEMPME_LIB)
+        if fn is not None:
+            L.check(fn(h, int(zero)), "tm_weights_set_node_zero")
 
     def dropin_edge_table(self, w=None):
         """The drop-in forward's table mode: lin_event's edge-feature product W[:, :de] E(e) for every row of

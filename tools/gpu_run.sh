@@ -89,7 +89,7 @@ for s in "$@"; do
         wab) step wab 1200 ./tools/walk_ab.sh ;;
         wabx) WAB_EXTRAS=" " step wab 1200 ./tools/walk_ab.sh ;;
         sab) step sab 1200 ./tools/streams_ab2.sh ;;
-        k:*) step pytest_k 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread -k "${s#k:}" ;;
+        k:*) kn=$(echo "${s#k:}" | tr -c 'A-Za-z0-9_\n' '_'); step "pytest_k_$kn" 600 python -u -m pytest tests -x -v -m gpu -rfEs --timeout 300 --timeout-method thread -k "${s#k:}" ;;
         micro:*) m=${s#micro:}; step micro_$m 200 ./micro/$m ;;   # a prebuilt micro-benchmark binary
         *) echo "unknown step $s"; exit 2 ;;
     esac
