@@ -84,7 +84,8 @@ def flops_model(de, dn, h, N, M, etab=False, zn=False):
     lin_event over the K steps below qt (the all-time-feature steps are a bias at dt = 0), event_gcn's
     first layer, the folded kv = G^T W1D (2h x 2h), A1D (h x 2h) and the u dot; per walk the head:
     MLP.0 folded with attention.MLP.3 (h+12 x h), MLP.3 (h x h+12) and the last row (h).  ``zn`` (zero node
-    features, tm_weights_set_node_zero): event_gcn's first layer runs on one branch (the two are bit-identical)."""
+    features, tm_weights_set_node_zero): event_gcn's first layer runs on one branch (the two are bit-identical)
+    and the layers reading both branches (A1D, kv, u, A1G, the score dot) on their column-folded forms."""
     kev = de + 3 + dn
     per_pos_gcn = kev * dn + 2 * (dn * h + h * h)                       # lin_event + event_gcn MLP x2
     per_walk_head = 3 * (2 * h) ** 2 + (2 * h) * h + h * h + (h + 12) ** 2 + (h + 12) * h + h + 2 * 2 * h
@@ -92,10 +93,10 @@ def flops_model(de, dn, h, N, M, etab=False, zn=False):
     W = N * M
     qt = (de + 3 + 15) // 16
     edge = de * dn if etab else 0
-    br = 1 if zn else 2
+    br = 1 if zn else 2           # event_gcn branches computed; the layers reading H take br * h inputs
     pos = kev * dn - edge + br * dn * h
-    slot = kev * dn - max(kev - 16 * qt, 0) * dn - edge + br * dn * h + h * 2 * h + (2 * h) ** 2 + 2 * h
-    exec_walk = 2 * (2 * (pos + h * 2 * h + 2 * h) + slot / M + (h + 12) * h + h * (h + 12) + h)
+    slot = kev * dn - max(kev - 16 * qt, 0) * dn - edge + br * dn * h + h * br * h + (br * h) ** 2 + br * h
+    exec_walk = 2 * (2 * (pos + h * br * h + br * h) + slot / M + (h + 12) * h + h * (h + 12) + h)
     walk = 2 * (3 * per_pos_gcn + per_walk_head)
     if etab:
         walk -= 2 * 3 * de * dn

@@ -33,22 +33,15 @@ void prof_end(const char *name, hipStream_t s, hipEvent_t a);
     } while (0)
 
 // ------------------------------------------------------------------ device graph layout
-// Adjacency entries as three parallel arrays in one allocation (16 B per entry in all): the 8-byte
-// {neighbour, edge id} record every sampled slot gathers, the timestamp as the fp32 every sampled output
-// carries, and the entry's rank inside its (node, neighbour) block (the number of earlier entries of the
-// node with the same neighbour; read only by step 2).  Split, the records the hop-2 gathers touch take
-// half the lines of the former 16-byte {ngh, eid, ts, brank} record, so the full-Enron graph's records
-// (2 MB) and timestamps (1 MB) fit one XCD's 4 MB L2.  The fp64 timestamps the bisects compare live in
-// their own array.
-struct __attribute__((aligned(8))) Rec {
-    int32_t ngh;
-    int32_t eid;
-};
-// a gathered entry: record + fp32 timestamp
-struct RecT {
+// One 16-byte record per adjacency entry, so a sampled slot is one dwordx4 load: the neighbour, the
+// edge id, the timestamp as the fp32 every sampled output carries, and the entry's rank inside its
+// (node, neighbour) block (the number of earlier entries of the node with the same neighbour).  The
+// fp64 timestamps the bisects compare live in their own array (8 B per entry: twice the density).
+struct __attribute__((aligned(16))) Rec {
     int32_t ngh;
     int32_t eid;
     float ts;
+    int32_t brank;
 };
 
 // e_idx -> (owner, slice length) for the (at most two) owners of an edge id.
@@ -114,9 +107,7 @@ struct DevGraph {
     int64_t n_entries;
     const int32_t *off;     // [V+1]
     const int2 *span;       // [V] {off[u], off[u+1]}: a node's range in one 8-B load
-    const Rec *rec;         // [n_entries] {neighbour, edge id}
-    const float *tsf;       // [n_entries] fp32 timestamps (the sampled outputs' ts)
-    const int32_t *brank;   // [n_entries] rank inside the entry's (node, neighbour) block
+    const Rec *rec;         // [n_entries]
     const double *tsd;      // [n_entries] fp64 timestamps (bisect keys)
     const EdgeEnds *ends;   // [max_eid+1]
     const int32_t *ppos;    // block search trees
@@ -248,19 +239,6 @@ __device__ __forceinline__ int32_t edge_len(const DevGraph &g, int32_t u, int32_
 }
 
 __device__ __forceinline__ int32_t deg(const DevGraph &g, int32_t u) { return g.off[u + 1] - g.off[u]; }
-
-// entry ix's record and fp32 timestamp (two independent loads)
-__device__ __forceinline__ RecT ld_rec(const DevGraph &g, int64_t ix) {
-    const Rec r = g.rec[ix];
-    return RecT{r.ngh, r.eid, g.tsf[ix]};
-}
-
-// the three arrays of the entry layout inside one allocation of 16 B per entry
-__host__ __device__ inline size_t rec_bytes(int64_t nn) { return (size_t)nn * (sizeof(Rec) + 2 * sizeof(int32_t)); }
-__host__ __device__ inline float *rec_tsf(Rec *base, int64_t nn) { return reinterpret_cast<float *>(base + nn); }
-__host__ __device__ inline int32_t *rec_brank(Rec *base, int64_t nn) {
-    return reinterpret_cast<int32_t *>(base + nn) + nn;
-}
 
 // bisect_left over node u's f64 timestamps (utils/graph.py:511-530)
 __device__ __forceinline__ int32_t bisect_ts(const DevGraph &g, int32_t u, double x) {

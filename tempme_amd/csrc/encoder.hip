@@ -556,12 +556,6 @@ constexpr int PFP = 4;     // weight-fragment ring depth (2, 4, 6 measured: 4 be
 // 12.25 KB LDS stash, the workgroup one constant table; 3 waves per SIMD and 8-wave workgroups measured slower)
 constexpr int WALK_WAVES = 2;
 constexpr int WALK_WPB = 4;
-// persistent walk_kernel waves: the grid is one round of resident workgroups looping over the units;
-// 1: static striding (wave w takes units w, w + stride, ...), 2: dynamic (each wave takes its next unit
-// from an atomic counter, requested at the start of its current unit)
-#ifndef TM_WALK_PERSIST
-#define TM_WALK_PERSIST 0
-#endif
 
 template <int NTO, int NQ, int NQL, int BASE>
 __device__ __forceinline__ void cgemm(__amdgpu_buffer_rsrc_t wr, const floatx4 (&x)[NQ], floatx4 (&o)[NTO]) {
@@ -766,7 +760,7 @@ struct WalkArgs {
     const double *cut;
     float *out;
     const float *etab;    // [n_ids][16*NTD] lin_event's edge-feature part + bias per edge id (Q0 > 0)
-    uint32_t *ticket;     // TM_WALK_PERSIST == 2: the launch's unit counter (zeroed before the launch)
+    uint32_t *ticket;     // the launch's unit counter (persistent waves; zeroed before the launch)
 };
 
 // Phase timing (debug builds only, -DTM_STAMPS; tools/stamps.py): s_memtime deltas of lane 0 per
@@ -1251,13 +1245,14 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * WALK_WAVES / WALK_WPB) walk
     const int lane = threadIdx.x & 63, col = lane & 15;
     const int32_t NS = a.W / a.M;
     const int64_t n_units = (a.n_slots + 15) / 16;
-    // persistent waves (not SPLIT): the grid is one round of resident workgroups; wave w takes units w,
-    // w + stride, ... or (dynamic) its next unit from the launch's counter (the constant table is loaded once per
-    // workgroup, the next unit's first scalars and table row are requested during the last pass of the current one)
-    constexpr int PERSIST = SPLIT ? 0 : TM_WALK_PERSIST;
+    // persistent waves (not SPLIT): the grid is one round of resident workgroups; a wave starts with unit = its
+    // global wave id and takes each next unit from the launch's counter (a ticket offset by the grid's waves),
+    // requested at the start of its current unit and consumed in that unit's last pass, where the next unit's
+    // scalars and table row are requested.  Static striding (unit w, w + stride, ...) measured 1.3 % slower
+    // than one unit per wave, dynamic tickets 1.4 % faster (profiles/r03_walk_xpf_ab.txt, r05_walk_ab.txt).
+    constexpr bool PERSIST = !SPLIT;
     const int64_t ustride = PERSIST ? (int64_t)gridDim.x * (blockDim.x >> 6) : n_units;
     int64_t unit = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    // the next unit (dynamic): a ticket from the launch's counter, offset by the first round (the grid's waves)
     auto ticket = [&]() -> int64_t {
         uint32_t t = 0;
         if (lane == 0) t = atomicAdd(a.ticket, 1u);
@@ -1310,7 +1305,7 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * WALK_WAVES / WALK_WPB) walk
 #endif
 #pragma nounroll
     for (;;) {
-    const int64_t unext = PERSIST == 2 ? ticket() : unit + ustride;
+    const int64_t unext = PERSIST ? ticket() : unit + ustride;
     bool vn;
     int64_t egn;
     int32_t jn;
@@ -1930,15 +1925,17 @@ static void launch_head(const EncW &P, int64_t n_walks, int64_t walks_per_group,
 // waves either way (1024 SIMDs x 2 waves), so the call's latency is the shorter pass chain
 constexpr int64_t WALK_SPLIT_UNITS = 512;
 
+static bool walk_split(int64_t units, int32_t M) { return units * M <= 3 * WALK_SPLIT_UNITS && units < WALK_SPLIT_UNITS; }
+
+// a.ticket zeroed on the stream before the launch unless walk_split (encoder_fwd_impl)
 template <int NQE, bool SEF = false, int Q0 = 0, bool ZN = false>
 static void launch_walk(const WalkArgs &a, unsigned blocks, hipStream_t s) {
     const int64_t units = (a.n_slots + 15) / 16;
-    if (!TM_WALK_PERSIST && units * a.M <= 3 * WALK_SPLIT_UNITS && units < WALK_SPLIT_UNITS) {
+    if (walk_split(units, a.M)) {
         const unsigned sb = (unsigned)((units * a.M + WALK_WPB - 1) / WALK_WPB);
         walk_kernel<NQE, 11, SEF, Q0, true, ZN><<<dim3(sb), 64 * WALK_WPB, 0, s>>>(a);
         return;
     }
-#if TM_WALK_PERSIST
     // one round of resident workgroups (occupancy x CUs of the current device), cached per instance
     static int cap[64] = {};
     int dev = 0;
@@ -1955,10 +1952,6 @@ static void launch_walk(const WalkArgs &a, unsigned blocks, hipStream_t s) {
         }
         if (cap[dev] > 0 && blocks > (unsigned)cap[dev]) blocks = (unsigned)cap[dev];
     }
-#if TM_WALK_PERSIST == 2
-    if (!a.ticket || hipMemsetAsync(a.ticket, 0, sizeof(uint32_t), s) != hipSuccess) return;
-#endif
-#endif
     walk_kernel<NQE, 11, SEF, Q0, false, ZN><<<dim3(blocks), 64 * WALK_WPB, 0, s>>>(a);
 }
 
@@ -2022,6 +2015,7 @@ static int encoder_fwd_impl(const tm_weights *w, const float *n_feat, const floa
                    reinterpret_cast<uint32_t *>(F)};
         const unsigned blocks = (unsigned)((units + WALK_WPB - 1) / WALK_WPB);
         const int q0 = etab ? etab_q0(P) : 0;
+        if (!walk_split(units, M)) TM_HIP(hipMemsetAsync(a.ticket, 0, sizeof(uint32_t), s));
         pe = prof_begin(s);
         if (q0 == 2 && w->node_zero) {   // edge table, zero node features: one event_gcn branch (ZN)
             if (nqe == 11) launch_walk<11, false, 2, true>(a, blocks, s);

@@ -137,8 +137,6 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
     g->h_dict = new int32_t[nn];
     g->h_ts = new double[nn];
     std::unique_ptr<Rec[]> rec(new Rec[nn]);          // every entry written by the node pass
-    std::unique_ptr<float[]> rec_ts(new float[nn]);
-    std::unique_ptr<int32_t[]> rec_rank(new int32_t[nn]);
     std::vector<int32_t> off32(n_nodes + 1);
     for (int32_t u = 0; u <= n_nodes; ++u) {
         g->h_off[u] = in_off[u];
@@ -244,9 +242,7 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
                 const int32_t bn = (int32_t)(j - i);
                 for (int64_t k = i; k < j; ++k) {
                     const int32_t p = (int32_t)(pair_key[s + k] & 0xFFFFFFFF);
-                    rec[s + p] = Rec{g->h_ngh[s + p], g->h_eid[s + p]};
-                    rec_ts[s + p] = (float)g->h_ts[s + p];
-                    rec_rank[s + p] = (int32_t)(k - i);
+                    rec[s + p] = Rec{g->h_ngh[s + p], g->h_eid[s + p], (float)g->h_ts[s + p], (int32_t)(k - i)};
                 }
                 if (bn > kBlkFan) len = (len + kBlkFan - 1) & ~(kBlkFan - 1);     // node-aligned tree
                 len += blk_region_len(bn);
@@ -402,7 +398,7 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
     hipError_t e = hipSuccess;
     e = e ? e : hipMalloc(&g->d_off, sizeof(int32_t) * (n_nodes + 1));
     e = e ? e : hipMalloc(&g->d_span, sizeof(int2) * n_nodes);
-    e = e ? e : hipMalloc(&g->d_rec, rec_bytes(nn));
+    e = e ? e : hipMalloc(&g->d_rec, sizeof(Rec) * nn);
     e = e ? e : hipMalloc(&g->d_tsd, sizeof(double) * nn);
     e = e ? e : hipMalloc(&g->d_ends, sizeof(EdgeEnds) * ends.size());
     e = e ? e : hipMalloc(&g->d_ppos, sizeof(int32_t) * n_ppos);
@@ -417,8 +413,6 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
         e = e ? e : hipMemcpy(g->d_span, span.data(), sizeof(int2) * n_nodes, hipMemcpyHostToDevice);
     }
     e = e ? e : hipMemcpy(g->d_rec, rec.get(), sizeof(Rec) * nn, hipMemcpyHostToDevice);
-    e = e ? e : hipMemcpy(rec_tsf(g->d_rec, nn), rec_ts.get(), sizeof(float) * nn, hipMemcpyHostToDevice);
-    e = e ? e : hipMemcpy(rec_brank(g->d_rec, nn), rec_rank.get(), sizeof(int32_t) * nn, hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(g->d_tsd, g->h_ts, sizeof(double) * nn, hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(g->d_ends, ends.data(), sizeof(EdgeEnds) * ends.size(), hipMemcpyHostToDevice);
     e = e ? e : hipMemcpy(g->d_ppos, ppos.get(), sizeof(int32_t) * n_ppos, hipMemcpyHostToDevice);
@@ -428,8 +422,8 @@ extern "C" int tm_graph_build(int32_t n_nodes, const int64_t *in_off, const int3
         return fail(TM_E_HIP, std::string("tm_graph_build: ") + hipGetErrorString(e));
     }
     tm.lap("upload");
-    g->d = DevGraph{n_nodes,   max_eid,   n,        g->d_off,  g->d_span, g->d_rec, rec_tsf(g->d_rec, nn),
-                    rec_brank(g->d_rec, nn), g->d_tsd,  g->d_ends, g->d_ppos, g->d_ets, ts_unique, g->d_pblk, cap - 1};
+    g->d = DevGraph{n_nodes,   max_eid,   n,        g->d_off,  g->d_span, g->d_rec,
+                    g->d_tsd,  g->d_ends, g->d_ppos, g->d_ets, ts_unique, g->d_pblk, cap - 1};
     *out = g;
     return TM_OK;
 }

@@ -117,7 +117,7 @@ __global__ void k_fill_i32(int64_t n, int32_t *a, int32_t v) {
 
 __global__ void k_dict(int64_t n, const int32_t *own, const int32_t *ngh, const int32_t *eid, const double *ts,
                        const int32_t *off, const int32_t *g0, const int32_t *gend, int32_t *dict, EdgeEnds *ends, Rec *rec,
-                       float *tsf, double *ets) {
+                       double *ets) {
     GS_LOOP(p, n) {
         const int32_t u = own[p], x = ngh[p], e = eid[p], s = off[u], d = off[u + 1] - s;
         const int32_t i = (int32_t)p - s, g = g0[p], j = (int32_t)p - g;
@@ -141,8 +141,7 @@ __global__ void k_dict(int64_t n, const int32_t *own, const int32_t *ngh, const 
             ends[e].node_b = u;
             ends[e].len_b = len;
         }
-        rec[p] = Rec{x, e};
-        tsf[p] = (float)ts[p];
+        rec[p] = Rec{x, e, (float)ts[p], 0};
         ets[e] = ts[p];
     }
 }
@@ -164,10 +163,10 @@ __global__ void k_block_heads(int64_t n, const int32_t *bperm, const int32_t *ow
 
 __global__ void k_block_info(int64_t n, const int32_t *bperm, const int32_t *own, const int32_t *ngh,
                              const int32_t *bstart, const int32_t *bincl, int32_t *bn, int32_t *bu, int32_t *bx,
-                             int32_t *bs, int32_t *brank) {
+                             int32_t *bs, Rec *rec) {
     GS_LOOP(k, n) {
         const int32_t q = bperm[k], b = bincl[k] - 1;
-        brank[q] = (int32_t)k - bstart[k];
+        rec[q].brank = (int32_t)k - bstart[k];
         const bool tail = k + 1 == n || bincl[k + 1] != bincl[k];
         if (tail) {
             bn[b] = (int32_t)k + 1 - bstart[k];
@@ -322,7 +321,7 @@ int tm_graph_build_edges_device(int32_t V, int64_t n_edges, const int64_t *src, 
         hipError_t e = hipSuccess;
         e = e ? e : hipMalloc(&g->d_off, sizeof(int32_t) * (V + 1));
         e = e ? e : hipMalloc(&g->d_span, sizeof(int2) * V);
-        e = e ? e : hipMalloc(&g->d_rec, rec_bytes(nn));
+        e = e ? e : hipMalloc(&g->d_rec, sizeof(Rec) * nn);
         e = e ? e : hipMalloc(&g->d_tsd, sizeof(double) * nn);
         e = e ? e : hipMalloc(&g->d_ends, sizeof(EdgeEnds) * ((size_t)max_eid + 1));
         e = e ? e : hipMalloc(&g->d_ets, sizeof(double) * ((size_t)max_eid + 1));
@@ -365,7 +364,7 @@ int tm_graph_build_edges_device(int32_t V, int64_t n_edges, const int64_t *src, 
             if (e == hipSuccess) {
                 k_group_ends<<<grid(n), TB, 0, s>>>(n, s_own, h_ts, g->d_off, g0, gend);
                 k_dict<<<grid(n), TB, 0, s>>>(n, s_own, g->d_hngh, g->d_heid, h_ts, g->d_off, g0, gend, g->d_dict,
-                                              g->d_ends, g->d_rec, rec_tsf(g->d_rec, nn), g->d_ets);
+                                              g->d_ends, g->d_rec, g->d_ets);
                 k_span<<<grid(V), TB, 0, s>>>(V, g->d_off, g->d_span);
                 e = hipGetLastError();
             }
@@ -392,8 +391,7 @@ int tm_graph_build_edges_device(int32_t V, int64_t n_edges, const int64_t *src, 
                     *rl = t.get<int32_t>(nb), *rbase = t.get<int32_t>(nb);
             e = e ? e : t.e;
             if (e == hipSuccess && n > 0) {
-                k_block_info<<<grid(n), TB, 0, s>>>(n, bperm, s_own, g->d_hngh, bstart, bincl, bn, bu, bx, bs,
-                                                   rec_brank(g->d_rec, nn));
+                k_block_info<<<grid(n), TB, 0, s>>>(n, bperm, s_own, g->d_hngh, bstart, bincl, bn, bu, bx, bs, g->d_rec);
                 k_region_len<<<grid(nb), TB, 0, s>>>(nb, bn, rl);
                 e = hipGetLastError();
             }
@@ -421,8 +419,7 @@ int tm_graph_build_edges_device(int32_t V, int64_t n_edges, const int64_t *src, 
             }
             e = e ? e : hipStreamSynchronize(s);
             if (e == hipSuccess) {
-                g->d = DevGraph{V,         max_eid,   n,         g->d_off, g->d_span, g->d_rec,
-                                rec_tsf(g->d_rec, nn), rec_brank(g->d_rec, nn), g->d_tsd,
+                g->d = DevGraph{V,         max_eid,   n,         g->d_off, g->d_span, g->d_rec, g->d_tsd,
                                 g->d_ends, g->d_ppos, g->d_ets, 1,        g->d_pblk, cap - 1};
                 g->dev_built = 1;
             }

@@ -252,7 +252,7 @@ __device__ Step3 final_step(const DevGraph &g, Key key, uint32_t ev, uint32_t w,
         int32_t pos = filt ? g.ppos[kb + rr] : rr;
         ent = ob0 + pos;
     }
-    const RecT rc = ld_rec(g, ent);
+    const Rec rc = g.rec[ent];
     o.ngh = rc.ngh;
     o.eid = rc.eid;
     o.ts = rc.ts;
@@ -339,11 +339,11 @@ __device__ __forceinline__ Step2 next_step(const DevGraph &g, Key key, uint32_t 
         o.pos = x - cu;
         ent = ov + (x - cu);
     }
-    const RecT rc = ld_rec(g, ent);
+    const Rec rc = g.rec[ent];
     o.ngh = rc.ngh;
     o.eid = rc.eid;
     o.ts = rc.ts;
-    o.rank = g.brank[ent];
+    o.rank = rc.brank;
     return o;
 }
 
@@ -404,10 +404,10 @@ __global__ void __launch_bounds__(256) khop_kernel(DevGraph g, Key key, uint32_t
 #pragma unroll
             for (int w = 0; w < 4; ++w) rank[w] += (di < d[w]) || (i < 4 * kb + w && di == d[w]);
         }
-    RecT rec[4];
+    Rec rec[4];
 #pragma unroll
     for (int w = 0; w < 4; ++w)
-        rec[w] = (c > 0 && 4 * kb + w < N) ? ld_rec(g, ro[lr] + (int32_t)d[w]) : RecT{0, 0, 0.f};
+        rec[w] = (c > 0 && 4 * kb + w < N) ? g.rec[ro[lr] + (int32_t)d[w]] : Rec{0, 0, 0.f, 0};
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
         const int32_t k = 4 * kb + w;
@@ -446,9 +446,9 @@ __device__ __forceinline__ void khop_emit(const DevGraph &g, int32_t N, const ui
                                           const uint32_t (&d)[4], int32_t c, int32_t o, int32_t *sn, int32_t *se,
                                           float *st) {
     // record gathers first (independent of the ranks), then the rank loop under their latency
-    RecT rec[4];
+    Rec rec[4];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) rec[w] = (c > 0 && 4 * kb + w < N) ? ld_rec(g, o + (int32_t)d[w]) : RecT{0, 0, 0.f};
+    for (int w = 0; w < 4; ++w) rec[w] = (c > 0 && 4 * kb + w < N) ? g.rec[o + (int32_t)d[w]] : Rec{0, 0, 0.f, 0};
     int32_t rank[4] = {0, 0, 0, 0};
     if (keyed && c > 0) {
         // dd holds (draw << 6 | index): unique keys, so the np.sort rank (ties by index) is one compare
@@ -669,12 +669,12 @@ __global__ void __launch_bounds__(256) khop2_kernel(DevGraph g, Key key, int32_t
     // gathers in output order: every store instruction writes one contiguous run per array
     const int32_t tot = rows2 * N;
     for (int32_t q0 = tid; q0 < tot; q0 += 4 * (int32_t)blockDim.x) {
-        RecT rc[4];
+        Rec rc[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int32_t q = q0 + k * (int32_t)blockDim.x;
             const int32_t ix = q < tot ? (int32_t)d2[q] : -1;
-            rc[k] = ix >= 0 ? ld_rec(g, ix) : RecT{0, 0, 0.f};
+            rc[k] = ix >= 0 ? g.rec[ix] : Rec{0, 0, 0.f, 0};
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -937,7 +937,7 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
             float t_ = 0.f;
             int32_t slot = tid;
             if (c > 0) {
-                const RecT rc = ld_rec(g, g.off[u] + (int32_t)d);
+                const Rec rc = g.rec[g.off[u] + (int32_t)d];
                 n_ = rc.ngh; e_ = rc.eid; t_ = rc.ts; slot = rank;
             }
             h1n[slot] = n_; h1e[slot] = e_; h1t[slot] = t_;
@@ -1016,12 +1016,12 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
     // gathers in output order, 4 in flight per lane: each store instruction writes one contiguous run per
     // array (stores scattered inside the rows cost the k-hop kernel a third of its time)
     for (int32_t q0 = tid; q0 < N * N; q0 += 4 * 64) {
-        RecT rc[4];
+        Rec rc[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int32_t q = q0 + 64 * k;
             const int32_t ix = q < N * N ? sidx[q] : -1;
-            rc[k] = ix >= 0 ? ld_rec(g, ix) : RecT{0, 0, 0.f};
+            rc[k] = ix >= 0 ? g.rec[ix] : Rec{0, 0, 0.f, 0};
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {

@@ -142,8 +142,12 @@ def _eval_worker(rank, world, port, q):
                 single = eval_one_epoch(args, base, ex, buf, *ev, seed=seed)
                 n = int(ev[0].shape[0]) - 1
                 assert sharded["n_batches"] == single["n_batches"] == math.ceil(n / args.test_bs) - 1
-                assert sharded == single, (sharded, single)
-                assert all(np.isfinite(v) for v in single.values())
+                # bitwise the same figures (a batch whose y_ori holds one class has no AUC: NaN, as in the reference)
+                assert sharded.keys() == single.keys()
+                for k in single:
+                    a, b = sharded[k], single[k]
+                    assert a == b or (np.isnan(a) and np.isnan(b)), (k, a, b)
+                assert all(np.isfinite(single[k]) for k in ("aps", "acc", "loss", "kl_loss", "ratio_aps"))
         if rank == 0:
             q.put("ok")
         dist.barrier()
