@@ -95,6 +95,9 @@ __global__ void __launch_bounds__(1024) std_cut_kernel(int32_t B, int32_t W, Cut
 
 // ------------------------------------------------------------------ event_gcn: 32 walk-positions per block
 // F[row] = [MLP(x_s + relu(x_t + L)) | MLP(x_t + relu(x_s + L))],  L = lin_event([E(e) | cnt | cos(dt)])
+// ZN (zero node features, tm_weights_set_node_zero): A = B, so MLP.0 / MLP.2 run on the 32 A rows and both halves
+// of F get the same (bit-identical) values
+template <bool ZN = false>
 __global__ void __launch_bounds__(256) gcn_kernel(EncW P, int64_t n_rows, const float *__restrict__ n_feat,
                                                   const float *__restrict__ e_feat, const int32_t *__restrict__ node6,
                                                   const int32_t *__restrict__ eid3, const float *__restrict__ ts3,
@@ -145,29 +148,38 @@ __global__ void __launch_bounds__(256) gcn_kernel(EncW P, int64_t n_rows, const 
             float a = 0.f, b = 0.f;
             if (c < dn) {
                 const float L = acc[r] + P.ev.b[c];
-                const float xs = n_feat[(int64_t)s_ns[row] * dn + c], xt = n_feat[(int64_t)s_nt[row] * dn + c];
+                const float xs = ZN ? 0.f : n_feat[(int64_t)s_ns[row] * dn + c];
+                const float xt = ZN ? 0.f : n_feat[(int64_t)s_nt[row] * dn + c];
                 a = xs + relu(xt + L);
                 b = xt + relu(xs + L);
             }
             AB[row * ldab + c] = a;
-            AB[(row + TILE_ROWS) * ldab + c] = b;
+            if (!ZN) AB[(row + TILE_ROWS) * ldab + c] = b;
         }
     });
     __syncthreads();
-    gemm<4>(AB, ldab, P.g1, [&](int mt, int nt, floatx4 acc) {
+    auto g1_epi = [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) H[erow(mt, r) * ldh + c] = relu(acc[r] + P.g1.b[c]);
-    });
+    };
+    if constexpr (ZN) gemm<2>(AB, ldab, P.g1, g1_epi);
+    else gemm<4>(AB, ldab, P.g1, g1_epi);
     __syncthreads();
-    gemm<4>(H, ldh, P.g2, [&](int mt, int nt, floatx4 acc) {
+    auto g2_epi = [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) {
             const int row = erow(mt, r);
             const int rr = row & (TILE_ROWS - 1), half = row >> 5;
             const int64_t gr = row0 + rr;
-            if (gr < n_rows && c < h) F[gr * (2 * h) + half * h + c] = acc[r] + P.g2.b[c];
+            if (gr < n_rows && c < h) {
+                const float v = acc[r] + P.g2.b[c];
+                F[gr * (2 * h) + half * h + c] = v;
+                if (ZN) F[gr * (2 * h) + h + c] = v;
+            }
         }
-    });
+    };
+    if constexpr (ZN) gemm<2>(H, ldh, P.g2, g2_epi);
+    else gemm<4>(H, ldh, P.g2, g2_epi);
 }
 
 // ------------------------------------------------------------------ attention head + final MLP: TR walks per block
@@ -1907,6 +1919,14 @@ static size_t gcn_lds(const EncW &P) {
     return sizeof(float) * (xsz + 2 * TILE_ROWS * (r16(P.dn) + 8));
 }
 static size_t head_lds(const EncW &P, int tr) { return sizeof(float) * (4 * tr * (2 * P.h + 8)); }
+static void launch_gcn(const EncW &P, int node_zero, int64_t n_rows, size_t lds, const float *n_feat,
+                       const float *e_feat, const int32_t *node6, const int32_t *eid3, const float *ts3, const float *cnt,
+                       float *F, hipStream_t s) {
+    const dim3 grid((unsigned)((n_rows + TILE_ROWS - 1) / TILE_ROWS));
+    if (node_zero) gcn_kernel<true><<<grid, 256, lds, s>>>(P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, F);
+    else gcn_kernel<false><<<grid, 256, lds, s>>>(P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, F);
+}
+
 // walks per head_kernel workgroup: 32 where the tiles fit the LDS, else 16
 static int head_tr(const EncW &P) { return head_lds(P, 32) <= 160 * 1024 ? 32 : 16; }
 static void launch_head(const EncW &P, int64_t n_walks, int64_t walks_per_group, int32_t W, const float *F,
@@ -2043,8 +2063,7 @@ static int encoder_fwd_impl(const tm_weights *w, const float *n_feat, const floa
     }
     const int64_t n_rows = n_walks * 3;
     pe = prof_begin(s);
-    gcn_kernel<<<dim3((unsigned)((n_rows + TILE_ROWS - 1) / TILE_ROWS)), 256, lds_g, s>>>(
-        P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, F);
+    launch_gcn(P, w->node_zero, n_rows, lds_g, n_feat, e_feat, node6, eid3, ts3, cnt, F, s);
     TM_CHECK_LAUNCH();
     prof_end("gcn_kernel", s, pe);
     pe = prof_begin(s);
@@ -2078,8 +2097,7 @@ extern "C" int tm_encoder_train_fwd(const tm_weights *w, const float *n_feat, co
     const int64_t n_rows = n_walks * 3;
     pe = prof_begin(s);
     if (!launch_gcn_fwd_reg(P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, F, s))
-        gcn_kernel<<<dim3((unsigned)((n_rows + TILE_ROWS - 1) / TILE_ROWS)), 256, lds_g, s>>>(
-            P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, F);
+        launch_gcn(P, w->node_zero, n_rows, lds_g, n_feat, e_feat, node6, eid3, ts3, cnt, F, s);
     TM_CHECK_LAUNCH();
     prof_end("gcn_kernel", s, pe);
     pe = prof_begin(s);

@@ -551,6 +551,11 @@ struct GcnBwdOut {
     float *dt;    // [R]            dt of the row (relative to walk position 2)
 };
 
+// ZN (zero node features): A = B, H_s = H_t and the relu masks agree, so every branch sum folds before its GEMM:
+// dZ_s + dZ_t = ((dU_s + dU_t) M2) * [z > 0] and d lev = ((dZ_s + dZ_t) M0) * [a > 0] run on 32 rows instead of 64.
+// The weight-gradient row pairs become (dZ_s + dZ_t, A) for MLP.0 and (dU_s + dU_t, H) for MLP.2: o.AB / o.H hold
+// A / H in half 0, o.dZ holds dZ_s + dZ_t in half 0 and dU_s + dU_t in half 1 (tm_encoder_wgrad's ZN jobs).
+template <bool ZN = false>
 __global__ void __launch_bounds__(256) gcn_bwd_kernel(EncW P, EncWT T, int64_t n_rows, const float *__restrict__ n_feat,
                                                       const float *__restrict__ e_feat,
                                                       const int32_t *__restrict__ node6, const int32_t *__restrict__ eid3,
@@ -607,7 +612,8 @@ __global__ void __launch_bounds__(256) gcn_bwd_kernel(EncW P, EncWT T, int64_t n
             uint8_t ma = 0, mb = 0;
             if (c < dn) {
                 const float L = acc[r] + P.ev.b[c];
-                const float xs = n_feat[(int64_t)s_ns[row] * dn + c], xt = n_feat[(int64_t)s_nt[row] * dn + c];
+                const float xs = ZN ? 0.f : n_feat[(int64_t)s_ns[row] * dn + c];
+                const float xt = ZN ? 0.f : n_feat[(int64_t)s_nt[row] * dn + c];
                 const float a = xt + L, b = xs + L;
                 hs = xs + relu(a);
                 ht = xt + relu(b);
@@ -615,21 +621,35 @@ __global__ void __launch_bounds__(256) gcn_bwd_kernel(EncW P, EncWT T, int64_t n
                 mb = b > 0.f;
             }
             AB[row * ldab + c] = hs;
-            AB[(row + TILE_ROWS) * ldab + c] = ht;
             MK[row * dn16 + c] = ma;
-            MK[(row + TILE_ROWS) * dn16 + c] = mb;
+            if (!ZN) {
+                AB[(row + TILE_ROWS) * ldab + c] = ht;
+                MK[(row + TILE_ROWS) * dn16 + c] = mb;
+            }
             if (valid(row)) {
                 o.AB[((row0 + row) * 2) * dn16 + c] = hs;
-                o.AB[((row0 + row) * 2 + 1) * dn16 + c] = ht;
+                if (!ZN) o.AB[((row0 + row) * 2 + 1) * dn16 + c] = ht;
             }
         }
     });
     __syncthreads();
-    for (int i = tid; i < 2 * TILE_ROWS * h; i += blockDim.x) {   // dU: d U_s rows 0..31, d U_t rows 32..63
-        const int row = i / h, c = i % h, r = row % TILE_ROWS, half = row / TILE_ROWS;
-        dU[row * ldh + c] = valid(r) ? dF[(row0 + r) * (2 * h) + half * h + c] : 0.f;
+    if (ZN) {   // dU_s + dU_t in rows 0..31, also the MLP.2 weight-gradient rows (o.dZ half 1)
+        for (int i = tid; i < TILE_ROWS * h; i += blockDim.x) {
+            const int r = i / h, c = i % h;
+            float v = 0.f;
+            if (valid(r)) {
+                v = dF[(row0 + r) * (2 * h) + c] + dF[(row0 + r) * (2 * h) + h + c];
+                o.dZ[((row0 + r) * 2 + 1) * h + c] = v;
+            }
+            dU[r * ldh + c] = v;
+        }
+    } else {
+        for (int i = tid; i < 2 * TILE_ROWS * h; i += blockDim.x) {   // dU: d U_s rows 0..31, d U_t rows 32..63
+            const int row = i / h, c = i % h, r = row % TILE_ROWS, half = row / TILE_ROWS;
+            dU[row * ldh + c] = valid(r) ? dF[(row0 + r) * (2 * h) + half * h + c] : 0.f;
+        }
     }
-    gemm<4>(AB, ldab, P.g1, [&](int mt, int nt, floatx4 acc) {
+    auto g1_epi = [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) {
             const int row = erow(mt, r), rr = row % TILE_ROWS, half = row / TILE_ROWS;
@@ -637,9 +657,11 @@ __global__ void __launch_bounds__(256) gcn_bwd_kernel(EncW P, EncWT T, int64_t n
             Hb[row * ldh + c] = v;
             if (valid(rr)) o.H[((row0 + rr) * 2 + half) * h + c] = v;
         }
-    });
+    };
+    if constexpr (ZN) gemm<2>(AB, ldab, P.g1, g1_epi);
+    else gemm<4>(AB, ldab, P.g1, g1_epi);
     __syncthreads();
-    gemm<4>(dU, ldh, T.g2T, [&](int mt, int nt, floatx4 acc) {   // dZ = (dU M2) * [z > 0]
+    auto g2_epi = [&](int mt, int nt, floatx4 acc) {   // dZ = (dU M2) * [z > 0]
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) {
             const int row = erow(mt, r), rr = row % TILE_ROWS, half = row / TILE_ROWS;
@@ -647,17 +669,22 @@ __global__ void __launch_bounds__(256) gcn_bwd_kernel(EncW P, EncWT T, int64_t n
             Hb[row * ldh + c] = v;
             if (valid(rr)) o.dZ[((row0 + rr) * 2 + half) * h + c] = v;
         }
-    });
+    };
+    if constexpr (ZN) gemm<2>(dU, ldh, T.g2T, g2_epi);
+    else gemm<4>(dU, ldh, T.g2T, g2_epi);
     __syncthreads();
     // d lev = (dZ_s M0) * [a > 0] + (dZ_t M0) * [b > 0]; rows r and r + 32 of one column land in the same
-    // lane (row tiles mt and mt + 2, in that order), so the sum needs no synchronisation.
+    // lane (row tiles mt and mt + 2, in that order), so the sum needs no synchronisation.  ZN: one product.
     float *DL = AB;
-    gemm<4>(Hb, ldh, T.g1T, [&](int mt, int nt, floatx4 acc) {
+    auto lev_epi = [&](int mt, int nt, floatx4 acc) {
         const int c = ecol(nt);
         for (int r = 0; r < 4; ++r) {
             const int row = erow(mt, r);
             const float v = MK[row * dn16 + c] ? acc[r] : 0.f;
-            if (mt < 2) {
+            if (ZN) {
+                DL[row * ldab + c] = v;
+                if (valid(row)) o.dlev[(row0 + row) * dn16 + c] = v;
+            } else if (mt < 2) {
                 DL[row * ldab + c] = v;
             } else {
                 const int rr = row - TILE_ROWS;
@@ -666,7 +693,9 @@ __global__ void __launch_bounds__(256) gcn_bwd_kernel(EncW P, EncWT T, int64_t n
                 if (valid(rr)) o.dlev[(row0 + rr) * dn16 + c] = s;
             }
         }
-    });
+    };
+    if constexpr (ZN) gemm<2>(Hb, ldh, T.g1T, lev_epi);
+    else gemm<4>(Hb, ldh, T.g1T, lev_epi);
     __syncthreads();
     gemm<2>(DL, ldab, T.evT, [&](int mt, int nt, floatx4 acc) {   // d time features -> * -sin(dt w + phi)
         const int j = ecol(nt);
@@ -1578,6 +1607,16 @@ extern "C" int tm_encoder_train_supported(int32_t de, int32_t dn, int32_t h, int
     return head_bwd_tr(P) && gcn_bwd_lds(P) <= lim && gate <= lim ? 1 : 0;
 }
 
+// the register-resident event_gcn backward runs (opt-in, dims it has an instance for); it has no zero-node form
+static bool gcn_bwd_uses_reg(const tm_weights *w) {
+    const EncW &P = w->P;
+    const int nqe = r16(P.kev) / 16;
+    return P.h == HID && r16(P.dn) == 176 && P.dn % 4 == 0 && P.de % 4 == 0 && nqe >= 11 && nqe <= 14 &&
+           P.g1.nt == 4 && P.g1.nq == 11 && w->T.g2T.nt == 4 && w->T.g1T.nt == 11 && w->T.g1T.nq == 4 &&
+           w->T.evT.nt == 11 && w->T.evT.nq == 11 && P.ev.nq == nqe && gcn_reg_enabled();
+}
+static bool zn_reg_bypass(const tm_weights *w) { return gcn_bwd_uses_reg(w); }
+
 extern "C" int tm_encoder_bwd(const tm_weights *w, const float *n_feat, const float *e_feat, int32_t n_groups,
                               int32_t B, int32_t W, const int32_t *node6, const int32_t *eid3, const float *ts3,
                               const int32_t *cat, const double *cut, const float *cnt, const uint8_t *drop,
@@ -1618,17 +1657,18 @@ extern "C" int tm_encoder_bwd(const tm_weights *w, const float *n_feat, const fl
     // register-resident instance: hid_dim 64, 11 node-feature tiles (dn 161..176, a multiple of 4), lin_event
     // with 11..14 K steps; the LDS-tiled kernel otherwise.  Opt-in (TEMPME_GCN_REG=1) until it has been
     // checked on the GPU (written in round 4 while the GPU pool was unavailable to this build)
-    const bool reg = P.h == HID && r16(P.dn) == 176 && P.dn % 4 == 0 && P.de % 4 == 0 && nqe >= 11 && nqe <= 14 &&
-                     P.g1.nt == 4 && P.g1.nq == 11 && w->T.g2T.nt == 4 && w->T.g1T.nt == 11 && w->T.g1T.nq == 4 &&
-                     w->T.evT.nt == 11 && w->T.evT.nq == 11 && P.ev.nq == nqe && gcn_reg_enabled();
+    const bool reg = gcn_bwd_uses_reg(w);
     if (reg) {
         const unsigned blocks = (unsigned)((n_rows + 63) / 64);
         if (nqe == 11) gcn_bwd_reg_kernel<11><<<dim3(blocks), 256, 0, s>>>(P, w->T, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, io->dF, go);
         else if (nqe == 12) gcn_bwd_reg_kernel<12><<<dim3(blocks), 256, 0, s>>>(P, w->T, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, io->dF, go);
         else if (nqe == 13) gcn_bwd_reg_kernel<13><<<dim3(blocks), 256, 0, s>>>(P, w->T, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, io->dF, go);
         else gcn_bwd_reg_kernel<14><<<dim3(blocks), 256, 0, s>>>(P, w->T, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, io->dF, go);
+    } else if (w->node_zero) {
+        gcn_bwd_kernel<true><<<dim3((unsigned)((n_rows + TILE_ROWS - 1) / TILE_ROWS)), 256, lg, s>>>(
+            P, w->T, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, io->dF, go);
     } else {
-        gcn_bwd_kernel<<<dim3((unsigned)((n_rows + TILE_ROWS - 1) / TILE_ROWS)), 256, lg, s>>>(
+        gcn_bwd_kernel<false><<<dim3((unsigned)((n_rows + TILE_ROWS - 1) / TILE_ROWS)), 256, lg, s>>>(
             P, w->T, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, io->dF, go);
     }
     TM_CHECK_LAUNCH();
@@ -1749,10 +1789,13 @@ extern "C" int tm_encoder_wgrad(const tm_weights *w, int32_t n_groups, int32_t B
     const int n = (int)n64, R = 3 * n, h = w->h, h2 = 2 * h, hm = w->P.hm;
     const int dn = w->dn, kev = w->P.kev, KE = r16(kev), DN = r16(dn), KM = r16(hm);
     const float *F = reinterpret_cast<const float *>(workspace);
+    // zero node features (gcn_bwd_kernel<true>): one row pair per position for MLP.0 / MLP.2, the branch sums
+    const bool zn = w->node_zero && !zn_reg_bypass(w);
+    const tm_wgrad_job zn0{io->dZ, io->AB, 2 * h, 2 * DN, h, dn, R}, zn2{io->dZ + h, io->H, 2 * h, 2 * h, h, h, R};
     const tm_wgrad_job jobs[] = {
         {io->dlev, io->ev, DN, KE, dn, kev, R},            // lin_event
-        {io->dZ, io->AB, h, DN, h, dn, 2 * R},             // event_conv.MLP.0
-        {io->dF, io->H, h, h, h, h, 2 * R},                // event_conv.MLP.2
+        zn ? zn0 : tm_wgrad_job{io->dZ, io->AB, h, DN, h, dn, 2 * R},   // event_conv.MLP.0
+        zn ? zn2 : tm_wgrad_job{io->dF, io->H, h, h, h, h, 2 * R},      // event_conv.MLP.2
         {io->dP, F + 2 * h2, h2, 3 * h2, h2, h2, n},       // attention.W1 (x = F[:, 2])
         {io->dQ, F, h2, 3 * h2, h2, h2, n},                // attention.W2, position 0
         {io->dQ + (int64_t)n * h2, F + h2, h2, 3 * h2, h2, h2, n},   // position 1
