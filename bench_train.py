@@ -53,6 +53,8 @@ def main():
     ap.add_argument("--graph", action="store_true", help="capture the step as a HIP graph with several ranks "
                     "too (the RCCL all-reduce is then captured inside the graph)")
     ap.add_argument("--no-fused-adam", action="store_true", help="torch's default (foreach) Adam")
+    ap.add_argument("--no-node-zero", action="store_true",
+                    help="do not use the zero-node-feature kernel forms (A/B; the graph's node features are zeros)")
     ap.add_argument("--overlap-prepare", action="store_true",
                     help="graphed step: the base model's original contrast as a second graph branch "
                          "(GraphedTrainStep(overlap_prepare=True))")
@@ -116,6 +118,7 @@ def main():
     base = base.to(dev).eval()
     ex = tm.TempME(base, "tgn", "enron", out_dim=40, hid_dim=64, device=dev,
                    null_model={k: 1.0 / 12 for k in range(1, 13)}).to(dev)
+    ex.node_zero_specialization = not args.no_node_zero
     use_graph = not args.no_graph and (world == 1 or (args.graph and backend == "nccl"))
     # fused Adam: one multi-tensor launch per step instead of ~70 per-parameter kernels (same update rule,
     # temp_exp_main.py's torch.optim.Adam(lr=1e-3) defaults)
@@ -206,6 +209,7 @@ def main():
                           "global_batches_per_step": per_step * world, "train_steps_per_rank_per_step": per_step,
                           "allreduce_overlap": (not args.no_overlap) and not use_graph,
                           "hip_graph": use_graph, "overlap_prepare": bool(args.overlap_prepare and use_graph),
+                          "zero_node_forms": bool(getattr(ex, "_node_zero", False)) and ex.node_zero_specialization,
                           "opt_in": {k: os.environ[k] for k in ("TEMPME_GCN_REG", "TEMPME_WGRAD_T", "TEMPME_EXPLAIN_PAD",
                                                                 "TEMPME_BETA_TORCH") if k in os.environ},
                           "grad_bucket_floats": sum(p.numel() for p in ex.parameters() if p.grad is not None)},

@@ -93,8 +93,12 @@ class Fast {
         }
         for (size_t k = 0; k < side_ids.size() && k < (size_t)kSides; ++k) {
             py::tuple s = side_ids[k];
-            side_[k] = c10::hip::HIPStream::unpack3(py::cast<int64_t>(s[0]), py::cast<int64_t>(s[1]),
-                                                    static_cast<c10::DeviceType>(py::cast<int64_t>(s[2])));
+            // torch's ROCm build hands out HIP streams typed as CUDA streams (masquerading); the c10::hip
+            // stream object wants the HIP device type for the same (index, id)
+            side_[k] = c10::hip::HIPStream(c10::Stream(c10::Stream::UNSAFE,
+                                                       c10::Device(c10::DeviceType::HIP,
+                                                                   static_cast<c10::DeviceIndex>(py::cast<int64_t>(s[1]))),
+                                                       static_cast<c10::StreamId>(py::cast<int64_t>(s[0]))));
         }
     }
 

@@ -58,7 +58,7 @@ def _inputs(de, G, B, N, seed, zero_nodes=False):
 @pytest.mark.parametrize("de,G,B,N,train,zn", [(32, 3, 20, 20, True, False), (1, 2, 7, 5, True, False),
                                                (32, 1, 9, 20, False, False), (32, 3, 20, 20, True, True),
                                                (32, 1, 9, 20, False, True)])
-def test_encoder_backward_matches_autograd(dev, de, G, B, N, train, zn=False):
+def test_encoder_backward_matches_autograd(dev, de, G, B, N, train, zn):
     """Forward within 1e-5 and all 22 gradients within 2e-4 of fp64 autograd through the oracle; zn: zero node
     features, i.e. gcn_kernel / gcn_bwd_kernel's one-branch forms and the summed MLP.0 / MLP.2 weight-gradient rows."""
     from tempme_amd import TempME

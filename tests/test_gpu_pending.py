@@ -35,7 +35,7 @@ def test_gcn_reg_and_wgrad_t_match_autograd(dev, monkeypatch, de, G, B, N, train
     from tests.test_gpu_encoder_train import test_encoder_backward_matches_autograd as check
     monkeypatch.setenv("TEMPME_GCN_REG", "1")
     monkeypatch.setenv("TEMPME_WGRAD_T", "1")
-    check(dev, de, G, B, N, train)
+    check(dev, de, G, B, N, train, False)
 
 
 def test_explain_pad_kernel_equals_torch_mask(dev, monkeypatch):
