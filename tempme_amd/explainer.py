@@ -28,11 +28,9 @@ import torch.nn.functional as F
 from . import _lib as L
 from .null_model import get_null_distribution
 
-# TEMPME_BETA_TORCH=1: the training explanation's Beta draw through torch.distributions (A/B of _BetaRsampleFn)
-_BETA_TORCH = os.environ.get("TEMPME_BETA_TORCH", "0") == "1"
-# TEMPME_EXPLAIN_PAD=1: the padding mask from the explanation kernel (tm_explain_train_fwd_pad) instead of a
-# torch comparison; opt-in until it has been checked on the GPU
-_EXPLAIN_PAD = os.environ.get("TEMPME_EXPLAIN_PAD", "0") == "1"
+# the training explanation's padding mask comes from the explanation kernel (tm_explain_train_fwd_pad) instead of
+# a torch comparison: bitwise the same mask (tests/test_gpu_variants.py flips this to compare the two)
+_EXPLAIN_PAD = True
 
 
 class TimeEncode(nn.Module):
@@ -181,8 +179,9 @@ _EXT = [None, False]
 
 def _dropin_ext():
     """tempme_amd/lib/_dropin_ext*.so (csrc/dropin_ext.cpp, built by __graft_entry__.build()): the C++ host
-    side of the drop-in fast path.  Without it the same fast path runs its host side in Python (same
-    kernels, same results), with a warning."""
+    side of the drop-in fast path (checked against the Python host side on the GPU,
+    tests/test_gpu_enron.py::test_dropin_cpp_host_side_equals_python_host_side).  Without it the same fast path
+    runs its host side in Python (same kernels, same results), with a warning."""
     if not _EXT[1]:
         _EXT[1] = True
         import importlib.machinery
@@ -191,14 +190,13 @@ def _dropin_ext():
         import sysconfig
         path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
                             "_dropin_ext" + sysconfig.get_config_var("EXT_SUFFIX"))
-        # opt-in (TEMPME_DROPIN_EXT=1) until the extension has been checked on the GPU
-        if os.path.exists(path) and os.environ.get("TEMPME_DROPIN_EXT", "0") == "1":
+        if os.path.exists(path):
             loader = importlib.machinery.ExtensionFileLoader("tempme_amd._dropin_ext", path)
             spec = importlib.util.spec_from_file_location("tempme_amd._dropin_ext", path, loader=loader)
             mod = importlib.util.module_from_spec(spec)
             loader.exec_module(mod)
             _EXT[0] = mod
-        elif os.environ.get("TEMPME_DROPIN_EXT", "0") == "1":
+        else:
             warnings.warn("tempme_amd/lib/_dropin_ext*.so not built (python tempme_amd/_build_ext.py): the drop-in "
                           "fast path's host side runs in Python", RuntimeWarning, stacklevel=3)
     return _EXT[0]
@@ -1027,8 +1025,8 @@ class TempME(nn.Module):
 
     def _fused_beta(self):
         """beta_sample(p, True) * mask may go through _BetaRsampleFn (bitwise the same as torch's Beta rsample):
-        not when the module's beta_sample is overridden (an instance attribute) or TEMPME_BETA_TORCH=1."""
-        return not _BETA_TORCH and "beta_sample" not in self.__dict__ and type(self).beta_sample is TempME.beta_sample
+        not when the module's beta_sample is overridden (an instance attribute or a subclass)."""
+        return "beta_sample" not in self.__dict__ and type(self).beta_sample is TempME.beta_sample
 
     def beta_sample(self, prob, training):
         """explainer_new.py:420-430."""

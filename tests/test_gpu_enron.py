@@ -500,8 +500,7 @@ def test_dropin_cpp_host_side_equals_python_host_side(dev, finder, g, z):
     Python (new version key) and the results follow the new weights."""
     from tempme_amd import explainer as X
     ex, P, A, cat_d, edge, cut = _bern_setup(dev, finder, g, z, E=100)
-    if X._dropin_ext() is None:
-        pytest.skip("the C++ drop-in host extension is opt-in (TEMPME_DROPIN_EXT=1, tempme_amd/_build_ext.py)")
+    assert X._dropin_ext() is not None, "tempme_amd/lib/_dropin_ext*.so missing (python tempme_amd/_build_ext.py)"
     ex.beta_sample = lambda prob, training: prob
     pk, ed = P.load_subgraph_margin(A(), cat_d, device=dev), P.load_edge(edge, dev)
 

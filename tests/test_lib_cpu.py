@@ -77,11 +77,9 @@ def test_flops_model_matches_survey():
 
 
 def test_dropin_extension_loads(monkeypatch):
-    """The drop-in fast path's C++ host side (csrc/dropin_ext.cpp, built by build(); opt-in at run time,
-    TEMPME_DROPIN_EXT=1) imports on the CPU and exposes its entry points (constructing one needs a HIP
-    device)."""
+    """The drop-in fast path's C++ host side (csrc/dropin_ext.cpp, built by build(), used whenever it is built)
+    imports on the CPU and exposes its entry points (constructing one needs a HIP device)."""
     from tempme_amd import explainer as X
-    monkeypatch.setenv("TEMPME_DROPIN_EXT", "1")
     monkeypatch.setattr(X, "_EXT", [None, False])
     m = X._dropin_ext()
     assert m is not None, "tempme_amd/lib/_dropin_ext*.so missing: python tempme_amd/_build_ext.py"
