@@ -55,9 +55,9 @@ def main():
     ap.add_argument("--no-fused-adam", action="store_true", help="torch's default (foreach) Adam")
     ap.add_argument("--no-node-zero", action="store_true",
                     help="do not use the zero-node-feature kernel forms (A/B; the graph's node features are zeros)")
-    ap.add_argument("--overlap-prepare", action="store_true",
-                    help="graphed step: the base model's original contrast as a second graph branch "
-                         "(GraphedTrainStep(overlap_prepare=True))")
+    ap.add_argument("--no-overlap-prepare", action="store_true",
+                    help="graphed step without the base model's original contrast as a second graph branch "
+                         "(GraphedTrainStep(overlap_prepare=False))")
     ap.add_argument("--global-batches", type=int, default=8,
                     help="reference batches per timed step over ALL ranks (strong scaling: each rank steps through "
                          "global-batches / N of them, one all-reduced Adam update per round of N batches)")
@@ -142,7 +142,7 @@ def main():
         rows = [r for r in rows if r.numel() == B]
         n_steps = min(n_steps, len(rows))
         graphed = GraphedTrainStep(ex, base, opt, buf, s_d, d_d, t_d, e_d, rows[:max(args.warmup, 1)],
-                                   grad_sync=sync, overlap_prepare=args.overlap_prepare)
+                                   grad_sync=sync, overlap_prepare=not args.no_overlap_prepare)
 
         def step(k):   # one timed step = per_step replays
             out = None
@@ -208,10 +208,8 @@ def main():
                           "batch_size": B, "train_events": int(len(src)), "parallelism": f"dp{world}",
                           "global_batches_per_step": per_step * world, "train_steps_per_rank_per_step": per_step,
                           "allreduce_overlap": (not args.no_overlap) and not use_graph,
-                          "hip_graph": use_graph, "overlap_prepare": bool(args.overlap_prepare and use_graph),
+                          "hip_graph": use_graph, "overlap_prepare": bool(not args.no_overlap_prepare and use_graph),
                           "zero_node_forms": bool(getattr(ex, "_node_zero", False)) and ex.node_zero_specialization,
-                          "opt_in": {k: os.environ[k] for k in ("TEMPME_GCN_REG", "TEMPME_WGRAD_T", "TEMPME_EXPLAIN_PAD",
-                                                                "TEMPME_BETA_TORCH") if k in os.environ},
                           "grad_bucket_floats": sum(p.numel() for p in ex.parameters() if p.grad is not None)},
                "loss_first_last": [round(losses[0], 5), round(losses[-1], 5)],
                "kernels": {k: {"avg_ms": round(ms / max(c, 1), 4), "launches": c} for k, (ms, c) in prof.items()},

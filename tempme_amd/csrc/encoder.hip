@@ -1083,10 +1083,47 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
         Hs[t] = ldsx4(cs + C::G1, t);
         if constexpr (!ZN) Ht[t] = ldsx4(cs + C::G1C, t);
     }
-    {
+    if constexpr (ZN) {
+        // one branch: 16 MFMAs per K step, too few to hide a weight fragment requested one step ahead (stamps:
+        // the phase ran at 69 % of the shared-pipe ideal), so the fragments come through a 3-deep ring, two
+        // steps ahead; the next phase's first fragments are requested at step NTD - 2
+        const int vo = lane_id() * 16;
+        float4 wz[3][4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            wz[0][t] = pre[t];
+            wz[1][t] = wload(wr, vo, LY::G1 / 4 + (t * NTD + 1) * 64);
+        }
+#pragma unroll
+        for (int q = 0; q < NTD; ++q) {
+            if (q + 2 < NTD) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) wz[(q + 2) % 3][t] = wload(wr, vo, LY::G1 / 4 + (t * NTD + q + 2) * 64);
+            } else if (q + 2 == NTD) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) wz[(q + 2) % 3][t] = wload(wr, vo, nx.o[t]);
+            }
+            extra(q);                                    // the caller's loads placed at step q
+            floatx4 A;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) A[r] = 0.f + relu(0.f + L[q][r]);
+            // the 4 tiles' chains interleaved; each tile accumulates its k values in the same order as below
+#pragma unroll
+            for (int t = 0; t < 4; ++t) Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wz[q % 3][t].x, A.x, Hs[t], 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wz[q % 3][t].y, A.y, Hs[t], 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wz[q % 3][t].z, A.z, Hs[t], 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wz[q % 3][t].w, A.w, Hs[t], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) pre[t] = wz[NTD % 3][t];
+    } else {
         const int vo = lane_id() * 16;
         float4 wq[2][4];
-        if constexpr (!ZN) {
+        {
 #pragma unroll
             for (int q = 0; q < JN - 1 && q < NTD; ++q) nload(q);
         }
@@ -1094,7 +1131,7 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
         for (int t = 0; t < 4; ++t) wq[0][t] = pre[t];
 #pragma unroll
         for (int q = 0; q < NTD; ++q) {
-            if (!ZN && q + JN - 1 < NTD) nload(q + JN - 1);
+            if (q + JN - 1 < NTD) nload(q + JN - 1);
             if (q + 1 < NTD) {
 #pragma unroll
                 for (int t = 0; t < 4; ++t) wq[(q + 1) & 1][t] = wload(wr, vo, LY::G1 / 4 + (t * NTD + q + 1) * 64);
@@ -1103,23 +1140,6 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
                 for (int t = 0; t < 4; ++t) wq[(q + 1) & 1][t] = wload(wr, vo, nx.o[t]);
             }
             extra(q);                                    // the caller's loads placed at step q
-            if constexpr (ZN) {
-                floatx4 A;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) A[r] = 0.f + relu(0.f + L[q][r]);
-                // the 4 tiles' chains interleaved (no MFMA waits on its predecessor); each tile accumulates
-                // its k values in the same order as below
-#pragma unroll
-                for (int t = 0; t < 4; ++t) Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[q & 1][t].x, A.x, Hs[t], 0, 0, 0);
-#pragma unroll
-                for (int t = 0; t < 4; ++t) Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[q & 1][t].y, A.y, Hs[t], 0, 0, 0);
-#pragma unroll
-                for (int t = 0; t < 4; ++t) Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[q & 1][t].z, A.z, Hs[t], 0, 0, 0);
-#pragma unroll
-                for (int t = 0; t < 4; ++t) Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[q & 1][t].w, A.w, Hs[t], 0, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
-                continue;
-            }
             const float4 xs4 = rs[q % JN], xt4 = rt[q % JN];
             const float sv[4] = {xs4.x, xs4.y, xs4.z, xs4.w}, tv[4] = {xt4.x, xt4.y, xt4.z, xt4.w};
             floatx4 A, Bq;
@@ -2096,7 +2116,7 @@ extern "C" int tm_encoder_train_fwd(const tm_weights *w, const float *n_feat, co
     prof_end("std_kernel", s, pe);
     const int64_t n_rows = n_walks * 3;
     pe = prof_begin(s);
-    if (!launch_gcn_fwd_reg(P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, F, s))
+    if (!launch_gcn_fwd_reg(P, w->node_zero, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, F, s))
         launch_gcn(P, w->node_zero, n_rows, lds_g, n_feat, e_feat, node6, eid3, ts3, cnt, F, s);
     TM_CHECK_LAUNCH();
     prof_end("gcn_kernel", s, pe);

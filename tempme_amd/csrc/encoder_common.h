@@ -255,8 +255,7 @@ __device__ __forceinline__ void rgemm(const Lin &L, const floatx4 (&x)[NQ], floa
 
 // the register-resident event_gcn forward of the training step (encoder_train.hip) for these dims: launched
 // on s (true), or no instance (false: the caller runs gcn_kernel)
-bool gcn_reg_enabled();
-bool launch_gcn_fwd_reg(const EncW &P, int64_t n_rows, const float *n_feat, const float *e_feat, const int32_t *node6,
+bool launch_gcn_fwd_reg(const EncW &P, int node_zero, int64_t n_rows, const float *n_feat, const float *e_feat, const int32_t *node6,
                         const int32_t *eid3, const float *ts3, const float *cnt, float *F, hipStream_t s);
 
 }  // namespace tmk

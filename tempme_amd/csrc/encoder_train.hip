@@ -728,7 +728,7 @@ struct GcnRow {
 // lin_event, A / B and event_gcn's first layer (pre-activation) of both branches; BWD also stores the event
 // features and A / B rows and dt for the weight gradients and returns the relu masks of a / b as bits.
 // tabw / tabp: the workgroup's LDS tables of the time encoder's frequency / phase on the event-feature axis.
-template <int NQE, bool BWD>
+template <int NQE, bool BWD, bool ZN = false>
 __device__ __forceinline__ GcnRow gcn_front(const EncW &P, int64_t n_rows, const float *__restrict__ n_feat,
                                             const float *__restrict__ e_feat, const int32_t *__restrict__ node6,
                                             const int32_t *__restrict__ eid3, const float *__restrict__ ts3,
@@ -786,8 +786,9 @@ __device__ __forceinline__ GcnRow gcn_front(const EncW &P, int64_t n_rows, const
     }
     // 2. A = x_s + relu(x_t + L), B = x_t + relu(x_s + L) (:93-96) K step by K step into event_gcn's first
     // layer for both branches (one weight fragment feeds both); relu masks of a / b kept as bits
-    const float4 *nrs = reinterpret_cast<const float4 *>(n_feat + (int64_t)ns * dn);
-    const float4 *nrt = reinterpret_cast<const float4 *>(n_feat + (int64_t)nt * dn);
+    // ZN (zero node features): A = B, one branch (Ht, mb unused)
+    const float4 *nrs = reinterpret_cast<const float4 *>(n_feat + (int64_t)(ZN ? 0 : ns) * dn);
+    const float4 *nrt = reinterpret_cast<const float4 *>(n_feat + (int64_t)(ZN ? 0 : nt) * dn);
     const auto wg1 = wrsrc(P.g1.w);
     const int vo = lane_id() * 16;
 #pragma unroll
@@ -803,7 +804,8 @@ __device__ __forceinline__ GcnRow gcn_front(const EncW &P, int64_t n_rows, const
             for (int t = 0; t < 4; ++t) wq[(q + 1) & 1][t] = wload(wg1, vo, (t * NTD + q + 1) * 64);
         }
         const int f4 = min(4 * q + g, dn / 4 - 1);
-        const float4 xs4 = nrs[f4], xt4 = nrt[f4];
+        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 xs4 = ZN ? z4 : nrs[f4], xt4 = ZN ? z4 : nrt[f4];
         const float xs[4] = {xs4.x, xs4.y, xs4.z, xs4.w}, xt[4] = {xt4.x, xt4.y, xt4.z, xt4.w};
         floatx4 A, Bq;
 #pragma unroll
@@ -820,7 +822,20 @@ __device__ __forceinline__ GcnRow gcn_front(const EncW &P, int64_t n_rows, const
         }
         if (BWD && valid) {
             *reinterpret_cast<float4 *>(o->AB + (r * 2) * DN + 16 * q + 4 * g) = make_float4(A[0], A[1], A[2], A[3]);
-            *reinterpret_cast<float4 *>(o->AB + (r * 2 + 1) * DN + 16 * q + 4 * g) = make_float4(Bq[0], Bq[1], Bq[2], Bq[3]);
+            if (!ZN)
+                *reinterpret_cast<float4 *>(o->AB + (r * 2 + 1) * DN + 16 * q + 4 * g) = make_float4(Bq[0], Bq[1], Bq[2], Bq[3]);
+        }
+        if constexpr (ZN) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[q & 1][t].x, A.x, Hs[t], 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[q & 1][t].y, A.y, Hs[t], 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[q & 1][t].z, A.z, Hs[t], 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) Hs[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[q & 1][t].w, A.w, Hs[t], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            continue;
         }
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -847,7 +862,89 @@ __device__ __forceinline__ GcnRow gcn_front(const EncW &P, int64_t n_rows, const
     return GcnRow{r, rc, valid, dt};
 }
 
+// the zero-node-feature tail of gcn_bwd_reg_kernel (steps 3-7 on one branch)
 template <int NQE>
+__device__ __forceinline__ void gcn_bwd_reg_zn(const EncW &P, const EncWT &T, const GcnRow &rw, const float *__restrict__ dF,
+                                               const GcnBwdOut &o, const floatx4 (&Hs)[4], uint64_t ma) {
+    constexpr int NTD = 11, DN = 16 * NTD, H = HID;
+    const int g = lane_id() >> 4, vo = lane_id() * 16, dn = P.dn;
+    const int64_t r = rw.r, rc = rw.rc;
+    const bool valid = rw.valid;
+    const float dt = rw.dt;
+    uint32_t mz = 0;
+    floatx4 dU[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const float4 b = *reinterpret_cast<const float4 *>(P.g1.b + 16 * t + 4 * g);
+        const float bb[4] = {b.x, b.y, b.z, b.w};
+        floatx4 z;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            z[s] = relu(Hs[t][s] + bb[s]);
+            mz |= (uint32_t)(z[s] > 0.f) << (4 * t + s);
+        }
+        const float4 us = *reinterpret_cast<const float4 *>(dF + rc * (2 * H) + 16 * t + 4 * g);
+        const float4 ut = *reinterpret_cast<const float4 *>(dF + rc * (2 * H) + H + 16 * t + 4 * g);
+        const float4 su = make_float4(us.x + ut.x, us.y + ut.y, us.z + ut.z, us.w + ut.w);
+        dU[t] = floatx4{valid ? su.x : 0.f, valid ? su.y : 0.f, valid ? su.z : 0.f, valid ? su.w : 0.f};
+        if (valid) {
+            *reinterpret_cast<float4 *>(o.H + (r * 2) * H + 16 * t + 4 * g) = make_float4(z[0], z[1], z[2], z[3]);
+            *reinterpret_cast<float4 *>(o.dZ + (r * 2 + 1) * H + 16 * t + 4 * g) = su;
+        }
+    }
+    asm volatile("" : "+v"(mz));
+    floatx4 dZ[4];
+    rgemm<4, 4, 4>(T.g2T, dU, dZ);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) dZ[t][s] = (mz >> (4 * t + s)) & 1u ? dZ[t][s] : 0.f;
+        if (valid)
+            *reinterpret_cast<float4 *>(o.dZ + (r * 2) * H + 16 * t + 4 * g) = make_float4(dZ[t][0], dZ[t][1], dZ[t][2], dZ[t][3]);
+    }
+    const auto wg1t = wrsrc(T.g1T.w);
+    floatx4 DL[NTD];
+#pragma unroll
+    for (int t = 0; t < NTD; ++t) {
+        float4 wf[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) wf[q] = wload(wg1t, vo, (t * 4 + q) * 64);
+        floatx4 as = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            as = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q].x, dZ[q].x, as, 0, 0, 0);
+            as = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q].y, dZ[q].y, as, 0, 0, 0);
+            as = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q].z, dZ[q].z, as, 0, 0, 0);
+            as = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[q].w, dZ[q].w, as, 0, 0, 0);
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) DL[t][s] = (ma >> (4 * t + s)) & 1u ? as[s] : 0.f;
+        if (valid)
+            *reinterpret_cast<float4 *>(o.dlev + r * DN + 16 * t + 4 * g) = make_float4(DL[t][0], DL[t][1], DL[t][2], DL[t][3]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    floatx4 GT[NTD];
+    rgemm<NTD, NTD, NTD>(T.evT, DL, GT);
+    if (valid) {
+#pragma unroll
+        for (int t = 0; t < NTD; ++t) {
+            float gv[4];
+            const float4 f4 = *reinterpret_cast<const float4 *>(P.freq + 16 * t + 4 * g);
+            const float4 h4 = *reinterpret_cast<const float4 *>(P.phase + 16 * t + 4 * g);
+            const float fv[4] = {f4.x, f4.y, f4.z, f4.w}, hv[4] = {h4.x, h4.y, h4.z, h4.w};
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int j = 16 * t + 4 * g + s;
+                gv[s] = (t < NTD - 1 || j < dn) ? -GT[t][s] * sin_rd(__fadd_rn(__fmul_rn(dt, fv[s]), hv[s])) : 0.f;
+            }
+            *reinterpret_cast<float4 *>(o.g + r * DN + 16 * t + 4 * g) = make_float4(gv[0], gv[1], gv[2], gv[3]);
+        }
+    }
+}
+
+// ZN: one branch; dZ_s + dZ_t = (M2^T (dU_s + dU_t)) * [z > 0] and d lev = (M0^T (dZ_s + dZ_t)) * [a > 0] (the
+// masks agree), stored as gcn_bwd_kernel<true> stores them (o.dZ half 0 = the dZ sum, half 1 = the dU sum)
+template <int NQE, bool ZN = false>
 __global__ void __launch_bounds__(256, 2) gcn_bwd_reg_kernel(EncW P, EncWT T, int64_t n_rows,
                                                               const float *__restrict__ n_feat,
                                                               const float *__restrict__ e_feat,
@@ -863,13 +960,17 @@ __global__ void __launch_bounds__(256, 2) gcn_bwd_reg_kernel(EncW P, EncWT T, in
     const int dn = P.dn;
     floatx4 Hs[4], Ht[4];
     uint64_t ma, mb;
-    const GcnRow rw = gcn_front<NQE, true>(P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, tabw, tabp, &o, Hs, Ht,
-                                           ma, mb);
+    const GcnRow rw = gcn_front<NQE, true, ZN>(P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, tabw, tabp, &o, Hs,
+                                               Ht, ma, mb);
     const int64_t r = rw.r, rc = rw.rc;
     const bool valid = rw.valid;
     const float dt = rw.dt;
     // 3. z = relu(MLP.0 . + b) of both branches (stored: MLP.2's inputs); 4. dU = dF (the head's gradient);
     // 5. dZ = (M2^T dU) * [z > 0]
+    if constexpr (ZN) {
+        gcn_bwd_reg_zn<NQE>(P, T, rw, dF, o, Hs, ma);
+        return;
+    }
     uint32_t mz = 0;
     floatx4 dUs[4], dUt[4];
 #pragma unroll
@@ -962,7 +1063,7 @@ __global__ void __launch_bounds__(256, 2) gcn_bwd_reg_kernel(EncW P, EncWT T, in
 // Register-resident event_gcn forward for the training step (hid_dim 64, 11 node tiles): F = [MLP(A) | MLP(B)]
 // per walk position (explainer_new.py:79-96), the front of gcn_bwd_reg_kernel plus MLP.2, with gcn_kernel's
 // accumulation order (the same F; tm_encoder_train_fwd keeps it for the head and the backward).
-template <int NQE>
+template <int NQE, bool ZN = false>
 __global__ void __launch_bounds__(256, 2) gcn_fwd_reg_kernel(EncW P, int64_t n_rows, const float *__restrict__ n_feat,
                                                               const float *__restrict__ e_feat,
                                                               const int32_t *__restrict__ node6,
@@ -974,8 +1075,27 @@ __global__ void __launch_bounds__(256, 2) gcn_fwd_reg_kernel(EncW P, int64_t n_r
     const int g = lane_id() >> 4;
     floatx4 Hs[4], Ht[4];
     uint64_t ma, mb;
-    const GcnRow rw = gcn_front<NQE, false>(P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, tabw, tabp, nullptr, Hs,
-                                            Ht, ma, mb);
+    const GcnRow rw = gcn_front<NQE, false, ZN>(P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, tabw, tabp, nullptr,
+                                                Hs, Ht, ma, mb);
+    if constexpr (ZN) {   // F = [MLP(A) | MLP(A)]
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const float4 b = *reinterpret_cast<const float4 *>(P.g1.b + 16 * t + 4 * g);
+            Hs[t] = floatx4{relu(Hs[t][0] + b.x), relu(Hs[t][1] + b.y), relu(Hs[t][2] + b.z), relu(Hs[t][3] + b.w)};
+        }
+        floatx4 Fs[4];
+        rgemm<4, 4, 4>(P.g2, Hs, Fs);
+        if (rw.valid) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float4 b = *reinterpret_cast<const float4 *>(P.g2.b + 16 * t + 4 * g);
+                const float4 v = make_float4(Fs[t][0] + b.x, Fs[t][1] + b.y, Fs[t][2] + b.z, Fs[t][3] + b.w);
+                *reinterpret_cast<float4 *>(F + rw.r * (2 * H) + 16 * t + 4 * g) = v;
+                *reinterpret_cast<float4 *>(F + rw.r * (2 * H) + H + 16 * t + 4 * g) = v;
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         const float4 b = *reinterpret_cast<const float4 *>(P.g1.b + 16 * t + 4 * g);
@@ -1111,82 +1231,6 @@ __global__ void __launch_bounds__(256) wgrad_partial_kernel(WgPlan P, float *__r
         for (int r = 0; r < 4; ++r) out[(16 * wave + 4 * g + r) * 64 + 16 * t + m] = acc[t][r];
 }
 
-// The same partial blocks with the row slabs staged TRANSPOSED in LDS ([column][row], pitch WG_TP): a lane's
-// four K values (four consecutive rows of one column) are one ds_read_b128, so a 16-row K block of a wave's
-// 2 x 2 tiles (32 x 32 of the 64 x 64 block) takes 4 LDS reads for 16 MFMAs instead of 5 reads per 4 MFMAs.
-// The rows inside a 16-row block go to the MFMAs in a different order than wgrad_partial_kernel's
-// (deterministic either way).
-constexpr int WG_TP = 68;
-__global__ void __launch_bounds__(256) wgrad_partial_t_kernel(WgPlan P, float *__restrict__ part) {
-    __shared__ __attribute__((aligned(16))) float Yt[2][64 * WG_TP], Xt[2][64 * WG_TP];
-    const int64_t bid = blockIdx.x;
-    int j = 0;
-    while (j + 1 < P.njob && bid >= P.job[j + 1].wg_begin) ++j;
-    const WgJob &J = P.job[j];
-    const int64_t local = bid - J.wg_begin;
-    const int nb = J.OB * J.IB;
-    const int chunk = (int)(local / nb), tb = (int)(local % nb), ob = tb / J.IB, ib = tb % J.IB;
-    const int o0 = ob * 64, i0 = ib * 64;
-    const int r_begin = chunk * WG_CHUNK, r_end = min(J.R, r_begin + WG_CHUNK);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, m = lane & 15;
-    const int wo = 32 * (wave >> 1), wi = 32 * (wave & 1);   // this wave's 32 x 32 quarter of the block
-    floatx4 acc[2][2];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
-    auto store_t = [&](const Slab &sl, float *Ys, float *Xs) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int e = tid + 256 * k, row = e >> 4, c = (e & 15) * 4;
-            const float yv[4] = {sl.y[k].x, sl.y[k].y, sl.y[k].z, sl.y[k].w};
-            const float xv[4] = {sl.x[k].x, sl.x[k].y, sl.x[k].z, sl.x[k].w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                Ys[(c + q) * WG_TP + row] = yv[q];
-                Xs[(c + q) * WG_TP + row] = xv[q];
-            }
-        }
-    };
-    Slab sl;
-    slab_load(J, r_begin, r_end, o0, i0, sl);
-    store_t(sl, Yt[0], Xt[0]);
-    __syncthreads();
-    int buf = 0;
-    for (int r0 = r_begin; r0 < r_end; r0 += 64) {
-        const bool more = r0 + 64 < r_end;
-        if (more) slab_load(J, r0 + 64, r_end, o0, i0, sl);
-        const float *Y = Yt[buf], *X = Xt[buf];
-#pragma unroll
-        for (int kb = 0; kb < 4; ++kb) {
-            float4 a[2], b[2];
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                a[t] = *reinterpret_cast<const float4 *>(Y + (wo + 16 * t + m) * WG_TP + 16 * kb + 4 * g);
-                b[t] = *reinterpret_cast<const float4 *>(X + (wi + 16 * t + m) * WG_TP + 16 * kb + 4 * g);
-            }
-#pragma unroll
-            for (int ot = 0; ot < 2; ++ot)
-#pragma unroll
-                for (int it = 0; it < 2; ++it) {
-                    acc[ot][it] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ot].x, b[it].x, acc[ot][it], 0, 0, 0);
-                    acc[ot][it] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ot].y, b[it].y, acc[ot][it], 0, 0, 0);
-                    acc[ot][it] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ot].z, b[it].z, acc[ot][it], 0, 0, 0);
-                    acc[ot][it] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ot].w, b[it].w, acc[ot][it], 0, 0, 0);
-                }
-        }
-        if (more) store_t(sl, Yt[buf ^ 1], Xt[buf ^ 1]);
-        __syncthreads();
-        buf ^= 1;
-    }
-    float *out = part + J.part_begin + local * 4096;
-#pragma unroll
-    for (int ot = 0; ot < 2; ++ot)
-#pragma unroll
-        for (int it = 0; it < 2; ++it)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) out[(wo + 16 * ot + 4 * g + r) * 64 + wi + 16 * it + m] = acc[ot][it][r];
-}
 
 __global__ void wgrad_reduce_kernel(WgPlan P, const float *__restrict__ part) {
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < P.total_out; e += (int64_t)gridDim.x * blockDim.x) {
@@ -1607,15 +1651,14 @@ extern "C" int tm_encoder_train_supported(int32_t de, int32_t dn, int32_t h, int
     return head_bwd_tr(P) && gcn_bwd_lds(P) <= lim && gate <= lim ? 1 : 0;
 }
 
-// the register-resident event_gcn backward runs (opt-in, dims it has an instance for); it has no zero-node form
+// the register-resident event_gcn backward runs (the dims it has an instance for; the LDS-tiled one otherwise)
 static bool gcn_bwd_uses_reg(const tm_weights *w) {
     const EncW &P = w->P;
     const int nqe = r16(P.kev) / 16;
     return P.h == HID && r16(P.dn) == 176 && P.dn % 4 == 0 && P.de % 4 == 0 && nqe >= 11 && nqe <= 14 &&
            P.g1.nt == 4 && P.g1.nq == 11 && w->T.g2T.nt == 4 && w->T.g1T.nt == 11 && w->T.g1T.nq == 4 &&
-           w->T.evT.nt == 11 && w->T.evT.nq == 11 && P.ev.nq == nqe && gcn_reg_enabled();
+           w->T.evT.nt == 11 && w->T.evT.nq == 11 && P.ev.nq == nqe;
 }
-static bool zn_reg_bypass(const tm_weights *w) { return gcn_bwd_uses_reg(w); }
 
 extern "C" int tm_encoder_bwd(const tm_weights *w, const float *n_feat, const float *e_feat, int32_t n_groups,
                               int32_t B, int32_t W, const int32_t *node6, const int32_t *eid3, const float *ts3,
@@ -1655,15 +1698,20 @@ extern "C" int tm_encoder_bwd(const tm_weights *w, const float *n_feat, const fl
     pe = prof_begin(s);
     const int nqe = r16(P.kev) / 16;
     // register-resident instance: hid_dim 64, 11 node-feature tiles (dn 161..176, a multiple of 4), lin_event
-    // with 11..14 K steps; the LDS-tiled kernel otherwise.  Opt-in (TEMPME_GCN_REG=1) until it has been
-    // checked on the GPU (written in round 4 while the GPU pool was unavailable to this build)
+    // with 11..14 K steps; the LDS-tiled kernel otherwise
     const bool reg = gcn_bwd_uses_reg(w);
     if (reg) {
         const unsigned blocks = (unsigned)((n_rows + 63) / 64);
-        if (nqe == 11) gcn_bwd_reg_kernel<11><<<dim3(blocks), 256, 0, s>>>(P, w->T, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, io->dF, go);
-        else if (nqe == 12) gcn_bwd_reg_kernel<12><<<dim3(blocks), 256, 0, s>>>(P, w->T, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, io->dF, go);
-        else if (nqe == 13) gcn_bwd_reg_kernel<13><<<dim3(blocks), 256, 0, s>>>(P, w->T, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, io->dF, go);
-        else gcn_bwd_reg_kernel<14><<<dim3(blocks), 256, 0, s>>>(P, w->T, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, io->dF, go);
+#define TM_BWD_REG(Q)                                                                                              \
+        (w->node_zero ? gcn_bwd_reg_kernel<Q, true><<<dim3(blocks), 256, 0, s>>>(P, w->T, n_rows, n_feat, e_feat, node6, \
+                                                                                 eid3, ts3, cnt, io->dF, go)          \
+                      : gcn_bwd_reg_kernel<Q, false><<<dim3(blocks), 256, 0, s>>>(P, w->T, n_rows, n_feat, e_feat, node6, \
+                                                                                  eid3, ts3, cnt, io->dF, go))
+        if (nqe == 11) TM_BWD_REG(11);
+        else if (nqe == 12) TM_BWD_REG(12);
+        else if (nqe == 13) TM_BWD_REG(13);
+        else TM_BWD_REG(14);
+#undef TM_BWD_REG
     } else if (w->node_zero) {
         gcn_bwd_kernel<true><<<dim3((unsigned)((n_rows + TILE_ROWS - 1) / TILE_ROWS)), 256, lg, s>>>(
             P, w->T, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, io->dF, go);
@@ -1676,25 +1724,26 @@ extern "C" int tm_encoder_bwd(const tm_weights *w, const float *n_feat, const fl
     return TM_OK;
 }
 
-// TEMPME_GCN_REG=1: the register-resident event_gcn forward / backward (gcn_fwd_reg_kernel, gcn_bwd_reg_kernel)
-bool tmk::gcn_reg_enabled() {   // read per launch (tests switch it inside one process)
-    const char *v = std::getenv("TEMPME_GCN_REG");
-    return v != nullptr && std::string(v) == "1";
-}
-
-bool tmk::launch_gcn_fwd_reg(const EncW &P, int64_t n_rows, const float *n_feat, const float *e_feat,
+// the register-resident event_gcn training forward (gcn_fwd_reg_kernel) for the dims it has an instance for:
+// 8 % faster per training step than the LDS-tiled gcn_kernel / gcn_bwd_kernel (round 5, tools/train_flags_ab.sh)
+bool tmk::launch_gcn_fwd_reg(const EncW &P, int node_zero, int64_t n_rows, const float *n_feat, const float *e_feat,
                              const int32_t *node6, const int32_t *eid3, const float *ts3, const float *cnt, float *F,
                              hipStream_t s) {
     const int nqe = r16(P.kev) / 16;
     if (!(P.h == HID && r16(P.dn) == 176 && P.dn % 4 == 0 && P.de % 4 == 0 && nqe >= 11 && nqe <= 14 &&
-          P.ev.nt == 11 && P.ev.nq == nqe && P.g1.nt == 4 && P.g1.nq == 11 && P.g2.nt == 4 && P.g2.nq == 4) ||
-        !gcn_reg_enabled())
+          P.ev.nt == 11 && P.ev.nq == nqe && P.g1.nt == 4 && P.g1.nq == 11 && P.g2.nt == 4 && P.g2.nq == 4))
         return false;
     const unsigned blocks = (unsigned)((n_rows + 63) / 64);
-    if (nqe == 11) gcn_fwd_reg_kernel<11><<<dim3(blocks), 256, 0, s>>>(P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, F);
-    else if (nqe == 12) gcn_fwd_reg_kernel<12><<<dim3(blocks), 256, 0, s>>>(P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, F);
-    else if (nqe == 13) gcn_fwd_reg_kernel<13><<<dim3(blocks), 256, 0, s>>>(P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, F);
-    else gcn_fwd_reg_kernel<14><<<dim3(blocks), 256, 0, s>>>(P, n_rows, n_feat, e_feat, node6, eid3, ts3, cnt, F);
+#define TM_FWD_REG(Q)                                                                                              \
+    (node_zero ? gcn_fwd_reg_kernel<Q, true><<<dim3(blocks), 256, 0, s>>>(P, n_rows, n_feat, e_feat, node6, eid3, ts3, \
+                                                                          cnt, F)                                    \
+               : gcn_fwd_reg_kernel<Q, false><<<dim3(blocks), 256, 0, s>>>(P, n_rows, n_feat, e_feat, node6, eid3, ts3, \
+                                                                           cnt, F))
+    if (nqe == 11) TM_FWD_REG(11);
+    else if (nqe == 12) TM_FWD_REG(12);
+    else if (nqe == 13) TM_FWD_REG(13);
+    else TM_FWD_REG(14);
+#undef TM_FWD_REG
     return true;
 }
 
@@ -1756,12 +1805,9 @@ static int run_wgrad(const tm_wgrad_job *jobs, int njob, const tm_wgrad_target *
     float *part = reinterpret_cast<float *>(scratch((size_t)pb * sizeof(float), s));
     if (!part) return fail(TM_E_HIP, std::string(what) + ": scratch allocation failed");
     hipEvent_t pe = prof_begin(s);
-    // the transposed-LDS form is opt-in (TEMPME_WGRAD_T=1) until it has been checked on the GPU
-    const char *wt = std::getenv("TEMPME_WGRAD_T");
-    if (wt != nullptr && std::string(wt) == "1")
-        wgrad_partial_t_kernel<<<dim3((unsigned)wg), 256, 0, s>>>(P, part);
-    else
-        wgrad_partial_kernel<<<dim3((unsigned)wg), 256, 0, s>>>(P, part);
+    // (a transposed-LDS form of the partials, 2 x 2 tiles per wave, measured 1.3 % slower per training step in
+    // round 5: tools/patches/training_variants.patch)
+    wgrad_partial_kernel<<<dim3((unsigned)wg), 256, 0, s>>>(P, part);
     TM_CHECK_LAUNCH();
     prof_end("wgrad_partial_kernel", s, pe);
     pe = prof_begin(s);
@@ -1790,7 +1836,7 @@ extern "C" int tm_encoder_wgrad(const tm_weights *w, int32_t n_groups, int32_t B
     const int dn = w->dn, kev = w->P.kev, KE = r16(kev), DN = r16(dn), KM = r16(hm);
     const float *F = reinterpret_cast<const float *>(workspace);
     // zero node features (gcn_bwd_kernel<true>): one row pair per position for MLP.0 / MLP.2, the branch sums
-    const bool zn = w->node_zero && !zn_reg_bypass(w);
+    const bool zn = w->node_zero;   // both event_gcn backward kernels have the zero-node form
     const tm_wgrad_job zn0{io->dZ, io->AB, 2 * h, 2 * DN, h, dn, R}, zn2{io->dZ + h, io->H, 2 * h, 2 * h, h, h, R};
     const tm_wgrad_job jobs[] = {
         {io->dlev, io->ev, DN, KE, dn, kev, R},            // lin_event

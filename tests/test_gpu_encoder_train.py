@@ -55,9 +55,12 @@ def _inputs(de, G, B, N, seed, zero_nodes=False):
     return n_feat, e_feat, node6, eid3, ts3, cat, cut, cnt
 
 
+# de = 32 runs the register-resident event_gcn kernels (hid_dim 64, 4 | de), de = 1 the LDS-tiled ones; zn = zero
+# node features (both kernels' one-branch forms)
 @pytest.mark.parametrize("de,G,B,N,train,zn", [(32, 3, 20, 20, True, False), (1, 2, 7, 5, True, False),
                                                (32, 1, 9, 20, False, False), (32, 3, 20, 20, True, True),
-                                               (32, 1, 9, 20, False, True)])
+                                               (32, 1, 9, 20, False, True), (1, 2, 7, 5, True, True),
+                                               (172, 2, 11, 20, True, False)])
 def test_encoder_backward_matches_autograd(dev, de, G, B, N, train, zn):
     """Forward within 1e-5 and all 22 gradients within 2e-4 of fp64 autograd through the oracle; zn: zero node
     features, i.e. gcn_kernel / gcn_bwd_kernel's one-branch forms and the summed MLP.0 / MLP.2 weight-gradient rows."""

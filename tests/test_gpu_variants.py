@@ -1,26 +1,17 @@
-"""GPU validation of the round-4 paths that are opt-in until they have run on an MI355X (they were written
-while the GPU pool was closed to this build): each against the validated default path or the oracle.
-Skipped unless TEMPME_VALIDATE_PENDING=1 (``tools/gpu_run.sh pending``); once green, the flags become
-defaults.
+"""GPU checks of alternative forms of the training and GraphMixer paths, each against the oracle or the default
+form (written in round 4, validated on the MI355X in round 5; the register-resident event_gcn training kernels,
+now the default for hid_dim 64, are covered by tests/test_gpu_encoder_train.py):
 
-* TEMPME_GCN_REG=1 -- gcn_fwd_reg_kernel / gcn_bwd_reg_kernel (register-resident event_gcn training
-  forward and backward) and TEMPME_WGRAD_T=1 -- wgrad_partial_t_kernel: the encoder backward test against
-  fp64 autograd through the oracle, with the flags on.
-* TEMPME_EXPLAIN_PAD=1 -- the padding mask from tm_explain_train_fwd_pad: bitwise the torch mask.
-* TEMPME_GM_BWD8=1 -- gm_bwd_kernel with 8 waves (N > 16): the d ew test against fp64 autograd through
-  the oracle, with the flag on.
-* GraphedTrainStep(overlap_prepare=True): the graph with the base contrast on a second branch = eager.
-* TEMPME_DROPIN_EXT=1 -- the C++ drop-in host side: tests/test_gpu_enron.py's cpp test runs instead of
-  skipping when the runner sets it."""
-import os
+* the padding mask from tm_explain_train_fwd_pad (the default): bitwise the torch mask;
+* gm_bwd_kernel with 8 waves (N > 16): the d ew test against fp64 autograd through the oracle;
+* GraphedTrainStep(overlap_prepare=False): the graph without the base contrast's second branch = eager (the
+  default, with the branch, is tests/test_gpu_train.py::test_graphed_step_equals_eager)."""
 
 import numpy as np
 import pytest
 import torch
 
-pytestmark = [pytest.mark.gpu,
-              pytest.mark.skipif(os.environ.get("TEMPME_VALIDATE_PENDING") != "1",
-                                 reason="round-4 opt-in paths: TEMPME_VALIDATE_PENDING=1 runs them")]
+pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
@@ -28,14 +19,6 @@ def dev():
     if not torch.cuda.is_available():
         pytest.fail("gpu tests need a HIP device")
     return torch.device("cuda", 0)
-
-
-@pytest.mark.parametrize("de,G,B,N,train", [(32, 3, 20, 20, True), (32, 1, 9, 20, False), (172, 2, 11, 20, True)])
-def test_gcn_reg_and_wgrad_t_match_autograd(dev, monkeypatch, de, G, B, N, train):
-    from tests.test_gpu_encoder_train import test_encoder_backward_matches_autograd as check
-    monkeypatch.setenv("TEMPME_GCN_REG", "1")
-    monkeypatch.setenv("TEMPME_WGRAD_T", "1")
-    check(dev, de, G, B, N, train, False)
 
 
 def test_explain_pad_kernel_equals_torch_mask(dev, monkeypatch):
@@ -75,13 +58,13 @@ def test_gm_bwd_8_waves_vs_oracle(dev, monkeypatch, N, C, L):
     check(dev, N, C, L)
 
 
-def test_graphed_step_with_prepare_branch_equals_eager(dev, monkeypatch):
+def test_graphed_step_without_prepare_branch_equals_eager(dev, monkeypatch):
     from tempme_amd import train as T
     from tests import test_gpu_train as TT
     orig = T.GraphedTrainStep.__init__
 
     def init(self, *a, **kw):
-        kw.setdefault("overlap_prepare", True)
+        kw.setdefault("overlap_prepare", False)
         orig(self, *a, **kw)
     monkeypatch.setattr(T.GraphedTrainStep, "__init__", init)
     TT.test_graphed_step_equals_eager(dev)

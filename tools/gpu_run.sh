@@ -67,20 +67,18 @@ for s in "$@"; do
                 --master-addr 127.0.0.1 --master-port 29512 bench_train.py --gpus 2 --steps 5 --warmup 1 ;;
         n30) step bench_n30 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --n-degree 30 ;;
         phases) step phases 300 python tools/train_phases.py ;;
-        pending) TEMPME_VALIDATE_PENDING=1 TEMPME_DROPIN_EXT=1 step pytest_pending 600 python -u -m pytest tests/test_gpu_pending.py tests/test_gpu_enron.py -x -v -m gpu --timeout 300 --timeout-method thread -k "pending or cpp_host" ;;
         trainflags) step train_flags 1100 ./tools/train_flags_ab.sh ;;
         gmab) step gm_ab 900 ./tools/gm_ab.sh ;;
         gmbab) step gmb_ab 900 ./tools/gmb_ab.sh ;;
-        gmbwd) step gm_bwd 300 python tools/gm_bwd_timing.py && TEMPME_GM_BWD4=1 step gm_bwd4 300 python tools/gm_bwd_timing.py ;;
+        gmbwd) step gm_bwd 300 python tools/gm_bwd_timing.py && TEMPME_GM_BWD8=1 step gm_bwd8 300 python tools/gm_bwd_timing.py ;;
         trainops) step trainops 300 python tools/train_ops.py ;;
         c2) step bench_c2 600 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config 2 ;;
         c4) step bench_c4 900 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config 4 ;;
         a3) step bench_a3 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --alpha 3.0 ;;
         dropint) step dropint 300 python tools/dropin_timing.py ;;
-        dropintx) TEMPME_DROPIN_EXT=1 step dropintx 300 python tools/dropin_timing.py ;;
         diag) step overlap_diag 300 python -u tools/overlap_diag.py ;;
         testsall) step pytest_gpu_all 1100 python -u -m pytest tests -q -m gpu -rfEs --timeout 300 --timeout-method thread ;;
-        pendingall) TEMPME_VALIDATE_PENDING=1 TEMPME_DROPIN_EXT=1 step pytest_pending 600 python -u -m pytest tests/test_gpu_pending.py tests/test_gpu_enron.py -v -m gpu -rfEs --timeout 300 --timeout-method thread -k "pending or cpp_host" ;;
+        variants) step pytest_variants 600 python -u -m pytest tests/test_gpu_variants.py tests/test_gpu_enron.py -v -m gpu -rfEs --timeout 300 --timeout-method thread -k "variants or cpp_host" ;;
         dropintrace) step dropintrace 300 rocprofv3 --kernel-trace -d gpurun_out/ditrace -o run --output-format csv -- python tools/dropin_timing.py ;;
         dropinprof) TEMPME_DROPIN_PROFILE=1 step dropinprof 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
         abtests:*)  # the GPU suite against tempme_amd/lib/ab/<name>.so

@@ -12,8 +12,5 @@ run() {  # run <label> <env...> -- <extra args>
 for r in 1 2; do
     run base X=0 --
     run nozn X=0 -- --no-node-zero
-    run gcn_reg TEMPME_GCN_REG=1 --
-    run wgrad_t TEMPME_WGRAD_T=1 --
-    run overlap X=0 -- --overlap-prepare
-    run all TEMPME_GCN_REG=1 TEMPME_WGRAD_T=1 TEMPME_EXPLAIN_PAD=1 -- --overlap-prepare
+    run no_overlap X=0 -- --no-overlap-prepare
 done
