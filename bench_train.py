@@ -23,20 +23,29 @@ import numpy as np
 import torch
 
 
-def kernel_flops(ex, B, N, M):
-    """Algorithmic FLOPs per launch of the training step's encoder kernels (one launch covers the three sides of
-    a batch: R = 3 B W walk positions x 3, n = 3 B W walks).  gcn_bwd_kernel per position: the recomputed
-    lin_event (kev x dn) and event_gcn first layer on both branches (2 dn h), then d MLP.2 (2 h h), d MLP.0 (2 h dn)
-    and the time-feature gradient through lin_event (dn x dn).  gcn_kernel per position: lin_event + both
-    branches of the two MLP layers."""
-    de, dn, h = ex.edge_dim, ex.node_dim, ex.hid_dim
+def kernel_flops(ex, B, N, M, zn=False):
+    """Algorithmic FLOPs per training step of the encoder kernels (one launch each covers the three sides of a
+    batch: n = 3 B W walks, R = 3 n walk positions; the explanation's gate runs on R positions too).
+    gcn_bwd_kernel per position: the recomputed lin_event (kev x dn) and event_gcn first layer (br branches of
+    dn x h), then d MLP.2 (h x h per branch), d MLP.0 (h x dn per branch) and the time-feature gradient through
+    lin_event (dn x dn); gcn_kernel per position: lin_event + the two MLP layers per branch.  zn: zero node
+    features, the kernels' one-branch forms (br = 1; the branch sums fold before the GEMMs).
+    wgrad_partial_kernel: dW = dY^T [X | 1] over the rows of every weight-gradient job of the step (the
+    encoder's 12 jobs and the gate's 4; tm_encoder_wgrad / tm_explain_train_bwd), 2 rows O (I + 1) each."""
+    de, dn, h, hm = ex.edge_dim, ex.node_dim, ex.hid_dim, ex.mlp_dim
     kev = de + 3 + dn
     W = N * M
     n = 3 * B * W
     R = 3 * n
-    gcn_bwd = R * 2 * (kev * dn + 2 * dn * h + 2 * h * h + 2 * h * dn + dn * dn)
-    gcn = R * 2 * (kev * dn + 2 * dn * h + 2 * h * h)
-    return {"gcn_bwd_kernel": gcn_bwd, "gcn_kernel": gcn}
+    br = 1 if zn else 2
+    gcn_bwd = R * 2 * (kev * dn + br * dn * h + br * h * h + br * h * dn + dn * dn)
+    gcn = R * 2 * (kev * dn + br * dn * h + br * h * h)
+    h2 = 2 * h
+    rows = br * R
+    enc = (R * dn * (kev + 1) + rows * h * (dn + 1) + rows * h * (h + 1) + n * h2 * (h2 + 1) + 2 * n * h2 * (h2 + 1)
+           + n * h * (h2 + 1) + n * h * (h + 1) + n * hm * (hm + 1) + n * h * (hm + 1) + n * (h + 1) + R * dn * 2)
+    gate = R * h * (de + dn + 1) + R * (h // 2) * (h + 1) + R * (h // 2 + 1) + R * dn * 2
+    return {"gcn_bwd_kernel": gcn_bwd, "gcn_kernel": gcn, "wgrad_partial_kernel": 2 * (enc + gate)}
 
 
 def main():
@@ -55,9 +64,9 @@ def main():
     ap.add_argument("--no-fused-adam", action="store_true", help="torch's default (foreach) Adam")
     ap.add_argument("--no-node-zero", action="store_true",
                     help="do not use the zero-node-feature kernel forms (A/B; the graph's node features are zeros)")
-    ap.add_argument("--no-overlap-prepare", action="store_true",
-                    help="graphed step without the base model's original contrast as a second graph branch "
-                         "(GraphedTrainStep(overlap_prepare=False))")
+    ap.add_argument("--overlap-prepare", action="store_true",
+                    help="graphed step with the base model's original contrast as a second graph branch "
+                         "(GraphedTrainStep(overlap_prepare=True); measured within noise, round 5)")
     ap.add_argument("--global-batches", type=int, default=8,
                     help="reference batches per timed step over ALL ranks (strong scaling: each rank steps through "
                          "global-batches / N of them, one all-reduced Adam update per round of N batches)")
@@ -142,7 +151,7 @@ def main():
         rows = [r for r in rows if r.numel() == B]
         n_steps = min(n_steps, len(rows))
         graphed = GraphedTrainStep(ex, base, opt, buf, s_d, d_d, t_d, e_d, rows[:max(args.warmup, 1)],
-                                   grad_sync=sync, overlap_prepare=not args.no_overlap_prepare)
+                                   grad_sync=sync, overlap_prepare=args.overlap_prepare)
 
         def step(k):   # one timed step = per_step replays
             out = None
@@ -208,21 +217,32 @@ def main():
                           "batch_size": B, "train_events": int(len(src)), "parallelism": f"dp{world}",
                           "global_batches_per_step": per_step * world, "train_steps_per_rank_per_step": per_step,
                           "allreduce_overlap": (not args.no_overlap) and not use_graph,
-                          "hip_graph": use_graph, "overlap_prepare": bool(not args.no_overlap_prepare and use_graph),
+                          "hip_graph": use_graph, "overlap_prepare": bool(args.overlap_prepare and use_graph),
                           "zero_node_forms": bool(getattr(ex, "_node_zero", False)) and ex.node_zero_specialization,
                           "grad_bucket_floats": sum(p.numel() for p in ex.parameters() if p.grad is not None)},
                "loss_first_last": [round(losses[0], 5), round(losses[-1], 5)],
                "kernels": {k: {"avg_ms": round(ms / max(c, 1), 4), "launches": c} for k, (ms, c) in prof.items()},
                "kernels_source": kern_src}
-        fl = kernel_flops(ex, B, N, M)
-        dom = max(((k, v) for k, v in out["kernels"].items() if k in fl), key=lambda kv: kv[1]["avg_ms"] * kv[1]["launches"],
-                  default=None)
-        if dom is not None:
-            k, v = dom
-            ach = fl[k] / (v["avg_ms"] * 1e-3) / 1e12
-            out["roofline"] = {"kernel": k, "bound": "mfma", "achieved": round(ach, 2), "peak": 157.3, "unit": "TFLOP/s",
-                               "frac": round(ach / 157.3, 4), "flop_per_launch": fl[k],
-                               "note": "algorithmic FLOPs of one launch (bench_train.kernel_flops) / its average time"}
+        zn = bool(getattr(ex, "_node_zero", False)) and ex.node_zero_specialization
+        fl = kernel_flops(ex, B, N, M, zn=zn)
+        # per kernel: its FLOPs per training step over its time per training step (the kernel table's launches
+        # cover the steps the table was taken over; wgrad_partial_kernel has two launches per step)
+        n_tab = len(eager) if use_graph and kern_src != "timed steps" else (n_timed - args.warmup) * per_step
+        roofs = {}
+        for k, f in fl.items():
+            v = out["kernels"].get(k)
+            if not v:
+                continue
+            per_step_ms = v["avg_ms"] * v["launches"] / max(n_tab, 1)
+            ach = f / (per_step_ms * 1e-3) / 1e12
+            roofs[k] = {"bound": "mfma", "achieved": round(ach, 2), "peak": 157.3, "unit": "TFLOP/s",
+                        "frac": round(ach / 157.3, 4), "flop_per_step": f, "ms_per_step": round(per_step_ms, 4)}
+        if roofs:
+            dom = max(roofs, key=lambda k: roofs[k]["ms_per_step"])
+            out["roofline"] = dict(roofs[dom], kernel=dom,
+                                   note="algorithmic FLOPs per training step (bench_train.kernel_flops) / the "
+                                        "kernel's time per training step")
+            out["rooflines"] = roofs
         print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()

@@ -354,6 +354,12 @@ void tm_dropin_free(tm_dropin *d);
 /* Use the caller's stream as side stream k (0..2) -- e.g. a torch stream, so that the caller's allocator
  * can hand out a call's outputs from that stream's pool -- instead of the context's own. */
 int tm_dropin_set_stream(tm_dropin *d, int32_t k, void *stream);
+/* A per-edge-id cache of the dependency-gate factor for edge ids [0, n_edge_rows) (the edge-feature table's
+ * rows; 0 = none): tm_dropin_forward's out_gfac then reads the factor of every walk position whose (edge id,
+ * fp32 time) was computed before and computes only the others (explainer_new.py:367-386 is a function of
+ * (E[e], t) alone: the results are bit-identical).  Emptied whenever the weights (tm_weights_pack /
+ * _variant / _set_node_zero) or the edge-feature table change. */
+int tm_dropin_gate_cache(tm_dropin *d, int64_t n_edge_rows);
 /* TempME.forward (explainer_new.py:174-201) for one call (B events x W walks) in one library call on side
  * stream k: with sync != 0 every side stream first waits (once) for `stream` (weights / tables prepared
  * there, or a device cut tensor); the cut times come from the host (cut_host, sent as kernel arguments;

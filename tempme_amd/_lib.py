@@ -39,7 +39,7 @@ EXPORTS = (
     "tm_encoder_workspace_bytes",
     "tm_encoder_fwd", "tm_encoder_fwd_tab", "tm_encoder_train_supported", "tm_encoder_train_fwd", "tm_encoder_bwd", "tm_encoder_wgrad", "tm_wgrad",
     "tm_explain_train_fwd", "tm_explain_train_fwd_pad", "tm_explain_train_bwd", "tm_kl_loss", "tm_edge_importance", "tm_edge_gate_table",
-    "tm_edge_table_cols", "tm_edge_tables", "tm_edge_feature_table", "tm_edge_importance_tab", "tm_tgn_attn_fwd", "tm_tgn_attn_bwd", "tm_gm_packed_floats", "tm_gm_pack", "tm_gm_embed", "tm_gm_embed_bwd_ok", "tm_gm_embed_bwd", "tm_gm_packed_a_floats", "tm_gm_pack_a", "tm_gm_fused_ok", "tm_dropin_create", "tm_dropin_free", "tm_dropin_forward", "tm_dropin_set_stream", "tm_edge_importance_gf", "tm_edge_importance_gf3", "tm_edge_importance_gf3_bern",
+    "tm_edge_table_cols", "tm_edge_tables", "tm_edge_feature_table", "tm_edge_importance_tab", "tm_tgn_attn_fwd", "tm_tgn_attn_bwd", "tm_gm_packed_floats", "tm_gm_pack", "tm_gm_embed", "tm_gm_embed_bwd_ok", "tm_gm_embed_bwd", "tm_gm_packed_a_floats", "tm_gm_pack_a", "tm_gm_fused_ok", "tm_dropin_create", "tm_dropin_free", "tm_dropin_forward", "tm_dropin_set_stream", "tm_dropin_gate_cache", "tm_edge_importance_gf", "tm_edge_importance_gf3", "tm_edge_importance_gf3_bern",
     "tm_mask_least_important", "tm_profile_enable", "tm_profile_sync", "tm_profile_entry",
     "tm_beta_params", "tm_beta_rsample_bwd",
 )
@@ -170,6 +170,7 @@ def _sig(L):
     L.tm_dropin_free.argtypes = [vp]
     L.tm_dropin_forward.argtypes = [vp, i32, i32, vp, vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.tm_dropin_set_stream.argtypes = [vp, i32, vp]
+    L.tm_dropin_gate_cache.argtypes = [vp, i64]
     L.tm_edge_importance_gf.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.tm_edge_importance_gf3.argtypes = [i32, i32, i32] + [vp] * 24
     L.tm_edge_importance_gf3_bern.argtypes = [i32, i32, i32] + [vp] * 26

@@ -201,24 +201,12 @@ __device__ __forceinline__ int32_t draw(Key k, uint32_t stage, uint32_t event, u
 // hardware v_cos_f32 (input in revolutions).  Max abs error vs cos of the same fp32 argument 1.8e-7
 // over the time encoder's whole argument range (micro/cosacc.hip, profiles/r03_cos_accuracy.txt: the
 // round-2 fp64-reduction + r^12 polynomial form measured 1.5e-7 at about twice the VALU cost; torch's
-// cosf 3.6e-8).  No slow path, so it interleaves with the MFMAs it feeds.
-#ifndef TM_COS_DF
-#define TM_COS_DF 0
-#endif
+// cosf 3.6e-8).  No slow path, so it interleaves with the MFMAs it feeds.  (An fp32-only reduction measured
+// 0.8 % faster in walk_kernel at 3.0e-7 max error, not adopted: tools/patches/cos_fp32.patch.)
 __device__ __forceinline__ float cos_rd(float xf) {
-#if TM_COS_DF
-    // fp32 only: x / (2 pi) as the exact product x * C_HI (p + e, e by an fma) plus x * C_LO, C_HI + C_LO =
-    // 1 / (2 pi); p - rint(p) is exact.  Max abs error 3.0e-7 over the argument range (vs 1.0e-7), no fp64
-    const float C_HI = 0.15915494f, C_LO = 6.4206382e-09f;
-    const float p = xf * C_HI;
-    const float e = __builtin_fmaf(xf, C_HI, -p);
-    const float f = (p - __builtin_rintf(p)) + __builtin_fmaf(xf, C_LO, e);
-    return __builtin_amdgcn_cosf(f);
-#else
     const double u = (double)xf * 0.15915494309189533577;
     const double f = u - __builtin_rint(u);
     return __builtin_amdgcn_cosf((float)f);
-#endif
 }
 
 // sin of an fp32 argument, the same branch-free reduction (fp64, in revolutions) and the hardware v_sin_f32

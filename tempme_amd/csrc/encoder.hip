@@ -1540,16 +1540,27 @@ __global__ void __launch_bounds__(256) gate_table_kernel(EncW P, int32_t n_ids, 
 // Per-position mode (row_eid != nullptr, tm_dropin_forward): column = walk position r of the call, its edge
 // id row_eid[r] and raw time row_t[r] (:371) instead of edge id r and its timestamp; gf[r] = the position's
 // gate factor (the same arithmetic as per edge id: the drop-in equals the pipeline bit for bit).
+// List mode (list != nullptr, per-position mode only): column i takes position list[i] for i < *list_n (the
+// gate-cache misses of tm_dropin_forward) and also stores (t, gate factor) in cache[edge id] (gate_cache_pack).
+__device__ __forceinline__ unsigned long long gate_cache_pack(float t, float f) {
+    return ((unsigned long long)__float_as_uint(t) << 32) | (unsigned long long)__float_as_uint(f);
+}
 template <int NQ, int NQX = 0, int NQL = 1>
 __global__ void __launch_bounds__(256) gate_reg_kernel(EncW P, int32_t n_ids, const double *__restrict__ ets,
                                                        const float *__restrict__ e_feat, float *__restrict__ gf,
                                                        float *__restrict__ etab = nullptr,
                                                        const int32_t *__restrict__ row_eid = nullptr,
-                                                       const float *__restrict__ row_t = nullptr) {
+                                                       const float *__restrict__ row_t = nullptr,
+                                                       const int32_t *__restrict__ list = nullptr,
+                                                       const uint32_t *__restrict__ list_n = nullptr,
+                                                       unsigned long long *__restrict__ cache = nullptr,
+                                                       int64_t n_cache = 0) {
     const int lane = threadIdx.x & 63, col = lane & 15, g = lane_id() >> 4;
-    const int64_t e = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + col;
-    if (((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 >= n_ids) return;   // wave-uniform
-    const bool valid = e < n_ids;
+    const int64_t i0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16;
+    if (list) n_ids = (int32_t)*list_n;
+    if (i0 >= n_ids) return;                             // wave-uniform
+    const bool valid = i0 + col < n_ids;
+    const int64_t e = !list ? i0 + col : valid ? (int64_t)list[i0 + col] : 0;
     const int64_t ec = !valid ? 0 : row_eid ? (int64_t)row_eid[e] : e;
     const int de = P.de, kdep = P.kdep;
     // no timestamps: edge table only (gf is null too)
@@ -1609,7 +1620,45 @@ __global__ void __launch_bounds__(256) gate_reg_kernel(EncW P, int32_t n_ids, co
     z += __shfl_xor(z, 16);
     z += __shfl_xor(z, 32);
     z += P.d3b[0];
-    if (gf && valid && g == 0) gf[e] = P.dep ? 0.5f + 0.5f * (1.f / (1.f + expf(-z))) : 1.f;
+    if (gf && valid && g == 0) {
+        const float f = P.dep ? 0.5f + 0.5f * (1.f / (1.f + expf(-z))) : 1.f;
+        gf[e] = f;
+        if (cache && ec >= 0 && ec < n_cache && __float_as_uint(t) != 0xFFFFFFFFu)
+            __atomic_store_n(&cache[ec], gate_cache_pack(t, f), __ATOMIC_RELAXED);
+    }
+}
+
+// The drop-in's gate-factor cache (tm_dropin_gate_cache): per walk position, a hit on (edge id, exact fp32 time)
+// gives the factor gate_reg_kernel computed for it; the misses go to a list (one atomic per wave) that the list
+// mode of gate_reg_kernel computes and stores.  The factor is a function of (E[e], t) alone, so the result equals
+// the uncached path's bit for bit.
+__global__ void __launch_bounds__(256) gate_cache_lookup_kernel(int64_t n_pos, const int32_t *__restrict__ eid,
+                                                                const float *__restrict__ ts,
+                                                                const unsigned long long *__restrict__ cache,
+                                                                int64_t n_cache, float *__restrict__ gf,
+                                                                int32_t *__restrict__ list, uint32_t *__restrict__ list_n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    bool miss = false;
+    if (i < n_pos) {
+        const int32_t e = eid[i];
+        const uint32_t tb = __float_as_uint(ts[i]);
+        miss = true;
+        if (e >= 0 && e < n_cache && tb != 0xFFFFFFFFu) {
+            const unsigned long long v = __atomic_load_n(&cache[e], __ATOMIC_RELAXED);
+            if ((uint32_t)(v >> 32) == tb) {
+                gf[i] = __uint_as_float((uint32_t)v);
+                miss = false;
+            }
+        }
+    }
+    const unsigned long long m = __ballot(miss);
+    if (m == 0) return;
+    const int first = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(list_n, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl(base, first);
+    if (miss) list[base + __popcll(m & ((1ull << lane) - 1))] = (int32_t)i;
 }
 
 // threads per (group, event) workgroup of explain_tab_kernel (its loops stride by blockDim.x): one wave
@@ -1808,11 +1857,13 @@ extern "C" int tm_weights_create_ex(int32_t de, int32_t dn, int32_t h, int32_t i
 extern "C" int tm_weights_set_node_zero(tm_weights *w, int32_t node_zero) {
     if (!w) return fail(TM_E_ARG, "tm_weights_set_node_zero: NULL weights");
     w->node_zero = node_zero ? 1 : 0;
+    ++w->version;
     return TM_OK;
 }
 
 extern "C" int tm_weights_variant(tm_weights *w, int32_t temporal_guidance, int32_t dependency_gate) {
     if (!w) return fail(TM_E_ARG, "tm_weights_variant: NULL weights");
+    ++w->version;
     w->P.tg = temporal_guidance ? 1 : 0;
     w->P.dep = dependency_gate ? 1 : 0;
     return TM_OK;
@@ -1823,6 +1874,7 @@ extern "C" int tm_weights_pack(tm_weights *w, const float *const *t, void *strea
     for (int i = 0; i < TM_N_WEIGHTS; ++i)
         if (!t[i]) return fail(TM_E_ARG, "tm_weights_pack: NULL tensor " + std::to_string(i));
     hipStream_t s = S_(stream);
+    ++w->version;
     pack_all_weights(w, t, s);
     TM_CHECK_LAUNCH();
     return TM_OK;
@@ -2189,6 +2241,15 @@ struct tm_dropin {
     void *ws[SIDES] = {};
     size_t ws_bytes[SIDES] = {};
     double *dcut[SIDES] = {};   // per side stream: the cut times its std_cut_kernel writes (stream-ordered reuse)
+    // gate-factor cache (tm_dropin_gate_cache): (fp32 time bits << 32 | factor bits) per edge id, all ones = empty;
+    // valid for the weights / version / edge-feature table it was filled with
+    unsigned long long *gcache = nullptr;
+    int64_t gcache_n = 0;
+    const void *gkey_w = nullptr;
+    uint64_t gkey_ver = 0;
+    const float *gkey_ef = nullptr;
+    int32_t *glist[SIDES] = {};   // per side: miss list [n_pos] and its counter (the list's last element)
+    int64_t glist_n[SIDES] = {};
 };
 
 extern "C" void tm_dropin_free(tm_dropin *d) {
@@ -2198,7 +2259,9 @@ extern "C" void tm_dropin_free(tm_dropin *d) {
     (void)hipSetDevice(d->device);
     for (int k = 0; k < tm_dropin::SIDES; ++k)
         if (d->side[k]) (void)hipStreamSynchronize(d->side[k]);
+    if (d->gcache) (void)hipFree(d->gcache);
     for (int k = 0; k < tm_dropin::SIDES; ++k) {
+        if (d->glist[k]) (void)hipFree(d->glist[k]);
         if (d->dcut[k]) (void)hipFree(d->dcut[k]);
         if (d->ws[k]) (void)hipFree(d->ws[k]);
         if (d->ev_side[k]) (void)hipEventDestroy(d->ev_side[k]);
@@ -2214,6 +2277,26 @@ extern "C" void tm_dropin_free(tm_dropin *d) {
     if (d->dring) (void)hipFree(d->dring);
     (void)hipSetDevice(prev);
     delete d;
+}
+
+extern "C" int tm_dropin_gate_cache(tm_dropin *d, int64_t n_edge_rows) {
+    if (!d || n_edge_rows < 0) return fail(TM_E_ARG, "tm_dropin_gate_cache: bad arguments");
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    hipError_t e = hipSetDevice(d->device);
+    for (int k = 0; k < tm_dropin::SIDES && e == hipSuccess; ++k)
+        if (d->side[k]) e = hipStreamSynchronize(d->side[k]);
+    if (e == hipSuccess && d->gcache) e = hipFree(d->gcache);
+    d->gcache = nullptr;
+    d->gcache_n = 0;
+    d->gkey_w = nullptr;
+    if (e == hipSuccess && n_edge_rows > 0) {
+        e = hipMalloc(&d->gcache, sizeof(unsigned long long) * (size_t)n_edge_rows);
+        if (e == hipSuccess) d->gcache_n = n_edge_rows;
+    }
+    (void)hipSetDevice(prev);
+    if (e != hipSuccess) return fail(TM_E_HIP, std::string("tm_dropin_gate_cache: ") + hipGetErrorString(e));
+    return TM_OK;
 }
 
 extern "C" int tm_dropin_create(int32_t device, tm_dropin **out) {
@@ -2273,6 +2356,15 @@ extern "C" int tm_dropin_forward(tm_dropin *d, int32_t k, int32_t sync, const tm
     if (cut_host && B > tm_dropin::SLOT_DOUBLES) return fail(TM_E_UNSUPPORTED, "tm_dropin_forward: batch too large");
     hipStream_t cur = S_(stream);
     hipStream_t side = d->side[k];
+    // gate-factor cache: new weights (or a repack) or another edge-feature table empty it, on the caller's stream
+    // (ordered after every earlier side call) before every side stream's next use
+    if (out_gfac && d->gcache && (d->gkey_w != w || d->gkey_ver != w->version || d->gkey_ef != e_feat)) {
+        TM_HIP(hipMemsetAsync(d->gcache, 0xFF, sizeof(unsigned long long) * (size_t)d->gcache_n, cur));
+        d->gkey_w = w;
+        d->gkey_ver = w->version;
+        d->gkey_ef = e_feat;
+        sync = 1;
+    }
     // sync: work on the caller's stream this call depends on (weights / tables repacked there, a device
     // cut tensor) -- every side stream waits for the caller's stream once, at its next use.  Otherwise
     // the side stream is not ordered after the caller's: it reads resident pack data and writes buffers
@@ -2355,7 +2447,30 @@ extern "C" int tm_dropin_forward(tm_dropin *d, int32_t k, int32_t sync, const tm
         const int nq = P.d1.nq;
         const bool reg = P.dep && P.d2.nq == 4 && P.d1.nt == 4 && P.d2.nt == 2 && n_pos < INT32_MAX &&
                          (nq == 11 || nq == 12 || nq == 13 || nq == 22);
-        if (reg && nq == 11)
+        if (reg && d->gcache) {
+            // cached: the hits read their factor, the misses (listed) run the register gate and fill the cache
+            if (d->glist_n[k] < n_pos) {
+                TM_HIP(hipStreamSynchronize(side));
+                if (d->glist[k]) TM_HIP(hipFree(d->glist[k]));
+                d->glist[k] = nullptr;
+                d->glist_n[k] = 0;
+                TM_HIP(hipMalloc(&d->glist[k], sizeof(int32_t) * ((size_t)n_pos + 1)));
+                d->glist_n[k] = n_pos;
+            }
+            int32_t *list = d->glist[k];
+            uint32_t *cnt_m = reinterpret_cast<uint32_t *>(list + d->glist_n[k]);
+            TM_HIP(hipMemsetAsync(cnt_m, 0, sizeof(uint32_t), side));
+            gate_cache_lookup_kernel<<<dim3((unsigned)((n_pos + 255) / 256)), 256, 0, side>>>(
+                n_pos, eid3, ts3, d->gcache, d->gcache_n, out_gfac, list, cnt_m);
+#define TM_GATE_LIST(Q)                                                                                            \
+    gate_reg_kernel<Q><<<dim3(rblocks), 256, 0, side>>>(P, (int32_t)n_pos, nullptr, e_feat, out_gfac, nullptr, eid3, \
+                                                         ts3, list, cnt_m, d->gcache, d->gcache_n)
+            if (nq == 11) TM_GATE_LIST(11);
+            else if (nq == 12) TM_GATE_LIST(12);
+            else if (nq == 13) TM_GATE_LIST(13);
+            else TM_GATE_LIST(22);
+#undef TM_GATE_LIST
+        } else if (reg && nq == 11)
             gate_reg_kernel<11><<<dim3(rblocks), 256, 0, side>>>(P, (int32_t)n_pos, nullptr, e_feat, out_gfac, nullptr, eid3, ts3);
         else if (reg && nq == 12)
             gate_reg_kernel<12><<<dim3(rblocks), 256, 0, side>>>(P, (int32_t)n_pos, nullptr, e_feat, out_gfac, nullptr, eid3, ts3);

@@ -272,6 +272,9 @@ struct tm_weights {
     // the caller's node-feature table is all zeros (tm_weights_set_node_zero): the fused eval kernel computes
     // one event_gcn branch, the other being bit-identical
     int node_zero = 0;
+    // bumped by every repack / variant change: caches of values computed from the weights (the drop-in's gate
+    // factors per edge id) key on it
+    uint64_t version = 0;
     // per linear: raw tensor index, nout, k
     struct Spec {
         Lin *lin;

@@ -1605,17 +1605,15 @@ extern "C" int tm_gm_embed_bwd(const tm_gm_embed_args *p, const float *d_x_mean,
     GmBwd b{d_x_mean, d_node_out, d_ew, q.layer_table};
     hipEvent_t pe = prof_begin((hipStream_t)stream);
     const bool t3 = gm_r16(q.C) / 16 <= 12;
-    // the eight-wave form is opt-in (TEMPME_GM_BWD8=1) until it has been checked on the GPU
-    const char *w8 = getenv("TEMPME_GM_BWD8");
-    const bool four = !(w8 != nullptr && w8[0] == '1');
+    // more than 16 neighbours: two token tiles, one per wave of the 8-wave form (two waves per SIMD instead of one:
+    // 7.85 -> 7.12 ms per 1,800 rows at configs[4] shapes, round 5; the 4-wave form is tools/patches/gm_variants.patch)
     auto launch = [&](auto kern, int threads) -> int {
         TM_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         kern<<<q.R, threads, lds, (hipStream_t)stream>>>(a, b);
         return TM_OK;
     };
     int rc;
-    if (q.N > 16 && !four) rc = t3 ? launch(gm_bwd_kernel<2, 3, true>, 512) : launch(gm_bwd_kernel<2, 4, true>, 512);
-    else if (q.N > 16) rc = t3 ? launch(gm_bwd_kernel<2, 3, false>, 256) : launch(gm_bwd_kernel<2, 4, false>, 256);
+    if (q.N > 16) rc = t3 ? launch(gm_bwd_kernel<2, 3, true>, 512) : launch(gm_bwd_kernel<2, 4, true>, 512);
     else rc = t3 ? launch(gm_bwd_kernel<1, 3, false>, 256) : launch(gm_bwd_kernel<1, 4, false>, 256);
     if (rc != TM_OK) return rc;
     TM_CHECK_LAUNCH();

@@ -701,6 +701,10 @@ class TempME(nn.Module):
             for k in range(3):
                 L.check(L.lib().tm_dropin_set_stream(h, k, ext[k].cuda_stream), "tm_dropin_set_stream")
             ctx.streams = ext      # alive as long as the context
+            # the dependency-gate factor per (edge id, time), cached across calls (bit-identical; emptied on new
+            # weights or tables)
+            _, et = self.feature_tables()
+            L.check(L.lib().tm_dropin_gate_cache(h, int(et.shape[0])), "tm_dropin_gate_cache")
             ctx.side_ids = [(x.stream_id, x.device_index, x.device_type) for x in ext]
             ctx.cur_obj = None
             ctx.fwd, ctx.expl = L.lib().tm_dropin_forward, L.lib().tm_edge_importance_gf3

@@ -354,7 +354,7 @@ class GraphedTrainStep:
     training steps).  Returns the static output dict of ``train_step`` (overwritten by every call)."""
 
     def __init__(self, explainer, base_model, optimizer, buf, src, dst, ts, e_idx, warmup_rows, *,
-                 overlap_prepare=True, **kw):
+                 overlap_prepare=False, **kw):
         dev = src.device
         self.args = (explainer, base_model, optimizer, buf, src, dst, ts, e_idx)
         self.kw = kw

@@ -274,13 +274,16 @@ def test_dropin_equals_pipeline(dev, finder, g, z):
     e_s, e_t, e_b = P.get_item_edge(edge, np.arange(E))
     cut = z["test_ts"][:E].astype(np.float64)
     assert ex.dropin_edge_table() is not None
-    with torch.no_grad():
-        i_s, i_t, i_b = ex(w_s, cut, e_s), ex(w_t, cut, e_t), ex(w_b, cut, e_b)
-        expl = ex.retrieve_explanation(sg_s, i_s, w_s, sg_t, i_t, w_t, sg_b, i_b, w_b, training=False)
-    for k, x in enumerate((i_s, i_t, i_b)):
-        assert torch.equal(x[..., 0], imp[k]), k
-    assert torch.equal(expl[0], h1.reshape(3 * E, N))
-    assert torch.equal(expl[1], h2.reshape(3 * E, N * N))
+    # twice: the second pass reads every dependency-gate factor from the drop-in's per-edge-id cache
+    # (tm_dropin_gate_cache), the first computes (and fills) them
+    for _ in range(2):
+        with torch.no_grad():
+            i_s, i_t, i_b = ex(w_s, cut, e_s), ex(w_t, cut, e_t), ex(w_b, cut, e_b)
+            expl = ex.retrieve_explanation(sg_s, i_s, w_s, sg_t, i_t, w_t, sg_b, i_b, w_b, training=False)
+        for k, x in enumerate((i_s, i_t, i_b)):
+            assert torch.equal(x[..., 0], imp[k]), k
+        assert torch.equal(expl[0], h1.reshape(3 * E, N))
+        assert torch.equal(expl[1], h2.reshape(3 * E, N * N))
 
 
 @pytest.mark.parametrize("where", ["device_pack", "host_pack_grad"])

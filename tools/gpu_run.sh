@@ -70,8 +70,9 @@ for s in "$@"; do
         trainflags) step train_flags 1100 ./tools/train_flags_ab.sh ;;
         gmab) step gm_ab 900 ./tools/gm_ab.sh ;;
         gmbab) step gmb_ab 900 ./tools/gmb_ab.sh ;;
-        gmbwd) step gm_bwd 300 python tools/gm_bwd_timing.py && TEMPME_GM_BWD8=1 step gm_bwd8 300 python tools/gm_bwd_timing.py ;;
+        gmbwd) step gm_bwd 300 python tools/gm_bwd_timing.py ;;
         trainops) step trainops 300 python tools/train_ops.py ;;
+        gemmprobe) step gemm_probe 300 python tools/gemm_probe.py ;;
         c2) step bench_c2 600 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config 2 ;;
         c4) step bench_c4 900 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config 4 ;;
         a3) step bench_a3 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --alpha 3.0 ;;

@@ -12,5 +12,5 @@ run() {  # run <label> <env...> -- <extra args>
 for r in 1 2; do
     run base X=0 --
     run nozn X=0 -- --no-node-zero
-    run no_overlap X=0 -- --no-overlap-prepare
+    run overlap X=0 -- --overlap-prepare
 done
