@@ -69,12 +69,35 @@ struct CutArg {
     double v[256];
 };
 
+// Launched with 1 + ceil(n_pos / 1024) workgroups when the drop-in's gate-factor cache is on: workgroups 1.. are
+// gate_cache_lookup's (1024 walk positions each), and workgroup 0 also zeroes the miss counter of the side's next
+// call (the counters alternate per call, so this call's lookup and gate kernels keep theirs).  B = 0: no cut times.
+__device__ __forceinline__ void gate_cache_lookup(int64_t i, const int32_t *__restrict__ eid, const float *__restrict__ ts,
+                                                  const unsigned long long *__restrict__ cache, int64_t n_cache,
+                                                  float *__restrict__ gf, int32_t *__restrict__ list,
+                                                  uint32_t *__restrict__ list_n, int64_t n_pos);
+struct GateLookup {
+    int64_t n_pos, n_cache;
+    const int32_t *eid;
+    const float *ts;
+    const unsigned long long *cache;
+    float *gf;
+    int32_t *list;
+    uint32_t *cnt, *cnt_next;
+};
+
 __global__ void __launch_bounds__(1024) std_cut_kernel(int32_t B, int32_t W, CutArg c, const float *__restrict__ ts3,
                                                        double *__restrict__ cut_out, float *__restrict__ std_out,
-                                                       int32_t do_std) {
+                                                       int32_t do_std, GateLookup gl) {
     __shared__ double red[16];
+    if (blockIdx.x > 0) {
+        gate_cache_lookup((int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x, gl.eid, gl.ts, gl.cache, gl.n_cache, gl.gf,
+                          gl.list, gl.cnt, gl.n_pos);
+        return;
+    }
+    if (threadIdx.x == 0 && gl.cnt_next) *gl.cnt_next = 0u;
     if ((int)threadIdx.x < B) cut_out[threadIdx.x] = c.v[threadIdx.x];
-    if (!do_std) return;
+    if (!do_std || B == 0) return;
     const int32_t nw = B * W;
     const int64_t n = (int64_t)nw * 2;
     double s = 0.0;
@@ -795,22 +818,27 @@ static_assert(EQ_MAX == 4, "load_ef holds 4 K steps");
 
 // per-position scalars of one pass (walk row gw, position p): edge, its two endpoints, the time
 // offset to position 2 (:326) and the three edge counts; loaded one pass ahead of their use
+// raw loads, unconditional (an invalid column's gw is a valid row: coords() gives it group 0, slot 0), so no
+// branch ends the block they are issued in and nothing waits for them there; the users apply v (invalid: zeros)
+// and form dt = ts3[2] - ts3[p] a pass later
 struct PosIn {
     int32_t e, ns, nt;
-    float dt, c0, c1, c2;
+    float ta, tb, c0, c1, c2;
+    bool v;
+    __device__ __forceinline__ int32_t edge() const { return v ? e : 0; }
 };
 
 __device__ __forceinline__ PosIn load_pos(const WalkArgs &a, int64_t gw, int p, bool valid) {
-    PosIn r{0, 0, 0, 0.f, 0.f, 0.f, 0.f};
-    if (valid) {
-        r.e = a.eid3[gw * 3 + p];
-        r.ns = a.node6[gw * 6 + 2 * p];
-        r.nt = a.node6[gw * 6 + 2 * p + 1];
-        r.dt = a.ts3[gw * 3 + 2] - a.ts3[gw * 3 + p];
-        r.c0 = a.cnt[gw * 9 + p * 3 + 0];
-        r.c1 = a.cnt[gw * 9 + p * 3 + 1];
-        r.c2 = a.cnt[gw * 9 + p * 3 + 2];
-    }
+    PosIn r;
+    r.v = valid;
+    r.e = a.eid3[gw * 3 + p];
+    r.ns = a.node6[gw * 6 + 2 * p];
+    r.nt = a.node6[gw * 6 + 2 * p + 1];
+    r.ta = a.ts3[gw * 3 + p];
+    r.tb = a.ts3[gw * 3 + 2];
+    r.c0 = a.cnt[gw * 9 + p * 3 + 0];
+    r.c1 = a.cnt[gw * 9 + p * 3 + 1];
+    r.c2 = a.cnt[gw * 9 + p * 3 + 2];
     return r;
 }
 
@@ -925,9 +953,10 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
     const EncW &P = a.P;
     const int g = lane_id() >> 4;
     const int de = P.de, dn = P.dn, kev = P.kev;
-    const float dt = pi.dt, c0 = pi.c0, c1 = pi.c1, c2 = pi.c2;
-    const float4 *nrow_s = reinterpret_cast<const float4 *>(a.n_feat + (int64_t)pi.ns * dn);
-    const float4 *nrow_t = reinterpret_cast<const float4 *>(a.n_feat + (int64_t)pi.nt * dn);
+    const float dt = pi.v ? pi.tb - pi.ta : 0.f, c0 = pi.v ? pi.c0 : 0.f, c1 = pi.v ? pi.c1 : 0.f,
+                c2 = pi.v ? pi.c2 : 0.f;
+    const float4 *nrow_s = reinterpret_cast<const float4 *>(a.n_feat + (int64_t)(pi.v ? pi.ns : 0) * dn);
+    const float4 *nrow_t = reinterpret_cast<const float4 *>(a.n_feat + (int64_t)(pi.v ? pi.nt : 0) * dn);
     floatx4 L[NTD];
     if constexpr (ETAB) {
 #pragma unroll
@@ -963,7 +992,7 @@ __device__ __forceinline__ void encode_position(const WalkArgs &a, __amdgpu_buff
         auto g1f = [](int k) { return LY::G1 / 4 + k * NTD * 64; };
         const int qend = p == 2 ? P.qt : NQE;            // slot pass: steps >= qt folded into evc / devc
         if constexpr (SEF) {
-            const float4 *erow4 = reinterpret_cast<const float4 *>(a.e_feat + (int64_t)pi.e * de);
+            const float4 *erow4 = reinterpret_cast<const float4 *>(a.e_feat + (int64_t)pi.edge() * de);
             float4 ring[2];
             ring[0] = make_float4(ef[0][0], ef[0][1], ef[0][2], ef[0][3]);
             ring[1] = make_float4(ef[1][0], ef[1][1], ef[1][2], ef[1][3]);
@@ -1184,9 +1213,12 @@ __device__ __forceinline__ float col_sum(float v) {
 }
 
 // per-walk scalars of the head, loaded at the start of the position-1 pass
+// raw loads (see PosIn): the head applies v (invalid: cut 0, std 1, times 0, category 12) and the std's epsilon
 struct HeadIn {
-    float cu, sd, t0, t1;
+    double cu;
+    float sd, t0, t1;
     int32_t c;
+    bool v;
 };
 
 // per-wave LDS stash of a slot's position-2 results, read by its walks' position-0/1 passes
@@ -1211,8 +1243,9 @@ __device__ __forceinline__ void walk_head(const WalkArgs &a, __amdgpu_buffer_rsr
     const int lane = threadIdx.x & 63, g = lane_id() >> 4;
     float tw0 = 1.f, tw1 = 1.f;                          // plain Attention (tg = 0): 0.7f + 0.3f == 1.0f exactly
     if (valid && P.tg) {
-        tw0 = expf(-fabsf(hi.cu - hi.t0) / hi.sd);
-        tw1 = expf(-fabsf(hi.cu - hi.t1) / hi.sd);
+        const float cu = hi.v ? (float)hi.cu : 0.f, sd = hi.v ? hi.sd + 1e-6f : 1.f;
+        tw0 = expf(-fabsf(cu - (hi.v ? hi.t0 : 0.f)) / sd);
+        tw1 = expf(-fabsf(cu - (hi.v ? hi.t1 : 0.f)) / sd);
     }
     // scores * (1.0 - 0.3 + 0.3 * time_weight) (:835-836), softmax over the 2 targets
     s0 *= __fadd_rn(0.7f, __fmul_rn(0.3f, tw0));
@@ -1228,7 +1261,7 @@ __device__ __forceinline__ void walk_head(const WalkArgs &a, __amdgpu_buffer_rsr
     }
     // MLP.0 over [attention out | one-hot(cat)] (compute_catogory_feautres :308-315): the one-hot column and
     // the biases come in as the accumulators' initial value, row cat of tc (row 12 for a padding column)
-    const int32_t c = (valid && hi.c >= 0 && hi.c < 12) ? hi.c : 12;
+    const int32_t c = (valid && hi.v && hi.c >= 0 && hi.c < 12) ? hi.c : 12;
     floatx4 M1[5];
 #pragma unroll
     for (int t = 0; t < 5; ++t) {
@@ -1329,8 +1362,8 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * WALK_WAVES / WALK_WPB) walk
     float4 pre[PFP];
 #pragma unroll
     for (int k = 0; k < PFP; ++k) pre[k] = wload(wr, lane_id() * 16, lin0.o[k]);
-    if constexpr (QE0 == 0) load_ef(a, cur.e, ef);
-    else load_et<QE0>(a, cur.e, et);
+    if constexpr (QE0 == 0) load_ef(a, cur.edge(), ef);
+    else load_et<QE0>(a, cur.edge(), et);
 #ifdef TM_STAMPS
     const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) atomicMax(&g_st[2][9], atomicAdd(&g_live, 1ull) + 1);   // waves resident at once (max)
@@ -1348,15 +1381,14 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * WALK_WAVES / WALK_WPB) walk
         const int m = SPLIT ? m0 : pass == 0 ? 0 : (pass - 1) >> 1;
         const int p = pass == 0 ? 2 : ((pass - 1) & 1);
         const int64_t gw = eg * a.W + (int64_t)j * a.M + m;
-        HeadIn hi{0.f, 1.f, 0.f, 0.f, -1};
-        auto load_hi = [&]() {                           // consumed by the head
-            if (p == 1 && valid) {
-                hi.cu = (float)a.cut[eg];
-                hi.sd = a.stdv[gw / a.BW] + 1e-6f;
-                hi.t0 = a.ts3[gw * 3 + 0];
-                hi.t1 = a.ts3[gw * 3 + 1];
-                hi.c = a.cat[gw];
-            }
+        HeadIn hi{0.0, 1.f, 0.f, 0.f, -1, false};
+        auto load_hi = [&]() {                           // consumed by the head (p == 1); issued every pass, so
+            hi.v = valid;                                // no branch holds the waits for them at the loads
+            hi.cu = a.cut[eg];
+            hi.sd = a.stdv[gw / a.BW];
+            hi.t0 = a.ts3[gw * 3 + 0];
+            hi.t1 = a.ts3[gw * 3 + 1];
+            hi.c = a.cat[gw];
         };
         // next pass's scalars (after the last pass: the next unit's slot pass); its edge features / table
         // row once this pass's lin_event is done
@@ -1379,8 +1411,8 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * WALK_WAVES / WALK_WPB) walk
         encode_position<NQE, NTD, SEF, QE0, ZN>(a, wr, cs, cur, ef, et, extra, p, H, pre,
                                             ZN ? pair_first<4>(p == 2 ? FoldLay::A1DZ / 4 : FoldLay::A1GZ / 4)
                                                : pair_first<8>(p == 2 ? FoldLay::A1D / 4 : FoldLay::A1G / 4), T);
-        if constexpr (QE0 == 0) load_ef(a, nxt.e, ef);
-        else load_et<QE0>(a, nxt.e, et);
+        if constexpr (QE0 == 0) load_ef(a, nxt.edge(), ef);
+        else load_et<QE0>(a, nxt.edge(), et);
         cur = nxt;
         TM_STAMP(6);
         // ZN: H = [U; U]: the layers reading H as their 64-column-folded forms on U (FoldLay KVZ ...)
@@ -1630,14 +1662,12 @@ __global__ void __launch_bounds__(256) gate_reg_kernel(EncW P, int32_t n_ids, co
 
 // The drop-in's gate-factor cache (tm_dropin_gate_cache): per walk position, a hit on (edge id, exact fp32 time)
 // gives the factor gate_reg_kernel computed for it; the misses go to a list (one atomic per wave) that the list
-// mode of gate_reg_kernel computes and stores.  The factor is a function of (E[e], t) alone, so the result equals
+// mode of gate_reg_kernel computes and stores.  Runs in std_cut_kernel's workgroups 1.. (one launch fewer).  The factor is a function of (E[e], t) alone, so the result equals
 // the uncached path's bit for bit.
-__global__ void __launch_bounds__(256) gate_cache_lookup_kernel(int64_t n_pos, const int32_t *__restrict__ eid,
-                                                                const float *__restrict__ ts,
-                                                                const unsigned long long *__restrict__ cache,
-                                                                int64_t n_cache, float *__restrict__ gf,
-                                                                int32_t *__restrict__ list, uint32_t *__restrict__ list_n) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void gate_cache_lookup(int64_t i, const int32_t *__restrict__ eid, const float *__restrict__ ts,
+                                                  const unsigned long long *__restrict__ cache, int64_t n_cache,
+                                                  float *__restrict__ gf, int32_t *__restrict__ list,
+                                                  uint32_t *__restrict__ list_n, int64_t n_pos) {
     const int lane = threadIdx.x & 63;
     bool miss = false;
     if (i < n_pos) {
@@ -2248,8 +2278,9 @@ struct tm_dropin {
     const void *gkey_w = nullptr;
     uint64_t gkey_ver = 0;
     const float *gkey_ef = nullptr;
-    int32_t *glist[SIDES] = {};   // per side: miss list [n_pos] and its counter (the list's last element)
+    int32_t *glist[SIDES] = {};   // per side: miss list [n_pos] and two miss counters after it (alternate calls)
     int64_t glist_n[SIDES] = {};
+    int gpar[SIDES] = {};         // the counter this side's next call uses
 };
 
 extern "C" void tm_dropin_free(tm_dropin *d) {
@@ -2389,6 +2420,31 @@ extern "C" int tm_dropin_forward(tm_dropin *d, int32_t k, int32_t sync, const tm
         TM_HIP(hipMalloc(&d->ws[k], need));
         d->ws_bytes[k] = need;
     }
+    // the gate factors: hid_dim 64 has the register-resident gate (one wave per 16 positions, MFMA chain in
+    // registers), cached per (edge id, time) when the drop-in has a cache; other dims the LDS-tiled gate
+    const EncW &P = w->P;
+    const int64_t n_pos = n_walks * 3;
+    const int nq = P.d1.nq;
+    const bool reg = out_gfac && P.dep && P.d2.nq == 4 && P.d1.nt == 4 && P.d2.nt == 2 && n_pos < INT32_MAX &&
+                     (nq == 11 || nq == 12 || nq == 13 || nq == 22);
+    GateLookup gl{};
+    if (reg && d->gcache) {
+        if (d->glist_n[k] < n_pos) {
+            TM_HIP(hipStreamSynchronize(side));
+            if (d->glist[k]) TM_HIP(hipFree(d->glist[k]));
+            d->glist[k] = nullptr;
+            d->glist_n[k] = 0;
+            TM_HIP(hipMalloc(&d->glist[k], sizeof(int32_t) * ((size_t)n_pos + 2)));
+            d->glist_n[k] = n_pos;
+            TM_HIP(hipMemsetAsync(d->glist[k] + n_pos, 0, 2 * sizeof(uint32_t), side));
+            d->gpar[k] = 0;
+        }
+        uint32_t *cnts = reinterpret_cast<uint32_t *>(d->glist[k] + d->glist_n[k]);
+        gl = GateLookup{n_pos, d->gcache_n, eid3, ts3, d->gcache, out_gfac, d->glist[k], cnts + d->gpar[k],
+                        cnts + (d->gpar[k] ^ 1)};
+        d->gpar[k] ^= 1;
+    }
+    const unsigned lookup_blocks = gl.cnt ? (unsigned)((n_pos + 1023) / 1024) : 0u;
     bool std_done = false;
     if (cut_host && B <= 256) {
         // the cut times travel as the std launch's argument; std_cut_kernel writes them to this side's
@@ -2397,7 +2453,7 @@ extern "C" int tm_dropin_forward(tm_dropin *d, int32_t k, int32_t sync, const tm
         memcpy(c.v, cut_host, sizeof(double) * (size_t)B);
         float *stdv = reinterpret_cast<float *>(d->ws[k]) + n_walks * 3 * 2 * w->P.h;
         hipEvent_t pe = prof_begin(side);
-        std_cut_kernel<<<1, 1024, 0, side>>>(B, W, c, ts3, d->dcut[k], stdv, w->P.tg ? 1 : 0);
+        std_cut_kernel<<<1 + lookup_blocks, 1024, 0, side>>>(B, W, c, ts3, d->dcut[k], stdv, w->P.tg ? 1 : 0, gl);
         TM_CHECK_LAUNCH();
         prof_end("std_kernel", side, pe);
         cut = d->dcut[k];
@@ -2432,39 +2488,25 @@ extern "C" int tm_dropin_forward(tm_dropin *d, int32_t k, int32_t sync, const tm
         }
         cut = d->dring + (size_t)slot * tm_dropin::SLOT_DOUBLES;
     }
+    if (!std_done && gl.cnt) {   // no cut times in the launch argument: the lookup alone (workgroup 0 idle but the reset)
+        CutArg c;
+        std_cut_kernel<<<1 + lookup_blocks, 1024, 0, side>>>(0, W, c, ts3, nullptr, nullptr, 0, gl);
+        TM_CHECK_LAUNCH();
+    }
     int rc = encoder_fwd_impl(w, n_feat, e_feat, etab, 1, B, W, 1, node6, eid3, ts3, cat, cut, cnt, d->ws[k], out_imp,
                               side, !std_done);
     if (rc != TM_OK) return rc;
     if (out_gfac) {
-        const EncW &P = w->P;
         const size_t lds = gate_lds(P);
         if (lds > 160 * 1024) return fail(TM_E_UNSUPPORTED, "tm_dropin_forward: LDS budget exceeded");
-        const int64_t n_pos = n_walks * 3;
         hipEvent_t pe = prof_begin(side);
-        // hid_dim 64: the register-resident gate (one wave per 16 positions, MFMA chain in registers); other
-        // dims: the LDS-tiled one
         const unsigned rblocks = (unsigned)((n_pos + 63) / 64);
-        const int nq = P.d1.nq;
-        const bool reg = P.dep && P.d2.nq == 4 && P.d1.nt == 4 && P.d2.nt == 2 && n_pos < INT32_MAX &&
-                         (nq == 11 || nq == 12 || nq == 13 || nq == 22);
-        if (reg && d->gcache) {
-            // cached: the hits read their factor, the misses (listed) run the register gate and fill the cache
-            if (d->glist_n[k] < n_pos) {
-                TM_HIP(hipStreamSynchronize(side));
-                if (d->glist[k]) TM_HIP(hipFree(d->glist[k]));
-                d->glist[k] = nullptr;
-                d->glist_n[k] = 0;
-                TM_HIP(hipMalloc(&d->glist[k], sizeof(int32_t) * ((size_t)n_pos + 1)));
-                d->glist_n[k] = n_pos;
-            }
-            int32_t *list = d->glist[k];
-            uint32_t *cnt_m = reinterpret_cast<uint32_t *>(list + d->glist_n[k]);
-            TM_HIP(hipMemsetAsync(cnt_m, 0, sizeof(uint32_t), side));
-            gate_cache_lookup_kernel<<<dim3((unsigned)((n_pos + 255) / 256)), 256, 0, side>>>(
-                n_pos, eid3, ts3, d->gcache, d->gcache_n, out_gfac, list, cnt_m);
+        if (gl.cnt) {
+            // cached: the hits have their factor (the lookup), the misses (listed) run the register gate and fill
+            // the cache
 #define TM_GATE_LIST(Q)                                                                                            \
     gate_reg_kernel<Q><<<dim3(rblocks), 256, 0, side>>>(P, (int32_t)n_pos, nullptr, e_feat, out_gfac, nullptr, eid3, \
-                                                         ts3, list, cnt_m, d->gcache, d->gcache_n)
+                                                         ts3, gl.list, gl.cnt, d->gcache, d->gcache_n)
             if (nq == 11) TM_GATE_LIST(11);
             else if (nq == 12) TM_GATE_LIST(12);
             else if (nq == 13) TM_GATE_LIST(13);

@@ -426,14 +426,6 @@ __global__ void gm_pack_kernel(const float *__restrict__ w, int32_t n_out, int32
 // mixing (both token tiles of a row) and the residual; the projection input's edge-feature rows are
 // staged in the same image first (coalesced row loads), the time features computed in the K loop.
 constexpr int GF_PF = 4;
-// A/B knob: token mixing two channel tiles per iteration (gm_fused_kernel), default off until measured
-#ifndef TM_GF_TOKPAIR
-#define TM_GF_TOKPAIR 0
-#endif
-// A/B knob: the projection's K loop over pairs of K tiles (see gm_fused_kernel), default off until measured
-#ifndef TM_GF_QG2
-#define TM_GF_QG2 0
-#endif
 
 // W [n_out][k] row-major -> A-operand fragments, tiles rounded up to multiples of n_mult / k_mult:
 // packed[((t * KT + q) * 64 + lane) * 4 + s] = W[16 t + (lane & 15)][16 q + 4 (lane >> 4) + s] (zero outside W)
@@ -574,10 +566,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 
         const bool tv = I.tok < N && a.nid[rowN + tokc] != 0;
         const float dt = (float)(a.cut[rr] - a.ts[rowN + tokc]);
         // KP = the pack's K tiles per output tile (tm_gm_pack_a k_mult 4: the fragment pitch); the loop runs
-        // QG K tiles per iteration up to KL.  TM_GF_QG2 (A/B knob): QG = 2, so the loop stops at the K tiles
-        // C + T needs rounded to pairs (22 instead of 24 at C = T = 172); the GF_PF-deep ring must stay within
-        // the next iteration's QG * NC fragments, hence QG = 4 for a single channel tile
-        constexpr int QG = (TM_GF_QG2 && NC >= 2) ? 2 : 4;
+        // QG K tiles per iteration up to KL: QG = 2, so the loop stops at the K tiles C + T needs rounded to pairs
+        // (22 instead of 24 at C = T = 172; 4-tile iterations measured 1 % slower, profiles/r05_gm_fused_ab.txt);
+        // the GF_PF-deep ring must stay within the next iteration's QG * NC fragments, hence QG = 4 for a single
+        // channel tile
+        constexpr int QG = NC >= 2 ? 2 : 4;
         const int KP = ((C + T + 63) / 64) * 4;
         const int KL = ((C + T + 16 * QG - 1) / (16 * QG)) * QG;
         const auto wr = gf_rsrc(a.proj_w);
@@ -663,9 +656,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 
                 }
 #pragma unroll
             for (int i = 0; i < 4; ++i) b1v[i] = 4 * g + i < HT ? tw3[4 * g + i] : 0.f;
-#if TM_GF_TOKPAIR
             // two of the wave's channel tiles per iteration: two independent MFMA / shuffle chains in flight
-            // (the same operations per tile, so the same results).  Branch-free: the image's rows past N and
+            // (the same operations per tile, so the same results; one tile per iteration measured 1 % slower,
+            // profiles/r05_gm_fused_ab.txt).  Branch-free: the image's rows past N and
             // columns past C hold zeros (the projection wrote them), lg / lb are zero past N, so loads and xn
             // need no select; the token mask of the variance is a float in a VGPR (a compare per element would
             // hold a lane mask in SGPRs); writes keep the lane's channel test (padding columns stay zero).
@@ -759,61 +752,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 
                     }
                 }
             }
-#else
-            for (int nt = I.tt; nt < NC; nt += NTT) {
-                const int c = 16 * nt + li;
-                const bool cv = c < C;
-                float v[NTT][4], sm = 0.f;
-#pragma unroll
-                for (int G = 0; G < NTT; ++G)
-#pragma unroll
-                    for (int s2 = 0; s2 < 4; ++s2) {
-                        const int t = 16 * G + 4 * s2 + g;
-                        v[G][s2] = (cv && t < N) ? I.Xr[t * XS + c] * I.sew[t] : 0.f;
-                        sm += v[G][s2];
-                    }
-                sm += __shfl_xor(sm, 16);
-                sm += __shfl_xor(sm, 32);
-                const float mean = sm / (float)N;
-                float q = 0.f;
-#pragma unroll
-                for (int G = 0; G < NTT; ++G)
-#pragma unroll
-                    for (int s2 = 0; s2 < 4; ++s2) {
-                        const float d = v[G][s2] - mean;
-                        q += 16 * G + 4 * s2 + g < N ? d * d : 0.f;
-                    }
-                q += __shfl_xor(q, 16);
-                q += __shfl_xor(q, 32);
-                const float rstd = 1.f / sqrtf(q / (float)N + 1e-5f);
-                gmx4 hacc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int G = 0; G < NTT; ++G)
-#pragma unroll
-                    for (int s2 = 0; s2 < 4; ++s2) {
-                        const int t = 16 * G + 4 * s2 + g;
-                        const float xn = (cv && t < N) ? (v[G][s2] - mean) * rstd * lg[G][s2] + lb[G][s2] : 0.f;
-                        hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[G][s2], xn, hacc, 0, 0, 0);
-                    }
-                float h[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) h[i] = 4 * g + i < HT ? gm_gelu(hacc[i] + b1v[i]) : 0.f;
-#pragma unroll
-                for (int mt = 0; mt < NTT; ++mt) {
-                    gmx4 yy = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                    for (int s2 = 0; s2 < 4; ++s2) yy = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[mt][s2], h[s2], yy, 0, 0, 0);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int t = 16 * mt + 4 * g + i;
-                        if (cv && t < N) {
-                            const int ix = t * XS + c;
-                            I.Xr[ix] = (yy[i] + b2v[mt][i]) * I.sew[t] + I.Xr[ix] * I.sew[t];
-                        }
-                    }
-                }
-            }
-#endif
         }
         __syncthreads();
         // ---- channel mixing (:300-305): the wave's token tile from the image; channel LayerNorm per
@@ -993,50 +931,7 @@ static __host__ __device__ inline size_t gmb_lds_floats(int C, int T, int L) {
     return (size_t)(L + 3) * GM_MT * XP + gmb_ulen(C, T) + GMB_TW + 5 * GM_MT + 2 * gm_r16(C);
 }
 
-// one channel's token mixing, recomputed: av[t] = X[t][c] ew_t, LayerNorm over the N tokens, FFN N -> HT -> N
-// (GELU); y[t] = FFN output + b2 (tokens t < N).  Weights from LDS: lg, lb [N], w1 [HT][N], b1 [HT], w2 [N][HT], b2 [N]
-__device__ __forceinline__ void gmb_tok_fwd(int N, int HT, const GmTokW &tw, const float (&av)[GM_MT], float &mean,
-                                            float &rstd, float (&z1)[GM_MT / 2], float (&y)[GM_MT]) {
-    float s = 0.f;
-#pragma unroll
-    for (int t = 0; t < GM_MT; ++t) s += t < N ? av[t] : 0.f;
-    mean = s / (float)N;
-    float q = 0.f;
-#pragma unroll
-    for (int t = 0; t < GM_MT; ++t) {
-        const float d = t < N ? av[t] - mean : 0.f;
-        q += d * d;
-    }
-    rstd = 1.f / sqrtf(q / (float)N + 1e-5f);
-    float xn[GM_MT], h[GM_MT / 2];
-#pragma unroll
-    for (int t = 0; t < GM_MT; ++t) xn[t] = t < N ? (av[t] - mean) * rstd * tw.lg[t] + tw.lb[t] : 0.f;
-#pragma unroll
-    for (int k = 0; k < GM_MT / 2; ++k) {
-        float acc = 0.f;
-        if (k < HT) {
-            acc = tw.b1[k];
-#pragma unroll
-            for (int t = 0; t < GM_MT; ++t)
-                if (t < N) acc += tw.w1[k * N + t] * xn[t];
-        }
-        z1[k] = acc;
-        h[k] = k < HT ? gm_gelu(acc) : 0.f;
-    }
-#pragma unroll
-    for (int t = 0; t < GM_MT; ++t) {
-        float acc = 0.f;
-        if (t < N) {
-            acc = tw.b2[t];
-#pragma unroll
-            for (int k = 0; k < GM_MT / 2; ++k)
-                if (k < HT) acc += tw.w2[t * HT + k] * h[k];
-        }
-        y[t] = acc;
-    }
-}
-
-// phase ablation of gm_bwd_kernel for timing builds only (wrong results): bit 1 skips the per-channel token
+// phase ablation of gm_bwd_kernel for timing builds only (wrong results): bit 1 skips the token
 // mixing (forward, recompute and backward), bit 2 the channel-FFN GEMMs, bit 4 the projection GEMM, bit 8 the
 // LayerNorm statistics / backward and per-token sums
 #ifndef TM_GMB_ABL
@@ -1051,6 +946,76 @@ __device__ __forceinline__ void gmb_token_sums(const float *V, int XP, int N, in
         for (int c = lane; c < C; c += 64) s += V[gm_idx(t, c, XP)];
         s = gm_wsum(s);
         if (lane == 0) out[t] += s;
+    }
+}
+
+// Token mixing on MFMA (gm_fused_kernel's formulation), one wave per 16-channel tile nt: lane (li = lane & 15,
+// g = lane >> 4) is channel c = 16 nt + li.  K operands hold tokens 16 G + 4 s2 + g (G < NMT) or hidden features
+// 4 g + s2; MFMA outputs hold hidden features 4 g + i or tokens 16 mt + 4 g + i.  The weight fragments are read
+// from the layer's LDS copy (w1 [HT][N], w2 [N][HT]) where they are used (held across the tile loop, they spill):
+//   z1 = W1 xn: W1[li][t];  y = W2 h: W2[16 mt + li][4 g + s2];  dh = W2^T dy: W2[t][li];
+//   dxn = W1^T dz1: W1[4 g + s2][16 mt + li]
+struct GmbTokF {
+    const GmTokW &tw;
+    int N, HT, li, g;
+    __device__ __forceinline__ float a1(int t) const { return (li < HT && t < N) ? tw.w1[li * N + t] : 0.f; }
+    __device__ __forceinline__ float a2(int tr, int jj) const { return (tr < N && jj < HT) ? tw.w2[tr * HT + jj] : 0.f; }
+    __device__ __forceinline__ float a2t(int t) const { return (li < HT && t < N) ? tw.w2[t * HT + li] : 0.f; }
+    __device__ __forceinline__ float a1t(int tr, int jj) const { return (jj < HT && tr < N) ? tw.w1[jj * N + tr] : 0.f; }
+    __device__ __forceinline__ float b1(int i) const { return 4 * g + i < HT ? tw.b1[4 * g + i] : 0.f; }
+};
+
+// one channel tile's token LayerNorm (statistics over the N tokens by two shuffles) and FFN: hacc = z1 - b1 at
+// hidden 4 g + i, h = gelu(z1), y at tokens 16 mt + 4 g + i (b2 included)
+template <int NMT>
+__device__ __forceinline__ void gmb_tok_mfma(const GmbTokF &f, const float *S, const float *sew, int XP, int N,
+                                             int HT, int c, bool cv, int g, float &mean, float &rstd, gmx4 &hacc,
+                                             float (&h)[4], float (&y)[NMT][4]) {
+    float v[NMT][4], sm = 0.f;
+#pragma unroll
+    for (int G = 0; G < NMT; ++G)
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+            const int t = 16 * G + 4 * s2 + g;
+            v[G][s2] = (cv && t < N) ? S[gm_idx(t, c, XP)] * sew[t] : 0.f;
+            sm += v[G][s2];
+        }
+    sm += __shfl_xor(sm, 16);
+    sm += __shfl_xor(sm, 32);
+    mean = sm / (float)N;
+    float q = 0.f;
+#pragma unroll
+    for (int G = 0; G < NMT; ++G)
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+            const float d = v[G][s2] - mean;
+            q += 16 * G + 4 * s2 + g < N ? d * d : 0.f;
+        }
+    q += __shfl_xor(q, 16);
+    q += __shfl_xor(q, 32);
+    rstd = 1.f / sqrtf(q / (float)N + 1e-5f);
+    hacc = gmx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int G = 0; G < NMT; ++G)
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+            const int t = 16 * G + 4 * s2 + g;
+            const float xn = (cv && t < N) ? (v[G][s2] - mean) * rstd * f.tw.lg[t] + f.tw.lb[t] : 0.f;
+            hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a1(t), xn, hacc, 0, 0, 0);
+        }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h[i] = 4 * g + i < HT ? gm_gelu(hacc[i] + f.b1(i)) : 0.f;
+#pragma unroll
+    for (int mt = 0; mt < NMT; ++mt) {
+        gmx4 yy = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2)
+            yy = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a2(16 * mt + f.li, 4 * g + s2), h[s2], yy, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int t = 16 * mt + 4 * g + i;
+            y[mt][i] = yy[i] + (t < N ? f.tw.b2[t] : 0.f);
+        }
     }
 }
 
@@ -1162,16 +1127,28 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
         return tw;
     };
     // token mixing of one channel c from image S into image Dst: Dst = (y) * ew + S * ew (thread per channel)
+    // (MFMA, one wave per 16-channel tile; S == Dst allowed: a lane rewrites only its own channel's tokens after
+    // the wave has read them)
     auto token_mix = [&](const GmTokW &tw, const float *S, float *Dst) {
         if (TM_GMB_ABL & 1) return;
-        for (int c = tid; c < C; c += blockDim.x) {
-            float av[GM_MT], z1[GM_MT / 2], y[GM_MT], mean, rstd;
+        const int tl = gm_tid(), li = tl & 15, g = (tl >> 4) & 3;   // laundered: no lane address hoisted out
+        const GmbTokF f{tw, N, HT, li, g};
+        for (int nt = tl >> 6; nt < NT; nt += NWV) {
+            const int c = 16 * nt + li;
+            const bool cv = c < C;
+            float mean, rstd, h[4], y[NMT][4];
+            gmx4 hacc;
+            gmb_tok_mfma<NMT>(f, S, sew, XP, N, HT, c, cv, g, mean, rstd, hacc, h, y);
 #pragma unroll
-            for (int t = 0; t < GM_MT; ++t) av[t] = t < N ? S[gm_idx(t, c, XP)] * sew[t] : 0.f;
-            gmb_tok_fwd(N, HT, tw, av, mean, rstd, z1, y);
+            for (int mt = 0; mt < NMT; ++mt)
 #pragma unroll
-            for (int t = 0; t < GM_MT; ++t)
-                if (t < N) Dst[gm_idx(t, c, XP)] = y[t] * sew[t] + av[t];
+                for (int i = 0; i < 4; ++i) {
+                    const int t = 16 * mt + 4 * g + i;
+                    if (cv && t < N) {
+                        const int ix = gm_idx(t, c, XP);
+                        Dst[ix] = y[mt][i] * sew[t] + S[ix] * sew[t];
+                    }
+                }
         }
     };
     // channel LayerNorm statistics of image S (one wave per token) into tmean / trstd, then this lane's rows
@@ -1406,50 +1383,66 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
             }
         }
         __syncthreads();
-        // token branch, thread per channel: G = d out1 -> d layer input; DY = the channel's terms of d sew
-        for (int c = tid; c < C && !(TM_GMB_ABL & 1); c += blockDim.x) {
-            float av[GM_MT], z1[GM_MT / 2], y[GM_MT], mean, rstd;
+        // token branch on MFMA, one wave per 16-channel tile: G = d out1 -> d layer input; DY = the channel's
+        // terms of d sew.  dy = G ew, dh = W2^T dy, dz1 = dh gelu'(z1), dxn = W1^T dz1, then the LayerNorm-over-
+        // tokens backward (sums over tokens by two shuffles)
+        if (!(TM_GMB_ABL & 1)) {
+            const int tl = gm_tid(), li = tl & 15, g = (tl >> 4) & 3;
+            const GmbTokF f{tw, N, HT, li, g};
+            for (int nt = tl >> 6; nt < NT; nt += NWV) {
+                const int c = 16 * nt + li;
+                const bool cv = c < C;
+                float mean, rstd, h[4], y[NMT][4];
+                gmx4 hacc;
+                gmb_tok_mfma<NMT>(f, XI, sew, XP, N, HT, c, cv, g, mean, rstd, hacc, h, y);
+                gmx4 dh = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int t = 0; t < GM_MT; ++t) av[t] = t < N ? XI[gm_idx(t, c, XP)] * sew[t] : 0.f;
-            gmb_tok_fwd(N, HT, tw, av, mean, rstd, z1, y);
-            float g[GM_MT], dz[GM_MT / 2];
+                for (int kb = 0; kb < NMT; ++kb)
 #pragma unroll
-            for (int t = 0; t < GM_MT; ++t) g[t] = t < N ? G[gm_idx(t, c, XP)] : 0.f;
-            // dh = W2^T (g ew), dz1 = dh gelu'(z1)
+                    for (int s2 = 0; s2 < 4; ++s2) {
+                        const int t = 16 * kb + 4 * s2 + g;
+                        const float dy = (cv && t < N) ? G[gm_idx(t, c, XP)] * sew[t] : 0.f;
+                        dh = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a2t(t), dy, dh, 0, 0, 0);
+                    }
+                float dz[4];
 #pragma unroll
-            for (int k = 0; k < GM_MT / 2; ++k) {
-                float s = 0.f;
-                if (k < HT) {
+                for (int i = 0; i < 4; ++i) dz[i] = 4 * g + i < HT ? dh[i] * gm_gelu_d(hacc[i] + f.b1(i)) : 0.f;
+                float dtg[NMT][4], xh[NMT][4], s1 = 0.f, s2v = 0.f;
 #pragma unroll
-                    for (int t = 0; t < GM_MT; ++t)
-                        if (t < N) s += tw.w2[t * HT + k] * g[t] * sew[t];
+                for (int mt = 0; mt < NMT; ++mt) {
+                    gmx4 dx = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int s2 = 0; s2 < 4; ++s2)
+                        dx = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a1t(16 * mt + li, 4 * g + s2), dz[s2], dx, 0, 0, 0);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int t = 16 * mt + 4 * g + i;
+                        const bool in = cv && t < N;
+                        dtg[mt][i] = in ? dx[i] * tw.lg[t] : 0.f;
+                        xh[mt][i] = in ? (XI[gm_idx(t, c, XP)] * sew[t] - mean) * rstd : 0.f;
+                        s1 += dtg[mt][i];
+                        s2v += dtg[mt][i] * xh[mt][i];
+                    }
                 }
-                dz[k] = k < HT ? s * gm_gelu_d(z1[k]) : 0.f;
-            }
-            // dT = W1^T dz1; LayerNorm-over-tokens backward
-            float s1 = 0.f, s2 = 0.f, dtg[GM_MT];
+                s1 += __shfl_xor(s1, 16);
+                s1 += __shfl_xor(s1, 32);
+                s2v += __shfl_xor(s2v, 16);
+                s2v += __shfl_xor(s2v, 32);
+                s1 /= (float)N;
+                s2v /= (float)N;
 #pragma unroll
-            for (int t = 0; t < GM_MT; ++t) {
-                float s = 0.f;
-                if (t < N) {
+                for (int mt = 0; mt < NMT; ++mt)
 #pragma unroll
-                    for (int k = 0; k < GM_MT / 2; ++k)
-                        if (k < HT) s += tw.w1[k * N + t] * dz[k];
-                }
-                dtg[t] = t < N ? s * tw.lg[t] : 0.f;
-                s1 += dtg[t];
-                s2 += t < N ? dtg[t] * (av[t] - mean) * rstd : 0.f;
-            }
-            s1 /= (float)N;
-            s2 /= (float)N;
-#pragma unroll
-            for (int t = 0; t < GM_MT; ++t) {
-                if (t < N) {
-                    const int ix = gm_idx(t, c, XP);
-                    const float da = g[t] + rstd * (dtg[t] - s1 - (av[t] - mean) * rstd * s2);
-                    DY[ix] = g[t] * y[t] + da * XI[ix];
-                    G[ix] = da * sew[t];
-                }
+                    for (int i = 0; i < 4; ++i) {
+                        const int t = 16 * mt + 4 * g + i;
+                        if (cv && t < N) {
+                            const int ix = gm_idx(t, c, XP);
+                            const float gv = G[ix];
+                            const float da = gv + rstd * (dtg[mt][i] - s1 - xh[mt][i] * s2v);
+                            DY[ix] = gv * y[mt][i] + da * XI[ix];
+                            G[ix] = da * sew[t];
+                        }
+                    }
             }
         }
         __syncthreads();
