@@ -1303,6 +1303,9 @@ __device__ __forceinline__ float score_dot(const Stash &st, const floatx4 (&H)[8
 // its unit's 16 slots -- the slot pass, then that walk's positions 0 and 1 (3 passes instead of 1 + 2M) --
 // so a unit's M walks run on M waves at once.  The slot pass is repeated by each of them (same values);
 // the chip is far from full at these sizes, and the latency of a call is one wave's pass chain.
+// (Running the three positions of an M == 1 unit on three waves at once, the stash and position 0's inputs
+// crossing LDS behind workgroup barriers, measured no faster for the drop-in: with three side calls in flight
+// the 3x waves no longer fit one round of residency -- profiles/r05_dropin_pp_ab.txt.)
 template <int NQE, int NTD, bool SEF = false, int QE0 = 0, bool SPLIT = false, bool ZN = false>
 __global__ void __launch_bounds__(64 * WALK_WPB, 4 * WALK_WAVES / WALK_WPB) walk_kernel(WalkArgs a) {
     using C = WalkConsts<NQE, NTD>;
@@ -1469,23 +1472,24 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * WALK_WAVES / WALK_WPB) walk
 #pragma unroll
             for (int t = 0; t < 4; ++t) st.P2[t][lane] = P2[t];
             st.cw[lane] = cw;
-        } else {
+        }
+        floatx4 R[4];
+        float s = 0.f;
+        if (p != 2) {
             // R = A1G H_p (attention.MLP.0 of W2's output for this position), score = V . H_p + cw
-            floatx4 R[4];
 #pragma unroll
             for (int t = 0; t < 4; ++t) R[t] = floatx4{0.f, 0.f, 0.f, 0.f};
             if constexpr (ZN) cgemm_p<4, 4, 4, FoldLay::A1GZ>(wr, Uv, R, pre, p == 1 ? pair_first<4>(FoldLay::M1A2 / 4) : lin0);
             else cgemm_p<4, 8, 8, FoldLay::A1G>(wr, H, R, pre, p == 1 ? pair_first<4>(FoldLay::M1A2 / 4) : lin0);
-            const float s = score_dot<ZN>(st, H);
+            s = score_dot<ZN>(st, H);
             TM_STAMP(7);
             if (p == 0) {
 #pragma unroll
                 for (int t = 0; t < 4; ++t) R0[t] = R[t];
                 s0 = s;
-            } else {
-                walk_head<NQE, NTD>(a, wr, cs, gw, valid, hi, st, s0, s, R0, R, pre, lin0);
             }
         }
+        if (p == 1) walk_head<NQE, NTD>(a, wr, cs, gw, valid, hi, st, s0, s, R0, R, pre, lin0);
         TM_STAMP(8);
 #ifdef TM_STAMPS
         if (lane == 0 && blockIdx.x % 16 == 5) {

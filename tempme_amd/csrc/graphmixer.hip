@@ -566,11 +566,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC <= 
         const bool tv = I.tok < N && a.nid[rowN + tokc] != 0;
         const float dt = (float)(a.cut[rr] - a.ts[rowN + tokc]);
         // KP = the pack's K tiles per output tile (tm_gm_pack_a k_mult 4: the fragment pitch); the loop runs
-        // QG K tiles per iteration up to KL: QG = 2, so the loop stops at the K tiles C + T needs rounded to pairs
-        // (22 instead of 24 at C = T = 172; 4-tile iterations measured 1 % slower, profiles/r05_gm_fused_ab.txt);
-        // the GF_PF-deep ring must stay within the next iteration's QG * NC fragments, hence QG = 4 for a single
-        // channel tile
-        constexpr int QG = NC >= 2 ? 2 : 4;
+        // QG K tiles per iteration up to KL.  The ring slot of fragment f is f % GF_PF in every iteration, so an
+        // iteration's QG * NC fragments must be a multiple of GF_PF: QG = 4 (pairs of K tiles, which stop at the
+        // K tiles C + T needs, broke that for odd NC: profiles/r05_gm_fused_ab.txt)
+        constexpr int QG = 4;
+        static_assert((QG * NC) % GF_PF == 0, "ring slots repeat per iteration");
         const int KP = ((C + T + 63) / 64) * 4;
         const int KL = ((C + T + 16 * QG - 1) / (16 * QG)) * QG;
         const auto wr = gf_rsrc(a.proj_w);
