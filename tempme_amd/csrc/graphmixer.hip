@@ -931,17 +931,10 @@ static __host__ __device__ inline size_t gmb_lds_floats(int C, int T, int L) {
     return (size_t)(L + 3) * GM_MT * XP + gmb_ulen(C, T) + GMB_TW + 5 * GM_MT + 2 * gm_r16(C);
 }
 
-// phase ablation of gm_bwd_kernel for timing builds only (wrong results): bit 1 skips the token
-// mixing (forward, recompute and backward), bit 2 the channel-FFN GEMMs, bit 4 the projection GEMM, bit 8 the
-// LayerNorm statistics / backward and per-token sums
-#ifndef TM_GMB_ABL
-#define TM_GMB_ABL 0
-#endif
-
 // sum over c < C of the LDS image V[t][c], one wave per token (nw waves), added to out[t]
 __device__ __forceinline__ void gmb_token_sums(const float *V, int XP, int N, int C, int nw, float *out) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int t = wave; t < N && !(TM_GMB_ABL & 8); t += nw) {
+    for (int t = wave; t < N; t += nw) {
         float s = 0.f;
         for (int c = lane; c < C; c += 64) s += V[gm_idx(t, c, XP)];
         s = gm_wsum(s);
@@ -1074,8 +1067,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
             gmx4 acc[NTW][2];
 #pragma unroll
             for (int i = 0; i < NTW; ++i) acc[i][0] = acc[i][1] = gmx4{0.f, 0.f, 0.f, 0.f};
-            if (!(TM_GMB_ABL & 4))
-                gm_gemm_mt<GMT, NTW, false>(X0 + 16 * mh * K0P, K0P, G0, a.proj_w, NT, wq, ntw, G0, nG, acc, nullptr,
+            gm_gemm_mt<GMT, NTW, false>(X0 + 16 * mh * K0P, K0P, G0, a.proj_w, NT, wq, ntw, G0, nG, acc, nullptr,
                                             nullptr, mr, rr);
 #pragma unroll
             for (int i = 0; i < NTW; ++i) {
@@ -1130,7 +1122,6 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
     // (MFMA, one wave per 16-channel tile; S == Dst allowed: a lane rewrites only its own channel's tokens after
     // the wave has read them)
     auto token_mix = [&](const GmTokW &tw, const float *S, float *Dst) {
-        if (TM_GMB_ABL & 1) return;
         const int tl = gm_tid(), li = tl & 15, g = (tl >> 4) & 3;   // laundered: no lane address hoisted out
         const GmbTokF f{tw, N, HT, li, g};
         for (int nt = tl >> 6; nt < NT; nt += NWV) {
@@ -1153,7 +1144,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
     };
     // channel LayerNorm statistics of image S (one wave per token) into tmean / trstd, then this lane's rows
     auto chan_stats = [&](const float *S) {
-        for (int t = wave; t < GM_MT && !(TM_GMB_ABL & 8); t += NWV) {
+        for (int t = wave; t < GM_MT; t += NWV) {
             float mean = 0.f, rstd = 0.f;
             if (t < N) {
                 float s = 0.f, q = 0.f;
@@ -1195,7 +1186,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
             gmx4 acc[GM_HCH / 64][2];
 #pragma unroll
             for (int i = 0; i < GM_HCH / 64; ++i) acc[i][0] = acc[i][1] = gmx4{0.f, 0.f, 0.f, 0.f};
-            if (!(TM_GMB_ABL & 2)) gm_gemm_mt<GMT, GM_HCH / 64, true>(X + 16 * mh * XP, XP, 0, W1, NH, h0 + wq, nw1, 0, C16 / 16, acc, lnw, lnb,
+            gm_gemm_mt<GMT, GM_HCH / 64, true>(X + 16 * mh * XP, XP, 0, W1, NH, h0 + wq, nw1, 0, C16 / 16, acc, lnw, lnb,
                                                mr, rr);
 #pragma unroll
             for (int i = 0; i < GM_HCH / 64; ++i) {
@@ -1211,7 +1202,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
                     }
             }
             __syncthreads();
-            if (!(TM_GMB_ABL & 2)) gm_gemm_mt<GMT, NTW, false>(H + 16 * mh * HP, HP, h0, W2, NT, wq, ntw, h0, nh, acc2, nullptr, nullptr, mr, rr);
+            gm_gemm_mt<GMT, NTW, false>(H + 16 * mh * HP, HP, h0, W2, NT, wq, ntw, h0, nh, acc2, nullptr, nullptr, mr, rr);
             __syncthreads();
         }
 #pragma unroll
@@ -1289,9 +1280,9 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
 #pragma unroll
             for (int i = 0; i < GM_HCH / 64; ++i)
                 acc[i][0] = acc[i][1] = accd[i][0] = accd[i][1] = gmx4{0.f, 0.f, 0.f, 0.f};
-            if (!(TM_GMB_ABL & 2)) gm_gemm_mt<GMT, GM_HCH / 64, true>(O1 + 16 * mh * XP, XP, 0, W1, NH, h0 + wq, nw1, 0, C16 / 16, acc, lnw, lnb,
+            gm_gemm_mt<GMT, GM_HCH / 64, true>(O1 + 16 * mh * XP, XP, 0, W1, NH, h0 + wq, nw1, 0, C16 / 16, acc, lnw, lnb,
                                                mr, rr);
-            if (!(TM_GMB_ABL & 2)) gm_gemm_mt<GMT, GM_HCH / 64, false>(DY + 16 * mh * XP, XP, 0, W2T, NH, h0 + wq, nw1, 0, C16 / 16, accd,
+            gm_gemm_mt<GMT, GM_HCH / 64, false>(DY + 16 * mh * XP, XP, 0, W2T, NH, h0 + wq, nw1, 0, C16 / 16, accd,
                                                 nullptr, nullptr, mr, rr);
             // H = gelu(Z2) for Y_ch; dZ2 = dG2 gelu'(Z2) kept in accd for the second pass through U
 #pragma unroll
@@ -1311,7 +1302,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
                     }
             }
             __syncthreads();
-            if (!(TM_GMB_ABL & 2)) gm_gemm_mt<GMT, NTW, false>(H + 16 * mh * HP, HP, h0, W2, NT, wq, ntw, h0, nh, acc2, nullptr, nullptr, mr, rr);
+            gm_gemm_mt<GMT, NTW, false>(H + 16 * mh * HP, HP, h0, W2, NT, wq, ntw, h0, nh, acc2, nullptr, nullptr, mr, rr);
             __syncthreads();
 #pragma unroll
             for (int i = 0; i < GM_HCH / 64; ++i) {
@@ -1326,7 +1317,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
                     }
             }
             __syncthreads();
-            if (!(TM_GMB_ABL & 2)) gm_gemm_mt<GMT, NTW, false>(H + 16 * mh * HP, HP, h0, W1T, NT, wq, ntw, h0, nh, accv, nullptr, nullptr, mr,
+            gm_gemm_mt<GMT, NTW, false>(H + 16 * mh * HP, HP, h0, W1T, NT, wq, ntw, h0, nh, accv, nullptr, nullptr, mr,
                                         rr);
             __syncthreads();
         }
@@ -1365,7 +1356,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
                 }
         }
         __syncthreads();
-        for (int t = wave; t < N && !(TM_GMB_ABL & 8); t += NWV) {
+        for (int t = wave; t < N; t += NWV) {
             const float mean = tmean[t], rstd = trstd[t];
             float s1 = 0.f, s2 = 0.f;
             for (int c = lane; c < C; c += 64) {
@@ -1386,7 +1377,7 @@ __global__ void __launch_bounds__(NMT == 2 && TS8 ? 512 : 256) gm_bwd_kernel(GmA
         // token branch on MFMA, one wave per 16-channel tile: G = d out1 -> d layer input; DY = the channel's
         // terms of d sew.  dy = G ew, dh = W2^T dy, dz1 = dh gelu'(z1), dxn = W1^T dz1, then the LayerNorm-over-
         // tokens backward (sums over tokens by two shuffles)
-        if (!(TM_GMB_ABL & 1)) {
+        {
             const int tl = gm_tid(), li = tl & 15, g = (tl >> 4) & 3;
             const GmbTokF f{tw, N, HT, li, g};
             for (int nt = tl >> 6; nt < NT; nt += NWV) {
