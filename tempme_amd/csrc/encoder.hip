@@ -100,17 +100,43 @@ __global__ void __launch_bounds__(1024) std_cut_kernel(int32_t B, int32_t W, Cut
     if (!do_std || B == 0) return;
     const int32_t nw = B * W;
     const int64_t n = (int64_t)nw * 2;
-    double s = 0.0;
-    for (int32_t w = threadIdx.x; w < nw; w += blockDim.x) {
-        const float cc = (float)c.v[w / W];
-        s += (double)fabsf(cc - ts3[w * 3]) + (double)fabsf(cc - ts3[w * 3 + 1]);
-    }
-    const double mean = block_sum(s, red) / (double)n;
-    double v = 0.0;
-    for (int32_t w = threadIdx.x; w < nw; w += blockDim.x) {
-        const float cc = (float)c.v[w / W];
-        const double d0 = (double)fabsf(cc - ts3[w * 3]) - mean, d1 = (double)fabsf(cc - ts3[w * 3 + 1]) - mean;
-        v += d0 * d0 + d1 * d1;
+    double s = 0.0, v = 0.0, mean;
+    constexpr int SR = 16;                              // walks per thread held in registers
+    if (nw <= SR * (int32_t)blockDim.x) {
+        // every |cut - t| of the thread requested at once (one memory latency, not one per walk), kept for the
+        // second pass; the same walks per thread and the same sums in the same order as below
+        float a0[SR], a1[SR];
+#pragma unroll
+        for (int k = 0; k < SR; ++k) {
+            const int32_t w = (int32_t)threadIdx.x + k * (int32_t)blockDim.x;
+            a0[k] = a1[k] = 0.f;
+            if (w < nw) {
+                const float cc = (float)c.v[w / W];
+                a0[k] = fabsf(cc - ts3[w * 3]);
+                a1[k] = fabsf(cc - ts3[w * 3 + 1]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < SR; ++k)
+            if ((int32_t)threadIdx.x + k * (int32_t)blockDim.x < nw) s += (double)a0[k] + (double)a1[k];
+        mean = block_sum(s, red) / (double)n;
+#pragma unroll
+        for (int k = 0; k < SR; ++k)
+            if ((int32_t)threadIdx.x + k * (int32_t)blockDim.x < nw) {
+                const double d0 = (double)a0[k] - mean, d1 = (double)a1[k] - mean;
+                v += d0 * d0 + d1 * d1;
+            }
+    } else {
+        for (int32_t w = threadIdx.x; w < nw; w += blockDim.x) {
+            const float cc = (float)c.v[w / W];
+            s += (double)fabsf(cc - ts3[w * 3]) + (double)fabsf(cc - ts3[w * 3 + 1]);
+        }
+        mean = block_sum(s, red) / (double)n;
+        for (int32_t w = threadIdx.x; w < nw; w += blockDim.x) {
+            const float cc = (float)c.v[w / W];
+            const double d0 = (double)fabsf(cc - ts3[w * 3]) - mean, d1 = (double)fabsf(cc - ts3[w * 3 + 1]) - mean;
+            v += d0 * d0 + d1 * d1;
+        }
     }
     const double var = block_sum(v, red);
     if (threadIdx.x == 0) std_out[0] = n > 1 ? (float)sqrt(var / (double)(n - 1)) : __builtin_nanf("");
