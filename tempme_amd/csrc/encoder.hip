@@ -2060,7 +2060,9 @@ static void launch_gcn(const EncW &P, int node_zero, int64_t n_rows, size_t lds,
 }
 
 // walks per head_kernel workgroup: 32 where the tiles fit the LDS, else 16
-static int head_tr(const EncW &P) { return head_lds(P, 32) <= 160 * 1024 ? 32 : 16; }
+// 16 walks per head_kernel workgroup (35 KB of LDS at hid_dim 64, four per CU; 32-walk ones hold two per CU
+// and measured 0-0.9 % slower per training step, profiles/r05_train_tiles_ab.txt)
+static int head_tr(const EncW &) { return 16; }
 static void launch_head(const EncW &P, int64_t n_walks, int64_t walks_per_group, int32_t W, const float *F,
                         const float *ts3, const double *cut, const int32_t *cat, const float *stdv, float *out,
                         const uint8_t *drop, float dscale, hipStream_t s) {

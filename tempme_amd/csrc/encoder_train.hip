@@ -282,7 +282,7 @@ __host__ __device__ constexpr size_t head_bwd_lds_floats(int h, int hm, int TR) 
     return (size_t)TR * (4 * (2 * h + 8) + 2 * (h + 8) + 2 * (r16(hm) + 8));
 }
 
-// TR = 32 walks per workgroup, or 16 where the 32-walk tiles exceed the LDS (hid_dim > 64 or so)
+// TR = 16 walks per workgroup (head_bwd_tr; the template also takes 32)
 template <int TR>
 __global__ void __launch_bounds__(256) head_bwd_kernel(EncW P, EncWT T, int64_t n_walks, int64_t walks_per_group,
                                                        int32_t W, const float *__restrict__ F,
@@ -1119,11 +1119,13 @@ __global__ void __launch_bounds__(256, 2) gcn_fwd_reg_kernel(EncW P, int64_t n_r
 
 // ------------------------------------------------------------------ weight gradients: dW = dY^T X over rows
 // One launch computes every weight / bias gradient of the encoder from the (dY, X) row pairs the two
-// backward kernels wrote: job j covers a 64 x 64 block of dW_j (its bias gradient = a virtual column of
-// ones appended to X) over CHUNK rows; the workgroup stages 64-row slabs of dY and X in LDS and each
-// wave runs a 16 x 64 strip on MFMA (k = rows), then stores its partial block.  A second launch sums
+// backward kernels wrote: job j covers a 64 x 64 block of dW_j over CHUNK rows (column block 0 also sums dY's
+// columns: the bias gradient); the workgroup stages WG_SR-row slabs of dY and X in LDS and each wave runs a
+// 16 x 64 strip on MFMA (k = rows), then stores its partial block.  A second launch sums
 // the partials of every output element in a fixed order (deterministic; no atomics).
 constexpr int WG_CHUNK = 1024, WG_LDS_LD = 80, MAX_WG_JOBS = 14, MAX_WG_TGTS = 12;
+// a workgroup's partial: its 64 x 64 block of dW, then (column block 0 only) the 64 dY column sums of its rows
+constexpr int WG_PART = 4096 + 64;
 struct WgJob {
     const float *y, *x;
     int32_t ldy, ldx, O, I, bias, OB, IB, R, vec;
@@ -1143,8 +1145,9 @@ struct WgPlan {
 
 // slab staging: 64 rows x 64 columns of dY (cols o0..) and X (cols i0.., the ones column at I), one
 // float4 per (thread, k) when the job's rows are 16-byte aligned (vec), else scalars
+template <int SR>
 struct Slab {
-    float4 y[4], x[4];
+    float4 y[SR / 16], x[SR / 16];
 };
 
 __device__ __forceinline__ float4 ld_cols(const float *p, int64_t row_off, int c0, int ncol, bool vec, bool ones,
@@ -1165,29 +1168,36 @@ __device__ __forceinline__ float4 ld_cols(const float *p, int64_t row_off, int c
     return make_float4(e[0], e[1], e[2], e[3]);
 }
 
-__device__ __forceinline__ void slab_load(const WgJob &J, int r0, int r_end, int o0, int i0, Slab &sl) {
+template <int SR>
+__device__ __forceinline__ void slab_load(const WgJob &J, int r0, int r_end, int o0, int i0, Slab<SR> &sl) {
     const int tid = threadIdx.x;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < SR / 16; ++k) {
         const int e = tid + 256 * k, row = e >> 4, c = (e & 15) * 4, r = r0 + row;
         const bool rv = r < r_end;
         sl.y[k] = ld_cols(J.y, (int64_t)r * J.ldy, o0 + c, J.O, J.vec, false, rv);
-        sl.x[k] = ld_cols(J.x, (int64_t)r * J.ldx, i0 + c, J.I, J.vec, J.bias != 0, rv);
+        sl.x[k] = ld_cols(J.x, (int64_t)r * J.ldx, i0 + c, J.I, J.vec, false, rv);
     }
 }
 
-__device__ __forceinline__ void slab_store(const Slab &sl, float *Ys, float *Xs) {
+template <int SR>
+__device__ __forceinline__ void slab_store(const Slab<SR> &sl, float *Ys, float *Xs) {
     const int tid = threadIdx.x;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < SR / 16; ++k) {
         const int e = tid + 256 * k, row = e >> 4, c = (e & 15) * 4;
         *reinterpret_cast<float4 *>(Ys + row * WG_LDS_LD + c) = sl.y[k];
         *reinterpret_cast<float4 *>(Xs + row * WG_LDS_LD + c) = sl.x[k];
     }
 }
 
+// rows per LDS slab: 16 (20 KB of LDS per workgroup, so the workgroups a CU holds are set by waves, not LDS):
+// 64-row slabs (80 KB, two workgroups per CU) ran this kernel 0.238 ms per launch, 32 rows 0.167, 16 rows 0.143 --
+// 36.1k -> 38.9k trained edges/s (round 5, tools/train_ab.sh, profiles/r05_train_tiles_ab.txt)
+constexpr int WG_SR = 16;
 __global__ void __launch_bounds__(256) wgrad_partial_kernel(WgPlan P, float *__restrict__ part) {
-    __shared__ __attribute__((aligned(16))) float Ys[2][64 * WG_LDS_LD], Xs[2][64 * WG_LDS_LD];
+    constexpr int SR = WG_SR;
+    __shared__ __attribute__((aligned(16))) float Ys[2][SR * WG_LDS_LD], Xs[2][SR * WG_LDS_LD];
     const int64_t bid = blockIdx.x;
     int j = 0;
     while (j + 1 < P.njob && bid >= P.job[j + 1].wg_begin) ++j;
@@ -1198,37 +1208,49 @@ __global__ void __launch_bounds__(256) wgrad_partial_kernel(WgPlan P, float *__r
     const int o0 = ob * 64, i0 = ib * 64;
     const int r_begin = chunk * WG_CHUNK, r_end = min(J.R, r_begin + WG_CHUNK);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, m = lane & 15;
+    // the bias gradient (dY's column sums) on the VALU in column block 0, from the A values the MFMAs read; the
+    // block's MFMA column tiles past I are skipped (a time-encoder job has one column)
+    const bool bias_blk = ib == 0;
+    const int nt = min(4, (J.I - i0 + 15) >> 4);
+    float ysum = 0.f;
     floatx4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
     // double-buffered: slab k+1 is loaded into registers while slab k's MFMAs run from LDS
-    Slab sl;
-    slab_load(J, r_begin, r_end, o0, i0, sl);
-    slab_store(sl, Ys[0], Xs[0]);
+    Slab<SR> sl;
+    slab_load<SR>(J, r_begin, r_end, o0, i0, sl);
+    slab_store<SR>(sl, Ys[0], Xs[0]);
     __syncthreads();
     int buf = 0;
-    for (int r0 = r_begin; r0 < r_end; r0 += 64) {
-        const bool more = r0 + 64 < r_end;
-        if (more) slab_load(J, r0 + 64, r_end, o0, i0, sl);
+    for (int r0 = r_begin; r0 < r_end; r0 += SR) {
+        const bool more = r0 + SR < r_end;
+        if (more) slab_load<SR>(J, r0 + SR, r_end, o0, i0, sl);
         const float *Y = Ys[buf], *X = Xs[buf];
 #pragma unroll 4
-        for (int s = 0; s < 16; ++s) {
+        for (int s = 0; s < SR / 4; ++s) {
             const float a = Y[(4 * s + g) * WG_LDS_LD + 16 * wave + m];
+            if (bias_blk) ysum += a;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
+                if (t >= nt) break;
                 const float b = X[(4 * s + g) * WG_LDS_LD + 16 * t + m];
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
             }
         }
-        if (more) slab_store(sl, Ys[buf ^ 1], Xs[buf ^ 1]);
+        if (more) slab_store<SR>(sl, Ys[buf ^ 1], Xs[buf ^ 1]);
         __syncthreads();
         buf ^= 1;
     }
-    float *out = part + J.part_begin + local * 4096;
+    float *out = part + J.part_begin + local * WG_PART;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) out[(16 * wave + 4 * g + r) * 64 + 16 * t + m] = acc[t][r];
+    if (bias_blk) {
+        ysum += __shfl_xor(ysum, 16);
+        ysum += __shfl_xor(ysum, 32);
+        if (g == 0) out[4096 + 16 * wave + m] = ysum;
+    }
 }
 
 
@@ -1244,9 +1266,10 @@ __global__ void wgrad_reduce_kernel(WgPlan P, const float *__restrict__ part) {
         for (int jj = 0; jj < T.nj; ++jj) {
             const WgJob &J = P.job[T.j0 + jj];
             const int nchunk = (J.R + WG_CHUNK - 1) / WG_CHUNK, nb = J.OB * J.IB;
-            const int tb = (o / 64) * J.IB + i / 64;
-            const float *p = part + J.part_begin + (int64_t)tb * 4096 + (o % 64) * 64 + (i % 64);
-            for (int c = 0; c < nchunk; ++c) s += p[(int64_t)c * nb * 4096];
+            const bool wcol = i < T.I;
+            const int tb = (o / 64) * J.IB + (wcol ? i / 64 : 0);
+            const float *p = part + J.part_begin + (int64_t)tb * WG_PART + (wcol ? (o % 64) * 64 + (i % 64) : 4096 + o % 64);
+            for (int c = 0; c < nchunk; ++c) s += p[(int64_t)c * nb * WG_PART];
         }
         if (i < T.I) T.w[(int64_t)o * T.I + i] = s;
         else T.b[o] = s;
@@ -1623,11 +1646,11 @@ void train_packs_free(tm_weights *w) {
     w->tbuf = nullptr;
 }
 
-// walks per head_bwd_kernel workgroup: 32 where the tiles fit the LDS, else 16; 0 = no instance
+// walks per head_bwd_kernel workgroup: 16 (0 = the tiles exceed the LDS).  32-walk workgroups (110 KB of LDS at
+// hid_dim 64: one per CU) ran 0.224 ms per launch, 16-walk ones (55 KB, two per CU) 0.175 (round 5,
+// profiles/r05_train_tiles_ab.txt)
 static int head_bwd_tr(const EncW &P) {
-    if (sizeof(float) * head_bwd_lds_floats(P.h, P.hm, 32) <= 160 * 1024) return 32;
-    if (sizeof(float) * head_bwd_lds_floats(P.h, P.hm, 16) <= 160 * 1024) return 16;
-    return 0;
+    return sizeof(float) * head_bwd_lds_floats(P.h, P.hm, 16) <= 160 * 1024 ? 16 : 0;
 }
 static size_t gcn_bwd_lds(const EncW &P) {
     const int ldx = r16(P.kev) + 8, ldab = r16(P.dn) + 8, ldh = r16(P.h) + 8;
@@ -1685,12 +1708,8 @@ extern "C" int tm_encoder_bwd(const tm_weights *w, const float *n_feat, const fl
     HeadBwdOut ho{io->imp, io->dlogit, io->M2, io->dM2, io->M1d, io->dM1, io->X, io->dY2, io->H1d, io->dH1, io->O,
                   io->dP,  io->dQ,     io->dF};
     hipEvent_t pe = prof_begin(s);
-    if (tr == 32)
-        head_bwd_kernel<32><<<dim3((unsigned)((n_walks + 31) / 32)), 256, lh, s>>>(
-            P, w->T, n_walks, (int64_t)B * W, W, F, ts3, cut, cat, stdv, drop, drop_scale, d_imp, ho);
-    else
-        head_bwd_kernel<16><<<dim3((unsigned)((n_walks + 15) / 16)), 256, lh, s>>>(
-            P, w->T, n_walks, (int64_t)B * W, W, F, ts3, cut, cat, stdv, drop, drop_scale, d_imp, ho);
+    head_bwd_kernel<16><<<dim3((unsigned)((n_walks + 15) / 16)), 256, lh, s>>>(
+        P, w->T, n_walks, (int64_t)B * W, W, F, ts3, cut, cat, stdv, drop, drop_scale, d_imp, ho);
     TM_CHECK_LAUNCH();
     prof_end("head_bwd_kernel", s, pe);
     const int64_t n_rows = n_walks * 3;
@@ -1761,17 +1780,17 @@ static int run_wgrad(const tm_wgrad_job *jobs, int njob, const tm_wgrad_target *
             return fail(TM_E_ARG, std::string(what) + ": bad job " + std::to_string(j));
         WgJob &J = P.job[j];
         J.y = d.dy; J.x = d.x; J.ldy = d.ldy; J.ldx = d.ldx; J.O = d.O; J.I = d.I; J.R = d.R;
-        J.bias = 1;   // a column of ones: every job adds its dY column sums to its target's bias gradient
+        J.bias = 1;   // every job adds its dY column sums to its target's bias gradient
         // float4 staging when both row arrays are 16-byte aligned row by row
         J.vec = (d.ldy % 4 == 0 && d.ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(d.dy) & 15) == 0 &&
                  (reinterpret_cast<uintptr_t>(d.x) & 15) == 0) ? 1 : 0;
         J.OB = (d.O + 63) / 64;
-        J.IB = (d.I + 1 + 63) / 64;
+        J.IB = (d.I + 63) / 64;   // the bias column is not a column of X (column block 0 sums dY)
         J.wg_begin = wg;
         J.part_begin = pb;
         const int64_t nchunk = (d.R + WG_CHUNK - 1) / WG_CHUNK;
         wg += nchunk * J.OB * J.IB;
-        pb += nchunk * J.OB * J.IB * 4096;
+        pb += nchunk * J.OB * J.IB * WG_PART;
     }
     P.total_wg = wg;
     P.ntgt = ntgt;

@@ -4,5 +4,11 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out && export TMPDIR=/tmp
 for r in 1 2; do for so in tempme_amd/lib/ab/*.so; do
   TEMPME_LIB="$PWD/$so" timeout -k 10 300 python bench_train.py --steps 20 --warmup 2 > gpurun_out/tab.log 2>&1 || exit $?
-  echo "$(basename $so) $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/tab.log)" | tee -a gpurun_out/tab.txt
+  python - "$so" "$r" <<'PY' | tee -a gpurun_out/tab.txt
+import json, sys, os
+d = json.loads([l for l in open("gpurun_out/tab.log") if l.startswith("{")][-1])
+k = d.get("kernels", {})
+print(os.path.basename(sys.argv[1]), "round", sys.argv[2], "value", d["value"], "ms_per_step", d["ms_per_step"],
+      {n: k[n]["avg_ms"] for n in ("wgrad_partial_kernel", "gcn_bwd_kernel", "head_bwd_kernel") if n in k})
+PY
 done; done
