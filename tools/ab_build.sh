@@ -1,7 +1,8 @@
 #!/bin/bash
 # tools/ab_build.sh <name> <encoder.hip>: build tempme_amd/lib/ab/<name>.so from the current sources
 # with encoder.hip replaced by the given file (A/B timing of walk_kernel variants on one box);
-# SAMPLER=<file> / TRAIN=<file> / GM=<file> replace sampler.hip / encoder_train.hip / graphmixer.hip the same way.
+# SAMPLER=<file> / TRAIN=<file> / GM=<file> / TGN=<file> replace sampler.hip / encoder_train.hip / graphmixer.hip /
+# tgn_attn.hip the same way.
 set -e
 cd "$(dirname "$0")/.."
 name=$1; enc=$2
@@ -12,6 +13,7 @@ cp "$enc" "$out/encoder.hip"
 [ -n "$SAMPLER" ] && cp "$SAMPLER" "$out/sampler.hip"
 [ -n "$TRAIN" ] && cp "$TRAIN" "$out/encoder_train.hip"
 [ -n "$GM" ] && cp "$GM" "$out/graphmixer.hip"
+[ -n "$TGN" ] && cp "$TGN" "$out/tgn_attn.hip"
 F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -mcode-object-version=5 -Wno-unused-result -Iinclude $EXTRA"
 pids=()
 for s in $(cd "$out" && ls *.cpp *.hip); do /opt/rocm/bin/hipcc $F -x hip -c "$out/$s" -o "$out/$s.o" & pids+=($!); done

@@ -9,6 +9,6 @@ import json, sys, os
 d = json.loads([l for l in open("gpurun_out/tab.log") if l.startswith("{")][-1])
 k = d.get("kernels", {})
 print(os.path.basename(sys.argv[1]), "round", sys.argv[2], "value", d["value"], "ms_per_step", d["ms_per_step"],
-      {n: k[n]["avg_ms"] for n in ("wgrad_partial_kernel", "gcn_bwd_kernel", "head_bwd_kernel") if n in k})
+      {n: k[n]["avg_ms"] for n in ("wgrad_partial_kernel", "gcn_bwd_kernel", "head_bwd_kernel", "tgn_attn_fwd_kernel", "tgn_attn_bwd_kernel") if n in k})
 PY
 done; done
