@@ -169,18 +169,18 @@ __global__ void __launch_bounds__(64 * ATT_WAVES) tgn_attn_fwd_kernel(tm_tgn_att
 // weighted key sum) merge through LDS in wave order.  A row's neighbours are independent gathers, so
 // four waves keep four of them in flight where one wave walked the chain alone; the 300-row root
 // layer of a bs=100 contrast had only 300 waves for 1,024 SIMDs.
-template <int KPL>
+template <int KPL, int HM>
 __global__ void __launch_bounds__(64 * ATT_WAVES) tgn_attn_fwd_split_kernel(tm_tgn_attn a, float *__restrict__ z,
                                                                             float *__restrict__ stats) {
-    __shared__ float s_acc[ATT_WAVES][ATT_MAXH][KPL][64], s_m[ATT_WAVES][ATT_MAXH], s_l[ATT_WAVES][ATT_MAXH];
+    __shared__ float s_acc[ATT_WAVES][HM][KPL][64], s_m[ATT_WAVES][HM], s_l[ATT_WAVES][HM];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t r = blockIdx.x;
     const int H = a.n_head, N = a.n_ngh, dk = a.d_node + a.d_edge + a.d_time;
     const KeyLane<KPL> L = key_lane<KPL>(a, lane);
-    float q[ATT_MAXH][KPL], acc[ATT_MAXH][KPL], m[ATT_MAXH], l[ATT_MAXH];
-    int64_t mr[ATT_MAXH];
+    float q[HM][KPL], acc[HM][KPL], m[HM], l[HM];
+    int64_t mr[HM];
 #pragma unroll
-    for (int h = 0; h < ATT_MAXH; ++h) {
+    for (int h = 0; h < HM; ++h) {
         m[h] = -__builtin_inff();
         l[h] = 0.f;
         mr[h] = h < H ? pair_row(a, r, h) : 0;
@@ -195,7 +195,7 @@ __global__ void __launch_bounds__(64 * ATT_WAVES) tgn_attn_fwd_split_kernel(tm_t
         float k[KPL];
         build_key<KPL>(a, L, r * N + j, k);
 #pragma unroll
-        for (int h = 0; h < ATT_MAXH; ++h) {
+        for (int h = 0; h < HM; ++h) {
             if (h < H) {
                 float p = 0.f;
 #pragma unroll
@@ -215,7 +215,7 @@ __global__ void __launch_bounds__(64 * ATT_WAVES) tgn_attn_fwd_split_kernel(tm_t
         }
     }
 #pragma unroll
-    for (int h = 0; h < ATT_MAXH; ++h) {
+    for (int h = 0; h < HM; ++h) {
 #pragma unroll
         for (int i = 0; i < KPL; ++i) s_acc[wv][h][i][lane] = acc[h][i];
         if (lane == 0) {
@@ -226,7 +226,7 @@ __global__ void __launch_bounds__(64 * ATT_WAVES) tgn_attn_fwd_split_kernel(tm_t
     __syncthreads();
     if (wv != 0) return;
 #pragma unroll
-    for (int h = 0; h < ATT_MAXH; ++h) {
+    for (int h = 0; h < HM; ++h) {
         if (h >= H) continue;
         float M = s_m[0][h];
 #pragma unroll
@@ -257,7 +257,7 @@ __global__ void __launch_bounds__(64 * ATT_WAVES) tgn_attn_fwd_split_kernel(tm_t
 //   c_j = gz_h.k_j;  d e_j += p_j c_j;  S_h = sum_j p_j e_j c_j;  ds_j = p_j (e_j c_j - S_h) (0 if masked)
 //   d k_j = sum_h p_j e_j gz_h + (ds_j / T) qf_h        (node-feature columns only are written)
 // Pass 1 rebuilds every key (scores and c_j); pass 2 needs only the per-(j,h) scalars kept in LDS.
-template <int KPL, bool DNODE>
+template <int KPL, bool DNODE, int HM>
 __global__ void __launch_bounds__(64 * ATT_WAVES) tgn_attn_bwd_kernel(tm_tgn_attn a, const float *__restrict__ stats,
                                                                       const float *__restrict__ gz,
                                                                       float *__restrict__ d_parts,
@@ -267,14 +267,14 @@ __global__ void __launch_bounds__(64 * ATT_WAVES) tgn_attn_bwd_kernel(tm_tgn_att
     const int64_t r = (int64_t)blockIdx.x * ATT_WAVES + wave;
     if (r >= a.rows) return;
     const int H = a.n_head, N = a.n_ngh, dk = a.d_node + a.d_edge + a.d_time;
-    float *pe_s = sh + (size_t)wave * 3 * N * ATT_MAXH;  // [N][MAXH] p*e
-    float *ds_s = pe_s + N * ATT_MAXH;                   // [N][MAXH] p (0 if masked)
-    float *ec_s = ds_s + N * ATT_MAXH;                   // [N][MAXH] e*c
+    float *pe_s = sh + (size_t)wave * 3 * N * HM;  // [N][MAXH] p*e
+    float *ds_s = pe_s + N * HM;                   // [N][MAXH] p (0 if masked)
+    float *ec_s = ds_s + N * HM;                   // [N][MAXH] e*c
     const KeyLane<KPL> L = key_lane<KPL>(a, lane);
-    float q[ATT_MAXH][KPL], g[ATT_MAXH][KPL], m[ATT_MAXH], il[ATT_MAXH], S[ATT_MAXH];
-    int64_t mr[ATT_MAXH];
+    float q[HM][KPL], g[HM][KPL], m[HM], il[HM], S[HM];
+    int64_t mr[HM];
 #pragma unroll
-    for (int h = 0; h < ATT_MAXH; ++h) {
+    for (int h = 0; h < HM; ++h) {
         S[h] = 0.f;
         mr[h] = h < H ? pair_row(a, r, h) : 0;
         m[h] = h < H ? stats[(r * H + h) * 2] : 0.f;
@@ -291,7 +291,7 @@ __global__ void __launch_bounds__(64 * ATT_WAVES) tgn_attn_bwd_kernel(tm_tgn_att
         float k[KPL];
         build_key<KPL>(a, L, r * N + j, k);
 #pragma unroll
-        for (int h = 0; h < ATT_MAXH; ++h) {
+        for (int h = 0; h < HM; ++h) {
             if (h < H) {
                 float ps = 0.f, pc = 0.f;
 #pragma unroll
@@ -310,9 +310,9 @@ __global__ void __launch_bounds__(64 * ATT_WAVES) tgn_attn_bwd_kernel(tm_tgn_att
                 if (lane == 0) {
                     d_parts[(r * H + h) * N + j] = p * c;
                     if (DNODE) {
-                        pe_s[j * ATT_MAXH + h] = p * e;
-                        ds_s[j * ATT_MAXH + h] = masked ? 0.f : p;
-                        ec_s[j * ATT_MAXH + h] = e * c;
+                        pe_s[j * HM + h] = p * e;
+                        ds_s[j * HM + h] = masked ? 0.f : p;
+                        ec_s[j * HM + h] = e * c;
                     }
                 }
             }
@@ -327,10 +327,10 @@ __global__ void __launch_bounds__(64 * ATT_WAVES) tgn_attn_bwd_kernel(tm_tgn_att
 #pragma unroll
         for (int i = 0; i < KPL; ++i) dkv[i] = 0.f;
 #pragma unroll
-        for (int h = 0; h < ATT_MAXH; ++h) {
+        for (int h = 0; h < HM; ++h) {
             if (h < H) {
-                const float pe = pe_s[j * ATT_MAXH + h];
-                const float ds = ds_s[j * ATT_MAXH + h] * (ec_s[j * ATT_MAXH + h] - S[h]) * invT;
+                const float pe = pe_s[j * HM + h];
+                const float ds = ds_s[j * HM + h] * (ec_s[j * HM + h] - S[h]) * invT;
 #pragma unroll
                 for (int i = 0; i < KPL; ++i) dkv[i] = __builtin_fmaf(pe, g[h][i], __builtin_fmaf(ds, q[h][i], dkv[i]));
             }
@@ -367,7 +367,10 @@ static int check_attn(const tm_tgn_attn *a, const char *who) {
 template <int KPL>
 static void launch_fwd(const tm_tgn_attn &a, float *z, float *stats, hipStream_t s) {
     if (a.n_ngh >= ATT_WAVES) {   // one row per workgroup, its neighbours over the waves
-        tgn_attn_fwd_split_kernel<KPL><<<dim3((unsigned)a.rows), 64 * ATT_WAVES, 0, s>>>(a, z, stats);
+        // the heads' register arrays sized for at most 2 heads where that covers them (TGN's default n_heads):
+        // 143 -> 96 VGPRs, 3 -> 5 waves per SIMD, 0.075 -> 0.055 ms per launch (round 5, profiles/r05_tgn_attn_ab.txt)
+        if (a.n_head <= 2) tgn_attn_fwd_split_kernel<KPL, 2><<<dim3((unsigned)a.rows), 64 * ATT_WAVES, 0, s>>>(a, z, stats);
+        else tgn_attn_fwd_split_kernel<KPL, ATT_MAXH><<<dim3((unsigned)a.rows), 64 * ATT_WAVES, 0, s>>>(a, z, stats);
         return;
     }
     const unsigned blocks = (unsigned)((a.rows + ATT_WAVES - 1) / ATT_WAVES);
@@ -378,8 +381,14 @@ template <int KPL>
 static void launch_bwd(const tm_tgn_attn &a, const float *stats, const float *gz, float *dp, float *dn, hipStream_t s) {
     const unsigned blocks = (unsigned)((a.rows + ATT_WAVES - 1) / ATT_WAVES);
     const size_t lds = dn ? sizeof(float) * 3 * a.n_ngh * ATT_MAXH * ATT_WAVES : 0;
-    if (dn) tgn_attn_bwd_kernel<KPL, true><<<dim3(blocks), 64 * ATT_WAVES, lds, s>>>(a, stats, gz, dp, dn);
-    else tgn_attn_bwd_kernel<KPL, false><<<dim3(blocks), 64 * ATT_WAVES, 0, s>>>(a, stats, gz, dp, dn);
+    // the heads' register arrays sized for at most 2 heads where that covers them (as the forward)
+    if (a.n_head <= 2) {
+        if (dn) tgn_attn_bwd_kernel<KPL, true, 2><<<dim3(blocks), 64 * ATT_WAVES, lds, s>>>(a, stats, gz, dp, dn);
+        else tgn_attn_bwd_kernel<KPL, false, 2><<<dim3(blocks), 64 * ATT_WAVES, 0, s>>>(a, stats, gz, dp, dn);
+    } else {
+        if (dn) tgn_attn_bwd_kernel<KPL, true, ATT_MAXH><<<dim3(blocks), 64 * ATT_WAVES, lds, s>>>(a, stats, gz, dp, dn);
+        else tgn_attn_bwd_kernel<KPL, false, ATT_MAXH><<<dim3(blocks), 64 * ATT_WAVES, 0, s>>>(a, stats, gz, dp, dn);
+    }
 }
 
 #define TM_KPL_DISPATCH(KPLV, CALL) \
