@@ -567,7 +567,9 @@ class TGN(nn.Module):
             prepared = self.prepare_contrast(src_idx, tgt_idx, bgd_idx, cut_time, subgraph_src, subgraph_tgt,
                                              subgraph_bgd, edge_attr)
         emb = self.node_embeddings(None, None, None, None, explain_weights, edge_attr, prepared=prepared)
-        return emb[:B], emb[B:2 * B], emb[2 * B:]
+        # split (one backward: a cat of the three gradients) rather than three slices (a zero-filled full-size
+        # gradient, a copy and an add each)
+        return tuple(emb.split(B)) if B > 0 else (emb[:0], emb[:0], emb[:0])
 
     def prepare_contrast(self, src_idx, tgt_idx, bgd_idx, cut_time, subgraph_src, subgraph_tgt, subgraph_bgd,
                          edge_attr=None):
@@ -599,10 +601,17 @@ class TGN(nn.Module):
         """tgn.py:201-218 -> (pos_score [B,1], neg_score [B,1]).  ``prepared``: prepare_contrast's
         output for these same inputs (optional, shared by several contrasts of one batch)."""
         B = len(src_idx)
-        s, d, n = self.get_node_emb(src_idx, tgt_idx, bgd_idx, cut_time, e_idx, subgraph_src, subgraph_tgt,
-                                    subgraph_bgd, explain_weights, edge_attr, prepared=prepared)
-        score = self.affinity(torch.cat([s, s], dim=0), _cat_rows([d, n])).squeeze(dim=0)   # d, n: rows of one emb
-        return score[:B], score[B:]
+        if prepared is None:
+            prepared = self.prepare_contrast(src_idx, tgt_idx, bgd_idx, cut_time, subgraph_src, subgraph_tgt,
+                                             subgraph_bgd, edge_attr)
+        emb = self.node_embeddings(None, None, None, None, explain_weights, edge_attr, prepared=prepared)
+        if B == 0:
+            return emb[:0, :1], emb[:0, :1]
+        # get_node_emb's (s, d, n) as two pieces of one split: [d; n] is emb's tail (no copy), and the backward
+        # is one cat instead of a zero-filled full-size gradient, a copy and an add per slice
+        s, dn = emb.split([B, 2 * B])
+        score = self.affinity(torch.cat([s, s], dim=0), dn).squeeze(dim=0)
+        return tuple(score.split(B))
 
     def retrieve_edge_features(self, subgraph_src, subgraph_tgt, subgraph_bgd):
         """tgn.py:220-228: [E_feat[hop-1 eids], E_feat[hop-2 eids]] for the three sides."""
