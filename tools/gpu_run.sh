@@ -81,6 +81,7 @@ for s in "$@"; do
         testsall) step pytest_gpu_all 1100 python -u -m pytest tests -q -m gpu -rfEs --timeout 300 --timeout-method thread ;;
         variants) step pytest_variants 600 python -u -m pytest tests/test_gpu_variants.py tests/test_gpu_enron.py -v -m gpu -rfEs --timeout 300 --timeout-method thread -k "variants or cpp_host" ;;
         tab) step tab 1100 ./tools/train_ab.sh ;;
+        strong) step strong 900 ./tools/strong.sh ;;
         dab) step dab 900 ./tools/dropin_ab.sh ;;
         dropintrace) step dropintrace 300 rocprofv3 --kernel-trace -d gpurun_out/ditrace -o run --output-format csv -- python tools/dropin_timing.py && python tools/dropin_trace_summary.py > gpurun_out/dropin_trace.txt 2>&1 ;;
         dropinprof) TEMPME_DROPIN_PROFILE=1 step dropinprof 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
