@@ -85,19 +85,9 @@ class ExplainPipeline:
         return self.h1, self.h2
 
     def run(self, src, dst, ts, eidx, event_ids):
-        """Returns (imp [3,E,W], hop-1 weights [3,E,N], hop-2 weights [3,E,N^2]) device tensors.  The per-edge-id
-        tables depend on the graph and the weights only, so they are built on a second stream while the events
-        are sampled (both small launches; the walk kernel waits for both)."""
-        self._alloc(int(src.numel()))
-        cur = torch.cuda.current_stream(self.dev)
-        if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(device=self.dev)
-        side = self._side
-        side.wait_stream(cur)            # ordered after everything before (the previous call's readers of gf / etab)
-        with torch.cuda.stream(side):
-            self.tables()
+        """Returns (imp [3,E,W], hop-1 weights [3,E,N], hop-2 weights [3,E,N^2]) device tensors."""
         self.sample(src, dst, ts, eidx, event_ids)
-        cur.wait_stream(side)
+        self.tables()
         self.encode(ts)
         self.explain()
         E, N, W = self._E, self.N, self.W
