@@ -400,7 +400,10 @@ def main():
     ap.add_argument("--weak", action="store_true", help="primary line weak scaling (--batches per rank)")
     ap.add_argument("--no-edge-table", action="store_true",
                     help="lin_event's edge-feature product per walk position instead of per edge id")
-    ap.add_argument("--streams", type=int, default=1, help="steps in flight (PipelinedExplainer)")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="steps in flight (PipelinedExplainer); 0 = auto: 2 when a rank holds <= 24 reference batches "
+                         "per step (the 8-GPU share of the metric's step: 1.140 -> 1.074 ms per step timed on one GPU, "
+                         "profiles/r05_strong_estimate.txt), else 1")
     ap.add_argument("--no-node-zero", action="store_true",
                     help="do not specialise the walk kernel for an all-zero node-feature table (A/B)")
     ap.add_argument("--contrast", choices=("auto", "graphmixer", "none"), default="auto",
@@ -476,7 +479,8 @@ def main():
     ex = tm.TempME(Base(), "tgn", cfg["name"], out_dim=40, hid_dim=64, device=dev,
                    null_model={k: 1.0 / 12 for k in range(1, 13)}).to(dev).eval()
     ex.node_zero_specialization = not args.no_node_zero
-    S = max(1, args.streams)
+    rank_batches = args.batches if args.weak else args.batches // max(1, world)
+    S = args.streams if args.streams > 0 else (2 if rank_batches <= 24 else 1)
     contrast = args.contrast if args.contrast != "auto" else ("graphmixer" if args.config == 4 else "none")
     gm = None
     if contrast == "graphmixer":
