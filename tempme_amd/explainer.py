@@ -281,9 +281,10 @@ class TempME(nn.Module):
     def _hip_eval_ok(self):
         """The eval kernels cover every constructor variant (use_temporal_guidance /
         use_dependency_aware_sampling through tm_weights_variant, if_cat_feature and hid_dim through
-        tm_weights_create_ex) for hid_dim a multiple of 16 up to 256: the fused walk kernel for the default
-        shape (hid_dim 64 with the category feature), the LDS-tiled kernels for the others."""
-        ok = self.hid_dim % 16 == 0 and 0 < self.hid_dim <= 256
+        tm_weights_create_ex) for hid_dim up to 256: the fused walk kernel for the default shape (hid_dim 64
+        with the category feature), the LDS-tiled kernels for the others; a hid_dim that is not a multiple of
+        16 runs them on weights zero-padded to the next one (_pad_hidden)."""
+        ok = 0 < self.hid_dim <= 256
         if not ok and not getattr(self, "_warned_torch", False):
             warnings.warn("TempME(if_cat_feature=%s, hid_dim=%d): no HIP kernel instance for this constructor "
                           "variant; forward / retrieve_edge_imp_node run the torch-op formulation on the device"
@@ -376,19 +377,63 @@ class TempME(nn.Module):
         if self._packed is None or self._packed_key != key or force:
             if self._packed is None:
                 h = L.C.c_void_p()
-                L.check(L.lib().tm_weights_create_ex(self.edge_dim, self.node_dim, self.hid_dim, int(bool(self.if_cat)),
-                                                     dev.index, L.C.byref(h)), "tm_weights_create")
+                L.check(L.lib().tm_weights_create_ex(self.edge_dim, self.node_dim, self._hid_packed(),
+                                                     int(bool(self.if_cat)), dev.index, L.C.byref(h)),
+                        "tm_weights_create")
                 self._packed = _Packed(h)
                 L.check(L.lib().tm_weights_variant(h, int(bool(self.use_temporal_guidance)),
                                                    int(bool(self.use_dependency_aware_sampling))), "tm_weights_variant")
                 self.feature_tables()
                 self._set_node_zero(h)
             self._raw = [w.detach().to(device=dev, dtype=torch.float32).contiguous() for w in ws]
+            if self._hid_packed() != self.hid_dim:
+                self._raw = self._pad_hidden(self._raw)
             arr = (L.C.c_void_p * L.N_WEIGHTS)(*[w.data_ptr() for w in self._raw])
             L.check(L.lib().tm_weights_pack(self._packed.h, arr, L.stream_ptr(dev)), "tm_weights_pack")
             self._packed_key = key
             self._prep_dirty = self._prep_dirty_fast = True   # side streams must wait for this work
         return self._packed.h
+
+    def _hid_packed(self):
+        """The hidden width the kernels run at: hid_dim rounded up to a multiple of 16 (their tile)."""
+        return -(-self.hid_dim // 16) * 16
+
+    def _pad_hidden(self, raw):
+        """The tm_weights-ordered tensors of a hid_dim h that is not a multiple of 16, zero-padded to the
+        packed width H (_hid_packed): every hidden unit past h gets zero weights and bias, so it carries
+        ReLU(0) = 0 and adds exact zeros to every later sum -- the padded network computes the same function.
+        The concatenations keep their parts' offsets at H: [u_s | u_t] (the attention's 2h input,
+        explainer_new.py:768-846) maps column j >= h to H + j - h, and [out | one-hot 12] (mlp_dim,
+        :174-201) the same; the gate's h // 2 layer pads to H // 2."""
+        h, H = self.hid_dim, self._hid_packed()
+        dev = raw[0].device
+        ar = lambda n, o=0: torch.arange(n, device=dev) + o  # noqa: E731
+        hm, gm = ar(h), ar(h // 2)
+        m2 = torch.cat([hm, ar(h, H)])
+        cm = torch.cat([hm, ar(12, H)]) if self.if_cat else hm
+        M2 = H + 12 if self.if_cat else H
+        one = ar(1)
+
+        def place(t, rows, nr, cols=None, nc=None):
+            if cols is None:     # a bias
+                out = t.new_zeros(nr)
+                out[rows] = t
+                return out
+            out = t.new_zeros(nr, nc)
+            out[rows[:, None], cols[None, :]] = t
+            return out
+
+        # (rows map, padded rows, cols map, padded cols) per weight; None keeps the tensor
+        spec = {2: (hm, H, ar(raw[2].shape[1]), raw[2].shape[1]), 4: (hm, H, hm, H),
+                6: (m2, 2 * H, m2, 2 * H), 8: (m2, 2 * H, m2, 2 * H), 10: (hm, H, m2, 2 * H), 12: (hm, H, hm, H),
+                14: (cm, M2, cm, M2), 16: (hm, H, cm, M2), 18: (one, 1, hm, H),
+                20: (hm, H, ar(raw[20].shape[1]), raw[20].shape[1]), 22: (gm, H // 2, hm, H), 24: (one, 1, gm, H // 2)}
+        out = list(raw)
+        for i, (rows, nr, cols, nc) in spec.items():
+            out[i] = place(raw[i], rows, nr, cols, nc).contiguous()
+            if nr > 1:
+                out[i + 1] = place(raw[i + 1], rows, nr).contiguous()
+        return out
 
     def feature_tables(self):
         dev = self._dev()
