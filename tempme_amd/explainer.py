@@ -297,7 +297,7 @@ class TempME(nn.Module):
         use_dependency_aware_sampling, if_cat_feature) for the dims tm_encoder_train_supported accepts:
         hid_dim a multiple of 16 whose tiles fit the LDS (every hid_dim up to 192 at Enron / Wikipedia
         feature dims)."""
-        key = (self.edge_dim, self.node_dim, self.hid_dim, bool(self.if_cat))
+        key = (self.edge_dim, self.node_dim, self._hid_packed(), bool(self.if_cat))
         c = self.__dict__.get("_train_ok")
         if c is None or c[0] != key:
             ok = self._hip_eval_ok() and bool(L.lib().tm_encoder_train_supported(*[int(x) for x in key]))
@@ -398,6 +398,28 @@ class TempME(nn.Module):
         """The hidden width the kernels run at: hid_dim rounded up to a multiple of 16 (their tile)."""
         return -(-self.hid_dim // 16) * 16
 
+    def _pad_maps(self, dev):
+        """Index maps of the zero-padding (_pad_hidden), cached per device: hm = the h hidden units, gm = the
+        gate's h // 2, m2 = [u_s | u_t] (2h -> 2H), cm = [out | one-hot 12] (mlp_dim -> H + 12), and per
+        tm_weights index i the (rows map, padded rows, cols map, padded cols) of its weight (its bias, at
+        i + 1, takes the rows map when padded rows > 1)."""
+        c = self.__dict__.get("_pad_c")
+        if c is not None and c[0] == dev:
+            return c[1]
+        h, H = self.hid_dim, self._hid_packed()
+        ar = lambda n, o=0: torch.arange(n, device=dev) + o  # noqa: E731
+        hm, gm, one = ar(h), ar(h // 2), ar(1)
+        m2 = torch.cat([hm, ar(h, H)])
+        cm = torch.cat([hm, ar(12, H)]) if self.if_cat else hm
+        M2 = H + 12 if self.if_cat else H
+        dn, kg = self.node_dim, self.edge_dim + self.time_dim
+        spec = {2: (hm, H, ar(dn), dn), 4: (hm, H, hm, H), 6: (m2, 2 * H, m2, 2 * H), 8: (m2, 2 * H, m2, 2 * H),
+                10: (hm, H, m2, 2 * H), 12: (hm, H, hm, H), 14: (cm, M2, cm, M2), 16: (hm, H, cm, M2),
+                18: (one, 1, hm, H), 20: (hm, H, ar(kg), kg), 22: (gm, H // 2, hm, H), 24: (one, 1, gm, H // 2)}
+        maps = dict(hm=hm, gm=gm, m2=m2, cm=cm, M2=M2, spec=spec)
+        self.__dict__["_pad_c"] = (dev, maps)
+        return maps
+
     def _pad_hidden(self, raw):
         """The tm_weights-ordered tensors of a hid_dim h that is not a multiple of 16, zero-padded to the
         packed width H (_hid_packed): every hidden unit past h gets zero weights and bias, so it carries
@@ -405,35 +427,63 @@ class TempME(nn.Module):
         The concatenations keep their parts' offsets at H: [u_s | u_t] (the attention's 2h input,
         explainer_new.py:768-846) maps column j >= h to H + j - h, and [out | one-hot 12] (mlp_dim,
         :174-201) the same; the gate's h // 2 layer pads to H // 2."""
-        h, H = self.hid_dim, self._hid_packed()
-        dev = raw[0].device
-        ar = lambda n, o=0: torch.arange(n, device=dev) + o  # noqa: E731
-        hm, gm = ar(h), ar(h // 2)
-        m2 = torch.cat([hm, ar(h, H)])
-        cm = torch.cat([hm, ar(12, H)]) if self.if_cat else hm
-        M2 = H + 12 if self.if_cat else H
-        one = ar(1)
-
-        def place(t, rows, nr, cols=None, nc=None):
-            if cols is None:     # a bias
-                out = t.new_zeros(nr)
-                out[rows] = t
-                return out
-            out = t.new_zeros(nr, nc)
-            out[rows[:, None], cols[None, :]] = t
-            return out
-
-        # (rows map, padded rows, cols map, padded cols) per weight; None keeps the tensor
-        spec = {2: (hm, H, ar(raw[2].shape[1]), raw[2].shape[1]), 4: (hm, H, hm, H),
-                6: (m2, 2 * H, m2, 2 * H), 8: (m2, 2 * H, m2, 2 * H), 10: (hm, H, m2, 2 * H), 12: (hm, H, hm, H),
-                14: (cm, M2, cm, M2), 16: (hm, H, cm, M2), 18: (one, 1, hm, H),
-                20: (hm, H, ar(raw[20].shape[1]), raw[20].shape[1]), 22: (gm, H // 2, hm, H), 24: (one, 1, gm, H // 2)}
         out = list(raw)
-        for i, (rows, nr, cols, nc) in spec.items():
-            out[i] = place(raw[i], rows, nr, cols, nc).contiguous()
+        for i, (rows, nr, cols, nc) in self._pad_maps(raw[0].device)["spec"].items():
+            w = raw[i].new_zeros(nr, nc)
+            w[rows[:, None], cols[None, :]] = raw[i]
+            out[i] = w
             if nr > 1:
-                out[i + 1] = place(raw[i + 1], rows, nr).contiguous()
+                b = raw[i + 1].new_zeros(nr)
+                b[rows] = raw[i + 1]
+                out[i + 1] = b
         return out
+
+    def _unpad_grads(self, grads, idx):
+        """Gradients the kernels wrote for the padded tensors of tm_weights indices ``idx`` -> the
+        gradients of the module's own (unpadded) parameters: the rows / columns _pad_hidden placed."""
+        if self._hid_packed() == self.hid_dim:
+            return grads
+        spec = self._pad_maps(grads[0].device)["spec"]
+        out = list(grads)
+        for k, i in enumerate(idx):
+            if i in spec:
+                rows, _, cols, _ = spec[i]
+                out[k] = grads[k][rows[:, None], cols[None, :]]
+            elif i - 1 in spec and spec[i - 1][1] > 1:
+                out[k] = grads[k][spec[i - 1][0]]
+        return out
+
+    def _padded_shapes(self, idx):
+        return [tuple(self._raw[i].shape) for i in idx]
+
+    def _drop_packed(self, drop):
+        """A dropout keep-mask in the module's column layout (dropout_cols: alpha 2 | attention.MLP hidden h |
+        MLP hidden mlp_dim) -> the padded kernels' layout (2 | H | H + 12); a padded unit's column repeats
+        column 0 (its activation is zero either way)."""
+        if drop is None or self._hid_packed() == self.hid_dim:
+            return drop
+        m = self._pad_maps(drop.device)
+        h, H = self.hid_dim, self._hid_packed()
+        ncol = -(-(2 + H + m["M2"]) // 16) * 16
+        src = torch.zeros(ncol, dtype=torch.long, device=drop.device)
+        src[:2] = torch.arange(2, device=drop.device)
+        src[2 + m["hm"]] = 2 + m["hm"]
+        src[2 + H + m["cm"]] = 2 + h + torch.arange(self.mlp_dim, device=drop.device)
+        return drop.index_select(1, src).contiguous()
+
+    def _gate_masks_packed(self, masks):
+        """edge_dependency_gcn's keep-masks [n_pos, h] / [n_pos, h // 2] -> [n_pos, H] / [n_pos, H // 2]."""
+        k1, k2, sc1, sc2 = masks
+        if k1 is None or self._hid_packed() == self.hid_dim:
+            return masks
+        m = self._pad_maps(k1.device)
+        H = self._hid_packed()
+
+        def widen(k, idx, n):
+            src = torch.zeros(n, dtype=torch.long, device=k.device)
+            src[idx] = torch.arange(idx.numel(), device=k.device)
+            return k.index_select(1, src).contiguous()
+        return widen(k1, m["hm"], H), widen(k2, m["gm"], H // 2), sc1, sc2
 
     def feature_tables(self):
         dev = self._dev()
@@ -555,6 +605,7 @@ class TempME(nn.Module):
         dev = self._dev()
         nt, et = self.feature_tables()
         n = G * B * W
+        drop = self._drop_packed(drop)
         out = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
         ws = torch.empty(L.lib().tm_encoder_workspace_bytes(self.packed_weights(), n), dtype=torch.uint8, device=dev)
         L.check(L.lib().tm_encoder_train_fwd(self.packed_weights(), L.ptr(nt), L.ptr(et), G, B, W, L.ptr(node6),
@@ -569,9 +620,10 @@ class TempME(nn.Module):
         nt, et = self.feature_tables()
         n = G * B * W
         R = 3 * n
-        de, dn, h = self.edge_dim, self.node_dim, self.hid_dim
+        drop = self._drop_packed(drop)
+        de, dn, h = self.edge_dim, self.node_dim, self._hid_packed()   # the packed (padded) widths
         kev = de + 3 + dn
-        KE, DN, KM = -(-kev // 16) * 16, -(-dn // 16) * 16, -(-self.mlp_dim // 16) * 16
+        KE, DN, KM = -(-kev // 16) * 16, -(-dn // 16) * 16, -(-(h + 12 if self.if_cat else h) // 16) * 16
         e = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
         b = dict(imp=None, dlogit=e(n), M2=e(n, h), dM2=e(n, h), M1d=e(n, KM), dM1=e(n, KM), X=e(n, KM), dY2=e(n, h),
                  H1d=e(n, h), dH1=e(n, h), O=e(n, 2 * h), dP=e(n, 2 * h), dQ=e(2, n, 2 * h), dF=e(n, 3, 2 * h),
@@ -582,11 +634,11 @@ class TempME(nn.Module):
                                        L.ptr(eid3), L.ptr(ts3), L.ptr(cat), L.ptr(cut), L.ptr(cnt), L.ptr(drop),
                                        drop_scale, L.ptr(ws), L.ptr(d_imp), L.C.byref(io), L.stream_ptr(dev)),
                 "TempME.forward backward")
-        grads = [torch.empty_like(p, memory_format=torch.contiguous_format) for p in self._encoder_params()]
+        grads = [e(*s) for s in self._padded_shapes(_ENC_IDX)]
         gp = (L.C.c_void_p * len(grads))(*[t.data_ptr() for t in grads])
         L.check(L.lib().tm_encoder_wgrad(self.packed_weights(), G, B, W, L.C.byref(io), L.ptr(ws), gp,
                                          L.stream_ptr(dev)), "TempME.forward weight gradients")
-        return tuple(grads)
+        return tuple(self._unpad_grads(grads, _ENC_IDX))
 
     def _gate_params(self):
         """edge_dependency_gcn's three Linear pairs and the time encoder (the cached weight list)."""
@@ -632,7 +684,7 @@ class TempME(nn.Module):
 
     def _expl_io(self, R):
         dev = self._dev()
-        h, dn = self.hid_dim, self.node_dim
+        h, dn = self._hid_packed(), self.node_dim
         KD, DN = -(-(self.edge_dim + dn) // 16) * 16, -(-dn // 16) * 16
         e = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
         b = dict(X=e(R, KD), G1=e(R, h), G2=e(R, h // 2), z=e(R), gate=e(R), d_gate=e(R), dz=e(R), dG2=e(R, h // 2),
@@ -642,7 +694,8 @@ class TempME(nn.Module):
     def _explain_fwd(self, args, imp):
         """-> p [G B N | G B N^2] (hop-1 then hop-2 maxima), and with the subgraph node ids in args their
         padding mask in the same layout (else None), and the backward's buffers."""
-        eid3, ts3, s1e, s2e, (k1, k2, sc1, sc2), G, B, W, N = args[:9]
+        eid3, ts3, s1e, s2e, masks, G, B, W, N = args[:9]
+        k1, k2, sc1, sc2 = self._gate_masks_packed(masks)
         dev = self._dev()
         _, et = self.feature_tables()
         b, io = self._expl_io(G * B * 3 * W)
@@ -665,11 +718,12 @@ class TempME(nn.Module):
         return p[:n1 + n2], (p[n1 + n2:2 * (n1 + n2)] if pad else None), (b, io)
 
     def _explain_bwd(self, args, imp, bufs, dp1, dp2):
-        eid3, ts3, s1e, s2e, (k1, k2, sc1, sc2), G, B, W, N = args[:9]
+        eid3, ts3, s1e, s2e, masks, G, B, W, N = args[:9]
+        k1, k2, sc1, sc2 = self._gate_masks_packed(masks)
         dev = self._dev()
         b, io = bufs
         d_imp = torch.empty(max(G * B * W, 1), dtype=torch.float32, device=dev)
-        grads = [torch.empty_like(p, memory_format=torch.contiguous_format) for p in self._gate_params()]
+        grads = [torch.empty(s, dtype=torch.float32, device=dev) for s in self._padded_shapes(_GATE_IDX)]
         gp = (L.C.c_void_p * len(grads))(*[t.data_ptr() for t in grads])
         dp1 = dp1.to(dev, torch.float32).contiguous()
         dp2 = dp2.to(dev, torch.float32).contiguous()
@@ -677,7 +731,7 @@ class TempME(nn.Module):
                                              L.ptr(s1e), L.ptr(s2e), L.ptr(k1), L.ptr(k2), sc1, sc2, L.ptr(dp1),
                                              L.ptr(dp2), L.C.byref(io), L.ptr(d_imp), gp, L.stream_ptr(dev)),
                 "retrieve_edge_imp_node backward")
-        return d_imp[:G * B * W], grads
+        return d_imp[:G * B * W], self._unpad_grads(grads, _GATE_IDX)
 
     # ------------------------------------------------------------------ reference API
     def forward(self, walks, cut_time_l, edge_identify):
@@ -1265,6 +1319,9 @@ def _C_APPLY(fn):
 
 
 _DP = torch.Tensor.data_ptr
+# tm_weights indices of TempME._encoder_params / _gate_params
+_ENC_IDX = tuple(range(20)) + (26, 27)
+_GATE_IDX = tuple(range(20, 26)) + (26, 27)
 _VER = operator.attrgetter("_version")
 _RG = operator.attrgetter("requires_grad")
 

@@ -103,11 +103,12 @@ def test_encoder_backward_matches_autograd(dev, de, G, B, N, train, zn):
 
 # constructor variants (explainer_new.py:103-105, :121-125): the plain Attention (no time scaling, no
 # alpha / hidden dropout), no category one-hot, and hid_dim 32 / 128 / 192 (128 and 192 run the 16-walk
-# head_bwd_kernel instance, 192 also the 16-walk head_kernel)
+# head_bwd_kernel instance, 192 also the 16-walk head_kernel); 40 / 20 run zero-padded to 48 / 32
+# (TempME._pad_hidden: the gradients are read back from the padded ones, the keep-masks widened)
 VARIANTS = {"notg": dict(use_temporal_guidance=False), "nocat": dict(if_cat_feature=False),
             "h32": dict(hid_dim=32), "h128": dict(hid_dim=128),
             "h128_notg_nocat": dict(hid_dim=128, use_temporal_guidance=False, if_cat_feature=False),
-            "h192": dict(hid_dim=192)}
+            "h192": dict(hid_dim=192), "h40": dict(hid_dim=40), "h20_nocat": dict(hid_dim=20, if_cat_feature=False)}
 
 
 @pytest.mark.parametrize("var", sorted(VARIANTS))

@@ -104,14 +104,14 @@ def test_explain_backward_matches_autograd(dev, de, G, B, N, train):
                                                                                float(gr.norm()))
 
 
-@pytest.mark.parametrize("var", ["nodep", "h32", "h128"])
+@pytest.mark.parametrize("var", ["nodep", "h32", "h128", "h40"])
 def test_explain_backward_variants_match_autograd(dev, var):
     """use_dependency_aware_sampling=False (no gate: d imp through the scatter-max alone, no gradient to the
-    time encoder from this path) and the gate at hid_dim 32 / 128."""
+    time encoder from this path) and the gate at hid_dim 32 / 128 / 40 (40: zero-padded to 48)."""
     from tempme_amd import TempME
     from tempme_amd.explainer import _ExplainFn
     kw = {"nodep": dict(hid_dim=64, use_dependency_aware_sampling=False), "h32": dict(hid_dim=32),
-          "h128": dict(hid_dim=128)}[var]
+          "h128": dict(hid_dim=128), "h40": dict(hid_dim=40)}[var]
     h = kw.pop("hid_dim")
     rng = np.random.RandomState(h)
     de, G, B, N = 32, 2, 6, 10

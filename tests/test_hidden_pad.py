@@ -55,3 +55,38 @@ def test_padded_weights_compute_the_same_function(hid, if_cat, tg):
         eb = er.edge_importance(sp, d["e_feat"].float(), a, x["eid"], x["ts"], x["sub_node"], x["sub_eid"])
         for u, v in zip(ea, eb):
             np.testing.assert_allclose(v.numpy(), u.numpy(), rtol=1e-5, atol=1e-6, err_msg=s)
+
+
+@pytest.mark.parametrize("hid,if_cat", [(40, True), (20, False)])
+def test_pad_maps_round_trip(hid, if_cat):
+    """The training side of the padding: _unpad_grads reads back exactly what _pad_hidden placed, and the
+    dropout / gate keep-masks move each hidden unit's column to its padded position."""
+    from tempme_amd import TempME
+    from tempme_amd.explainer import _ENC_IDX, _GATE_IDX
+    d = load("synth")
+    torch.manual_seed(hid)
+    ex = TempME(_Base(d["n_feat"], d["e_feat"]), "tgn", "x", out_dim=40, hid_dim=hid, if_cat_feature=if_cat,
+                null_model={k + 1: float(v) for k, v in enumerate(d["null"])}).train()
+    H = ex._hid_packed()
+    raw = [w.detach().float().contiguous() for w in ex._weight_list()]
+    pad = ex._pad_hidden(raw)
+    ex._raw = pad
+    for idx in (_ENC_IDX, _GATE_IDX):
+        assert ex._padded_shapes(idx) == [tuple(pad[i].shape) for i in idx]
+        back = ex._unpad_grads([pad[i] for i in idx], idx)
+        for i, b in zip(idx, back):
+            assert torch.equal(b, raw[i]), i
+    n = 7
+    drop = torch.randint(0, 2, (n, ex.dropout_cols()), dtype=torch.uint8)
+    dp = ex._drop_packed(drop)
+    hm = 12 if if_cat else 0
+    assert dp.shape == (n, -(-(2 + H + H + hm) // 16) * 16)
+    assert torch.equal(dp[:, :2 + hid], drop[:, :2 + hid])
+    assert torch.equal(dp[:, 2 + H:2 + H + hid], drop[:, 2 + hid:2 + 2 * hid])
+    if if_cat:
+        assert torch.equal(dp[:, 2 + 2 * H:2 + 2 * H + 12], drop[:, 2 + 2 * hid:2 + 2 * hid + 12])
+    k1 = torch.randint(0, 2, (n, hid), dtype=torch.uint8)
+    k2 = torch.randint(0, 2, (n, hid // 2), dtype=torch.uint8)
+    p1, p2, _, _ = ex._gate_masks_packed((k1, k2, 1.0, 1.0))
+    assert p1.shape == (n, H) and p2.shape == (n, H // 2)
+    assert torch.equal(p1[:, :hid], k1) and torch.equal(p2[:, :hid // 2], k2)
