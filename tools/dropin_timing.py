@@ -109,6 +109,27 @@ def main():
         setattr(lib, name, f)
     for name in ("_fast_state", "_dropin_ctx", "_hip_eval_ok"):
         del ex.__dict__[name]
+    # one side's forward, split: the module call, forward() without nn.Module.__call__, and the C++ host
+    # side's entry alone (csrc/dropin_ext.cpp Fast.forward: checks, output allocation, tm_dropin_forward)
+    fx = ex.__dict__.get("_fastx")
+    if fx is not None:
+        ins = []
+        for b in range(nb):
+            idx = np.arange(b * B, (b + 1) * B)
+            _, _, _, w_s, _, _, _ = P.get_item(pk, idx)
+            e_s, _, _ = P.get_item_edge(ed, idx)
+            ins.append((w_s, cut[idx], e_s))
+        calls = (("module call", lambda w, c, e: ex(w, c, e)), ("forward()", lambda w, c, e: ex.forward(w, c, e)),
+                 ("C++ Fast.forward", lambda w, c, e, _f=fx[0].forward: _f(w[0], w[1], w[2], w[3], c, e)))
+        for name, fn in calls:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for r in range(reps):
+                for w, c, e in ins:
+                    fn(w, c, e)
+            el = time.perf_counter() - t0
+            torch.cuda.synchronize()
+            print("  one side, %-18s %6.1f us per call" % (name, el / (reps * nb) * 1e6))
     # one batch alone, GPU included
     lat = []
     for b in range(nb):
