@@ -121,7 +121,7 @@ def main():
             ins.append((w_s, cut[idx], e_s))
         calls = (("module call", lambda w, c, e: ex(w, c, e)), ("forward()", lambda w, c, e: ex.forward(w, c, e)),
                  ("C++ Fast.forward", lambda w, c, e, _f=fx[0].forward: _f(w[0], w[1], w[2], w[3], c, e)))
-        for name, fn in calls:
+        for name, fn in calls[::-1] + calls:     # both orders: the first loop of a run pays any warm-up
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for r in range(reps):
