@@ -524,7 +524,9 @@ def main():
     inputs = make_inputs(n_steps, rank, world, per_rank, (src, dst, ts, eidx), dev)
     for k in range(S):                             # every stream's buffers allocated before timing
         run_step(inputs[k % n_steps])
+    builds0 = pipe.tabs.builds
     el, prof = timed(run_step, pipes, inputs, args.warmup, args.steps, dist, backend, dev, L)
+    tab_builds = pipe.tabs.builds - builds0
     weak = None
     if world > 1:
         # the secondary figure: the other scaling mode on the same ranks
@@ -567,6 +569,14 @@ def main():
         samp = dict(kernels.get("events_kernel", {}))
         if samp and traffic.get("events_kernel") is not None:
             samp["traffic"] = traffic["events_kernel"]
+        # the per-edge-id tables (gate factor + lin_event's edge product over all edge ids) are a function of the
+        # weight state, the edge-feature table and the graph: built once (EdgeTables), timed here alone
+        pipe.tabs.build(timed=True)
+        edge_tables = {"ms": round(pipe.tabs.build_ms, 3), "edge_ids": int(pipe.gf.numel()),
+                       "builds_in_timed_region": tab_builds,
+                       "what": "tm_edge_tables (gate_reg_kernel) over every edge id: built once per weight state "
+                               "(tm_weights_version), edge-feature table and graph, outside the per-step unit; the "
+                               "reference recomputes the gate per walk position (same values)"}
         total = world * args.steps * per_rank
         out = {"metric": METRIC, "value": round(total / el, 2), "unit": "edges/s", "n_gpus": n_gpus, "ranks": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
@@ -578,8 +588,9 @@ def main():
                           "batch_size": B, "global_batches_per_step": per_rank * world // B,
                           "events_per_step_per_gpu": per_rank, "parallelism": f"dp{world} (whole batches per rank)",
                           "steps_in_flight": S, "base_contrast": contrast,
+                          "edge_tables": "per weight state (see edge_tables), not per step",
                           "walk_kernel_zero_node_features": zn},
-               "roofline": roof, "kernels": kernels, "sampling_roofline": samp or None}
+               "roofline": roof, "kernels": kernels, "sampling_roofline": samp or None, "edge_tables": edge_tables}
         if weak is not None:
             out["weak" if strong else "strong"] = weak
         if not args.no_extras:

@@ -175,6 +175,10 @@ int tm_weights_variant(tm_weights *w, int32_t temporal_guidance, int32_t depende
  * the event projection, bit for bit, and tm_encoder_fwd_tab computes one of them and reads no node row.  The
  * caller re-asserts it whenever the table changes; 0 (the default) makes no assumption. */
 int tm_weights_set_node_zero(tm_weights *w, int32_t node_zero);
+/* A process-wide stamp of the weights' packed state: every create / pack / variant / node-zero change takes
+ * the next value of one global counter (never 0), so a cache keyed on it can never confuse two weight states,
+ * even of two objects allocated at the same address.  Caches of per-edge-id tables (tm_edge_tables) key on it. */
+uint64_t tm_weights_version(const tm_weights *w);
 int tm_weights_free(tm_weights *w);
 
 /* Workspace bytes tm_encoder_fwd needs for n_walks walks. */
@@ -358,8 +362,10 @@ int tm_dropin_set_stream(tm_dropin *d, int32_t k, void *stream);
  * rows; 0 = none): tm_dropin_forward's out_gfac then reads the factor of every walk position whose (edge id,
  * fp32 time) was computed before and computes only the others (explainer_new.py:367-386 is a function of
  * (E[e], t) alone: the results are bit-identical).  Emptied whenever the weights (tm_weights_pack /
- * _variant / _set_node_zero) or the edge-feature table change. */
+ * _variant / _set_node_zero: tm_weights_version changes) or the edge-feature table's address change; a
+ * caller that rewrites the table IN PLACE calls tm_dropin_gate_cache_clear. */
 int tm_dropin_gate_cache(tm_dropin *d, int64_t n_edge_rows);
+int tm_dropin_gate_cache_clear(tm_dropin *d);
 /* TempME.forward (explainer_new.py:174-201) for one call (B events x W walks) in one library call on side
  * stream k: with sync != 0 every side stream first waits (once) for `stream` (weights / tables prepared
  * there, or a device cut tensor); the cut times come from the host (cut_host, sent as kernel arguments;

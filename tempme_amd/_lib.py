@@ -35,11 +35,11 @@ EXPORTS = (
     "tm_last_error", "tm_version", "tm_graph_build", "tm_graph_build_edges", "tm_graph_free", "tm_graph_info", "tm_graph_export",
     "tm_graph_strict_view",
     "tm_sample_khop", "tm_sample_walks", "tm_neg_sample", "tm_perm_keys", "tm_motif_hist", "tm_edge_counts",
-    "tm_sample_events", "tm_gather_rows", "tm_weights_create", "tm_weights_create_ex", "tm_weights_pack", "tm_weights_variant", "tm_weights_set_node_zero", "tm_weights_free",
+    "tm_sample_events", "tm_gather_rows", "tm_weights_create", "tm_weights_create_ex", "tm_weights_pack", "tm_weights_variant", "tm_weights_set_node_zero", "tm_weights_version", "tm_weights_free",
     "tm_encoder_workspace_bytes",
     "tm_encoder_fwd", "tm_encoder_fwd_tab", "tm_encoder_train_supported", "tm_encoder_train_fwd", "tm_encoder_bwd", "tm_encoder_wgrad", "tm_wgrad",
     "tm_explain_train_fwd", "tm_explain_train_fwd_pad", "tm_explain_train_bwd", "tm_kl_loss", "tm_edge_importance", "tm_edge_gate_table",
-    "tm_edge_table_cols", "tm_edge_tables", "tm_edge_feature_table", "tm_edge_importance_tab", "tm_tgn_attn_fwd", "tm_tgn_attn_bwd", "tm_gm_packed_floats", "tm_gm_pack", "tm_gm_embed", "tm_gm_embed_bwd_ok", "tm_gm_embed_bwd", "tm_gm_packed_a_floats", "tm_gm_pack_a", "tm_gm_fused_ok", "tm_dropin_create", "tm_dropin_free", "tm_dropin_forward", "tm_dropin_set_stream", "tm_dropin_gate_cache", "tm_edge_importance_gf", "tm_edge_importance_gf3", "tm_edge_importance_gf3_bern",
+    "tm_edge_table_cols", "tm_edge_tables", "tm_edge_feature_table", "tm_edge_importance_tab", "tm_tgn_attn_fwd", "tm_tgn_attn_bwd", "tm_gm_packed_floats", "tm_gm_pack", "tm_gm_embed", "tm_gm_embed_bwd_ok", "tm_gm_embed_bwd", "tm_gm_packed_a_floats", "tm_gm_pack_a", "tm_gm_fused_ok", "tm_dropin_create", "tm_dropin_free", "tm_dropin_forward", "tm_dropin_set_stream", "tm_dropin_gate_cache", "tm_dropin_gate_cache_clear", "tm_edge_importance_gf", "tm_edge_importance_gf3", "tm_edge_importance_gf3_bern",
     "tm_mask_least_important", "tm_profile_enable", "tm_profile_sync", "tm_profile_entry",
     "tm_beta_params", "tm_beta_rsample_bwd",
 )
@@ -130,6 +130,8 @@ def _sig(L):
     L.tm_weights_pack.argtypes = [vp, C.POINTER(vp), vp]
     L.tm_weights_variant.argtypes = [vp, i32, i32]
     L.tm_weights_set_node_zero.argtypes = [vp, i32]
+    L.tm_weights_version.argtypes = [vp]
+    L.tm_weights_version.restype = u64
     L.tm_weights_free.argtypes = [vp]
     L.tm_encoder_workspace_bytes.restype = i64
     L.tm_encoder_workspace_bytes.argtypes = [vp, i64]
@@ -171,6 +173,7 @@ def _sig(L):
     L.tm_dropin_forward.argtypes = [vp, i32, i32, vp, vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.tm_dropin_set_stream.argtypes = [vp, i32, vp]
     L.tm_dropin_gate_cache.argtypes = [vp, i64]
+    L.tm_dropin_gate_cache_clear.argtypes = [vp]
     L.tm_edge_importance_gf.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.tm_edge_importance_gf3.argtypes = [i32, i32, i32] + [vp] * 24
     L.tm_edge_importance_gf3_bern.argtypes = [i32, i32, i32] + [vp] * 26

@@ -16,6 +16,8 @@
 //                   gather at subgraph edge ids, Beta mean, node==0 mask
 // Every dense projection runs on MFMA with the packed weight stream read from L2 and the
 // activations staged in LDS (row stride K16+8 floats: conflict-free ds_read_b128).
+#include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <vector>
 
@@ -838,6 +840,12 @@ __device__ unsigned long long g_live;   // waves inside the pass loop right now
 #else
 #define TM_STAMP(k) (void)T
 #endif
+// Wave timeline (debug builds only, -DTM_TRACE; tools/walk_trace.py): per wave of the last launch, s_memrealtime
+// (100 MHz) at [0] entry, [1] after the constant table, [2..15] the end of each pass of its first two units,
+// [16..27] the end of each of its first 12 units, [28] its unit count, [29] HW_ID | XCC_ID << 32
+#ifdef TM_TRACE
+__device__ unsigned long long g_tr[8192][32];
+#endif
 
 constexpr int EQ_MAX = 4;   // edge features span at most 4 K steps (de <= 64, checked on the host)
 static_assert(EQ_MAX == 4, "load_ef holds 4 K steps");
@@ -1341,8 +1349,9 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * WALK_WAVES / WALK_WPB) walk
     const int64_t n_units = (a.n_slots + 15) / 16;
     // persistent waves (not SPLIT): the grid is one round of resident workgroups; a wave starts with unit = its
     // global wave id and takes each next unit from the launch's counter (a ticket offset by the grid's waves),
-    // requested at the start of its current unit and consumed in that unit's last pass, where the next unit's
-    // scalars and table row are requested.  Static striding (unit w, w + stride, ...) measured 1.3 % slower
+    // requested at the top of its current unit's last pass, where the next unit's scalars and table row are
+    // requested (round 6; before, at the start of the current unit: a reserved unit then waited a whole unit time,
+    // which widened the end-of-grid spread, tools/walk_trace.py).  Static striding (unit w, w + stride, ...) measured 1.3 % slower
     // than one unit per wave, dynamic tickets 1.4 % faster (profiles/r03_walk_xpf_ab.txt, r05_walk_ab.txt).
     constexpr bool PERSIST = !SPLIT;
     const int64_t ustride = PERSIST ? (int64_t)gridDim.x * (blockDim.x >> 6) : n_units;
@@ -1372,8 +1381,21 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * WALK_WAVES / WALK_WPB) walk
     __shared__ Stash stash[WALK_WPB];
     __shared__ float4 cs4[(C::SIZE + 3) / 4];
     float *cs = reinterpret_cast<float *>(cs4);
+#ifdef TM_TRACE
+    const int64_t trw = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    int trn = 0;
+    const unsigned long long tr0 = __builtin_amdgcn_s_memrealtime();
+#endif
     load_consts<NQE, NTD, ZN>(P, cs);
     __syncthreads();
+#ifdef TM_TRACE
+    if (lane == 0 && trw < 8192) {
+        g_tr[trw][0] = tr0;
+        g_tr[trw][1] = __builtin_amdgcn_s_memrealtime();
+        g_tr[trw][28] = 0;
+        g_tr[trw][29] = (unsigned)__builtin_amdgcn_s_getreg(63492) | ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg(30740) << 32);
+    }
+#endif
     if (unit >= n_units) return;                        // whole wave idle (wave-uniform)
     Stash &st = stash[threadIdx.x >> 6];
     // every weight fragment off one buffer resource (WalkLay offsets from the folded region's base)
@@ -1399,14 +1421,21 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * WALK_WAVES / WALK_WPB) walk
 #endif
 #pragma nounroll
     for (;;) {
-    const int64_t unext = PERSIST ? ticket() : unit + ustride;
-    bool vn;
-    int64_t egn;
-    int32_t jn;
-    coords(unext, vn, egn, jn);
+    // the next unit: a persistent wave takes its ticket at the top of its current unit's LAST pass (the next unit's
+    // slot-pass scalars are requested inside that pass), so no wave holds a reserved unit for a whole unit time --
+    // the waves' end times then spread over one unit's last pass plus one unit, not two units
+    int64_t unext = unit + ustride;
+    bool vn = false;
+    int64_t egn = 0;
+    int32_t jn = 0;
+    if constexpr (!PERSIST) coords(unext, vn, egn, jn);
     // pass 0: position 2 once per slot (walk j*M carries it); then per walk m: position 0, position 1
 #pragma nounroll
     for (int pass = 0; pass < n_pass; ++pass) {
+        if (PERSIST && pass + 1 == n_pass) {
+            unext = ticket();
+            coords(unext, vn, egn, jn);
+        }
         const int m = SPLIT ? m0 : pass == 0 ? 0 : (pass - 1) >> 1;
         const int p = pass == 0 ? 2 : ((pass - 1) & 1);
         const int64_t gw = eg * a.W + (int64_t)j * a.M + m;
@@ -1517,6 +1546,9 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * WALK_WAVES / WALK_WPB) walk
         }
         if (p == 1) walk_head<NQE, NTD>(a, wr, cs, gw, valid, hi, st, s0, s, R0, R, pre, lin0);
         TM_STAMP(8);
+#ifdef TM_TRACE
+        if (lane == 0 && trw < 8192 && trn < 2 && pass < 7) g_tr[trw][2 + 7 * trn + pass] = __builtin_amdgcn_s_memrealtime();
+#endif
 #ifdef TM_STAMPS
         if (lane == 0 && blockIdx.x % 16 == 5) {
             for (int k = 0; k < 8; ++k) atomicAdd(&g_st[p][k], T[k + 1] - T[k]);
@@ -1524,6 +1556,12 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * WALK_WAVES / WALK_WPB) walk
         }
 #endif
     }
+#ifdef TM_TRACE
+    if (lane == 0 && trw < 8192) {
+        if (trn < 12) g_tr[trw][16 + trn] = __builtin_amdgcn_s_memrealtime();
+        g_tr[trw][28] = ++trn;
+    }
+#endif
     unit = unext;
     if (unit >= n_units) break;                         // wave-uniform: every wave leaves after its last unit
     valid = vn;
@@ -1910,20 +1948,26 @@ extern "C" int tm_weights_create_ex(int32_t de, int32_t dn, int32_t h, int32_t i
         tm_weights_free(w);
         return rc;
     }
+    tm_weights_bump(w);
     *out = w;
     return TM_OK;
 }
 
+static std::atomic<uint64_t> g_weights_stamp{0};
+void tm_weights_bump(tm_weights *w) { w->version = g_weights_stamp.fetch_add(1, std::memory_order_relaxed) + 1; }
+
+extern "C" uint64_t tm_weights_version(const tm_weights *w) { return w ? w->version : 0; }
+
 extern "C" int tm_weights_set_node_zero(tm_weights *w, int32_t node_zero) {
     if (!w) return fail(TM_E_ARG, "tm_weights_set_node_zero: NULL weights");
     w->node_zero = node_zero ? 1 : 0;
-    ++w->version;
+    tm_weights_bump(w);
     return TM_OK;
 }
 
 extern "C" int tm_weights_variant(tm_weights *w, int32_t temporal_guidance, int32_t dependency_gate) {
     if (!w) return fail(TM_E_ARG, "tm_weights_variant: NULL weights");
-    ++w->version;
+    tm_weights_bump(w);
     w->P.tg = temporal_guidance ? 1 : 0;
     w->P.dep = dependency_gate ? 1 : 0;
     return TM_OK;
@@ -1934,7 +1978,7 @@ extern "C" int tm_weights_pack(tm_weights *w, const float *const *t, void *strea
     for (int i = 0; i < TM_N_WEIGHTS; ++i)
         if (!t[i]) return fail(TM_E_ARG, "tm_weights_pack: NULL tensor " + std::to_string(i));
     hipStream_t s = S_(stream);
-    ++w->version;
+    tm_weights_bump(w);
     pack_all_weights(w, t, s);
     TM_CHECK_LAUNCH();
     return TM_OK;
@@ -2362,6 +2406,14 @@ extern "C" int tm_dropin_gate_cache(tm_dropin *d, int64_t n_edge_rows) {
     return TM_OK;
 }
 
+// the caller rewrote the edge-feature table in place (same address): the next tm_dropin_forward with out_gfac
+// empties the cache (a stamp of 0 matches no weight state)
+extern "C" int tm_dropin_gate_cache_clear(tm_dropin *d) {
+    if (!d) return fail(TM_E_ARG, "tm_dropin_gate_cache_clear: NULL context");
+    d->gkey_ver = 0;
+    return TM_OK;
+}
+
 extern "C" int tm_dropin_create(int32_t device, tm_dropin **out) {
     if (!out) return fail(TM_E_ARG, "tm_dropin_create: NULL out");
     *out = nullptr;
@@ -2419,8 +2471,9 @@ extern "C" int tm_dropin_forward(tm_dropin *d, int32_t k, int32_t sync, const tm
     if (cut_host && B > tm_dropin::SLOT_DOUBLES) return fail(TM_E_UNSUPPORTED, "tm_dropin_forward: batch too large");
     hipStream_t cur = S_(stream);
     hipStream_t side = d->side[k];
-    // gate-factor cache: new weights (or a repack) or another edge-feature table empty it, on the caller's stream
-    // (ordered after every earlier side call) before every side stream's next use
+    // gate-factor cache: new weights (or a repack: w->version is a process-wide stamp, so a freed and re-created
+    // tm_weights at the same address never matches), another edge-feature table or tm_dropin_gate_cache_clear
+    // empty it, on the caller's stream (ordered after every earlier side call) before every side stream's next use
     if (out_gfac && d->gcache && (d->gkey_w != w || d->gkey_ver != w->version || d->gkey_ef != e_feat)) {
         TM_HIP(hipMemsetAsync(d->gcache, 0xFF, sizeof(unsigned long long) * (size_t)d->gcache_n, cur));
         d->gkey_w = w;
@@ -2647,6 +2700,12 @@ extern "C" int tm_edge_importance_gf(const float *gfac, int32_t n_groups, int32_
     return TM_OK;
 }
 
+#ifdef TM_TRACE
+extern "C" int tm_debug_trace(unsigned long long *host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(tmk::g_tr), sizeof(unsigned long long) * 8192 * 32, 0,
+                                    hipMemcpyDeviceToHost);
+}
+#endif
 #ifdef TM_STAMPS
 extern "C" int tm_debug_stamps(unsigned long long *host) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(tmk::g_st), sizeof(unsigned long long) * 30, 0,

@@ -272,8 +272,10 @@ struct tm_weights {
     // the caller's node-feature table is all zeros (tm_weights_set_node_zero): the fused eval kernel computes
     // one event_gcn branch, the other being bit-identical
     int node_zero = 0;
-    // bumped by every repack / variant change: caches of values computed from the weights (the drop-in's gate
-    // factors per edge id) key on it
+    // a process-wide stamp (tm_weights_bump: every create / repack / variant / node-zero change takes the next
+    // value of one global counter): caches of values computed from the weights (the drop-in's gate factors per
+    // edge id, the pipeline's per-edge-id tables) key on it, and no two weight states -- of this object or of
+    // another one later allocated at the same address -- ever share a stamp
     uint64_t version = 0;
     // per linear: raw tensor index, nout, k
     struct Spec {
@@ -290,6 +292,8 @@ struct tm_weights {
     double *fold64 = nullptr;
     float *fold32 = nullptr;
 };
+
+void tm_weights_bump(tm_weights *w);   // encoder.hip: w->version = the next process-wide stamp
 
 // encoder_train.hip: transposed packs (tm_weights_create / _free) and the one-launch packing of every tensor
 int train_packs_create(tm_weights *w);

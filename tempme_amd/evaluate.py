@@ -32,6 +32,10 @@ from .train import batch_from_pack, encode_sides, explain_sides, prepare_step
 BATCH_FIGURES = ("aps", "auc", "acc", "fid_prob", "fid_logit", "loss", "pred_loss", "kl_loss")
 RATIO_FIGURES = ("ratio_aps", "ratio_auc", "ratio_acc", "ratio_prob", "ratio_logit")
 FIGURES = BATCH_FIGURES + RATIO_FIGURES
+# a row is FIGURES + this flag: 1.0 when the batch ran threshold_test (the reference appends to its ratio lists only
+# then, temp_exp_main.py:479-494), so a NaN ratio figure from threshold_test itself (a one-class y_ori has no AUC)
+# is told apart from "not run" and propagates into the epoch mean as in the reference's np.mean
+THRESHOLD_RAN = len(FIGURES)
 
 
 def eval_spans(num_instance, test_bs):
@@ -60,11 +64,12 @@ def _metrics_sklearn(y, yp):
 
 
 def eval_batch(args, base_model, explainer, batch):
-    """The figures of one reference batch (temp_exp_main.py:440-494) as a float64 [13] row (ratio
-    figures NaN unless ``args.test_threshold``)."""
+    """The figures of one reference batch (temp_exp_main.py:440-494) as a float64 [14] row: FIGURES (ratio
+    figures NaN unless ``args.test_threshold``) and the THRESHOLD_RAN flag."""
     from . import fidelity
     criterion = torch.nn.BCEWithLogitsLoss()
-    row = np.full(len(FIGURES), np.nan)
+    row = np.full(len(FIGURES) + 1, np.nan)
+    row[THRESHOLD_RAN] = 0.0
     with torch.no_grad():
         kw, pos_out_ori, neg_out_ori, y_ori = prepare_step(base_model, batch)
         explainer.eval()
@@ -94,8 +99,10 @@ def eval_batch(args, base_model, explainer, batch):
                    float(kl_loss))
         if getattr(args, "test_threshold", False):
             expl0 = explain_sides(explainer, batch, imps, False)
-            row[8:] = fidelity.threshold_test(args, expl0, base_model, batch.src, batch.dst, batch.fake, batch.ts,
-                                              batch.e_idx, pos_out_ori, neg_out_ori, y_ori, sg_s, sg_t, sg_b)
+            row[8:THRESHOLD_RAN] = fidelity.threshold_test(args, expl0, base_model, batch.src, batch.dst, batch.fake,
+                                                           batch.ts, batch.e_idx, pos_out_ori, neg_out_ori, y_ori,
+                                                           sg_s, sg_t, sg_b)
+            row[THRESHOLD_RAN] = 1.0
     return row
 
 
@@ -130,12 +137,18 @@ def gather_rows(rows, world=1, group=None, device=None, collective=None):
 
 def reduce_epoch(allr):
     """The epoch's figures from the per-batch rows in batch order (temp_exp_main.py:495-507): means over
-    batches; the ratio figures 0 when no batch ran threshold_test."""
+    batches; the ratio figures are the mean over the batches that ran threshold_test (THRESHOLD_RAN flag; a NaN
+    figure of such a batch makes the mean NaN, as np.mean does in the reference), 0 when none did."""
     out = {}
+    n_rows = len(allr)
+    if n_rows and allr.shape[1] > 1 + THRESHOLD_RAN:
+        ran = allr[:, 1 + THRESHOLD_RAN] == 1.0
+    else:   # rows without the flag: a batch ran threshold_test when any of its ratio figures is set
+        ran = ~np.isnan(allr[:, 1 + len(BATCH_FIGURES):1 + len(FIGURES)]).all(axis=1) if n_rows else np.zeros(0, bool)
     for j, name in enumerate(FIGURES):
-        col = allr[:, 1 + j] if len(allr) else np.zeros(0)
+        col = allr[:, 1 + j] if n_rows else np.zeros(0)
         if name in RATIO_FIGURES:
-            col = col[~np.isnan(col)]
+            col = col[ran]
             out[name] = float(np.mean(col)) if len(col) else 0.0
         else:
             out[name] = float(np.mean(col)) if len(col) else float("nan")
@@ -168,8 +181,19 @@ def eval_one_epoch(args, base_model, explainer, buf, src, dst, ts, e_idx, *, ran
         rows_idx = torch.arange(s, e, dtype=torch.int64, device=dev)
         return eval_batch(args, base_model, explainer, batch_from_pack(buf, src, dst, ts, e_idx, rows_idx))
     gdev = dev if (world > 1 and dist.get_backend(group) == "nccl") else None
-    return run_sharded(spans, one, rank, world, group, gdev)
+    if seed is None:
+        return run_sharded(spans, one, rank, world, group, gdev)
+    # per-batch reseeding must not leak into the caller's RNG streams (the reference never reseeds in eval):
+    # the CPU and device generators are restored afterwards
+    cpu_state = torch.get_rng_state()
+    dev_state = torch.cuda.get_rng_state(dev) if dev.type == "cuda" else None
+    try:
+        return run_sharded(spans, one, rank, world, group, gdev)
+    finally:
+        torch.set_rng_state(cpu_state)
+        if dev_state is not None:
+            torch.cuda.set_rng_state(dev_state, dev)
 
 
 __all__ = ["eval_one_epoch", "eval_batch", "eval_spans", "shard_spans", "gather_rows", "reduce_epoch", "run_sharded",
-           "FIGURES"]
+           "FIGURES", "THRESHOLD_RAN"]

@@ -499,6 +499,13 @@ class TempME(nn.Module):
             self._prep_dirty = self._prep_dirty_fast = True   # side streams must wait for this work
             if getattr(self, "_packed", None) is not None:
                 self._set_node_zero(self._packed.h)
+            c = self.__dict__.get("_dropin_c")
+            if c is not None:
+                # the edge-feature table may have been rewritten in place (same address): the drop-in's gate-factor
+                # cache keys on the address, so empty it explicitly
+                fn = getattr(L.lib(), "tm_dropin_gate_cache_clear", None)   # absent in an older A/B build
+                if fn is not None:
+                    L.check(fn(c[1].h), "tm_dropin_gate_cache_clear")
         return self._n_tab, self._e_tab
 
     def _set_node_zero(self, h):

@@ -6,26 +6,96 @@ retrieve_explanation(training=False)), without host round trips:
 
     tm_sample_events        fake dst, 2-hop subgraphs x3, walks x3, categories, edge counts
     tm_edge_tables          per edge id: the dependency gate and lin_event's edge-feature product
+                            (EdgeTables: built once per weight state -- tm_weights_version -- edge-feature
+                            table and graph, not per call; an eval epoch's weights do not change)
     tm_encoder_fwd_tab      graphlet importance for the 3 * E/B groups (one std per group)
     tm_edge_importance_tab  explanation weights hop-1 [3, E, N] and hop-2 [3, E, N^2]
 
 Outputs are side-major: rows [s, b*B:(b+1)*B] of batch b are the reference's
 ``retrieve_explanation`` rows [s*B:(s+1)*B].
 """
+import time
+
 import torch
 
 from . import _lib as L
 from .preprocess import EventBuffers, sample_events
 
 
+class EdgeTables:
+    """The per-edge-id tables of one (explainer, graph): the dependency-gate factor of every edge id
+    (retrieve_edge_imp_node's depMLP, explainer_new.py:367-386: a function of (E[e], t_e) and the gate
+    weights alone) and lin_event's edge-feature product (event_gcn, :79-96: a function of E[e] and
+    lin_event's weights alone).  Both are pure functions of (weight state, edge-feature table, the graph's
+    edge timestamps), so they are built once per key -- tm_weights_version (a process-wide stamp taken by
+    every repack / variant / node-zero change), the edge-feature table's identity and version, the graph
+    handle -- and reused by every call until one of them changes.  The reference recomputes the gate per
+    walk position per batch; the values are the same (tests compare against the per-call build bitwise).
+
+    Streams: a build is recorded with an event; a call on another stream waits for it once."""
+
+    def __init__(self, explainer, graph, edge_table=True):
+        self.ex, self.graph, self.dev = explainer, graph, graph.device
+        n = graph.max_eid + 1
+        self.gf = torch.empty(n, dtype=torch.float32, device=self.dev)
+        cols = L.lib().tm_edge_table_cols(explainer.packed_weights()) if edge_table else 0
+        self.etab = torch.empty((n, cols), dtype=torch.float32, device=self.dev) if cols else None
+        self.key = None
+        self.builds = 0
+        self.build_ms = None           # host-timed duration of the last build (synchronised; see build())
+        self._ready = None
+        self._waited = set()
+
+    def _key(self):
+        w = self.ex.packed_weights()
+        _, et = self.ex.feature_tables()
+        fn = getattr(L.lib(), "tm_weights_version", None)    # absent in an older A/B build (TEMPME_LIB)
+        ver = int(fn(w)) if fn is not None else (w.value, self.ex._packed_key)
+        return (ver, et.data_ptr(), getattr(self.ex, "_tables_key", None), self.graph.handle.value)
+
+    def build(self, timed=False):
+        """Rebuild on the current stream (one tm_edge_tables launch over every edge id); ``timed`` measures
+        it alone (synchronising before and after) for the bench's ``aux.edge_tables_ms``."""
+        w = self.ex.packed_weights()
+        _, et = self.ex.feature_tables()
+        st = torch.cuda.current_stream(self.dev)
+        if timed:
+            torch.cuda.synchronize(self.dev)
+            t0 = time.perf_counter()
+        L.check(L.lib().tm_edge_tables(w, self.graph.handle, L.ptr(et), L.ptr(self.gf), L.ptr(self.etab),
+                                       st.cuda_stream), "tm_edge_tables")
+        if timed:
+            torch.cuda.synchronize(self.dev)
+            self.build_ms = (time.perf_counter() - t0) * 1e3
+        self.key = self._key()
+        self.builds += 1
+        self._ready = torch.cuda.Event()
+        self._ready.record(st)
+        self._waited = {st.cuda_stream}
+
+    def ensure(self):
+        """The tables for the current weights on the current stream: built if stale, else (once per build and
+        stream) the stream waits for the build."""
+        if self.key != self._key():
+            self.build()
+            return
+        st = torch.cuda.current_stream(self.dev)
+        if st.cuda_stream not in self._waited:
+            st.wait_event(self._ready)
+            self._waited.add(st.cuda_stream)
+
+
 class ExplainPipeline:
-    def __init__(self, explainer, graph, dst_list, N, M=3, B=100, seed=0, split=L.SPLIT_TEST, edge_table=True):
+    def __init__(self, explainer, graph, dst_list, N, M=3, B=100, seed=0, split=L.SPLIT_TEST, edge_table=True,
+                 tables=None):
         """``edge_table=False`` keeps lin_event's edge-feature product inside the walk kernel
         (tm_encoder_fwd, bit-identical to the drop-in TempME.forward) instead of reading it from the
-        per-edge-id table (a re-association of the same sum, within the 1e-5 contract)."""
+        per-edge-id table (a re-association of the same sum, within the 1e-5 contract).  ``tables``: an
+        EdgeTables shared with other pipelines of the same explainer and graph."""
         self.ex = explainer
         self.edge_table = bool(edge_table)
         self.graph = graph
+        self.tabs = tables if tables is not None else EdgeTables(explainer, graph, edge_table)
         self.dev = graph.device
         self.dst_list = dst_list.to(self.dev, torch.int32).contiguous()
         self.N, self.M, self.B, self.W = int(N), int(M), int(B), int(N) * int(M)
@@ -43,10 +113,15 @@ class ExplainPipeline:
         self.ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         self.h1 = torch.empty(max(3 * E * N, 1), dtype=torch.float32, device=dev)
         self.h2 = torch.empty(max(3 * E * N * N, 1), dtype=torch.float32, device=dev)
-        self.gf = torch.empty(self.graph.max_eid + 1, dtype=torch.float32, device=dev)
-        cols = L.lib().tm_edge_table_cols(self.ex.packed_weights()) if self.edge_table else 0
-        self.etab = torch.empty((self.graph.max_eid + 1, cols), dtype=torch.float32, device=dev) if cols else None
         self._E = E
+
+    @property
+    def gf(self):
+        return self.tabs.gf
+
+    @property
+    def etab(self):
+        return self.tabs.etab
 
     def sample(self, src, dst, ts, eidx, event_ids):
         self._alloc(int(src.numel()))
@@ -63,13 +138,15 @@ class ExplainPipeline:
                             M=self.M, etab=self.etab)
         return self.imp
 
-    def tables(self):
-        """Once per call, per edge id of the graph: the dependency gate (retrieve_edge_imp_node's
-        depMLP, explainer_new.py:367-386) and, when the encoder has a table mode, lin_event's
-        edge-feature product (event_gcn, :79-96) -- one launch, the edge features read once."""
-        _, et = self.ex.feature_tables()
-        L.check(L.lib().tm_edge_tables(self.ex.packed_weights(), self.graph.handle, L.ptr(et), L.ptr(self.gf),
-                                       L.ptr(self.etab), L.stream_ptr(self.dev)), "tm_edge_tables")
+    def tables(self, rebuild=False):
+        """Per edge id of the graph: the dependency gate (retrieve_edge_imp_node's depMLP,
+        explainer_new.py:367-386) and, when the encoder has a table mode, lin_event's edge-feature product
+        (event_gcn, :79-96) -- one launch, the edge features read once; rebuilt only when the weights, the
+        edge-feature table or the graph changed (EdgeTables), or when ``rebuild``."""
+        if rebuild:
+            self.tabs.build()
+        else:
+            self.tabs.ensure()
 
     def explain(self):
         """retrieve_explanation(training=False) for all groups: the table-driven scatter-max / gather /
@@ -115,7 +192,8 @@ class PipelinedExplainer:
                  edge_table=True):
         dev = graph.device
         self.depth = max(1, int(depth))
-        self.pipes = [ExplainPipeline(explainer, graph, dst_list, N, M, B, seed, split, edge_table)
+        tabs = EdgeTables(explainer, graph, edge_table)
+        self.pipes = [ExplainPipeline(explainer, graph, dst_list, N, M, B, seed, split, edge_table, tables=tabs)
                       for _ in range(self.depth)]
         self.streams = [torch.cuda.Stream(device=dev) for _ in range(self.depth)]
         self._k = 0

@@ -86,7 +86,7 @@ def _reference_batch(args, base, ex, b):
         expl0 = ex.retrieve_explanation(sg_s, g_s, w_s, sg_t, g_t, w_t, sg_b, g_b, w_b, training=False)
         row += list(fidelity.threshold_test(args, expl0, base, b.src, b.dst, b.fake, b.ts, b.e_idx, pos_out_ori,
                                             neg_out_ori, y_ori, sg_s, sg_t, sg_b))
-    return np.array(row)
+    return np.array(row + [1.0])          # + the THRESHOLD_RAN flag (threshold_test ran)
 
 
 def test_eval_batch_equals_reference_loop_body():
@@ -147,7 +147,9 @@ def _eval_worker(rank, world, port, q):
                 for k in single:
                     a, b = sharded[k], single[k]
                     assert a == b or (np.isnan(a) and np.isnan(b)), (k, a, b)
-                assert all(np.isfinite(single[k]) for k in ("aps", "acc", "loss", "kl_loss", "ratio_aps"))
+                assert all(np.isfinite(single[k]) for k in ("aps", "acc", "loss", "kl_loss"))
+                if args.test_threshold:   # threshold_test ran (a NaN figure of a batch propagates, as in the reference)
+                    assert single["ratio_aps"] != 0.0
         if rank == 0:
             q.put("ok")
         dist.barrier()
@@ -191,9 +193,9 @@ def _nccl_worker(rank, world, port, q):
         assert len(sync.local) == len(sync.synced) > 0
         for a, b in zip(sync.local, sync.synced):
             assert torch.equal(a, b)                                  # the average over one rank
-        rows = {3: np.arange(13.0), 1: np.ones(13)}
+        rows = {3: np.arange(14.0), 1: np.ones(14)}
         allr = gather_rows(rows, world, device=dev, collective=True)
-        assert allr.shape == (2, 14) and list(allr[:, 0]) == [1.0, 3.0]
+        assert allr.shape == (2, 15) and list(allr[:, 0]) == [1.0, 3.0]
         q.put("ok")
     except Exception as exc:      # noqa: BLE001
         q.put(repr(exc))

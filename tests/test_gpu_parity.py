@@ -558,6 +558,66 @@ def test_edge_table_path(tm, de):
     np.testing.assert_allclose(a[2].cpu().numpy(), b[2].cpu().numpy(), rtol=RTOL, atol=ATOL)
 
 
+def test_edge_tables_cached_per_weight_state(tm):
+    """The pipeline's per-edge-id tables (gate factor + lin_event's edge product) are built once per weight
+    state and reused: repeated calls build nothing and give bitwise the same outputs; the cached tables equal
+    a forced rebuild bitwise; an in-place change of the gate weights or of lin_event rebuilds them (the new
+    tables equal a fresh pipeline's); two steps in flight share one build."""
+    from tempme_amd.pipeline import ExplainPipeline, PipelinedExplainer
+    from tempme_amd.workload import enron_like, split
+    g = enron_like(n_nodes=120, n_edges=4000, alpha=1.3, seed=23)
+    (src, dst, ts, eidx), rows, pool = split(g)
+    dev = torch.device("cuda", 0)
+    f = _finder(tm, g["src"][rows], g["dst"][rows], g["eidx"][rows], g["ts"][rows], g["n_nodes"], seed=4)
+    torch.manual_seed(5)
+    ex = tm.TempME(_Base(g["n_feat"], g["e_feat"], dev), "tgn", "x", 40, 64, device=dev,
+                   null_model={k: 1 / 12 for k in range(1, 13)}).to(dev).eval()
+    N, B, E = 20, 50, 100
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a[:E], dtype=dt)).to(dev)  # noqa: E731
+    args = (t(src, np.int32), t(dst, np.int32), t(ts, np.float64), t(eidx, np.int32),
+            torch.arange(E, dtype=torch.int32, device=dev))
+    p = ExplainPipeline(ex, f.graph, torch.from_numpy(pool), N, 3, B, seed=4)
+    a = [x.clone() for x in p.run(*args)]
+    b = [x.clone() for x in p.run(*args)]
+    assert p.tabs.builds == 1
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    gf0, et0 = p.gf.clone(), p.etab.clone()
+    p.tables(rebuild=True)
+    torch.cuda.synchronize()
+    assert torch.equal(gf0, p.gf) and torch.equal(et0, p.etab)
+    with torch.no_grad():
+        ex.edge_dependency_gcn[0].weight.mul_(1.25)
+    p.run(*args)
+    assert p.tabs.builds == 3
+    fresh = ExplainPipeline(ex, f.graph, torch.from_numpy(pool), N, 3, B, seed=4)
+    c = [x.clone() for x in fresh.run(*args)]
+    torch.cuda.synchronize()
+    assert not torch.equal(gf0, p.gf) and torch.equal(fresh.gf, p.gf)
+    with torch.no_grad():
+        ex.event_conv.lin_event.weight.mul_(0.75)
+    d = [x.clone() for x in p.run(*args)]
+    fresh2 = ExplainPipeline(ex, f.graph, torch.from_numpy(pool), N, 3, B, seed=4)
+    e = [x.clone() for x in fresh2.run(*args)]
+    torch.cuda.synchronize()
+    assert p.tabs.builds == 4 and torch.equal(fresh2.etab, p.etab) and not torch.equal(et0, p.etab)
+    for x, y in zip(d, e):
+        assert torch.equal(x, y)
+    assert not torch.equal(c[0], d[0])
+    fl = PipelinedExplainer(ex, f.graph, torch.from_numpy(pool), N, 3, B, seed=4, depth=2)
+    outs = []
+    for _ in range(4):
+        (imp, h1, h2), st = fl.submit(*args)
+        torch.cuda.current_stream().wait_stream(st)
+        outs.append([imp.clone(), h1.clone(), h2.clone()])
+    torch.cuda.synchronize()
+    fl.check_errors()
+    assert fl.pipes[0].tabs is fl.pipes[1].tabs and fl.pipes[0].tabs.builds == 1
+    for o in outs:
+        for x, y in zip(o, e):
+            assert torch.equal(x, y)
+
+
 @pytest.mark.parametrize("hid,if_cat,tg", [(128, True, True), (64, False, True), (32, False, False), (48, True, True),
                                              (40, True, True), (20, False, True)])
 def test_constructor_shapes_on_hip(tm, hid, if_cat, tg):
