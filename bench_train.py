@@ -61,7 +61,9 @@ def main():
                     "instead of replaying the step captured as a HIP graph (the default with one GPU)")
     ap.add_argument("--graph", action="store_true", help="capture the step as a HIP graph with several ranks "
                     "too (the RCCL all-reduce is then captured inside the graph)")
-    ap.add_argument("--no-fused-adam", action="store_true", help="torch's default (foreach) Adam")
+    ap.add_argument("--optim", choices=("hip", "torch-fused", "torch"), default="hip",
+                    help="hip: tempme_amd.optim.FusedAdam (one HIP kernel over the flat parameter / gradient bucket the "
+                         "all-reduce also runs on); torch-fused: torch.optim.Adam(fused=True); torch: its foreach form")
     ap.add_argument("--no-node-zero", action="store_true",
                     help="do not use the zero-node-feature kernel forms (A/B; the graph's node features are zeros)")
     ap.add_argument("--overlap-prepare", action="store_true",
@@ -129,11 +131,15 @@ def main():
                    null_model={k: 1.0 / 12 for k in range(1, 13)}).to(dev)
     ex.node_zero_specialization = not args.no_node_zero
     use_graph = not args.no_graph and (world == 1 or (args.graph and backend == "nccl"))
-    # fused Adam: one multi-tensor launch per step instead of ~70 per-parameter kernels (same update rule,
-    # temp_exp_main.py's torch.optim.Adam(lr=1e-3) defaults)
-    opt = torch.optim.Adam(ex.parameters(), lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0,
-                           capturable=use_graph, fused=not args.no_fused_adam)
-    sync = GradAllReduce(ex)
+    # temp_exp_main.py's torch.optim.Adam(lr=1e-3) update rule; default: one HIP kernel over the flat bucket
+    if args.optim == "hip":
+        from tempme_amd.optim import FusedAdam
+        opt = FusedAdam(ex.parameters(), lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0)
+        sync = GradAllReduce(ex, flat_grad=opt.flat_grad)
+    else:
+        opt = torch.optim.Adam(ex.parameters(), lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0,
+                               capturable=use_graph, fused=args.optim == "torch-fused")
+        sync = GradAllReduce(ex)
     ex.train()
 
     if not args.weak and args.global_batches % world:
@@ -218,6 +224,7 @@ def main():
                           "global_batches_per_step": per_step * world, "train_steps_per_rank_per_step": per_step,
                           "allreduce_overlap": (not args.no_overlap) and not use_graph,
                           "hip_graph": use_graph, "overlap_prepare": bool(args.overlap_prepare and use_graph),
+                          "optimizer": args.optim,
                           "zero_node_forms": bool(getattr(ex, "_node_zero", False)) and ex.node_zero_specialization,
                           "grad_bucket_floats": sum(p.numel() for p in ex.parameters() if p.grad is not None)},
                "loss_first_last": [round(losses[0], 5), round(losses[-1], 5)],

@@ -55,6 +55,18 @@ typedef struct {
 const char *tm_last_error(void);
 int tm_version(void);
 
+/* Test / diagnostic options, process-wide, all 0 (off) in the product path -- the library reads no environment
+ * variables.  TM_DEBUG_FORCE_UNKEYED: the samplers' two-compare rank kernels on any graph (tests compare them with
+ * the keyed one-compare kernels); TM_DEBUG_HOST_BUILD: tm_graph_build_edges on the host builder (tests compare it
+ * with the device builder); TM_DEBUG_GRAPH_TIMING: the graph build's phase times on stderr. */
+#define TM_DEBUG_FORCE_UNKEYED 1
+#define TM_DEBUG_HOST_BUILD 2
+#define TM_DEBUG_GRAPH_TIMING 3
+#define TM_DEBUG_N_OPTS 4
+int tm_debug_set(int32_t opt, int32_t value);
+/* Threads of the host-side graph builder (0 = the CPUs this process may run on, at most 64). */
+int tm_set_host_threads(int32_t n);
+
 /* ---------------------------------------------------------------- graph (host inputs)
  * Replaces NeighborFinder.__init__ / init_off_set / get_ts2idx (utils/graph.py:13-101).
  * Adjacency lists in insertion order, owner-major: entries [in_off[u], in_off[u+1]) are
@@ -338,6 +350,16 @@ int tm_kl_loss(const float *prob, const int32_t *cat, const float *null12, float
  * [n] from g = d(x[:,0] * pad), the sample x [n,2] and d = torch._dirichlet_grad(x, conc, total) -- the
  * same fp32 operations as torch's autograd graph of Beta(...).rsample() * pad. */
 int tm_beta_params(const float *p, int64_t n, float *conc, float *total, void *stream);
+
+/* The explainer's optimizer step (temp_exp_main.py:631-632: torch.optim.Adam, amsgrad off) in ONE launch over a
+ * flat fp32 bucket of n parameters and their gradients (16-byte aligned): exp_avg / exp_avg_sq updated in place,
+ * g = grad * grad_scale (+ weight_decay * param), bias corrections from the device step count `step` (the count
+ * before this step; the kernel advances it, so a captured HIP graph replays correctly) and `done`, a device
+ * uint32 that must be 0 before the first launch (the kernel leaves it 0).  Replaces torch.optim.Adam.step /
+ * torch's fused Adam over the explainer's parameters (tempme_amd/optim.py FusedAdam). */
+int tm_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, float lr, float beta1,
+                 float beta2, float eps, float weight_decay, float grad_scale, float *step, uint32_t *done,
+                 void *stream);
 int tm_beta_rsample_bwd(const float *g, const float *pad, const float *x, const float *d, const float *p, int64_t n,
                         float *dp, void *stream);
 

@@ -28,11 +28,12 @@ TM_E_UNSUPPORTED = -5
 
 SIDE_NONE, SIDE_SRC, SIDE_TGT, SIDE_BGD = 0, 1, 2, 3
 SPLIT_TRAIN, SPLIT_TEST, SPLIT_NULL = 0, 1, 2
+TM_DEBUG_FORCE_UNKEYED, TM_DEBUG_HOST_BUILD, TM_DEBUG_GRAPH_TIMING = 1, 2, 3   # tm_debug_set (tests only)
 N_WEIGHTS = 28
 
 # every symbol include/tempme.h declares
 EXPORTS = (
-    "tm_last_error", "tm_version", "tm_graph_build", "tm_graph_build_edges", "tm_graph_free", "tm_graph_info", "tm_graph_export",
+    "tm_last_error", "tm_version", "tm_debug_set", "tm_set_host_threads", "tm_graph_build", "tm_graph_build_edges", "tm_graph_free", "tm_graph_info", "tm_graph_export",
     "tm_graph_strict_view",
     "tm_sample_khop", "tm_sample_walks", "tm_neg_sample", "tm_perm_keys", "tm_motif_hist", "tm_edge_counts",
     "tm_sample_events", "tm_gather_rows", "tm_weights_create", "tm_weights_create_ex", "tm_weights_pack", "tm_weights_variant", "tm_weights_set_node_zero", "tm_weights_version", "tm_weights_free",
@@ -41,7 +42,7 @@ EXPORTS = (
     "tm_explain_train_fwd", "tm_explain_train_fwd_pad", "tm_explain_train_bwd", "tm_kl_loss", "tm_edge_importance", "tm_edge_gate_table",
     "tm_edge_table_cols", "tm_edge_tables", "tm_edge_feature_table", "tm_edge_importance_tab", "tm_tgn_attn_fwd", "tm_tgn_attn_bwd", "tm_gm_packed_floats", "tm_gm_pack", "tm_gm_embed", "tm_gm_embed_bwd_ok", "tm_gm_embed_bwd", "tm_gm_packed_a_floats", "tm_gm_pack_a", "tm_gm_fused_ok", "tm_dropin_create", "tm_dropin_free", "tm_dropin_forward", "tm_dropin_set_stream", "tm_dropin_gate_cache", "tm_dropin_gate_cache_clear", "tm_edge_importance_gf", "tm_edge_importance_gf3", "tm_edge_importance_gf3_bern",
     "tm_mask_least_important", "tm_profile_enable", "tm_profile_sync", "tm_profile_entry",
-    "tm_beta_params", "tm_beta_rsample_bwd",
+    "tm_beta_params", "tm_beta_rsample_bwd", "tm_adam_step",
 )
 
 
@@ -112,6 +113,8 @@ i32, i64, u32, u64 = C.c_int32, C.c_int64, C.c_uint32, C.c_uint64
 def _sig(L):
     L.tm_last_error.restype = C.c_char_p
     L.tm_version.restype = C.c_int
+    L.tm_debug_set.argtypes = [i32, i32]
+    L.tm_set_host_threads.argtypes = [i32]
     L.tm_graph_build.argtypes = [i32, vp, vp, vp, vp, C.c_int, C.POINTER(vp)]
     L.tm_graph_build_edges.argtypes = [i32, i64, vp, vp, vp, vp, C.c_int, C.POINTER(vp)]
     L.tm_graph_free.argtypes = [vp]
@@ -182,6 +185,8 @@ def _sig(L):
     L.tm_mask_least_important.argtypes = [vp, i32, i32, vp, i32, vp, vp, vp]
     L.tm_profile_enable.argtypes = [C.c_int]
     L.tm_beta_params.argtypes = [vp, i64, vp, vp, vp]
+    f32 = C.c_float
+    L.tm_adam_step.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, f32, vp, vp, vp]
     L.tm_beta_rsample_bwd.argtypes = [vp, vp, vp, vp, vp, i64, vp, vp]
     L.tm_profile_entry.argtypes = [C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(i64)]
     for name in EXPORTS:
@@ -215,6 +220,13 @@ def lib():
         # to one of them fails with AttributeError
         _sig(_Lenient(L) if os.environ.get("TEMPME_LIB") else L)
         _lib = L
+        # the host-side graph builder's threads: this process's CPU share (the GPU box sets OMP_NUM_THREADS to it)
+        fn = getattr(L, "tm_set_host_threads", None)
+        if fn is not None:
+            n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+            if n <= 0 and hasattr(os, "sched_getaffinity"):
+                n = len(os.sched_getaffinity(0))
+            fn(max(0, min(n, 64)))
     return _lib
 
 

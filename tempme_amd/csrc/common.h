@@ -11,6 +11,9 @@ namespace tmk {
 void set_error(const std::string &msg);
 int fail(int code, const std::string &msg);
 
+// test / diagnostic options (tm_debug_set, graph.cpp): process-wide, all 0 in the product path
+int debug_opt(int opt);
+
 // library-internal device scratch per (device, stream), grown on demand (scratch.cpp); nullptr on failure
 void *scratch(size_t bytes, hipStream_t stream);
 

@@ -14,6 +14,7 @@
 #include <memory>
 #include <mutex>
 #include <numeric>
+#include <sched.h>
 #include <thread>
 #include <vector>
 
@@ -31,17 +32,35 @@ int fail(int code, const std::string &msg) {
 using namespace tmk;
 
 extern "C" const char *tm_last_error(void) { return tmk::g_last_error.c_str(); }
-extern "C" int tm_version(void) { return 2; }
+extern "C" int tm_version(void) { return 3; }
+
+namespace tmk {
+static std::atomic<int> g_debug[TM_DEBUG_N_OPTS];
+static std::atomic<int> g_host_threads{0};
+int debug_opt(int opt) { return opt > 0 && opt < TM_DEBUG_N_OPTS ? g_debug[opt].load(std::memory_order_relaxed) : 0; }
+}  // namespace tmk
+
+extern "C" int tm_debug_set(int32_t opt, int32_t value) {
+    if (opt <= 0 || opt >= TM_DEBUG_N_OPTS) return fail(TM_E_ARG, "tm_debug_set: unknown option");
+    g_debug[opt].store(value, std::memory_order_relaxed);
+    return TM_OK;
+}
+
+extern "C" int tm_set_host_threads(int32_t n) {
+    if (n < 0) return fail(TM_E_ARG, "tm_set_host_threads: negative");
+    g_host_threads.store(n, std::memory_order_relaxed);
+    return TM_OK;
+}
 
 namespace {
 
-// threads for the host build: TEMPME_THREADS, else OMP_NUM_THREADS (the GPU box sets it to its CPU
-// share), else the hardware threads, at most 64
+// threads for the host build: tm_set_host_threads (the Python loader passes the process's CPU share), else the
+// CPUs this process may run on, at most 64
 int build_threads() {
-    for (const char *v : {"TEMPME_THREADS", "OMP_NUM_THREADS"}) {
-        const char *s = std::getenv(v);
-        if (s && std::atoi(s) > 0) return std::min(64, std::atoi(s));
-    }
+    const int n = g_host_threads.load(std::memory_order_relaxed);
+    if (n > 0) return std::min(64, n);
+    cpu_set_t cs;
+    if (sched_getaffinity(0, sizeof(cs), &cs) == 0) return std::max(1, std::min(64, CPU_COUNT(&cs)));
     return (int)std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
 }
 
@@ -65,7 +84,7 @@ int parallel_for(int64_t n, int64_t grain, F f) {
 }
 
 struct Timer {
-    bool on = std::getenv("TEMPME_GRAPH_TIMING") != nullptr;
+    bool on = debug_opt(TM_DEBUG_GRAPH_TIMING) != 0;
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
     void lap(const char *what) {
         if (!on) return;
@@ -441,8 +460,8 @@ extern "C" int tm_graph_build_edges(int32_t n_nodes, int64_t n_edges, const int6
     if (2 * n_edges >= INT32_MAX / 2) return fail(TM_E_UNSUPPORTED, "tm_graph_build_edges: too many edges");
     *out = nullptr;
     // the device builder (graph_dev.hip); the host builder below for rows that repeat an edge id, or on
-    // request (TEMPME_HOST_BUILD=1)
-    if (!std::getenv("TEMPME_HOST_BUILD")) {
+    // request (tm_debug_set(TM_DEBUG_HOST_BUILD, 1): the tests that compare the two builders)
+    if (!debug_opt(TM_DEBUG_HOST_BUILD)) {
         Timer tmd;
         const int rc = tm_graph_build_edges_device(n_nodes, n_edges, src, dst, eidx, ts, device, out);
         tmd.lap("device build");

@@ -1104,10 +1104,10 @@ using namespace tmk;
 
 static inline hipStream_t S(void *s) { return (hipStream_t)s; }
 
-// keyed one-compare ranks need draw << 6 to fit 32 bits: draws are < n_entries.  TEMPME_FORCE_UNKEYED
-// (tests) selects the two-compare kernels on any graph.
+// keyed one-compare ranks need draw << 6 to fit 32 bits: draws are < n_entries.  tm_debug_set(
+// TM_DEBUG_FORCE_UNKEYED, 1) (tests) selects the two-compare kernels on any graph.
 static inline bool use_keyed(const tm_graph *g) {
-    return g->d.n_entries < ((int64_t)1 << 26) && !std::getenv("TEMPME_FORCE_UNKEYED");
+    return g->d.n_entries < ((int64_t)1 << 26) && !debug_opt(TM_DEBUG_FORCE_UNKEYED);
 }
 
 extern "C" int tm_sample_khop(const tm_graph *g, tm_rng rng, int32_t k, int32_t N, int32_t B, const int32_t *root,

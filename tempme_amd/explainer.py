@@ -284,13 +284,12 @@ class TempME(nn.Module):
         tm_weights_create_ex) for hid_dim up to 256: the fused walk kernel for the default shape (hid_dim 64
         with the category feature), the LDS-tiled kernels for the others; a hid_dim that is not a multiple of
         16 runs them on weights zero-padded to the next one (_pad_hidden)."""
-        ok = 0 < self.hid_dim <= 256
-        if not ok and not getattr(self, "_warned_torch", False):
-            warnings.warn("TempME(if_cat_feature=%s, hid_dim=%d): no HIP kernel instance for this constructor "
-                          "variant; forward / retrieve_edge_imp_node run the torch-op formulation on the device"
-                          % (self.if_cat, self.hid_dim), RuntimeWarning, stacklevel=3)
-            self._warned_torch = True
-        return ok
+        if not 0 < self.hid_dim <= 256:
+            # no silent fallback: the eval kernels' LDS tiles hold at most a 256-wide hidden layer
+            raise L.TempMEError("TempME(hid_dim=%d): the HIP encoder kernels cover hid_dim 1..256 (their LDS tiles "
+                                "hold at most a 256-wide hidden layer); no other path exists on the device"
+                                % self.hid_dim)
+        return True
 
     def _hip_ok(self):
         """The training kernels (f3) cover every constructor variant (use_temporal_guidance,

@@ -1,0 +1,132 @@
+"""The explainer's optimizer (temp_exp_main.py:555, :631-632: ``torch.optim.Adam(explainer.parameters(), lr=...,
+weight_decay=...)``) as one HIP kernel over a flat fp32 bucket (csrc/optim.hip, ``tm_adam_step``).
+
+``FusedAdam(params, lr, betas, eps, weight_decay)`` takes the module's parameters and moves them into ONE contiguous
+device buffer (``flat_param``; every parameter becomes a view of it, same Parameter objects), with their gradients
+views of a second buffer (``flat_grad``: autograd accumulates into the views in place) and the Adam moments in two
+more.  ``step()`` is one launch (no per-parameter or multi-tensor dispatch); ``zero_grad()`` one fill.  The
+data-parallel gradient all-reduce (train.GradAllReduce(flat_grad=opt.flat_grad)) runs on ``flat_grad`` itself:
+no packing copies before the collective and none after.  The step count lives on the device, so the step is
+capturable in a HIP graph (train.GraphedTrainStep).
+
+Semantics = torch.optim.Adam with amsgrad=False, maximize=False (the reference's arguments).  One difference by
+construction: torch skips a parameter whose ``.grad`` is None; here every parameter has a gradient view (zero when
+nothing reached it), so such a parameter's moments decay and, with m = v = 0 and weight_decay = 0, it does not move
+-- the same result as skipping it for parameters that never receive a gradient.
+"""
+import torch
+from torch.autograd.graph import increment_version
+
+from . import _lib as L
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, amsgrad=False):
+        if amsgrad:
+            raise ValueError("FusedAdam: amsgrad is not supported (the reference does not use it)")
+        if not 0.0 <= lr or not 0.0 <= eps or not all(0.0 <= b < 1.0 for b in betas) or not 0.0 <= weight_decay:
+            raise ValueError("FusedAdam: bad hyper-parameters")
+        super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay))
+        if len(self.param_groups) != 1:
+            raise ValueError("FusedAdam: one parameter group (the explainer's parameters)")
+        # parameters that cannot receive a gradient (frozen feature tables) stay outside the bucket and are never
+        # touched -- torch.optim.Adam skips them the same way (their .grad stays None)
+        ps = [p for p in self.param_groups[0]["params"] if p.requires_grad]
+        if not ps:
+            raise ValueError("FusedAdam: no trainable parameters")
+        dev = ps[0].device
+        if dev.type != "cuda" or any(p.device != dev or p.dtype != torch.float32 for p in ps):
+            raise ValueError("FusedAdam: fp32 parameters on one GPU")
+        if len({p.data_ptr() for p in ps}) != len(ps):
+            raise ValueError("FusedAdam: a parameter is listed twice")
+        n = sum(p.numel() for p in ps)
+        self.flat_param = torch.empty(n, dtype=torch.float32, device=dev)
+        self.flat_grad = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.exp_avg = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.step_t = torch.zeros(1, dtype=torch.float32, device=dev)
+        self._done = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._spans = []
+        off = 0
+        with torch.no_grad():
+            for p in ps:
+                k = p.numel()
+                self.flat_param[off:off + k].copy_(p.reshape(-1))
+                self._spans.append((p, off, k))
+                off += k
+        self._params = [p for p, _, _ in self._spans]
+        self._bind()
+
+    def _bind(self):
+        """Every parameter, its gradient and its Adam state as views of the flat buffers."""
+        for p, off, k in self._spans:
+            p.data = self.flat_param[off:off + k].view_as(p)
+            p.grad = self.flat_grad[off:off + k].view_as(p)
+            self.state[p] = {"step": self.step_t, "exp_avg": self.exp_avg[off:off + k].view_as(p),
+                             "exp_avg_sq": self.exp_avg_sq[off:off + k].view_as(p)}
+
+    def _grads_bound(self):
+        for p, off, k in self._spans:
+            g = p.grad
+            if g is None or g.data_ptr() != self.flat_grad[off:].data_ptr():
+                return False
+        return True
+
+    @torch.no_grad()
+    def zero_grad(self, set_to_none=True):
+        """One fill of the flat gradient bucket (the views stay bound: ``set_to_none`` is not applied)."""
+        self.flat_grad.zero_()
+        if not self._grads_bound():
+            for p, off, k in self._spans:
+                p.grad = self.flat_grad[off:off + k].view_as(p)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        if not self._grads_bound():
+            # a caller replaced a .grad (e.g. set it to None and ran backward): copy it into the bucket
+            for p, off, k in self._spans:
+                if p.grad is None:
+                    self.flat_grad[off:off + k].zero_()
+                elif p.grad.data_ptr() != self.flat_grad[off:].data_ptr():
+                    self.flat_grad[off:off + k].copy_(p.grad.reshape(-1))
+                p.grad = self.flat_grad[off:off + k].view_as(p)
+        for p, off, k in self._spans:
+            if p.data_ptr() != self.flat_param[off:].data_ptr():
+                raise RuntimeError("FusedAdam: a parameter was rebound away from the flat bucket")
+        g = self.param_groups[0]
+        b1, b2 = g["betas"]
+        L.check(L.lib().tm_adam_step(L.ptr(self.flat_param), L.ptr(self.flat_grad), L.ptr(self.exp_avg),
+                                     L.ptr(self.exp_avg_sq), self.flat_param.numel(), float(g["lr"]), float(b1),
+                                     float(b2), float(g["eps"]), float(g["weight_decay"]), 1.0, L.ptr(self.step_t),
+                                     L.ptr(self._done), L.stream_ptr(self.flat_param.device)), "FusedAdam.step")
+        # the kernel wrote the parameters behind autograd's back: bump their version counters as torch's in-place
+        # update would, so caches keyed on them (the explainer's packed weights) see the change
+        increment_version(self._params)
+        return loss
+
+    def load_state_dict(self, state_dict):
+        """torch.optim's state dict (per-parameter exp_avg / exp_avg_sq / step), copied into the flat buffers."""
+        super().load_state_dict(state_dict)
+        with torch.no_grad():
+            steps = []
+            for p, off, k in self._spans:
+                st = self.state.get(p, {})
+                if "exp_avg" in st:
+                    self.exp_avg[off:off + k].copy_(st["exp_avg"].reshape(-1))
+                    self.exp_avg_sq[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
+                else:
+                    self.exp_avg[off:off + k].zero_()
+                    self.exp_avg_sq[off:off + k].zero_()
+                if "step" in st:
+                    steps.append(float(st["step"]))
+            if len(set(steps)) > 1:
+                raise ValueError("FusedAdam: parameters at different step counts cannot share one bucket")
+            self.step_t.fill_(steps[0] if steps else 0.0)
+        self._bind()
+
+
+__all__ = ["FusedAdam"]

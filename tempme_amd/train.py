@@ -146,16 +146,23 @@ class GradAllReduce:
     both back to back.  ``force``: run the collective even in a group of one (exercises the backend's
     path, e.g. RCCL on one GPU; at world size 1 the average is the gradient itself)."""
 
-    def __init__(self, module, group=None, force=False):
+    def __init__(self, module, group=None, force=False, flat_grad=None):
+        """``flat_grad``: the one buffer every gradient of ``module`` is a view of (optim.FusedAdam.flat_grad):
+        the all-reduce runs on it in place -- no packing copies before the collective or after it."""
         self.module, self.group = module, group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.force = bool(force) and dist.is_initialized()
+        self.flat_grad = flat_grad
         self._flat = None
         self._work = None
         self._grads = None
 
     def start(self):
         if self.world == 1 and not self.force:
+            return
+        if self.flat_grad is not None:
+            self._flat, self._grads = self.flat_grad, None
+            self._work = dist.all_reduce(self._flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
             return
         grads = [p.grad for p in self.module.parameters() if p.grad is not None]
         if not grads:
@@ -176,6 +183,8 @@ class GradAllReduce:
         self._work.wait()
         self._work = None
         self._flat.div_(self.world)
+        if self._grads is None:          # the flat bucket IS the gradients
+            return
         off = 0
         for g in self._grads:
             g.copy_(self._flat[off:off + g.numel()].view_as(g))

@@ -1,5 +1,5 @@
 """GPU: the device CSR build (graph_dev.hip, tm_graph_build_edges) against the host builder (graph.cpp,
-TEMPME_HOST_BUILD=1) on the same edge rows -- every exported column (off / ngh / eid / ts / get_ts2idx
+tm_debug_set(TM_DEBUG_HOST_BUILD, 1)) on the same edge rows -- every exported column (off / ngh / eid / ts / get_ts2idx
 values) identical, and every sampled output of the fused sampler identical (which exercises the e_idx
 table, the block search trees, the block ranks and the block hash table).  Tie-heavy graphs with
 self-loops and a node 0, an Enron-shaped hub graph, a sparse 100k-node graph, and rows that repeat an
@@ -48,12 +48,12 @@ def _enron(n_nodes, n_edges, alpha, seed):
 
 
 def _build(dev, rows, host):
-    if host:
-        os.environ["TEMPME_HOST_BUILD"] = "1"
+    from tempme_amd import _lib as L
+    L.check(L.lib().tm_debug_set(L.TM_DEBUG_HOST_BUILD, int(host)), "tm_debug_set")
     try:
         return tm.NeighborFinder.from_edges(*rows[:4], rows[4], device=dev, seed=3)
     finally:
-        os.environ.pop("TEMPME_HOST_BUILD", None)
+        L.check(L.lib().tm_debug_set(L.TM_DEBUG_HOST_BUILD, 0), "tm_debug_set")
 
 
 CASES = {

@@ -378,9 +378,10 @@ def test_khop2_fused_equals_per_level_and_oracle(tm, N):
             assert np.array_equal(two[a][h].reshape(-1), np.asarray(o[a][h]).reshape(-1)), (h, a)
 
 
-def test_unkeyed_kernels_equal_keyed(tm, monkeypatch):
+def test_unkeyed_kernels_equal_keyed(tm):
     """The one-compare keyed rank kernels (graphs < 2^26 entries) and the two-compare kernels must
-    give identical samples (TEMPME_FORCE_UNKEYED selects the latter)."""
+    give identical samples (tm_debug_set(TM_DEBUG_FORCE_UNKEYED, 1) selects the latter)."""
+    from tempme_amd import _lib as L
     from tempme_amd.preprocess import sample_events
     g, rows, (src, dst, ts, eidx), pool, f = _pareto_finder(tm, seed=6)
     dev = f.device
@@ -390,9 +391,12 @@ def test_unkeyed_kernels_equal_keyed(tm, monkeypatch):
             t(eidx, np.int32), torch.arange(E, dtype=torch.int32, device=dev), torch.from_numpy(pool).to(dev))
     a = sample_events(*args)
     ka = f.find_k_hop(2, src[:E], ts[:E], N, e_idx_l=eidx[:E], event_ids=np.arange(E), side=px.SIDE_TGT)
-    monkeypatch.setenv("TEMPME_FORCE_UNKEYED", "1")
-    b = sample_events(*args)
-    kb = f.find_k_hop(2, src[:E], ts[:E], N, e_idx_l=eidx[:E], event_ids=np.arange(E), side=px.SIDE_TGT)
+    L.check(L.lib().tm_debug_set(L.TM_DEBUG_FORCE_UNKEYED, 1), "tm_debug_set")
+    try:
+        b = sample_events(*args)
+        kb = f.find_k_hop(2, src[:E], ts[:E], N, e_idx_l=eidx[:E], event_ids=np.arange(E), side=px.SIDE_TGT)
+    finally:
+        L.check(L.lib().tm_debug_set(L.TM_DEBUG_FORCE_UNKEYED, 0), "tm_debug_set")
     for name in ("dst_fake", "node6", "eid3", "ts3", "cat", "cnt", "hist", "sub1_node", "sub1_eid", "sub1_ts",
                  "sub2_node", "sub2_eid", "sub2_ts"):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
@@ -655,7 +659,21 @@ def test_constructor_shapes_on_hip(tm, hid, if_cat, tg):
         B = r0.shape[0]
         np.testing.assert_allclose(expl[0][k * B:(k + 1) * B].cpu().numpy(), r0.numpy(), rtol=RTOL, atol=ATOL)
         np.testing.assert_allclose(expl[1][k * B:(k + 1) * B].cpu().numpy(), r1.numpy(), rtol=RTOL, atol=ATOL)
-    assert ex._packed is not None and not getattr(ex, "_warned_torch", False), "the HIP encoder did not run"
+    assert ex._packed is not None, "the HIP encoder did not run"
+
+
+def test_hid_dim_above_256_fails_loudly(tm):
+    """hid_dim > 256 has no HIP kernel instance: the forward raises TempMEError (no silent torch path)."""
+    from tempme_amd import _lib as L
+    from tests.encoder_inputs import load
+    d = load("synth")
+    dev = torch.device("cuda", 0)
+    ex = tm.TempME(_Base(d["n_feat"], d["e_feat"], dev), "tgn", "x", out_dim=40, hid_dim=272, device=dev,
+                   null_model={k + 1: float(v) for k, v in enumerate(d["null"])}).to(dev).eval()
+    x = d["src"]
+    with pytest.raises(L.TempMEError, match="hid_dim 1..256"):
+        with torch.no_grad():
+            ex((x["node"], x["eid"], x["ts"], x["cat"], x["marg"]), d["ts_cut"], x["cnt"])
 
 
 def test_strict_temporal_view_vs_oracle(tm):

@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     for f in header_functions():
         assert hasattr(L, f), f
     assert set(header_functions()) == set(_lib.EXPORTS)
-    assert L.tm_version() == 2
+    assert L.tm_version() == 3
 
 
 def test_library_is_gfx950_code_object():

@@ -179,6 +179,61 @@ def test_grad_all_reduce_two_ranks():
     assert all(p.exitcode == 0 for p in procs)
 
 
+def _flat_grad_worker(rank, world, port, q):
+    """GradAllReduce(flat_grad=...): every gradient a view of one bucket (optim.FusedAdam's layout), the all-reduce
+    on the bucket in place; the averages equal the per-parameter path's."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tempme_amd.train import GradAllReduce
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(torch.nn.Linear(5, 7), torch.nn.ReLU(), torch.nn.Linear(7, 1))
+        n = sum(p.numel() for p in net.parameters())
+        flat = torch.zeros(n)
+        off = 0
+        for p in net.parameters():
+            p.grad = flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        sync = GradAllReduce(net, flat_grad=flat)
+        for step in range(3):
+            x = torch.randn(4, 5, generator=torch.Generator().manual_seed(100 * step + rank))
+            flat.zero_()
+            net[2](net[1](net[0](x))).pow(2).mean().backward()
+            local = flat.clone()
+            sync.start()
+            sync.finish()
+            gl = [None] * world
+            dist.all_gather_object(gl, local)
+            if rank == 0:
+                torch.testing.assert_close(flat, sum(gl) / world)
+                off = 0
+                for p in net.parameters():                 # the .grad views see the averages
+                    assert p.grad.data_ptr() == flat[off:].data_ptr()
+                    off += p.numel()
+        if rank == 0:
+            q.put("ok")
+        dist.barrier()
+    except Exception as exc:
+        q.put(repr(exc))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_all_reduce_flat_bucket_two_ranks():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_flat_grad_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == "ok", res
+    assert all(p.exitcode == 0 for p in procs)
+
+
 def _bench_env():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
                                                             "MASTER_PORT")}
