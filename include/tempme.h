@@ -350,18 +350,20 @@ int tm_kl_loss(const float *prob, const int32_t *cat, const float *null12, float
  * [n] from g = d(x[:,0] * pad), the sample x [n,2] and d = torch._dirichlet_grad(x, conc, total) -- the
  * same fp32 operations as torch's autograd graph of Beta(...).rsample() * pad. */
 int tm_beta_params(const float *p, int64_t n, float *conc, float *total, void *stream);
+int tm_beta_rsample_bwd(const float *g, const float *pad, const float *x, const float *d, const float *p, int64_t n,
+                        float *dp, void *stream);
 
 /* The explainer's optimizer step (temp_exp_main.py:631-632: torch.optim.Adam, amsgrad off) in ONE launch over a
- * flat fp32 bucket of n parameters and their gradients (16-byte aligned): exp_avg / exp_avg_sq updated in place,
+ * flat fp32 bucket of n parameters and their gradients (the four buffers at one offset within 16 bytes, so a span of
+ * a larger bucket works): exp_avg / exp_avg_sq updated in place,
  * g = grad * grad_scale (+ weight_decay * param), bias corrections from the device step count `step` (the count
- * before this step; the kernel advances it, so a captured HIP graph replays correctly) and `done`, a device
- * uint32 that must be 0 before the first launch (the kernel leaves it 0).  Replaces torch.optim.Adam.step /
+ * before this step; a launch with advance != 0 advances it -- the last of a step's launches when a step updates
+ * several spans --, so a captured HIP graph replays correctly) and `done`, a device uint32 that must be 0 before the
+ * first launch (the kernel leaves it 0).  Replaces torch.optim.Adam.step /
  * torch's fused Adam over the explainer's parameters (tempme_amd/optim.py FusedAdam). */
 int tm_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, float lr, float beta1,
                  float beta2, float eps, float weight_decay, float grad_scale, float *step, uint32_t *done,
-                 void *stream);
-int tm_beta_rsample_bwd(const float *g, const float *pad, const float *x, const float *d, const float *p, int64_t n,
-                        float *dp, void *stream);
+                 int32_t advance, void *stream);
 
 /* retrieve_edge_imp_node, eval (explainer_new.py:354-406, :420-430) for each of the G*B
  * (group, event) rows: dependency gate, walk->edge scatter-max, gather at the subgraph eids,

@@ -186,7 +186,7 @@ def _sig(L):
     L.tm_profile_enable.argtypes = [C.c_int]
     L.tm_beta_params.argtypes = [vp, i64, vp, vp, vp]
     f32 = C.c_float
-    L.tm_adam_step.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, f32, vp, vp, vp]
+    L.tm_adam_step.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, f32, vp, vp, i32, vp]
     L.tm_beta_rsample_bwd.argtypes = [vp, vp, vp, vp, vp, i64, vp, vp]
     L.tm_profile_entry.argtypes = [C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(i64)]
     for name in EXPORTS:

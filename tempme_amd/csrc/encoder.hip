@@ -1436,6 +1436,19 @@ __global__ void __launch_bounds__(64 * WALK_WPB, 4 * WALK_WAVES / WALK_WPB) walk
             unext = ticket();
             coords(unext, vn, egn, jn);
         }
+        // remaining-work priority (s_setprio 3 -> 0 over the unit's passes): of the two waves sharing a SIMD's
+        // MFMA pipe, the one with more of its unit left issues first, so a pair ends its units together; the
+        // default oldest-first arbitration starves the younger wave (its units took 100-300 us at the 8-rank
+        // share) and leaves its last unit running alone at the end of the grid (tools/walk_trace.py).  With the
+        // late tickets: walk_kernel 0.872 -> 0.852 ms at 24 batches, 6.083 -> 6.038 ms at 192
+        // (profiles/r06_walk_tail_ab.txt)
+        if (PERSIST) {
+            const int q = (pass * 4) / n_pass;
+            if (q == 0) __builtin_amdgcn_s_setprio(3);
+            else if (q == 1) __builtin_amdgcn_s_setprio(2);
+            else if (q == 2) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
         const int m = SPLIT ? m0 : pass == 0 ? 0 : (pass - 1) >> 1;
         const int p = pass == 0 ? 2 : ((pass - 1) & 1);
         const int64_t gw = eg * a.W + (int64_t)j * a.M + m;

@@ -24,6 +24,8 @@ struct AdamArgs {
     float lr, beta1, beta2, eps, weight_decay, grad_scale;
     float *step;          // device: the step count before this step (torch's state["step"])
     uint32_t *done;       // device: completion counter, 0 between launches
+    int64_t head;         // elements before the first 16-byte-aligned one (the four buffers share the offset)
+    int advance;          // this launch advances the step count (the last of a step's launches)
 };
 
 __device__ __forceinline__ void adam_elem(float &p, float g, float &m, float &v, const AdamArgs &a, float step_size,
@@ -41,12 +43,12 @@ __global__ void __launch_bounds__(256) adam_kernel(AdamArgs a) {
     const double bc1 = 1.0 - pow((double)a.beta1, t), bc2 = 1.0 - pow((double)a.beta2, t);
     const float step_size = (float)((double)a.lr / bc1);
     const float bc2_sqrt = (float)sqrt(bc2);
-    const int64_t n4 = a.n >> 2;
+    const int64_t h = a.head, n4 = (a.n - h) >> 2;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    float4 *p4 = reinterpret_cast<float4 *>(a.p);
-    float4 *m4 = reinterpret_cast<float4 *>(a.m);
-    float4 *v4 = reinterpret_cast<float4 *>(a.v);
-    const float4 *g4 = reinterpret_cast<const float4 *>(a.g);
+    float4 *p4 = reinterpret_cast<float4 *>(a.p + h);
+    float4 *m4 = reinterpret_cast<float4 *>(a.m + h);
+    float4 *v4 = reinterpret_cast<float4 *>(a.v + h);
+    const float4 *g4 = reinterpret_cast<const float4 *>(a.g + h);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
         float4 p = p4[i], m = m4[i], v = v4[i];
         const float4 g = g4[i];
@@ -58,8 +60,10 @@ __global__ void __launch_bounds__(256) adam_kernel(AdamArgs a) {
         m4[i] = m;
         v4[i] = v;
     }
-    if (blockIdx.x == 0 && threadIdx.x < (a.n & 3)) {
-        const int64_t i = (n4 << 2) + threadIdx.x;
+    // the unaligned head and the tail after the last float4 (at most 3 + 3 elements)
+    const int64_t tail = (a.n - h) & 3;
+    if (blockIdx.x == 0 && threadIdx.x < h + tail) {
+        const int64_t i = threadIdx.x < h ? (int64_t)threadIdx.x : h + (n4 << 2) + (threadIdx.x - h);
         float p = a.p[i], m = a.m[i], v = a.v[i];
         adam_elem(p, a.g[i], m, v, a, step_size, bc2_sqrt);
         a.p[i] = p;
@@ -67,6 +71,7 @@ __global__ void __launch_bounds__(256) adam_kernel(AdamArgs a) {
         a.v[i] = v;
     }
     // the last workgroup advances the step count (every workgroup has read it by then) and resets the counter
+    if (!a.advance) return;
     __syncthreads();
     if (threadIdx.x == 0) {
         __threadfence();
@@ -84,15 +89,19 @@ using namespace tmk;
 
 extern "C" int tm_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, float lr,
                             float beta1, float beta2, float eps, float weight_decay, float grad_scale, float *step,
-                            uint32_t *done, void *stream) {
+                            uint32_t *done, int32_t advance, void *stream) {
     if (n < 0 || !(lr >= 0.f) || !(beta1 >= 0.f && beta1 < 1.f) || !(beta2 >= 0.f && beta2 < 1.f) || !(eps >= 0.f))
         return fail(TM_E_ARG, "tm_adam_step: bad arguments");
     if (n == 0) return TM_OK;
     if (!param || !grad || !exp_avg || !exp_avg_sq || !step || !done) return fail(TM_E_ARG, "tm_adam_step: NULL pointer");
-    for (const void *q : {(const void *)param, (const void *)grad, (const void *)exp_avg, (const void *)exp_avg_sq})
-        if (reinterpret_cast<uintptr_t>(q) & 15) return fail(TM_E_ARG, "tm_adam_step: buffers must be 16-byte aligned");
-    AdamArgs a{param, grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, grad_scale, step, done};
-    const int64_t n4 = n >> 2;
+    const uintptr_t mis = reinterpret_cast<uintptr_t>(param) & 15;
+    for (const void *q : {(const void *)grad, (const void *)exp_avg, (const void *)exp_avg_sq})
+        if ((reinterpret_cast<uintptr_t>(q) & 15) != mis || (mis & 3))
+            return fail(TM_E_ARG, "tm_adam_step: the four buffers must share their offset within 16 bytes");
+    const int64_t head = std::min<int64_t>(n, (int64_t)((16 - mis) & 15) / 4);
+    AdamArgs a{param, grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, grad_scale, step, done,
+               head, advance ? 1 : 0};
+    const int64_t n4 = (n - head) >> 2;
     const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n4 + 255) / 256, 2048));
     hipEvent_t pe = prof_begin((hipStream_t)stream);
     adam_kernel<<<dim3(blocks), 256, 0, (hipStream_t)stream>>>(a);

@@ -9,10 +9,12 @@ data-parallel gradient all-reduce (train.GradAllReduce(flat_grad=opt.flat_grad))
 no packing copies before the collective and none after.  The step count lives on the device, so the step is
 capturable in a HIP graph (train.GraphedTrainStep).
 
-Semantics = torch.optim.Adam with amsgrad=False, maximize=False (the reference's arguments).  One difference by
-construction: torch skips a parameter whose ``.grad`` is None; here every parameter has a gradient view (zero when
-nothing reached it), so such a parameter's moments decay and, with m = v = 0 and weight_decay = 0, it does not move
--- the same result as skipping it for parameters that never receive a gradient.
+Semantics = torch.optim.Adam with amsgrad=False, maximize=False (the reference's arguments).  torch skips a parameter
+whose ``.grad`` is None (nothing reached it in backward); here every parameter has a gradient view, so a
+post-accumulate-grad hook records which parameters autograd reached since ``zero_grad`` and the step updates only
+their spans (one launch when every parameter was reached, the common case; a launch per contiguous run otherwise).
+One step count is shared by the bucket, as torch's per-parameter counts are equal when the same parameters receive
+gradients every step (the reference's training loop).
 """
 import torch
 from torch.autograd.graph import increment_version
@@ -55,6 +57,9 @@ class FusedAdam(torch.optim.Optimizer):
                 self._spans.append((p, off, k))
                 off += k
         self._params = [p for p, _, _ in self._spans]
+        self._reached = set()
+        for i, p in enumerate(self._params):
+            p.register_post_accumulate_grad_hook(lambda _p, i=i: self._reached.add(i))
         self._bind()
 
     def _bind(self):
@@ -76,6 +81,7 @@ class FusedAdam(torch.optim.Optimizer):
     def zero_grad(self, set_to_none=True):
         """One fill of the flat gradient bucket (the views stay bound: ``set_to_none`` is not applied)."""
         self.flat_grad.zero_()
+        self._reached.clear()
         if not self._grads_bound():
             for p, off, k in self._spans:
                 p.grad = self.flat_grad[off:off + k].view_as(p)
@@ -88,21 +94,34 @@ class FusedAdam(torch.optim.Optimizer):
                 loss = closure()
         if not self._grads_bound():
             # a caller replaced a .grad (e.g. set it to None and ran backward): copy it into the bucket
-            for p, off, k in self._spans:
+            for i, (p, off, k) in enumerate(self._spans):
                 if p.grad is None:
                     self.flat_grad[off:off + k].zero_()
+                    self._reached.discard(i)
                 elif p.grad.data_ptr() != self.flat_grad[off:].data_ptr():
                     self.flat_grad[off:off + k].copy_(p.grad.reshape(-1))
+                    self._reached.add(i)
                 p.grad = self.flat_grad[off:off + k].view_as(p)
         for p, off, k in self._spans:
             if p.data_ptr() != self.flat_param[off:].data_ptr():
                 raise RuntimeError("FusedAdam: a parameter was rebound away from the flat bucket")
         g = self.param_groups[0]
         b1, b2 = g["betas"]
-        L.check(L.lib().tm_adam_step(L.ptr(self.flat_param), L.ptr(self.flat_grad), L.ptr(self.exp_avg),
-                                     L.ptr(self.exp_avg_sq), self.flat_param.numel(), float(g["lr"]), float(b1),
-                                     float(b2), float(g["eps"]), float(g["weight_decay"]), 1.0, L.ptr(self.step_t),
-                                     L.ptr(self._done), L.stream_ptr(self.flat_param.device)), "FusedAdam.step")
+        # contiguous runs of the parameters autograd reached (torch.optim.Adam skips the others)
+        runs, start = [], None
+        for i, (p, off, k) in enumerate(self._spans + [(None, self.flat_param.numel(), 0)]):
+            hit = i < len(self._spans) and i in self._reached
+            if hit and start is None:
+                start = off
+            elif not hit and start is not None:
+                runs.append((start, off))
+                start = None
+        fn, st = L.lib().tm_adam_step, L.stream_ptr(self.flat_param.device)
+        for r, (a, b) in enumerate(runs):
+            L.check(fn(self.flat_param.data_ptr() + 4 * a, self.flat_grad.data_ptr() + 4 * a,
+                       self.exp_avg.data_ptr() + 4 * a, self.exp_avg_sq.data_ptr() + 4 * a, b - a, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
+                       float(g["weight_decay"]), 1.0, L.ptr(self.step_t), L.ptr(self._done), int(r + 1 == len(runs)),
+                       st), "FusedAdam.step")
         # the kernel wrote the parameters behind autograd's back: bump their version counters as torch's in-place
         # update would, so caches keyed on them (the explainer's packed weights) see the change
         increment_version(self._params)
