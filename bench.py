@@ -427,9 +427,15 @@ def main():
     ap.add_argument("--no-edge-table", action="store_true",
                     help="lin_event's edge-feature product per walk position instead of per edge id")
     ap.add_argument("--streams", type=int, default=0,
-                    help="steps in flight (PipelinedExplainer); 0 = auto: 2 when a rank holds <= 24 reference batches "
-                         "per step (the 8-GPU share of the metric's step: 1.140 -> 1.074 ms per step timed on one GPU, "
-                         "profiles/r05_strong_estimate.txt), else 1")
+                    help="steps in flight (PipelinedExplainer); 0 = auto: 1 with one rank (the kernel-level roofline of "
+                         "record: every launch alone on the chip; the N=1 line reports the 3-in-flight figure beside "
+                         "it as 'pipelined'), 3 with overlapping walk kernels with several ranks (a rank's share of the "
+                         "step is small there: 0.99 -> 0.93 ms per step at the 8-rank share, "
+                         "profiles/r06_flight_ab.txt)")
+    ap.add_argument("--overlap-walk", action="store_true",
+                    help="with steps in flight, let one step's walk kernel start while the previous one's grid drains "
+                         "(PipelinedExplainer(chain_encoders=False)) instead of chaining the encoders (auto with "
+                         "--streams 0 and several ranks)")
     ap.add_argument("--no-node-zero", action="store_true",
                     help="do not specialise the walk kernel for an all-zero node-feature table (A/B)")
     ap.add_argument("--contrast", choices=("auto", "graphmixer", "none"), default="auto",
@@ -506,7 +512,8 @@ def main():
                    null_model={k: 1.0 / 12 for k in range(1, 13)}).to(dev).eval()
     ex.node_zero_specialization = not args.no_node_zero
     rank_batches = args.batches if args.weak else args.batches // max(1, world)
-    S = args.streams if args.streams > 0 else (2 if rank_batches <= 24 else 1)
+    S = args.streams if args.streams > 0 else (1 if world == 1 else 3)
+    overlap = S > 1 and (args.overlap_walk or args.streams == 0)
     contrast = args.contrast if args.contrast != "auto" else ("graphmixer" if args.config == 4 else "none")
     gm = None
     if contrast == "graphmixer":
@@ -527,7 +534,7 @@ def main():
                 gm_contrast(gm, pipe.buf, x, h1)
     else:
         flight = PipelinedExplainer(ex, finder.graph, torch.from_numpy(pool), N, M, B, seed=args.seed, depth=S,
-                                    edge_table=not args.no_edge_table)
+                                    edge_table=not args.no_edge_table, chain_encoders=not overlap)
         pipes = flight.pipes
         pipe = pipes[0]
 
@@ -562,6 +569,20 @@ def main():
         el2, _ = timed(run_step, pipes, inputs2, args.warmup, args.steps, dist, backend, dev, L)
         weak = {"scaling": "weak" if strong else "strong", "value": round(world * args.steps * per_rank2 / el2, 2),
                 "ms_per_step": round(el2 / args.steps * 1e3, 3), "events_per_step_per_gpu": per_rank2}
+    pipelined = None
+    if world == 1 and S == 1 and not args.no_extras and gm is None:
+        # like-for-like with the multi-rank lines: the same step with 3 steps in flight and overlapping walk kernels
+        fl3 = PipelinedExplainer(ex, finder.graph, torch.from_numpy(pool), N, M, B, seed=args.seed, depth=3,
+                                 edge_table=not args.no_edge_table, chain_encoders=False)
+        for k in range(3):
+            fl3.submit(*inputs[k % n_steps])
+        el3, _ = timed(lambda x: fl3.submit(*x), fl3.pipes, inputs, args.warmup, args.steps, dist, backend, dev, L)
+        pipelined = {"value": round(args.steps * per_rank / el3, 2), "ms_per_step": round(el3 / args.steps * 1e3, 3),
+                     "steps_in_flight": 3, "walk_overlap": True,
+                     "what": "the same timed steps with 3 steps in flight, consecutive walk kernels overlapping (the "
+                             "multi-rank lines' mode); per-launch kernel durations then include the sharing, so the "
+                             "kernel roofline of record is the serial line's"}
+        del fl3
 
     if rank == 0:
         E = per_rank
@@ -592,6 +613,14 @@ def main():
                             "§8(d) per-walk model minus the edge-table MACs, for the same launch time")
         if tsrc:
             roof["traffic_source"] = tsrc
+        if overlap and dom in executed:
+            # consecutive steps' walk kernels overlap: a launch's duration includes the sharing, so credit the kernel
+            # with the whole step time instead (a lower bound on its rate)
+            ach = executed[dom] / (el / args.steps) / 1e12
+            roof.update(achieved=round(ach, 2), frac=round(ach / FP32_MFMA_PEAK_TF, 4),
+                        credited_frac=round(units[dom][1] / (el / args.steps) / 1e12 / FP32_MFMA_PEAK_TF, 4),
+                        basis="the step time (walk kernels of consecutive steps overlap, so per-launch durations "
+                              "include the sharing): a lower bound on the kernel's rate")
         samp = dict(kernels.get("events_kernel", {}))
         if samp and traffic.get("events_kernel") is not None:
             samp["traffic"] = traffic["events_kernel"]
@@ -613,12 +642,14 @@ def main():
                           "metric (full Enron + TGN, n_degree=20)", "n_degree": N, "walks_per_slot": M,
                           "batch_size": B, "global_batches_per_step": per_rank * world // B,
                           "events_per_step_per_gpu": per_rank, "parallelism": f"dp{world} (whole batches per rank)",
-                          "steps_in_flight": S, "base_contrast": contrast,
+                          "steps_in_flight": S, "walk_overlap": overlap, "base_contrast": contrast,
                           "edge_tables": "per weight state (see edge_tables), not per step",
                           "walk_kernel_zero_node_features": zn},
                "roofline": roof, "kernels": kernels, "sampling_roofline": samp or None, "edge_tables": edge_tables}
         if weak is not None:
             out["weak" if strong else "strong"] = weak
+        if pipelined is not None:
+            out["pipelined"] = pipelined
         if not args.no_extras:
             out["khop_roofline"] = khop_alone(pipe, inputs, min(args.steps, 5), N, group=8)
             out["dropin"] = dropin_leg(ex, pipe, inputs, B, N)

@@ -189,7 +189,7 @@ class PipelinedExplainer:
     before using them there); they are overwritten by call k + depth, so consume them first."""
 
     def __init__(self, explainer, graph, dst_list, N, M=3, B=100, seed=0, split=L.SPLIT_TEST, depth=2,
-                 edge_table=True):
+                 edge_table=True, chain_encoders=True):
         dev = graph.device
         self.depth = max(1, int(depth))
         tabs = EdgeTables(explainer, graph, edge_table)
@@ -198,6 +198,9 @@ class PipelinedExplainer:
         self.streams = [torch.cuda.Stream(device=dev) for _ in range(self.depth)]
         self._k = 0
         self._enc_done = None
+        # chain_encoders=False: call k+1's encoder may start while call k's runs -- its persistent workgroups take
+        # the CU slots call k's release at the end of its grid (the walk kernel holds every slot until then)
+        self.chain = bool(chain_encoders)
 
     def submit(self, src, dst, ts, eidx, event_ids):
         i = self._k % self.depth
@@ -208,7 +211,7 @@ class PipelinedExplainer:
             st.wait_event(ready)
             p.sample(src, dst, ts, eidx, event_ids)
             p.tables()
-            if self._enc_done is not None:
+            if self.chain and self._enc_done is not None:
                 st.wait_event(self._enc_done)
             p.encode(ts)
             self._enc_done = torch.cuda.Event()
