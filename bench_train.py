@@ -135,7 +135,7 @@ def main():
     if args.optim == "hip":
         from tempme_amd.optim import FusedAdam
         opt = FusedAdam(ex.parameters(), lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0)
-        sync = GradAllReduce(ex, flat_grad=opt.flat_grad)
+        sync = GradAllReduce(ex, bucket=opt)
     else:
         opt = torch.optim.Adam(ex.parameters(), lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0,
                                capturable=use_graph, fused=args.optim == "torch-fused")

@@ -353,6 +353,29 @@ int tm_beta_params(const float *p, int64_t n, float *conc, float *total, void *s
 int tm_beta_rsample_bwd(const float *g, const float *pad, const float *x, const float *d, const float *p, int64_t n,
                         float *dp, void *stream);
 
+/* Host arrays read in place by the GPU: the drop-in's host-pack path (the reference's eval loop hands
+ * TempME.forward / retrieve_explanation float64 / int64 numpy views of its load_subgraph_margin pack and
+ * np.load edge array per batch, utils/batch_loader.py:119-242, temp_exp_main.py:441-453).
+ * tm_host_register pins and maps [ptr, ptr + bytes) (page-rounded; the caller keeps the memory alive until
+ * tm_host_unregister(ptr)) and returns the device address of ptr; tm_stage_cast runs up to 16 jobs in one
+ * launch, each gathering an ndim <= 5 strided view (byte strides) of src (a device-accessible address: device
+ * memory or a registered host array's device address) into dst contiguous, converting its type (C conversions:
+ * truncation toward zero for integers, round to nearest for float32 -- numpy's astype / torch's .to). */
+#define TM_I32 1
+#define TM_F32 2
+#define TM_I64 3
+#define TM_F64 4
+typedef struct tm_stage_job {
+    const void *src;
+    void *dst;
+    int32_t src_type, dst_type, ndim, reserved;
+    int64_t shape[5];
+    int64_t stride[5];   /* bytes */
+} tm_stage_job;
+int tm_host_register(void *ptr, int64_t bytes, void **dev_ptr);
+int tm_host_unregister(void *ptr);
+int tm_stage_cast(const tm_stage_job *jobs, int32_t n_jobs, void *stream);
+
 /* The explainer's optimizer step (temp_exp_main.py:631-632: torch.optim.Adam, amsgrad off) in ONE launch over a
  * flat fp32 bucket of n parameters and their gradients (the four buffers at one offset within 16 bytes, so a span of
  * a larger bucket works): exp_avg / exp_avg_sq updated in place,
@@ -364,6 +387,14 @@ int tm_beta_rsample_bwd(const float *g, const float *pad, const float *x, const 
 int tm_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, float lr, float beta1,
                  float beta2, float eps, float weight_decay, float grad_scale, float *step, uint32_t *done,
                  int32_t advance, void *stream);
+/* Up to 32 fp32 copies in one launch (dst[0:n) = src[0:n) per job): the parameters' gradients, as autograd
+ * produced them, into the flat bucket tm_adam_step and the gradient all-reduce read. */
+typedef struct tm_copy_job {
+    const float *src;
+    float *dst;
+    int64_t n;
+} tm_copy_job;
+int tm_copy_many(const tm_copy_job *jobs, int32_t n_jobs, void *stream);
 
 /* retrieve_edge_imp_node, eval (explainer_new.py:354-406, :420-430) for each of the G*B
  * (group, event) rows: dependency gate, walk->edge scatter-max, gather at the subgraph eids,

@@ -42,7 +42,8 @@ EXPORTS = (
     "tm_explain_train_fwd", "tm_explain_train_fwd_pad", "tm_explain_train_bwd", "tm_kl_loss", "tm_edge_importance", "tm_edge_gate_table",
     "tm_edge_table_cols", "tm_edge_tables", "tm_edge_feature_table", "tm_edge_importance_tab", "tm_tgn_attn_fwd", "tm_tgn_attn_bwd", "tm_gm_packed_floats", "tm_gm_pack", "tm_gm_embed", "tm_gm_embed_bwd_ok", "tm_gm_embed_bwd", "tm_gm_packed_a_floats", "tm_gm_pack_a", "tm_gm_fused_ok", "tm_dropin_create", "tm_dropin_free", "tm_dropin_forward", "tm_dropin_set_stream", "tm_dropin_gate_cache", "tm_dropin_gate_cache_clear", "tm_edge_importance_gf", "tm_edge_importance_gf3", "tm_edge_importance_gf3_bern",
     "tm_mask_least_important", "tm_profile_enable", "tm_profile_sync", "tm_profile_entry",
-    "tm_beta_params", "tm_beta_rsample_bwd", "tm_adam_step",
+    "tm_beta_params", "tm_beta_rsample_bwd", "tm_adam_step", "tm_copy_many", "tm_host_register", "tm_host_unregister",
+    "tm_stage_cast",
 )
 
 
@@ -95,6 +96,20 @@ class WgradJob(C.Structure):
 class GatherJob(C.Structure):
     _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("row_bytes", C.c_int64), ("src_side_stride", C.c_int64),
                 ("dst_side_stride", C.c_int64), ("src_rows", C.c_int64), ("sides", C.c_int32), ("reserved", C.c_int32)]
+
+
+class CopyJob(C.Structure):
+    """tm_copy_job (include/tempme.h)."""
+    _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("n", C.c_int64)]
+
+
+class StageJob(C.Structure):
+    """tm_stage_job (include/tempme.h)."""
+    _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("src_type", C.c_int32), ("dst_type", C.c_int32),
+                ("ndim", C.c_int32), ("reserved", C.c_int32), ("shape", C.c_int64 * 5), ("stride", C.c_int64 * 5)]
+
+
+TM_I32, TM_F32, TM_I64, TM_F64 = 1, 2, 3, 4
 
 
 class WgradTarget(C.Structure):
@@ -187,6 +202,10 @@ def _sig(L):
     L.tm_beta_params.argtypes = [vp, i64, vp, vp, vp]
     f32 = C.c_float
     L.tm_adam_step.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, f32, vp, vp, i32, vp]
+    L.tm_copy_many.argtypes = [C.POINTER(CopyJob), i32, vp]
+    L.tm_host_register.argtypes = [vp, i64, C.POINTER(vp)]
+    L.tm_host_unregister.argtypes = [vp]
+    L.tm_stage_cast.argtypes = [vp, i32, vp]   # tm_stage_job rows (hoststage builds them as int64 words)
     L.tm_beta_rsample_bwd.argtypes = [vp, vp, vp, vp, vp, i64, vp, vp]
     L.tm_profile_entry.argtypes = [C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(i64)]
     for name in EXPORTS:

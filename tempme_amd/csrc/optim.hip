@@ -83,9 +83,43 @@ __global__ void __launch_bounds__(256) adam_kernel(AdamArgs a) {
     }
 }
 
+constexpr int kMaxCopyJobs = 32;
+
+struct CopyArgs {
+    tm_copy_job job[kMaxCopyJobs];
+};
+
+// blockIdx.y = job: dst[0:n) = src[0:n), grid-strided over blockIdx.x
+__global__ void __launch_bounds__(256) copy_many_kernel(CopyArgs a) {
+    const tm_copy_job &j = a.job[blockIdx.y];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < j.n; i += (int64_t)gridDim.x * blockDim.x)
+        j.dst[i] = j.src[i];
+}
+
 }  // namespace tmk
 
 using namespace tmk;
+
+// The parameters' gradients into the flat bucket (FusedAdam.sync_grads: autograd's own gradient tensors, one launch
+// per 32 parameters instead of an accumulation kernel per parameter per step)
+extern "C" int tm_copy_many(const tm_copy_job *jobs, int32_t n_jobs, void *stream) {
+    if (n_jobs < 0 || n_jobs > kMaxCopyJobs) return fail(TM_E_ARG, "tm_copy_many: bad job count");
+    if (n_jobs == 0) return TM_OK;
+    if (!jobs) return fail(TM_E_ARG, "tm_copy_many: NULL jobs");
+    CopyArgs a{};
+    int64_t most = 0;
+    for (int i = 0; i < n_jobs; ++i) {
+        if (jobs[i].n < 0 || (jobs[i].n > 0 && (!jobs[i].src || !jobs[i].dst)))
+            return fail(TM_E_ARG, "tm_copy_many: bad job " + std::to_string(i));
+        a.job[i] = jobs[i];
+        most = std::max(most, jobs[i].n);
+    }
+    if (most == 0) return TM_OK;
+    const unsigned bx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((most + 255) / 256, 256));
+    copy_many_kernel<<<dim3(bx, (unsigned)n_jobs), 256, 0, (hipStream_t)stream>>>(a);
+    TM_CHECK_LAUNCH();
+    return TM_OK;
+}
 
 extern "C" int tm_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, float lr,
                             float beta1, float beta2, float eps, float weight_decay, float grad_scale, float *step,

@@ -380,7 +380,10 @@ static void launch_fwd(const tm_tgn_attn &a, float *z, float *stats, hipStream_t
 template <int KPL>
 static void launch_bwd(const tm_tgn_attn &a, const float *stats, const float *gz, float *dp, float *dn, hipStream_t s) {
     const unsigned blocks = (unsigned)((a.rows + ATT_WAVES - 1) / ATT_WAVES);
-    const size_t lds = dn ? sizeof(float) * 3 * a.n_ngh * ATT_MAXH * ATT_WAVES : 0;
+    // the per-wave (p e, p, e c) rows are [n_ngh][HM]: LDS sized for the instance launched, so the 2-head form
+    // does not reserve (and lose occupancy to) 4 heads' worth
+    const int hm = a.n_head <= 2 ? 2 : ATT_MAXH;
+    const size_t lds = dn ? sizeof(float) * 3 * a.n_ngh * hm * ATT_WAVES : 0;
     // the heads' register arrays sized for at most 2 heads where that covers them (as the forward)
     if (a.n_head <= 2) {
         if (dn) tgn_attn_bwd_kernel<KPL, true, 2><<<dim3(blocks), 64 * ATT_WAVES, lds, s>>>(a, stats, gz, dp, dn);

@@ -202,6 +202,11 @@ def _dropin_ext():
     return _EXT[0]
 
 
+def _hoststage():
+    from . import hoststage
+    return hoststage
+
+
 def _to_many(device, *items):
     """[_to(a, device, dtype) for (a, dtype) in items], staged through one pinned copy when every
     array is a host numpy array and the device is a GPU."""
@@ -865,15 +870,25 @@ class TempME(nn.Module):
                             edge_identify, 1, B, W)
                     imp = _apply(_EvalEncoderBundleFn, self, args, imp, fx[1].bundle(self, "enc"))
                 return imp
-        if not (getattr(edge_idx, "_tm_resident", False) and getattr(node_idx, "_tm_resident", False) and
-                getattr(time_idx, "_tm_resident", False) and getattr(cat_feat, "_tm_resident", False) and
-                getattr(edge_identify, "_tm_resident", False)):
+        # host arrays: the reference's own numpy views of its pack (load_subgraph_margin / np.load), staged on the
+        # side stream below (read in place from pinned host memory, hoststage) and then the same launches
+        host = node_idx.__class__ is np.ndarray
+        if host:
+            if not (edge_idx.__class__ is np.ndarray and time_idx.__class__ is np.ndarray and
+                    cat_feat.__class__ is np.ndarray and edge_identify.__class__ is np.ndarray and edge_idx.ndim == 3):
+                return None
+        elif not (getattr(edge_idx, "_tm_resident", False) and getattr(node_idx, "_tm_resident", False) and
+                  getattr(time_idx, "_tm_resident", False) and getattr(cat_feat, "_tm_resident", False) and
+                  getattr(edge_identify, "_tm_resident", False)):
             return None
         # resident views are int32 / float32 slices of one pack: check that they are one batch's
         B, W, three = edge_idx.shape
-        if three != 3 or B == 0 or node_idx.shape != (B, W, 6) or time_idx.shape != (B, W, 3) or \
-                cat_feat.shape[:2] != (B, W) or edge_identify.shape != (B, W, 3, 3) or \
-                edge_idx.dtype is not torch.int32 or time_idx.dtype is not torch.float32:
+        if three != 3 or B == 0 or tuple(node_idx.shape) != (B, W, 6) or tuple(time_idx.shape) != (B, W, 3) or \
+                tuple(cat_feat.shape[:2]) != (B, W) or tuple(edge_identify.shape) != (B, W, 3, 3):
+            return None
+        if not host and (edge_idx.dtype is not torch.int32 or time_idx.dtype is not torch.float32):
+            return None
+        if host and (cat_feat.size != B * W or edge_idx.dtype.kind not in "iuf" or node_idx.dtype.kind not in "iuf"):
             return None
         dev = self._dev()
         cut_h = cut_d = None
@@ -891,6 +906,8 @@ class TempME(nn.Module):
         if not self._hip_eval_ok():
             return None
         fs = self._fast_state()
+        if host and edge_idx.size and (edge_idx.max() >= fs.keep[2].shape[0] or edge_idx.min() < 0):
+            raise IndexError("index out of range in self")     # what the reference's embedding lookup raises
         _, ctx, ext, nk = self._dropin_ctx(dev)
         k = nk[0]
         nk[0] = (k + 1) % 3
@@ -902,11 +919,23 @@ class TempME(nn.Module):
             st = torch.cuda.Stream(stream_id=cur[0], device_index=cur[1], device_type=cur[2])
             cobj = ctx.cur_obj = (cur, st, st.cuda_stream)
         torch._C._cuda_setStream(*ctx.side_ids[k])
+        host_keys = staged = None
         try:
             out = torch.empty(B * W * 4, dtype=torch.float32, device=dev)   # imp [B*W] | gate factors [B*W*3]
+            if host:
+                items = ((node_idx, torch.int32), (edge_idx, torch.int32), (time_idx, torch.float32),
+                         (cat_feat, torch.int32), (edge_identify, torch.float32))
+                staged = _hoststage().stage(dev, items)         # the current stream is side stream k here
+                if staged is None:                           # small / non-owning bases: pinned host-cast copy
+                    staged = _to_many(dev, *items)
+                host_keys = (edge_idx, time_idx)
+                node_idx, edge_idx, time_idx, cat_feat, edge_identify = staged
         finally:
             torch._C._cuda_setStream(*cur)
         out.record_stream(cobj[1])
+        if staged is not None:
+            # read on the caller's stream later (retrieve, backward): the views share one allocation
+            staged[0].record_stream(cobj[1])
         sync = 1 if (cut_d is not None or self.__dict__.get("_prep_dirty_fast", True)) else 0
         if sync:
             self._prep_dirty_fast = False
@@ -917,9 +946,14 @@ class TempME(nn.Module):
         if rc:
             L.check(rc, "TempME.forward")
         imp = out.as_strided((B, W, 1), (W, 1, 1))
-        # the gate factors, for retrieve_explanation with these very walk tensors (identity + version)
+        # the gate factors, for retrieve_explanation with these very walk tensors (identity + version) or host arrays
+        # (identity; their staged device copies ride along)
         gcache = self.__dict__.setdefault("_gf_cache", [])
-        gcache.append((edge_idx, time_idx, edge_idx._version, time_idx._version, fs.gate_key, out, B * W, B, W, fs))
+        if host:
+            gcache.append((host_keys[0], host_keys[1], 0, 0, fs.gate_key, out, B * W, B, W, fs, (edge_idx, time_idx)))
+        else:
+            gcache.append((edge_idx, time_idx, edge_idx._version, time_idx._version, fs.gate_key, out, B * W, B, W, fs,
+                           None))
         if len(gcache) > 6:
             del gcache[0]
         if fs.enc_grad and torch.is_grad_enabled():
@@ -928,7 +962,8 @@ class TempME(nn.Module):
             args = (node_idx, edge_idx, time_idx, cat_feat,
                     np.array(cut_time_l, dtype=np.float64) if cut_d is None else cut_time_l, edge_identify, 1, B, W)
             imp = _apply(_EvalEncoderBundleFn, self, args, imp, fs.bundle(self, "enc"))
-        self._make_fastx(fs, ctx, dev, (edge_idx, time_idx, out, B, W))
+        if not host:
+            self._make_fastx(fs, ctx, dev, (edge_idx, time_idx, out, B, W))
         return imp
 
     def _make_fastx(self, fs, ctx, dev, entry):
@@ -971,6 +1006,7 @@ class TempME(nn.Module):
         gc = self.__dict__.get("_gf_cache", ())
         gk = None
         got = []
+        host = sides[0][2][1].__class__ is np.ndarray
         for subgraph, imp, walks in sides:
             e3, t3 = walks[1], walks[2]
             h = None
@@ -978,7 +1014,7 @@ class TempME(nn.Module):
                 if ent[0] is e3 and ent[1] is t3:
                     h = ent
                     break
-            if h is None or e3._version != h[2] or t3._version != h[3]:
+            if h is None or (h[10] is not None) != host or (not host and (e3._version != h[2] or t3._version != h[3])):
                 return None
             if gk is None:
                 gk = self._gate_key(self._weight_list())
@@ -987,13 +1023,17 @@ class TempME(nn.Module):
             B, W = h[7], h[8]
             n1, n2 = subgraph[0]
             x1, x2 = subgraph[1]
-            for t in (n1, x1, n2, x2):
-                if not getattr(t, "_tm_resident", False):
+            if host:
+                if not all(t.__class__ is np.ndarray and t.ndim == 2 for t in (n1, x1, n2, x2)):
                     return None
+                e3, t3 = h[10]                           # the forward's staged device copies
+            elif not all(getattr(t, "_tm_resident", False) for t in (n1, x1, n2, x2)):
+                return None
             N = n1.shape[1]
             if imp.__class__ is not torch.Tensor or imp.dtype is not torch.float32 or imp.numel() != B * W or \
-                    not imp.is_contiguous() or n1.shape[0] != B or x1.shape != n1.shape or n2.shape != (B, N * N) or \
-                    x2.shape != n2.shape or n1.dtype is not torch.int32:
+                    not imp.is_contiguous() or n1.shape[0] != B or tuple(x1.shape) != tuple(n1.shape) or \
+                    tuple(n2.shape) != (B, N * N) or tuple(x2.shape) != tuple(n2.shape) or \
+                    (not host and n1.dtype is not torch.int32):
                 return None
             got.append((h, e3, t3, imp, n1, x1, n2, x2, B, W, N))
         B, W, N = got[0][8], got[0][9], got[0][10]
@@ -1001,6 +1041,13 @@ class TempME(nn.Module):
             if g[8] != B or g[9] != W or g[10] != N:
                 return None
         dev = self._dev()
+        if host:
+            # the three sides' hop-1 / hop-2 node and edge ids (float64 views of the reference's pack) in one launch
+            items = [(x, torch.int32) for g in got for x in g[4:8]]
+            st = _hoststage().stage(dev, items)
+            if st is None:
+                st = _to_many(dev, *items)
+            got = [g[:4] + tuple(st[4 * i:4 * i + 4]) + g[8:] for i, g in enumerate(got)]
         ctx = self.__dict__["_dropin_c"][1]
         n_out = 3 * B * (N + N * N)
         o = torch.empty(n_out * (2 if bern else 1), dtype=torch.float32, device=dev)

@@ -2,17 +2,19 @@
 weight_decay=...)``) as one HIP kernel over a flat fp32 bucket (csrc/optim.hip, ``tm_adam_step``).
 
 ``FusedAdam(params, lr, betas, eps, weight_decay)`` takes the module's parameters and moves them into ONE contiguous
-device buffer (``flat_param``; every parameter becomes a view of it, same Parameter objects), with their gradients
-views of a second buffer (``flat_grad``: autograd accumulates into the views in place) and the Adam moments in two
-more.  ``step()`` is one launch (no per-parameter or multi-tensor dispatch); ``zero_grad()`` one fill.  The
-data-parallel gradient all-reduce (train.GradAllReduce(flat_grad=opt.flat_grad)) runs on ``flat_grad`` itself:
-no packing copies before the collective and none after.  The step count lives on the device, so the step is
-capturable in a HIP graph (train.GraphedTrainStep).
+device buffer (``flat_param``; every parameter becomes a view of it, same Parameter objects), their gradients into a
+second (``flat_grad``) and the Adam moments into two more.  ``zero_grad()`` sets the gradients to None as torch's
+default does, so autograd hands each parameter its gradient tensor without an accumulation kernel;
+``sync_grads()`` (called by ``step()`` and by the data-parallel all-reduce, train.GradAllReduce(bucket=opt)) copies
+them into ``flat_grad`` in one launch per 32 parameters (``tm_copy_many``) and rebinds each ``.grad`` to its view
+of the bucket.  ``step()`` is then one launch (no per-parameter or multi-tensor dispatch), and the all-reduce runs
+on ``flat_grad`` itself.  The step count lives on the device, so the step is capturable in a HIP graph
+(train.GraphedTrainStep).
 
 Semantics = torch.optim.Adam with amsgrad=False, maximize=False (the reference's arguments).  torch skips a parameter
-whose ``.grad`` is None (nothing reached it in backward); here every parameter has a gradient view, so a
-post-accumulate-grad hook records which parameters autograd reached since ``zero_grad`` and the step updates only
-their spans (one launch when every parameter was reached, the common case; a launch per contiguous run otherwise).
+whose ``.grad`` is None (nothing reached it in backward); a post-accumulate-grad hook records which parameters
+autograd reached since ``zero_grad`` and the step updates only their spans (one launch when every parameter was
+reached, the common case; a launch per contiguous run otherwise).
 One step count is shared by the bucket, as torch's per-parameter counts are equal when the same parameters receive
 gradients every step (the reference's training loop).
 """
@@ -57,6 +59,7 @@ class FusedAdam(torch.optim.Optimizer):
                 self._spans.append((p, off, k))
                 off += k
         self._params = [p for p, _, _ in self._spans]
+        self._index = {id(p): i for i, p in enumerate(self._params)}
         self._reached = set()
         for i, p in enumerate(self._params):
             p.register_post_accumulate_grad_hook(lambda _p, i=i: self._reached.add(i))
@@ -79,12 +82,43 @@ class FusedAdam(torch.optim.Optimizer):
 
     @torch.no_grad()
     def zero_grad(self, set_to_none=True):
-        """One fill of the flat gradient bucket (the views stay bound: ``set_to_none`` is not applied)."""
-        self.flat_grad.zero_()
+        """``set_to_none`` (torch's default): every ``.grad`` None, so backward hands each parameter autograd's own
+        gradient tensor (no accumulation kernel); else one fill of the bucket with the views bound."""
         self._reached.clear()
+        if set_to_none:
+            for p in self._params:
+                p.grad = None
+            return
+        self.flat_grad.zero_()
         if not self._grads_bound():
             for p, off, k in self._spans:
                 p.grad = self.flat_grad[off:off + k].view_as(p)
+
+    @torch.no_grad()
+    def sync_grads(self):
+        """Every reached parameter's gradient into the bucket (tm_copy_many, up to 32 per launch) and its
+        ``.grad`` rebound to the bucket view; idempotent."""
+        jobs, rebind = [], []
+        for p, off, k in self._spans:
+            g = p.grad
+            if g is None:
+                continue
+            dst = self.flat_grad.data_ptr() + 4 * off
+            if g.data_ptr() == dst:
+                continue
+            if g.dtype != torch.float32 or not g.is_contiguous() or g.device != self.flat_grad.device or \
+                    g.numel() != k:
+                self.flat_grad[off:off + k].copy_(g.reshape(-1))
+            else:
+                jobs.append(L.CopyJob(g.data_ptr(), dst, k))
+            rebind.append((p, off, k, g))
+        st = L.stream_ptr(self.flat_grad.device)
+        for i in range(0, len(jobs), 32):
+            arr = (L.CopyJob * len(jobs[i:i + 32]))(*jobs[i:i + 32])
+            L.check(L.lib().tm_copy_many(arr, len(jobs[i:i + 32]), st), "FusedAdam.sync_grads")
+        for p, off, k, g in rebind:
+            p.grad = self.flat_grad[off:off + k].view_as(p)
+        return rebind
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -92,16 +126,11 @@ class FusedAdam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        if not self._grads_bound():
-            # a caller replaced a .grad (e.g. set it to None and ran backward): copy it into the bucket
-            for i, (p, off, k) in enumerate(self._spans):
-                if p.grad is None:
-                    self.flat_grad[off:off + k].zero_()
-                    self._reached.discard(i)
-                elif p.grad.data_ptr() != self.flat_grad[off:].data_ptr():
-                    self.flat_grad[off:off + k].copy_(p.grad.reshape(-1))
-                    self._reached.add(i)
-                p.grad = self.flat_grad[off:off + k].view_as(p)
+        # the reached parameters' gradients into the bucket (a .grad set by the caller counts as reached)
+        for p, g0 in [(p, p.grad) for p, _, _ in self._spans]:
+            if g0 is not None and g0.data_ptr() != self.flat_grad.data_ptr() + 4 * self._spans[self._index[id(p)]][1]:
+                self._reached.add(self._index[id(p)])
+        self.sync_grads()
         for p, off, k in self._spans:
             if p.data_ptr() != self.flat_param[off:].data_ptr():
                 raise RuntimeError("FusedAdam: a parameter was rebound away from the flat bucket")

@@ -146,13 +146,15 @@ class GradAllReduce:
     both back to back.  ``force``: run the collective even in a group of one (exercises the backend's
     path, e.g. RCCL on one GPU; at world size 1 the average is the gradient itself)."""
 
-    def __init__(self, module, group=None, force=False, flat_grad=None):
-        """``flat_grad``: the one buffer every gradient of ``module`` is a view of (optim.FusedAdam.flat_grad):
-        the all-reduce runs on it in place -- no packing copies before the collective or after it."""
+    def __init__(self, module, group=None, force=False, bucket=None):
+        """``bucket``: the module's optimizer when it keeps the gradients in one flat buffer (optim.FusedAdam):
+        ``start`` gathers them there (``bucket.sync_grads()``, one launch per 32 parameters) and the all-reduce runs
+        on ``bucket.flat_grad`` in place -- no per-parameter packing copies before the collective or after it."""
         self.module, self.group = module, group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.force = bool(force) and dist.is_initialized()
-        self.flat_grad = flat_grad
+        self.bucket = bucket
+        self.flat_grad = None if bucket is None else bucket.flat_grad
         self._flat = None
         self._work = None
         self._grads = None
@@ -161,6 +163,7 @@ class GradAllReduce:
         if self.world == 1 and not self.force:
             return
         if self.flat_grad is not None:
+            self.bucket.sync_grads()
             self._flat, self._grads = self.flat_grad, None
             self._work = dist.all_reduce(self._flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
             return

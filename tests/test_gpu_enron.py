@@ -334,11 +334,23 @@ def test_dropin_device_pack_and_grad_equal_pipeline(dev, finder, g, z, where):
     assert torch.equal(e2, h2.reshape(3 * E, N * N))
 
 
+def _general_inputs(dev, item, edges):
+    """get_item / get_item_edge outputs as plain (non-resident) device tensors: the drop-in's general path (per-side
+    calls, every parameter an input of its node), the fast paths' reference."""
+    def t(a, dt):
+        return torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)
+    sgs = [([t(x, torch.int32) for x in sg[0]], [t(x, torch.int32) for x in sg[1]], sg[2]) for sg in item[:3]]
+    ws = [(t(w[0], torch.int32), t(w[1], torch.int32), t(w[2], torch.float32), t(w[3], torch.int32), w[4])
+          for w in item[3:6]]
+    return sgs, ws, [t(e, torch.float32) for e in edges]
+
+
 def test_dropin_fast_path_gradients_match_general_path(dev, finder, g, z):
-    """The device-pack fast path (tm_dropin_forward + tm_edge_importance_gf, parameters behind bundle
-    tensors in the autograd nodes) against the general path (host pack: per-side calls, every parameter
-    an input of its node): same outputs bit for bit, and the same gradients of a loss over the
-    explanation and the three graphlet importances, for every explainer parameter and the importances."""
+    """The drop-in fast path (tm_dropin_forward + tm_edge_importance_gf, parameters behind bundle tensors in the
+    autograd nodes) on a device pack and on the reference's host pack (its numpy views staged on the side stream)
+    against the general path (plain device tensors: per-side calls, every parameter an input of its node): same
+    outputs bit for bit, and the same gradients of a loss over the explanation and the three graphlet
+    importances, for every explainer parameter and the importances."""
     from tempme_amd import explainer as X
     from tempme_amd import pack as P
     from tempme_amd.pipeline import ExplainPipeline
@@ -355,20 +367,25 @@ def test_dropin_fast_path_gradients_match_general_path(dev, finder, g, z):
         n_degree = N
     cut = z["test_ts"][:E].astype(np.float64)
     res = {}
-    for where in ("device", "host"):
+    for where in ("device", "host", "general"):
         pk, ed = ((P.load_subgraph_margin(A(), cat_d, device=dev), P.load_edge(edge, dev)) if where == "device"
                   else (P.load_subgraph_margin(A(), cat_d), edge))
         ex.zero_grad()
         ex.__dict__.pop("_gf_cache", None)
         ex.__dict__.pop("_fastx", None)
         idx = np.arange(25, 50)
-        sg_s, sg_t, sg_b, w_s, w_t, w_b, _ = P.get_item(pk, idx)
-        e_s, e_t, e_b = P.get_item_edge(ed, idx)
+        item = P.get_item(pk, idx)
+        edges = P.get_item_edge(ed, idx)
+        if where == "general":
+            (sg_s, sg_t, sg_b), (w_s, w_t, w_b), (e_s, e_t, e_b) = _general_inputs(dev, item, edges)
+        else:
+            sg_s, sg_t, sg_b, w_s, w_t, w_b, _ = item
+            e_s, e_t, e_b = edges
         imps = [ex(w_s, cut[idx], e_s), ex(w_t, cut[idx], e_t), ex(w_b, cut[idx], e_b)]
         for i in imps:
             i.retain_grad()
         expl = ex.retrieve_explanation(sg_s, imps[0], w_s, sg_t, imps[1], w_t, sg_b, imps[2], w_b, training=False)
-        assert (where == "device") == bool(ex.__dict__.get("_gf_cache")), "fast path taken only on device views"
+        assert (where != "general") == bool(ex.__dict__.get("_gf_cache")), "fast path on device / host pack views"
         if where == "device" and X._dropin_ext() is not None:
             # the first forward built the C++ host side; the other calls went through it
             assert ex.__dict__["_fastx"][0].hits == 3
@@ -376,14 +393,16 @@ def test_dropin_fast_path_gradients_match_general_path(dev, finder, g, z):
         loss.backward()
         res[where] = ([x.detach().clone() for x in expl], [i.grad.clone() for i in imps],
                       {n: p.grad.detach().clone() for n, p in ex.named_parameters() if p.grad is not None})
-    (xd, gd, pd), (xh, gh, ph) = res["device"], res["host"]
-    for a_, b_ in zip(xd, xh):
-        assert torch.equal(a_, b_)
-    for a_, b_ in zip(gd, gh):
-        torch.testing.assert_close(a_, b_, rtol=1e-5, atol=1e-7)
-    assert pd.keys() == ph.keys() and len(pd) >= 26
-    for n in pd:
-        torch.testing.assert_close(pd[n], ph[n], rtol=1e-5, atol=1e-7, msg=n)
+    xg, gg, pg = res["general"]
+    for fast in ("device", "host"):
+        xf, gf_, pf = res[fast]
+        for a_, b_ in zip(xf, xg):
+            assert torch.equal(a_, b_), fast
+        for a_, b_ in zip(gf_, gg):
+            torch.testing.assert_close(a_, b_, rtol=1e-5, atol=1e-7, msg=fast)
+        assert pf.keys() == pg.keys() and len(pf) >= 26
+        for n in pf:
+            torch.testing.assert_close(pf[n], pg[n], rtol=1e-5, atol=1e-7, msg=f"{fast} {n}")
 
 
 def test_eval_forward_grad_matches_torch(dev, finder, g, z):
@@ -434,34 +453,41 @@ def test_dropin_bern_fast_path_matches_general_path(dev, finder, g, z):
     ex, P, A, cat_d, edge, cut = _bern_setup(dev, finder, g, z)
     ex.beta_sample = lambda prob, training: prob     # instance attribute: both paths call self.beta_sample
     res = {}
-    for where in ("device", "host"):
+    for where in ("device", "host", "general"):
         pk, ed = ((P.load_subgraph_margin(A(), cat_d, device=dev), P.load_edge(edge, dev)) if where == "device"
                   else (P.load_subgraph_margin(A(), cat_d), edge))
         ex.zero_grad()
         ex.__dict__.pop("_gf_cache", None)
         ex.__dict__.pop("_fastx", None)
         idx = np.arange(25, 50)
-        sg_s, sg_t, sg_b, w_s, w_t, w_b, _ = P.get_item(pk, idx)
-        e_s, e_t, e_b = P.get_item_edge(ed, idx)
+        item = P.get_item(pk, idx)
+        edges = P.get_item_edge(ed, idx)
+        if where == "general":
+            (sg_s, sg_t, sg_b), (w_s, w_t, w_b), (e_s, e_t, e_b) = _general_inputs(dev, item, edges)
+        else:
+            sg_s, sg_t, sg_b, w_s, w_t, w_b, _ = item
+            e_s, e_t, e_b = edges
         imps = [ex(w_s, cut[idx], e_s), ex(w_t, cut[idx], e_t), ex(w_b, cut[idx], e_b)]
         for i in imps:
             i.retain_grad()
         expl = ex.retrieve_explanation(sg_s, imps[0], w_s, sg_t, imps[1], w_t, sg_b, imps[2], w_b, training=True)
-        assert (where == "device") == bool(ex.__dict__.get("_gf_cache"))
+        assert (where != "general") == bool(ex.__dict__.get("_gf_cache"))
         if where == "device" and X._dropin_ext() is not None:
             assert ex.__dict__["_fastx"][0].hits == 3
         loss = expl[0].pow(2).sum() + 0.5 * expl[1].sum() + (imps[0] * imps[1]).sum()
         loss.backward()
         res[where] = ([x.detach().clone() for x in expl], [i.grad.clone() for i in imps],
                       {n: p.grad.detach().clone() for n, p in ex.named_parameters() if p.grad is not None})
-    (xd, gd, pd), (xh, gh, ph) = res["device"], res["host"]
-    for a_, b_ in zip(xd, xh):
-        assert torch.equal(a_, b_)
-    for a_, b_ in zip(gd, gh):
-        torch.testing.assert_close(a_, b_, rtol=1e-5, atol=1e-7)
-    assert pd.keys() == ph.keys() and len(pd) >= 26
-    for n in pd:
-        torch.testing.assert_close(pd[n], ph[n], rtol=1e-5, atol=1e-7, msg=n)
+    xg, gg, pg = res["general"]
+    for fast in ("device", "host"):
+        xf, gf_, pf = res[fast]
+        for a_, b_ in zip(xf, xg):
+            assert torch.equal(a_, b_), fast
+        for a_, b_ in zip(gf_, gg):
+            torch.testing.assert_close(a_, b_, rtol=1e-5, atol=1e-7, msg=fast)
+        assert pf.keys() == pg.keys() and len(pf) >= 26
+        for n in pf:
+            torch.testing.assert_close(pf[n], pg[n], rtol=1e-5, atol=1e-7, msg=f"{fast} {n}")
 
 
 def test_dropin_bern_draws_are_beta(dev, finder, g, z):

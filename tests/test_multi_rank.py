@@ -194,7 +194,13 @@ def _flat_grad_worker(rank, world, port, q):
         for p in net.parameters():
             p.grad = flat[off:off + p.numel()].view_as(p)
             off += p.numel()
-        sync = GradAllReduce(net, flat_grad=flat)
+        class Bucket:                                     # optim.FusedAdam's interface: the gradients already bound
+            flat_grad = flat
+
+            @staticmethod
+            def sync_grads():
+                return []
+        sync = GradAllReduce(net, bucket=Bucket())
         for step in range(3):
             x = torch.randn(4, 5, generator=torch.Generator().manual_seed(100 * step + rank))
             flat.zero_()

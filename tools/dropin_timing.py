@@ -44,7 +44,11 @@ def main():
     class A:
         n_degree = N
     cut = ts[sl].astype(np.float64)
-    pk, ed = P.load_subgraph_margin(A(), cat_d, device=dev), P.load_edge(edge, dev)
+    host = "host" in sys.argv[1:]     # the reference's host float64 pack (load_subgraph_margin(args, f)) and edge array
+    if host:
+        pk, ed = P.load_subgraph_margin(A(), cat_d), edge
+    else:
+        pk, ed = P.load_subgraph_margin(A(), cat_d, device=dev), P.load_edge(edge, dev)
     seg = {k: 0.0 for k in ("get_item", "get_item_edge", "forward_src", "forward_tgt", "forward_bgd", "retrieve")}
 
     def one(b, t=None):
@@ -109,6 +113,16 @@ def main():
         setattr(lib, name, f)
     for name in ("_fast_state", "_dropin_ctx", "_hip_eval_ok"):
         del ex.__dict__[name]
+    if "profile" in sys.argv[1:]:
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        for b in range(nb):
+            one(b)
+        torch.cuda.synchronize()
+        pr.disable()
+        pstats.Stats(pr).sort_stats("tottime").print_stats(25)
     # one side's forward, split: the module call, forward() without nn.Module.__call__, and the C++ host
     # side's entry alone (csrc/dropin_ext.cpp Fast.forward: checks, output allocation, tm_dropin_forward)
     fx = ex.__dict__.get("_fastx")
