@@ -47,13 +47,19 @@ def main():
         t3 = graph_time(lambda: torch.addmm(bias[:, None], w, x.t()).t().contiguous())
         fl = 2 * M * N * K / 1e6
         prev = torch.backends.cuda.preferred_blas_library()
-        torch.backends.cuda.preferred_blas_library("rocblas")
-        t4 = graph_time(lambda: torch.addmm(bias, x, w.t()))
-        err4 = float((torch.addmm(bias, x, w.t()) - ref).abs().max())
-        torch.backends.cuda.preferred_blas_library(prev)
+        other = []
+        for lib in ("hipblas", "ck"):
+            try:
+                torch.backends.cuda.preferred_blas_library(lib)
+                t4 = graph_time(lambda: torch.addmm(bias, x, w.t()))
+                err4 = float((torch.addmm(bias, x, w.t()) - ref).abs().max())
+                other.append(f"{lib} {t4:7.1f} us ({fl / t4:5.1f}) diff {err4:.1e}")
+            except Exception as e:      # noqa: BLE001
+                other.append(f"{lib} failed: {str(e)[:60]}")
+            finally:
+                torch.backends.cuda.preferred_blas_library(prev)
         print(f"{name:20s} M={M} K={K} N={N}: addmm {t1:7.1f} us ({fl / t1:5.1f} TF/s) | swapped {t2:7.1f} us "
-              f"({fl / t2:5.1f}) | swapped+copy {t3:7.1f} us | max diff {err:.2e} | rocblas {t4:7.1f} us "
-              f"({fl / t4:5.1f}) diff {err4:.2e}")
+              f"({fl / t2:5.1f}) | swapped+copy {t3:7.1f} us | max diff {err:.2e} | " + " | ".join(other))
 
 
 if __name__ == "__main__":
