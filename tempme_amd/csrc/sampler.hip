@@ -177,6 +177,20 @@ __device__ __forceinline__ int32_t blk_lb(const DevGraph &g, int32_t base, int32
     return r[0];
 }
 
+// phase stamps inside final_step (debug builds only, -DTM_STAMPS): s_memtime into T[k] at wave-uniform points
+#ifdef TM_STAMPS
+#define TM_FS(k)                                            \
+    do {                                                    \
+        if (T) {                                            \
+            __builtin_amdgcn_sched_barrier(0);              \
+            T[k] = __builtin_amdgcn_s_memtime();            \
+            __builtin_amdgcn_sched_barrier(0);              \
+        }                                                   \
+    } while (0)
+#else
+#define TM_FS(k) (void)T
+#endif
+
 struct Step3 {
     int32_t src, ngh, eid;
     float ts;
@@ -191,7 +205,8 @@ struct Step3 {
 // none).  In the filtered cases the a-side node is src2 and a2 = tgt2, so when the cut of e2 is the
 // record's own position (no tie group moved it) the count of a2-entries before the cut is rank2.
 __device__ Step3 final_step(const DevGraph &g, Key key, uint32_t ev, uint32_t w, int32_t src1, int32_t tgt1,
-                            int32_t src2, int32_t tgt2, int32_t e2, int32_t pos2, int32_t rank2) {
+                            int32_t src2, int32_t tgt2, int32_t e2, int32_t pos2, int32_t rank2,
+                            unsigned long long *T = nullptr) {
     int32_t code, a_node, a1 = 0, a2 = 0, b_node, bf = 0;
     bool filt;
     if (src1 == src2 && tgt1 != tgt2) {
@@ -215,6 +230,7 @@ __device__ Step3 final_step(const DevGraph &g, Key key, uint32_t ev, uint32_t w,
         if (vb && x2.node_a != b_node && x2.node_b != b_node) cb = bisect_ts(g, b_node, t2);
     }
     int32_t na, nb, k1 = 0, n1 = 0, k2 = 0, n2 = 0, kb = 0;
+    TM_FS(8);
     if (filt) {
         // filtered counts: the (node, neighbour) block of each of the three neighbours from the block
         // table, then the entries before the cut inside each block down its search tree; the lookups
@@ -238,8 +254,13 @@ __device__ Step3 final_step(const DevGraph &g, Key key, uint32_t ev, uint32_t w,
         na = ca;
         nb = cb;
     }
+    TM_FS(9);
     Step3 o{0, 0, 0, 0.f, code, 0};
-    if (na + nb == 0) return o;
+    if (na + nb == 0) {
+        TM_FS(10);
+        TM_FS(11);
+        return o;
+    }
     const int32_t r = draw(key, TM_STAGE_STEP3, ev, w, 0, (uint32_t)(na + nb));
     int32_t ent;
     if (r < na) {
@@ -252,6 +273,7 @@ __device__ Step3 final_step(const DevGraph &g, Key key, uint32_t ev, uint32_t w,
         int32_t pos = filt ? g.ppos[kb + rr] : rr;
         ent = ob0 + pos;
     }
+    TM_FS(10);
     const Rec rc = g.rec[ent];
     o.ngh = rc.ngh;
     o.eid = rc.eid;
@@ -267,6 +289,7 @@ __device__ Step3 final_step(const DevGraph &g, Key key, uint32_t ev, uint32_t w,
             : (s == tgt1 && n == src1) ? 1 : 0;
     }
     o.t = t;
+    TM_FS(11);
     return o;
 }
 
@@ -871,7 +894,7 @@ __host__ __device__ inline size_t events_lds_bytes(int32_t N, int32_t M) {
 
 // Phase timing (debug builds only, -DTM_STAMPS): s_memtime deltas of lane 0 for events 2000..3999
 #ifdef TM_STAMPS
-__device__ unsigned long long g_est[8];
+__device__ unsigned long long g_est[16];
 #define TM_EST(k)                                   \
     do {                                            \
         __builtin_amdgcn_sched_barrier(0);          \
@@ -882,12 +905,15 @@ __device__ unsigned long long g_est[8];
 #define TM_EST(k) (void)T
 #endif
 
-template <bool keyed, int MC>
+// NC > 0: n_degree is the compile-time constant NC (the reference's default 20): the row / column splits of
+// the draw and rank loops are constant divisions and their trip counts known (SQ_INSTS_VALU per wave, see
+// profiles/r06_pmc_events_summary.json); NC = 0: any N <= kMaxN.  MC > 0 likewise fixes M.
+template <bool keyed, int MC, int NC = 0>
 __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
-    unsigned long long T[8];
+    unsigned long long T[12];
     TM_EST(0);
     extern __shared__ int32_t ev_lds[];
-    const int32_t N = a.N, M = a.M, W = N * M;
+    const int32_t N = NC > 0 ? NC : a.N, M = MC > 0 ? MC : a.M, W = N * M;
     int32_t *h1n = ev_lds, *h1e = h1n + N;
     float *h1t = reinterpret_cast<float *>(h1e + N);
     uint32_t *d2 = reinterpret_cast<uint32_t *>(h1e + 2 * N);
@@ -994,15 +1020,32 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
             dr[u] = x < N * N ? d2[x] : 0u;
             rank[u] = 0;
         }
-        // the 4 rows' comparisons interleaved, 4 columns per iteration: 16 LDS reads in flight
-#pragma unroll 4
-        for (int32_t i = 0; i < N; ++i)
+        if (NC > 0 && (NC & 3) == 0) {
+            // rows of a multiple of 4 draws are 16-B aligned: 4 columns per b128 read, one read per row in flight
+            // (unrolling the column loop spends VGPRs the kernel's occupancy needs)
+#pragma unroll 1
+            for (int32_t i = 0; i < N; i += 4)
 #pragma unroll
-            for (int u = 0; u < HB; ++u) {
-                const uint32_t di = d2[jr[u] * N + i];
-                if (keyed) rank[u] += di < dr[u];
-                else rank[u] += (di < dr[u]) || (i < kr[u] && di == dr[u]);
-            }
+                for (int u = 0; u < HB; ++u) {
+                    const uint4 q = *reinterpret_cast<const uint4 *>(d2 + jr[u] * N + i);
+                    const uint32_t dq[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        if (keyed) rank[u] += dq[t] < dr[u];
+                        else rank[u] += (dq[t] < dr[u]) || (i + t < kr[u] && dq[t] == dr[u]);
+                    }
+                }
+        } else {
+            // the 4 rows' comparisons interleaved, 4 columns per iteration: 16 LDS reads in flight
+#pragma unroll 4
+            for (int32_t i = 0; i < N; ++i)
+#pragma unroll
+                for (int u = 0; u < HB; ++u) {
+                    const uint32_t di = d2[jr[u] * N + i];
+                    if (keyed) rank[u] += di < dr[u];
+                    else rank[u] += (di < dr[u]) || (i < kr[u] && di == dr[u]);
+                }
+        }
 #pragma unroll
         for (int u = 0; u < HB; ++u) {
             const int32_t x = x0 + u * 64 + tid;
@@ -1049,7 +1092,13 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
         const int32_t j = w / M, m = w % M;
         const int32_t v1 = h1n[j], e1 = h1e[j];
         const Step2 s2 = next_step<MC>(g, key, ev, j, M, m, u, v1, s2c[j]);
+        TM_EST(6);
+#ifdef TM_STAMPS
+        const Step3 s3 = final_step(g, key, ev, w, u, v1, s2.src, s2.ngh, s2.eid, s2.pos, s2.rank, T);
+#else
         const Step3 s3 = final_step(g, key, ev, w, u, v1, s2.src, s2.ngh, s2.eid, s2.pos, s2.rank);
+#endif
+        TM_EST(7);
         const int64_t o = se * W + w;
         const auto nd = o_node6 + o * 6;
         // per-lane row stores (24 / 12 B per walk); staging them in LDS for contiguous runs measured
@@ -1090,7 +1139,16 @@ __global__ void __launch_bounds__(64) events_kernel(EventArgs a) {
 #ifdef TM_STAMPS
     if (tid == 0 && e >= 2000 && e < 4000) {
         for (int k = 0; k < 5; ++k) atomicAdd(&g_est[k], T[k + 1] - T[k]);
-        atomicAdd(&g_est[7], 1ull);
+        // inside steps 2 + 3: next_step (from the hop-2 end, incl. the table clear), final_step's loads, its
+        // filtered counts, its draw + k-th selection, its record load, then stores / histogram / table inserts
+        atomicAdd(&g_est[5], T[6] - T[3]);
+        atomicAdd(&g_est[6], T[8] - T[6]);
+        atomicAdd(&g_est[8], T[9] - T[8]);
+        atomicAdd(&g_est[9], T[10] - T[9]);
+        atomicAdd(&g_est[10], T[11] - T[10]);
+        atomicAdd(&g_est[11], T[7] - T[11]);
+        atomicAdd(&g_est[12], T[4] - T[7]);
+        atomicAdd(&g_est[15], 1ull);
     }
 #endif
     // per-(event, side) bins, summed by hist_reduce_kernel: 12 same-address device-scope atomics from
@@ -1244,7 +1302,13 @@ extern "C" int tm_sample_events(const tm_graph *g, uint64_t seed, uint32_t split
     const size_t lds = events_lds_bytes(N, M);
     const dim3 grid(n_events, 3);
     const bool kd = use_keyed(g);
-    if (M == 3) {
+    if (M == 3 && N == 20) {
+        if (kd) events_kernel<true, 3, 20><<<grid, 64, lds, S(stream)>>>(a);
+        else events_kernel<false, 3, 20><<<grid, 64, lds, S(stream)>>>(a);
+    } else if (M == 1 && N == 20) {
+        if (kd) events_kernel<true, 1, 20><<<grid, 64, lds, S(stream)>>>(a);
+        else events_kernel<false, 1, 20><<<grid, 64, lds, S(stream)>>>(a);
+    } else if (M == 3) {
         if (kd) events_kernel<true, 3><<<grid, 64, lds, S(stream)>>>(a);
         else events_kernel<false, 3><<<grid, 64, lds, S(stream)>>>(a);
     } else if (M == 1) {
@@ -1266,7 +1330,7 @@ extern "C" int tm_sample_events(const tm_graph *g, uint64_t seed, uint32_t split
 
 #ifdef TM_STAMPS
 extern "C" int tm_debug_event_stamps(unsigned long long *host) {
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(tmk::g_est), sizeof(unsigned long long) * 8, 0,
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(tmk::g_est), sizeof(unsigned long long) * 16, 0,
                                     hipMemcpyDeviceToHost);
 }
 #endif

@@ -9,12 +9,16 @@ sys.argv = ["bench.py", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "-
 runpy.run_path("bench.py", run_name="__main__")
 from tempme_amd import _lib  # noqa: E402
 
-ev = (C.c_ulonglong * 8)()
+ev = (C.c_ulonglong * 16)()
 if hasattr(_lib.lib(), "tm_debug_event_stamps"):   # sampler.hip built with -DTM_STAMPS too
     assert _lib.lib().tm_debug_event_stamps(ev) == 0
-    n = max(1, ev[7])
-    print("events_kernel n=%d" % ev[7], " ".join("%s=%.0f" % (nm, ev[k] / n) for k, nm in
-                                                 enumerate(["hop1", "hop2_cuts", "hop2", "walks", "edge_counts"])))
+    n = max(1, ev[15])
+    print("events_kernel n=%d" % ev[15], " ".join("%s=%.0f" % (nm, ev[k] / n) for k, nm in
+                                                  enumerate(["hop1", "hop2_cuts", "hop2", "walks", "edge_counts"])))
+    print("  walks:", " ".join("%s=%.0f" % (nm, ev[k] / n) for k, nm in
+                               ((5, "clear+next_step"), (6, "final_loads"), (8, "final_filtered_counts"),
+                                (9, "final_draw+kth"), (10, "final_rec"), (11, "final_ret"),
+                                (12, "stores+hist+inserts"))))
 buf = (C.c_ulonglong * 30)()
 assert _lib.lib().tm_debug_stamps(buf) == 0
 names = ["issue", "lin_event", "A/B", "g1", "relu", "next row", "folded gemms", "head/stash"]
