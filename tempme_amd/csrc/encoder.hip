@@ -88,15 +88,11 @@ struct GateLookup {
     uint32_t *cnt, *cnt_next;
 };
 
-__global__ void __launch_bounds__(1024) std_cut_kernel(int32_t B, int32_t W, CutArg c, const float *__restrict__ ts3,
-                                                       double *__restrict__ cut_out, float *__restrict__ std_out,
-                                                       int32_t do_std, GateLookup gl) {
+// workgroup 0's part: the cut times to cut_out and the group's std
+__device__ __forceinline__ void std_cut_body(int32_t B, int32_t W, const CutArg &c, const float *__restrict__ ts3,
+                                             double *__restrict__ cut_out, float *__restrict__ std_out, int32_t do_std,
+                                             const GateLookup &gl) {
     __shared__ double red[16];
-    if (blockIdx.x > 0) {
-        gate_cache_lookup((int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x, gl.eid, gl.ts, gl.cache, gl.n_cache, gl.gf,
-                          gl.list, gl.cnt, gl.n_pos);
-        return;
-    }
     if (threadIdx.x == 0 && gl.cnt_next) *gl.cnt_next = 0u;
     if ((int)threadIdx.x < B) cut_out[threadIdx.x] = c.v[threadIdx.x];
     if (!do_std || B == 0) return;
@@ -142,6 +138,17 @@ __global__ void __launch_bounds__(1024) std_cut_kernel(int32_t B, int32_t W, Cut
     }
     const double var = block_sum(v, red);
     if (threadIdx.x == 0) std_out[0] = n > 1 ? (float)sqrt(var / (double)(n - 1)) : __builtin_nanf("");
+}
+
+__global__ void __launch_bounds__(1024) std_cut_kernel(int32_t B, int32_t W, CutArg c, const float *__restrict__ ts3,
+                                                       double *__restrict__ cut_out, float *__restrict__ std_out,
+                                                       int32_t do_std, GateLookup gl) {
+    if (blockIdx.x > 0) {
+        gate_cache_lookup((int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x, gl.eid, gl.ts, gl.cache, gl.n_cache, gl.gf,
+                          gl.list, gl.cnt, gl.n_pos);
+        return;
+    }
+    std_cut_body(B, W, c, ts3, cut_out, std_out, do_std, gl);
 }
 
 // ------------------------------------------------------------------ event_gcn: 32 walk-positions per block
@@ -1658,20 +1665,14 @@ __global__ void __launch_bounds__(256) gate_table_kernel(EncW P, int32_t n_ids, 
 __device__ __forceinline__ unsigned long long gate_cache_pack(float t, float f) {
     return ((unsigned long long)__float_as_uint(t) << 32) | (unsigned long long)__float_as_uint(f);
 }
+// one wave's 16 columns i0 .. i0 + 15 (of n_ids; i0 < n_ids, wave-uniform)
 template <int NQ, int NQX = 0, int NQL = 1>
-__global__ void __launch_bounds__(256) gate_reg_kernel(EncW P, int32_t n_ids, const double *__restrict__ ets,
-                                                       const float *__restrict__ e_feat, float *__restrict__ gf,
-                                                       float *__restrict__ etab = nullptr,
-                                                       const int32_t *__restrict__ row_eid = nullptr,
-                                                       const float *__restrict__ row_t = nullptr,
-                                                       const int32_t *__restrict__ list = nullptr,
-                                                       const uint32_t *__restrict__ list_n = nullptr,
-                                                       unsigned long long *__restrict__ cache = nullptr,
-                                                       int64_t n_cache = 0) {
+__device__ __forceinline__ void gate_reg_cols(const EncW &P, int64_t i0, int32_t n_ids, const double *__restrict__ ets,
+                                              const float *__restrict__ e_feat, float *__restrict__ gf,
+                                              float *__restrict__ etab, const int32_t *__restrict__ row_eid,
+                                              const float *__restrict__ row_t, const int32_t *list,
+                                              unsigned long long *__restrict__ cache, int64_t n_cache) {
     const int lane = threadIdx.x & 63, col = lane & 15, g = lane_id() >> 4;
-    const int64_t i0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16;
-    if (list) n_ids = (int32_t)*list_n;
-    if (i0 >= n_ids) return;                             // wave-uniform
     const bool valid = i0 + col < n_ids;
     const int64_t e = !list ? i0 + col : valid ? (int64_t)list[i0 + col] : 0;
     const int64_t ec = !valid ? 0 : row_eid ? (int64_t)row_eid[e] : e;
@@ -1741,6 +1742,22 @@ __global__ void __launch_bounds__(256) gate_reg_kernel(EncW P, int32_t n_ids, co
     }
 }
 
+template <int NQ, int NQX = 0, int NQL = 1>
+__global__ void __launch_bounds__(256) gate_reg_kernel(EncW P, int32_t n_ids, const double *__restrict__ ets,
+                                                       const float *__restrict__ e_feat, float *__restrict__ gf,
+                                                       float *__restrict__ etab = nullptr,
+                                                       const int32_t *__restrict__ row_eid = nullptr,
+                                                       const float *__restrict__ row_t = nullptr,
+                                                       const int32_t *__restrict__ list = nullptr,
+                                                       const uint32_t *__restrict__ list_n = nullptr,
+                                                       unsigned long long *__restrict__ cache = nullptr,
+                                                       int64_t n_cache = 0) {
+    const int64_t i0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16;
+    if (list) n_ids = (int32_t)*list_n;
+    if (i0 >= n_ids) return;                             // wave-uniform
+    gate_reg_cols<NQ, NQX, NQL>(P, i0, n_ids, ets, e_feat, gf, etab, row_eid, row_t, list, cache, n_cache);
+}
+
 // The drop-in's gate-factor cache (tm_dropin_gate_cache): per walk position, a hit on (edge id, exact fp32 time)
 // gives the factor gate_reg_kernel computed for it; the misses go to a list (one atomic per wave) that the list
 // mode of gate_reg_kernel computes and stores.  Runs in std_cut_kernel's workgroups 1.. (one launch fewer).  The factor is a function of (E[e], t) alone, so the result equals
@@ -1770,6 +1787,33 @@ __device__ __forceinline__ void gate_cache_lookup(int64_t i, const int32_t *__re
     if (lane == first) base = atomicAdd(list_n, (uint32_t)__popcll(m));
     base = (uint32_t)__shfl(base, first);
     if (miss) list[base + __popcll(m & ((1ull << lane) - 1))] = (int32_t)i;
+}
+
+// std_cut_kernel with the cache misses computed where they are found (tm_dropin_forward with the gate cache and the
+// register gate): workgroups 1.. look up their 1024 walk positions, list the misses in LDS, and their 16 waves run
+// gate_reg_kernel's list mode over that list (the same arithmetic: bit-identical factors, the cache filled the same
+// way) -- one launch per side call instead of two.  Two workgroups missing the same (edge id, time) both compute
+// it (same value); a hit on an entry another workgroup just stored is the same value too.
+template <int NQ>
+__global__ void __launch_bounds__(1024) std_cut_gate_kernel(int32_t B, int32_t W, CutArg c, const float *__restrict__ ts3,
+                                                            double *__restrict__ cut_out, float *__restrict__ std_out,
+                                                            int32_t do_std, GateLookup gl, EncW P,
+                                                            const float *__restrict__ e_feat) {
+    if (blockIdx.x == 0) {
+        std_cut_body(B, W, c, ts3, cut_out, std_out, do_std, gl);
+        return;
+    }
+    __shared__ int32_t miss[1024];
+    __shared__ uint32_t n_miss;
+    if (threadIdx.x == 0) n_miss = 0u;
+    __syncthreads();
+    gate_cache_lookup((int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x, gl.eid, gl.ts, gl.cache, gl.n_cache, gl.gf,
+                      miss, &n_miss, gl.n_pos);
+    __syncthreads();
+    const int32_t n = (int32_t)n_miss;
+    for (int32_t i0 = (int32_t)(threadIdx.x >> 6) * 16; i0 < n; i0 += (int32_t)(blockDim.x >> 6) * 16)
+        gate_reg_cols<NQ>(P, i0, n, nullptr, e_feat, gl.gf, nullptr, gl.eid, gl.ts, miss,
+                          const_cast<unsigned long long *>(gl.cache), gl.n_cache);
 }
 
 // threads per (group, event) workgroup of explain_tab_kernel (its loops stride by blockDim.x): one wave
@@ -2543,6 +2587,15 @@ extern "C" int tm_dropin_forward(tm_dropin *d, int32_t k, int32_t sync, const tm
         d->gpar[k] ^= 1;
     }
     const unsigned lookup_blocks = gl.cnt ? (unsigned)((n_pos + 1023) / 1024) : 0u;
+    // with the cache: the misses are computed by the lookup's own workgroups (std_cut_gate_kernel), no gate launch
+    const bool fused_gate = gl.cnt != nullptr && (nq == 11 || nq == 12 || nq == 13);
+    auto launch_std = [&](int32_t b_, const CutArg &c, double *cut_out, float *std_out, int32_t do_std) {
+        const dim3 grid(1 + lookup_blocks);
+        if (!fused_gate) std_cut_kernel<<<grid, 1024, 0, side>>>(b_, W, c, ts3, cut_out, std_out, do_std, gl);
+        else if (nq == 11) std_cut_gate_kernel<11><<<grid, 1024, 0, side>>>(b_, W, c, ts3, cut_out, std_out, do_std, gl, P, e_feat);
+        else if (nq == 12) std_cut_gate_kernel<12><<<grid, 1024, 0, side>>>(b_, W, c, ts3, cut_out, std_out, do_std, gl, P, e_feat);
+        else std_cut_gate_kernel<13><<<grid, 1024, 0, side>>>(b_, W, c, ts3, cut_out, std_out, do_std, gl, P, e_feat);
+    };
     bool std_done = false;
     if (cut_host && B <= 256) {
         // the cut times travel as the std launch's argument; std_cut_kernel writes them to this side's
@@ -2551,7 +2604,7 @@ extern "C" int tm_dropin_forward(tm_dropin *d, int32_t k, int32_t sync, const tm
         memcpy(c.v, cut_host, sizeof(double) * (size_t)B);
         float *stdv = reinterpret_cast<float *>(d->ws[k]) + n_walks * 3 * 2 * w->P.h;
         hipEvent_t pe = prof_begin(side);
-        std_cut_kernel<<<1 + lookup_blocks, 1024, 0, side>>>(B, W, c, ts3, d->dcut[k], stdv, w->P.tg ? 1 : 0, gl);
+        launch_std(B, c, d->dcut[k], stdv, w->P.tg ? 1 : 0);
         TM_CHECK_LAUNCH();
         prof_end("std_kernel", side, pe);
         cut = d->dcut[k];
@@ -2588,13 +2641,13 @@ extern "C" int tm_dropin_forward(tm_dropin *d, int32_t k, int32_t sync, const tm
     }
     if (!std_done && gl.cnt) {   // no cut times in the launch argument: the lookup alone (workgroup 0 idle but the reset)
         CutArg c;
-        std_cut_kernel<<<1 + lookup_blocks, 1024, 0, side>>>(0, W, c, ts3, nullptr, nullptr, 0, gl);
+        launch_std(0, c, nullptr, nullptr, 0);
         TM_CHECK_LAUNCH();
     }
     int rc = encoder_fwd_impl(w, n_feat, e_feat, etab, 1, B, W, 1, node6, eid3, ts3, cat, cut, cnt, d->ws[k], out_imp,
                               side, !std_done);
     if (rc != TM_OK) return rc;
-    if (out_gfac) {
+    if (out_gfac && !fused_gate) {
         const size_t lds = gate_lds(P);
         if (lds > 160 * 1024) return fail(TM_E_UNSUPPORTED, "tm_dropin_forward: LDS budget exceeded");
         hipEvent_t pe = prof_begin(side);
