@@ -45,7 +45,18 @@ def kernel_flops(ex, B, N, M, zn=False):
     enc = (R * dn * (kev + 1) + rows * h * (dn + 1) + rows * h * (h + 1) + n * h2 * (h2 + 1) + 2 * n * h2 * (h2 + 1)
            + n * h * (h2 + 1) + n * h * (h + 1) + n * hm * (hm + 1) + n * h * (hm + 1) + n * (h + 1) + R * dn * 2)
     gate = R * h * (de + dn + 1) + R * (h // 2) * (h + 1) + R * (h // 2 + 1) + R * dn * 2
-    return {"gcn_bwd_kernel": gcn_bwd, "gcn_kernel": gcn, "wgrad_partial_kernel": 2 * (enc + gate)}
+    # head_kernel per walk (TemporalAwareAttention :789-846 + the category MLP :122-125; the GEMMs of the wgrad job
+    # list above): W1 on position 2 and W2 on positions 0, 1 (h2 x h2 each), the two bmm's (2 h2 each), MLP h2 -> h
+    # -> h, the category MLP (hm x hm, hm -> h, h -> 1).  head_bwd_kernel recomputes that forward and runs the
+    # data-gradient GEMM of every layer (same sizes): twice the forward.
+    head = 2 * n * (3 * h2 * h2 + 4 * h2 + h * h2 + h * h + hm * hm + h * hm + h)
+    # gate_train_fwd_kernel per position: [E | cos] (de + dn) -> h -> h/2 -> 1; gate_train_bwd_kernel: d G2 -> d G1
+    # (h/2 x h) -> d time features (h x dn)
+    gate_fwd = 2 * R * ((de + dn) * h + h * (h // 2) + h // 2)
+    gate_bwd = 2 * R * ((h // 2) * h + h * dn)
+    return {"gcn_bwd_kernel": gcn_bwd, "gcn_kernel": gcn, "wgrad_partial_kernel": 2 * (enc + gate),
+            "head_kernel": head, "head_bwd_kernel": 2 * head, "gate_train_fwd_kernel": gate_fwd,
+            "gate_train_bwd_kernel": gate_bwd}
 
 
 def main():
