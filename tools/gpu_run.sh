@@ -77,6 +77,7 @@ for s in "$@"; do
         c4) step bench_c4 900 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config 4 ;;
         a3) step bench_a3 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --alpha 3.0 ;;
         dropint) step dropint 300 python tools/dropin_timing.py ;;
+        dropinth) step dropinth 300 python tools/dropin_timing.py host ;;
         diag) step overlap_diag 300 python -u tools/overlap_diag.py ;;
         testsall) step pytest_gpu_all 1100 python -u -m pytest tests -q -m gpu -rfEs --timeout 300 --timeout-method thread ;;
         variants) step pytest_variants 600 python -u -m pytest tests/test_gpu_variants.py tests/test_gpu_enron.py -v -m gpu -rfEs --timeout 300 --timeout-method thread -k "variants or cpp_host" ;;
