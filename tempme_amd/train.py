@@ -384,6 +384,9 @@ class GraphedTrainStep:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, stream=self.stream):
             self.out = self._body()
+        # the capture recorded the repack without running it (the device packs are the last warm-up step's,
+        # from before its optimizer step): an eager call before the first replay must repack
+        explainer._packed_key = None
 
     def _body(self):
         ex, base, opt, buf, src, dst, ts, e_idx = self.args
