@@ -279,12 +279,14 @@ def _cpu_model():
     return None
 
 
-def cpu_baseline(g, rows, events, pool, N, M, B, seed, sd, budget_s=4.0, max_batches=150, reps=3):
+def cpu_baseline(g, rows, events, pool, N, M, B, seed, sd, budget_s=4.0, max_batches=150, reps=3, gm_sd=None):
     """The oracle port (C sampler + torch-fp32 encoder) on the host cores, bounded samples: ``reps`` repeats on the
     process's CPU share (OpenMP and torch threads = the cgroup quota, at most the CPUs it may run on) -- ``value`` is
     their median, ``spread`` min / max -- and one single-thread repeat (the least sensitive to other tenants of the
-    box's cores)."""
+    box's cores).  ``gm_sd`` (configs[4]): the GraphMixer contrast of every batch with its hop-1 explanation too
+    (oracle/graphmixer_ref.py, 2 mixer layers), as the GPU line times it."""
     from oracle import encoder_ref as er
+    from oracle import graphmixer_ref as gr
     from oracle import oracle as orc
     use, nproc, quota = _cpu_cores()
     threads = int(os.environ.get("TEMPME_CPU_THREADS", use))
@@ -302,12 +304,18 @@ def cpu_baseline(g, rows, events, pool, N, M, B, seed, sd, budget_s=4.0, max_bat
             o = orc.event_pipeline(og, seed, 1, N, M, src[sl], dst[sl], ts[sl], eidx[sl], np.arange(done, done + B),
                                    pool, nthr)
             with torch.no_grad():
+                h1 = []
                 for s in range(3):
                     imp = er.forward(sd, nf, ef, o["node6"][:, s], o["eid3"][:, s], o["ts3"][:, s], o["cat"][:, s],
                                      ts[sl], o["cnt"][:, s].astype(np.float64))
-                    er.edge_importance(sd, ef, imp, o["eid3"][:, s], o["ts3"][:, s],
-                                       [o["sub1_node"][:, s], o["sub2_node"][:, s]],
-                                       [o["sub1_eid"][:, s], o["sub2_eid"][:, s]])
+                    h1.append(er.edge_importance(sd, ef, imp, o["eid3"][:, s], o["ts3"][:, s],
+                                                 [o["sub1_node"][:, s], o["sub2_node"][:, s]],
+                                                 [o["sub1_eid"][:, s], o["sub2_eid"][:, s]])[0])
+                if gm_sd is not None:
+                    sg = [([o["sub1_node"][:, s]], [o["sub1_eid"][:, s]], [o["sub1_ts"][:, s].astype(np.float64)])
+                          for s in range(3)]
+                    gr.contrast(gm_sd, 2, src[sl], dst[sl], o["dst_fake"], ts[sl], *sg,
+                                explain_weights=[torch.cat(h1).float()])
             done += B
         el = time.perf_counter() - t0
         return done / el, done, el
@@ -324,8 +332,10 @@ def cpu_baseline(g, rows, events, pool, N, M, B, seed, sd, budget_s=4.0, max_bat
             "sample": f"{reps} repeats (median reported) of up to {max_batches} reference batches of {B} target events or "
                       f"{budget_s:.0f} s each ({sum(r[1] for r in runs)} events in {sum(r[2] for r in runs):.1f} s) of "
                       f"the same workload: oracle/tempme_oracle.c sampling+motif ({threads} OpenMP threads) + "
-                      f"oracle/encoder_ref.py torch-fp32 encoder+explanation ({threads} threads); single_thread = one "
-                      f"more repeat on 1 thread ({single[1]} events in {single[2]:.1f} s)"}
+                      f"oracle/encoder_ref.py torch-fp32 encoder+explanation ({threads} threads)"
+                      + (" + oracle/graphmixer_ref.py GraphMixer contrast with the hop-1 explanation" if gm_sd is not None
+                         else "") + f"; single_thread = one more repeat on 1 thread ({single[1]} events in "
+                      f"{single[2]:.1f} s)"}
 
 
 # ----------------------------------------------------------------------------------------------- timing
@@ -656,7 +666,8 @@ def main():
             out["aux"] = aux_rows(finder, src, dst, ts, eidx, pool, graph_build_ms)
         if world == 1 and not args.no_cpu_baseline:
             sd = {k: v.detach().cpu() for k, v in ex.state_dict().items()}
-            out["cpu_baseline"] = cpu_baseline(g, rows, (src, dst, ts, eidx), pool, N, M, B, args.seed, sd)
+            gm_sd = None if gm is None else {k: v.detach().cpu() for k, v in gm.state_dict().items()}
+            out["cpu_baseline"] = cpu_baseline(g, rows, (src, dst, ts, eidx), pool, N, M, B, args.seed, sd, gm_sd=gm_sd)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

@@ -74,7 +74,7 @@ for s in "$@"; do
         trainops) step trainops 300 python tools/train_ops.py ;;
         gemmprobe) step gemm_probe 300 python tools/gemm_probe.py ;;
         c2) step bench_c2 600 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config 2 ;;
-        c4) step bench_c4 900 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config 4 ;;
+        c4) step bench_c4 900 python bench.py --steps 5 --warmup 1 --config 4 ;;
         a3) step bench_a3 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --alpha 3.0 ;;
         dropint) step dropint 300 python tools/dropin_timing.py ;;
         dropinth) step dropinth 300 python tools/dropin_timing.py host ;;
