@@ -360,7 +360,10 @@ int tm_beta_rsample_bwd(const float *g, const float *pad, const float *x, const 
  * tm_host_unregister(ptr)) and returns the device address of ptr; tm_stage_cast runs up to 16 jobs in one
  * launch, each gathering an ndim <= 5 strided view (byte strides) of src (a device-accessible address: device
  * memory or a registered host array's device address) into dst contiguous, converting its type (C conversions:
- * truncation toward zero for integers, round to nearest for float32 -- numpy's astype / torch's .to). */
+ * truncation toward zero for integers, round to nearest for float32 -- numpy's astype / torch's .to).
+ * bound > 0 (int32 destinations: row indices of a table with `bound` rows) clamps each value into [0, bound):
+ * a guard for ids the caller validated once per array (values in range are unchanged), so a pack rewritten
+ * after that check can never make a later kernel read outside the table. */
 #define TM_I32 1
 #define TM_F32 2
 #define TM_I64 3
@@ -368,7 +371,7 @@ int tm_beta_rsample_bwd(const float *g, const float *pad, const float *x, const 
 typedef struct tm_stage_job {
     const void *src;
     void *dst;
-    int32_t src_type, dst_type, ndim, reserved;
+    int32_t src_type, dst_type, ndim, bound;
     int64_t shape[5];
     int64_t stride[5];   /* bytes */
 } tm_stage_job;

@@ -106,7 +106,7 @@ class CopyJob(C.Structure):
 class StageJob(C.Structure):
     """tm_stage_job (include/tempme.h)."""
     _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("src_type", C.c_int32), ("dst_type", C.c_int32),
-                ("ndim", C.c_int32), ("reserved", C.c_int32), ("shape", C.c_int64 * 5), ("stride", C.c_int64 * 5)]
+                ("ndim", C.c_int32), ("bound", C.c_int32), ("shape", C.c_int64 * 5), ("stride", C.c_int64 * 5)]
 
 
 TM_I32, TM_F32, TM_I64, TM_F64 = 1, 2, 3, 4

@@ -15,6 +15,7 @@
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <deque>
 #include <vector>
@@ -291,9 +292,98 @@ class Fast {
     std::deque<GfEntry> cache_;
 };
 
+// include/tempme.h tm_stage_job / tm_stage_cast (the host-pack staging of hoststage.stage)
+struct StageJob {
+    const void *src;
+    void *dst;
+    int32_t src_type, dst_type, ndim, bound;
+    int64_t shape[5];
+    int64_t stride[5];
+};
+using StageFn = int (*)(const StageJob *jobs, int32_t n_jobs, void *stream);
+constexpr int kI32 = 1, kF32 = 2, kI64 = 3, kF64 = 4, kMaxStage = 16;
+
+int buffer_type(const char *f, Py_ssize_t itemsize) {
+    if (!f) return 0;
+    while (*f == '<' || *f == '=' || *f == '@') ++f;
+    if (f[0] == 0 || f[1] != 0) return 0;
+    switch (f[0]) {
+        case 'd': return itemsize == 8 ? kF64 : 0;
+        case 'f': return itemsize == 4 ? kF32 : 0;
+        case 'i': return itemsize == 4 ? kI32 : 0;
+        case 'l': case 'q': return itemsize == 8 ? kI64 : 0;
+        default: return 0;
+    }
+}
+
+// hoststage.stage's per-call work for views of registered host arrays, on the current stream of `device`:
+// items = [(array, dst type 1 int32 | 2 float32, bound, registered start, registered length, its device address)].
+// Every view must lie inside its registration; one allocation, one tm_stage_cast launch.  The outputs (torch
+// tensors shaped as the views) or None when any item does not qualify (the Python path then decides).
+py::object stage_host(py::list items, int device, int64_t fn) {
+    const size_t n = items.size();
+    if (n == 0 || n > (size_t)kMaxStage) return py::none();
+    StageJob jobs[kMaxStage] = {};
+    std::vector<std::vector<int64_t>> shapes(n);
+    int64_t off[kMaxStage], total = 0;
+    for (size_t i = 0; i < n; ++i) {
+        py::tuple it = items[i].cast<py::tuple>();
+        Py_buffer v;
+        if (PyObject_GetBuffer(it[0].ptr(), &v, PyBUF_RECORDS_RO) != 0) {
+            PyErr_Clear();
+            return py::none();
+        }
+        const int st = buffer_type(v.format, v.itemsize);
+        const int dt = it[1].cast<int>();
+        const int64_t bound = it[2].cast<int64_t>(), lo = it[3].cast<int64_t>(), len = it[4].cast<int64_t>(),
+                      dev = it[5].cast<int64_t>();
+        bool ok = st != 0 && (dt == kI32 || dt == kF32) && v.ndim <= 5 && bound >= 0 && bound < INT32_MAX;
+        const uintptr_t p = reinterpret_cast<uintptr_t>(v.buf);
+        intptr_t a = (intptr_t)p, b = (intptr_t)p;
+        int64_t elems = 1;
+        StageJob &j = jobs[i];
+        j.ndim = v.ndim > 0 ? v.ndim : 1;
+        j.shape[0] = 1;
+        for (int d = 0; ok && d < v.ndim; ++d) {
+            const int64_t e = v.shape[d], s = v.strides ? v.strides[d] : 0;
+            if (e <= 0) ok = false;
+            a += std::min<int64_t>(0, (e - 1) * s);
+            b += std::max<int64_t>(0, (e - 1) * s);
+            j.shape[d] = e;
+            j.stride[d] = s;
+            elems *= e;
+            shapes[i].push_back(e);
+        }
+        b += v.itemsize;
+        PyBuffer_Release(&v);   // the array stays alive: the caller holds it (and the registry holds its base)
+        if (!ok || a < lo || b > lo + len) return py::none();
+        j.src = reinterpret_cast<const void *>(dev + ((intptr_t)p - lo));
+        j.src_type = st;
+        j.dst_type = dt;
+        j.bound = dt == kI32 ? (int32_t)bound : 0;
+        off[i] = total;
+        total += (elems * 4 + 15) & ~int64_t(15);
+    }
+    c10::hip::HIPGuard g(device);
+    at::Tensor buf = at::empty({std::max<int64_t>(total, 16)}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, device));
+    char *base = static_cast<char *>(buf.data_ptr());
+    for (size_t i = 0; i < n; ++i) jobs[i].dst = base + off[i];
+    const int rc = reinterpret_cast<StageFn>(fn)(jobs, (int32_t)n, c10::hip::getCurrentHIPStream(device).stream());
+    if (rc != 0) return py::make_tuple(py::none(), rc);
+    py::list out;
+    for (size_t i = 0; i < n; ++i) {
+        int64_t elems = 1;
+        for (int64_t e : shapes[i]) elems *= e;
+        at::Tensor t = buf.narrow(0, off[i], elems * 4).view(jobs[i].dst_type == kI32 ? at::kInt : at::kFloat);
+        out.append(py::reinterpret_steal<py::object>(THPVariable_Wrap(t.view(shapes[i]))));
+    }
+    return py::make_tuple(out, 0);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_dropin_ext, m) {
+    m.def("stage_host", &stage_host);
     m.doc() = "C++ host side of TempME's drop-in eval fast path (tempme_amd/csrc/dropin_ext.cpp)";
     py::class_<Fast>(m, "Fast")
         .def(py::init<py::list, py::list, py::object, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t,

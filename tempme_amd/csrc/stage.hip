@@ -6,7 +6,8 @@
 // a call's views straight from that memory (no host-side cast and no pinned staging copy): one launch gathers every
 // view of the call -- any dtype of the pack (int64 / float64 / int32 / float32), up to 5 dims with arbitrary byte
 // strides -- converts it to the kernels' int32 / float32 (C conversions: truncation toward zero, round to nearest,
-// as numpy's astype and torch's .to) and writes it contiguous on the device.
+// as numpy's astype and torch's .to) and writes it contiguous on the device; a job with a bound clamps its int32
+// row indices into the table (the caller checked them once per array: a guard, not a conversion).
 #include <mutex>
 #include <unistd.h>
 #include <unordered_map>
@@ -49,6 +50,7 @@ __global__ void __launch_bounds__(256) stage_cast_kernel(StageArgs a) {
             if (j.src_type == TM_I64) v = (int32_t)*reinterpret_cast<const int64_t *>(p);
             else if (j.src_type == TM_I32) v = *reinterpret_cast<const int32_t *>(p);
             else v = (int32_t)load_as_double(p, j.src_type);
+            if (j.bound > 0) v = min(max(v, 0), j.bound - 1);
             static_cast<int32_t *>(j.dst)[i] = v;
         } else if (j.dst_type == TM_F32) {
             static_cast<float *>(j.dst)[i] = j.src_type == TM_F32 ? *reinterpret_cast<const float *>(p)
@@ -120,7 +122,7 @@ extern "C" int tm_stage_cast(const tm_stage_job *jobs, int32_t n_jobs, void *str
     for (int i = 0; i < n_jobs; ++i) {
         const tm_stage_job &j = jobs[i];
         if (!j.src || !j.dst || j.ndim < 1 || j.ndim > 5 || j.src_type < TM_I32 || j.src_type > TM_F64 ||
-            j.dst_type < TM_I32 || j.dst_type > TM_F64)
+            j.dst_type < TM_I32 || j.dst_type > TM_F64 || j.bound < 0 || (j.bound > 0 && j.dst_type != TM_I32))
             return fail(TM_E_ARG, "tm_stage_cast: bad job " + std::to_string(i));
         int64_t n = 1;
         for (int d = 0; d < j.ndim; ++d) {

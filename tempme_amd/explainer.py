@@ -827,6 +827,11 @@ class TempME(nn.Module):
         """What the drop-in fast path derives from the weights and feature tables (packed weights, edge
         table, table pointers, parameter bundles), rebuilt when one key over the packed parameters'
         (data_ptr, version, requires_grad) and the two feature tables' (data_ptr, version) changes."""
+        fx = self.__dict__.get("_fastx")
+        if fx is not None and fx[0].current():
+            # the C++ host side watches the same tensors (data_ptr, version, requires_grad) and the module
+            # registrations: its state is the current one
+            return fx[1]
         ws = self._weight_list()
         ne = self._modules["node_raw_embed"]._parameters["weight"]
         ee = self._modules["edge_raw_embed"]._parameters["weight"]
@@ -906,8 +911,16 @@ class TempME(nn.Module):
         if not self._hip_eval_ok():
             return None
         fs = self._fast_state()
-        if host and edge_idx.size and (edge_idx.max() >= fs.keep[2].shape[0] or edge_idx.min() < 0):
-            raise IndexError("index out of range in self")     # what the reference's embedding lookup raises
+        if host:
+            # ids outside the node / edge tables raise what the reference's embedding lookups raise.  The check
+            # runs once per pack array and layout (hoststage.window_bounds: these columns over every batch of the
+            # array), per call only when that fails or the array is not registered; staging then clamps the ids
+            # into the tables (tm_stage_job.bound), so a pack rewritten after the check is never read out of range
+            n_node, n_edge = fs.keep[1].shape[0], fs.keep[2].shape[0]
+            for a, n in ((edge_idx, n_edge), (node_idx, n_node)):
+                wb = _hoststage().window_bounds(a)
+                if (wb is None or not (wb[0] >= 0 and wb[1] < n)) and a.size and (a.max() >= n or a.min() < 0):
+                    raise IndexError("index out of range in self")
         _, ctx, ext, nk = self._dropin_ctx(dev)
         k = nk[0]
         nk[0] = (k + 1) % 3
@@ -923,11 +936,11 @@ class TempME(nn.Module):
         try:
             out = torch.empty(B * W * 4, dtype=torch.float32, device=dev)   # imp [B*W] | gate factors [B*W*3]
             if host:
-                items = ((node_idx, torch.int32), (edge_idx, torch.int32), (time_idx, torch.float32),
+                items = ((node_idx, torch.int32, n_node), (edge_idx, torch.int32, n_edge), (time_idx, torch.float32),
                          (cat_feat, torch.int32), (edge_identify, torch.float32))
                 staged = _hoststage().stage(dev, items)         # the current stream is side stream k here
                 if staged is None:                           # small / non-owning bases: pinned host-cast copy
-                    staged = _to_many(dev, *items)
+                    staged = _to_many(dev, *[it[:2] for it in items])
                 host_keys = (edge_idx, time_idx)
                 node_idx, edge_idx, time_idx, cat_feat, edge_identify = staged
         finally:
@@ -962,8 +975,9 @@ class TempME(nn.Module):
             args = (node_idx, edge_idx, time_idx, cat_feat,
                     np.array(cut_time_l, dtype=np.float64) if cut_d is None else cut_time_l, edge_identify, 1, B, W)
             imp = _apply(_EvalEncoderBundleFn, self, args, imp, fs.bundle(self, "enc"))
-        if not host:
-            self._make_fastx(fs, ctx, dev, (edge_idx, time_idx, out, B, W))
+        # the C++ host side for later calls (device-pack views; with host arrays its state check keeps _fast_state
+        # cheap); its gate-factor cache entry: the walk tensors the kernels read (host arrays: the staged copies)
+        self._make_fastx(fs, ctx, dev, (edge_idx, time_idx, out, B, W))
         return imp
 
     def _make_fastx(self, fs, ctx, dev, entry):

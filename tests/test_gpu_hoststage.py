@@ -38,6 +38,54 @@ def test_stage_cast_equals_numpy_astype():
     assert len(H._REG.regs) == n and torch.equal(again[0], got[0])
 
 
+def test_window_bounds_and_staging_bound():
+    """window_bounds = min / max of the view's columns over every row of its owning array (cached per layout);
+    a staging bound clamps int32 ids into [0, bound) and leaves in-range ids unchanged."""
+    from tempme_amd import hoststage as H
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(1)
+    w = rng.integers(0, 5000, size=(3000, 60, 14)).astype(np.float64)      # 20 MB: registered
+    w[2500, 7, 7] = 7777.0
+    v = w[100:200, :, 6:9]
+    assert H.window_bounds(v) == (w[:, :, 6:9].min(), w[:, :, 6:9].max())
+    assert H.window_bounds(w[300:400, :, 6:9]) == H.window_bounds(v)           # same layout: cached
+    assert H.window_bounds(w[100:200, :, 0:6]) == (w[:, :, 0:6].min(), w[:, :, 0:6].max())
+    v[0, 0, 0] = 6000.0                                                          # out of a 5,000-row table
+    v[0, 0, 1] = -3.0
+    st = torch.cuda.Stream()
+    got = H.stage(dev, [(v, torch.int32, 5000), (v, torch.int32)], st)
+    torch.cuda.synchronize()
+    want = np.ascontiguousarray(v.astype(np.int32))
+    assert torch.equal(got[1].cpu(), torch.from_numpy(want))
+    want[0, 0, 0], want[0, 0, 1] = 4999, 0
+    assert torch.equal(got[0].cpu(), torch.from_numpy(want))
+
+
+def test_stage_cpp_host_side_equals_python():
+    """hoststage.stage on the current stream (the C++ per-view work of dropin_ext.stage_host) = the Python job
+    builder on an explicit stream, bitwise, bounds included."""
+    from tempme_amd import hoststage as H
+    from tempme_amd.explainer import _dropin_ext
+    if _dropin_ext() is None:
+        pytest.skip("drop-in extension not built")
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(2)
+    w = rng.integers(-3, 9000, size=(2500, 60, 14)).astype(np.float64)
+    e = rng.integers(0, 4, size=(3, 2500, 60, 3, 3)).astype(np.float64)
+    node = w[:, :, :6].astype(np.int64)
+    rows = slice(200, 300)
+    items = [(node[rows], torch.int32, 5000), (w[rows, :, 6:9], torch.int32, 8000), (w[rows, :, 9:12], torch.float32),
+             (w[rows, :, 12], torch.int32), (e[2][rows], torch.float32)]
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        a = H.stage(dev, items)
+    b = H._stage_py(dev, items, st)
+    torch.cuda.synchronize()
+    assert a is not None and b is not None
+    for x, y in zip(a, b):
+        assert x.dtype == y.dtype and x.shape == y.shape and torch.equal(x, y)
+
+
 def test_stage_refuses_what_it_cannot_read_in_place():
     from tempme_amd import hoststage as H
     dev = torch.device("cuda", 0)
@@ -98,3 +146,13 @@ def test_host_pack_dropin_reads_pack_in_place(tmp_path):
         assert torch.equal(expl[1], h2[:, sl].reshape(3 * B, N * N))
     # the walk / subgraph / edge bases went through the in-place path (at least the large ones)
     assert sum(1 for e in H._REG.regs.values() if e[3] is not None) >= 3
+    # an edge id outside the edge table raises what the reference's embedding lookup raises (a small copy: the
+    # per-call check of the pinned host-cast path)
+    idx = np.arange(0, B)
+    _, _, _, w_s, _, _, _ = P.get_item(pk, idx)
+    e_s = P.get_item_edge(edge, idx)[0]
+    bad = [np.array(x, copy=True) if isinstance(x, np.ndarray) else x for x in w_s]
+    bad[1][0, 0, 0] = float(g["e_feat"].shape[0] + 5)
+    with pytest.raises(IndexError):
+        with torch.no_grad():
+            ex(bad, cut[idx], e_s)

@@ -87,6 +87,26 @@ def main():
             ctime[_n] = ctime.get(_n, 0.0) + time.perf_counter() - t0
             return r
         setattr(lib, name, wrap)
+    # the host-pack path's staging (hoststage) and the context's own library entry (bound at context creation)
+    from tempme_amd import hoststage as HS
+    horig = {n: getattr(HS, n) for n in ("stage", "window_bounds")}
+    for name, f in horig.items():
+        def wraph(*a, _f=f, _n=name, **kw):
+            t0 = time.perf_counter()
+            r = _f(*a, **kw)
+            ctime["hoststage." + _n] = ctime.get("hoststage." + _n, 0.0) + time.perf_counter() - t0
+            return r
+        setattr(HS, name, wraph)
+    dctx = ex.__dict__.get("_dropin_c")
+    if dctx is not None:
+        cf = dctx[1].fwd
+
+        def wrapc(*a, _f=cf):
+            t0 = time.perf_counter()
+            r = _f(*a)
+            ctime["ctx.fwd (tm_dropin_forward)"] = ctime.get("ctx.fwd (tm_dropin_forward)", 0.0) + time.perf_counter() - t0
+            return r
+        dctx[1].fwd = wrapc
     # Python methods of the fast path, timed the same way
     for name in ("_fast_state", "_dropin_ctx", "_hip_eval_ok"):
         f = getattr(ex, name)
@@ -113,6 +133,10 @@ def main():
         setattr(lib, name, f)
     for name in ("_fast_state", "_dropin_ctx", "_hip_eval_ok"):
         del ex.__dict__[name]
+    for name, f in horig.items():
+        setattr(HS, name, f)
+    if dctx is not None:
+        dctx[1].fwd = cf
     if "profile" in sys.argv[1:]:
         import cProfile
         import pstats
