@@ -380,10 +380,23 @@ py::object stage_host(py::list items, int device, int64_t fn) {
     return py::make_tuple(out, 0);
 }
 
+// the data address of a buffer-protocol object (a numpy view), or -1
+int64_t buf_addr(py::handle o) {
+    Py_buffer v;
+    if (PyObject_GetBuffer(o.ptr(), &v, PyBUF_RECORDS_RO) != 0) {
+        PyErr_Clear();
+        return -1;
+    }
+    const int64_t a = (int64_t) reinterpret_cast<uintptr_t>(v.buf);
+    PyBuffer_Release(&v);
+    return a;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_dropin_ext, m) {
     m.def("stage_host", &stage_host);
+    m.def("buf_addr", &buf_addr);
     m.doc() = "C++ host side of TempME's drop-in eval fast path (tempme_amd/csrc/dropin_ext.cpp)";
     py::class_<Fast>(m, "Fast")
         .def(py::init<py::list, py::list, py::object, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t,

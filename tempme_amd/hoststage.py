@@ -42,8 +42,16 @@ class _Registry:
         self.lock = threading.Lock()
 
     def entry(self, base):
-        """[base, lo, length, device address of lo or None]: ``base``'s registration (made on first use)."""
+        """[base, lo, length, device address of lo or None, bounds cache, base address]: ``base``'s registration
+        (made on first use)."""
         key = id(base)
+        e = self.regs.get(key)
+        if e is not None and e[0] is base:
+            try:
+                self.regs.move_to_end(key)
+                return e
+            except KeyError:             # released meanwhile: the locked path below
+                pass
         with self.lock:
             e = self.regs.get(key)
             if e is not None and e[0] is base:
@@ -58,13 +66,13 @@ class _Registry:
             dev = C.c_void_p()
             ok = L.lib().tm_host_register(lo, hi - lo, C.byref(dev)) == 0
             # a refusal is remembered too: the slow path serves that base from then on
-            e = self.regs[key] = [base, lo, hi - lo, dev.value if ok else None, {}]
+            e = self.regs[key] = [base, lo, hi - lo, dev.value if ok else None, {}, ptr]
             if ok:
                 self.bytes += hi - lo
             return e
 
     def _release(self, key):
-        base, ptr, n, dev, _ = self.regs.pop(key)
+        base, ptr, n, dev, *_ = self.regs.pop(key)
         if dev is not None:
             # launched work may still read it: the whole device drains first (a release is rare: LRU eviction past
             # CAP_BYTES, clear(), interpreter exit)
@@ -117,7 +125,10 @@ def window_bounds(a):
     s0 = a.strides[0]
     if s0 <= 0 or min(a.strides) < 0:
         return None
-    off0 = (a.__array_interface__["data"][0] - base.__array_interface__["data"][0]) % s0
+    from .explainer import _dropin_ext
+    ext = _dropin_ext()
+    p = ext.buf_addr(a) if ext is not None else a.__array_interface__["data"][0]
+    off0 = (p - e[5]) % s0
     key = (off0, a.shape[1:], a.strides, a.dtype.str)
     hit = e[4].get(key)
     if hit is None:
