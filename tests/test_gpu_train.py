@@ -207,6 +207,8 @@ def test_graphed_step_equals_eager(dev):
         losses = []
         if graphed:
             step = GraphedTrainStep(ex, base, opt, buf, s_d, d_d, t_d, e_d, batches[:1], if_bern=False)
+            # the capture recorded the repack without running it: an eager call before the first replay repacks
+            assert ex._packed_key is None
             for r in batches[1:]:
                 losses.append(float(step(r)["loss"]))
         else:
