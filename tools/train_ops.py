@@ -40,7 +40,7 @@ def main():
     torch.cuda.synchronize()
     from torch.profiler import ProfilerActivity, profile
     steps = batches[4:12]
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True, record_shapes=True) as prof:
         for b in steps:
             train_step(ex, base, opt, b)
         torch.cuda.synchronize()
@@ -49,6 +49,14 @@ def main():
     rows_ = sorted(ka, key=lambda e: -e.device_time_total)[:45]
     for e in rows_:
         print("%9.1f us %6.1f calls  %s" % (e.device_time_total / len(steps), e.count / len(steps), e.key[:90]))
+    print("=== small glue ops by input shapes (per step) ===")
+    glue = ("aten::add", "aten::add_", "aten::cat", "aten::fill_", "aten::zero_", "aten::copy_", "aten::clamp",
+            "aten::clamp_min", "aten::mul", "aten::sub", "aten::threshold_backward", "aten::_to_copy", "aten::sum")
+    ksh = prof.key_averages(group_by_input_shape=True)
+    for e in sorted(ksh, key=lambda e: -e.device_time_total):
+        if e.key in glue and e.device_time_total > 0:
+            print("%9.1f us %5.1f calls  %-24s %s" % (e.device_time_total / len(steps), e.count / len(steps), e.key,
+                                                     str(e.input_shapes)[:150]))
     print("=== by stack (top 40, per step) ===")
     ks = prof.key_averages(group_by_stack_n=4)
     for e in sorted(ks, key=lambda e: -e.device_time_total)[:40]:
