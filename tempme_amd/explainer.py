@@ -691,7 +691,10 @@ class TempME(nn.Module):
             e = _BetaRsampleFn.apply(p, pad)
         else:
             e = self.beta_sample(p, training) * pad    # beta_sample then masked_fill(node == 0, 0) (:400-404, :420-430)
-        return e[:n1].view(n_groups, B, N), e[n1:].view(n_groups, B, N * N)
+        # one split, not two slices: its backward is one cat of the two gradients instead of two zero-filled
+        # full-size buffers, two copies and their sum
+        e1, e2 = torch.split(e, [n1, e.numel() - n1])
+        return e1.view(n_groups, B, N), e2.view(n_groups, B, N * N)
 
     def _expl_io(self, R):
         dev = self._dev()
