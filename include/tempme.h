@@ -62,7 +62,8 @@ int tm_version(void);
 #define TM_DEBUG_FORCE_UNKEYED 1
 #define TM_DEBUG_HOST_BUILD 2
 #define TM_DEBUG_GRAPH_TIMING 3
-#define TM_DEBUG_N_OPTS 4
+#define TM_DEBUG_WALK_BLOCKS 4   /* > 0: cap the persistent walk kernel's grid at this many workgroups (A/B tools) */
+#define TM_DEBUG_N_OPTS 5
 int tm_debug_set(int32_t opt, int32_t value);
 /* Threads of the host-side graph builder (0 = the CPUs this process may run on, at most 64). */
 int tm_set_host_threads(int32_t n);

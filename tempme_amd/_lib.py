@@ -28,7 +28,7 @@ TM_E_UNSUPPORTED = -5
 
 SIDE_NONE, SIDE_SRC, SIDE_TGT, SIDE_BGD = 0, 1, 2, 3
 SPLIT_TRAIN, SPLIT_TEST, SPLIT_NULL = 0, 1, 2
-TM_DEBUG_FORCE_UNKEYED, TM_DEBUG_HOST_BUILD, TM_DEBUG_GRAPH_TIMING = 1, 2, 3   # tm_debug_set (tests only)
+TM_DEBUG_FORCE_UNKEYED, TM_DEBUG_HOST_BUILD, TM_DEBUG_GRAPH_TIMING, TM_DEBUG_WALK_BLOCKS = 1, 2, 3, 4   # tm_debug_set (tests, A/B tools)
 N_WEIGHTS = 28
 
 # every symbol include/tempme.h declares

@@ -2207,6 +2207,8 @@ static void launch_walk(const WalkArgs &a, unsigned blocks, hipStream_t s) {
         }
         if (cap[dev] > 0 && blocks > (unsigned)cap[dev]) blocks = (unsigned)cap[dev];
     }
+    const int dbg = debug_opt(TM_DEBUG_WALK_BLOCKS);   // A/B of smaller persistent grids (tools/walk_grid_ab.sh)
+    if (dbg > 0 && blocks > (unsigned)dbg) blocks = (unsigned)dbg;
     walk_kernel<NQE, 11, SEF, Q0, false, ZN><<<dim3(blocks), 64 * WALK_WPB, 0, s>>>(a);
 }
 
