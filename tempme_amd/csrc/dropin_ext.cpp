@@ -16,6 +16,7 @@
 #include <c10/hip/HIPStream.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <deque>
 #include <vector>
@@ -42,6 +43,15 @@ using Gf3BernFn = int (*)(int32_t B, int32_t W, int32_t N, const float *, const 
                           void *);
 
 constexpr int kSides = 3, kCache = 6, kMaxHostCut = 512;
+
+// host-time split of Fast.forward (diagnostics: prof_enable / prof_read, tools/dropin_timing.py): nanoseconds per
+// segment summed over the calls since enabled
+bool g_prof_on = false;
+int64_t g_prof[8] = {}, g_prof_n = 0;
+inline int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
 
 bool is_tensor(PyObject *o) { return THPVariable_Check(o); }
 
@@ -119,9 +129,13 @@ class Fast {
     // TempME.forward (eval) on device-pack views of one batch: (imp [B, W, 1], rc, needs_grad) or None
     py::object forward(py::handle node_idx, py::handle edge_idx, py::handle time_idx, py::handle cat_feat,
                        py::handle cut_time, py::handle edge_identify) {
+        int64_t T[8];
+        const bool pr = g_prof_on;
+        if (pr) T[0] = now_ns();
         if (!(resident(edge_idx.ptr()) && resident(node_idx.ptr()) && resident(time_idx.ptr()) &&
               resident(cat_feat.ptr()) && resident(edge_identify.ptr())))
             return py::none();
+        if (pr) T[1] = now_ns();
         const at::Tensor &e3 = THPVariable_Unpack(edge_idx.ptr());
         const at::Tensor &n6 = THPVariable_Unpack(node_idx.ptr());
         const at::Tensor &t3 = THPVariable_Unpack(time_idx.ptr());
@@ -155,7 +169,9 @@ class Fast {
             PyBuffer_Release(&view);   // the array object itself stays alive for this call (the caller holds it)
             if (!ok) return py::none();
         }
+        if (pr) T[2] = now_ns();
         if (!current()) return py::none();
+        if (pr) T[3] = now_ns();
         const int k = next_k_;
         next_k_ = (k + 1) % kSides;
         c10::hip::HIPStream cur = c10::hip::getCurrentHIPStream(device_);
@@ -166,7 +182,9 @@ class Fast {
             c10::hip::HIPStreamGuard g(side_[k]);
             out = at::empty({B * W * 4}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, device_));
         }
+        if (pr) T[4] = now_ns();
         c10::hip::HIPCachingAllocator::recordStream(out.storage().data_ptr(), cur);
+        if (pr) T[5] = now_ns();
         const int sync = (cut_d != nullptr || dirty_) ? 1 : 0;
         dirty_ = false;
         float *o = out.data_ptr<float>();
@@ -174,12 +192,19 @@ class Fast {
                             e3.data_ptr<int32_t>(), t3.data_ptr<float>(), ct.data_ptr<int32_t>(), cut_h, cut_d,
                             cn.data_ptr<float>(), o, o + B * W, cur.stream());
         if (rc != 0) return py::make_tuple(py::none(), rc, false);
+        if (pr) T[6] = now_ns();
         at::Tensor imp = out.as_strided({B, W, 1}, {W, 1, 1});
         cache_.push_back(GfEntry{e3, t3, out, e3._version(), t3._version(), B, W});
         if (cache_.size() > kCache) cache_.pop_front();
         ++hits_;
         const bool grad = enc_grad_ && c10::GradMode::is_enabled();
-        return py::make_tuple(py::reinterpret_steal<py::object>(THPVariable_Wrap(imp)), 0, grad);
+        py::object res = py::make_tuple(py::reinterpret_steal<py::object>(THPVariable_Wrap(imp)), 0, grad);
+        if (pr) {
+            T[7] = now_ns();
+            for (int i = 0; i < 7; ++i) g_prof[i] += T[i + 1] - T[i];
+            ++g_prof_n;
+        }
+        return res;
     }
 
     // retrieve_explanation for the three sides' (subgraph, graphlet_imp, walks) whose walks went through
@@ -396,6 +421,16 @@ int64_t buf_addr(py::handle o) {
 
 PYBIND11_MODULE(_dropin_ext, m) {
     m.def("stage_host", &stage_host);
+    m.def("prof_enable", [](bool on) {
+        g_prof_on = on;
+        for (auto &x : g_prof) x = 0;
+        g_prof_n = 0;
+    });
+    m.def("prof_read", []() {
+        py::list l;
+        for (int i = 0; i < 7; ++i) l.append(g_prof_n ? (double)g_prof[i] / g_prof_n / 1e3 : 0.0);
+        return py::make_tuple(l, g_prof_n);
+    });
     m.def("buf_addr", &buf_addr);
     m.doc() = "C++ host side of TempME's drop-in eval fast path (tempme_amd/csrc/dropin_ext.cpp)";
     py::class_<Fast>(m, "Fast")

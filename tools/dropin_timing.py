@@ -117,6 +117,10 @@ def main():
             ctime[_n] = ctime.get(_n, 0.0) + time.perf_counter() - t0
             return r
         ex.__dict__[name] = wrapm
+    from tempme_amd.explainer import _dropin_ext
+    xm = _dropin_ext()
+    if xm is not None and hasattr(xm, "prof_enable"):
+        xm.prof_enable(True)
     reps = 8
     t0 = time.perf_counter()
     for r in range(reps):
@@ -129,6 +133,12 @@ def main():
         print("  %-14s %7.1f us" % (k, v / (reps * nb) * 1e6))
     for k, v in ctime.items():
         print("  inside %-22s %7.1f us per batch" % (k, v / (reps * nb) * 1e6))
+    if xm is not None and hasattr(xm, "prof_read"):
+        segs, n = xm.prof_read()
+        xm.prof_enable(False)
+        names = ("resident checks", "shape / cut checks", "state check", "output alloc", "recordStream",
+                 "tm_dropin_forward", "cache + wrap")
+        print("  C++ Fast.forward split (%d calls): " % n + ", ".join("%s %.2f us" % (a, b) for a, b in zip(names, segs)))
     for name, f in orig.items():     # the original function objects (they carry the argtypes)
         setattr(lib, name, f)
     for name in ("_fast_state", "_dropin_ctx", "_hip_eval_ok"):
